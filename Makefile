@@ -1,0 +1,25 @@
+# Build the MI355X engine (gfx950) and the C oracle.  No cmake needed.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
+SRC = kmamiz_amd/csrc/kmz_kernels.hip kmamiz_amd/csrc/kmz_api.hip
+HDR = include/kmz.h kmamiz_amd/csrc/kmz_common.h kmamiz_amd/csrc/kmz_synth.h kmamiz_amd/csrc/kmz_kernels.h
+OBJ = build/kmz_kernels.o build/kmz_api.o
+
+all: kmamiz_amd/libkmz.so oracle
+
+build/%.o: kmamiz_amd/csrc/%.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+kmamiz_amd/libkmz.so: $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build kmamiz_amd/libkmz.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,227 @@
+"""Benchmark: spans/sec through the endpoint dependency graph + combined stats.
+
+One step = one pass of the hot path over one device-resident synthetic batch:
+K1 build + K2 resolve + K4 walk (dependency graph) and K3 (combined stats),
+finalisation, the multi-GPU merge (N > 1, RCCL via torch.distributed) and the
+download of the results (groups, endpoint records, edge keys) to the host.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config mesh|bookinfo]
+
+Weak scaling: every rank owns a fixed shard of whole traces (config 3's
+100M-span 500-service mesh per GPU by default; N=8 is config 4's ~1B-span
+mesh).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# algorithmic bytes per unit (DESIGN.md "Roofline accounting")
+BYTES_PER_SPAN = {"build": 20, "resolve": 37, "stats": 19}
+BYTES_PER_RELATION = {"walk": 12}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=["mesh", "bookinfo"], default="mesh")
+    ap.add_argument("--spans", type=float, default=None, help="spans per GPU (default: 1e8 mesh, 1e6 bookinfo)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-fetch", action="store_true", help="leave results on the device")
+    return ap.parse_args()
+
+
+def cpu_baseline(config, target_seconds):
+    """The C oracle (single thread, sequential Welford + JS-Map walk) on a
+    bounded prefix of the same synthetic workload."""
+    import numpy as np  # noqa: F401
+
+    from kmamiz_amd import synth
+    from oracle import c_oracle
+
+    table = synth.shape_table(config)
+
+    def run(ntr):
+        batch, _ = synth.host_batch(config, 0, ntr)
+        t = time.perf_counter()
+        c_oracle.stats(batch, table.tag_ep, table.n_tag_ep, table.n_status)
+        c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+        return len(batch), time.perf_counter() - t
+
+    n0, t0 = run(2000)
+    rate0 = n0 / max(t0, 1e-6)
+    ntr = max(2000, int(2000 * target_seconds * rate0 / n0))
+    n, t = run(ntr)
+    return {
+        "value": n / t,
+        "unit": "spans/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {ntr} traces ({n} spans) of the same synthetic workload, seed 0x4B4D414D495A, "
+        f"oracle/kmz_oracle.c stats+deps, {t:.1f} s",
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+
+    from kmamiz_amd import Engine
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import dist as kdist
+    from kmamiz_amd import synth
+
+    config = synth.MESH if args.config == "mesh" else synth.BOOKINFO
+    target = int(args.spans or (1e8 if args.config == "mesh" else 1e6))
+    sample_tr = 20000
+    per_trace = synth.count_spans(config, 0, sample_tr) / sample_tr
+    traces_per_gpu = max(1, int(round(target / per_trace)))
+    t_begin, t_end = rank * traces_per_gpu, (rank + 1) * traces_per_gpu
+
+    stream = torch.cuda.current_stream()
+    eng = Engine(local, stream=stream.cuda_stream)
+    n_local = eng.load_synthetic(config, synth.SEED, t_begin, t_end)
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS
+    dev = torch.device("cuda", local)
+    state = {}
+
+    def step():
+        eng.run(flags)
+        if world > 1:
+            gw = eng.partials_words(L.PART_GROUPS)
+            ew = eng.partials_words(L.PART_ENDPOINTS)
+            tw = eng.partials_words(L.PART_TRIPLES)
+            g = torch.empty(gw, dtype=torch.int64, device=dev)
+            e = torch.empty(ew, dtype=torch.int64, device=dev)
+            t = torch.empty(max(1, tw), dtype=torch.int64, device=dev)
+            eng.export_partials(L.PART_GROUPS, g.data_ptr(), gw, True)
+            eng.export_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
+            eng.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, True)
+            kdist.merge_group_partials(g, gw // 6)
+            kdist.merge_endpoint_partials(e, ew // 2)
+            keys = kdist.merge_edge_keys(t[:tw])
+            eng.import_partials(L.PART_GROUPS, g.data_ptr(), gw, True)
+            eng.import_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
+            eng.finalize()
+            state["keys"] = keys.cpu() if not args.no_fetch else keys
+        elif not args.no_fetch:
+            state["keys"] = eng.triples()
+        if not args.no_fetch:
+            state["groups"] = eng.groups()
+            state["endpoints"] = eng.endpoints()
+
+    for _ in range(args.warmup):
+        step()
+    info = eng.info()
+    eng.kernel_times(reset=True)
+    eng.set_profiling(True)
+
+    def barrier():
+        dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    barrier()
+    t1 = time.perf_counter()
+    eng.set_profiling(False)
+    ktimes = eng.kernel_times(reset=True)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if world > 1 else "cpu")
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        tot = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        n_total = int(tot.item())
+    else:
+        n_total = n_local
+    secs = float(elapsed.item())
+    spans_per_s = n_total * args.steps / secs
+
+    # roofline of the dominant kernel (HIP events around every launch)
+    A = info["n_relations"]
+    per_kernel = {}
+    for k, (ms, calls) in ktimes.items():
+        if not calls:
+            continue
+        avg = ms / calls
+        alg = BYTES_PER_SPAN.get(k, 0) * n_local + BYTES_PER_RELATION.get(k, 0) * A
+        per_kernel[k] = {"avg_ms": round(avg, 4), "alg_bytes": alg,
+                         "gbs": round(alg / (avg * 1e-3) / 1e9, 1) if alg else None}
+    dom = max((k for k in per_kernel if per_kernel[k]["alg_bytes"]), key=lambda k: per_kernel[k]["avg_ms"])
+    d = per_kernel[dom]
+    kern_ms = sum(v["avg_ms"] for v in per_kernel.values()) / max(1, 1)
+    pipe_bytes = sum(v["alg_bytes"] for v in per_kernel.values())
+    if rank == 0:
+        cpu = None
+        if args.cpu_seconds > 0:
+            cpu = cpu_baseline(config, args.cpu_seconds)
+        line = {
+            "metric": "spans/sec -> endpoint dependency graph + combined stats (node); % HBM roofline",
+            "value": round(spans_per_s, 1),
+            "unit": "spans/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(secs / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64+f64",
+            "data": "synthetic (device-generated, seed 0x4B4D414D495A)",
+            "config": {
+                "workload": ("config3: 500-service/20k-endpoint mesh, depth-8 chains, "
+                             if config == synth.MESH else "config2: Bookinfo-shaped mesh, ")
+                + f"{n_local} spans/GPU ({traces_per_gpu} traces/GPU)"
+                + (", sharded by whole traces (config 4 at N=8)" if config == synth.MESH else ""),
+                "spans_per_gpu": n_local,
+                "spans_total": n_total,
+                "relations_per_gpu": A,
+                "edge_keys": info["n_triples"],
+                "parallelism": f"traceId-shard x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": d["gbs"],
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(d["gbs"] / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "pipeline_gbs": round(pipe_bytes / (kern_ms * 1e-3) / 1e9, 1),
+                "kernels": per_kernel,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    eng.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,225 @@
+/*
+ * kmz.h -- C ABI of the MI355X trace-processing engine (libkmz.so).
+ *
+ * Drop-in boundary for KMamiz's hot path (Zipkin span -> realtime data ->
+ * combined stats + endpoint dependency graph).  Every entry point is plain C:
+ * pointers and sizes only, no torch / HIP types in the signatures (streams are
+ * passed as opaque `void*` = hipStream_t).
+ *
+ * What each call replaces in the reference (TypeScript, /root/reference):
+ *
+ *   kmz_load          new Traces(Trace[][])                  src/classes/Traces.ts:17-21
+ *                     (the columnar form of Trace.ts:1-38, produced by the host
+ *                      ingest: ids hex->u64, strings interned into "shapes")
+ *   kmz_run(STATS_*)  Traces.toRealTimeData / combineLogsToRealtimeData
+ *                     + RealtimeDataList.toCombinedRealtimeData
+ *                                                            Traces.ts:27-106,
+ *                                                            RealtimeDataList.ts:22-118
+ *   kmz_run(DEPS)     Traces.toEndpointDependencies          Traces.ts:112-211
+ *                     reduced through EndpointDependencies.combineWith/trim
+ *                                                            EndpointDependencies.ts:91-112,499-563
+ *   kmz_get_groups    CombinedRealtimeDataList rows (count, latestTimestamp,
+ *                     latency.mean, latency.cv)              RealtimeDataList.ts:71-89
+ *   kmz_get_endpoints per-endpoint lastUsageTimestamp, first row,
+ *                     isDependedByExternal of the merged row Traces.ts:182-208,
+ *                                                            EndpointDependencies.ts:508-541
+ *   kmz_get_triples   the deduplicated (ancestor, descendant, distance) edge set
+ *                     behind dependingBy / dependingOn       Traces.ts:128-180
+ *   kmz_get_span_links per-span first-non-CLIENT ancestor + row position, from
+ *                     which the host materialises the exact per-row JSON
+ *                     (Traces.ts:145-190) at small batch sizes
+ *
+ * Ownership: the context owns its device buffers; results are copied into
+ * caller buffers (host or device, as each call states).  Calls on one context
+ * are not thread safe; contexts are independent (no global state besides the
+ * HIP runtime).  Every call returns 0 on success or a negative KMZ_E* code;
+ * kmz_last_error() gives a message.  (The reference's own failure modes:
+ * a TypeError from ExplodeUrl on malformed names is raised by the host ingest;
+ * the endless loop on cyclic parent chains, Traces.ts:131-142, becomes
+ * KMZ_E_CYCLE.)
+ */
+#ifndef KMZ_H
+#define KMZ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMZ_ABI_VERSION 1
+
+/* span kinds (Trace.kind) */
+#define KMZ_KIND_OTHER 0u
+#define KMZ_KIND_SERVER 1u
+#define KMZ_KIND_CLIENT 2u
+
+#define KMZ_NONE 0xFFFFFFFFu
+
+/* error codes */
+#define KMZ_OK 0
+#define KMZ_E_ARG -1      /* bad argument / shape mismatch */
+#define KMZ_E_HIP -2      /* HIP runtime error */
+#define KMZ_E_CYCLE -3    /* cyclic parentId chain (reference would not terminate) */
+#define KMZ_E_ZERO_ID -4  /* span_id 0 is reserved ("absent") */
+#define KMZ_E_RANGE -5    /* shape / status / endpoint id out of range */
+#define KMZ_E_OVERFLOW -6 /* internal table overflow (retried internally; surfaced if persistent) */
+#define KMZ_E_STATE -7    /* call order (e.g. kmz_get_* before kmz_run) */
+#define KMZ_E_RCCL -8     /* collective failed */
+
+/* kmz_run flags */
+#define KMZ_RUN_STATS_RT 1u  /* group by toRealTimeData identity (Traces.ts:32-46) */
+#define KMZ_RUN_STATS_TAG 2u /* group by combineLogsToRealtimeData identity (Traces.ts:73-99) */
+#define KMZ_RUN_DEPS 4u      /* dependency graph (Traces.ts:112-211) */
+#define KMZ_RUN_SPAN_LINKS 8u/* keep per-span links for kmz_get_span_links */
+
+/* where a kmz_load buffer lives */
+#define KMZ_MEM_HOST 0
+#define KMZ_MEM_DEVICE 1
+
+typedef struct kmz_ctx kmz_ctx;
+
+/* A batch of spans in flatten order (this._traces.flat(), Traces.ts:29). */
+typedef struct kmz_spans {
+  uint64_t n;
+  const uint64_t *span_id;   /* Trace.id as u64, never 0 (host remaps)        */
+  const uint64_t *parent_id; /* Trace.parentId, 0 = absent or "" (falsy)      */
+  const uint8_t *kind;       /* KMZ_KIND_*                                    */
+  const uint32_t *shape;     /* interned (name, tags) tuple                   */
+  const uint16_t *status;    /* interned tags["http.status_code"]             */
+  const uint32_t *duration;  /* Trace.duration, microseconds                  */
+  const int64_t *timestamp;  /* Trace.timestamp, microseconds                 */
+  uint64_t index_base;       /* global flatten index of span 0 (sharding)     */
+} kmz_spans;
+
+/* Per-shape identities, computed once per distinct shape on the host. */
+typedef struct kmz_shapes {
+  uint32_t n_shapes;
+  const uint32_t *rt_ep;  /* shape -> toRealTimeData uniqueEndpointName id          */
+  const uint32_t *tag_ep; /* shape -> combineLogsToRealtimeData uniqueEndpointName id */
+  const uint32_t *dep_ep; /* shape -> ToEndpointInfo uniqueEndpointName id          */
+  uint32_t n_rt_ep, n_tag_ep, n_dep_ep;
+  uint32_t n_status;
+} kmz_shapes;
+
+/* One (endpoint x status) group of toCombinedRealtimeData, finalised. */
+typedef struct kmz_group {
+  uint64_t combined;        /* subGroup.length                                  */
+  uint64_t first;           /* global index of the first span of the group      */
+  int64_t latest_timestamp; /* max Trace.timestamp (us)                         */
+  double mean;              /* ToPrecise(mean latency, ms)                      */
+  double cv;                /* ToPrecise(coefficient of variation)              */
+} kmz_group;
+
+/* Per dependency endpoint (ToEndpointInfo uniqueEndpointName). */
+typedef struct kmz_endpoint {
+  int64_t last_ts;    /* max timestamp (us) over its occurrences, INT64_MIN if none */
+  uint64_t first_row; /* global index of its first row, UINT64_MAX if no row      */
+  uint32_t external;  /* isDependedByExternal of that first row                   */
+  uint32_t has_row;
+} kmz_endpoint;
+
+typedef struct kmz_info {
+  uint64_t n_spans;
+  uint64_t n_server;    /* realtime rows                                  */
+  uint64_t n_rows;      /* dependency rows (unique ids whose last value is SERVER) */
+  uint64_t n_relations; /* (row, non-CLIENT ancestor) pairs = A            */
+  uint64_t n_triples;   /* unique (anc_ep, desc_ep, distance, on) keys     */
+  uint64_t n_dups;      /* span occurrences whose id was seen before       */
+  uint64_t max_depth;
+  uint64_t n_groups;    /* group slots = n_ep * n_status                    */
+  uint32_t flags;       /* internal error bits                             */
+  uint32_t pad;
+} kmz_info;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int kmz_abi_version(void);
+/* stream: hipStream_t to launch on (NULL = the context creates its own). */
+kmz_ctx *kmz_create(int device, void *stream);
+void kmz_destroy(kmz_ctx *ctx);
+const char *kmz_last_error(kmz_ctx *ctx);
+int kmz_sync(kmz_ctx *ctx);
+
+/* ---- input --------------------------------------------------------------- */
+/* where: KMZ_MEM_HOST copies the arrays to HBM; KMZ_MEM_DEVICE borrows device
+ * pointers (must stay valid until the next kmz_load / kmz_destroy). The shape
+ * table is always host memory. */
+int kmz_load(kmz_ctx *ctx, const kmz_spans *spans, const kmz_shapes *shapes, int where);
+
+/* ---- compute (asynchronous on the context stream) ------------------------ */
+int kmz_run(kmz_ctx *ctx, uint32_t flags);
+
+/* ---- results (synchronise the stream) ------------------------------------- */
+int kmz_get_info(kmz_ctx *ctx, kmz_info *out);
+/* finalised groups, dense [n_ep * n_status] (ep-major), of the last STATS run */
+int kmz_get_groups(kmz_ctx *ctx, kmz_group *out, uint64_t cap);
+int kmz_get_endpoints(kmz_ctx *ctx, kmz_endpoint *out, uint64_t cap);
+/* unique edge keys, unordered: key = anc_ep<<40 | desc_ep<<16 | distance<<1 | on */
+int kmz_get_triples(kmz_ctx *ctx, uint64_t *out, uint64_t cap, uint64_t *n_out);
+/* per span: first non-CLIENT ancestor (KMZ_NONE if none) and, for rows, the
+ * row's global first-occurrence index (KMZ_NONE if the span is not a row) */
+int kmz_get_span_links(kmz_ctx *ctx, uint32_t *cparent, uint64_t *rowpos, uint64_t cap);
+
+/* ---- multi-GPU partials (traceId-sharded batches) ------------------------ */
+/* Raw group partials: 6 arrays of n_groups u64, in this order:
+ *   [0] count, [1] sum(dur), [2] sum(lo32(dur^2)), [3] sum(hi32(dur^2))  (SUM)
+ *   [4] max(timestamp ^ 1<<63)                                           (MAX)
+ *   [5] min(first global index)                                          (MIN)
+ * Endpoint partials: 2 arrays of n_dep_ep u64:
+ *   [0] max(timestamp ^ 1<<63)  (MAX), [1] min(first_row<<1 | !external) (MIN) */
+int kmz_group_partials(kmz_ctx *ctx, void **dev_ptr, uint64_t *n_groups);
+int kmz_endpoint_partials(kmz_ctx *ctx, void **dev_ptr, uint64_t *n_ep);
+/* Copy partials between the context and a caller buffer (host or device
+ * memory of the same GPU), for reductions done by the caller (e.g. RCCL via
+ * torch.distributed).  which: KMZ_PART_*; direction 0 = export (ctx -> buf),
+ * 1 = import (buf -> ctx; not for triples).  kmz_partials_size gives the word
+ * count (u64) of each. */
+#define KMZ_PART_GROUPS 0
+#define KMZ_PART_ENDPOINTS 1
+#define KMZ_PART_TRIPLES 2
+int kmz_partials_size(kmz_ctx *ctx, int which, uint64_t *words);
+int kmz_partials_copy(kmz_ctx *ctx, int which, void *buf, uint64_t words, int mem, int direction);
+/* re-finalise the groups after the partials were reduced in place */
+int kmz_finalize(kmz_ctx *ctx);
+/* host-side finalisation of one partial (same arithmetic as the device) */
+void kmz_finalize_host(const uint64_t *partials, uint64_t n_groups, kmz_group *out);
+
+/* ---- per-kernel timing (HIP events around each launch) ------------------- */
+#define KMZ_K_MEMSET 0
+#define KMZ_K_BUILD 1   /* K1 span-id table build     */
+#define KMZ_K_FIXUP 2   /* K1 duplicate-id fixup      */
+#define KMZ_K_RESOLVE 3 /* K2 parent join + contraction */
+#define KMZ_K_STATS 4   /* K3 segmented reduction     */
+#define KMZ_K_WALK 5    /* K4 ancestor traversal      */
+#define KMZ_K_FINAL 6   /* finalise + compaction      */
+#define KMZ_K_COUNT 7
+int kmz_set_profiling(kmz_ctx *ctx, int on);
+/* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
+int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);
+
+/* ---- synthetic workload (BASELINE.json configs 2-5), generated in HBM ---- */
+#define KMZ_SYNTH_BOOKINFO 2
+#define KMZ_SYNTH_MESH 3
+typedef struct kmz_synth_desc {
+  uint32_t n_shapes, n_status;
+  uint32_t n_endpoints;
+} kmz_synth_desc;
+int kmz_synth_describe(int config, kmz_synth_desc *out);
+/* Generate traces [trace_begin, trace_end) of `config` into the context as its
+ * loaded batch (device resident); index_base = number of spans in the traces
+ * before trace_begin (computed by the call). Returns the span count. */
+int kmz_synth_load(kmz_ctx *ctx, int config, uint64_t seed, uint64_t trace_begin, uint64_t trace_end,
+                   uint64_t *n_spans_out);
+/* Host-side generation of the same traces into caller arrays (cap spans);
+ * trace_off receives trace_end-trace_begin+1 offsets. */
+int kmz_synth_host(int config, uint64_t seed, uint64_t trace_begin, uint64_t trace_end, uint64_t cap,
+                   uint64_t *span_id, uint64_t *parent_id, uint8_t *kind, uint32_t *shape, uint16_t *status,
+                   uint32_t *duration, int64_t *timestamp, uint64_t *trace_off, uint64_t *n_spans_out);
+/* identity tables of a synthetic config (shape == endpoint for synthetic) */
+int kmz_synth_shape_ids(int config, uint32_t *rt_ep, uint32_t *tag_ep, uint32_t *dep_ep, uint32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMZ_H */

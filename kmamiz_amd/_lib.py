@@ -1,0 +1,162 @@
+"""ctypes binding of ``include/kmz.h`` (libkmz.so, built in-tree).
+
+The product path is the HIP engine: importing this module fails loudly when
+``kmamiz_amd/libkmz.so`` is missing, and :func:`create` raises when no GPU is
+visible.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkmz.so")
+
+KIND_OTHER, KIND_SERVER, KIND_CLIENT = 0, 1, 2
+NONE32 = 0xFFFFFFFF
+NONE64 = 0xFFFFFFFFFFFFFFFF
+
+RUN_STATS_RT, RUN_STATS_TAG, RUN_DEPS, RUN_SPAN_LINKS = 1, 2, 4, 8
+MEM_HOST, MEM_DEVICE = 0, 1
+
+ERRORS = {
+    -1: "KMZ_E_ARG",
+    -2: "KMZ_E_HIP",
+    -3: "KMZ_E_CYCLE",
+    -4: "KMZ_E_ZERO_ID",
+    -5: "KMZ_E_RANGE",
+    -6: "KMZ_E_OVERFLOW",
+    -7: "KMZ_E_STATE",
+    -8: "KMZ_E_RCCL",
+}
+
+KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final"]
+SYNTH_BOOKINFO, SYNTH_MESH = 2, 3
+PART_GROUPS, PART_ENDPOINTS, PART_TRIPLES = 0, 1, 2
+
+
+class KmzError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class CycleError(KmzError):
+    """The reference loops forever on a cyclic parentId chain (Traces.ts:131-142)."""
+
+
+class Spans(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("span_id", C.c_void_p),
+        ("parent_id", C.c_void_p),
+        ("kind", C.c_void_p),
+        ("shape", C.c_void_p),
+        ("status", C.c_void_p),
+        ("duration", C.c_void_p),
+        ("timestamp", C.c_void_p),
+        ("index_base", C.c_uint64),
+    ]
+
+
+class Shapes(C.Structure):
+    _fields_ = [
+        ("n_shapes", C.c_uint32),
+        ("rt_ep", C.c_void_p),
+        ("tag_ep", C.c_void_p),
+        ("dep_ep", C.c_void_p),
+        ("n_rt_ep", C.c_uint32),
+        ("n_tag_ep", C.c_uint32),
+        ("n_dep_ep", C.c_uint32),
+        ("n_status", C.c_uint32),
+    ]
+
+
+class Info(C.Structure):
+    _fields_ = [
+        ("n_spans", C.c_uint64),
+        ("n_server", C.c_uint64),
+        ("n_rows", C.c_uint64),
+        ("n_relations", C.c_uint64),
+        ("n_triples", C.c_uint64),
+        ("n_dups", C.c_uint64),
+        ("max_depth", C.c_uint64),
+        ("n_groups", C.c_uint64),
+        ("flags", C.c_uint32),
+        ("pad", C.c_uint32),
+    ]
+
+
+class SynthDesc(C.Structure):
+    _fields_ = [("n_shapes", C.c_uint32), ("n_status", C.c_uint32), ("n_endpoints", C.c_uint32)]
+
+
+GROUP_DTYPE = np.dtype(
+    [("combined", "<u8"), ("first", "<u8"), ("latest_timestamp", "<i8"), ("mean", "<f8"), ("cv", "<f8")]
+)
+ENDPOINT_DTYPE = np.dtype([("last_ts", "<i8"), ("first_row", "<u8"), ("external", "<u4"), ("has_row", "<u4")])
+
+# (name, restype, argtypes) for every symbol declared in include/kmz.h
+_P = C.c_void_p
+SIGNATURES = [
+    ("kmz_abi_version", C.c_int, []),
+    ("kmz_create", _P, [C.c_int, _P]),
+    ("kmz_destroy", None, [_P]),
+    ("kmz_last_error", C.c_char_p, [_P]),
+    ("kmz_sync", C.c_int, [_P]),
+    ("kmz_load", C.c_int, [_P, C.POINTER(Spans), C.POINTER(Shapes), C.c_int]),
+    ("kmz_run", C.c_int, [_P, C.c_uint32]),
+    ("kmz_get_info", C.c_int, [_P, C.POINTER(Info)]),
+    ("kmz_get_groups", C.c_int, [_P, _P, C.c_uint64]),
+    ("kmz_get_endpoints", C.c_int, [_P, _P, C.c_uint64]),
+    ("kmz_get_triples", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("kmz_get_span_links", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("kmz_group_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    ("kmz_endpoint_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
+    ("kmz_partials_size", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
+    ("kmz_partials_copy", C.c_int, [_P, C.c_int, _P, C.c_uint64, C.c_int, C.c_int]),
+    ("kmz_finalize", C.c_int, [_P]),
+    ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
+    ("kmz_set_profiling", C.c_int, [_P, C.c_int]),
+    ("kmz_kernel_times", C.c_int, [_P, _P, _P, C.c_int]),
+    ("kmz_synth_describe", C.c_int, [C.c_int, C.POINTER(SynthDesc)]),
+    ("kmz_synth_load", C.c_int, [_P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
+    (
+        "kmz_synth_host",
+        C.c_int,
+        [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, _P, _P, _P, _P, _P, _P, _P, _P, C.POINTER(C.c_uint64)],
+    ),
+    ("kmz_synth_shape_ids", C.c_int, [C.c_int, _P, _P, _P, C.c_uint32]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libkmz.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build()) first")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def check(ctx, rc):
+    if rc != 0:
+        msg = lib().kmz_last_error(ctx).decode(errors="replace") if ctx else ""
+        if rc == -3:
+            raise CycleError(rc, msg)
+        raise KmzError(rc, msg)
+    return rc

@@ -1,0 +1,721 @@
+// kmz_api.hip -- context, buffers, launch sequencing and the C ABI (kmz.h).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kmz_kernels.h"
+
+using namespace kmz;
+
+namespace {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+
+struct EventPair {
+  hipEvent_t a = nullptr, b = nullptr;
+  int kernel = 0;
+};
+
+}  // namespace
+
+struct kmz_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+
+  // loaded batch
+  bool loaded = false;
+  uint64_t n = 0, index_base = 0;
+  const uint64_t *sid = nullptr, *pid = nullptr;
+  const uint8_t *kind = nullptr;
+  const uint32_t *shape = nullptr;
+  const uint16_t *status = nullptr;
+  const uint32_t *dur = nullptr;
+  const int64_t *ts = nullptr;
+  DevBuf in_sid, in_pid, in_kind, in_shape, in_status, in_dur, in_ts;
+
+  // shapes
+  uint32_t n_shapes = 0, n_rt = 0, n_tag = 0, n_dep = 0, n_status = 0;
+  DevBuf d_rt, d_tag, d_dep;
+
+  // workspace
+  DevBuf table, dups, dkey, dval, cparent, rowpos, grp, grp_final, epp, trip, trip_out, counters, stats64, scratch;
+  DevBuf synth_cnt, synth_off, dur_table;
+  uint64_t cap = 0, tcap = 1ull << 16;
+  uint32_t dcap = 1024;
+
+  // last run
+  uint32_t ran = 0;
+  uint32_t G = 0;        // group slots of the last stats run
+  uint32_t ep_mode = 0;  // which ep table the groups use
+  bool links = false;
+
+  // profiling
+  bool prof = false;
+  std::vector<EventPair> pending;
+  std::vector<hipEvent_t> pool;
+  double ms[KMZ_K_COUNT] = {0};
+  uint64_t calls[KMZ_K_COUNT] = {0};
+};
+
+namespace {
+
+int fail(kmz_ctx *c, int code, const std::string &msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(c, x)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess) return fail((c), KMZ_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+int ensure(kmz_ctx *c, DevBuf &b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return 0;
+  if (b.p) {
+    hipStreamSynchronize(c->stream);
+    hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) return fail(c, KMZ_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+  b.bytes = bytes;
+  return 0;
+}
+
+template <class T>
+T *P(DevBuf &b) {
+  return reinterpret_cast<T *>(b.p);
+}
+
+hipEvent_t ev_get(kmz_ctx *c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+struct Timed {
+  kmz_ctx *c;
+  EventPair ep;
+  Timed(kmz_ctx *ctx, int k) : c(ctx) {
+    if (!c->prof) return;
+    ep.kernel = k;
+    ep.a = ev_get(c);
+    ep.b = ev_get(c);
+    hipEventRecord(ep.a, c->stream);
+  }
+  ~Timed() {
+    if (!c->prof) return;
+    hipEventRecord(ep.b, c->stream);
+    c->pending.push_back(ep);
+  }
+};
+
+void harvest(kmz_ctx *c) {
+  for (auto &ep : c->pending) {
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, ep.a, ep.b) == hipSuccess) {
+      c->ms[ep.kernel] += t;
+      c->calls[ep.kernel] += 1;
+    }
+    c->pool.push_back(ep.a);
+    c->pool.push_back(ep.b);
+  }
+  c->pending.clear();
+}
+
+// ---- lognormal(ln 2000us, 0.75) quantile table (host computed, shared) ----
+double inv_norm(double p) {  // Acklam's rational approximation, |rel err| < 1.2e-9
+  static const double a[] = {-3.969683028665376e+01, 2.209460984245205e+02, -2.759285104469687e+02,
+                             1.383577518672690e+02,  -3.066479806614716e+01, 2.506628277459239e+00};
+  static const double b[] = {-5.447609879822406e+01, 1.615858368580409e+02, -1.556989798598866e+02,
+                             6.680131188771972e+01,  -1.328068155288572e+01};
+  static const double cc[] = {-7.784894002430293e-03, -3.223964580411365e-01, -2.400758277161838e+00,
+                              -2.549732539343734e+00, 4.374664141464968e+00,  2.938163982698783e+00};
+  static const double d[] = {7.784695709041462e-03, 3.224671290700398e-01, 2.445134137142996e+00,
+                             3.754408661907416e+00};
+  const double pl = 0.02425, ph = 1 - pl;
+  if (p < pl) {
+    double q = std::sqrt(-2 * std::log(p));
+    return (((((cc[0] * q + cc[1]) * q + cc[2]) * q + cc[3]) * q + cc[4]) * q + cc[5]) /
+           ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1);
+  }
+  if (p <= ph) {
+    double q = p - 0.5, r = q * q;
+    return (((((a[0] * r + a[1]) * r + a[2]) * r + a[3]) * r + a[4]) * r + a[5]) * q /
+           (((((b[0] * r + b[1]) * r + b[2]) * r + b[3]) * r + b[4]) * r + 1);
+  }
+  double q = std::sqrt(-2 * std::log(1 - p));
+  return -(((((cc[0] * q + cc[1]) * q + cc[2]) * q + cc[3]) * q + cc[4]) * q + cc[5]) /
+         ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1);
+}
+
+const std::vector<uint32_t> &dur_table_host() {
+  static std::vector<uint32_t> t;
+  if (t.empty()) {
+    const uint32_t n = 1u << SYN_DUR_BITS;
+    t.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+      double z = inv_norm((i + 0.5) / n);
+      double v = std::exp(std::log(2000.0) + 0.75 * z);
+      double r = std::floor(v + 0.5);
+      if (r < 50) r = 50;
+      if (r > 1e7) r = 1e7;
+      t[i] = (uint32_t)r;
+    }
+  }
+  return t;
+}
+
+int check_flags(kmz_ctx *c, uint32_t flags) {
+  if (flags & F_CYCLE) return fail(c, KMZ_E_CYCLE, "cyclic parentId chain (depth > 16384)");
+  if (flags & F_ZERO_ID) return fail(c, KMZ_E_ZERO_ID, "span_id 0 is reserved");
+  if (flags & F_RANGE) return fail(c, KMZ_E_RANGE, "shape/status/endpoint id out of range");
+  if (flags & F_TABLE_FULL) return fail(c, KMZ_E_OVERFLOW, "span table full");
+  return KMZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kmz_abi_version(void) { return KMZ_ABI_VERSION; }
+
+kmz_ctx *kmz_create(int device, void *stream) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  kmz_ctx *c = new kmz_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      return nullptr;
+    }
+    c->own_stream = true;
+  }
+  if (ensure(c, c->counters, C_COUNT * 4) || ensure(c, c->stats64, S_COUNT * 8)) {
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+void kmz_destroy(kmz_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  harvest(c);
+  for (auto e : c->pool) hipEventDestroy(e);
+  DevBuf *bufs[] = {&c->in_sid, &c->in_pid,    &c->in_kind,  &c->in_shape,  &c->in_status, &c->in_dur,
+                    &c->in_ts,  &c->d_rt,      &c->d_tag,    &c->d_dep,     &c->table,     &c->dups,
+                    &c->dkey,   &c->dval,      &c->cparent,  &c->rowpos,    &c->grp,       &c->grp_final,
+                    &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->stats64,   &c->scratch,
+                    &c->synth_cnt, &c->synth_off, &c->dur_table};
+  for (DevBuf *b : bufs)
+    if (b->p) hipFree(b->p);
+  if (c->own_stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char *kmz_last_error(kmz_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int kmz_sync(kmz_ctx *c) {
+  if (!c) return KMZ_E_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  harvest(c);
+  return KMZ_OK;
+}
+
+static int load_shapes(kmz_ctx *c, const kmz_shapes *sh) {
+  if (!sh || !sh->rt_ep || !sh->tag_ep || !sh->dep_ep) return fail(c, KMZ_E_ARG, "shape table missing");
+  if (sh->n_dep_ep >= (1u << 24) || sh->n_status == 0 || sh->n_status > 65535)
+    return fail(c, KMZ_E_ARG, "endpoint/status count out of range");
+  c->n_shapes = sh->n_shapes;
+  c->n_rt = sh->n_rt_ep;
+  c->n_tag = sh->n_tag_ep;
+  c->n_dep = sh->n_dep_ep;
+  c->n_status = sh->n_status;
+  size_t b = (size_t)sh->n_shapes * 4;
+  if (ensure(c, c->d_rt, b) || ensure(c, c->d_tag, b) || ensure(c, c->d_dep, b)) return KMZ_E_HIP;
+  if (b) {
+    HIPCHK(c, hipMemcpyAsync(c->d_rt.p, sh->rt_ep, b, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_tag.p, sh->tag_ep, b, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_dep.p, sh->dep_ep, b, hipMemcpyHostToDevice, c->stream));
+  }
+  return KMZ_OK;
+}
+
+int kmz_load(kmz_ctx *c, const kmz_spans *s, const kmz_shapes *sh, int where) {
+  if (!c || !s) return KMZ_E_ARG;
+  hipSetDevice(c->device);
+  if (s->n >= 0xFFFFFFFFull) return fail(c, KMZ_E_ARG, "batch too large (n must be < 2^32-1)");
+  if (s->n && (!s->span_id || !s->parent_id || !s->kind || !s->shape || !s->status || !s->duration || !s->timestamp))
+    return fail(c, KMZ_E_ARG, "null column");
+  int r = load_shapes(c, sh);
+  if (r) return r;
+  c->n = s->n;
+  c->index_base = s->index_base;
+  c->ran = 0;
+  if (where == KMZ_MEM_DEVICE) {
+    c->sid = s->span_id;
+    c->pid = s->parent_id;
+    c->kind = s->kind;
+    c->shape = s->shape;
+    c->status = s->status;
+    c->dur = s->duration;
+    c->ts = s->timestamp;
+  } else {
+    size_t n = s->n;
+    if (ensure(c, c->in_sid, n * 8) || ensure(c, c->in_pid, n * 8) || ensure(c, c->in_kind, n) ||
+        ensure(c, c->in_shape, n * 4) || ensure(c, c->in_status, n * 2) || ensure(c, c->in_dur, n * 4) ||
+        ensure(c, c->in_ts, n * 8))
+      return KMZ_E_HIP;
+    if (n) {
+      HIPCHK(c, hipMemcpyAsync(c->in_sid.p, s->span_id, n * 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->in_pid.p, s->parent_id, n * 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->in_kind.p, s->kind, n, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->in_shape.p, s->shape, n * 4, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->in_status.p, s->status, n * 2, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->in_dur.p, s->duration, n * 4, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->in_ts.p, s->timestamp, n * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    c->sid = P<uint64_t>(c->in_sid);
+    c->pid = P<uint64_t>(c->in_pid);
+    c->kind = P<uint8_t>(c->in_kind);
+    c->shape = P<uint32_t>(c->in_shape);
+    c->status = P<uint16_t>(c->in_status);
+    c->dur = P<uint32_t>(c->in_dur);
+    c->ts = P<int64_t>(c->in_ts);
+  }
+  c->loaded = true;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+static int run_deps(kmz_ctx *c, bool links) {
+  const uint32_t n = (uint32_t)c->n;
+  c->cap = c->n * 5 / 3 + 64;  // load factor 0.6
+  if (ensure(c, c->table, c->cap * 8) || ensure(c, c->dups, (size_t)(n + 1) * sizeof(DupEntry)) ||
+      ensure(c, c->dkey, (size_t)c->dcap * 4) || ensure(c, c->dval, (size_t)c->dcap * 4) ||
+      ensure(c, c->cparent, (size_t)(n + 1) * 4) || ensure(c, c->trip, c->tcap * 8) ||
+      ensure(c, c->trip_out, c->tcap * 8) || ensure(c, c->epp, (size_t)(c->n_dep + 1) * 16) ||
+      (links && ensure(c, c->rowpos, (size_t)(n + 1) * 8)))
+    return KMZ_E_HIP;
+  unsigned int *cnt = P<unsigned int>(c->counters);
+  unsigned long long *st = P<unsigned long long>(c->stats64);
+  unsigned long long *epp = P<unsigned long long>(c->epp);
+  {
+    Timed t(c, KMZ_K_MEMSET);
+    HIPCHK(c, hipMemsetAsync(c->table.p, 0, c->cap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->dkey.p, 0, (size_t)c->dcap * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->dval.p, 0xFF, (size_t)c->dcap * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
+  }
+  {
+    Timed t(c, KMZ_K_BUILD);
+    launch_build(c->stream, c->sid, n, P<unsigned long long>(c->table), c->cap, P<DupEntry>(c->dups), n + 1, cnt);
+  }
+  {
+    Timed t(c, KMZ_K_FIXUP);
+    launch_fixup(c->stream, P<DupEntry>(c->dups), cnt, n + 1, P<unsigned long long>(c->table), P<unsigned int>(c->dkey),
+                 P<unsigned int>(c->dval), c->dcap);
+  }
+  {
+    Timed t(c, KMZ_K_RESOLVE);
+    launch_resolve(c->stream, c->sid, c->pid, c->kind, n, P<unsigned long long>(c->table), c->cap,
+                   P<uint32_t>(c->cparent), cnt);
+  }
+  {
+    Timed t(c, KMZ_K_WALK);
+    launch_walk(c->stream, c->sid, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
+                c->n_shapes, c->n_dep, c->index_base, P<unsigned long long>(c->table), c->cap,
+                P<unsigned int>(c->dkey), P<unsigned int>(c->dval), c->dcap, P<unsigned long long>(c->trip), c->tcap,
+                epp, epp + c->n_dep, links ? P<unsigned long long>(c->rowpos) : nullptr, cnt, st);
+  }
+  {
+    Timed t(c, KMZ_K_FINAL);
+    launch_compact(c->stream, P<unsigned long long>(c->trip), c->tcap, P<unsigned long long>(c->trip_out),
+                   st + S_TRIP_OUT);
+  }
+  return KMZ_OK;
+}
+
+static int run_stats(kmz_ctx *c, uint32_t mode) {
+  const uint32_t n = (uint32_t)c->n;
+  uint32_t n_ep = mode == KMZ_RUN_STATS_RT ? c->n_rt : c->n_tag;
+  const uint32_t *tab = mode == KMZ_RUN_STATS_RT ? P<uint32_t>(c->d_rt) : P<uint32_t>(c->d_tag);
+  uint64_t G = (uint64_t)n_ep * c->n_status;
+  if (G >= 0xFFFFFFFFull) return fail(c, KMZ_E_ARG, "too many groups");
+  c->G = (uint32_t)G;
+  c->ep_mode = mode;
+  if (ensure(c, c->grp, (G + 1) * 48) || ensure(c, c->grp_final, (G + 1) * sizeof(kmz_group))) return KMZ_E_HIP;
+  unsigned long long *grp = P<unsigned long long>(c->grp);
+  {
+    Timed t(c, KMZ_K_MEMSET);
+    HIPCHK(c, hipMemsetAsync(grp, 0, G * 40, c->stream));
+    HIPCHK(c, hipMemsetAsync(grp + 5 * G, 0xFF, G * 8, c->stream));
+  }
+  {
+    Timed t(c, KMZ_K_STATS);
+    launch_stats(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, tab, c->n_shapes, n_ep, c->n_status,
+                 c->index_base, grp, P<unsigned int>(c->counters), P<unsigned long long>(c->stats64) + S_SERVER);
+  }
+  {
+    Timed t(c, KMZ_K_FINAL);
+    launch_finalize(c->stream, grp, c->G, P<kmz_group>(c->grp_final));
+  }
+  return KMZ_OK;
+}
+
+int kmz_run(kmz_ctx *c, uint32_t flags) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_run before kmz_load");
+  uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
+  if (smode == (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG)) return fail(c, KMZ_E_ARG, "choose one stats identity per run");
+  hipSetDevice(c->device);
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->stats64.p, 0, S_COUNT * 8, c->stream));
+    int r;
+    if (smode && (r = run_stats(c, smode))) return r;
+    if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, (flags & KMZ_RUN_SPAN_LINKS) != 0))) return r;
+    unsigned int h[C_COUNT];
+    HIPCHK(c, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    harvest(c);
+    bool retry = false;
+    if (h[C_FLAGS] & F_TRIPLE_OVERFLOW) {
+      c->tcap *= 4;
+      retry = true;
+    }
+    if ((flags & KMZ_RUN_DEPS) && (uint64_t)h[C_DUPS] * 2 > c->dcap) {
+      c->dcap = (uint32_t)std::min<uint64_t>(4ull * h[C_DUPS] + 1024, 0xFFFFFFF0ull);
+      retry = true;
+    }
+    if (!retry) {
+      int e = check_flags(c, h[C_FLAGS]);
+      if (e) return e;
+      c->ran = flags;
+      c->links = (flags & KMZ_RUN_SPAN_LINKS) != 0;
+      return KMZ_OK;
+    }
+  }
+  return fail(c, KMZ_E_OVERFLOW, "table growth did not converge");
+}
+
+int kmz_get_info(kmz_ctx *c, kmz_info *out) {
+  if (!c || !out) return KMZ_E_ARG;
+  unsigned int h[C_COUNT];
+  unsigned long long s[S_COUNT];
+  HIPCHK(c, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  memset(out, 0, sizeof(*out));
+  out->n_spans = c->n;
+  out->n_server = s[S_SERVER];
+  out->n_rows = s[S_ROWS];
+  out->n_relations = s[S_REL];
+  out->n_triples = s[S_TRIP_OUT];
+  out->n_dups = h[C_DUPS];
+  out->max_depth = s[S_MAXD];
+  out->n_groups = c->G;
+  out->flags = h[C_FLAGS];
+  return KMZ_OK;
+}
+
+int kmz_get_groups(kmz_ctx *c, kmz_group *out, uint64_t cap) {
+  if (!c) return KMZ_E_ARG;
+  if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
+  if (cap < c->G) return fail(c, KMZ_E_ARG, "output too small");
+  if (c->G) HIPCHK(c, hipMemcpyAsync(out, c->grp_final.p, (size_t)c->G * sizeof(kmz_group), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_get_endpoints(kmz_ctx *c, kmz_endpoint *out, uint64_t cap) {
+  if (!c) return KMZ_E_ARG;
+  if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+  if (cap < c->n_dep) return fail(c, KMZ_E_ARG, "output too small");
+  std::vector<uint64_t> h((size_t)c->n_dep * 2 + 1);
+  if (c->n_dep)
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->epp.p, (size_t)c->n_dep * 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (uint32_t e = 0; e < c->n_dep; ++e) {
+    uint64_t tsx = h[e], f = h[c->n_dep + e];
+    out[e].last_ts = tsx == 0 ? INT64_MIN : (int64_t)(tsx ^ TS_BIAS);
+    out[e].has_row = f != ~0ull;
+    out[e].first_row = f == ~0ull ? ~0ull : (f >> 1);
+    out[e].external = f == ~0ull ? 0u : (uint32_t)((f & 1) == 0);
+  }
+  return KMZ_OK;
+}
+
+int kmz_get_triples(kmz_ctx *c, uint64_t *out, uint64_t cap, uint64_t *n_out) {
+  if (!c || !n_out) return KMZ_E_ARG;
+  if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+  unsigned long long s[S_COUNT];
+  HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *n_out = s[S_TRIP_OUT];
+  if (!out) return KMZ_OK;
+  if (cap < s[S_TRIP_OUT]) return fail(c, KMZ_E_ARG, "output too small");
+  if (s[S_TRIP_OUT])
+    HIPCHK(c, hipMemcpyAsync(out, c->trip_out.p, s[S_TRIP_OUT] * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_get_span_links(kmz_ctx *c, uint32_t *cparent, uint64_t *rowpos, uint64_t cap) {
+  if (!c) return KMZ_E_ARG;
+  if (!(c->ran & KMZ_RUN_DEPS) || !c->links) return fail(c, KMZ_E_STATE, "run with KMZ_RUN_DEPS|KMZ_RUN_SPAN_LINKS first");
+  if (cap < c->n) return fail(c, KMZ_E_ARG, "output too small");
+  if (c->n) {
+    if (cparent) HIPCHK(c, hipMemcpyAsync(cparent, c->cparent.p, c->n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (rowpos) HIPCHK(c, hipMemcpyAsync(rowpos, c->rowpos.p, c->n * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_group_partials(kmz_ctx *c, void **dev_ptr, uint64_t *n_groups) {
+  if (!c || !dev_ptr || !n_groups) return KMZ_E_ARG;
+  if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
+  *dev_ptr = c->grp.p;
+  *n_groups = c->G;
+  return KMZ_OK;
+}
+
+int kmz_endpoint_partials(kmz_ctx *c, void **dev_ptr, uint64_t *n_ep) {
+  if (!c || !dev_ptr || !n_ep) return KMZ_E_ARG;
+  if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+  *dev_ptr = c->epp.p;
+  *n_ep = c->n_dep;
+  return KMZ_OK;
+}
+
+int kmz_partials_size(kmz_ctx *c, int which, uint64_t *words) {
+  if (!c || !words) return KMZ_E_ARG;
+  if (which == KMZ_PART_GROUPS) {
+    if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
+    *words = 6ull * c->G;
+  } else if (which == KMZ_PART_ENDPOINTS) {
+    if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+    *words = 2ull * c->n_dep;
+  } else if (which == KMZ_PART_TRIPLES) {
+    if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+    unsigned long long s[S_COUNT];
+    HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *words = s[S_TRIP_OUT];
+  } else {
+    return fail(c, KMZ_E_ARG, "unknown partial");
+  }
+  return KMZ_OK;
+}
+
+int kmz_partials_copy(kmz_ctx *c, int which, void *buf, uint64_t words, int mem, int direction) {
+  uint64_t need = 0;
+  int r = kmz_partials_size(c, which, &need);
+  if (r) return r;
+  if (words < need) return fail(c, KMZ_E_ARG, "buffer too small");
+  if (which == KMZ_PART_TRIPLES && direction) return fail(c, KMZ_E_ARG, "triples are export-only");
+  void *mine = which == KMZ_PART_GROUPS ? c->grp.p : (which == KMZ_PART_ENDPOINTS ? c->epp.p : c->trip_out.p);
+  hipMemcpyKind k = direction ? (mem == KMZ_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice)
+                              : (mem == KMZ_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost);
+  if (need) {
+    if (direction)
+      HIPCHK(c, hipMemcpyAsync(mine, buf, need * 8, k, c->stream));
+    else
+      HIPCHK(c, hipMemcpyAsync(buf, mine, need * 8, k, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_finalize(kmz_ctx *c) {
+  if (!c) return KMZ_E_ARG;
+  if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
+  {
+    Timed t(c, KMZ_K_FINAL);
+    launch_finalize(c->stream, P<unsigned long long>(c->grp), c->G, P<kmz_group>(c->grp_final));
+  }
+  return kmz_sync(c);
+}
+
+void kmz_finalize_host(const uint64_t *p, uint64_t G, kmz_group *out) {
+  for (uint64_t g = 0; g < G; ++g) {
+    kmz_group r;
+    r.combined = p[g];
+    r.first = p[5 * G + g];
+    r.latest_timestamp = (int64_t)(p[4 * G + g] ^ TS_BIAS);
+    finalize_moments(p[g], p[G + g], p[2 * G + g], p[3 * G + g], &r.mean, &r.cv);
+    out[g] = r;
+  }
+}
+
+int kmz_set_profiling(kmz_ctx *c, int on) {
+  if (!c) return KMZ_E_ARG;
+  c->prof = on != 0;
+  return KMZ_OK;
+}
+
+int kmz_kernel_times(kmz_ctx *c, double *ms, uint64_t *calls, int reset) {
+  if (!c) return KMZ_E_ARG;
+  int r = kmz_sync(c);
+  if (r) return r;
+  for (int k = 0; k < KMZ_K_COUNT; ++k) {
+    if (ms) ms[k] = c->ms[k];
+    if (calls) calls[k] = c->calls[k];
+    if (reset) {
+      c->ms[k] = 0;
+      c->calls[k] = 0;
+    }
+  }
+  return KMZ_OK;
+}
+
+// ---- synthetic ---------------------------------------------------------------
+int kmz_synth_describe(int config, kmz_synth_desc *out) {
+  if (!out) return KMZ_E_ARG;
+  if (config == KMZ_SYNTH_BOOKINFO) {
+    out->n_shapes = out->n_endpoints = BOOK_EPS;
+  } else if (config == KMZ_SYNTH_MESH) {
+    out->n_shapes = out->n_endpoints = MESH_EPS;
+  } else {
+    return KMZ_E_ARG;
+  }
+  out->n_status = 3;
+  return KMZ_OK;
+}
+
+int kmz_synth_shape_ids(int config, uint32_t *rt, uint32_t *tag, uint32_t *dep, uint32_t cap) {
+  kmz_synth_desc d;
+  if (kmz_synth_describe(config, &d)) return KMZ_E_ARG;
+  if (cap < d.n_shapes) return KMZ_E_ARG;
+  for (uint32_t i = 0; i < d.n_shapes; ++i) {
+    if (rt) rt[i] = i;
+    if (tag) tag[i] = i;
+    if (dep) dep[i] = i;
+  }
+  return KMZ_OK;
+}
+
+int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t t1, uint64_t *n_out) {
+  if (!c || t1 < t0) return KMZ_E_ARG;
+  kmz_synth_desc d;
+  if (kmz_synth_describe(config, &d)) return fail(c, KMZ_E_ARG, "unknown synthetic config");
+  hipSetDevice(c->device);
+  const auto &dt = dur_table_host();
+  if (ensure(c, c->dur_table, dt.size() * 4)) return KMZ_E_HIP;
+  HIPCHK(c, hipMemcpyAsync(c->dur_table.p, dt.data(), dt.size() * 4, hipMemcpyHostToDevice, c->stream));
+  uint64_t nt = t1 - t0;
+  // spans before t0 (global flatten index of the first generated span)
+  uint64_t base = 0;
+  size_t tmp_bytes = 0;
+  if (t0) {
+    if (ensure(c, c->synth_cnt, t0 * 8) || ensure(c, c->synth_off, 16)) return KMZ_E_HIP;
+    launch_synth_count(c->stream, config, seed, 0, t0, P<uint64_t>(c->synth_cnt));
+    HIPCHK(c, hipcub::DeviceReduce::Sum(nullptr, tmp_bytes, P<uint64_t>(c->synth_cnt), P<uint64_t>(c->synth_off),
+                                         (int)t0, c->stream));
+    if (ensure(c, c->scratch, tmp_bytes)) return KMZ_E_HIP;
+    HIPCHK(c, hipcub::DeviceReduce::Sum(c->scratch.p, tmp_bytes, P<uint64_t>(c->synth_cnt), P<uint64_t>(c->synth_off),
+                                         (int)t0, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&base, c->synth_off.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  if (ensure(c, c->synth_cnt, (nt + 1) * 8) || ensure(c, c->synth_off, (nt + 1) * 8)) return KMZ_E_HIP;
+  launch_synth_count(c->stream, config, seed, t0, nt, P<uint64_t>(c->synth_cnt));
+  tmp_bytes = 0;
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, P<uint64_t>(c->synth_cnt), P<uint64_t>(c->synth_off),
+                                              (int)nt, c->stream));
+  if (ensure(c, c->scratch, tmp_bytes)) return KMZ_E_HIP;
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scratch.p, tmp_bytes, P<uint64_t>(c->synth_cnt),
+                                              P<uint64_t>(c->synth_off), (int)nt, c->stream));
+  uint64_t last_off = 0, last_cnt = 0;
+  if (nt) {
+    HIPCHK(c, hipMemcpyAsync(&last_off, P<uint64_t>(c->synth_off) + nt - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&last_cnt, P<uint64_t>(c->synth_cnt) + nt - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  uint64_t n = last_off + last_cnt;
+  if (n >= 0xFFFFFFFFull) return fail(c, KMZ_E_ARG, "synthetic batch too large for one context");
+  if (ensure(c, c->in_sid, n * 8) || ensure(c, c->in_pid, n * 8) || ensure(c, c->in_kind, n) ||
+      ensure(c, c->in_shape, n * 4) || ensure(c, c->in_status, n * 2) || ensure(c, c->in_dur, n * 4) ||
+      ensure(c, c->in_ts, n * 8))
+    return KMZ_E_HIP;
+  SynthOut o{P<uint64_t>(c->in_sid), P<uint64_t>(c->in_pid), P<uint8_t>(c->in_kind), P<uint32_t>(c->in_shape),
+             P<uint16_t>(c->in_status), P<uint32_t>(c->in_dur), P<int64_t>(c->in_ts)};
+  launch_synth_fill(c->stream, config, seed, t0, nt, P<uint64_t>(c->synth_off), base, P<uint32_t>(c->dur_table), o);
+  HIPCHK(c, hipGetLastError());
+  std::vector<uint32_t> ids(d.n_shapes);
+  kmz_synth_shape_ids(config, ids.data(), nullptr, nullptr, d.n_shapes);
+  kmz_shapes sh{d.n_shapes, ids.data(), ids.data(), ids.data(), d.n_endpoints, d.n_endpoints, d.n_endpoints,
+                d.n_status};
+  int r = load_shapes(c, &sh);
+  if (r) return r;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->n = n;
+  c->index_base = base;
+  c->sid = o.span_id;
+  c->pid = o.parent_id;
+  c->kind = o.kind;
+  c->shape = o.shape;
+  c->status = o.status;
+  c->dur = o.duration;
+  c->ts = o.timestamp;
+  c->loaded = true;
+  c->ran = 0;
+  if (n_out) *n_out = n;
+  return KMZ_OK;
+}
+
+int kmz_synth_host(int config, uint64_t seed, uint64_t t0, uint64_t t1, uint64_t cap, uint64_t *span_id,
+                   uint64_t *parent_id, uint8_t *kind, uint32_t *shape, uint16_t *status, uint32_t *duration,
+                   int64_t *timestamp, uint64_t *trace_off, uint64_t *n_out) {
+  if (t1 < t0 || (config != KMZ_SYNTH_BOOKINFO && config != KMZ_SYNTH_MESH)) return KMZ_E_ARG;
+  const auto &dt = dur_table_host();
+  uint64_t base = 0;
+  for (uint64_t t = 0; t < t0; ++t)
+    base += config == 2 ? synth_trace<2>(seed, t, 0, 0, nullptr, nullptr) : synth_trace<3>(seed, t, 0, 0, nullptr, nullptr);
+  SynthOut o{span_id, parent_id, kind, shape, status, duration, timestamp};
+  uint64_t off = 0;
+  for (uint64_t t = t0; t < t1; ++t) {
+    uint32_t cnt = config == 2 ? synth_trace<2>(seed, t, 0, 0, nullptr, nullptr) : synth_trace<3>(seed, t, 0, 0, nullptr, nullptr);
+    if (trace_off) trace_off[t - t0] = off;
+    if (span_id && off + cnt > cap) return KMZ_E_ARG;
+    if (span_id) {
+      if (config == 2)
+        synth_trace<2>(seed, t, base + off, off, dt.data(), &o);
+      else
+        synth_trace<3>(seed, t, base + off, off, dt.data(), &o);
+    }
+    off += cnt;
+  }
+  if (trace_off) trace_off[t1 - t0] = off;
+  if (n_out) *n_out = off;
+  return KMZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+// kmz_common.h -- host+device helpers shared by the kernels, the C ABI and the
+// host-side finaliser.  Everything here is integer or correctly-rounded fp64
+// arithmetic (compiled with -ffp-contract=off) so host and device agree bit
+// for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define KMZ_HD __host__ __device__ __forceinline__
+
+namespace kmz {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t CYC = 0xFFFFFFFEu;  // cparent of a span whose CLIENT chain loops
+constexpr uint64_t NONE64 = ~0ull;
+constexpr uint64_t TS_BIAS = 1ull << 63;  // signed -> order-preserving unsigned
+constexpr uint32_t MAX_DEPTH = 1u << 14;  // cycle guard (reference: unbounded)
+
+// error bits (device-side, folded into kmz_info.flags)
+constexpr uint32_t F_CYCLE = 1u;
+constexpr uint32_t F_ZERO_ID = 2u;
+constexpr uint32_t F_RANGE = 4u;
+constexpr uint32_t F_DUP_OVERFLOW = 8u;
+constexpr uint32_t F_TRIPLE_OVERFLOW = 16u;
+constexpr uint32_t F_TABLE_FULL = 32u;
+
+// splitmix64 finaliser: a bijection on u64 with mix64(0) == 0.
+KMZ_HD uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+KMZ_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+// position of key k in a table of `cap` slots (any cap, no pow2 rounding)
+KMZ_HD uint64_t slot_of(uint64_t k, uint64_t cap) { return mulhi64(mix64(k ^ 0x5bd1e9955bd1e995ull), cap); }
+KMZ_HD uint32_t tag_of(uint64_t k) { return (uint32_t)(mix64(k + 0x9e3779b97f4a7c15ull) >> 32); }
+
+// ---- JS number semantics ----------------------------------------------------
+// Math.round: nearest, ties toward +inf (ECMA-262 Math.round)
+KMZ_HD double js_round(double x) {
+  double r = floor(x);
+  if (x - r >= 0.5) r += 1.0;
+  return r;
+}
+// Utils.ToPrecise (src/utils/Utils.ts:311-313)
+KMZ_HD double to_precise(double x) {
+  const double eps = 2.220446049250313e-16;  // Number.EPSILON
+  double t = x + eps;  // add and multiply round separately (-ffp-contract=off)
+  double u = t * 1e14;
+  return js_round(u) / 1e14;
+}
+
+KMZ_HD double u128_to_double(uint64_t hi, uint64_t lo) {
+  // (double)hi * 2^64 + (double)lo : <= 1 ulp from the exact value
+  return (double)hi * 18446744073709551616.0 + (double)lo;
+}
+
+// Finalise one (endpoint x status) group from exact integer moments of the
+// durations d_i (us):  n, S1 = sum d, S2 = sum d^2 = s2a + s2b * 2^32.
+//   mean_ms = S1 / (1000 n)                       (RealtimeDataList.ts:100-118
+//   cv      = sqrt(n*S2 - S1^2) / S1               computes the same quantities
+// both exact-then-rounded, so they differ from the reference's sequential
+// Welford only by the reference's own rounding (<= ~1e-15 relative).
+KMZ_HD void finalize_moments(uint64_t n, uint64_t s1, uint64_t s2a, uint64_t s2b, double *mean_out,
+                             double *cv_out) {
+  if (n == 0) {
+    *mean_out = 0.0;
+    *cv_out = 0.0;
+    return;
+  }
+  // S2 = s2a + s2b<<32 as 128-bit (hi, lo)
+  uint64_t lo = s2a + (s2b << 32);
+  uint64_t carry = lo < s2a ? 1ull : 0ull;
+  uint64_t hi = (s2b >> 32) + carry;
+  // n * S2 (n < 2^32, S2 < 2^96 -> < 2^128)
+  uint64_t p_lo = n * lo;
+  uint64_t p_hi = mulhi64(n, lo) + n * hi;
+  // S1^2
+  uint64_t q_lo = s1 * s1;
+  uint64_t q_hi = mulhi64(s1, s1);
+  // n*S2 - S1^2 >= 0 (Cauchy-Schwarz)
+  uint64_t r_lo = p_lo - q_lo;
+  uint64_t borrow = p_lo < q_lo ? 1ull : 0ull;
+  uint64_t r_hi = p_hi - q_hi - borrow;
+  double mean = (double)s1 / ((double)n * 1000.0);
+  double cv = 0.0;
+  if (s1 != 0) {
+    double num = u128_to_double(r_hi, r_lo);
+    cv = sqrt(num) / (double)s1;
+  }
+  *mean_out = to_precise(mean);
+  *cv_out = to_precise(cv);
+}
+
+}  // namespace kmz

@@ -1,0 +1,47 @@
+// kmz_kernels.h -- kernel launchers shared between kmz_kernels.hip and kmz_api.hip
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/kmz.h"
+#include "kmz_common.h"
+#include "kmz_synth.h"
+
+namespace kmz {
+
+constexpr uint8_t KIND_SERVER = KMZ_KIND_SERVER;
+constexpr uint8_t KIND_CLIENT = KMZ_KIND_CLIENT;
+
+// u32 device counters
+enum { C_FLAGS = 0, C_DUPS = 1, C_TRIPLES = 2, C_COUNT = 4 };
+// u64 device statistics
+enum { S_ROWS = 0, S_REL = 1, S_MAXD = 2, S_SERVER = 3, S_TRIP_OUT = 4, S_COUNT = 8 };
+
+struct DupEntry {
+  uint32_t pos, idx, winner, pad;
+};
+
+void launch_build(hipStream_t s, const uint64_t *sid, uint32_t n, unsigned long long *table, uint64_t cap,
+                  DupEntry *dups, uint32_t dup_cap, unsigned int *counters);
+void launch_fixup(hipStream_t s, const DupEntry *dups, const unsigned int *counters, uint32_t dup_cap,
+                  unsigned long long *table, unsigned int *dkey, unsigned int *dval, uint32_t dcap);
+void launch_resolve(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
+                    const unsigned long long *table, uint64_t cap, uint32_t *cparent, unsigned int *counters);
+void launch_stats(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status, const uint32_t *dur,
+                  const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape, uint32_t n_shapes, uint32_t n_ep,
+                  uint32_t n_status, uint64_t index_base, unsigned long long *grp, unsigned int *counters,
+                  unsigned long long *n_server);
+void launch_walk(hipStream_t s, const uint64_t *sid, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+                 const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
+                 uint64_t index_base, const unsigned long long *table, uint64_t cap, const unsigned int *dkey,
+                 const unsigned int *dval, uint32_t dcap, unsigned long long *trip, uint64_t tcap,
+                 unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *rowpos,
+                 unsigned int *counters, unsigned long long *stats64);
+void launch_finalize(hipStream_t s, unsigned long long *grp, uint32_t G, kmz_group *out);
+void launch_compact(hipStream_t s, const unsigned long long *trip, uint64_t tcap, unsigned long long *out,
+                    unsigned long long *count);
+void launch_synth_count(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, uint64_t *cnt);
+void launch_synth_fill(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, const uint64_t *off,
+                       uint64_t gbase, const uint32_t *dur_table, SynthOut out);
+
+}  // namespace kmz

@@ -1,0 +1,575 @@
+// kmz_kernels.hip -- the four hot-path kernels for gfx950 (MI355X).
+//
+//   K1 build    span-id -> row hash table in HBM (8-byte {tag, index} slots,
+//               verified through the span_id column, which is trace-local)
+//   K1 fixup    duplicate span ids: last occurrence wins the value, the first
+//               keeps the position (JS Map semantics, Traces.ts:117-123)
+//   K2 resolve  parent join + CLIENT contraction: for every non-CLIENT span the
+//               first non-CLIENT ancestor row (Traces.ts:128-137)
+//   K3 stats    segmented (endpoint x status) reduction of exact integer
+//               moments, LDS-privatised per workgroup (Traces.ts:27-106,
+//               RealtimeDataList.ts:22-118)
+//   K4 walk     ancestor traversal over the contracted links: dependency
+//               edge triples (LDS-deduplicated, then a global hash set),
+//               per-endpoint lastUsage / first row / external (Traces.ts:138-208)
+//
+// All integer work is exact; the only floating point (finalisation) is shared
+// with the host through kmz_common.h and compiled with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include "kmz_kernels.h"
+
+namespace kmz {
+
+// ---------------------------------------------------------------------------
+// wave helpers (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ void wave_add_u64(unsigned long long *dst, uint64_t v) {
+  // sum over the active lanes, one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if (lane_id() == (uint32_t)__ffsll((long long)__ballot(1)) - 1) atomicAdd(dst, (unsigned long long)v);
+}
+
+// ---------------------------------------------------------------------------
+// K1: build the span-id table
+// ---------------------------------------------------------------------------
+// slot = tag(key) << 32 | (index + 1); 0 = empty.  Insert claims an empty slot
+// with one 64-bit CAS; a slot whose tag matches is verified against
+// span_id[index] (the winner's row, usually in the same trace => cached).
+__global__ void __launch_bounds__(256) k_build(const uint64_t *__restrict__ sid, uint32_t n,
+                                               unsigned long long *__restrict__ table, uint64_t cap,
+                                               DupEntry *__restrict__ dups, uint32_t dup_cap,
+                                               unsigned int *__restrict__ counters) {
+  uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t key = sid[i];
+    if (key == 0) {
+      atomicOr(&counters[C_FLAGS], F_ZERO_ID);
+      continue;
+    }
+    uint32_t tag = tag_of(key);
+    uint64_t val = ((uint64_t)tag << 32) | (uint64_t)(i + 1);
+    uint64_t pos = slot_of(key, cap);
+    for (uint64_t probe = 0; probe < cap; ++probe) {
+      uint64_t cur = table[pos];
+      if (cur == 0) {
+        cur = atomicCAS(&table[pos], 0ull, (unsigned long long)val);
+        if (cur == 0) break;  // claimed
+      }
+      if ((uint32_t)(cur >> 32) == tag) {
+        uint32_t w = (uint32_t)cur - 1;
+        if (sid[w] == key) {  // duplicate id: defer to the fixup
+          uint32_t d = atomicAdd(&counters[C_DUPS], 1u);
+          if (d < dup_cap) {
+            dups[d].pos = (uint32_t)pos;
+            dups[d].idx = i;
+            dups[d].winner = w;
+          } else {
+            atomicOr(&counters[C_FLAGS], F_DUP_OVERFLOW);
+          }
+          break;
+        }
+      }
+      pos = (pos + 1 == cap) ? 0 : pos + 1;
+      if (probe + 1 == cap) atomicOr(&counters[C_FLAGS], F_TABLE_FULL);
+    }
+  }
+}
+
+// Duplicate ids: slot index := max occurrence (the Map value), dupmap[pos] :=
+// min occurrence (the Map position).
+__global__ void __launch_bounds__(256) k_fixup(const DupEntry *__restrict__ dups, const unsigned int *__restrict__ counters,
+                                               uint32_t dup_cap, unsigned long long *__restrict__ table,
+                                               unsigned int *__restrict__ dkey, unsigned int *__restrict__ dval,
+                                               uint32_t dcap) {
+  uint32_t nd = min(counters[C_DUPS], dup_cap);
+  uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < nd; e += stride) {
+    DupEntry d = dups[e];
+    uint64_t cur = table[d.pos];
+    atomicMax(&table[d.pos], (unsigned long long)((cur & 0xFFFFFFFF00000000ull) | (uint64_t)(d.idx + 1)));
+    uint32_t first = min(d.idx, d.winner);
+    uint32_t h = (uint32_t)slot_of(d.pos, dcap);
+    for (uint32_t p = 0; p < dcap; ++p) {
+      uint32_t k = dkey[h];
+      if (k == 0) k = atomicCAS(&dkey[h], 0u, d.pos + 1);
+      if (k == 0 || k == d.pos + 1) {
+        atomicMin(&dval[h], first);
+        break;
+      }
+      h = (h + 1 == dcap) ? 0 : h + 1;
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lookup(uint64_t key, const uint64_t *__restrict__ sid,
+                                           const unsigned long long *__restrict__ table, uint64_t cap) {
+  uint32_t tag = tag_of(key);
+  uint64_t pos = slot_of(key, cap);
+  for (uint64_t probe = 0; probe < cap; ++probe) {
+    uint64_t cur = table[pos];
+    if (cur == 0) return NONE;
+    if ((uint32_t)(cur >> 32) == tag) {
+      uint32_t w = (uint32_t)cur - 1;
+      if (sid[w] == key) return w;
+    }
+    pos = (pos + 1 == cap) ? 0 : pos + 1;
+  }
+  return NONE;
+}
+
+__device__ __forceinline__ uint32_t dup_first(uint64_t pos, const unsigned int *__restrict__ dkey,
+                                              const unsigned int *__restrict__ dval, uint32_t dcap) {
+  uint32_t h = (uint32_t)slot_of(pos, dcap);
+  for (uint32_t p = 0; p < dcap; ++p) {
+    uint32_t k = dkey[h];
+    if (k == 0) return NONE;
+    if (k == (uint32_t)pos + 1) return dval[h];
+    h = (h + 1 == dcap) ? 0 : h + 1;
+  }
+  return NONE;
+}
+
+// ---------------------------------------------------------------------------
+// K2: parent join + CLIENT contraction
+// ---------------------------------------------------------------------------
+// cparent[i] = the row reached from span i's parentId after skipping CLIENT
+// spans (Traces.ts:131-137), KMZ_NONE when the walk ends.  CLIENT spans never
+// start or continue a walk past themselves, so they get NONE.  A CLIENT-only
+// loop yields CYC; it is an error only when a row's walk reaches it (K4), as
+// the reference only loops on chains it actually walks.
+__global__ void __launch_bounds__(256) k_resolve(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
+                                                 const uint8_t *__restrict__ kind, uint32_t n,
+                                                 const unsigned long long *__restrict__ table, uint64_t cap,
+                                                 uint32_t *__restrict__ cparent, unsigned int *__restrict__ counters) {
+  uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint32_t q = NONE;
+    if (kind[i] != KIND_CLIENT) {
+      uint64_t p = pid[i];
+      uint32_t hops = 0;
+      while (p != 0) {
+        q = lookup(p, sid, table, cap);
+        if (q == NONE || kind[q] != KIND_CLIENT) break;
+        p = pid[q];
+        q = NONE;
+        if (++hops > MAX_DEPTH) {  // only an error if a row's walk reaches it (K4)
+          q = CYC;
+          break;
+        }
+      }
+    }
+    cparent[i] = q;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3: (endpoint x status) reduction
+// ---------------------------------------------------------------------------
+// Per SERVER span (every occurrence, Traces.ts:28-31): g = ep * n_status + status,
+//   count += 1, s1 += d, s2a += lo32(d*d), s2b += hi32(d*d),
+//   tsmax = max(ts ^ 2^63), first = min(global index).
+// Workgroups privatise the accumulators in LDS: DIRECT indexes them by g when
+// all groups fit, HASHED keeps an open-addressing LDS table of recently seen
+// groups and falls back to global atomics when it is full.
+struct GroupAcc {
+  unsigned long long *cnt, *s1, *s2a, *s2b, *tsx, *fst;
+};
+
+__device__ __forceinline__ void acc_global(const GroupAcc &a, uint32_t g, uint64_t d, uint64_t tsx, uint64_t gi) {
+  uint64_t dd = d * d;
+  atomicAdd(&a.cnt[g], 1ull);
+  atomicAdd(&a.s1[g], (unsigned long long)d);
+  atomicAdd(&a.s2a[g], (unsigned long long)(dd & 0xFFFFFFFFull));
+  atomicAdd(&a.s2b[g], (unsigned long long)(dd >> 32));
+  atomicMax(&a.tsx[g], (unsigned long long)tsx);
+  atomicMin(&a.fst[g], (unsigned long long)gi);
+}
+
+constexpr uint32_t K3_DIRECT_MAX = 1024;  // groups held directly in LDS (48 KiB)
+constexpr uint32_t K3_HASH_CAP = 1024;    // LDS hash entries (52 KiB)
+
+template <bool DIRECT>
+__global__ void __launch_bounds__(256) k_stats(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
+                                               const uint16_t *__restrict__ status,
+                                               const uint32_t *__restrict__ dur, const int64_t *__restrict__ ts,
+                                               uint32_t n, uint32_t chunk, const uint32_t *__restrict__ ep_of_shape,
+                                               uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint64_t index_base,
+                                               GroupAcc acc, unsigned int *__restrict__ counters,
+                                               unsigned long long *__restrict__ n_server) {
+  __shared__ unsigned long long l_cnt[K3_HASH_CAP], l_s1[K3_HASH_CAP], l_s2a[K3_HASH_CAP], l_s2b[K3_HASH_CAP],
+      l_tsx[K3_HASH_CAP], l_fst[K3_HASH_CAP];
+  __shared__ unsigned int l_key[DIRECT ? 1 : K3_HASH_CAP];
+  const uint32_t G = n_ep * n_status;
+  const uint32_t slots = DIRECT ? G : K3_HASH_CAP;
+  for (uint32_t s = threadIdx.x; s < slots; s += blockDim.x) {
+    l_cnt[s] = 0;
+    l_s1[s] = 0;
+    l_s2a[s] = 0;
+    l_s2b[s] = 0;
+    l_tsx[s] = 0;
+    l_fst[s] = ~0ull;
+    if (!DIRECT) l_key[s] = 0;
+  }
+  __syncthreads();
+  uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+  uint32_t end = (uint32_t)min<uint64_t>(c0 + chunk, n);
+  uint32_t servers = 0;
+  for (uint32_t i = (uint32_t)c0 + threadIdx.x; i < end; i += blockDim.x) {
+    if (kind[i] != KIND_SERVER) continue;
+    ++servers;
+    uint32_t sh = shape[i];
+    uint32_t st = status[i];
+    uint32_t ep = sh < n_shapes ? ep_of_shape[sh] : NONE;
+    if (ep >= n_ep || st >= n_status) {
+      atomicOr(&counters[C_FLAGS], F_RANGE);
+      continue;
+    }
+    uint32_t g = ep * n_status + st;
+    uint64_t d = dur[i];
+    uint64_t dd = d * d;
+    uint64_t tsx = (uint64_t)ts[i] ^ TS_BIAS;
+    uint64_t gi = index_base + i;
+    uint32_t s = NONE;
+    if (DIRECT) {
+      s = g;
+    } else {
+      uint32_t h = (g * 2654435761u) >> 22;  // 10 bits
+      for (uint32_t p = 0; p < 32; ++p) {
+        uint32_t k = l_key[h];
+        if (k == 0) k = atomicCAS(&l_key[h], 0u, g + 1);
+        if (k == 0 || k == g + 1) {
+          s = h;
+          break;
+        }
+        h = (h + 1) & (K3_HASH_CAP - 1);
+      }
+    }
+    if (s == NONE) {
+      acc_global(acc, g, d, tsx, gi);
+      continue;
+    }
+    atomicAdd(&l_cnt[s], 1ull);
+    atomicAdd(&l_s1[s], (unsigned long long)d);
+    atomicAdd(&l_s2a[s], (unsigned long long)(dd & 0xFFFFFFFFull));
+    atomicAdd(&l_s2b[s], (unsigned long long)(dd >> 32));
+    atomicMax(&l_tsx[s], (unsigned long long)tsx);
+    atomicMin(&l_fst[s], (unsigned long long)gi);
+  }
+  wave_add_u64(n_server, servers);
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < slots; s += blockDim.x) {
+    if (l_cnt[s] == 0) continue;
+    uint32_t g = DIRECT ? s : l_key[s] - 1;
+    atomicAdd(&acc.cnt[g], l_cnt[s]);
+    atomicAdd(&acc.s1[g], l_s1[s]);
+    atomicAdd(&acc.s2a[g], l_s2a[s]);
+    atomicAdd(&acc.s2b[g], l_s2b[s]);
+    atomicMax(&acc.tsx[g], l_tsx[s]);
+    atomicMin(&acc.fst[g], l_fst[s]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4: ancestor traversal
+// ---------------------------------------------------------------------------
+constexpr uint32_t K4_TSET = 2048;      // LDS triple set (16 KiB)
+constexpr uint32_t K4_EP_DIRECT = 2048; // endpoints privatised in LDS (32 KiB)
+
+__device__ __forceinline__ void triple_global(uint64_t key, unsigned long long *__restrict__ trip, uint64_t tcap,
+                                              unsigned int *__restrict__ counters) {
+  uint64_t pos = slot_of(key, tcap);
+  for (uint64_t p = 0; p < tcap; ++p) {
+    uint64_t cur = trip[pos];
+    if (cur == key) return;
+    if (cur == 0) {
+      cur = atomicCAS(&trip[pos], 0ull, (unsigned long long)key);
+      if (cur == 0) {
+        uint32_t c = atomicAdd(&counters[C_TRIPLES], 1u) + 1;
+        if ((uint64_t)c * 10 > tcap * 7) atomicOr(&counters[C_FLAGS], F_TRIPLE_OVERFLOW);
+        return;
+      }
+      if (cur == key) return;
+    }
+    pos = (pos + 1 == tcap) ? 0 : pos + 1;
+  }
+  atomicOr(&counters[C_FLAGS], F_TRIPLE_OVERFLOW);
+}
+
+template <bool EP_DIRECT>
+__global__ void __launch_bounds__(256) k_walk(const uint64_t *__restrict__ sid, const uint8_t *__restrict__ kind,
+                                              const uint32_t *__restrict__ shape, const int64_t *__restrict__ ts,
+                                              const uint32_t *__restrict__ cparent, uint32_t n, uint32_t chunk,
+                                              const uint32_t *__restrict__ dep_ep, uint32_t n_shapes, uint32_t n_ep,
+                                              uint64_t index_base, const unsigned long long *__restrict__ table,
+                                              uint64_t cap, const unsigned int *__restrict__ dkey,
+                                              const unsigned int *__restrict__ dval, uint32_t dcap,
+                                              unsigned long long *__restrict__ trip, uint64_t tcap,
+                                              unsigned long long *__restrict__ ep_ts,
+                                              unsigned long long *__restrict__ ep_first,
+                                              unsigned long long *__restrict__ rowpos_out,
+                                              unsigned int *__restrict__ counters,
+                                              unsigned long long *__restrict__ stats64) {
+  __shared__ unsigned long long l_set[K4_TSET];
+  __shared__ unsigned long long l_ts[EP_DIRECT ? K4_EP_DIRECT : 1], l_first[EP_DIRECT ? K4_EP_DIRECT : 1];
+  for (uint32_t s = threadIdx.x; s < K4_TSET; s += blockDim.x) l_set[s] = 0;
+  if (EP_DIRECT)
+    for (uint32_t s = threadIdx.x; s < n_ep; s += blockDim.x) {
+      l_ts[s] = 0;
+      l_first[s] = ~0ull;
+    }
+  __syncthreads();
+  const bool have_dups = counters[C_DUPS] != 0;
+  uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+  uint32_t end = (uint32_t)min<uint64_t>(c0 + chunk, n);
+  uint64_t rel = 0, rows = 0;
+  uint32_t maxd = 0;
+  for (uint32_t i = (uint32_t)c0 + threadIdx.x; i < end; i += blockDim.x) {
+    uint64_t rp = NONE64;
+    if (kind[i] == KIND_SERVER) {
+      uint32_t first = i;
+      bool is_row = true;
+      if (have_dups) {  // the row of an id is its LAST occurrence, at its FIRST position
+        uint32_t last = lookup(sid[i], sid, table, cap);
+        if (last != i) {
+          is_row = false;
+        } else {
+          uint64_t pos = slot_of(sid[i], cap);
+          // find the slot index of this key for the dupmap
+          for (uint64_t p = 0; p < cap; ++p) {
+            uint64_t cur = table[pos];
+            if ((uint32_t)cur - 1 == i) break;
+            pos = (pos + 1 == cap) ? 0 : pos + 1;
+          }
+          uint32_t f = dup_first(pos, dkey, dval, dcap);
+          if (f != NONE) first = f;
+        }
+      }
+      if (is_row) {
+        ++rows;
+        rp = index_base + first;
+        uint32_t sh = shape[i];
+        uint32_t es = sh < n_shapes ? dep_ep[sh] : NONE;
+        if (es >= n_ep) {
+          atomicOr(&counters[C_FLAGS], F_RANGE);
+        } else {
+          uint32_t cur = cparent[i];
+          uint64_t fkey = (rp << 1) | (cur != NONE ? 1ull : 0ull);
+          uint64_t tsx = (uint64_t)ts[i] ^ TS_BIAS;
+          if (EP_DIRECT) {
+            atomicMax(&l_ts[es], (unsigned long long)tsx);
+            atomicMin(&l_first[es], (unsigned long long)fkey);
+          } else {
+            atomicMax(&ep_ts[es], (unsigned long long)tsx);
+            atomicMin(&ep_first[es], (unsigned long long)fkey);
+          }
+          uint32_t d = 0;
+          while (cur != NONE) {
+            ++d;
+            if (d > MAX_DEPTH || cur == CYC) {
+              atomicOr(&counters[C_FLAGS], F_CYCLE);
+              break;
+            }
+            uint8_t ka = kind[cur];
+            uint32_t sa = shape[cur];
+            uint32_t ea = sa < n_shapes ? dep_ep[sa] : NONE;
+            if (ea >= n_ep) {
+              atomicOr(&counters[C_FLAGS], F_RANGE);
+              break;
+            }
+            uint64_t key = ((uint64_t)ea << 40) | ((uint64_t)es << 16) | ((uint64_t)d << 1) |
+                           (ka == KIND_SERVER ? 1ull : 0ull);
+            // LDS dedup, then the global set
+            uint32_t h = (uint32_t)(mix64(key) >> 53);  // 11 bits
+            bool done = false;
+            for (uint32_t p = 0; p < 8; ++p) {
+              uint64_t c = l_set[h];
+              if (c == key) {
+                done = true;
+                break;
+              }
+              if (c == 0) {
+                c = atomicCAS(&l_set[h], 0ull, (unsigned long long)key);
+                if (c == 0) break;  // new in this workgroup
+                if (c == key) {
+                  done = true;
+                  break;
+                }
+              }
+              h = (h + 1) & (K4_TSET - 1);
+            }
+            if (!done) triple_global(key, trip, tcap, counters);
+            if (ka != KIND_SERVER) {  // non-SERVER ancestors are not rows: count their use here
+              uint64_t tsa = (uint64_t)ts[cur] ^ TS_BIAS;
+              if (EP_DIRECT)
+                atomicMax(&l_ts[ea], (unsigned long long)tsa);
+              else
+                atomicMax(&ep_ts[ea], (unsigned long long)tsa);
+            }
+            cur = cparent[cur];
+          }
+          rel += d;
+          maxd = max(maxd, d);
+        }
+      }
+    }
+    if (rowpos_out) rowpos_out[i] = rp;
+  }
+  wave_add_u64(&stats64[S_ROWS], rows);
+  wave_add_u64(&stats64[S_REL], rel);
+  for (int off = 32; off > 0; off >>= 1) maxd = max(maxd, (uint32_t)__shfl_xor(maxd, off, 64));
+  if (lane_id() == 0 && maxd) atomicMax(&stats64[S_MAXD], (unsigned long long)maxd);
+  if (EP_DIRECT) {
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < n_ep; s += blockDim.x) {
+      if (l_ts[s]) atomicMax(&ep_ts[s], l_ts[s]);
+      if (l_first[s] != ~0ull) atomicMin(&ep_first[s], l_first[s]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// finalisation / compaction
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_finalize(GroupAcc acc, uint32_t G, kmz_group *__restrict__ out) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+    kmz_group r;
+    r.combined = acc.cnt[g];
+    r.first = acc.fst[g];
+    r.latest_timestamp = (int64_t)(acc.tsx[g] ^ TS_BIAS);
+    finalize_moments(acc.cnt[g], acc.s1[g], acc.s2a[g], acc.s2b[g], &r.mean, &r.cv);
+    out[g] = r;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_compact(const unsigned long long *__restrict__ trip, uint64_t tcap,
+                                                 unsigned long long *__restrict__ out,
+                                                 unsigned long long *__restrict__ count) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < tcap; p += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t k = trip[p];
+    if (k) out[atomicAdd(count, 1ull)] = k;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic generation
+// ---------------------------------------------------------------------------
+template <int CONFIG>
+__global__ void __launch_bounds__(256) k_synth_count(uint64_t seed, uint64_t t0, uint64_t nt, uint64_t *__restrict__ cnt) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += (uint64_t)gridDim.x * blockDim.x)
+    cnt[t] = synth_trace<CONFIG>(seed, t0 + t, 0, 0, nullptr, nullptr);
+}
+
+template <int CONFIG>
+__global__ void __launch_bounds__(256) k_synth_fill(uint64_t seed, uint64_t t0, uint64_t nt,
+                                                    const uint64_t *__restrict__ off, uint64_t gbase,
+                                                    const uint32_t *__restrict__ dur_table, SynthOut out) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += (uint64_t)gridDim.x * blockDim.x)
+    synth_trace<CONFIG>(seed, t0 + t, gbase + off[t], off[t], dur_table, &out);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static inline uint32_t grid_for(uint64_t work, uint32_t cap_blocks = 8192) {
+  uint64_t b = (work + 255) / 256;
+  if (b < 1) b = 1;
+  return (uint32_t)(b < cap_blocks ? b : cap_blocks);
+}
+
+void launch_build(hipStream_t s, const uint64_t *sid, uint32_t n, unsigned long long *table, uint64_t cap,
+                  DupEntry *dups, uint32_t dup_cap, unsigned int *counters) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_build, dim3(grid_for(n)), dim3(256), 0, s, sid, n, table, cap, dups, dup_cap, counters);
+}
+void launch_fixup(hipStream_t s, const DupEntry *dups, const unsigned int *counters, uint32_t dup_cap,
+                  unsigned long long *table, unsigned int *dkey, unsigned int *dval, uint32_t dcap) {
+  hipLaunchKernelGGL(k_fixup, dim3(grid_for(dup_cap, 1024)), dim3(256), 0, s, dups, counters, dup_cap, table, dkey, dval,
+                     dcap);
+}
+void launch_resolve(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
+                    const unsigned long long *table, uint64_t cap, uint32_t *cparent, unsigned int *counters) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_resolve, dim3(grid_for(n)), dim3(256), 0, s, sid, pid, kind, n, table, cap, cparent, counters);
+}
+
+static inline uint32_t chunk_for(uint32_t n, uint32_t min_chunk) {
+  // >= ~2048 workgroups for a full chip when n allows it, chunks of >= min_chunk
+  uint32_t c = (n + 2047) / 2048;
+  if (c < min_chunk) c = min_chunk;
+  return (c + 255) / 256 * 256;
+}
+
+void launch_stats(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status, const uint32_t *dur,
+                  const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape, uint32_t n_shapes, uint32_t n_ep,
+                  uint32_t n_status, uint64_t index_base, unsigned long long *grp, unsigned int *counters,
+                  unsigned long long *n_server) {
+  if (!n) return;
+  uint64_t G = (uint64_t)n_ep * n_status;
+  GroupAcc a{grp, grp + G, grp + 2 * G, grp + 3 * G, grp + 4 * G, grp + 5 * G};
+  if (G <= K3_DIRECT_MAX) {
+    uint32_t chunk = chunk_for(n, (uint32_t)(4 * G > 1024 ? 4 * G : 1024));
+    uint32_t blocks = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_stats<true>, dim3(blocks), dim3(256), 0, s, kind, shape, status, dur, ts, n, chunk, ep_of_shape,
+                       n_shapes, n_ep, n_status, index_base, a, counters, n_server);
+  } else {
+    uint32_t chunk = chunk_for(n, 4096);
+    uint32_t blocks = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_stats<false>, dim3(blocks), dim3(256), 0, s, kind, shape, status, dur, ts, n, chunk,
+                       ep_of_shape, n_shapes, n_ep, n_status, index_base, a, counters, n_server);
+  }
+}
+
+void launch_walk(hipStream_t s, const uint64_t *sid, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+                 const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
+                 uint64_t index_base, const unsigned long long *table, uint64_t cap, const unsigned int *dkey,
+                 const unsigned int *dval, uint32_t dcap, unsigned long long *trip, uint64_t tcap,
+                 unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *rowpos,
+                 unsigned int *counters, unsigned long long *stats64) {
+  if (!n) return;
+  if (n_ep <= K4_EP_DIRECT) {
+    uint32_t chunk = chunk_for(n, 4 * n_ep > 1024 ? 4 * n_ep : 1024);
+    uint32_t blocks = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_walk<true>, dim3(blocks), dim3(256), 0, s, sid, kind, shape, ts, cparent, n, chunk, dep_ep,
+                       n_shapes, n_ep, index_base, table, cap, dkey, dval, dcap, trip, tcap, ep_ts, ep_first, rowpos,
+                       counters, stats64);
+  } else {
+    uint32_t chunk = chunk_for(n, 1024);
+    uint32_t blocks = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_walk<false>, dim3(blocks), dim3(256), 0, s, sid, kind, shape, ts, cparent, n, chunk, dep_ep,
+                       n_shapes, n_ep, index_base, table, cap, dkey, dval, dcap, trip, tcap, ep_ts, ep_first, rowpos,
+                       counters, stats64);
+  }
+}
+
+void launch_finalize(hipStream_t s, unsigned long long *grp, uint32_t G, kmz_group *out) {
+  if (!G) return;
+  GroupAcc a{grp, grp + G, grp + 2ull * G, grp + 3ull * G, grp + 4ull * G, grp + 5ull * G};
+  hipLaunchKernelGGL(k_finalize, dim3(grid_for(G, 1024)), dim3(256), 0, s, a, G, out);
+}
+
+void launch_compact(hipStream_t s, const unsigned long long *trip, uint64_t tcap, unsigned long long *out,
+                    unsigned long long *count) {
+  hipLaunchKernelGGL(k_compact, dim3(grid_for(tcap, 4096)), dim3(256), 0, s, trip, tcap, out, count);
+}
+
+void launch_synth_count(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, uint64_t *cnt) {
+  if (!nt) return;
+  if (config == 2)
+    hipLaunchKernelGGL(k_synth_count<2>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, cnt);
+  else
+    hipLaunchKernelGGL(k_synth_count<3>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, cnt);
+}
+
+void launch_synth_fill(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, const uint64_t *off,
+                       uint64_t gbase, const uint32_t *dur_table, SynthOut out) {
+  if (!nt) return;
+  if (config == 2)
+    hipLaunchKernelGGL(k_synth_fill<2>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, off, gbase, dur_table, out);
+  else
+    hipLaunchKernelGGL(k_synth_fill<3>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, off, gbase, dur_table, out);
+}
+
+}  // namespace kmz

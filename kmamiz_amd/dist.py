@@ -1,0 +1,74 @@
+"""Multi-GPU merge of traceId-sharded batches.
+
+Each rank runs the whole pipeline on its own shard (whole traces, global
+flatten indices via ``index_base``); no span crosses a GPU.  The per-rank
+partials then merge with collectives over the default process group:
+
+* group partials    [count, sum d, sum lo32(d^2), sum hi32(d^2)]  all_reduce SUM
+                    [max timestamp]                                all_reduce MAX
+                    [min first index]                              all_reduce MIN
+* endpoint partials [max timestamp] MAX, [min first_row<<1|!external] MIN
+* edge keys         size all_reduce MAX, padded all_gather, unique
+
+Integer moments make the merge exact: the merged groups are bit-identical to a
+single-GPU run over the whole batch (the reference's pooled-variance formula,
+CombinedRealtimeDataList.ts:278-315, is not needed for this).
+
+Works with any backend: ``nccl`` (RCCL over xGMI) on device tensors in
+production, ``gloo`` on CPU tensors in the tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+_BIAS = -(1 << 63)  # flips the sign bit: u64 order <-> i64 order
+_I64_MAX = (1 << 63) - 1
+
+
+def _as_signed_order(x: torch.Tensor) -> torch.Tensor:
+    return torch.bitwise_xor(x, torch.tensor(_BIAS, dtype=torch.int64, device=x.device))
+
+
+def merge_group_partials(p: torch.Tensor, n_groups: int) -> torch.Tensor:
+    """In-place merge of a [6 * G] int64 view of the u64 group partials."""
+    G = n_groups
+    if dist.get_world_size() == 1 or G == 0:
+        return p
+    dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM)  # modular: exact for u64
+    ts = _as_signed_order(p[4 * G : 5 * G])
+    dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+    p[4 * G : 5 * G] = _as_signed_order(ts)
+    first = p[5 * G :]
+    first = torch.where(first == -1, torch.full_like(first, _I64_MAX), first)
+    dist.all_reduce(first, op=dist.ReduceOp.MIN)
+    p[5 * G :] = torch.where(first == _I64_MAX, torch.full_like(first, -1), first)
+    return p
+
+
+def merge_endpoint_partials(e: torch.Tensor, n_ep: int) -> torch.Tensor:
+    """In-place merge of a [2 * E] int64 view of the endpoint partials."""
+    if dist.get_world_size() == 1 or n_ep == 0:
+        return e
+    ts = _as_signed_order(e[:n_ep])
+    dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+    e[:n_ep] = _as_signed_order(ts)
+    f = e[n_ep:]
+    f = torch.where(f == -1, torch.full_like(f, _I64_MAX), f)
+    dist.all_reduce(f, op=dist.ReduceOp.MIN)
+    e[n_ep:] = torch.where(f == _I64_MAX, torch.full_like(f, -1), f)
+    return e
+
+
+def merge_edge_keys(keys: torch.Tensor) -> torch.Tensor:
+    """Union of every rank's unique edge keys (int64 view, keys are > 0)."""
+    if dist.get_world_size() == 1:
+        return torch.unique(keys)
+    n = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX)
+    pad = torch.zeros(int(n.item()), dtype=torch.int64, device=keys.device)
+    pad[: keys.numel()] = keys
+    parts = [torch.empty_like(pad) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, pad)
+    allk = torch.unique(torch.cat(parts))
+    return allk[allk != 0]

@@ -1,0 +1,232 @@
+"""Engine: one HIP context (one GPU, one stream) holding a device-resident
+span batch and running the four hot-path kernels on it.
+
+This is the Python face of ``include/kmz.h``; the TypeScript-facing mirror of
+the reference classes lives in :mod:`kmamiz_amd.classes`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class SpanBatch:
+    """Columnar span batch in flatten order (layout of ``kmz_spans``)."""
+
+    span_id: np.ndarray  # u64
+    parent_id: np.ndarray  # u64, 0 = none
+    kind: np.ndarray  # u8
+    shape: np.ndarray  # u32
+    status: np.ndarray  # u16
+    duration: np.ndarray  # u32 (us)
+    timestamp: np.ndarray  # i64 (us)
+    index_base: int = 0
+
+    def __post_init__(self):
+        self.span_id = np.ascontiguousarray(self.span_id, dtype=np.uint64)
+        self.parent_id = np.ascontiguousarray(self.parent_id, dtype=np.uint64)
+        self.kind = np.ascontiguousarray(self.kind, dtype=np.uint8)
+        self.shape = np.ascontiguousarray(self.shape, dtype=np.uint32)
+        self.status = np.ascontiguousarray(self.status, dtype=np.uint16)
+        self.duration = np.ascontiguousarray(self.duration, dtype=np.uint32)
+        self.timestamp = np.ascontiguousarray(self.timestamp, dtype=np.int64)
+        n = len(self.span_id)
+        for f in ("parent_id", "kind", "shape", "status", "duration", "timestamp"):
+            if len(getattr(self, f)) != n:
+                raise ValueError(f"column {f} has {len(getattr(self, f))} rows, expected {n}")
+
+    def __len__(self):
+        return len(self.span_id)
+
+    def c_struct(self) -> L.Spans:
+        return L.Spans(
+            len(self),
+            L.ptr(self.span_id),
+            L.ptr(self.parent_id),
+            L.ptr(self.kind),
+            L.ptr(self.shape),
+            L.ptr(self.status),
+            L.ptr(self.duration),
+            L.ptr(self.timestamp),
+            int(self.index_base),
+        )
+
+
+@dataclass
+class ShapeTable:
+    rt_ep: np.ndarray
+    tag_ep: np.ndarray
+    dep_ep: np.ndarray
+    n_rt_ep: int
+    n_tag_ep: int
+    n_dep_ep: int
+    n_status: int
+
+    def __post_init__(self):
+        self.rt_ep = np.ascontiguousarray(self.rt_ep, dtype=np.uint32)
+        self.tag_ep = np.ascontiguousarray(self.tag_ep, dtype=np.uint32)
+        self.dep_ep = np.ascontiguousarray(self.dep_ep, dtype=np.uint32)
+
+    def c_struct(self) -> L.Shapes:
+        return L.Shapes(
+            len(self.rt_ep),
+            L.ptr(self.rt_ep),
+            L.ptr(self.tag_ep),
+            L.ptr(self.dep_ep),
+            self.n_rt_ep,
+            self.n_tag_ep,
+            self.n_dep_ep,
+            max(1, self.n_status),
+        )
+
+
+class Engine:
+    """One ``kmz_ctx``.  ``stream`` is an optional hipStream_t (int/pointer)."""
+
+    def __init__(self, device: int = 0, stream: Optional[int] = None):
+        self._lib = L.lib()
+        self.ctx = self._lib.kmz_create(device, C.c_void_p(stream) if stream else None)
+        if not self.ctx:
+            raise RuntimeError(f"kmz_create({device}) failed: no HIP device visible (the engine has no CPU path)")
+        self.n = 0
+        self.index_base = 0
+        self.n_dep_ep = 0
+        self.n_status = 1
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self._lib.kmz_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- input ---------------------------------------------------------------
+    def load(self, batch: SpanBatch, shapes: ShapeTable):
+        s = batch.c_struct()
+        sh = shapes.c_struct()
+        L.check(self.ctx, self._lib.kmz_load(self.ctx, C.byref(s), C.byref(sh), L.MEM_HOST))
+        self.n = len(batch)
+        self.index_base = batch.index_base
+        self.n_dep_ep = shapes.n_dep_ep
+        self.n_status = max(1, shapes.n_status)
+
+    def load_synthetic(self, config: int, seed: int, trace_begin: int, trace_end: int) -> int:
+        n = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_synth_load(self.ctx, config, seed, trace_begin, trace_end, C.byref(n)))
+        d = L.SynthDesc()
+        self._lib.kmz_synth_describe(config, C.byref(d))
+        self.n = n.value
+        self.n_dep_ep = d.n_endpoints
+        self.n_status = d.n_status
+        return self.n
+
+    # ---- compute -------------------------------------------------------------
+    def run(self, flags: int):
+        L.check(self.ctx, self._lib.kmz_run(self.ctx, flags))
+
+    def sync(self):
+        L.check(self.ctx, self._lib.kmz_sync(self.ctx))
+
+    # ---- results -------------------------------------------------------------
+    def info(self) -> dict:
+        i = L.Info()
+        L.check(self.ctx, self._lib.kmz_get_info(self.ctx, C.byref(i)))
+        return {f: getattr(i, f) for f, _ in L.Info._fields_ if f != "pad"}
+
+    def groups(self) -> np.ndarray:
+        G = self.info()["n_groups"]
+        out = np.zeros(G, dtype=L.GROUP_DTYPE)
+        L.check(self.ctx, self._lib.kmz_get_groups(self.ctx, L.ptr(out), G))
+        return out
+
+    def endpoints(self) -> np.ndarray:
+        out = np.zeros(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE)
+        L.check(self.ctx, self._lib.kmz_get_endpoints(self.ctx, L.ptr(out), self.n_dep_ep))
+        return out
+
+    def triples(self) -> np.ndarray:
+        n = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, None, 0, C.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint64)
+        L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, L.ptr(out), n.value, C.byref(n)))
+        out.sort()
+        return out
+
+    def span_links(self):
+        cp = np.zeros(self.n, dtype=np.uint32)
+        rp = np.zeros(self.n, dtype=np.uint64)
+        L.check(self.ctx, self._lib.kmz_get_span_links(self.ctx, L.ptr(cp), L.ptr(rp), self.n))
+        return cp, rp
+
+    # ---- multi-GPU partials ----------------------------------------------------
+    def group_partials_ptr(self):
+        p, g = C.c_void_p(), C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_group_partials(self.ctx, C.byref(p), C.byref(g)))
+        return p.value, g.value
+
+    def endpoint_partials_ptr(self):
+        p, e = C.c_void_p(), C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_endpoint_partials(self.ctx, C.byref(p), C.byref(e)))
+        return p.value, e.value
+
+    def partials_words(self, which: int) -> int:
+        w = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_partials_size(self.ctx, which, C.byref(w)))
+        return w.value
+
+    def export_partials(self, which: int, dst_ptr: int, words: int, device: bool):
+        L.check(self.ctx, self._lib.kmz_partials_copy(self.ctx, which, C.c_void_p(dst_ptr), words,
+                                                      L.MEM_DEVICE if device else L.MEM_HOST, 0))
+
+    def import_partials(self, which: int, src_ptr: int, words: int, device: bool):
+        L.check(self.ctx, self._lib.kmz_partials_copy(self.ctx, which, C.c_void_p(src_ptr), words,
+                                                      L.MEM_DEVICE if device else L.MEM_HOST, 1))
+
+    def finalize(self):
+        L.check(self.ctx, self._lib.kmz_finalize(self.ctx))
+
+    # ---- profiling -------------------------------------------------------------
+    def set_profiling(self, on: bool):
+        L.check(self.ctx, self._lib.kmz_set_profiling(self.ctx, 1 if on else 0))
+
+    def kernel_times(self, reset: bool = False) -> dict:
+        ms = np.zeros(8, dtype=np.float64)
+        calls = np.zeros(8, dtype=np.uint64)
+        L.check(self.ctx, self._lib.kmz_kernel_times(self.ctx, L.ptr(ms), L.ptr(calls), 1 if reset else 0))
+        return {k: (float(ms[i]), int(calls[i])) for i, k in enumerate(L.KERNELS)}
+
+
+def finalize_host(partials: np.ndarray, n_groups: int) -> np.ndarray:
+    """Host finalisation of raw group partials (same arithmetic as the device)."""
+    p = np.ascontiguousarray(partials, dtype=np.uint64)
+    out = np.zeros(n_groups, dtype=L.GROUP_DTYPE)
+    L.lib().kmz_finalize_host(L.ptr(p), n_groups, L.ptr(out))
+    return out
+
+
+def decode_triples(keys: np.ndarray):
+    """key = anc_ep<<40 | desc_ep<<16 | distance<<1 | on  ->  column arrays."""
+    k = np.asarray(keys, dtype=np.uint64)
+    return (
+        (k >> np.uint64(40)).astype(np.int64),
+        ((k >> np.uint64(16)) & np.uint64(0xFFFFFF)).astype(np.int64),
+        ((k >> np.uint64(1)) & np.uint64(0x7FFF)).astype(np.int64),
+        (k & np.uint64(1)).astype(bool),
+    )

@@ -1,0 +1,171 @@
+"""Service-level risk (tail of the path).
+
+Mirror of ``src/utils/RiskAnalyzer.ts`` and ``src/utils/Normalizer.ts`` over
+the combined stats (engine K3 output) and service dependencies.  Host code:
+at most a few thousand services, O(services + links).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Sequence
+
+MINIMUM_PROB = 0.01
+
+
+def _to_precise(x: float) -> float:
+    t = (x + 2.220446049250313e-16) * 1e14
+    r = math.floor(t)
+    if t - r >= 0.5:
+        r += 1
+    return float(r) / 1e14
+
+
+class Normalizer:
+    """Normalizer.ts:17-70."""
+
+    @staticmethod
+    def Numbers(inp: Sequence[float], strategy, *args):
+        return strategy(list(inp), *args)
+
+    class Strategy:
+        @staticmethod
+        def BetweenFixedNumber(inp):
+            hi = max(inp) if inp else -math.inf
+            lo = min(inp) if inp else math.inf
+            if hi - lo == 0:
+                return [0.1]  # Normalizer.ts:22, a single element, as in the TS
+            return [((v - lo) / (hi - lo)) * 0.9 + 0.1 for v in inp]
+
+        @staticmethod
+        def Sigmoid(inp):
+            return [1 / (1 + math.exp(-v)) for v in inp]
+
+        @staticmethod
+        def SigmoidAdj(inp):
+            z = 2 * math.log(3)
+            return [_to_precise(1 / (1 + math.exp(-z * (v - 1.5)))) for v in inp]
+
+        @staticmethod
+        def FixedRatio(inp):
+            hi = max(inp) if inp else -math.inf
+            return inp if hi == 0 else [v / hi for v in inp]
+
+        @staticmethod
+        def Linear(inp, minimum=0.1):
+            if minimum >= 1:
+                return inp
+            return [v * (1 - minimum) + minimum for v in Normalizer.Strategy.FixedRatio(inp)]
+
+
+def _gateway(dep) -> bool:
+    return any(len(d["dependingBy"]) == 0 for d in dep["dependency"])
+
+
+def absolute_criticality(service_deps: List[dict]) -> List[dict]:
+    """RiskAnalyzer.ts:145-169: AIS = distance-1 dependents (+1 for a gateway),
+    ADS = distance-1 dependencies, ACS = AIS * ADS."""
+    out = []
+    for s in service_deps:
+        ais = 1 if _gateway(s) else 0
+        ads = 0
+        for l in s["links"]:
+            for det in l["details"]:
+                if det["distance"] == 1:
+                    ais += det["dependingBy"] > 0
+                    ads += det["dependingOn"] > 0
+        out.append({"uniqueServiceName": s["uniqueServiceName"], "factor": ais * ads, "ais": ais, "ads": ads})
+    return out
+
+
+def relying_factor(service_deps: List[dict]) -> List[dict]:
+    """RiskAnalyzer.ts:124-137."""
+    fm: Dict[str, float] = {}
+    for s in service_deps:
+        f = 0
+        for l in s["links"]:
+            for det in l["details"]:
+                f = f + det["dependingBy"] / det["distance"]
+        fm[s["uniqueServiceName"]] = f + (1 if _gateway(s) else 0)
+    return [{"uniqueServiceName": k, "factor": v} for k, v in fm.items()]
+
+
+def _collation_key(s: str):
+    # localeCompare on the ASCII service names KMamiz produces: punctuation <
+    # digits < letters, case-insensitive first (ICU root order); the synthetic
+    # names are zero padded so this equals code-unit order there.
+    prim = [(0, ord(c)) if not c.isalnum() else ((1, c) if c.isdigit() else (2, c.lower())) for c in s]
+    return prim, [c.isupper() for c in s]
+
+
+def impact(service_deps: List[dict], replicas: List[dict]) -> List[dict]:
+    """RiskAnalyzer.ts:51-85 (localeCompare-sorted factors zipped with a
+    code-unit-sorted name list, as the TS does)."""
+
+    def norm(lst):
+        lst = sorted(lst, key=lambda x: _collation_key(x["uniqueServiceName"]))
+        return Normalizer.Strategy.FixedRatio([x["factor"] for x in lst])
+
+    nrf = norm(relying_factor(service_deps))
+    nacs = norm(absolute_criticality(service_deps))
+    rep = {}
+    for r in replicas or []:
+        rep.setdefault(r["uniqueServiceName"], r.get("replicas"))
+    raw = []
+    for i, usn in enumerate(sorted(s["uniqueServiceName"] for s in service_deps)):
+        div = rep.get(usn) or 1
+        raw.append({"uniqueServiceName": usn, "impact": (nrf[i] + nacs[i]) / div})
+    ni = Normalizer.Strategy.Linear([r["impact"] for r in raw])
+    return [{**r, "impact": ni[i]} for i, r in enumerate(raw)]
+
+
+def probability(data: List[dict]) -> List[dict]:
+    """RiskAnalyzer.ts:87-122, 171-248."""
+    # latency CV per service weighted by request count (228-248)
+    cv: Dict[str, List[float]] = {}
+    for d in data:
+        a = cv.setdefault(d["uniqueServiceName"], [0.0, 0])
+        a[0] += d["latency"]["cv"] * d["combined"]
+        a[1] += d["combined"]
+    rel_names = list(cv)
+    rel_norm = Normalizer.Strategy.SigmoidAdj([cv[k][0] / cv[k][1] if cv[k][1] else math.nan for k in rel_names])
+    # invoke probability and 5xx error rate (171-213)
+    cnt: Dict[str, List[int]] = {}
+    for d in data:
+        a = cnt.setdefault(d["uniqueServiceName"], [0, 0])
+        a[0] += d["combined"]
+        a[1] += d["combined"] if str(d["status"]).startswith("5") else 0
+    total = 0
+    for v in cnt.values():
+        total += v[0]
+    names = list(cnt)
+    npro = [(cnt[k][0] / total) * (1 - MINIMUM_PROB) + MINIMUM_PROB for k in names]
+    nerr = [(cnt[k][1] / cnt[k][0]) * (1 - MINIMUM_PROB) + MINIMUM_PROB for k in names]
+    base = Normalizer.Strategy.Linear([p * nerr[i] for i, p in enumerate(npro)], MINIMUM_PROB)
+    base_of = dict(zip(names, base))
+    out = []
+    for k, nm in zip(rel_names, rel_norm):
+        b = base_of[k]
+        p = nm * (MINIMUM_PROB if b < MINIMUM_PROB else b)
+        out.append({"uniqueServiceName": k, "probability": p * (1 - MINIMUM_PROB) + MINIMUM_PROB})
+    return out
+
+
+def realtime_risk(data: List[dict], service_deps: List[dict], replicas: List[dict]) -> List[dict]:
+    """RiskAnalyzer.RealtimeRisk (RiskAnalyzer.ts:10-49)."""
+    imp = {}
+    for i in impact(service_deps, replicas):
+        imp.setdefault(i["uniqueServiceName"], i["impact"])
+    prob = {}
+    for p in probability(data):
+        prob.setdefault(p["uniqueServiceName"], p["probability"])
+    risks = []
+    for usn in dict.fromkeys(d["uniqueServiceName"] for d in data):
+        s, n, v = (usn.split("\t") + [None] * 3)[:3]
+        i = imp.get(usn) or 0
+        p = prob.get(usn) or MINIMUM_PROB
+        risks.append(
+            {"uniqueServiceName": usn, "service": s, "namespace": n, "version": v, "risk": i * p, "impact": i,
+             "probability": p}
+        )
+    norm = Normalizer.Strategy.BetweenFixedNumber([r["risk"] for r in risks])
+    return [{**r, **({"norm": norm[i]} if i < len(norm) else {})} for i, r in enumerate(risks)]

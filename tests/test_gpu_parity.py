@@ -1,0 +1,299 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracles.
+
+* reference fixtures (MockData) through the drop-in classes vs the reference's
+  own expected outputs / the Python oracle (order-exact JSON);
+* randomized "messy" batches (duplicate ids, cross-trace and missing parents,
+  CLIENT chains, non-SERVER ancestors, unparsable names) vs the Python oracle;
+* synthetic configs 2/3 vs the C oracle (bit-exact integers, 1e-9 latency);
+* size-independent properties at BASELINE.json's full sizes.
+"""
+import math
+import random
+
+import numpy as np
+import pytest
+
+from conftest import fixture
+from oracle import c_oracle
+from oracle import kmz_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-9  # north_star tolerance for latency statistics
+
+
+def _stats_equal(got, exp):
+    assert len(got) == len(exp)
+    for a, b in zip(got, exp):
+        for k in ("uniqueEndpointName", "uniqueServiceName", "service", "namespace", "version", "method", "status",
+                  "combined", "latestTimestamp", "avgReplica"):
+            assert a.get(k) == b.get(k), (k, a.get(k), b.get(k))
+        for k in ("mean", "cv"):
+            assert a["latency"][k] == pytest.approx(b["latency"][k], rel=REL, abs=1e-13), k
+
+
+def _run_both(traces, replicas=None):
+    from kmamiz_amd import Traces
+
+    ours = Traces(traces)
+    ref = O.Traces(traces)
+    return ours, ref
+
+
+# ---------------------------------------------------------------------------
+# reference fixtures
+# ---------------------------------------------------------------------------
+def test_pdas_endpoint_dependencies_exact(engine):
+    from kmamiz_amd import Traces
+
+    deps = Traces([fixture("MockTracePDAS")], engine=engine).toEndpointDependencies()
+    assert deps.toJSON() == fixture("MockEndpointDependenciesPDAS")  # Traces.test.ts:16-20
+
+
+def test_pdas_realtime_rows_exact(engine):
+    from kmamiz_amd import Traces
+
+    rl = Traces([fixture("MockTracePDAS")], engine=engine).toRealTimeData()
+    assert rl.toJSON() == fixture("MockRlDataPDAS")  # Traces.test.ts:11-14
+
+
+def test_endpoint_info_exact():
+    from kmamiz_amd import Traces
+
+    assert Traces.ToEndpointInfo(fixture("MockTracePDAS")[0]) == fixture("MockEndpointInfoPDAS1")
+
+
+def test_realtime_list_known_answer(engine):
+    from kmamiz_amd import RealtimeDataList
+
+    got = RealtimeDataList(fixture("MockBaseRlData1")).toCombinedRealtimeData().toJSON()
+    exp = fixture("MockBaseCrlData1")  # RealtimeDataList.test.ts:10-13, cv 0.17888543819998
+    assert len(got) == 1
+    for k in ("combined", "latestTimestamp", "avgReplica", "status", "uniqueEndpointName"):
+        assert got[0][k] == exp[0][k]
+    assert got[0]["latency"] == exp[0]["latency"]
+
+
+@pytest.mark.parametrize("fx", ["MockTracePDAS", "MockTrace", "MockData2_traces"])
+@pytest.mark.parametrize("rule", ["rt", "tag"])
+def test_fixture_stats_vs_oracle(engine, fx, rule):
+    traces = fixture(fx)
+    if fx != "MockTrace":
+        traces = [traces]
+    ours, ref = _run_both(traces)
+    reps = [{"uniqueServiceName": "details\tbook\tv1", "replicas": 3}]
+    if rule == "rt":
+        got = ours.toRealTimeData(reps).toCombinedRealtimeData().toJSON()
+        exp = ref.toRealTimeData(reps).toCombinedRealtimeData().toJSON()
+    else:
+        got = ours.combineLogsToRealtimeData([], reps).toCombinedRealtimeData().toJSON()
+        exp = ref.combineLogsToRealtimeData([], reps).toCombinedRealtimeData().toJSON()
+    _stats_equal(got, O.strip_undef(exp))
+
+
+@pytest.mark.parametrize("fx", ["MockTracePDAS", "MockTrace", "MockData2_traces"])
+def test_fixture_dependencies_vs_oracle(engine, fx):
+    traces = fixture(fx)
+    if fx != "MockTrace":
+        traces = [traces]
+    ours, ref = _run_both(traces)
+    got = ours.toEndpointDependencies()
+    exp = ref.toEndpointDependencies()
+    assert got.toJSON() == O.strip_undef(exp.toJSON())
+    # the worker's merge + the cache's trim (RealtimeWorkerImpl.ts:67-70)
+    from kmamiz_amd import EndpointDependencies
+
+    g2 = EndpointDependencies([]).combineWith(ours.toEndpointDependencies()).trim().toJSON()
+    e2 = O.EndpointDependencies([]).combineWith(ref.toEndpointDependencies()).trim().toJSON()
+    assert g2 == O.strip_undef(e2)
+    # service-level tail
+    gd = EndpointDependencies(g2)
+    od = O.EndpointDependencies(O.strip_undef(e2))
+    assert gd.toServiceInstability() == od.toServiceInstability()
+    assert gd.toServiceCoupling() == od.toServiceCoupling()
+    assert gd.toServiceEndpointCohesion() == od.toServiceEndpointCohesion()
+    assert gd.toChordData() == od.toChordData()
+
+
+# ---------------------------------------------------------------------------
+# randomized messy batches vs the Python oracle
+# ---------------------------------------------------------------------------
+NAMES = [
+    "a.ns1.svc.cluster.local:80/x",
+    "b.ns1.svc.cluster.local:9080/*",
+    "c.ns2.svc.c2:80/y",
+    "istio-ingressgateway",  # no ".svc." -> tag fallback in ToEndpointInfo
+    "dsvc.ns3.svc:81/z",
+    "e.svc.cluster.local/q",
+]
+URLS = ["http://a:80/x", "http://b/y?q=1", "https://10.0.0.1:8443/z#f", "c.ns2.svc.c2/p", "http://e"]
+
+
+def messy_batch(rng: random.Random, n_traces: int, pool: int):
+    ids = [f"{rng.getrandbits(64):016x}" for _ in range(pool)] + ["", "not-hex", "0000000000000000"]
+    traces = []
+    ts = 1646208338000000
+    for _ in range(n_traces):
+        tr = []
+        for _ in range(rng.randint(0, 7)):
+            s = {
+                "traceId": "t",
+                "id": rng.choice(ids),
+                "kind": rng.choice(["SERVER", "SERVER", "CLIENT", "CLIENT", "PRODUCER"]),
+                "name": rng.choice(NAMES),
+                "timestamp": ts + rng.randint(0, 10**7),
+                "duration": rng.randint(0, 10**6),
+                "tags": {
+                    "http.method": rng.choice(["GET", "POST"]),
+                    "http.url": rng.choice(URLS),
+                    "http.status_code": rng.choice(["200", "404", "500", "200 "]),
+                    "istio.canonical_service": rng.choice(["a", "b", "c"]),
+                    "istio.namespace": rng.choice(["ns1", "ns2"]),
+                    "istio.mesh_id": "cluster.local",
+                },
+            }
+            if rng.random() < 0.8:
+                s["tags"]["istio.canonical_revision"] = rng.choice(["v1", "v2", "latest"])
+            if rng.random() < 0.9:
+                s["parentId"] = rng.choice(ids)
+            tr.append(s)
+        traces.append(tr)
+    return traces
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_messy_batches_vs_oracle(engine, seed):
+    from kmamiz_amd import CycleError, Traces
+
+    rng = random.Random(seed)
+    traces = messy_batch(rng, rng.randint(0, 12), rng.choice([4, 8, 32]))
+    ref = O.Traces(traces)
+    try:
+        exp_deps = O.strip_undef(ref.toEndpointDependencies(max_depth=10000).toJSON())
+    except RuntimeError:
+        with pytest.raises(CycleError):
+            Traces(traces, engine=engine).toEndpointDependencies().toJSON()
+        return
+    ours = Traces(traces, engine=engine)
+    assert ours.toEndpointDependencies().toJSON() == exp_deps
+    for rule in ("rt", "tag"):
+        try:
+            exp = (ref.toRealTimeData() if rule == "rt" else ref.combineLogsToRealtimeData([])).toCombinedRealtimeData()
+        except TypeError:
+            with pytest.raises(TypeError):
+                ours.toRealTimeData().toCombinedRealtimeData()
+            continue
+        got = (ours.toRealTimeData() if rule == "rt" else ours.combineLogsToRealtimeData([])).toCombinedRealtimeData()
+        _stats_equal(got.toJSON(), O.strip_undef(exp.toJSON()))
+
+
+def test_empty_batch(engine):
+    from kmamiz_amd import Traces
+
+    t = Traces([], engine=engine)
+    assert t.toEndpointDependencies().toJSON() == []
+    assert t.toRealTimeData().toCombinedRealtimeData().toJSON() == []
+
+
+def test_cycle_is_reported(engine):
+    from kmamiz_amd import CycleError, Traces
+
+    a = {"id": "00000000000000aa", "parentId": "00000000000000bb", "kind": "SERVER", "name": "a.b.svc.c:1/x",
+         "timestamp": 1, "duration": 1, "tags": {"http.url": "http://a/x"}}
+    b = {**a, "id": "00000000000000bb", "parentId": "00000000000000aa"}
+    with pytest.raises(CycleError):
+        Traces([[a, b]], engine=engine).toEndpointDependencies()
+
+
+# ---------------------------------------------------------------------------
+# synthetic configs vs the C oracle
+# ---------------------------------------------------------------------------
+def _compare_synth(engine, batch, table):
+    from kmamiz_amd import _lib as L
+
+    engine.load(batch, table)
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    g = engine.groups()
+    o = c_oracle.stats(batch, table.tag_ep, table.n_tag_ep, table.n_status)
+    assert np.array_equal(g["combined"], o["combined"])
+    used = o["combined"] > 0
+    assert np.array_equal(g["latest_timestamp"][used], o["latest_timestamp"][used])
+    assert np.array_equal(g["first"][used], o["first"][used])
+    np.testing.assert_allclose(g["mean"][used], o["mean"][used], rtol=REL, atol=0)
+    np.testing.assert_allclose(g["cv"][used], o["cv"][used], rtol=REL, atol=1e-13)
+    keys = engine.triples()
+    ep = engine.endpoints()
+    info = engine.info()
+    okeys, oep, ocnt = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    assert np.array_equal(keys, okeys)
+    assert np.array_equal(ep["has_row"].astype(bool), oep["has_row"])
+    assert np.array_equal(ep["first_row"][oep["has_row"]], oep["first"][oep["has_row"]])
+    assert np.array_equal(ep["external"][oep["has_row"]].astype(bool), oep["external"][oep["has_row"]])
+    seen = ep["last_ts"] != np.iinfo(np.int64).min
+    last = np.where(seen, np.maximum(ep["last_ts"] / 1000.0, 0.0), 0.0)
+    assert np.array_equal(last, oep["last"])
+    assert info["n_rows"] == ocnt["rows"]
+    assert info["n_relations"] == ocnt["relations"]
+    assert info["max_depth"] == ocnt["max_depth"]
+    return info
+
+
+@pytest.mark.parametrize("config,ntr", [(2, 30000), (3, 4000)])
+def test_synthetic_vs_c_oracle(engine, config, ntr):
+    from kmamiz_amd import synth
+
+    batch, off = synth.host_batch(config, 0, ntr)
+    info = _compare_synth(engine, batch, synth.shape_table(config))
+    assert info["n_dups"] == 0
+
+
+def test_synthetic_shard_base_vs_c_oracle(engine):
+    from kmamiz_amd import synth
+
+    batch, off = synth.host_batch(3, 1000, 2500)
+    assert batch.index_base == synth.count_spans(3, 0, 1000)
+    _compare_synth(engine, batch, synth.shape_table(3))
+
+
+def test_device_generation_equals_host(engine):
+    """kmz_synth_load (device) produces the same batch as kmz_synth_host."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    for config, (t0, t1) in ((2, (5, 20000)), (3, (17, 3000))):
+        batch, _ = synth.host_batch(config, t0, t1)
+        table = synth.shape_table(config)
+        engine.load(batch, table)
+        engine.run(L.RUN_STATS_RT | L.RUN_DEPS)
+        a = (engine.groups(), engine.triples(), engine.endpoints(), engine.info())
+        n = engine.load_synthetic(config, synth.SEED, t0, t1)
+        assert n == len(batch)
+        engine.run(L.RUN_STATS_RT | L.RUN_DEPS)
+        b = (engine.groups(), engine.triples(), engine.endpoints(), engine.info())
+        assert a[0].tobytes() == b[0].tobytes()
+        assert np.array_equal(a[1], b[1])
+        assert a[2].tobytes() == b[2].tobytes()
+        assert a[3] == b[3]
+
+
+@pytest.mark.parametrize("config,ntr", [(2, 136000)])
+def test_full_size_properties(engine, config, ntr):
+    """Config 2 at its BASELINE size (1M spans): conservation + idempotence."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    n = engine.load_synthetic(config, synth.SEED, 0, ntr)
+    assert n > 990000
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    g1, k1, e1, i1 = engine.groups(), engine.triples(), engine.endpoints(), engine.info()
+    assert int(g1["combined"].sum()) == i1["n_server"] == i1["n_rows"]  # unique ids: every SERVER is a row
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    assert engine.groups().tobytes() == g1.tobytes()
+    assert np.array_equal(engine.triples(), k1)
+    # Bookinfo shape: exactly these (anc, desc, distance) edges
+    from kmamiz_amd import decode_triples
+
+    a, d, dist, on = decode_triples(k1)
+    edges = set(zip(a.tolist(), d.tolist(), dist.tolist(), on.tolist()))
+    assert edges == {(0, 1, 1, True), (0, 2, 1, True), (0, 3, 1, True), (0, 4, 1, True), (3, 5, 1, True),
+                     (4, 5, 1, True), (0, 5, 2, True)}
