@@ -315,6 +315,8 @@ int kmz_load(kmz_ctx *c, const kmz_spans *s, const kmz_shapes *sh, int where) {
 static int run_deps(kmz_ctx *c, bool links) {
   const uint32_t n = (uint32_t)c->n;
   c->cap = c->n * 5 / 3 + 64;  // load factor 0.6
+  // unique edge keys are far fewer than spans; start at ~n/32 (grown on overflow)
+  while (c->tcap < (1ull << 26) && c->tcap * 32 < c->n) c->tcap *= 2;
   if (ensure(c, c->table, c->cap * 8) || ensure(c, c->dups, (size_t)(n + 1) * sizeof(DupEntry)) ||
       ensure(c, c->dkey, (size_t)c->dcap * 4) || ensure(c, c->dval, (size_t)c->dcap * 4) ||
       ensure(c, c->cparent, (size_t)(n + 1) * 4) || ensure(c, c->trip, c->tcap * 8) ||

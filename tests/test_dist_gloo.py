@@ -1,0 +1,110 @@
+"""Multi-rank merge (kmamiz_amd.dist) with world_size 2 on gloo/CPU.
+
+Each rank takes half of the traces of a synthetic batch (whole traces, global
+indices via index_base), forms the engine's partial layout for its shard, and
+merges through the same functions the GPU path uses over RCCL.  The merged
+result must equal the single-batch oracle exactly (integers) / within 1e-9."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+U64 = np.uint64
+
+
+def shard_partials(batch, ep_of_shape, n_ep, n_status, dep_ep, n_dep):
+    """Engine partial layout for one shard (test-side restatement of K3/K4's
+    accumulators: integer moments, biased max timestamp, min first index)."""
+    G = n_ep * n_status
+    p = np.zeros(6 * G, dtype=U64)
+    p[4 * G : 5 * G] = 0
+    p[5 * G :] = U64(0xFFFFFFFFFFFFFFFF)
+    srv = np.nonzero(batch.kind == 1)[0]
+    g = ep_of_shape[batch.shape[srv]].astype(np.int64) * n_status + batch.status[srv]
+    d = batch.duration[srv].astype(U64)
+    dd = d * d
+    np.add.at(p, g, U64(1))
+    np.add.at(p, G + g, d)
+    np.add.at(p, 2 * G + g, dd & U64(0xFFFFFFFF))
+    np.add.at(p, 3 * G + g, dd >> U64(32))
+    tsx = batch.timestamp[srv].astype(np.int64).view(U64) ^ U64(1 << 63)
+    np.maximum.at(p, 4 * G + g, tsx)
+    np.minimum.at(p, 5 * G + g, (srv + batch.index_base).astype(U64))
+    # endpoint partials: rows = SERVER spans (unique ids in the synthetic data)
+    e = np.zeros(2 * n_dep, dtype=U64)
+    e[n_dep:] = U64(0xFFFFFFFFFFFFFFFF)
+    es = dep_ep[batch.shape[srv]].astype(np.int64)
+    np.maximum.at(e, es, tsx)
+    idx = {int(s): i for i, s in enumerate(batch.span_id.tolist())}
+    ext = np.array([0 if (batch.parent_id[i] and batch.kind[idx[int(batch.parent_id[i])]] == 2 and
+                          batch.parent_id[idx[int(batch.parent_id[i])]] != 0) else 1 for i in srv], dtype=U64)
+    np.minimum.at(e, n_dep + es, ((srv + batch.index_base).astype(U64) << U64(1)) | (U64(1) - ext))
+    return p, e
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kmamiz_amd import dist as kdist
+        from kmamiz_amd import finalize_host, synth
+        from oracle import c_oracle
+
+        cfg, ntr = synth.MESH, 600
+        table = synth.shape_table(cfg)
+        cut = [0, 250, ntr]
+        batch, _ = synth.host_batch(cfg, cut[rank], cut[rank + 1])
+        p, e = shard_partials(batch, table.tag_ep, table.n_tag_ep, table.n_status, table.dep_ep, table.n_dep_ep)
+        keys, _, _ = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+        G = table.n_tag_ep * table.n_status
+        pt = torch.from_numpy(p.view(np.int64).copy())
+        et = torch.from_numpy(e.view(np.int64).copy())
+        kdist.merge_group_partials(pt, G)
+        kdist.merge_endpoint_partials(et, table.n_dep_ep)
+        merged_keys = kdist.merge_edge_keys(torch.from_numpy(keys.view(np.int64).copy()))
+        if rank == 0:
+            full, _ = synth.host_batch(cfg, 0, ntr)
+            groups = finalize_host(pt.numpy().view(U64), G)
+            o = c_oracle.stats(full, table.tag_ep, table.n_tag_ep, table.n_status)
+            ok = bool(np.array_equal(groups["combined"], o["combined"]))
+            used = o["combined"] > 0
+            ok &= bool(np.array_equal(groups["latest_timestamp"][used], o["latest_timestamp"][used]))
+            ok &= bool(np.array_equal(groups["first"][used], o["first"][used]))
+            ok &= bool(np.allclose(groups["mean"][used], o["mean"][used], rtol=1e-9, atol=0))
+            ok &= bool(np.allclose(groups["cv"][used], o["cv"][used], rtol=1e-9, atol=1e-13))
+            okeys, oep, _ = c_oracle.deps(full, table.dep_ep, table.n_dep_ep)
+            ok &= bool(np.array_equal(np.sort(merged_keys.numpy().view(U64)), okeys))
+            ev = et.numpy().view(U64)
+            E = table.n_dep_ep
+            has = ev[E:] != U64(0xFFFFFFFFFFFFFFFF)
+            ok &= bool(np.array_equal(has, oep["has_row"]))
+            ok &= bool(np.array_equal(ev[E:][has] >> U64(1), oep["first"][has]))
+            ok &= bool(np.array_equal((ev[E:][has] & U64(1)) == 0, oep["external"][has]))
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_merge_equals_single_batch():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs)
+    assert q.get(timeout=10) is True
