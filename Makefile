@@ -6,7 +6,7 @@ SRC = kmamiz_amd/csrc/kmz_kernels.hip kmamiz_amd/csrc/kmz_api.hip
 HDR = include/kmz.h kmamiz_amd/csrc/kmz_common.h kmamiz_amd/csrc/kmz_synth.h kmamiz_amd/csrc/kmz_kernels.h
 OBJ = build/kmz_kernels.o build/kmz_api.o
 
-all: kmamiz_amd/libkmz.so oracle
+all: kmamiz_amd/libkmz.so oracle addon
 
 build/%.o: kmamiz_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
@@ -23,3 +23,12 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# Node N-API addon (seam 1 of SURVEY.md 8b); built when node headers exist
+NODE_INC ?= /usr/include/node
+js/kmz.node: js/kmz_napi.c include/kmz.h kmamiz_amd/libkmz.so
+	gcc -O2 -fPIC -shared -Wall -I$(NODE_INC) -o $@ js/kmz_napi.c -Lkmamiz_amd -lkmz -Wl,-rpath,'$$ORIGIN/../kmamiz_amd'
+
+addon:
+	@if [ -f $(NODE_INC)/node_api.h ]; then $(MAKE) js/kmz.node; else echo "no node headers: addon skipped"; fi
+.PHONY: addon

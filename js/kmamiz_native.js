@@ -1,0 +1,390 @@
+"use strict";
+/*
+ * kmamiz_native.js -- Node side of the drop-in boundary (SURVEY.md 8b seam 1).
+ *
+ * Turns KMamiz's `Trace[][]` into the columnar batch of include/kmz.h,
+ * calls the MI355X engine through the N-API addon (kmz.node), and returns
+ * the exact objects the reference's methods return:
+ *
+ *   NativeTraces#toRealTimeData(replicas)            Traces.ts:27-53
+ *   NativeTraces#combineLogsToRealtimeData([], reps) Traces.ts:55-106 (no-log case)
+ *   NativeRealtimeDataList#toCombinedRealtimeData()  RealtimeDataList.ts:22-97
+ *   NativeTraces#toEndpointDependencies()            Traces.ts:112-211
+ *   NativeTraces.ToEndpointInfo(trace)               Traces.ts:213-241
+ *
+ * The results are plain TRealtimeData / TCombinedRealtimeData /
+ * TEndpointDependency arrays.  Integration (INTEGRATION.md) wraps them in the
+ * reference's own RealtimeDataList / CombinedRealtimeDataList /
+ * EndpointDependencies classes, whose merge and service-level methods run
+ * unchanged.
+ *
+ * Node 12 compatible (no ?. / ??).
+ */
+const path = require("path");
+const addon = require(path.join(__dirname, "kmz.node"));
+
+const KIND_SERVER = 1;
+const KIND_CLIENT = 2;
+const NONE32 = 0xffffffff;
+const NONE64 = BigInt("0xffffffffffffffff");
+const SHAPE_TAGS = [
+  "http.method",
+  "http.url",
+  "istio.canonical_revision",
+  "istio.canonical_service",
+  "istio.namespace",
+  "istio.mesh_id",
+];
+
+// Utils.ExplodeUrl (Utils.ts:83-106): [host, port, path(, service, namespace, clusterName)]
+function explodeUrl(url, isServiceUrl) {
+  if (url.search(/[a-z]+:\/\//) === -1) url = "://" + url;
+  const m = url.match(/:\/\/([^:/]*)([:0-9]*)(.*)/) || [];
+  const out = [m[1], m[2], m[3]];
+  if (isServiceUrl) {
+    const s = m[1].match(/(.*).svc[.]*(.*)/) || [];
+    if (s[1]) {
+      const cut = s[1].lastIndexOf(".");
+      out.push(s[1].slice(0, cut), s[1].slice(cut + 1), s[2] || "cluster.local");
+    }
+  }
+  return out;
+}
+
+function tagsOf(key) {
+  const t = {};
+  for (let i = 0; i < SHAPE_TAGS.length; i++) t[SHAPE_TAGS[i]] = key[i + 1];
+  return t;
+}
+
+// identity rules, evaluated once per distinct shape
+const RULES = {
+  rt(key) {
+    const ex = explodeUrl(key[0], true);
+    const t = tagsOf(key);
+    const usn = `${ex[3]}\t${ex[4]}\t${t["istio.canonical_revision"]}`;
+    return {
+      service: ex[3],
+      namespace: ex[4],
+      version: t["istio.canonical_revision"],
+      method: t["http.method"],
+      uniqueServiceName: usn,
+      uniqueEndpointName: `${usn}\t${t["http.method"]}\t${t["http.url"]}`,
+    };
+  },
+  tag(key) {
+    const t = tagsOf(key);
+    const usn = `${t["istio.canonical_service"]}\t${t["istio.namespace"]}\t${t["istio.canonical_revision"]}`;
+    return {
+      service: t["istio.canonical_service"],
+      namespace: t["istio.namespace"],
+      version: t["istio.canonical_revision"],
+      method: t["http.method"],
+      uniqueServiceName: usn,
+      uniqueEndpointName: `${usn}\t${t["http.method"]}\t${t["http.url"]}`,
+    };
+  },
+  dep(key) {
+    const t = tagsOf(key);
+    const u = explodeUrl(t["http.url"]);
+    const ex = explodeUrl(key[0], true);
+    let service = ex[3], namespace = ex[4], clusterName = ex[5];
+    if (!key[0].includes(".svc.")) {
+      service = t["istio.canonical_service"];
+      namespace = t["istio.namespace"];
+      clusterName = t["istio.mesh_id"];
+    }
+    const version = t["istio.canonical_revision"] || "NONE";
+    const usn = `${service}\t${namespace}\t${version}`;
+    return {
+      version,
+      service,
+      namespace,
+      url: t["http.url"],
+      host: u[0],
+      path: u[2],
+      port: u[1] || "80",
+      clusterName,
+      method: t["http.method"],
+      uniqueServiceName: usn,
+      uniqueEndpointName: `${usn}\t${t["http.method"]}\t${t["http.url"]}`,
+    };
+  },
+};
+
+const HEX16 = /^[0-9a-f]{16}$/;
+
+// Trace[][] -> columnar batch + dictionaries
+function ingest(traces) {
+  const flat = [];
+  for (const t of traces) for (const s of t) flat.push(s);
+  const n = flat.length;
+  const sid = new BigUint64Array(n), pid = new BigUint64Array(n);
+  const kind = new Uint8Array(n), shape = new Uint32Array(n), status = new Uint16Array(n);
+  const duration = new Uint32Array(n), timestamp = new BigInt64Array(n);
+  const shapeIndex = new Map(), shapes = [];
+  const statusIndex = new Map(), statuses = [];
+  const canonical = new Set(), other = new Map();
+  const pendSid = [], pendPid = [];
+  const idOf = (v, i, pend) => {
+    if (typeof v === "string" && HEX16.test(v) && v !== "0000000000000000") {
+      const x = BigInt("0x" + v);
+      canonical.add(x);
+      return x;
+    }
+    if (!other.has(v)) other.set(v, 0n);
+    pend.push([i, v]);
+    return 0n;
+  };
+  for (let i = 0; i < n; i++) {
+    const s = flat[i];
+    const tags = s.tags || {};
+    sid[i] = idOf(s.id, i, pendSid);
+    if (s.parentId) pid[i] = idOf(s.parentId, i, pendPid);
+    kind[i] = s.kind === "SERVER" ? KIND_SERVER : s.kind === "CLIENT" ? KIND_CLIENT : 0;
+    const key = [s.name].concat(SHAPE_TAGS.map((k) => tags[k]));
+    const hk = JSON.stringify(key.map((v) => (v === undefined ? { u: 1 } : v)));
+    let si = shapeIndex.get(hk);
+    if (si === undefined) {
+      si = shapes.length;
+      shapeIndex.set(hk, si);
+      shapes.push(key);
+    }
+    shape[i] = si;
+    const st = tags["http.status_code"];
+    let k = statusIndex.get(st);
+    if (k === undefined) {
+      k = statuses.length;
+      statusIndex.set(st, k);
+      statuses.push(st);
+    }
+    status[i] = k;
+    if (!Number.isInteger(s.duration) || s.duration < 0 || s.duration >= 2 ** 32)
+      throw new RangeError(`span ${i}: duration ${s.duration} is not an integer number of microseconds`);
+    if (!Number.isInteger(s.timestamp)) throw new RangeError(`span ${i}: timestamp is not an integer`);
+    duration[i] = s.duration;
+    timestamp[i] = BigInt(s.timestamp);
+  }
+  // non-canonical ids: values no canonical id of the batch uses
+  let next = 1n;
+  for (const key of other.keys()) {
+    while (canonical.has(next)) next++;
+    other.set(key, next++);
+  }
+  for (const [i, v] of pendSid) sid[i] = other.get(v);
+  for (const [i, v] of pendPid) pid[i] = other.get(v);
+  // identities per shape and rule (errors kept, raised only when used)
+  const ident = {}, epOf = {}, epNames = {}, poison = {};
+  for (const rule of ["rt", "tag", "dep"]) {
+    const names = new Map();
+    ident[rule] = [];
+    epOf[rule] = new Uint32Array(shapes.length);
+    epNames[rule] = [];
+    poison[rule] = new Map();
+    shapes.forEach((key, i) => {
+      let f, err;
+      try {
+        f = RULES[rule](key);
+      } catch (e) {
+        err = e;
+      }
+      ident[rule].push(f);
+      let e;
+      if (err) {
+        e = epNames[rule].length;
+        epNames[rule].push(null);
+        poison[rule].set(e, err);
+      } else {
+        e = names.get(f.uniqueEndpointName);
+        if (e === undefined) {
+          e = epNames[rule].length;
+          names.set(f.uniqueEndpointName, e);
+          epNames[rule].push(f.uniqueEndpointName);
+        }
+      }
+      epOf[rule][i] = e;
+    });
+  }
+  return {
+    flat,
+    spans: { span_id: sid, parent_id: pid, kind, shape, status, duration, timestamp, index_base: 0 },
+    shapesTable: {
+      rt_ep: epOf.rt,
+      tag_ep: epOf.tag,
+      dep_ep: epOf.dep,
+      n_rt_ep: epNames.rt.length,
+      n_tag_ep: epNames.tag.length,
+      n_dep_ep: epNames.dep.length,
+      n_status: Math.max(1, statuses.length),
+    },
+    statuses,
+    ident,
+    poison,
+  };
+}
+
+function strip(o) {
+  const r = {};
+  for (const k of Object.keys(o)) if (o[k] !== undefined) r[k] = o[k];
+  return r;
+}
+
+function replicaOf(replicas, usn) {
+  if (!replicas) return undefined;
+  const r = replicas.find((x) => x.uniqueServiceName === usn);
+  return r ? r.replicas : undefined;
+}
+
+class NativeTraces {
+  constructor(traces, device) {
+    this._traces = traces;
+    this._device = device || 0;
+    this._b = null;
+    this._ctx = null;
+  }
+  toJSON() {
+    return this._traces;
+  }
+  _batch() {
+    if (!this._b) this._b = ingest(this._traces);
+    return this._b;
+  }
+  _engine() {
+    if (!this._ctx) {
+      const b = this._batch();
+      this._ctx = addon.create(this._device);
+      addon.load(this._ctx, b.spans, b.shapesTable);
+    }
+    return this._ctx;
+  }
+  toRealTimeData(replicas) {
+    return new NativeRealtimeDataList(this, "rt", replicas);
+  }
+  combineLogsToRealtimeData(structuredLogs, replicas) {
+    if ((structuredLogs || []).some((l) => l.traces.length))
+      throw new Error("Envoy log bodies (SURVEY.md 8f item 3) are not handled by the engine yet");
+    return new NativeRealtimeDataList(this, "tag", replicas);
+  }
+  toEndpointDependencies() {
+    const b = this._batch();
+    const ctx = this._engine();
+    addon.run(ctx, addon.RUN_DEPS | addon.RUN_SPAN_LINKS);
+    const n = b.flat.length;
+    const links = addon.spanLinks(ctx, n);
+    const E = b.shapesTable.n_dep_ep;
+    const ep = new DataView(addon.endpoints(ctx, E));
+    const dep = b.shapesTable.dep_ep;
+    const info = (i) => {
+      const f = b.ident.dep[b.spans.shape[i]];
+      if (!f) throw b.poison.dep.get(dep[b.spans.shape[i]]);
+      return strip(Object.assign({}, f, { timestamp: b.flat[i].timestamp / 1000 }));
+    };
+    const rows = [];
+    for (let i = 0; i < n; i++) if (links.rowpos[i] !== NONE64) rows.push(i);
+    rows.sort((a, c) => (links.rowpos[a] < links.rowpos[c] ? -1 : 1));
+    const lower = new Map();
+    const uppers = rows.map((s) => {
+      const chain = [];
+      for (let q = links.cparent[s], d = 1; q !== NONE32; q = links.cparent[q], d++) {
+        chain.push([q, d]);
+        if (!lower.has(q)) lower.set(q, []);
+        lower.get(q).push([s, d]);
+      }
+      return chain;
+    });
+    return rows.map((s, r) => {
+      const by = uppers[r].map(([q, d]) => ({ endpoint: info(q), distance: d, type: "CLIENT" }));
+      const seen = new Map();
+      for (const [t, d] of lower.get(s) || []) seen.set(`${dep[b.spans.shape[t]]}\t${d}`, [t, d]);
+      const on = [...seen.values()].map(([t, d]) => ({ endpoint: info(t), distance: d, type: "SERVER" }));
+      const e = dep[b.spans.shape[s]];
+      const last = ep.getBigInt64(e * 24, true);
+      const lastMs = Number(last) / 1000;
+      return {
+        endpoint: info(s),
+        lastUsageTimestamp: lastMs > 0 ? lastMs : 0,
+        isDependedByExternal: by.length === 0,
+        dependingBy: by,
+        dependingOn: on,
+      };
+    });
+  }
+  static ToEndpointInfo(trace) {
+    const tags = trace.tags || {};
+    const key = [trace.name].concat(SHAPE_TAGS.map((k) => tags[k]));
+    return strip(Object.assign(RULES.dep(key), { timestamp: trace.timestamp / 1000 }));
+  }
+}
+
+class NativeRealtimeDataList {
+  constructor(traces, rule, replicas) {
+    this._t = traces;
+    this._rule = rule;
+    this._replicas = replicas;
+  }
+  toJSON() {
+    const b = this._t._batch();
+    const out = [];
+    b.flat.forEach((s, i) => {
+      if (b.spans.kind[i] !== KIND_SERVER) return;
+      const f = b.ident[this._rule][b.spans.shape[i]];
+      if (!f) throw b.poison[this._rule].get(b.shapesTable[this._rule + "_ep"][b.spans.shape[i]]);
+      out.push(
+        strip({
+          timestamp: s.timestamp,
+          service: f.service,
+          namespace: f.namespace,
+          version: f.version,
+          method: f.method,
+          latency: s.duration / 1000,
+          status: (s.tags || {})["http.status_code"],
+          uniqueServiceName: f.uniqueServiceName,
+          uniqueEndpointName: f.uniqueEndpointName,
+          replica: replicaOf(this._replicas, f.uniqueServiceName),
+        })
+      );
+    });
+    return out;
+  }
+  toCombinedRealtimeData() {
+    const b = this._t._batch();
+    const ctx = this._t._engine();
+    addon.run(ctx, this._rule === "rt" ? addon.RUN_STATS_RT : addon.RUN_STATS_TAG);
+    const buf = addon.groups(ctx);
+    const G = buf.byteLength / 40;
+    const v = new DataView(buf);
+    const S = b.shapesTable.n_status;
+    const used = [];
+    const epFirst = new Map();
+    for (let g = 0; g < G; g++) {
+      const n = Number(v.getBigUint64(g * 40, true));
+      if (!n) continue;
+      const first = Number(v.getBigUint64(g * 40 + 8, true));
+      const e = Math.floor(g / S);
+      if (!epFirst.has(e) || first < epFirst.get(e)) epFirst.set(e, first);
+      used.push({ g, e, n, first });
+    }
+    used.sort((a, c) => epFirst.get(a.e) - epFirst.get(c.e) || a.first - c.first);
+    return used.map(({ g, e, n }) => {
+      const i = epFirst.get(e);
+      const f = b.ident[this._rule][b.spans.shape[i]];
+      if (!f) throw b.poison[this._rule].get(e);
+      const r = replicaOf(this._replicas, f.uniqueServiceName);
+      return strip({
+        uniqueServiceName: f.uniqueServiceName,
+        uniqueEndpointName: f.uniqueEndpointName,
+        service: f.service,
+        namespace: f.namespace,
+        version: f.version,
+        method: f.method,
+        status: b.statuses[g % S],
+        combined: n,
+        avgReplica: r ? (r * n) / n : undefined,
+        latestTimestamp: Number(v.getBigInt64(g * 40 + 16, true)),
+        latency: { mean: v.getFloat64(g * 40 + 24, true), cv: v.getFloat64(g * 40 + 32, true) },
+      });
+    });
+  }
+}
+
+module.exports = { NativeTraces, NativeRealtimeDataList, explodeUrl, ingest, addon };

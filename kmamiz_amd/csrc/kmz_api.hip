@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -58,6 +59,7 @@ struct kmz_ctx {
   uint32_t G = 0;        // group slots of the last stats run
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
+  uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
 
   // profiling
   bool prof = false;
@@ -213,6 +215,7 @@ kmz_ctx *kmz_create(int device, void *stream) {
     }
     c->own_stream = true;
   }
+  if (const char *a = getenv("KMZ_ABLATE")) c->ablate = (uint32_t)strtoul(a, nullptr, 0);
   if (ensure(c, c->counters, C_COUNT * 4) || ensure(c, c->stats64, S_COUNT * 8)) {
     delete c;
     return nullptr;
@@ -354,7 +357,7 @@ static int run_deps(kmz_ctx *c, bool links) {
     launch_walk(c->stream, c->sid, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
                 c->n_shapes, c->n_dep, c->index_base, P<unsigned long long>(c->table), c->cap,
                 P<unsigned int>(c->dkey), P<unsigned int>(c->dval), c->dcap, P<unsigned long long>(c->trip), c->tcap,
-                epp, epp + c->n_dep, links ? P<unsigned long long>(c->rowpos) : nullptr, cnt, st);
+                epp, epp + c->n_dep, links ? P<unsigned long long>(c->rowpos) : nullptr, cnt, st, c->ablate);
   }
   {
     Timed t(c, KMZ_K_FINAL);

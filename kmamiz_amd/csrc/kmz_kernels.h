@@ -36,7 +36,7 @@ void launch_walk(hipStream_t s, const uint64_t *sid, const uint8_t *kind, const 
                  uint64_t index_base, const unsigned long long *table, uint64_t cap, const unsigned int *dkey,
                  const unsigned int *dval, uint32_t dcap, unsigned long long *trip, uint64_t tcap,
                  unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *rowpos,
-                 unsigned int *counters, unsigned long long *stats64);
+                 unsigned int *counters, unsigned long long *stats64, uint32_t ablate = 0);
 void launch_finalize(hipStream_t s, unsigned long long *grp, uint32_t G, kmz_group *out);
 void launch_compact(hipStream_t s, const unsigned long long *trip, uint64_t tcap, unsigned long long *out,
                     unsigned long long *count);

@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(256) k_walk(const uint64_t *__restrict__ sid, 
                                               unsigned long long *__restrict__ ep_first,
                                               unsigned long long *__restrict__ rowpos_out,
                                               unsigned int *__restrict__ counters,
-                                              unsigned long long *__restrict__ stats64) {
+                                              unsigned long long *__restrict__ stats64, uint32_t ablate) {
   __shared__ unsigned long long l_set[K4_TSET];
   __shared__ unsigned long long l_ts[EP_DIRECT ? K4_EP_DIRECT : 1], l_first[EP_DIRECT ? K4_EP_DIRECT : 1];
   for (uint32_t s = threadIdx.x; s < K4_TSET; s += blockDim.x) l_set[s] = 0;
@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(256) k_walk(const uint64_t *__restrict__ sid, 
           if (EP_DIRECT) {
             atomicMax(&l_ts[es], (unsigned long long)tsx);
             atomicMin(&l_first[es], (unsigned long long)fkey);
-          } else {
+          } else if (!(ablate & 4)) {
             atomicMax(&ep_ts[es], (unsigned long long)tsx);
             atomicMin(&ep_first[es], (unsigned long long)fkey);
           }
@@ -385,7 +385,7 @@ __global__ void __launch_bounds__(256) k_walk(const uint64_t *__restrict__ sid, 
                            (ka == KIND_SERVER ? 1ull : 0ull);
             // LDS dedup, then the global set
             uint32_t h = (uint32_t)(mix64(key) >> 53);  // 11 bits
-            bool done = false;
+            bool done = (ablate & 1) != 0;  // diagnostic: skip edge-key dedup
             for (uint32_t p = 0; p < 8; ++p) {
               uint64_t c = l_set[h];
               if (c == key) {
@@ -402,7 +402,7 @@ __global__ void __launch_bounds__(256) k_walk(const uint64_t *__restrict__ sid, 
               }
               h = (h + 1) & (K4_TSET - 1);
             }
-            if (!done) triple_global(key, trip, tcap, counters);
+            if (!done && !(ablate & 2)) triple_global(key, trip, tcap, counters);
             if (ka != KIND_SERVER) {  // non-SERVER ancestors are not rows: count their use here
               uint64_t tsa = (uint64_t)ts[cur] ^ TS_BIAS;
               if (EP_DIRECT)
@@ -529,20 +529,20 @@ void launch_walk(hipStream_t s, const uint64_t *sid, const uint8_t *kind, const 
                  uint64_t index_base, const unsigned long long *table, uint64_t cap, const unsigned int *dkey,
                  const unsigned int *dval, uint32_t dcap, unsigned long long *trip, uint64_t tcap,
                  unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *rowpos,
-                 unsigned int *counters, unsigned long long *stats64) {
+                 unsigned int *counters, unsigned long long *stats64, uint32_t ablate) {
   if (!n) return;
   if (n_ep <= K4_EP_DIRECT) {
     uint32_t chunk = chunk_for(n, 4 * n_ep > 1024 ? 4 * n_ep : 1024);
     uint32_t blocks = (n + chunk - 1) / chunk;
     hipLaunchKernelGGL(k_walk<true>, dim3(blocks), dim3(256), 0, s, sid, kind, shape, ts, cparent, n, chunk, dep_ep,
                        n_shapes, n_ep, index_base, table, cap, dkey, dval, dcap, trip, tcap, ep_ts, ep_first, rowpos,
-                       counters, stats64);
+                       counters, stats64, ablate);
   } else {
     uint32_t chunk = chunk_for(n, 1024);
     uint32_t blocks = (n + chunk - 1) / chunk;
     hipLaunchKernelGGL(k_walk<false>, dim3(blocks), dim3(256), 0, s, sid, kind, shape, ts, cparent, n, chunk, dep_ep,
                        n_shapes, n_ep, index_base, table, cap, dkey, dval, dcap, trip, tcap, ep_ts, ep_first, rowpos,
-                       counters, stats64);
+                       counters, stats64, ablate);
   }
 }
 

@@ -1,0 +1,77 @@
+"""The Node side of the boundary (js/): N-API addon + JS ingest.
+
+CPU: the addon loads (context-aware N-API), its JS ExplodeUrl / ToEndpointInfo
+/ ingest agree with the oracle.  GPU: the whole path through Node equals the
+oracle (order-exact dependencies, 1e-9 latency stats)."""
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import FIX, ROOT, fixture
+from oracle import kmz_oracle as O
+
+NODE = shutil.which("node")
+ADDON = os.path.join(ROOT, "js", "kmz.node")
+pytestmark = pytest.mark.skipif(not NODE or not os.path.exists(ADDON), reason="node or js/kmz.node not available")
+
+
+def node(script, *args):
+    r = subprocess.run([NODE, "-e", script, *args], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+def test_addon_exports():
+    out = node("const k=require('./js/kmz.node');process.stdout.write(JSON.stringify(Object.keys(k)))")
+    assert {"create", "load", "run", "groups", "endpoints", "triples", "spanLinks", "info"} <= set(out)
+
+
+def test_js_explode_url_and_endpoint_info():
+    urls = ["http://example.com:8080/test/test", "https://192.168.1.1/test#123",
+            "service.test.svc.cluster.local:80/test/endpoint", "e.svc.cluster.local/q", "dsvc.ns3.svc:81/z"]
+    got = node(
+        "const {explodeUrl}=require('./js/kmamiz_native');"
+        "const u=JSON.parse(process.argv[1]);"
+        "process.stdout.write(JSON.stringify(u.map(x=>[explodeUrl(x),explodeUrl(x,true)])))",
+        json.dumps(urls),
+    )
+    for u, (a, b) in zip(urls, got):
+        assert a == [None if v is O.UNDEF else v for v in O.explode_url(u)]
+        assert b == [None if v is O.UNDEF else v for v in O.explode_url(u, True)]
+    traces = fixture("MockTrace")
+    info = node(
+        "const {NativeTraces}=require('./js/kmamiz_native');const fs=require('fs');"
+        "const t=JSON.parse(fs.readFileSync(process.argv[1]));"
+        "process.stdout.write(JSON.stringify([].concat(...t).map(s=>NativeTraces.ToEndpointInfo(s))))",
+        os.path.join(FIX, "MockTrace.json"),
+    )
+    assert info == [O.strip_undef(O.Traces.ToEndpointInfo(s)) for tr in traces for s in tr]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fx", ["MockTracePDAS", "MockTrace", "MockData2_traces"])
+def test_node_path_vs_oracle(fx, tmp_path):
+    traces = fixture(fx)
+    if fx != "MockTrace":
+        traces = [traces]
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(traces))
+    r = subprocess.run([NODE, "js/run_fixture.js", str(p)], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    ref = O.Traces(traces)
+    assert out["deps"] == O.strip_undef(ref.toEndpointDependencies().toJSON())
+    assert out["rl"] == O.strip_undef(ref.toRealTimeData().toJSON())
+    reps = [{"uniqueServiceName": "details\tbook\tv1", "replicas": 3}]
+    for key, exp in (("crl_rt", ref.toRealTimeData(reps)), ("crl_tag", ref.combineLogsToRealtimeData([], reps))):
+        e = O.strip_undef(exp.toCombinedRealtimeData().toJSON())
+        g = out[key]
+        assert [(x["uniqueEndpointName"], x["status"], x["combined"], x["latestTimestamp"], x.get("avgReplica"))
+                for x in g] == [(x["uniqueEndpointName"], x["status"], x["combined"], x["latestTimestamp"],
+                                 x.get("avgReplica")) for x in e]
+        for a, b in zip(g, e):
+            assert a["latency"]["mean"] == pytest.approx(b["latency"]["mean"], rel=1e-9)
+            assert a["latency"]["cv"] == pytest.approx(b["latency"]["cv"], rel=1e-9, abs=1e-13)
