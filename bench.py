@@ -126,7 +126,7 @@ def main():
             eng.finalize()
             state["keys"] = keys.cpu() if not args.no_fetch else keys
         elif not args.no_fetch:
-            state["keys"] = eng.triples()
+            state["keys"] = eng.triples(sort=False)
         if not args.no_fetch:
             state["groups"] = eng.groups()
             state["endpoints"] = eng.endpoints()

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -51,6 +52,10 @@ struct kmz_ctx {
   // workspace
   DevBuf table, dups, dkey, dval, cparent, rowpos, grp, grp_final, epp, trip, trip_out, counters, stats64, scratch;
   DevBuf synth_cnt, synth_off, dur_table;
+  DevBuf k3pool, k3dir, k3part, kdir, koff, kpool, scan_tmp, rdir, roff, rpool, tile_tmp;
+  uint32_t edge_R = 0;     // descendant endpoints per edge partition (K4T), 0 = auto
+  int path = 0;            // last dependency path: 1 = global table + walk, 2 = LDS-window tiles
+  bool tiles_off = false;  // a descendant endpoint overflowed the LDS edge set: global set for this batch
   uint64_t cap = 0, tcap = 1ull << 16;
   uint32_t dcap = 1024;
 
@@ -233,7 +238,9 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->in_ts,  &c->d_rt,      &c->d_tag,    &c->d_dep,     &c->table,     &c->dups,
                     &c->dkey,   &c->dval,      &c->cparent,  &c->rowpos,    &c->grp,       &c->grp_final,
                     &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->stats64,   &c->scratch,
-                    &c->synth_cnt, &c->synth_off, &c->dur_table};
+                    &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
+                    &c->kdir,   &c->koff,      &c->kpool,    &c->scan_tmp, &c->rdir, &c->roff, &c->rpool,
+                    &c->tile_tmp};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->own_stream) hipStreamDestroy(c->stream);
@@ -311,8 +318,68 @@ int kmz_load(kmz_ctx *c, const kmz_spans *s, const kmz_shapes *sh, int where) {
     c->ts = P<int64_t>(c->in_ts);
   }
   c->loaded = true;
+  c->tiles_off = false;
+  c->edge_R = 0;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KMZ_OK;
+}
+
+// K4 on LDS windows + partitioned edge-key dedup (unique span ids only)
+static int scan_u32(kmz_ctx *c, const uint32_t *in, uint32_t *out, size_t n) {
+  size_t tb = 0;
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)n, c->stream));
+  if (ensure(c, c->scan_tmp, tb)) return KMZ_E_HIP;
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tb, in, out, (int)n, c->stream));
+  return KMZ_OK;
+}
+
+static int run_walk_tiles(kmz_ctx *c, bool links) {
+  const uint32_t n = (uint32_t)c->n;
+  unsigned int *cnt = P<unsigned int>(c->counters);
+  unsigned long long *st = P<unsigned long long>(c->stats64);
+  unsigned long long *epp = P<unsigned long long>(c->epp);
+  if (n == 0 || c->n_dep == 0) return KMZ_OK;
+  // edge partitions, hashed by descendant endpoint: <= 6144 distinct keys each
+  if (!c->edge_R) c->edge_R = std::min<uint32_t>(k4_pmax(), std::max<uint32_t>(1, std::min(c->n_dep, 256u)));
+  for (;;) {
+    const uint32_t Pp = c->edge_R, nt = k4_tiles(n);
+    const size_t nd = (size_t)Pp * nt;
+    if (ensure(c, c->kdir, nd * 4) || ensure(c, c->rdir, nd * 4) || ensure(c, c->tile_tmp, (size_t)nt * 16) ||
+        ensure(c, c->kpool, k4_kreg_words(n) * 8) || ensure(c, c->rpool, k4_rreg_words(n) * 8) ||
+        ensure(c, c->trip_out, ((uint64_t)Pp * k4_set_cap() + 1) * 8))
+      return KMZ_E_HIP;
+    {
+      Timed t(c, KMZ_K_WALK);
+      launch_k4_walk(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
+                     c->n_shapes, c->n_dep, c->index_base, Pp, P<uint32_t>(c->kdir), P<unsigned long long>(c->kpool),
+                     P<uint32_t>(c->rdir), P<unsigned long long>(c->rpool),
+                     links ? P<unsigned long long>(c->rowpos) : nullptr, cnt, P<uint32_t>(c->tile_tmp), st);
+    }
+    {
+      Timed t(c, KMZ_K_FINAL);
+      launch_k4_dedup(c->stream, P<uint32_t>(c->kdir), P<unsigned long long>(c->kpool), P<uint32_t>(c->rdir),
+                      P<unsigned long long>(c->rpool), n, Pp, epp, epp + c->n_dep, P<unsigned long long>(c->trip_out),
+                      st, cnt);
+    }
+    unsigned int h[C_COUNT];
+    HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (h[C_FLAGS] & (F_CYCLE | F_RANGE)) return KMZ_OK;  // reported by kmz_run
+    if (!(h[C_FLAGS] & F_TRIPLE_OVERFLOW)) return KMZ_OK;
+    if (Pp * 4 > k4_pmax() || Pp >= c->n_dep) {
+      // staging or a single endpoint's edge set too large: global edge set
+      c->edge_R = 0;
+      return -100;
+    }
+    // too many distinct keys / endpoints in a partition: more partitions, redo
+    c->edge_R = Pp * 4;
+    HIPCHK(c, hipMemsetAsync(cnt + C_FLAGS, 0, 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(cnt + C_TRIPLES, 0, 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(st + S_ROWS, 0, 3 * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(st + S_TRIP_OUT, 0, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
+  }
 }
 
 static int run_deps(kmz_ctx *c, bool links) {
@@ -352,6 +419,22 @@ static int run_deps(kmz_ctx *c, bool links) {
     launch_resolve(c->stream, c->sid, c->pid, c->kind, n, P<unsigned long long>(c->table), c->cap,
                    P<uint32_t>(c->cparent), cnt);
   }
+  unsigned int hc[C_COUNT];
+  HIPCHK(c, hipMemcpyAsync(hc, c->counters.p, sizeof(hc), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (hc[C_DUPS] == 0 && !(c->ablate & 16) && !c->tiles_off) {
+    c->path = 2;
+    int r = run_walk_tiles(c, links);
+    if (r != -100) return r;
+    c->tiles_off = true;
+    // fall through to the global-set walk: reset what the tile path touched
+    HIPCHK(c, hipMemsetAsync(cnt + C_FLAGS, 0, 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(st + S_ROWS, 0, 3 * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(st + S_TRIP_OUT, 0, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
+  }
+  c->path = 1;
   {
     Timed t(c, KMZ_K_WALK);
     launch_walk(c->stream, c->sid, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
@@ -382,7 +465,19 @@ static int run_stats(kmz_ctx *c, uint32_t mode) {
     HIPCHK(c, hipMemsetAsync(grp, 0, G * 40, c->stream));
     HIPCHK(c, hipMemsetAsync(grp + 5 * G, 0xFF, G * 8, c->stream));
   }
-  {
+  const bool part = G > 1024 && k3_partitions((uint32_t)G) <= k3_pmax() && !(c->ablate & 8);
+  if (part) {
+    uint32_t Pp = k3_partitions((uint32_t)G), nt = k3_tiles(n);
+    uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(64, 2048 / Pp));
+    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, (size_t)Pp * nt * 4 + 4) ||
+        ensure(c, c->k3part, (size_t)S * 6 * G * 8) || ensure(c, c->tile_tmp, (size_t)nt * 16))
+      return KMZ_E_HIP;
+    Timed t(c, KMZ_K_STATS);
+    launch_k3_partitioned(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, tab, c->n_shapes, n_ep,
+                          c->n_status, c->index_base, grp, P<unsigned int>(c->counters),
+                          P<unsigned long long>(c->stats64) + S_SERVER, c->k3pool.p, P<uint32_t>(c->k3dir),
+                          P<unsigned long long>(c->k3part), S, P<uint32_t>(c->tile_tmp));
+  } else {
     Timed t(c, KMZ_K_STATS);
     launch_stats(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, tab, c->n_shapes, n_ep, c->n_status,
                  c->index_base, grp, P<unsigned int>(c->counters), P<unsigned long long>(c->stats64) + S_SERVER);
@@ -692,6 +787,8 @@ int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t 
   c->ts = o.timestamp;
   c->loaded = true;
   c->ran = 0;
+  c->tiles_off = false;
+  c->edge_R = 0;
   if (n_out) *n_out = n;
   return KMZ_OK;
 }

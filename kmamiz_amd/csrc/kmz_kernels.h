@@ -44,4 +44,29 @@ void launch_synth_count(hipStream_t s, int config, uint64_t seed, uint64_t t0, u
 void launch_synth_fill(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, const uint64_t *off,
                        uint64_t gbase, const uint32_t *dur_table, SynthOut out);
 
+// partitioned K3 / K4 (kmz_part.hip)
+void launch_k3_partitioned(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
+                           const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
+                           uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint64_t index_base,
+                           unsigned long long *grp, unsigned int *counters, unsigned long long *n_server, void *pool,
+                           uint32_t *dir, unsigned long long *part, uint32_t S, uint32_t *tile_tmp);
+uint32_t k3_partitions(uint32_t G);
+uint32_t k3_pmax();
+uint64_t k3_pool_bytes(uint32_t n);
+uint32_t k3_tiles(uint32_t n);
+uint32_t k4_tiles(uint32_t n);
+uint32_t k4_pmax();
+uint32_t k4_set_cap();
+uint64_t k4_kreg_words(uint32_t n);
+uint64_t k4_rreg_words(uint32_t n);
+void launch_k4_walk(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+                    const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
+                    uint64_t index_base, uint32_t P, uint32_t *kdir, unsigned long long *kreg, uint32_t *rdir,
+                    unsigned long long *rreg, unsigned long long *rowpos, unsigned int *counters,
+                    uint32_t *tile_stats, unsigned long long *stats64);
+void launch_k4_dedup(hipStream_t s, const uint32_t *kdir, const unsigned long long *kreg, const uint32_t *rdir,
+                     const unsigned long long *rreg, uint32_t n, uint32_t P, unsigned long long *ep_ts,
+                     unsigned long long *ep_first, unsigned long long *out, unsigned long long *stats64,
+                     unsigned int *counters);
+
 }  // namespace kmz

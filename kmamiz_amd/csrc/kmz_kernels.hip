@@ -449,9 +449,18 @@ __global__ void __launch_bounds__(256) k_finalize(GroupAcc acc, uint32_t G, kmz_
 __global__ void __launch_bounds__(256) k_compact(const unsigned long long *__restrict__ trip, uint64_t tcap,
                                                  unsigned long long *__restrict__ out,
                                                  unsigned long long *__restrict__ count) {
-  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < tcap; p += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t k = trip[p];
-    if (k) out[atomicAdd(count, 1ull)] = k;
+  // wave-aggregated: one atomic per wave that found keys
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t end = (tcap + stride - 1) / stride * stride;
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < end; p += stride) {
+    uint64_t k = p < tcap ? trip[p] : 0;
+    uint64_t m = __ballot(k != 0);
+    if (!m) continue;
+    uint32_t lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (k) out[base + __popcll(m & ((1ull << lane) - 1))] = k;
   }
 }
 

@@ -161,12 +161,13 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_get_endpoints(self.ctx, L.ptr(out), self.n_dep_ep))
         return out
 
-    def triples(self) -> np.ndarray:
+    def triples(self, sort: bool = True) -> np.ndarray:
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, None, 0, C.byref(n)))
         out = np.zeros(n.value, dtype=np.uint64)
         L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, L.ptr(out), n.value, C.byref(n)))
-        out.sort()
+        if sort:
+            out.sort()
         return out
 
     def span_links(self):

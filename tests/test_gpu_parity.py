@@ -297,3 +297,28 @@ def test_full_size_properties(engine, config, ntr):
     edges = set(zip(a.tolist(), d.tolist(), dist.tolist(), on.tolist()))
     assert edges == {(0, 1, 1, True), (0, 2, 1, True), (0, 3, 1, True), (0, 4, 1, True), (3, 5, 1, True),
                      (4, 5, 1, True), (0, 5, 2, True)}
+
+
+def test_hot_descendant_falls_back_to_global_edge_set(engine):
+    """One endpoint with > 6144 distinct (ancestor, distance) edges overflows the
+    LDS edge set of the tile path; the engine must fall back, not drop edges."""
+    from kmamiz_amd import Traces
+
+    traces = []
+    for k in range(7000):
+        base = f"{k + 1:012x}"
+        tags = lambda svc: {"http.url": f"http://{svc}/x", "http.method": "GET", "istio.canonical_revision": "v1",
+                            "http.status_code": "200"}
+        traces.append([
+            {"id": base + "0001", "kind": "SERVER", "name": f"a{k}.ns.svc.cluster.local:80/x", "timestamp": 1 + k,
+             "duration": 10, "tags": tags(f"a{k}")},
+            {"id": base + "0002", "parentId": base + "0001", "kind": "CLIENT", "name": "x.ns.svc.cluster.local:80/x",
+             "timestamp": 2 + k, "duration": 5, "tags": tags("x")},
+            {"id": base + "0003", "parentId": base + "0002", "kind": "SERVER", "name": "x.ns.svc.cluster.local:80/x",
+             "timestamp": 3 + k, "duration": 4, "tags": tags("x")},
+        ])
+    got = Traces(traces, engine=engine).toEndpointDependencies()
+    keys, _ = got.reduced()
+    assert len(keys) == 7000
+    exp = O.strip_undef(O.Traces(traces).toEndpointDependencies().toJSON())
+    assert got.toJSON() == exp
