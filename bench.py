@@ -126,9 +126,9 @@ def main():
             eng.finalize()
             state["keys"] = keys.cpu() if not args.no_fetch else keys
         elif not args.no_fetch:
-            state["keys"] = eng.triples(sort=False)
+            state["keys"] = eng.triples(sort=False, copy=False)
         if not args.no_fetch:
-            state["groups"] = eng.groups()
+            state["groups"] = eng.groups(copy=False)
             state["endpoints"] = eng.endpoints()
 
     for _ in range(args.warmup):

@@ -185,6 +185,10 @@ int kmz_finalize(kmz_ctx *ctx);
 /* host-side finalisation of one partial (same arithmetic as the device) */
 void kmz_finalize_host(const uint64_t *partials, uint64_t n_groups, kmz_group *out);
 
+/* ---- pinned host memory for result buffers (fast D2H) ---------------------- */
+void *kmz_host_alloc(uint64_t bytes);
+void kmz_host_free(void *p);
+
 /* ---- per-kernel timing (HIP events around each launch) ------------------- */
 #define KMZ_K_MEMSET 0
 #define KMZ_K_BUILD 1   /* K1 span-id table build     */

@@ -119,6 +119,8 @@ SIGNATURES = [
     ("kmz_partials_copy", C.c_int, [_P, C.c_int, _P, C.c_uint64, C.c_int, C.c_int]),
     ("kmz_finalize", C.c_int, [_P]),
     ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
+    ("kmz_host_alloc", _P, [C.c_uint64]),
+    ("kmz_host_free", None, [_P]),
     ("kmz_set_profiling", C.c_int, [_P, C.c_int]),
     ("kmz_kernel_times", C.c_int, [_P, _P, _P, C.c_int]),
     ("kmz_synth_describe", C.c_int, [C.c_int, C.POINTER(SynthDesc)]),

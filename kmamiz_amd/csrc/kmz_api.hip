@@ -340,39 +340,53 @@ static int run_walk_tiles(kmz_ctx *c, bool links) {
   unsigned long long *epp = P<unsigned long long>(c->epp);
   if (n == 0 || c->n_dep == 0) return KMZ_OK;
   // edge partitions, hashed by descendant endpoint: <= 6144 distinct keys each
-  if (!c->edge_R) c->edge_R = std::min<uint32_t>(k4_pmax(), std::max<uint32_t>(1, std::min(c->n_dep, 256u)));
+  if (!c->edge_R) c->edge_R = std::min<uint32_t>(k4_pmax(), std::max<uint32_t>(1, std::min(c->n_dep, 512u)));
   for (;;) {
     const uint32_t Pp = c->edge_R, nt = k4_tiles(n);
-    const size_t nd = (size_t)Pp * nt;
-    if (ensure(c, c->kdir, nd * 4) || ensure(c, c->rdir, nd * 4) || ensure(c, c->tile_tmp, (size_t)nt * 16) ||
-        ensure(c, c->kpool, k4_kreg_words(n) * 8) || ensure(c, c->rpool, k4_rreg_words(n) * 8) ||
+    const size_t nd = (size_t)Pp * nt + 1;
+    if (ensure(c, c->kdir, nd * 4) || ensure(c, c->koff, nd * 4) || ensure(c, c->rdir, nd * 4) ||
+        ensure(c, c->roff, nd * 4) || ensure(c, c->tile_tmp, (size_t)nt * 16))
+      return KMZ_E_HIP;
+    HIPCHK(c, hipMemsetAsync(P<uint32_t>(c->kdir) + nd - 1, 0, 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint32_t>(c->rdir) + nd - 1, 0, 4, c->stream));
+    {
+      Timed t(c, KMZ_K_WALK);
+      launch_k4_count(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
+                      c->n_shapes, c->n_dep, c->index_base, Pp, P<uint32_t>(c->kdir), P<uint32_t>(c->rdir),
+                      links ? P<unsigned long long>(c->rowpos) : nullptr, cnt, P<uint32_t>(c->tile_tmp), st);
+      int r = scan_u32(c, P<uint32_t>(c->kdir), P<uint32_t>(c->koff), nd);
+      if (!r) r = scan_u32(c, P<uint32_t>(c->rdir), P<uint32_t>(c->roff), nd);
+      if (r) return r;
+    }
+    unsigned int h[C_COUNT];
+    uint32_t tot[2] = {0, 0};
+    HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tot[0], P<uint32_t>(c->koff) + nd - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tot[1], P<uint32_t>(c->roff) + nd - 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (h[C_FLAGS] & (F_CYCLE | F_RANGE)) return KMZ_OK;  // reported by kmz_run
+    if (ensure(c, c->kpool, ((uint64_t)tot[0] + 1) * 8) || ensure(c, c->rpool, ((uint64_t)tot[1] + 1) * 16) ||
         ensure(c, c->trip_out, ((uint64_t)Pp * k4_set_cap() + 1) * 8))
       return KMZ_E_HIP;
     {
-      Timed t(c, KMZ_K_WALK);
-      launch_k4_walk(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
-                     c->n_shapes, c->n_dep, c->index_base, Pp, P<uint32_t>(c->kdir), P<unsigned long long>(c->kpool),
-                     P<uint32_t>(c->rdir), P<unsigned long long>(c->rpool),
-                     links ? P<unsigned long long>(c->rowpos) : nullptr, cnt, P<uint32_t>(c->tile_tmp), st);
-    }
-    {
       Timed t(c, KMZ_K_FINAL);
-      launch_k4_dedup(c->stream, P<uint32_t>(c->kdir), P<unsigned long long>(c->kpool), P<uint32_t>(c->rdir),
-                      P<unsigned long long>(c->rpool), n, Pp, epp, epp + c->n_dep, P<unsigned long long>(c->trip_out),
-                      st, cnt);
+      launch_k4_emit(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
+                     c->n_shapes, c->n_dep, c->index_base, Pp, P<uint32_t>(c->koff), P<unsigned long long>(c->kpool),
+                     P<uint32_t>(c->roff), P<unsigned long long>(c->rpool), cnt);
+      launch_k4_dedup(c->stream, P<unsigned long long>(c->kpool), P<uint32_t>(c->koff),
+                      P<unsigned long long>(c->rpool), P<uint32_t>(c->roff), n, Pp, epp, epp + c->n_dep,
+                      P<unsigned long long>(c->trip_out), st, cnt);
     }
-    unsigned int h[C_COUNT];
     HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (h[C_FLAGS] & (F_CYCLE | F_RANGE)) return KMZ_OK;  // reported by kmz_run
     if (!(h[C_FLAGS] & F_TRIPLE_OVERFLOW)) return KMZ_OK;
-    if (Pp * 4 > k4_pmax() || Pp >= c->n_dep) {
-      // staging or a single endpoint's edge set too large: global edge set
+    if (Pp * 2 > k4_pmax() || Pp >= c->n_dep) {
+      // a single endpoint's edge set exceeds the LDS set: global edge set
       c->edge_R = 0;
       return -100;
     }
     // too many distinct keys / endpoints in a partition: more partitions, redo
-    c->edge_R = Pp * 4;
+    c->edge_R = Pp * 2;
     HIPCHK(c, hipMemsetAsync(cnt + C_FLAGS, 0, 4, c->stream));
     HIPCHK(c, hipMemsetAsync(cnt + C_TRIPLES, 0, 4, c->stream));
     HIPCHK(c, hipMemsetAsync(st + S_ROWS, 0, 3 * 8, c->stream));
@@ -673,6 +687,16 @@ void kmz_finalize_host(const uint64_t *p, uint64_t G, kmz_group *out) {
     finalize_moments(p[g], p[G + g], p[2 * G + g], p[3 * G + g], &r.mean, &r.cv);
     out[g] = r;
   }
+}
+
+void *kmz_host_alloc(uint64_t bytes) {
+  void *p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 8, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+void kmz_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
 }
 
 int kmz_set_profiling(kmz_ctx *c, int on) {

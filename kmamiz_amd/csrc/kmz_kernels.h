@@ -57,16 +57,17 @@ uint32_t k3_tiles(uint32_t n);
 uint32_t k4_tiles(uint32_t n);
 uint32_t k4_pmax();
 uint32_t k4_set_cap();
-uint64_t k4_kreg_words(uint32_t n);
-uint64_t k4_rreg_words(uint32_t n);
-void launch_k4_walk(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+void launch_k4_count(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+                     const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
+                     uint64_t index_base, uint32_t P, uint32_t *kdir, uint32_t *rdir, unsigned long long *rowpos,
+                     unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64);
+void launch_k4_emit(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
                     const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
-                    uint64_t index_base, uint32_t P, uint32_t *kdir, unsigned long long *kreg, uint32_t *rdir,
-                    unsigned long long *rreg, unsigned long long *rowpos, unsigned int *counters,
-                    uint32_t *tile_stats, unsigned long long *stats64);
-void launch_k4_dedup(hipStream_t s, const uint32_t *kdir, const unsigned long long *kreg, const uint32_t *rdir,
-                     const unsigned long long *rreg, uint32_t n, uint32_t P, unsigned long long *ep_ts,
-                     unsigned long long *ep_first, unsigned long long *out, unsigned long long *stats64,
-                     unsigned int *counters);
+                    uint64_t index_base, uint32_t P, const uint32_t *koff, unsigned long long *kpool,
+                    const uint32_t *roff, unsigned long long *rpool, unsigned int *counters);
+void launch_k4_dedup(hipStream_t s, const unsigned long long *kpool, const uint32_t *koff,
+                     const unsigned long long *rpool, const uint32_t *roff, uint32_t n, uint32_t P,
+                     unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *out,
+                     unsigned long long *stats64, unsigned int *counters);
 
 }  // namespace kmz

@@ -38,41 +38,76 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long *dst, uint64_t v
 // slot = tag(key) << 32 | (index + 1); 0 = empty.  Insert claims an empty slot
 // with one 64-bit CAS; a slot whose tag matches is verified against
 // span_id[index] (the winner's row, usually in the same trace => cached).
+// Every thread carries KQ independent inserts in lockstep so that their slot
+// loads / CASes overlap (the probe chains are latency bound).
+constexpr int KQ = 4;
+
 __global__ void __launch_bounds__(256) k_build(const uint64_t *__restrict__ sid, uint32_t n,
                                                unsigned long long *__restrict__ table, uint64_t cap,
                                                DupEntry *__restrict__ dups, uint32_t dup_cap,
                                                unsigned int *__restrict__ counters) {
-  uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    uint64_t key = sid[i];
-    if (key == 0) {
-      atomicOr(&counters[C_FLAGS], F_ZERO_ID);
-      continue;
+  const uint64_t tile = (uint64_t)blockDim.x * KQ;
+  for (uint64_t b = (uint64_t)blockIdx.x * tile; b < n; b += (uint64_t)gridDim.x * tile) {
+    uint64_t key[KQ], val[KQ], pos[KQ];
+    uint32_t tag[KQ], idx[KQ];
+    bool act[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      uint64_t i = b + (uint64_t)q * blockDim.x + threadIdx.x;
+      act[q] = i < n;
+      idx[q] = (uint32_t)i;
+      key[q] = act[q] ? sid[i] : 0;
     }
-    uint32_t tag = tag_of(key);
-    uint64_t val = ((uint64_t)tag << 32) | (uint64_t)(i + 1);
-    uint64_t pos = slot_of(key, cap);
-    for (uint64_t probe = 0; probe < cap; ++probe) {
-      uint64_t cur = table[pos];
-      if (cur == 0) {
-        cur = atomicCAS(&table[pos], 0ull, (unsigned long long)val);
-        if (cur == 0) break;  // claimed
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      if (act[q] && key[q] == 0) {
+        atomicOr(&counters[C_FLAGS], F_ZERO_ID);
+        act[q] = false;
       }
-      if ((uint32_t)(cur >> 32) == tag) {
-        uint32_t w = (uint32_t)cur - 1;
-        if (sid[w] == key) {  // duplicate id: defer to the fixup
+      tag[q] = tag_of(key[q]);
+      val[q] = ((uint64_t)tag[q] << 32) | (uint64_t)(idx[q] + 1);
+      pos[q] = slot_of(key[q], cap);
+    }
+    for (uint64_t probe = 0; probe < cap; ++probe) {
+      bool any = false;
+      uint64_t cur[KQ];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) cur[q] = act[q] ? table[pos[q]] : 0;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+        if (act[q] && cur[q] == 0) cur[q] = atomicCAS(&table[pos[q]], 0ull, (unsigned long long)val[q]);
+      uint32_t w[KQ];
+      uint64_t wk[KQ];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        w[q] = (uint32_t)cur[q] - 1;
+        wk[q] = 0;
+        if (!act[q]) continue;
+        if (cur[q] == 0) {  // claimed
+          act[q] = false;
+          continue;
+        }
+        if ((uint32_t)(cur[q] >> 32) == tag[q]) wk[q] = sid[w[q]];
+      }
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        if (!act[q]) continue;
+        if ((uint32_t)(cur[q] >> 32) == tag[q] && wk[q] == key[q]) {  // duplicate id: defer to the fixup
           uint32_t d = atomicAdd(&counters[C_DUPS], 1u);
           if (d < dup_cap) {
-            dups[d].pos = (uint32_t)pos;
-            dups[d].idx = i;
-            dups[d].winner = w;
+            dups[d].pos = (uint32_t)pos[q];
+            dups[d].idx = idx[q];
+            dups[d].winner = w[q];
           } else {
             atomicOr(&counters[C_FLAGS], F_DUP_OVERFLOW);
           }
-          break;
+          act[q] = false;
+          continue;
         }
+        pos[q] = (pos[q] + 1 == cap) ? 0 : pos[q] + 1;
+        any = true;
       }
-      pos = (pos + 1 == cap) ? 0 : pos + 1;
+      if (!any) break;
       if (probe + 1 == cap) atomicOr(&counters[C_FLAGS], F_TABLE_FULL);
     }
   }
@@ -144,24 +179,90 @@ __global__ void __launch_bounds__(256) k_resolve(const uint64_t *__restrict__ si
                                                  const uint8_t *__restrict__ kind, uint32_t n,
                                                  const unsigned long long *__restrict__ table, uint64_t cap,
                                                  uint32_t *__restrict__ cparent, unsigned int *__restrict__ counters) {
-  uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    uint32_t q = NONE;
-    if (kind[i] != KIND_CLIENT) {
-      uint64_t p = pid[i];
-      uint32_t hops = 0;
-      while (p != 0) {
-        q = lookup(p, sid, table, cap);
-        if (q == NONE || kind[q] != KIND_CLIENT) break;
-        p = pid[q];
-        q = NONE;
-        if (++hops > MAX_DEPTH) {  // only an error if a row's walk reaches it (K4)
-          q = CYC;
-          break;
+  // KQ spans per thread walk their lookups in lockstep: one slot load per
+  // pending lookup per round, then the candidate's (span_id, kind, parent_id)
+  // together, so every round keeps KQ independent chains in flight.
+  const uint64_t tile = (uint64_t)blockDim.x * KQ;
+  for (uint64_t b = (uint64_t)blockIdx.x * tile; b < n; b += (uint64_t)gridDim.x * tile) {
+    uint64_t p[KQ], pos[KQ];
+    uint32_t tag[KQ], res[KQ], hops[KQ];
+    bool act[KQ];
+    uint8_t k0[KQ];
+    uint64_t p0[KQ];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      uint64_t i = b + (uint64_t)q * blockDim.x + threadIdx.x;
+      k0[q] = i < n ? kind[i] : KIND_CLIENT;
+      p0[q] = i < n ? pid[i] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      p[q] = k0[q] != KIND_CLIENT ? p0[q] : 0;
+      act[q] = p[q] != 0;
+      res[q] = NONE;
+      hops[q] = 0;
+      tag[q] = tag_of(p[q]);
+      pos[q] = slot_of(p[q], cap);
+    }
+    for (uint32_t round = 0; round < 4 * MAX_DEPTH; ++round) {
+      uint64_t cur[KQ];
+      bool any = false;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) cur[q] = act[q] ? table[pos[q]] : 0;
+      uint64_t vs[KQ], vp[KQ];
+      uint8_t vk[KQ];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        vs[q] = 0;
+        vp[q] = 0;
+        vk[q] = 0;
+        if (act[q] && cur[q] != 0 && (uint32_t)(cur[q] >> 32) == tag[q]) {
+          uint32_t w = (uint32_t)cur[q] - 1;
+          vs[q] = sid[w];
+          vk[q] = kind[w];
+          vp[q] = pid[w];
         }
       }
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        if (!act[q]) continue;
+        if (cur[q] == 0) {  // parent id absent: the walk stops (Traces.ts:133)
+          act[q] = false;
+          continue;
+        }
+        if ((uint32_t)(cur[q] >> 32) == tag[q] && vs[q] == p[q]) {
+          uint32_t w = (uint32_t)cur[q] - 1;
+          if (vk[q] != KIND_CLIENT) {
+            res[q] = w;
+            act[q] = false;
+            continue;
+          }
+          // CLIENT: skip it and continue with its parent (Traces.ts:134-137)
+          if (++hops[q] > MAX_DEPTH) {  // only an error if a row's walk reaches it (K4)
+            res[q] = CYC;
+            act[q] = false;
+            continue;
+          }
+          p[q] = vp[q];
+          if (p[q] == 0) {
+            act[q] = false;
+            continue;
+          }
+          tag[q] = tag_of(p[q]);
+          pos[q] = slot_of(p[q], cap);
+          any = true;
+          continue;
+        }
+        pos[q] = (pos[q] + 1 == cap) ? 0 : pos[q] + 1;
+        any = true;
+      }
+      if (!any) break;
     }
-    cparent[i] = q;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+      uint64_t i = b + (uint64_t)q * blockDim.x + threadIdx.x;
+      if (i < n) cparent[i] = res[q];
+    }
   }
 }
 
@@ -493,7 +594,8 @@ static inline uint32_t grid_for(uint64_t work, uint32_t cap_blocks = 8192) {
 void launch_build(hipStream_t s, const uint64_t *sid, uint32_t n, unsigned long long *table, uint64_t cap,
                   DupEntry *dups, uint32_t dup_cap, unsigned int *counters) {
   if (!n) return;
-  hipLaunchKernelGGL(k_build, dim3(grid_for(n)), dim3(256), 0, s, sid, n, table, cap, dups, dup_cap, counters);
+  hipLaunchKernelGGL(k_build, dim3(grid_for((n + KQ - 1) / KQ)), dim3(256), 0, s, sid, n, table, cap, dups, dup_cap,
+                     counters);
 }
 void launch_fixup(hipStream_t s, const DupEntry *dups, const unsigned int *counters, uint32_t dup_cap,
                   unsigned long long *table, unsigned int *dkey, unsigned int *dval, uint32_t dcap) {
@@ -503,7 +605,8 @@ void launch_fixup(hipStream_t s, const DupEntry *dups, const unsigned int *count
 void launch_resolve(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
                     const unsigned long long *table, uint64_t cap, uint32_t *cparent, unsigned int *counters) {
   if (!n) return;
-  hipLaunchKernelGGL(k_resolve, dim3(grid_for(n)), dim3(256), 0, s, sid, pid, kind, n, table, cap, cparent, counters);
+  hipLaunchKernelGGL(k_resolve, dim3(grid_for((n + KQ - 1) / KQ)), dim3(256), 0, s, sid, pid, kind, n, table, cap,
+                     cparent, counters);
 }
 
 static inline uint32_t chunk_for(uint32_t n, uint32_t min_chunk) {

@@ -252,17 +252,22 @@ uint64_t k3_pool_bytes(uint32_t n) { return (uint64_t)((n + K3T - 1) / K3T) * K3
 uint32_t k3_tiles(uint32_t n) { return (n + K3T - 1) / K3T; }
 
 // ===========================================================================
-// K4T -- one pass per 1024-span tile: LDS window walk, keys and endpoint
-// records staged in LDS sorted by edge partition, then written as ONE
-// contiguous block into the tile's fixed region (coalesced).  k4_dedup reads,
-// per partition, the partition's run of every tile.
+// K4T -- two passes over 2048-span tiles with their +-512-span LDS window:
+//   count: walk every row in LDS, count keys / endpoint records per edge
+//          partition -> dense [partition][tile] counts (+ per-tile stats);
+//   (exclusive scans place every (partition, tile) run contiguously)
+//   emit:  walk again, write keys / endpoint records at their final place;
+//   dedup: one workgroup per partition streams its contiguous keys into an
+//          LDS hash set and reduces the endpoint records it owns.
+// Partitions are hashed by DESCENDANT endpoint, so a key and its endpoint's
+// records always meet in one workgroup: the LDS set is exact, no global
+// atomics anywhere.
 // ===========================================================================
-constexpr uint32_t K4T = 1024, K4H = 512, K4W = K4T + 2 * K4H;
+constexpr uint32_t K4T = 2048, K4H = 512, K4W = K4T + 2 * K4H;
 constexpr uint16_t L_NONE = 0xFFFF, L_CYC = 0xFFFE, L_OUT = 0xFFFD;
 constexpr uint32_t K4PMAX = 1024;  // edge partitions
-constexpr int K4TT = 1024;         // walk threads (one own span each)
-constexpr uint32_t K4KCAP = 4096;  // keys staged per tile (32 KiB)
-constexpr uint32_t K4RCAP = 1536;  // endpoint records staged per tile (24 KiB)
+constexpr int K4TT = 512;          // walk threads
+constexpr int K4PER = K4T / K4TT;  // own spans per thread
 constexpr uint32_t K4SET = 8192;   // reducer LDS set slots (64 KiB)
 constexpr uint64_t FKEY_MASK = (1ull << 40) - 1;  // first_row<<1|!external, 40 bits
 constexpr uint32_t K4EMAP = 1024;  // endpoints per edge partition (LDS map slots)
@@ -301,140 +306,164 @@ __device__ __forceinline__ uint32_t edge_part(uint32_t es, uint32_t P) {
   return (uint32_t)(((uint64_t)(uint32_t)(mix64(es + 0x632BE59BD9B4E019ull) >> 32) * P) >> 32);
 }
 
+// window -> LDS with every global load of a thread issued before any is used
+__device__ __forceinline__ void load_window(uint32_t w0, uint32_t w1, const uint32_t *__restrict__ cparent,
+                                            const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
+                                            const uint32_t *__restrict__ dep_ep, uint32_t n_shapes, uint16_t *lcp,
+                                            uint8_t *lkind, uint32_t *lep) {
+  constexpr int PERW = (K4W + K4TT - 1) / K4TT;
+  uint32_t c[PERW], sh[PERW];
+  uint8_t k[PERW];
+#pragma unroll
+  for (int q = 0; q < PERW; ++q) {
+    uint32_t j = w0 + q * K4TT + threadIdx.x;
+    bool ok = j < w1;
+    c[q] = ok ? cparent[j] : NONE;
+    k[q] = ok ? kind[j] : 0;
+    sh[q] = ok ? shape[j] : NONE;
+  }
+  uint32_t e[PERW];
+#pragma unroll
+  for (int q = 0; q < PERW; ++q) e[q] = (k[q] != KIND_CLIENT && sh[q] < n_shapes) ? dep_ep[sh[q]] : NONE;
+#pragma unroll
+  for (int q = 0; q < PERW; ++q) {
+    uint32_t j = w0 + q * K4TT + threadIdx.x;
+    if (j < w1) {
+      lkind[j - w0] = k[q];
+      lep[j - w0] = e[q];
+      lcp[j - w0] =
+          c[q] == NONE ? L_NONE : (c[q] == CYC ? L_CYC : ((c[q] >= w0 && c[q] < w1) ? (uint16_t)(c[q] - w0) : L_OUT));
+    }
+  }
+}
+
+template <bool EMIT>
 __global__ void __launch_bounds__(K4TT) k4_walk(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
                                                 const int64_t *__restrict__ ts, const uint32_t *__restrict__ cparent,
                                                 uint32_t n, const uint32_t *__restrict__ dep_ep, uint32_t n_shapes,
                                                 uint32_t n_ep, uint64_t index_base, uint32_t P,
-                                                uint32_t *__restrict__ kdir, unsigned long long *__restrict__ kreg,
-                                                uint32_t *__restrict__ rdir, unsigned long long *__restrict__ rreg,
+                                                uint32_t *__restrict__ kdir, uint32_t *__restrict__ rdir,
+                                                const uint32_t *__restrict__ koff, const uint32_t *__restrict__ roff,
+                                                unsigned long long *__restrict__ kpool,
+                                                unsigned long long *__restrict__ rpool,
                                                 unsigned long long *__restrict__ rowpos_out,
                                                 unsigned int *__restrict__ counters,
                                                 uint32_t *__restrict__ tile_stats) {
   __shared__ uint16_t lcp[K4W];
   __shared__ uint8_t lkind[K4W];
   __shared__ uint32_t lep[K4W];
-  __shared__ uint32_t kcnt[K4PMAX], rcnt[K4PMAX], koff[K4PMAX], roff[K4PMAX];
-  __shared__ unsigned long long kst[K4KCAP];
-  __shared__ unsigned long long rst[2 * K4RCAP];
-  __shared__ uint32_t wave_tot[K4TT / 64 + 1];
+  __shared__ uint32_t kcnt[K4PMAX], rcnt[K4PMAX];
   __shared__ uint32_t red[K4TT / 64][3];
-  __shared__ uint32_t ktot, rtot;
-  const uint32_t tile = blockIdx.x, t0 = tile * K4T, t1 = min(n, t0 + K4T);
+  if (EMIT && (counters[C_FLAGS] & (F_CYCLE | F_RANGE))) return;  // the run fails anyway
+  const uint32_t tile = blockIdx.x, ntiles = gridDim.x, t0 = tile * K4T, t1 = min(n, t0 + K4T);
   const uint32_t w0 = t0 > K4H ? t0 - K4H : 0, w1 = min(n, t1 + K4H);
-  for (uint32_t p = threadIdx.x; p < P; p += K4TT) kcnt[p] = rcnt[p] = 0;
-  for (uint32_t j = w0 + threadIdx.x; j < w1; j += K4TT) {
-    uint32_t c = cparent[j];
-    uint8_t k = kind[j];
-    uint32_t sh = shape[j];
-    lkind[j - w0] = k;
-    lep[j - w0] = (k != KIND_CLIENT && sh < n_shapes) ? dep_ep[sh] : NONE;
-    lcp[j - w0] = c == NONE ? L_NONE : (c == CYC ? L_CYC : ((c >= w0 && c < w1) ? (uint16_t)(c - w0) : L_OUT));
-  }
+  for (uint32_t q = threadIdx.x; q < P; q += K4TT) kcnt[q] = rcnt[q] = 0;
+  load_window(w0, w1, cparent, kind, shape, dep_ep, n_shapes, lcp, lkind, lep);
   __syncthreads();
   const Window W{lcp, lkind, lep, w0, w1, cparent, kind, shape, dep_ep, n_shapes};
-  const uint32_t i = t0 + threadIdx.x;
-  const bool row = i < t1 && lkind[i - w0] == KIND_SERVER;
-  uint32_t es = NONE, p = 0, D = 0;
-  bool bad = false;
-  // pass 1: count keys / endpoint records per partition
-  if (row) {
-    es = lep[i - w0];
-    if (es >= n_ep) {
-      atomicOr(&counters[C_FLAGS], F_RANGE);
-      bad = true;
-    } else {
-      p = edge_part(es, P);
-      atomicAdd(&rcnt[p], 1u);
-      for (uint32_t cur = W.next(i); cur != NONE; cur = W.next(cur)) {
-        if (D >= MAX_DEPTH || cur == CYC) {
-          atomicOr(&counters[C_FLAGS], F_CYCLE);
-          bad = true;
-          break;
-        }
-        uint32_t ea = W.ep_of(cur);
-        if (ea >= n_ep) {
-          atomicOr(&counters[C_FLAGS], F_RANGE);
-          bad = true;
-          break;
-        }
-        if (W.kind_of(cur) != KIND_SERVER) atomicAdd(&rcnt[edge_part(ea, P)], 1u);
-        ++D;
-      }
-      if (!bad) atomicAdd(&kcnt[p], D);
+  uint32_t rows = 0, rel = 0, maxd = 0;
+  int64_t tsv[K4PER];
+  if (EMIT) {
+#pragma unroll
+    for (int q = 0; q < K4PER; ++q) {
+      uint32_t i = t0 + q * K4TT + threadIdx.x;
+      tsv[q] = (i < t1 && lkind[i - w0] == KIND_SERVER) ? ts[i] : 0;
     }
   }
-  if (rowpos_out && i < t1) rowpos_out[i] = row && !bad ? index_base + i : NONE64;
-  __syncthreads();
-  // tile-local offsets (partition-sorted staging)
-  uint32_t kt = block_excl_scan_pairs<K4TT>(kcnt, koff, P, wave_tot);
-  if (threadIdx.x == 0) ktot = kt;
-  __syncthreads();
-  uint32_t rt = block_excl_scan_pairs<K4TT>(rcnt, roff, P, wave_tot);
-  if (threadIdx.x == 0) rtot = rt;
-  __syncthreads();
-  if (ktot > K4KCAP || rtot > K4RCAP) {  // tile too dense for the staging: host retries smaller
-    if (threadIdx.x == 0) atomicOr(&counters[C_FLAGS], F_TRIPLE_OVERFLOW);
-    return;
-  }
-  for (uint32_t q = threadIdx.x; q < P; q += K4TT) {
-    kdir[(uint64_t)q * gridDim.x + tile] = (koff[q] << 16) | kcnt[q];
-    rdir[(uint64_t)q * gridDim.x + tile] = (roff[q] << 16) | rcnt[q];
-    kcnt[q] = 0;
-    rcnt[q] = 0;
-  }
-  __syncthreads();
-  // pass 2: stage keys and endpoint records
-  if (row && !bad) {
-    uint32_t kpos = koff[p] + atomicAdd(&kcnt[p], D);
-    uint32_t rpos = roff[p] + atomicAdd(&rcnt[p], 1u);
-    uint32_t cur = W.next(i);
-    rst[2 * rpos] = ((uint64_t)es << 40) | ((((index_base + i) << 1) | (cur != NONE ? 1ull : 0ull)) & FKEY_MASK);
-    rst[2 * rpos + 1] = (uint64_t)ts[i] ^ TS_BIAS;
-    for (uint32_t d = 1; d <= D; ++d, cur = W.next(cur)) {
-      uint8_t ka = W.kind_of(cur);
-      uint32_t ea = W.ep_of(cur);
-      kst[kpos + d - 1] =
-          ((uint64_t)ea << 40) | ((uint64_t)es << 16) | ((uint64_t)d << 1) | (ka == KIND_SERVER ? 1ull : 0ull);
-      if (ka != KIND_SERVER) {  // non-SERVER ancestors are not rows: their use counts for lastUsage
-        uint32_t pa = edge_part(ea, P);
-        uint32_t r = roff[pa] + atomicAdd(&rcnt[pa], 1u);
-        rst[2 * r] = ((uint64_t)ea << 40) | FKEY_MASK;
-        rst[2 * r + 1] = (uint64_t)ts[cur] ^ TS_BIAS;
+#pragma unroll
+  for (int q = 0; q < K4PER; ++q) {
+    const uint32_t i = t0 + q * K4TT + threadIdx.x;
+    uint64_t rp = NONE64;
+    if (i < t1 && lkind[i - w0] == KIND_SERVER) {
+      const uint32_t es = lep[i - w0];
+      if (es >= n_ep) {
+        atomicOr(&counters[C_FLAGS], F_RANGE);
+      } else {
+        const uint32_t p = edge_part(es, P);
+        const uint32_t first = W.next(i);
+        uint32_t D = 0;
+        bool bad = false;
+        for (uint32_t cur = first; cur != NONE; cur = W.next(cur)) {
+          if (D >= MAX_DEPTH || cur == CYC) {
+            atomicOr(&counters[C_FLAGS], F_CYCLE);
+            bad = true;
+            break;
+          }
+          uint32_t ea = W.ep_of(cur);
+          if (ea >= n_ep) {
+            atomicOr(&counters[C_FLAGS], F_RANGE);
+            bad = true;
+            break;
+          }
+          if (!EMIT && W.kind_of(cur) != KIND_SERVER) atomicAdd(&rcnt[edge_part(ea, P)], 1u);
+          ++D;
+        }
+        if (!bad) {
+          rp = index_base + i;
+          if (!EMIT) {
+            atomicAdd(&kcnt[p], D);
+            atomicAdd(&rcnt[p], 1u);
+            ++rows;
+            rel += D;
+            maxd = max(maxd, D);
+          } else {
+            uint64_t kb = koff[(uint64_t)p * ntiles + tile] + atomicAdd(&kcnt[p], D);
+            uint64_t rb = roff[(uint64_t)p * ntiles + tile] + atomicAdd(&rcnt[p], 1u);
+            rpool[2 * rb] = ((uint64_t)es << 40) | (((rp << 1) | (first != NONE ? 1ull : 0ull)) & FKEY_MASK);
+            rpool[2 * rb + 1] = (uint64_t)tsv[q] ^ TS_BIAS;
+            uint32_t cur = first;
+            for (uint32_t d = 1; d <= D; ++d, cur = W.next(cur)) {
+              uint8_t ka = W.kind_of(cur);
+              uint32_t ea = W.ep_of(cur);
+              kpool[kb + d - 1] = ((uint64_t)ea << 40) | ((uint64_t)es << 16) | ((uint64_t)d << 1) |
+                                  (ka == KIND_SERVER ? 1ull : 0ull);
+              if (ka != KIND_SERVER) {  // non-SERVER ancestors are not rows: their use counts for lastUsage
+                uint32_t pa = edge_part(ea, P);
+                uint64_t r = roff[(uint64_t)pa * ntiles + tile] + atomicAdd(&rcnt[pa], 1u);
+                rpool[2 * r] = ((uint64_t)ea << 40) | FKEY_MASK;
+                rpool[2 * r + 1] = (uint64_t)ts[cur] ^ TS_BIAS;
+              }
+            }
+          }
+        }
       }
     }
+    if (!EMIT && rowpos_out && i < t1) rowpos_out[i] = rp;
   }
-  __syncthreads();
-  // one contiguous block per tile
-  unsigned long long *kd = kreg + (uint64_t)tile * K4KCAP;
-  for (uint32_t w = threadIdx.x; w < ktot; w += K4TT) kd[w] = kst[w];
-  unsigned long long *rd = rreg + (uint64_t)tile * 2 * K4RCAP;
-  for (uint32_t w = threadIdx.x; w < 2 * rtot; w += K4TT) rd[w] = rst[w];
-  // per-tile statistics (summed by one workgroup later)
-  uint32_t r32 = row && !bad ? 1u : 0u, l32 = row && !bad ? D : 0u, md = l32;
-  for (int o = 32; o > 0; o >>= 1) {
-    l32 += __shfl_xor(l32, o, 64);
-    r32 += __shfl_xor(r32, o, 64);
-    md = max(md, (uint32_t)__shfl_xor(md, o, 64));
-  }
-  if ((threadIdx.x & 63) == 0) {
-    red[threadIdx.x >> 6][0] = r32;
-    red[threadIdx.x >> 6][1] = l32;
-    red[threadIdx.x >> 6][2] = md;
-  }
-  __syncthreads();
-  if (threadIdx.x < 3) {
-    uint32_t a = 0;
-    for (int w = 0; w < K4TT / 64; ++w) a = threadIdx.x == 2 ? max(a, red[w][2]) : a + red[w][threadIdx.x];
-    tile_stats[(uint64_t)tile * 4 + threadIdx.x] = a;
+  if (!EMIT) {
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < P; q += K4TT) {
+      kdir[(uint64_t)q * ntiles + tile] = kcnt[q];
+      rdir[(uint64_t)q * ntiles + tile] = rcnt[q];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      rel += __shfl_xor(rel, o, 64);
+      rows += __shfl_xor(rows, o, 64);
+      maxd = max(maxd, (uint32_t)__shfl_xor(maxd, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      red[threadIdx.x >> 6][0] = rows;
+      red[threadIdx.x >> 6][1] = rel;
+      red[threadIdx.x >> 6][2] = maxd;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      uint32_t a = 0;
+      for (int w = 0; w < K4TT / 64; ++w) a = threadIdx.x == 2 ? max(a, red[w][2]) : a + red[w][threadIdx.x];
+      tile_stats[(uint64_t)tile * 4 + threadIdx.x] = a;
+    }
   }
 }
 
 // one workgroup per edge partition: exact key dedup in an LDS hash set and the
-// per-endpoint (max ts, min first row) of the endpoints the partition owns
-__global__ void __launch_bounds__(1024) k4_dedup(const uint32_t *__restrict__ kdir,
-                                                 const unsigned long long *__restrict__ kreg,
-                                                 const uint32_t *__restrict__ rdir,
-                                                 const unsigned long long *__restrict__ rreg, uint32_t ntiles,
+// per-endpoint (max ts, min first row) of the endpoints the partition owns.
+// Loads are issued 8 per thread before they are consumed (memory-level
+// parallelism: the LDS work in between would otherwise serialise them).
+constexpr int K4B = 8;
+__global__ void __launch_bounds__(1024) k4_dedup(const unsigned long long *__restrict__ kpool,
+                                                 const uint32_t *__restrict__ koff,
+                                                 const unsigned long long *__restrict__ rpool,
+                                                 const uint32_t *__restrict__ roff, uint32_t ntiles,
                                                  unsigned long long *__restrict__ ep_ts,
                                                  unsigned long long *__restrict__ ep_first,
                                                  unsigned long long *__restrict__ out,
@@ -455,50 +484,67 @@ __global__ void __launch_bounds__(1024) k4_dedup(const uint32_t *__restrict__ kd
   if (threadIdx.x == 0) used = cursor = 0;
   __syncthreads();
   bool full = false;
-  const uint32_t *kd = kdir + (uint64_t)p * ntiles, *rd = rdir + (uint64_t)p * ntiles;
-  for (uint32_t t = threadIdx.x; t < ntiles; t += blockDim.x) {
-    // endpoint records of this tile's run
-    uint32_t w = rd[t];
-    const unsigned long long *r = rreg + (uint64_t)t * 2 * K4RCAP + 2 * (w >> 16);
-    for (uint32_t q = 0; q < (w & 0xFFFF); ++q) {
-      uint64_t a = r[2 * q], tsx = r[2 * q + 1];
-      uint32_t e = (uint32_t)(a >> 40), f = e + 1;
-      uint32_t h = (uint32_t)(mix64(e) >> 54);  // 10 bits
-      uint32_t z = 0;
-      for (; z < K4EMAP; ++z) {
-        uint32_t c = mkey[h];
-        if (c == 0) c = atomicCAS(&mkey[h], 0u, f);
-        if (c == 0 || c == f) break;
-        h = (h + 1) & (K4EMAP - 1);
+  {  // endpoint records
+    const uint64_t b = roff[(uint64_t)p * ntiles], e = roff[(uint64_t)(p + 1) * ntiles];
+    for (uint64_t j0 = b; j0 < e; j0 += (uint64_t)K4B * blockDim.x) {
+      uint64_t a[K4B], t[K4B];
+#pragma unroll
+      for (int q = 0; q < K4B; ++q) {
+        uint64_t j = j0 + (uint64_t)q * blockDim.x + threadIdx.x;
+        a[q] = j < e ? rpool[2 * j] : ~0ull;
+        t[q] = j < e ? rpool[2 * j + 1] : 0;
       }
-      if (z == K4EMAP) {
-        full = true;
-        continue;
-      }
-      atomicMax(&mts[h], (unsigned long long)tsx);
-      if ((a & FKEY_MASK) != FKEY_MASK) atomicMin(&mfirst[h], (unsigned long long)(a & FKEY_MASK));
-    }
-    // edge keys of this tile's run
-    w = kd[t];
-    const unsigned long long *k = kreg + (uint64_t)t * K4KCAP + (w >> 16);
-    for (uint32_t q = 0; q < (w & 0xFFFF); ++q) {
-      uint64_t key = k[q];
-      uint32_t h = (uint32_t)(mix64(key) >> 51);  // 13 bits
-      uint32_t z = 0;
-      for (; z < 128; ++z) {
-        uint64_t c = set[h];
-        if (c == key) break;
-        if (c == 0) {
-          c = atomicCAS(&set[h], 0ull, (unsigned long long)key);
-          if (c == 0) {
-            atomicAdd(&used, 1u);
-            break;
-          }
-          if (c == key) break;
+#pragma unroll
+      for (int q = 0; q < K4B; ++q) {
+        if (a[q] == ~0ull) continue;
+        uint32_t ee = (uint32_t)(a[q] >> 40), f = ee + 1;
+        uint32_t h = (uint32_t)(mix64(ee) >> 54);  // 10 bits
+        uint32_t z = 0;
+        for (; z < K4EMAP; ++z) {
+          uint32_t c = mkey[h];
+          if (c == 0) c = atomicCAS(&mkey[h], 0u, f);
+          if (c == 0 || c == f) break;
+          h = (h + 1) & (K4EMAP - 1);
         }
-        h = (h + 1) & (K4SET - 1);
+        if (z == K4EMAP) {
+          full = true;
+          continue;
+        }
+        atomicMax(&mts[h], (unsigned long long)t[q]);
+        if ((a[q] & FKEY_MASK) != FKEY_MASK) atomicMin(&mfirst[h], (unsigned long long)(a[q] & FKEY_MASK));
       }
-      if (z == 128) full = true;
+    }
+  }
+  {  // edge keys
+    const uint64_t b = koff[(uint64_t)p * ntiles], e = koff[(uint64_t)(p + 1) * ntiles];
+    for (uint64_t j0 = b; j0 < e; j0 += (uint64_t)K4B * blockDim.x) {
+      uint64_t kk[K4B];
+#pragma unroll
+      for (int q = 0; q < K4B; ++q) {
+        uint64_t j = j0 + (uint64_t)q * blockDim.x + threadIdx.x;
+        kk[q] = j < e ? kpool[j] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < K4B; ++q) {
+        const uint64_t key = kk[q];
+        if (!key) continue;
+        uint32_t h = (uint32_t)(mix64(key) >> 51);  // 13 bits
+        uint32_t z = 0;
+        for (; z < 128; ++z) {
+          uint64_t c = set[h];
+          if (c == key) break;
+          if (c == 0) {
+            c = atomicCAS(&set[h], 0ull, (unsigned long long)key);
+            if (c == 0) {
+              atomicAdd(&used, 1u);
+              break;
+            }
+            if (c == key) break;
+          }
+          h = (h + 1) & (K4SET - 1);
+        }
+        if (z == 128) full = true;
+      }
     }
   }
   if (full) atomicOr(&counters[C_FLAGS], F_TRIPLE_OVERFLOW);
@@ -534,27 +580,34 @@ __global__ void __launch_bounds__(1024) k4_dedup(const uint32_t *__restrict__ kd
 uint32_t k4_tiles(uint32_t n) { return (n + K4T - 1) / K4T; }
 uint32_t k4_pmax() { return K4PMAX; }
 uint32_t k4_set_cap() { return K4SET * 3 / 4; }
-uint64_t k4_kreg_words(uint32_t n) { return (uint64_t)k4_tiles(n) * K4KCAP; }
-uint64_t k4_rreg_words(uint32_t n) { return (uint64_t)k4_tiles(n) * 2 * K4RCAP; }
 
-void launch_k4_walk(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
-                    const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
-                    uint64_t index_base, uint32_t P, uint32_t *kdir, unsigned long long *kreg, uint32_t *rdir,
-                    unsigned long long *rreg, unsigned long long *rowpos, unsigned int *counters,
-                    uint32_t *tile_stats, unsigned long long *stats64) {
+void launch_k4_count(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+                     const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
+                     uint64_t index_base, uint32_t P, uint32_t *kdir, uint32_t *rdir, unsigned long long *rowpos,
+                     unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64) {
   uint32_t nt = k4_tiles(n);
   if (!nt) return;
-  hipLaunchKernelGGL(k4_walk, dim3(nt), dim3(K4TT), 0, s, kind, shape, ts, cparent, n, dep_ep, n_shapes, n_ep,
-                     index_base, P, kdir, kreg, rdir, rreg, rowpos, counters, tile_stats);
+  hipLaunchKernelGGL((k4_walk<false>), dim3(nt), dim3(K4TT), 0, s, kind, shape, ts, cparent, n, dep_ep, n_shapes, n_ep,
+                     index_base, P, kdir, rdir, nullptr, nullptr, nullptr, nullptr, rowpos, counters, tile_stats);
   hipLaunchKernelGGL(k_tile_sum, dim3(1), dim3(1024), 0, s, tile_stats, nt, 4u, 3u, stats64 + S_ROWS, 2u);
 }
 
-void launch_k4_dedup(hipStream_t s, const uint32_t *kdir, const unsigned long long *kreg, const uint32_t *rdir,
-                     const unsigned long long *rreg, uint32_t n, uint32_t P, unsigned long long *ep_ts,
-                     unsigned long long *ep_first, unsigned long long *out, unsigned long long *stats64,
-                     unsigned int *counters) {
+void launch_k4_emit(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+                    const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
+                    uint64_t index_base, uint32_t P, const uint32_t *koff, unsigned long long *kpool,
+                    const uint32_t *roff, unsigned long long *rpool, unsigned int *counters) {
+  uint32_t nt = k4_tiles(n);
+  if (!nt) return;
+  hipLaunchKernelGGL((k4_walk<true>), dim3(nt), dim3(K4TT), 0, s, kind, shape, ts, cparent, n, dep_ep, n_shapes, n_ep,
+                     index_base, P, nullptr, nullptr, koff, roff, kpool, rpool, nullptr, counters, nullptr);
+}
+
+void launch_k4_dedup(hipStream_t s, const unsigned long long *kpool, const uint32_t *koff,
+                     const unsigned long long *rpool, const uint32_t *roff, uint32_t n, uint32_t P,
+                     unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *out,
+                     unsigned long long *stats64, unsigned int *counters) {
   if (!P || !n) return;
-  hipLaunchKernelGGL(k4_dedup, dim3(P), dim3(1024), 0, s, kdir, kreg, rdir, rreg, k4_tiles(n), ep_ts, ep_first, out,
+  hipLaunchKernelGGL(k4_dedup, dim3(P), dim3(1024), 0, s, kpool, koff, rpool, roff, k4_tiles(n), ep_ts, ep_first, out,
                      stats64, counters);
 }
 

@@ -98,12 +98,31 @@ class Engine:
         self.index_base = 0
         self.n_dep_ep = 0
         self.n_status = 1
-        self._keep = None
+        self._pinned = {}  # name -> (ptr, bytes): reused page-locked result buffers
 
     def close(self):
         if getattr(self, "ctx", None):
             self._lib.kmz_destroy(self.ctx)
             self.ctx = None
+        for ptr_, _ in getattr(self, "_pinned", {}).values():
+            self._lib.kmz_host_free(ptr_)
+        self._pinned = {}
+
+    def _pinned_array(self, name: str, count: int, dtype) -> np.ndarray:
+        """numpy view of a reused page-locked buffer (D2H at full PCIe rate)."""
+        dtype = np.dtype(dtype)
+        nbytes = max(8, count * dtype.itemsize)
+        cur = self._pinned.get(name)
+        if cur is None or cur[1] < nbytes:
+            if cur is not None:
+                self._lib.kmz_host_free(cur[0])
+            p = self._lib.kmz_host_alloc(max(nbytes, 2 * (cur[1] if cur else 0)))
+            if not p:
+                raise MemoryError("kmz_host_alloc failed")
+            cur = (p, max(nbytes, 2 * (cur[1] if cur else 0)))
+            self._pinned[name] = cur
+        buf = (C.c_char * cur[1]).from_address(cur[0])
+        return np.frombuffer(buf, dtype=dtype, count=count)
 
     def __del__(self):
         try:
@@ -150,22 +169,25 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_get_info(self.ctx, C.byref(i)))
         return {f: getattr(i, f) for f, _ in L.Info._fields_ if f != "pad"}
 
-    def groups(self) -> np.ndarray:
+    def groups(self, copy: bool = True) -> np.ndarray:
+        """Finalised groups; copy=False returns a view of a reused pinned buffer."""
         G = self.info()["n_groups"]
-        out = np.zeros(G, dtype=L.GROUP_DTYPE)
+        out = self._pinned_array("groups", G, L.GROUP_DTYPE)
         L.check(self.ctx, self._lib.kmz_get_groups(self.ctx, L.ptr(out), G))
-        return out
+        return out.copy() if copy else out
 
     def endpoints(self) -> np.ndarray:
         out = np.zeros(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE)
         L.check(self.ctx, self._lib.kmz_get_endpoints(self.ctx, L.ptr(out), self.n_dep_ep))
         return out
 
-    def triples(self, sort: bool = True) -> np.ndarray:
+    def triples(self, sort: bool = True, copy: bool = True) -> np.ndarray:
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, None, 0, C.byref(n)))
-        out = np.zeros(n.value, dtype=np.uint64)
+        out = self._pinned_array("triples", n.value, np.uint64)
         L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, L.ptr(out), n.value, C.byref(n)))
+        if copy or sort:
+            out = out.copy()
         if sort:
             out.sort()
         return out
