@@ -130,7 +130,8 @@ typedef struct kmz_info {
   uint64_t max_depth;
   uint64_t n_groups;    /* group slots = n_ep * n_status                    */
   uint32_t flags;       /* internal error bits                             */
-  uint32_t pad;
+  uint32_t path;        /* last dependency run: bit 0 window join (else global span table),
+                           bit 1 LDS-tile walk (else global edge set)      */
 } kmz_info;
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -197,7 +198,9 @@ void kmz_host_free(void *p);
 #define KMZ_K_STATS 4   /* K3 segmented reduction     */
 #define KMZ_K_WALK 5    /* K4 ancestor traversal      */
 #define KMZ_K_FINAL 6   /* finalise + compaction      */
-#define KMZ_K_COUNT 7
+#define KMZ_K_JOIN 7    /* K1' window parent join + contraction */
+#define KMZ_K_CERT 8    /* K1' exact global span-id uniqueness check */
+#define KMZ_K_COUNT 9
 int kmz_set_profiling(kmz_ctx *ctx, int on);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);

@@ -32,7 +32,7 @@ ERRORS = {
     -8: "KMZ_E_RCCL",
 }
 
-KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final"]
+KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final", "join", "cert"]
 SYNTH_BOOKINFO, SYNTH_MESH = 2, 3
 PART_GROUPS, PART_ENDPOINTS, PART_TRIPLES = 0, 1, 2
 
@@ -85,7 +85,7 @@ class Info(C.Structure):
         ("max_depth", C.c_uint64),
         ("n_groups", C.c_uint64),
         ("flags", C.c_uint32),
-        ("pad", C.c_uint32),
+        ("path", C.c_uint32),
     ]
 
 

@@ -53,8 +53,9 @@ struct kmz_ctx {
   DevBuf table, dups, dkey, dval, cparent, rowpos, grp, grp_final, epp, trip, trip_out, counters, stats64, scratch;
   DevBuf synth_cnt, synth_off, dur_table;
   DevBuf k3pool, k3dir, k3part, kdir, koff, kpool, scan_tmp, rdir, roff, rpool, tile_tmp;
+  DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
   uint32_t edge_R = 0;     // descendant endpoints per edge partition (K4T), 0 = auto
-  int path = 0;            // last dependency path: 1 = global table + walk, 2 = LDS-window tiles
+  int path = 0;            // kmz_info.path of the last dependency run
   bool tiles_off = false;  // a descendant endpoint overflowed the LDS edge set: global set for this batch
   uint64_t cap = 0, tcap = 1ull << 16;
   uint32_t dcap = 1024;
@@ -240,7 +241,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->stats64,   &c->scratch,
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->kdir,   &c->koff,      &c->kpool,    &c->scan_tmp, &c->rdir, &c->roff, &c->rpool,
-                    &c->tile_tmp};
+                    &c->tile_tmp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey, &c->mval};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->own_stream) hipStreamDestroy(c->stream);
@@ -396,28 +397,68 @@ static int run_walk_tiles(kmz_ctx *c, bool links) {
   }
 }
 
-static int run_deps(kmz_ctx *c, bool links) {
+// K1': window join + uniqueness certificate.  *ok = false when the batch
+// needs the global table (a repeated span id, or a batch too large for the
+// certificate's two partition levels).
+static int run_join(kmz_ctx *c, bool *ok) {
   const uint32_t n = (uint32_t)c->n;
-  c->cap = c->n * 5 / 3 + 64;  // load factor 0.6
-  // unique edge keys are far fewer than spans; start at ~n/32 (grown on overflow)
-  while (c->tcap < (1ull << 26) && c->tcap * 32 < c->n) c->tcap *= 2;
-  if (ensure(c, c->table, c->cap * 8) || ensure(c, c->dups, (size_t)(n + 1) * sizeof(DupEntry)) ||
-      ensure(c, c->dkey, (size_t)c->dcap * 4) || ensure(c, c->dval, (size_t)c->dcap * 4) ||
-      ensure(c, c->cparent, (size_t)(n + 1) * 4) || ensure(c, c->trip, c->tcap * 8) ||
-      ensure(c, c->trip_out, c->tcap * 8) || ensure(c, c->epp, (size_t)(c->n_dep + 1) * 16) ||
-      (links && ensure(c, c->rowpos, (size_t)(n + 1) * 8)))
+  *ok = false;
+  CertPlan pl;
+  if (n == 0 || !cert_plan(n, &pl) || (c->ablate & 32)) return KMZ_OK;
+  const size_t nsub = (size_t)cert_bins() << pl.B2;
+  if (ensure(c, c->dp, (size_t)(n + 1) * 4) || ensure(c, c->cpool1, cert_pool1_words(n) * 8) ||
+      ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) ||
+      ensure(c, c->cdir, cert_dir_entries(n) * 2))
     return KMZ_E_HIP;
   unsigned int *cnt = P<unsigned int>(c->counters);
-  unsigned long long *st = P<unsigned long long>(c->stats64);
-  unsigned long long *epp = P<unsigned long long>(c->epp);
+  unsigned int *cur2 = P<unsigned int>(c->ccur);
+  HIPCHK(c, hipMemsetAsync(cur2, 0, nsub * 4, c->stream));
+  {
+    Timed t(c, KMZ_K_JOIN);
+    launch_join(c->stream, c->sid, c->pid, c->kind, n, P<uint32_t>(c->cparent), P<uint32_t>(c->dp),
+                P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, c->ablate);
+  }
+  {
+    Timed t(c, KMZ_K_CERT);
+    launch_cert(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
+                P<unsigned long long>(c->cpool2), cur2, cnt);
+  }
+  unsigned int h[C_COUNT];
+  HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (h[C_CERT]) {
+    HIPCHK(c, hipMemsetAsync(cnt + C_MISS, 0, 3 * 4, c->stream));
+    return KMZ_OK;
+  }
+  if (h[C_MISS] || h[C_PEND]) {
+    Timed t(c, KMZ_K_RESOLVE);
+    if (h[C_MISS]) {
+      uint32_t mcap = (uint32_t)std::min<uint64_t>(2ull * h[C_MISS] + 64, 0xFFFFFFF0ull);
+      if (ensure(c, c->mkey, (size_t)mcap * 8) || ensure(c, c->mval, (size_t)mcap * 4)) return KMZ_E_HIP;
+      HIPCHK(c, hipMemsetAsync(c->mkey.p, 0, (size_t)mcap * 8, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->mval.p, 0xFF, (size_t)mcap * 4, c->stream));
+      launch_miss(c->stream, c->sid, c->pid, P<uint32_t>(c->dp), n, P<unsigned long long>(c->mkey),
+                  P<uint32_t>(c->mval), mcap);
+    }
+    if (h[C_PEND]) launch_pend(c->stream, c->kind, P<uint32_t>(c->dp), n, P<uint32_t>(c->cparent));
+  }
+  *ok = true;
+  return KMZ_OK;
+}
+
+// K1 (global span-id table) + K2: any batch, including repeated span ids
+static int run_table(kmz_ctx *c) {
+  const uint32_t n = (uint32_t)c->n;
+  c->cap = c->n * 5 / 3 + 64;  // load factor 0.6
+  if (ensure(c, c->table, c->cap * 8) || ensure(c, c->dups, (size_t)(n + 1) * sizeof(DupEntry)) ||
+      ensure(c, c->dkey, (size_t)c->dcap * 4) || ensure(c, c->dval, (size_t)c->dcap * 4))
+    return KMZ_E_HIP;
+  unsigned int *cnt = P<unsigned int>(c->counters);
   {
     Timed t(c, KMZ_K_MEMSET);
     HIPCHK(c, hipMemsetAsync(c->table.p, 0, c->cap * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(c->dkey.p, 0, (size_t)c->dcap * 4, c->stream));
     HIPCHK(c, hipMemsetAsync(c->dval.p, 0xFF, (size_t)c->dcap * 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
   }
   {
     Timed t(c, KMZ_K_BUILD);
@@ -433,12 +474,39 @@ static int run_deps(kmz_ctx *c, bool links) {
     launch_resolve(c->stream, c->sid, c->pid, c->kind, n, P<unsigned long long>(c->table), c->cap,
                    P<uint32_t>(c->cparent), cnt);
   }
-  unsigned int hc[C_COUNT];
-  HIPCHK(c, hipMemcpyAsync(hc, c->counters.p, sizeof(hc), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (hc[C_DUPS] == 0 && !(c->ablate & 16) && !c->tiles_off) {
-    c->path = 2;
-    int r = run_walk_tiles(c, links);
+  return KMZ_OK;
+}
+
+static int run_deps(kmz_ctx *c, bool links) {
+  const uint32_t n = (uint32_t)c->n;
+  // unique edge keys are far fewer than spans; start at ~n/32 (grown on overflow)
+  while (c->tcap < (1ull << 26) && c->tcap * 32 < c->n) c->tcap *= 2;
+  if (ensure(c, c->cparent, (size_t)(n + 1) * 4) || ensure(c, c->epp, (size_t)(c->n_dep + 1) * 16) ||
+      (links && ensure(c, c->rowpos, (size_t)(n + 1) * 8)))
+    return KMZ_E_HIP;
+  unsigned int *cnt = P<unsigned int>(c->counters);
+  unsigned long long *st = P<unsigned long long>(c->stats64);
+  unsigned long long *epp = P<unsigned long long>(c->epp);
+  {
+    Timed t(c, KMZ_K_MEMSET);
+    HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
+  }
+  bool joined = false;
+  int r = run_join(c, &joined);
+  if (r) return r;
+  uint32_t dups = 0;
+  if (!joined) {
+    c->cap = 0;
+    if ((r = run_table(c))) return r;
+    unsigned int hc[C_COUNT];
+    HIPCHK(c, hipMemcpyAsync(hc, c->counters.p, sizeof(hc), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dups = hc[C_DUPS];
+  }
+  if (dups == 0 && !(c->ablate & 16) && !c->tiles_off) {
+    c->path = joined ? 3 : 2;  // bit 0 window join, bit 1 tile walk
+    r = run_walk_tiles(c, links);
     if (r != -100) return r;
     c->tiles_off = true;
     // fall through to the global-set walk: reset what the tile path touched
@@ -448,8 +516,11 @@ static int run_deps(kmz_ctx *c, bool links) {
     HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
     HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
   }
-  c->path = 1;
+  c->path = joined ? 1 : 0;
+  if (ensure(c, c->trip, c->tcap * 8) || ensure(c, c->trip_out, c->tcap * 8)) return KMZ_E_HIP;
+  HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
   {
+    // the table is read only for repeated ids (dups > 0), which implies run_table
     Timed t(c, KMZ_K_WALK);
     launch_walk(c->stream, c->sid, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
                 c->n_shapes, c->n_dep, c->index_base, P<unsigned long long>(c->table), c->cap,
@@ -556,6 +627,7 @@ int kmz_get_info(kmz_ctx *c, kmz_info *out) {
   out->max_depth = s[S_MAXD];
   out->n_groups = c->G;
   out->flags = h[C_FLAGS];
+  out->path = (uint32_t)c->path;
   return KMZ_OK;
 }
 

@@ -1,0 +1,604 @@
+// kmz_join.hip -- K1': the span-id parent join without a global hash table.
+//
+// The reference builds one Map over every span of the batch (Traces.ts:117-123)
+// and then resolves each parentId through it, skipping CLIENT spans
+// (Traces.ts:128-137).  A global HBM hash table makes that two random accesses
+// per span into a table far larger than the MALL; on MI355X that is bound by
+// random-line throughput, not bandwidth.  Parents are, however, almost always
+// a few rows away (Zipkin returns a trace's spans together), so:
+//
+//   k_join_window   tile of JT spans + JH halo on each side in LDS: an LDS
+//                   hash of the window's span ids, each span's parent found
+//                   in the window (dp), CLIENT contraction inside the window
+//                   (cparent).  Chains that leave the window are PEND, parent
+//                   ids not in the window MISS.  The same kernel scatters the
+//                   tile's hashed ids into 64 bins (pass 1 of the certificate).
+//   k_cert_split    pass 2: each bin chunk is split into 2^B2 sub-bins.
+//   k_cert_check    pass 3: exact duplicate check of each sub-bin in LDS.
+//
+// A window hit is the Map's answer only if the id occurs once in the whole
+// batch; the certificate proves that (mix64 is a bijection, so equal hashes
+// are equal ids).  If any id repeats, the host runs the global table path
+// (kmz_kernels.hip: K1 build/fixup, K2 resolve), which implements the Map's
+// last-value/first-position rule.  MISS parents are looked up with a
+// semi-join of the missing ids against all span ids (k_miss_*), and PEND
+// chains are finished over the global dp array (k_pend).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kmz_kernels.h"
+
+namespace kmz {
+
+constexpr uint32_t JT = 2048, JH = 512, JW = JT + 2 * JH, JTT = 1024;
+static_assert(JW < 4096, "local index + 1 must fit an entry's 12 bits");
+constexpr uint16_t L_NONE = 0xFFFF, L_MISS = 0xFFFE;
+constexpr uint32_t CERT_B1 = 6, CERT_BINS = 1u << CERT_B1;
+constexpr uint32_t CERT_CHUNK = 8192;  // records per pass-2 workgroup (LDS staging)
+constexpr uint32_t CERT_TPC = 192;     // tiles per pass-2 workgroup: ~6144 records of one bin
+constexpr uint32_t CERT_SET = 8192;    // pass-3 LDS set (u64), sub-bins <= 6144 records
+
+
+// exclusive scan of LDS u32 array a[0..m) in place, any m <= 64 * blockDim.x
+__host__ __device__ uint32_t join_tiles(uint32_t n) { return (n + JT - 1) / JT; }
+
+__device__ void block_scan_lds(uint32_t *a, uint32_t m, uint32_t *wsum) {
+  const uint32_t per = (m + blockDim.x - 1) / blockDim.x;
+  const uint32_t b = threadIdx.x * per, e = min(m, b + per);
+  uint32_t s = 0;
+  for (uint32_t k = b; k < e; ++k) s += a[k];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = s;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
+      uint32_t t = wsum[k];
+      wsum[k] = acc;
+      acc += t;
+    }
+  }
+  __syncthreads();
+  uint32_t run = wsum[w] + x - s;
+  for (uint32_t k = b; k < e; ++k) {
+    uint32_t t = a[k];
+    a[k] = run;
+    run += t;
+  }
+  __syncthreads();
+}
+
+// LDS hash of a window: two-choice buckets of 8 u16 entries (one 16-byte LDS
+// read each), entry = fingerprint (4 bits of mix64(id)) << 12 | local index + 1.
+// A lookup reads its two buckets and compares 16 fingerprints; only a
+// fingerprint hit reads the 64-bit id.  Entries that find both buckets full go
+// to a small stash that lookups scan (broadcast reads) when it is not empty.
+// No probe loops: constant work per span, no wave waiting on its unluckiest lane.
+constexpr uint32_t JB = 2048;     // buckets (16384 entries, load <= 0.19)
+constexpr uint32_t JSTASH = 64;
+__device__ __forceinline__ uint32_t jb1(uint64_t h) { return (uint32_t)h & (JB - 1); }
+__device__ __forceinline__ uint32_t jb2(uint64_t h) { return (uint32_t)(h >> 11) & (JB - 1); }
+__device__ __forceinline__ uint32_t jfp(uint64_t h) { return (uint32_t)(h >> 22) & 0xF; }
+
+// lanes of this wave whose `v` (6 bits) equals mine, among `valid` lanes
+__device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
+  uint64_t m = valid;
+#pragma unroll
+  for (int bit = 0; bit < 6; ++bit) {
+    const uint64_t b = __ballot((v >> bit) & 1);
+    m &= ((v >> bit) & 1) ? b : ~b;
+  }
+  return m;
+}
+
+__global__ void __launch_bounds__(JTT) k_join_window(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
+                                                     const uint8_t *__restrict__ kind, uint32_t n,
+                                                     uint32_t *__restrict__ cparent, uint32_t *__restrict__ dp,
+                                                     unsigned long long *__restrict__ pool1,
+                                                     uint16_t *__restrict__ jdir,
+                                                     unsigned int *__restrict__ counters, uint32_t ablate) {
+  constexpr uint32_t NW = JTT / 64;
+  __shared__ uint64_t lsid[JW];
+  __shared__ uint4 lbkt[JB];  // later: staging of the tile's hashed ids
+  __shared__ uint32_t lcnt[JB];
+  __shared__ uint16_t ldp[JW];
+  __shared__ uint8_t lkind[JW];
+  __shared__ uint32_t wcnt[CERT_BINS * NW], wsum[NW];
+  __shared__ uint16_t stash[JSTASH];
+  __shared__ uint32_t nstash;
+  constexpr int PW = JW / JTT, PT = JT / JTT;
+  const uint32_t t0 = blockIdx.x * JT, t1 = min(n, t0 + JT);
+  const uint32_t w0 = t0 > JH ? t0 - JH : 0, w1 = min(n, t1 + JH);
+  for (uint32_t k = threadIdx.x; k < JB; k += JTT) {
+    lbkt[k] = make_uint4(0, 0, 0, 0);
+    lcnt[k] = 0;
+  }
+  if (threadIdx.x == 0) nstash = 0;
+  // one round of window loads (ids, kinds, parent ids), all in flight together
+  uint64_t s[PW], p[PW];
+  uint8_t k[PW];
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    const uint32_t j = w0 + q * JTT + threadIdx.x;
+    const bool ok = j < w1;
+    s[q] = ok ? sid[j] : 0;
+    p[q] = ok ? pid[j] : 0;
+    k[q] = ok ? kind[j] : 0;
+  }
+  uint64_t hs[PW];
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    const uint32_t jl = q * JTT + threadIdx.x;
+    hs[q] = mix64(s[q]);
+    if (w0 + jl < w1) {
+      lsid[jl] = s[q];
+      lkind[jl] = k[q];
+    }
+  }
+  __syncthreads();
+  bool ovf = false;
+  if (!(ablate & 256)) {  // insert: the emptier of the two buckets, else the other, else the stash
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      const uint32_t jl = q * JTT + threadIdx.x;
+      if (w0 + jl >= w1 || s[q] == 0) continue;
+      const uint32_t b1 = jb1(hs[q]), b2 = jb2(hs[q]);
+      const uint16_t e = (uint16_t)((jfp(hs[q]) << 12) | (jl + 1));
+      uint32_t b = lcnt[b1] <= lcnt[b2] ? b1 : b2;
+      uint32_t slot = atomicAdd(&lcnt[b], 1u);
+      if (slot >= 8) {
+        b = b ^ b1 ^ b2;
+        slot = atomicAdd(&lcnt[b], 1u);
+      }
+      if (slot < 8) {
+        reinterpret_cast<uint16_t *>(&lbkt[b])[slot] = e;
+      } else {
+        const uint32_t t = atomicAdd(&nstash, 1u);
+        if (t < JSTASH)
+          stash[t] = e;
+        else
+          ovf = true;  // this tile cannot answer: the table path runs
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t ns = min(nstash, JSTASH);
+  // window parents: tile spans, and CLIENT spans of the halo (chains pass through them)
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    const uint32_t jl = q * JTT + threadIdx.x, j = w0 + jl;
+    if (j >= w1) continue;
+    uint32_t r = L_NONE;
+    if (p[q] != 0 && ((j >= t0 && j < t1) || k[q] == KIND_CLIENT) && !(ablate & 512)) {
+      r = L_MISS;
+      const uint64_t h = mix64(p[q]);
+      const uint32_t f = jfp(h);
+      const uint4 x = lbkt[jb1(h)], y = lbkt[jb2(h)];
+      const uint32_t c[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const uint32_t en = (c[t >> 1] >> (16 * (t & 1))) & 0xFFFF;
+        if (en && (en >> 12) == f && lsid[(en & 4095) - 1] == p[q]) r = (en & 4095) - 1;
+      }
+      for (uint32_t t = 0; t < ns; ++t) {
+        const uint32_t en = stash[t];
+        if ((en >> 12) == f && lsid[(en & 4095) - 1] == p[q]) r = (en & 4095) - 1;
+      }
+    }
+    ldp[jl] = (uint16_t)r;
+  }
+  if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
+  __syncthreads();
+  // tile: CLIENT contraction inside the window (Traces.ts:131-137), lockstep
+  uint32_t miss = 0, pend = 0, zero = 0;
+  uint64_t hv[PT];
+  {
+    uint32_t j[PT], cp[PT], hops[PT], d0[PT];
+    bool act[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const uint32_t i = t0 + q * JTT + threadIdx.x, il = i - w0;
+      const bool ok = i < t1;
+      d0[q] = ok ? ldp[il] : L_NONE;
+      act[q] = ok && lkind[il] != KIND_CLIENT;
+      j[q] = d0[q];
+      cp[q] = NONE;
+      hops[q] = 0;
+    }
+    for (;;) {
+      bool any = false;
+      uint8_t kj[PT];
+#pragma unroll
+      for (int q = 0; q < PT; ++q) kj[q] = (act[q] && j[q] < JW) ? lkind[j[q]] : 0;
+#pragma unroll
+      for (int q = 0; q < PT; ++q) {
+        if (!act[q]) continue;
+        if (j[q] >= JW) {  // markers (a compare, not a switch: see Window::next in kmz_part.hip)
+          cp[q] = j[q] == L_NONE ? NONE : PEND;
+          act[q] = false;
+        } else if (kj[q] != KIND_CLIENT) {
+          cp[q] = w0 + j[q];
+          act[q] = false;
+        } else if (++hops[q] > MAX_DEPTH) {
+          cp[q] = CYC;
+          act[q] = false;
+        } else {
+          j[q] = ldp[j[q]];
+          any = true;
+        }
+      }
+      if (!any) break;
+    }
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const uint32_t i = t0 + q * JTT + threadIdx.x;
+      hv[q] = 0;
+      if (i >= t1) continue;
+      cparent[i] = cp[q];
+      dp[i] = d0[q] == L_NONE ? NONE : (d0[q] == L_MISS ? MISSV : w0 + d0[q]);
+      miss += d0[q] == L_MISS;
+      pend += cp[q] == PEND;
+      const uint64_t key = lsid[i - w0];
+      zero += key == 0;
+      hv[q] = mix64(key);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    miss += __shfl_xor(miss, o, 64);
+    pend += __shfl_xor(pend, o, 64);
+    zero += __shfl_xor(zero, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (miss) atomicAdd(&counters[C_MISS], miss);
+    if (pend) atomicAdd(&counters[C_PEND], pend);
+    if (zero) atomicOr(&counters[C_FLAGS], F_ZERO_ID);
+  }
+  if (ablate & 64) return;  // diagnostic: no certificate pass 1
+  // certificate pass 1: the tile's hashed ids into 64 bins.  Ranks come from
+  // wave ballots and per-wave counters (no LDS atomics on 64 hot words).
+  for (uint32_t e = threadIdx.x; e < CERT_BINS * NW; e += JTT) wcnt[e] = 0;
+  __syncthreads();  // lbkt free from here on
+  uint64_t *stg = reinterpret_cast<uint64_t *>(lbkt);
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t rk[PT];
+#pragma unroll
+  for (int q = 0; q < PT; ++q) {
+    const uint32_t i = t0 + q * JTT + threadIdx.x;
+    const bool ok = i < t1;
+    const uint32_t bin = (uint32_t)(hv[q] >> (64 - CERT_B1));
+    const uint64_t peers = match6(bin, __ballot(ok));
+    uint32_t prior = 0;
+    if (ok) prior = wcnt[bin * NW + w];
+    rk[q] = prior + __popcll(peers & lt);
+    if (ok && (peers & lt) == 0) wcnt[bin * NW + w] = prior + __popcll(peers);
+  }
+  __syncthreads();
+  block_scan_lds(wcnt, CERT_BINS * NW, wsum);  // bin-major, wave-minor offsets
+  // tile-major output, bins in order: no global atomics; the bin offsets go
+  // to the tile's directory row for pass 2
+  if (threadIdx.x < CERT_BINS) jdir[(uint64_t)blockIdx.x * CERT_BINS + threadIdx.x] = (uint16_t)wcnt[threadIdx.x * NW];
+#pragma unroll
+  for (int q = 0; q < PT; ++q) {
+    const uint32_t i = t0 + q * JTT + threadIdx.x;
+    if (i < t1) stg[wcnt[(uint32_t)(hv[q] >> (64 - CERT_B1)) * NW + w] + rk[q]] = hv[q];
+  }
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) pool1[(uint64_t)t0 + e] = stg[e];
+}
+
+// pass 2: for one bin, the runs of CERT_TPC tiles -> 2^B2 sub-bins (dynamic
+// LDS: CERT_CHUNK u64 staging + 2 * 2^B2 u32)
+__global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *__restrict__ pool1,
+                                                     const uint16_t *__restrict__ jdir, uint32_t n, uint32_t chunks,
+                                                     uint32_t B2, unsigned long long *__restrict__ pool2,
+                                                     uint32_t cap2, unsigned int *__restrict__ cur2,
+                                                     unsigned int *__restrict__ counters) {
+  extern __shared__ uint64_t dyn[];
+  __shared__ uint32_t wsum[16], tcnt[CERT_TPC], toff[CERT_TPC], ttot;
+  uint64_t *stg = dyn;
+  const uint32_t M = 1u << B2;
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn + CERT_CHUNK), *base = cnt + M;
+  const uint32_t b = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  const uint32_t ntiles = join_tiles(n), T0 = ch * CERT_TPC;
+  if (T0 >= ntiles) return;
+  const uint32_t nt = min(CERT_TPC, ntiles - T0);
+  for (uint32_t k = threadIdx.x; k < M; k += blockDim.x) cnt[k] = 0;
+  if (threadIdx.x < CERT_TPC) {
+    uint32_t c = 0, o = 0;
+    if (threadIdx.x < nt) {
+      const uint32_t t = T0 + threadIdx.x;
+      const uint32_t tsize = min(JT, n - t * JT);
+      o = jdir[(uint64_t)t * CERT_BINS + b];
+      const uint32_t e = b + 1 < CERT_BINS ? jdir[(uint64_t)t * CERT_BINS + b + 1] : tsize;
+      c = e - o;
+    }
+    tcnt[threadIdx.x] = c;
+    toff[threadIdx.x] = o;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t t = 0; t < CERT_TPC; ++t) {
+      const uint32_t c = tcnt[t];
+      tcnt[t] = acc;  // tcnt := position of the tile's run in the chunk
+      acc += c;
+      if (t + 1 == CERT_TPC) ttot = acc;
+    }
+  }
+  __syncthreads();
+  const uint32_t cn = ttot;
+  if (cn > CERT_CHUNK) {  // cannot happen for hashed ids short of ~20 sigma
+    if (threadIdx.x == 0) atomicOr(&counters[C_CERT], CERT_OVF);
+    return;
+  }
+  {  // gather: one wave per tile run
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (uint32_t t = w; t < nt; t += blockDim.x / 64) {
+      const uint32_t beg = tcnt[t], end = t + 1 < CERT_TPC ? tcnt[t + 1] : cn;
+      const unsigned long long *src = pool1 + (uint64_t)(T0 + t) * JT + toff[t];
+      for (uint32_t l = lane; l < end - beg; l += 64) stg[beg + l] = src[l];
+    }
+  }
+  __syncthreads();
+  constexpr int PQ = CERT_CHUNK / 1024;
+  uint64_t h[PQ];
+  uint32_t rk[PQ];
+#pragma unroll
+  for (int q = 0; q < PQ; ++q) {
+    const uint32_t e = q * 1024 + threadIdx.x;
+    h[q] = e < cn ? stg[e] : 0;
+  }
+  const uint32_t sh = 64 - CERT_B1 - B2;
+#pragma unroll
+  for (int q = 0; q < PQ; ++q) {
+    const uint32_t e = q * 1024 + threadIdx.x;
+    rk[q] = e < cn ? atomicAdd(&cnt[(uint32_t)(h[q] >> sh) & (M - 1)], 1u) : 0;
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < M; k += blockDim.x) {
+    const uint32_t c = cnt[k];
+    base[k] = c ? atomicAdd(&cur2[(b << B2) | k], c) : 0;
+  }
+  __syncthreads();
+  block_scan_lds(cnt, M, wsum);  // cnt := local offsets
+#pragma unroll
+  for (int q = 0; q < PQ; ++q) {
+    const uint32_t e = q * 1024 + threadIdx.x;
+    if (e < cn) stg[cnt[(uint32_t)(h[q] >> sh) & (M - 1)] + rk[q]] = h[q];
+  }
+  __syncthreads();
+  bool ovf = false;
+  for (uint32_t e = threadIdx.x; e < cn; e += blockDim.x) {
+    const uint64_t x = stg[e];
+    const uint32_t sb = (uint32_t)(x >> sh) & (M - 1);
+    const uint32_t pos = base[sb] + e - cnt[sb];
+    if (pos < cap2)
+      pool2[(uint64_t)((b << B2) | sb) * cap2 + pos] = x;
+    else
+      ovf = true;
+  }
+  if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
+}
+
+// pass 3: exact duplicate check of one sub-bin.  Two-choice buckets of eight
+// 64-bit hashed ids (+ a small stash); after all inserts, every id counts its
+// equals in its two buckets and the stash (an id that occurs twice finds two).
+// No CAS loops.
+constexpr uint32_t CB = CERT_SET / 8, CSTASH = 64;
+__device__ __forceinline__ uint32_t count_eq(const ulonglong2 *b, uint64_t h) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const ulonglong2 v = b[t];
+    c += (v.x == h) + (v.y == h);
+  }
+  return c;
+}
+
+__global__ void __launch_bounds__(1024) k_cert_check(const unsigned long long *__restrict__ pool, uint32_t cap,
+                                                    const unsigned int *__restrict__ cur, uint32_t cur_stride,
+                                                    unsigned int *__restrict__ counters) {
+  __shared__ ulonglong2 set2[CB * 4];  // bucket b = set2[4b .. 4b+3]
+  __shared__ uint32_t cnt[CB];
+  __shared__ uint64_t stash[CSTASH];
+  __shared__ uint32_t nstash;
+  const uint32_t sb = blockIdx.x;
+  const uint32_t m = min(cur[(uint64_t)sb * cur_stride], cap);
+  if (m == 0) return;
+  for (uint32_t k = threadIdx.x; k < CB * 4; k += blockDim.x) set2[k] = make_ulonglong2(0, 0);
+  for (uint32_t k = threadIdx.x; k < CB; k += blockDim.x) cnt[k] = 0;
+  if (threadIdx.x == 0) nstash = 0;
+  __syncthreads();
+  unsigned long long *set = reinterpret_cast<unsigned long long *>(set2);
+  const unsigned long long *src = pool + (uint64_t)sb * cap;
+  bool bad = false;
+  for (uint32_t e0 = 0; e0 < m; e0 += 8 * 1024) {
+    uint64_t h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t e = e0 + q * 1024 + threadIdx.x;
+      h[q] = e < m ? src[e] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (h[q] == 0) continue;  // mix64(0) == 0: span id 0, reported as F_ZERO_ID
+      const uint32_t b1 = (uint32_t)h[q] & (CB - 1), b2 = (uint32_t)(h[q] >> 10) & (CB - 1);
+      uint32_t b = cnt[b1] <= cnt[b2] ? b1 : b2;
+      uint32_t slot = atomicAdd(&cnt[b], 1u);
+      if (slot >= 8) {
+        b = b ^ b1 ^ b2;
+        slot = atomicAdd(&cnt[b], 1u);
+      }
+      if (slot < 8) {
+        set[8 * b + slot] = h[q];
+      } else {
+        const uint32_t t = atomicAdd(&nstash, 1u);
+        if (t < CSTASH)
+          stash[t] = h[q];
+        else
+          bad = true;  // no verdict for this sub-bin
+      }
+    }
+  }
+  if (bad) atomicOr(&counters[C_CERT], CERT_OVF);
+  __syncthreads();
+  const uint32_t ns = min(nstash, CSTASH);
+  bool dup = false;
+  for (uint32_t e0 = 0; e0 < m; e0 += 8 * 1024) {
+    uint64_t h[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t e = e0 + q * 1024 + threadIdx.x;
+      h[q] = e < m ? src[e] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (h[q] == 0) continue;
+      const uint32_t b1 = (uint32_t)h[q] & (CB - 1), b2 = (uint32_t)(h[q] >> 10) & (CB - 1);
+      uint32_t c = count_eq(&set2[4 * b1], h[q]);
+      if (b2 != b1) c += count_eq(&set2[4 * b2], h[q]);
+      for (uint32_t t = 0; t < ns; ++t) c += stash[t] == h[q];
+      dup |= c > 1;
+    }
+  }
+  if (dup) atomicOr(&counters[C_CERT], CERT_DUP);
+}
+
+// ---- MISS parents: semi-join of the missing parent ids against all span ids
+__device__ __forceinline__ uint64_t mslot(uint64_t key, uint32_t mcap) { return slot_of(key ^ 0x7F4A7C159E3779B9ull, mcap); }
+
+__global__ void __launch_bounds__(256) k_miss_insert(const uint64_t *__restrict__ pid, const uint32_t *__restrict__ dp,
+                                                     uint32_t n, unsigned long long *__restrict__ mkey, uint32_t mcap) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (dp[i] != MISSV) continue;
+    const uint64_t key = pid[i];
+    uint32_t pos = (uint32_t)mslot(key, mcap);
+    for (uint32_t z = 0; z < mcap; ++z) {
+      unsigned long long c = atomicCAS(&mkey[pos], 0ull, (unsigned long long)key);
+      if (c == 0 || c == key) break;
+      pos = pos + 1 == mcap ? 0 : pos + 1;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_miss_probe(const uint64_t *__restrict__ sid, uint32_t n,
+                                                    const unsigned long long *__restrict__ mkey,
+                                                    uint32_t *__restrict__ mval, uint32_t mcap) {
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    const uint64_t key = sid[j];
+    if (key == 0) continue;
+    uint32_t pos = (uint32_t)mslot(key, mcap);
+    for (uint32_t z = 0; z < mcap; ++z) {
+      const unsigned long long c = mkey[pos];
+      if (c == 0) break;
+      if (c == key) {
+        mval[pos] = j;  // ids are unique (certificate): one writer per slot
+        break;
+      }
+      pos = pos + 1 == mcap ? 0 : pos + 1;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_miss_fix(const uint64_t *__restrict__ pid, uint32_t *__restrict__ dp,
+                                                  uint32_t n, const unsigned long long *__restrict__ mkey,
+                                                  const uint32_t *__restrict__ mval, uint32_t mcap) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (dp[i] != MISSV) continue;
+    const uint64_t key = pid[i];
+    uint32_t pos = (uint32_t)mslot(key, mcap), r = NONE;
+    for (uint32_t z = 0; z < mcap; ++z) {
+      const unsigned long long c = mkey[pos];
+      if (c == 0) break;
+      if (c == key) {
+        r = mval[pos];
+        break;
+      }
+      pos = pos + 1 == mcap ? 0 : pos + 1;
+    }
+    dp[i] = r;
+  }
+}
+
+// PEND chains over the global dp array
+__global__ void __launch_bounds__(256) k_pend(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ dp,
+                                              uint32_t n, uint32_t *__restrict__ cparent) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (cparent[i] != PEND) continue;
+    uint32_t j = dp[i], hops = 0, cp;
+    for (;;) {
+      if (j >= n) {
+        cp = NONE;
+        break;
+      }
+      if (kind[j] != KIND_CLIENT) {
+        cp = j;
+        break;
+      }
+      if (++hops > MAX_DEPTH) {
+        cp = CYC;
+        break;
+      }
+      j = dp[j];
+    }
+    cparent[i] = cp;
+  }
+}
+
+// ---------------------------------------------------------------------------
+
+bool cert_plan(uint32_t n, CertPlan *pl) {
+  uint32_t B2 = 0;
+  while (B2 < 12 && (uint64_t)n > (3072ull << (CERT_B1 + B2))) ++B2;
+  const double mean2 = (double)n / ((uint64_t)CERT_BINS << B2);
+  pl->B2 = B2;
+  pl->cap2 = (uint32_t)(mean2 * 1.15) + 256;
+  pl->chunks = (join_tiles(n) + CERT_TPC - 1) / CERT_TPC;
+  return pl->cap2 <= CERT_SET * 3 / 4;
+}
+
+uint32_t cert_bins() { return CERT_BINS; }
+uint64_t cert_pool1_words(uint32_t n) { return (uint64_t)join_tiles(n) * JT; }
+uint64_t cert_dir_entries(uint32_t n) { return (uint64_t)join_tiles(n) * CERT_BINS; }
+
+void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
+                 uint32_t *cparent, uint32_t *dp, unsigned long long *pool1, uint16_t *jdir, unsigned int *counters,
+                 uint32_t ablate) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_join_window, dim3(join_tiles(n)), dim3(JTT), 0, s, sid, pid, kind, n, cparent, dp, pool1, jdir,
+                     counters, ablate);
+}
+
+void launch_cert(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir, const CertPlan &pl,
+                 unsigned long long *pool2, unsigned int *cur2, unsigned int *counters) {
+  if (!n) return;
+  const size_t lds = CERT_CHUNK * 8 + (size_t)2 * (1u << pl.B2) * 4;
+  hipLaunchKernelGGL(k_cert_split, dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n, pl.chunks, pl.B2,
+                     pool2, pl.cap2, cur2, counters);
+  hipLaunchKernelGGL(k_cert_check, dim3(CERT_BINS << pl.B2), dim3(1024), 0, s, (const unsigned long long *)pool2,
+                     pl.cap2, (const unsigned int *)cur2, 1u, counters);
+}
+
+void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,
+                 unsigned long long *mkey, uint32_t *mval, uint32_t mcap) {
+  if (!n) return;
+  const uint32_t g = std::min<uint32_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_miss_insert, dim3(g), dim3(256), 0, s, pid, dp, n, mkey, mcap);
+  hipLaunchKernelGGL(k_miss_probe, dim3(g), dim3(256), 0, s, sid, n, mkey, mval, mcap);
+  hipLaunchKernelGGL(k_miss_fix, dim3(g), dim3(256), 0, s, pid, dp, n, mkey, mval, mcap);
+}
+
+void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent) {
+  if (!n) return;
+  const uint32_t g = std::min<uint32_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_pend, dim3(g), dim3(256), 0, s, kind, dp, n, cparent);
+}
+
+}  // namespace kmz

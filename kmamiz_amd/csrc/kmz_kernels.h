@@ -13,7 +13,11 @@ constexpr uint8_t KIND_SERVER = KMZ_KIND_SERVER;
 constexpr uint8_t KIND_CLIENT = KMZ_KIND_CLIENT;
 
 // u32 device counters
-enum { C_FLAGS = 0, C_DUPS = 1, C_TRIPLES = 2, C_COUNT = 4 };
+enum { C_FLAGS = 0, C_DUPS = 1, C_TRIPLES = 2, C_MISS = 3, C_PEND = 4, C_CERT = 5, C_COUNT = 8 };
+// C_CERT bits: the window join's answers cannot be used (global table path)
+constexpr uint32_t CERT_DUP = 1u, CERT_OVF = 2u;
+constexpr uint32_t MISSV = 0xFFFFFFFDu;  // dp: parent id not in the span's window
+constexpr uint32_t PEND = 0xFFFFFFFCu;   // cparent: CLIENT chain leaves the window
 // u64 device statistics
 enum { S_ROWS = 0, S_REL = 1, S_MAXD = 2, S_SERVER = 3, S_TRIP_OUT = 4, S_COUNT = 8 };
 
@@ -69,5 +73,23 @@ void launch_k4_dedup(hipStream_t s, const unsigned long long *kpool, const uint3
                      const unsigned long long *rpool, const uint32_t *roff, uint32_t n, uint32_t P,
                      unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *out,
                      unsigned long long *stats64, unsigned int *counters);
+
+// window parent join + uniqueness certificate (kmz_join.hip)
+struct CertPlan {
+  uint32_t B2, cap2, chunks;
+};
+bool cert_plan(uint32_t n, CertPlan *pl);
+uint32_t cert_bins();
+uint64_t cert_pool1_words(uint32_t n);
+uint64_t cert_dir_entries(uint32_t n);
+__host__ __device__ uint32_t join_tiles(uint32_t n);
+void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
+                 uint32_t *cparent, uint32_t *dp, unsigned long long *pool1, uint16_t *jdir, unsigned int *counters,
+                 uint32_t ablate = 0);
+void launch_cert(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir, const CertPlan &pl,
+                 unsigned long long *pool2, unsigned int *cur2, unsigned int *counters);
+void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,
+                 unsigned long long *mkey, uint32_t *mval, uint32_t mcap);
+void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent);
 
 }  // namespace kmz

@@ -285,10 +285,11 @@ struct Window {
   __device__ __forceinline__ bool in(uint32_t g) const { return g >= w0 && g < w1; }
   __device__ __forceinline__ uint32_t next(uint32_t g) const {
     if (in(g)) {
-      uint16_t c = lcp[g - w0];
+      // no switch here: hipcc (ROCm 7.2) lowers a switch over these u16
+      // markers with a wrong signed range split that sends L_OUT to CYC
+      const uint32_t c = lcp[g - w0];
       if (c < K4W) return w0 + c;
-      if (c == L_NONE) return NONE;
-      if (c == L_CYC) return CYC;
+      if (c != L_OUT) return 0xFFFF0000u | c;  // L_NONE -> NONE, L_CYC -> CYC
     }
     return cparent[g];
   }
@@ -336,6 +337,8 @@ __device__ __forceinline__ void load_window(uint32_t w0, uint32_t w1, const uint
     }
   }
 }
+
+__device__ unsigned long long g_k4dbg[64];
 
 template <bool EMIT>
 __global__ void __launch_bounds__(K4TT) k4_walk(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
@@ -386,6 +389,13 @@ __global__ void __launch_bounds__(K4TT) k4_walk(const uint8_t *__restrict__ kind
         for (uint32_t cur = first; cur != NONE; cur = W.next(cur)) {
           if (D >= MAX_DEPTH || cur == CYC) {
             atomicOr(&counters[C_FLAGS], F_CYCLE);
+            unsigned long long k = atomicAdd(&g_k4dbg[0], 1ull);
+            if (k < 15) {
+              g_k4dbg[1 + 4 * k] = i;
+              g_k4dbg[2 + 4 * k] = first;
+              g_k4dbg[3 + 4 * k] = cur;
+              g_k4dbg[4 + 4 * k] = ((uint64_t)lcp[i - w0] << 32) | cparent[i];
+            }
             bad = true;
             break;
           }
@@ -577,6 +587,11 @@ __global__ void __launch_bounds__(1024) k4_dedup(const unsigned long long *__res
   }
 }
 
+}  // namespace kmz
+extern "C" int kmz__debug_k4(unsigned long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(kmz::g_k4dbg), sizeof(kmz::g_k4dbg)) == hipSuccess ? 0 : -1;
+}
+namespace kmz {
 uint32_t k4_tiles(uint32_t n) { return (n + K4T - 1) / K4T; }
 uint32_t k4_pmax() { return K4PMAX; }
 uint32_t k4_set_cap() { return K4SET * 3 / 4; }

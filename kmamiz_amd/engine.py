@@ -167,7 +167,7 @@ class Engine:
     def info(self) -> dict:
         i = L.Info()
         L.check(self.ctx, self._lib.kmz_get_info(self.ctx, C.byref(i)))
-        return {f: getattr(i, f) for f, _ in L.Info._fields_ if f != "pad"}
+        return {f: getattr(i, f) for f, _ in L.Info._fields_}
 
     def groups(self, copy: bool = True) -> np.ndarray:
         """Finalised groups; copy=False returns a view of a reused pinned buffer."""
@@ -230,8 +230,8 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_set_profiling(self.ctx, 1 if on else 0))
 
     def kernel_times(self, reset: bool = False) -> dict:
-        ms = np.zeros(8, dtype=np.float64)
-        calls = np.zeros(8, dtype=np.uint64)
+        ms = np.zeros(len(L.KERNELS), dtype=np.float64)
+        calls = np.zeros(len(L.KERNELS), dtype=np.uint64)
         L.check(self.ctx, self._lib.kmz_kernel_times(self.ctx, L.ptr(ms), L.ptr(calls), 1 if reset else 0))
         return {k: (float(ms[i]), int(calls[i])) for i, k in enumerate(L.KERNELS)}
 

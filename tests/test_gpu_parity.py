@@ -322,3 +322,76 @@ def test_hot_descendant_falls_back_to_global_edge_set(engine):
     assert len(keys) == 7000
     exp = O.strip_undef(O.Traces(traces).toEndpointDependencies().toJSON())
     assert got.toJSON() == exp
+
+
+# ---------------------------------------------------------------------------
+# K1' window join: far parents, repeated ids far apart, CLIENT chains that
+# leave the window (kmz_join.hip)
+# ---------------------------------------------------------------------------
+def _permuted(batch, perm):
+    from kmamiz_amd.engine import SpanBatch
+
+    return SpanBatch(batch.span_id[perm], batch.parent_id[perm], batch.kind[perm], batch.shape[perm],
+                     batch.status[perm], batch.duration[perm], batch.timestamp[perm], batch.index_base)
+
+
+@pytest.mark.parametrize("frac", [1.0, 0.02])
+def test_far_parents_vs_c_oracle(engine, frac):
+    """Spans moved far from their trace (all of them, or 2%): parents outside
+    the LDS window go through the MISS semi-join and PEND chains."""
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(3, 0, 3000)
+    n = len(batch)
+    rng = np.random.default_rng(7)
+    perm = np.arange(n)
+    sel = np.flatnonzero(rng.random(n) < frac)
+    perm[sel] = perm[rng.permutation(sel)]
+    info = _compare_synth(engine, _permuted(batch, perm), synth.shape_table(3))
+    assert info["path"] & 1  # window join (ids unique)
+
+
+@pytest.mark.parametrize("where", ["far", "near"])
+def test_repeated_id_falls_back_to_span_table(engine, where):
+    """A span id repeated anywhere in the batch voids the window answers: the
+    certificate must catch it and the global Map rule must apply."""
+    from kmamiz_amd import synth
+
+    batch, off = synth.host_batch(3, 0, 3000)
+    n = len(batch)
+    # i and j in different traces (no cycle): far apart, or in one LDS window
+    i, j = (10, n - 10) if where == "far" else (int(off[200]), int(off[201]) + 1)
+    batch.span_id[j] = batch.span_id[i]
+    info = _compare_synth(engine, batch, synth.shape_table(3))
+    assert info["n_dups"] == 1
+    assert not (info["path"] & 1)
+
+
+def test_window_join_matches_span_table(engine):
+    """Same batch through both resolve paths (KMZ_ABLATE bit 32 forces the table)."""
+    import os
+
+    from kmamiz_amd import Engine
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    def run(e):
+        e.load_synthetic(3, synth.SEED, 0, 20000)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS | L.RUN_SPAN_LINKS)
+        cp, rp = e.span_links()
+        return cp, rp, e.triples(), e.endpoints(), e.info()
+
+    a = run(engine)
+    os.environ["KMZ_ABLATE"] = "32"
+    try:
+        e2 = Engine(0)
+    finally:
+        del os.environ["KMZ_ABLATE"]
+    try:
+        b = run(e2)
+    finally:
+        e2.close()
+    assert a[4]["path"] == 3 and b[4]["path"] == 2
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert a[3].tobytes() == b[3].tobytes()
+    assert {k: v for k, v in a[4].items() if k != "path"} == {k: v for k, v in b[4].items() if k != "path"}

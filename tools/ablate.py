@@ -1,6 +1,7 @@
 """Diagnostic: per-kernel times of the mesh pipeline under KMZ_ABLATE knobs
 (bit 1 = skip edge-key dedup, 2 = skip the global edge set, 4 = skip global
-endpoint atomics).  Prints one JSON line per setting."""
+endpoint atomics, 64 = skip certificate pass 1 in the join, 128 = skip its
+global bin atomics).  Prints one JSON line per setting."""
 import json
 import os
 import subprocess
@@ -27,6 +28,6 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
                       **{k: round(v[0] / max(1, v[1]), 3) for k, v in t.items()}}))
 else:
     ntr = sys.argv[1] if len(sys.argv) > 1 else "3650000"
-    for a in ["0", "1", "2", "4", "7"]:
+    for a in sys.argv[2:] or ["0", "1", "2", "4", "7"]:
         env = dict(os.environ, KMZ_ABLATE=a)
         subprocess.run([sys.executable, __file__, "child", ntr], env=env, check=True)
