@@ -22,9 +22,21 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# algorithmic bytes per unit (DESIGN.md "Roofline accounting")
-BYTES_PER_SPAN = {"build": 20, "resolve": 37, "stats": 19}
-BYTES_PER_RELATION = {"walk": 12}
+# Algorithmic bytes per launch of each hot-path kernel (DESIGN.md section 3;
+# SURVEY.md 8d budgets K2 57 B/span, K3 19 B/span, K4 12 B/relation).
+#   join   k_join_window  K2 parent join + CLIENT contraction   57 B/span
+#   stats  k3_produce     K3 (read ep/status/kind/dur/ts)       19 B/span
+#   reduce k3_reduce      K3 second pass: the partitioned records it must
+#                         read (dur 4 + ts 8 + key/index 4)      16 B/SERVER span
+#   walk   k4_chain       K4 traversal                          12 B/relation
+#   cert   k_cert_split   uniqueness certificate: one radix split of the
+#                         8-B hashed span id (read + write)      16 B/span
+#   check  k_cert_check   certificate check: one read of it       8 B/span
+def alg_bytes(kernel, n, n_server, relations):
+    return {"join": 57 * n, "stats": 19 * n, "reduce": 16 * n_server, "walk": 12 * relations,
+            "cert": 16 * n, "check": 8 * n}.get(kernel, 0)
+
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
@@ -163,20 +175,22 @@ def main():
     secs = float(elapsed.item())
     spans_per_s = n_total * args.steps / secs
 
-    # roofline of the dominant kernel (HIP events around every launch)
+    # roofline of the dominant kernel (HIP events around every launch, on the
+    # engine's stream)
     A = info["n_relations"]
     per_kernel = {}
     for k, (ms, calls) in ktimes.items():
         if not calls:
             continue
         avg = ms / calls
-        alg = BYTES_PER_SPAN.get(k, 0) * n_local + BYTES_PER_RELATION.get(k, 0) * A
-        per_kernel[k] = {"avg_ms": round(avg, 4), "alg_bytes": alg,
+        alg = alg_bytes(k, n_local, info["n_server"], A) if calls == args.steps else 0
+        per_kernel[k] = {"ms_per_step": round(ms / args.steps, 4), "calls_per_step": round(calls / args.steps, 2),
+                         "avg_ms": round(avg, 4), "alg_bytes": alg,
                          "gbs": round(alg / (avg * 1e-3) / 1e9, 1) if alg else None}
     dom = max((k for k in per_kernel if per_kernel[k]["alg_bytes"]), key=lambda k: per_kernel[k]["avg_ms"])
     d = per_kernel[dom]
-    kern_ms = sum(v["avg_ms"] for v in per_kernel.values()) / max(1, 1)
-    pipe_bytes = sum(v["alg_bytes"] for v in per_kernel.values())
+    kern_ms = sum(v["ms_per_step"] for v in per_kernel.values())
+    pipe_bytes = sum(v["alg_bytes"] for v in per_kernel.values() if v["alg_bytes"])
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0:
@@ -207,13 +221,16 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": dom,
+                "kernel": {"join": "k_join_window", "stats": "k3_produce" if "reduce" in per_kernel else "k_stats",
+                           "reduce": "k3_reduce",
+                           "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check"}[dom],
                 "achieved": d["gbs"],
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(d["gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": None,
                 "pipeline_gbs": round(pipe_bytes / (kern_ms * 1e-3) / 1e9, 1),
+                "kernel_ms_per_step": round(kern_ms, 4),
                 "kernels": per_kernel,
             },
             "cpu_baseline": cpu,

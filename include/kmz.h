@@ -131,7 +131,7 @@ typedef struct kmz_info {
   uint64_t n_groups;    /* group slots = n_ep * n_status                    */
   uint32_t flags;       /* internal error bits                             */
   uint32_t path;        /* last dependency run: bit 0 window join (else global span table),
-                           bit 1 LDS-tile walk (else global edge set)      */
+                           bit 1 chain-interning walk (else per-relation global walk) */
 } kmz_info;
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -191,16 +191,21 @@ void *kmz_host_alloc(uint64_t bytes);
 void kmz_host_free(void *p);
 
 /* ---- per-kernel timing (HIP events around each launch) ------------------- */
-#define KMZ_K_MEMSET 0
-#define KMZ_K_BUILD 1   /* K1 span-id table build     */
-#define KMZ_K_FIXUP 2   /* K1 duplicate-id fixup      */
-#define KMZ_K_RESOLVE 3 /* K2 parent join + contraction */
-#define KMZ_K_STATS 4   /* K3 segmented reduction     */
-#define KMZ_K_WALK 5    /* K4 ancestor traversal      */
-#define KMZ_K_FINAL 6   /* finalise + compaction      */
-#define KMZ_K_JOIN 7    /* K1' window parent join + contraction */
-#define KMZ_K_CERT 8    /* K1' exact global span-id uniqueness check */
-#define KMZ_K_COUNT 9
+/* One id per kernel of the hot path (small helper launches are folded into the
+ * kernel they serve), so bench.py can price each launch against the roofline. */
+#define KMZ_K_MEMSET 0   /* memsets of the per-run workspace                     */
+#define KMZ_K_BUILD 1    /* K1 span-id table build (repeated ids only)           */
+#define KMZ_K_FIXUP 2    /* K1 duplicate-id fixup (repeated ids only)            */
+#define KMZ_K_RESOLVE 3  /* K2 table resolve / window-join MISS + PEND fix-ups    */
+#define KMZ_K_STATS 4    /* K3 k3_produce (or the one-pass LDS k_stats)           */
+#define KMZ_K_WALK 5     /* K4 k4_chain (or the global k_walk for repeated ids)   */
+#define KMZ_K_FINAL 6    /* finalise, collapse, edge-set compaction               */
+#define KMZ_K_JOIN 7     /* K2 k_join_window: parent join + CLIENT contraction    */
+#define KMZ_K_CERT 8     /* uniqueness certificate pass 2 (k_cert_split)          */
+#define KMZ_K_REDUCE 9   /* K3 k3_reduce + k3_combine                             */
+#define KMZ_K_PEND 10    /* K4 chains whose ancestry leaves the LDS window        */
+#define KMZ_K_CHECK 11   /* uniqueness certificate pass 3 (k_cert_check)          */
+#define KMZ_K_COUNT 12
 int kmz_set_profiling(kmz_ctx *ctx, int on);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);

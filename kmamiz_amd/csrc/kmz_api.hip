@@ -52,12 +52,14 @@ struct kmz_ctx {
   // workspace
   DevBuf table, dups, dkey, dval, cparent, rowpos, grp, grp_final, epp, trip, trip_out, counters, stats64, scratch;
   DevBuf synth_cnt, synth_off, dur_table;
-  DevBuf k3pool, k3dir, k3part, kdir, koff, kpool, scan_tmp, rdir, roff, rpool, tile_tmp;
+  DevBuf k3pool, k3dir, k3part, tile_tmp, sgrp;
   DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
-  uint32_t edge_R = 0;     // descendant endpoints per edge partition (K4T), 0 = auto
-  int path = 0;            // kmz_info.path of the last dependency run
-  bool tiles_off = false;  // a descendant endpoint overflowed the LDS edge set: global set for this batch
-  uint64_t cap = 0, tcap = 1ull << 16;
+  DevBuf ctab, plist;                                 // K4 chain interning
+  int path = 0;             // kmz_info.path of the last dependency run
+  bool sstats = false;      // shape-level K3 partials computed in this run
+  bool chain_ran = false;   // this run's dependency graph came from k4_chain
+  uint64_t cap = 0, tcap = 1ull << 16, ccap = 1ull << 20;
+  uint64_t sig_seed = 0x4B4D5A5349470001ull;  // K4 ancestry-hash seed (changed after a collision)
   uint32_t dcap = 1024;
 
   // last run
@@ -240,8 +242,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->dkey,   &c->dval,      &c->cparent,  &c->rowpos,    &c->grp,       &c->grp_final,
                     &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->stats64,   &c->scratch,
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
-                    &c->kdir,   &c->koff,      &c->kpool,    &c->scan_tmp, &c->rdir, &c->roff, &c->rpool,
-                    &c->tile_tmp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey, &c->mval};
+                    &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
+                    &c->mval, &c->ctab, &c->plist};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->own_stream) hipStreamDestroy(c->stream);
@@ -319,82 +321,8 @@ int kmz_load(kmz_ctx *c, const kmz_spans *s, const kmz_shapes *sh, int where) {
     c->ts = P<int64_t>(c->in_ts);
   }
   c->loaded = true;
-  c->tiles_off = false;
-  c->edge_R = 0;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KMZ_OK;
-}
-
-// K4 on LDS windows + partitioned edge-key dedup (unique span ids only)
-static int scan_u32(kmz_ctx *c, const uint32_t *in, uint32_t *out, size_t n) {
-  size_t tb = 0;
-  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)n, c->stream));
-  if (ensure(c, c->scan_tmp, tb)) return KMZ_E_HIP;
-  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tb, in, out, (int)n, c->stream));
-  return KMZ_OK;
-}
-
-static int run_walk_tiles(kmz_ctx *c, bool links) {
-  const uint32_t n = (uint32_t)c->n;
-  unsigned int *cnt = P<unsigned int>(c->counters);
-  unsigned long long *st = P<unsigned long long>(c->stats64);
-  unsigned long long *epp = P<unsigned long long>(c->epp);
-  if (n == 0 || c->n_dep == 0) return KMZ_OK;
-  // edge partitions, hashed by descendant endpoint: <= 6144 distinct keys each
-  if (!c->edge_R) c->edge_R = std::min<uint32_t>(k4_pmax(), std::max<uint32_t>(1, std::min(c->n_dep, 512u)));
-  for (;;) {
-    const uint32_t Pp = c->edge_R, nt = k4_tiles(n);
-    const size_t nd = (size_t)Pp * nt + 1;
-    if (ensure(c, c->kdir, nd * 4) || ensure(c, c->koff, nd * 4) || ensure(c, c->rdir, nd * 4) ||
-        ensure(c, c->roff, nd * 4) || ensure(c, c->tile_tmp, (size_t)nt * 16))
-      return KMZ_E_HIP;
-    HIPCHK(c, hipMemsetAsync(P<uint32_t>(c->kdir) + nd - 1, 0, 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(P<uint32_t>(c->rdir) + nd - 1, 0, 4, c->stream));
-    {
-      Timed t(c, KMZ_K_WALK);
-      launch_k4_count(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
-                      c->n_shapes, c->n_dep, c->index_base, Pp, P<uint32_t>(c->kdir), P<uint32_t>(c->rdir),
-                      links ? P<unsigned long long>(c->rowpos) : nullptr, cnt, P<uint32_t>(c->tile_tmp), st);
-      int r = scan_u32(c, P<uint32_t>(c->kdir), P<uint32_t>(c->koff), nd);
-      if (!r) r = scan_u32(c, P<uint32_t>(c->rdir), P<uint32_t>(c->roff), nd);
-      if (r) return r;
-    }
-    unsigned int h[C_COUNT];
-    uint32_t tot[2] = {0, 0};
-    HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&tot[0], P<uint32_t>(c->koff) + nd - 1, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&tot[1], P<uint32_t>(c->roff) + nd - 1, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (h[C_FLAGS] & (F_CYCLE | F_RANGE)) return KMZ_OK;  // reported by kmz_run
-    if (ensure(c, c->kpool, ((uint64_t)tot[0] + 1) * 8) || ensure(c, c->rpool, ((uint64_t)tot[1] + 1) * 16) ||
-        ensure(c, c->trip_out, ((uint64_t)Pp * k4_set_cap() + 1) * 8))
-      return KMZ_E_HIP;
-    {
-      Timed t(c, KMZ_K_FINAL);
-      launch_k4_emit(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
-                     c->n_shapes, c->n_dep, c->index_base, Pp, P<uint32_t>(c->koff), P<unsigned long long>(c->kpool),
-                     P<uint32_t>(c->roff), P<unsigned long long>(c->rpool), cnt);
-      launch_k4_dedup(c->stream, P<unsigned long long>(c->kpool), P<uint32_t>(c->koff),
-                      P<unsigned long long>(c->rpool), P<uint32_t>(c->roff), n, Pp, epp, epp + c->n_dep,
-                      P<unsigned long long>(c->trip_out), st, cnt);
-    }
-    HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (!(h[C_FLAGS] & F_TRIPLE_OVERFLOW)) return KMZ_OK;
-    if (Pp * 2 > k4_pmax() || Pp >= c->n_dep) {
-      // a single endpoint's edge set exceeds the LDS set: global edge set
-      c->edge_R = 0;
-      return -100;
-    }
-    // too many distinct keys / endpoints in a partition: more partitions, redo
-    c->edge_R = Pp * 2;
-    HIPCHK(c, hipMemsetAsync(cnt + C_FLAGS, 0, 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(cnt + C_TRIPLES, 0, 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(st + S_ROWS, 0, 3 * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(st + S_TRIP_OUT, 0, 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
-  }
 }
 
 // K1': window join + uniqueness certificate.  *ok = false when the batch
@@ -420,8 +348,12 @@ static int run_join(kmz_ctx *c, bool *ok) {
   }
   {
     Timed t(c, KMZ_K_CERT);
-    launch_cert(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
-                P<unsigned long long>(c->cpool2), cur2, cnt);
+    launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
+                      P<unsigned long long>(c->cpool2), cur2, cnt);
+  }
+  {
+    Timed t(c, KMZ_K_CHECK);
+    launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
   }
   unsigned int h[C_COUNT];
   HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -477,6 +409,47 @@ static int run_table(kmz_ctx *c) {
   return KMZ_OK;
 }
 
+// K3 once per batch over (shape x status); every grouping the path needs is a
+// union of these groups (k_collapse_groups / k_collapse_endpoints).
+static int run_shape_stats(kmz_ctx *c) {
+  const uint32_t n = (uint32_t)c->n;
+  const uint64_t Gs = (uint64_t)c->n_shapes * c->n_status;
+  if (Gs >= 0xFFFFFFFFull) return fail(c, KMZ_E_ARG, "too many (shape x status) groups");
+  if (ensure(c, c->sgrp, (Gs + 1) * 48)) return KMZ_E_HIP;
+  unsigned long long *sg = P<unsigned long long>(c->sgrp);
+  unsigned int *cnt = P<unsigned int>(c->counters);
+  unsigned long long *nsrv = P<unsigned long long>(c->stats64) + S_SERVER;
+  const bool part = Gs > 1024 && k3_partitions((uint32_t)Gs) <= k3_pmax() && !(c->ablate & 8);
+  {
+    Timed t(c, KMZ_K_MEMSET);
+    HIPCHK(c, hipMemsetAsync(sg, 0, Gs * 40, c->stream));
+    HIPCHK(c, hipMemsetAsync(sg + 5 * Gs, 0xFF, Gs * 8, c->stream));
+  }
+  if (part) {
+    const uint32_t Pp = k3_partitions((uint32_t)Gs), nt = k3_tiles(n);
+    const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(64, 2048 / Pp));
+    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, (size_t)Pp * nt * 4 + 4) ||
+        ensure(c, c->k3part, (size_t)S * 6 * Gs * 8) || ensure(c, c->tile_tmp, (size_t)nt * 16))
+      return KMZ_E_HIP;
+    {
+      Timed t(c, KMZ_K_STATS);
+      launch_k3_produce(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_shapes,
+                        c->n_status, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp));
+    }
+    {
+      Timed t(c, KMZ_K_REDUCE);
+      launch_k3_reduce(c->stream, n, (uint32_t)Gs, c->index_base, c->k3pool.p, P<uint32_t>(c->k3dir),
+                       P<unsigned long long>(c->k3part), S, sg);
+    }
+  } else {
+    Timed t(c, KMZ_K_STATS);
+    launch_stats(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_shapes,
+                 c->n_status, c->index_base, sg, cnt, nsrv);
+  }
+  c->sstats = true;
+  return KMZ_OK;
+}
+
 static int run_deps(kmz_ctx *c, bool links) {
   const uint32_t n = (uint32_t)c->n;
   // unique edge keys are far fewer than spans; start at ~n/32 (grown on overflow)
@@ -504,20 +477,47 @@ static int run_deps(kmz_ctx *c, bool links) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     dups = hc[C_DUPS];
   }
-  if (dups == 0 && !(c->ablate & 16) && !c->tiles_off) {
-    c->path = joined ? 3 : 2;  // bit 0 window join, bit 1 tile walk
-    r = run_walk_tiles(c, links);
-    if (r != -100) return r;
-    c->tiles_off = true;
-    // fall through to the global-set walk: reset what the tile path touched
-    HIPCHK(c, hipMemsetAsync(cnt + C_FLAGS, 0, 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(st + S_ROWS, 0, 3 * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(st + S_TRIP_OUT, 0, 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
-  }
-  c->path = joined ? 1 : 0;
   if (ensure(c, c->trip, c->tcap * 8) || ensure(c, c->trip_out, c->tcap * 8)) return KMZ_E_HIP;
+  if (dups == 0 && !(c->ablate & 16)) {
+    // unique span ids: rows are the SERVER spans; chain interning (kmz_chain.hip)
+    if (!c->sstats && (r = run_shape_stats(c))) return r;
+    const uint32_t nt = chain_tiles(n);
+    if (ensure(c, c->ctab, c->ccap * 32) || ensure(c, c->tile_tmp, (size_t)nt * 16) ||
+        ensure(c, c->plist, (size_t)(n + 1) * 4))
+      return KMZ_E_HIP;
+    {
+      Timed t(c, KMZ_K_MEMSET);
+      HIPCHK(c, hipMemsetAsync(c->ctab.p, 0, c->ccap * 32, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
+    }
+    {
+      Timed t(c, KMZ_K_WALK);
+      launch_chain(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
+                   c->n_shapes, c->n_dep, c->index_base, c->sig_seed, c->ctab.p, c->ccap,
+                   P<unsigned long long>(c->trip), c->tcap, epp, links ? P<unsigned long long>(c->rowpos) : nullptr,
+                   P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->tile_tmp), st, c->ablate);
+    }
+    {  // ancestries that left their window: one pass, sized on the device (no host round trip)
+      Timed t(c, KMZ_K_PEND);
+      launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent),
+                        P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
+                        P<unsigned long long>(c->trip), c->tcap, epp, cnt, st);
+    }
+    {
+      Timed t(c, KMZ_K_FINAL);
+      launch_compact(c->stream, P<unsigned long long>(c->trip), c->tcap, P<unsigned long long>(c->trip_out),
+                     st + S_TRIP_OUT);
+      launch_collapse_endpoints(c->stream, P<unsigned long long>(c->sgrp), c->n_shapes, c->n_status,
+                                P<uint32_t>(c->d_dep), c->n_dep, P<uint32_t>(c->cparent), c->index_base, epp,
+                                epp + c->n_dep, cnt);
+    }
+    c->path = (joined ? 1 : 0) | 2;
+    c->chain_ran = true;
+    return KMZ_OK;
+  }
+  // repeated span ids: the row of an id is its last occurrence at its first
+  // position; one global walk per row over the table path's links
+  c->path = joined ? 1 : 0;
   HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
   {
     // the table is read only for repeated ids (dups > 0), which implies run_table
@@ -536,13 +536,14 @@ static int run_deps(kmz_ctx *c, bool links) {
 }
 
 static int run_stats(kmz_ctx *c, uint32_t mode) {
-  const uint32_t n = (uint32_t)c->n;
   uint32_t n_ep = mode == KMZ_RUN_STATS_RT ? c->n_rt : c->n_tag;
   const uint32_t *tab = mode == KMZ_RUN_STATS_RT ? P<uint32_t>(c->d_rt) : P<uint32_t>(c->d_tag);
   uint64_t G = (uint64_t)n_ep * c->n_status;
   if (G >= 0xFFFFFFFFull) return fail(c, KMZ_E_ARG, "too many groups");
   c->G = (uint32_t)G;
   c->ep_mode = mode;
+  int r;
+  if (!c->sstats && (r = run_shape_stats(c))) return r;
   if (ensure(c, c->grp, (G + 1) * 48) || ensure(c, c->grp_final, (G + 1) * sizeof(kmz_group))) return KMZ_E_HIP;
   unsigned long long *grp = P<unsigned long long>(c->grp);
   {
@@ -550,25 +551,10 @@ static int run_stats(kmz_ctx *c, uint32_t mode) {
     HIPCHK(c, hipMemsetAsync(grp, 0, G * 40, c->stream));
     HIPCHK(c, hipMemsetAsync(grp + 5 * G, 0xFF, G * 8, c->stream));
   }
-  const bool part = G > 1024 && k3_partitions((uint32_t)G) <= k3_pmax() && !(c->ablate & 8);
-  if (part) {
-    uint32_t Pp = k3_partitions((uint32_t)G), nt = k3_tiles(n);
-    uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(64, 2048 / Pp));
-    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, (size_t)Pp * nt * 4 + 4) ||
-        ensure(c, c->k3part, (size_t)S * 6 * G * 8) || ensure(c, c->tile_tmp, (size_t)nt * 16))
-      return KMZ_E_HIP;
-    Timed t(c, KMZ_K_STATS);
-    launch_k3_partitioned(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, tab, c->n_shapes, n_ep,
-                          c->n_status, c->index_base, grp, P<unsigned int>(c->counters),
-                          P<unsigned long long>(c->stats64) + S_SERVER, c->k3pool.p, P<uint32_t>(c->k3dir),
-                          P<unsigned long long>(c->k3part), S, P<uint32_t>(c->tile_tmp));
-  } else {
-    Timed t(c, KMZ_K_STATS);
-    launch_stats(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, tab, c->n_shapes, n_ep, c->n_status,
-                 c->index_base, grp, P<unsigned int>(c->counters), P<unsigned long long>(c->stats64) + S_SERVER);
-  }
   {
     Timed t(c, KMZ_K_FINAL);
+    launch_collapse_groups(c->stream, P<unsigned long long>(c->sgrp), c->n_shapes, c->n_status, tab, n_ep, grp,
+                           P<unsigned int>(c->counters));
     launch_finalize(c->stream, grp, c->G, P<kmz_group>(c->grp_final));
   }
   return KMZ_OK;
@@ -579,20 +565,39 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_run before kmz_load");
   uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
   if (smode == (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG)) return fail(c, KMZ_E_ARG, "choose one stats identity per run");
+  const bool links = (flags & KMZ_RUN_SPAN_LINKS) != 0;
   hipSetDevice(c->device);
   for (int attempt = 0; attempt < 8; ++attempt) {
+    c->sstats = false;
+    c->chain_ran = false;
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4, c->stream));
     HIPCHK(c, hipMemsetAsync(c->stats64.p, 0, S_COUNT * 8, c->stream));
     int r;
     if (smode && (r = run_stats(c, smode))) return r;
-    if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, (flags & KMZ_RUN_SPAN_LINKS) != 0))) return r;
+    if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, links))) return r;
     unsigned int h[C_COUNT];
     HIPCHK(c, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
+    {  // hash-table load factors: grow for the next run (correctness never
+       // depends on it: an overfull probe raises the overflow flags below)
+      unsigned long long s64[S_COUNT];
+      HIPCHK(c, hipMemcpy(s64, c->stats64.p, sizeof(s64), hipMemcpyDeviceToHost));
+      if (c->chain_ran && s64[S_CHAINS] * 2 > c->ccap && c->ccap < (1ull << 31)) c->ccap *= 2;
+      if ((flags & KMZ_RUN_DEPS) && s64[S_TRIP_OUT] * 2 > c->tcap) c->tcap *= 2;
+    }
     bool retry = false;
     if (h[C_FLAGS] & F_TRIPLE_OVERFLOW) {
       c->tcap *= 4;
+      retry = true;
+    }
+    if (h[C_FLAGS] & F_SIG) {  // an ancestry-hash collision: same run, another seed
+      c->sig_seed = mix64(c->sig_seed + 0x9E3779B97F4A7C15ull);
+      retry = true;
+    }
+    if (h[C_FLAGS] & F_CHAIN_OVERFLOW) {
+      if (c->ccap >= (1ull << 31)) return fail(c, KMZ_E_OVERFLOW, "chain table full");
+      c->ccap *= 4;
       retry = true;
     }
     if ((flags & KMZ_RUN_DEPS) && (uint64_t)h[C_DUPS] * 2 > c->dcap) {
@@ -603,7 +608,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
       int e = check_flags(c, h[C_FLAGS]);
       if (e) return e;
       c->ran = flags;
-      c->links = (flags & KMZ_RUN_SPAN_LINKS) != 0;
+      c->links = links;
       return KMZ_OK;
     }
   }
@@ -883,8 +888,6 @@ int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t 
   c->ts = o.timestamp;
   c->loaded = true;
   c->ran = 0;
-  c->tiles_off = false;
-  c->edge_R = 0;
   if (n_out) *n_out = n;
   return KMZ_OK;
 }

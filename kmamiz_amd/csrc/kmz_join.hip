@@ -576,14 +576,18 @@ void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const 
                      counters, ablate);
 }
 
-void launch_cert(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir, const CertPlan &pl,
-                 unsigned long long *pool2, unsigned int *cur2, unsigned int *counters) {
+void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
+                       const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters) {
   if (!n) return;
   const size_t lds = CERT_CHUNK * 8 + (size_t)2 * (1u << pl.B2) * 4;
   hipLaunchKernelGGL(k_cert_split, dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n, pl.chunks, pl.B2,
                      pool2, pl.cap2, cur2, counters);
-  hipLaunchKernelGGL(k_cert_check, dim3(CERT_BINS << pl.B2), dim3(1024), 0, s, (const unsigned long long *)pool2,
-                     pl.cap2, (const unsigned int *)cur2, 1u, counters);
+}
+
+void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
+                       const unsigned int *cur2, unsigned int *counters) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_cert_check, dim3(CERT_BINS << pl.B2), dim3(1024), 0, s, pool2, pl.cap2, cur2, 1u, counters);
 }
 
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,

@@ -13,13 +13,22 @@ constexpr uint8_t KIND_SERVER = KMZ_KIND_SERVER;
 constexpr uint8_t KIND_CLIENT = KMZ_KIND_CLIENT;
 
 // u32 device counters
-enum { C_FLAGS = 0, C_DUPS = 1, C_TRIPLES = 2, C_MISS = 3, C_PEND = 4, C_CERT = 5, C_COUNT = 8 };
+enum {
+  C_FLAGS = 0,
+  C_DUPS = 1,
+  C_TRIPLES = 2,
+  C_MISS = 3,
+  C_PEND = 4,
+  C_CERT = 5,
+  C_PLIST = 6,  // K4 spans whose ancestry leaves their LDS window (pending list length)
+  C_COUNT = 8
+};
 // C_CERT bits: the window join's answers cannot be used (global table path)
 constexpr uint32_t CERT_DUP = 1u, CERT_OVF = 2u;
 constexpr uint32_t MISSV = 0xFFFFFFFDu;  // dp: parent id not in the span's window
 constexpr uint32_t PEND = 0xFFFFFFFCu;   // cparent: CLIENT chain leaves the window
 // u64 device statistics
-enum { S_ROWS = 0, S_REL = 1, S_MAXD = 2, S_SERVER = 3, S_TRIP_OUT = 4, S_COUNT = 8 };
+enum { S_ROWS = 0, S_REL = 1, S_MAXD = 2, S_CHAINS = 3, S_SERVER = 4, S_TRIP_OUT = 5, S_COUNT = 8 };
 
 struct DupEntry {
   uint32_t pos, idx, winner, pad;
@@ -49,30 +58,38 @@ void launch_synth_fill(hipStream_t s, int config, uint64_t seed, uint64_t t0, ui
                        uint64_t gbase, const uint32_t *dur_table, SynthOut out);
 
 // partitioned K3 / K4 (kmz_part.hip)
-void launch_k3_partitioned(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
-                           const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
-                           uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint64_t index_base,
-                           unsigned long long *grp, unsigned int *counters, unsigned long long *n_server, void *pool,
-                           uint32_t *dir, unsigned long long *part, uint32_t S, uint32_t *tile_tmp);
+void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
+                       const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
+                       uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, unsigned int *counters,
+                       unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp);
+void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
+                      const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp);
 uint32_t k3_partitions(uint32_t G);
 uint32_t k3_pmax();
 uint64_t k3_pool_bytes(uint32_t n);
 uint32_t k3_tiles(uint32_t n);
-uint32_t k4_tiles(uint32_t n);
-uint32_t k4_pmax();
-uint32_t k4_set_cap();
-void launch_k4_count(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
-                     const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
-                     uint64_t index_base, uint32_t P, uint32_t *kdir, uint32_t *rdir, unsigned long long *rowpos,
-                     unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64);
-void launch_k4_emit(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
-                    const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
-                    uint64_t index_base, uint32_t P, const uint32_t *koff, unsigned long long *kpool,
-                    const uint32_t *roff, unsigned long long *rpool, unsigned int *counters);
-void launch_k4_dedup(hipStream_t s, const unsigned long long *kpool, const uint32_t *koff,
-                     const unsigned long long *rpool, const uint32_t *roff, uint32_t n, uint32_t P,
-                     unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *out,
-                     unsigned long long *stats64, unsigned int *counters);
+void launch_tile_sum(hipStream_t s, const uint32_t *v, uint32_t ntiles, uint32_t stride, uint32_t fields,
+                     unsigned long long *out, uint32_t max_field);
+
+// K4 by ancestor-chain interning (kmz_chain.hip)
+uint32_t chain_tiles(uint32_t n);
+void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+                  const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
+                  uint64_t index_base, uint64_t seed, void *ctab, uint64_t ccap, unsigned long long *trip,
+                  uint64_t tcap, unsigned long long *ep_ts, unsigned long long *rowpos, uint32_t *plist,
+                  uint32_t pcap, unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64,
+                  uint32_t ablate = 0);
+void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,
+                       const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, const uint32_t *dep_ep,
+                       uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
+                       unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
+                       unsigned long long *stats64);
+// shape-level K3 partials -> endpoint groups / dependency-endpoint records
+void launch_collapse_groups(hipStream_t s, const unsigned long long *sg, uint32_t n_shapes, uint32_t S,
+                            const uint32_t *map, uint32_t n_ep, unsigned long long *grp, unsigned int *counters);
+void launch_collapse_endpoints(hipStream_t s, const unsigned long long *sg, uint32_t n_shapes, uint32_t S,
+                               const uint32_t *dep_map, uint32_t n_dep, const uint32_t *cparent, uint64_t index_base,
+                               unsigned long long *ep_ts, unsigned long long *ep_first, unsigned int *counters);
 
 // window parent join + uniqueness certificate (kmz_join.hip)
 struct CertPlan {
@@ -86,8 +103,10 @@ __host__ __device__ uint32_t join_tiles(uint32_t n);
 void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
                  uint32_t *cparent, uint32_t *dp, unsigned long long *pool1, uint16_t *jdir, unsigned int *counters,
                  uint32_t ablate = 0);
-void launch_cert(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir, const CertPlan &pl,
-                 unsigned long long *pool2, unsigned int *cur2, unsigned int *counters);
+void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
+                       const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters);
+void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
+                       const unsigned int *cur2, unsigned int *counters);
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,
                  unsigned long long *mkey, uint32_t *mval, uint32_t mcap);
 void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent);

@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(256) k_stats(const uint8_t *__restrict__ kind,
     ++servers;
     uint32_t sh = shape[i];
     uint32_t st = status[i];
-    uint32_t ep = sh < n_shapes ? ep_of_shape[sh] : NONE;
+    uint32_t ep = sh < n_shapes ? (ep_of_shape ? ep_of_shape[sh] : sh) : NONE;  // null map: group by shape
     if (ep >= n_ep || st >= n_status) {
       atomicOr(&counters[C_FLAGS], F_RANGE);
       continue;
@@ -547,21 +547,103 @@ __global__ void __launch_bounds__(256) k_finalize(GroupAcc acc, uint32_t G, kmz_
   }
 }
 
+// K3 runs once per batch over (shape x status).  The endpoint groups of either
+// realtime identity (Traces.ts:32-46 / 73-99) are unions of shape groups; the
+// integer moments, max timestamp and min first index combine exactly.
+__global__ void __launch_bounds__(256) k_collapse_groups(const unsigned long long *__restrict__ sg, uint32_t n_shapes,
+                                                         uint32_t S, const uint32_t *__restrict__ map, uint32_t n_ep,
+                                                         unsigned long long *__restrict__ grp,
+                                                         unsigned int *__restrict__ counters) {
+  const uint64_t Gs = (uint64_t)n_shapes * S, G = (uint64_t)n_ep * S;
+  for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < Gs; x += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long c = sg[x];
+    if (!c) continue;
+    const uint32_t sh = (uint32_t)(x / S), st = (uint32_t)(x % S);
+    const uint32_t e = map[sh];
+    if (e >= n_ep) {
+      atomicOr(&counters[C_FLAGS], F_RANGE);
+      continue;
+    }
+    const uint64_t g = (uint64_t)e * S + st;
+    atomicAdd(&grp[g], c);
+    atomicAdd(&grp[G + g], sg[Gs + x]);
+    atomicAdd(&grp[2 * G + g], sg[2 * Gs + x]);
+    atomicAdd(&grp[3 * G + g], sg[3 * Gs + x]);
+    atomicMax(&grp[4 * G + g], sg[4 * Gs + x]);
+    atomicMin(&grp[5 * G + g], sg[5 * Gs + x]);
+  }
+}
+
+// Rows of a batch with unique span ids are its SERVER spans, so the per
+// dependency endpoint lastUsage (max timestamp of its rows) and first row (min
+// index) are unions of shape groups too; `external` is read off the first
+// row's contracted parent (Traces.ts:182-190, EndpointDependencies.ts:508-541).
+__global__ void __launch_bounds__(256) k_collapse_endpoints(const unsigned long long *__restrict__ sg, uint32_t n_shapes,
+                                                            uint32_t S, const uint32_t *__restrict__ dep_map,
+                                                            uint32_t n_dep, const uint32_t *__restrict__ cparent,
+                                                            uint64_t index_base,
+                                                            unsigned long long *__restrict__ ep_ts,
+                                                            unsigned long long *__restrict__ ep_first,
+                                                            unsigned int *__restrict__ counters) {
+  const uint64_t Gs = (uint64_t)n_shapes * S;
+  for (uint32_t sh = blockIdx.x * blockDim.x + threadIdx.x; sh < n_shapes; sh += gridDim.x * blockDim.x) {
+    unsigned long long tsx = 0, fst = ~0ull;
+    for (uint32_t st = 0; st < S; ++st) {
+      const uint64_t x = (uint64_t)sh * S + st;
+      if (!sg[x]) continue;
+      tsx = max(tsx, sg[4 * Gs + x]);
+      fst = min(fst, sg[5 * Gs + x]);
+    }
+    if (fst == ~0ull) continue;
+    const uint32_t e = dep_map ? dep_map[sh] : sh;
+    if (e >= n_dep) {
+      atomicOr(&counters[C_FLAGS], F_RANGE);
+      continue;
+    }
+    atomicMax(&ep_ts[e], tsx);
+    const uint32_t cp = cparent[fst - index_base];
+    atomicMin(&ep_first[e], (fst << 1) | (cp != NONE ? 1ull : 0ull));
+  }
+}
+
+// Edge-set compaction: each workgroup owns a contiguous slice of the table,
+// counts its keys, reserves their output range with ONE atomic, then writes
+// them (a second, cache-resident read of the slice).  Output order is free
+// (the keys are a set).
+constexpr uint32_t COMPACT_BLOCKS = 512;
 __global__ void __launch_bounds__(256) k_compact(const unsigned long long *__restrict__ trip, uint64_t tcap,
                                                  unsigned long long *__restrict__ out,
                                                  unsigned long long *__restrict__ count) {
-  // wave-aggregated: one atomic per wave that found keys
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t end = (tcap + stride - 1) / stride * stride;
-  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < end; p += stride) {
-    uint64_t k = p < tcap ? trip[p] : 0;
-    uint64_t m = __ballot(k != 0);
-    if (!m) continue;
-    uint32_t lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
-    base = __shfl(base, leader, 64);
-    if (k) out[base + __popcll(m & ((1ull << lane) - 1))] = k;
+  __shared__ uint32_t wsum[4];
+  __shared__ unsigned long long base;
+  const uint64_t per = (tcap + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(tcap, b0 + per);
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t c = 0;
+  for (uint64_t p = b0 + threadIdx.x; p < b1; p += 256) c += trip[p] != 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) wsum[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    base = t ? atomicAdd(count, (unsigned long long)t) : 0;
+  }
+  __syncthreads();
+  unsigned long long run = base;
+  for (uint64_t p0 = b0; p0 < b1; p0 += 256) {
+    const uint64_t p = p0 + threadIdx.x;
+    const unsigned long long k = p < b1 ? trip[p] : 0;
+    const uint64_t m = __ballot(k != 0);
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t v = 0; v < 4; ++v) {
+      before += v < w ? wsum[v] : 0;
+      tot += wsum[v];
+    }
+    if (k) out[run + before + __popcll(m & ((1ull << lane) - 1))] = k;
+    run += tot;
+    __syncthreads();
   }
 }
 
@@ -664,9 +746,25 @@ void launch_finalize(hipStream_t s, unsigned long long *grp, uint32_t G, kmz_gro
   hipLaunchKernelGGL(k_finalize, dim3(grid_for(G, 1024)), dim3(256), 0, s, a, G, out);
 }
 
+void launch_collapse_groups(hipStream_t s, const unsigned long long *sg, uint32_t n_shapes, uint32_t S,
+                            const uint32_t *map, uint32_t n_ep, unsigned long long *grp, unsigned int *counters) {
+  const uint64_t Gs = (uint64_t)n_shapes * S;
+  if (!Gs) return;
+  hipLaunchKernelGGL(k_collapse_groups, dim3(grid_for(Gs, 2048)), dim3(256), 0, s, sg, n_shapes, S, map, n_ep, grp,
+                     counters);
+}
+
+void launch_collapse_endpoints(hipStream_t s, const unsigned long long *sg, uint32_t n_shapes, uint32_t S,
+                               const uint32_t *dep_map, uint32_t n_dep, const uint32_t *cparent, uint64_t index_base,
+                               unsigned long long *ep_ts, unsigned long long *ep_first, unsigned int *counters) {
+  if (!n_shapes) return;
+  hipLaunchKernelGGL(k_collapse_endpoints, dim3(grid_for(n_shapes, 2048)), dim3(256), 0, s, sg, n_shapes, S, dep_map,
+                     n_dep, cparent, index_base, ep_ts, ep_first, counters);
+}
+
 void launch_compact(hipStream_t s, const unsigned long long *trip, uint64_t tcap, unsigned long long *out,
                     unsigned long long *count) {
-  hipLaunchKernelGGL(k_compact, dim3(grid_for(tcap, 4096)), dim3(256), 0, s, trip, tcap, out, count);
+  hipLaunchKernelGGL(k_compact, dim3(COMPACT_BLOCKS), dim3(256), 0, s, trip, tcap, out, count);
 }
 
 void launch_synth_count(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, uint64_t *cnt) {
