@@ -25,7 +25,8 @@
 //
 //   k4_chain       2048-span tile + 512-span halo per side in LDS (contracted
 //                  parent, kind, endpoint).  Marks the tile's spans and their
-//                  in-window ancestors, hashes the ancestries, probes, inserts
+//                  in-window ancestors, hashes the ancestries (a Horner walk
+//                  over LDS element hashes), probes, inserts
 //                  the new chains (one leader per distinct chain per
 //                  workgroup), then emits the new chains' keys with the whole
 //                  workgroup.  Ancestries that leave the window (or are deeper
@@ -123,25 +124,6 @@ __device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, 
 
 __device__ unsigned long long g_chain_dbg[8];  // diagnostic counters (KMZ_ABLATE bit 21 only)
 
-// Hash of the ancestry (s, a1, ..., aD) walked in LDS: sum_k elem(a_k) M^k,
-// finalised with D.  Returns the marker that ended the walk: W_NONE (reached
-// the root: *sig and *d valid), W_OUT (left the window, or deeper than
-// WIN_DEPTH) or W_CYC (a CLIENT loop).
-__device__ __forceinline__ uint32_t ancestry_sig(const uint16_t *lcp, const uint8_t *lkind, const uint32_t *lep,
-                                                 uint32_t jl, uint64_t seed, uint64_t *sig, uint32_t *d_out) {
-  uint64_t acc = sig_elem(lep[jl], lkind[jl] == KIND_SERVER, seed), m = SIG_M;
-  uint32_t d = 0, a = lcp[jl];
-  while (a < CW) {
-    if (++d > WIN_DEPTH) return W_OUT;
-    acc += sig_elem(lep[a], lkind[a] == KIND_SERVER, seed) * m;
-    m *= SIG_M;
-    a = lcp[a];
-  }
-  *sig = sig_final(acc, d, seed);
-  *d_out = d;
-  return a;
-}
-
 __global__ void __launch_bounds__(CTT, 4) k4_chain(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
                                                    const int64_t *__restrict__ ts,
                                                    const uint32_t *__restrict__ cparent, uint32_t n,
@@ -170,16 +152,18 @@ __global__ void __launch_bounds__(CTT, 4) k4_chain(const uint8_t *__restrict__ k
     uint32_t c[CPW], sh[CPW];
     uint8_t k[CPW];
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const uint32_t j = w0 + q * CTT + threadIdx.x;
-      const bool ok = j < w1;
-      c[q] = ok ? cparent[j] : NONE;
-      k[q] = ok ? kind[j] : 0;
-      sh[q] = ok ? shape[j] : NONE;
+    for (int q = 0; q < CPW; ++q) {  // clamped, unconditional: no branch between the loads
+      const uint32_t j = min(w0 + q * CTT + threadIdx.x, n - 1);
+      c[q] = cparent[j];
+      k[q] = kind[j];
+      sh[q] = shape[j];
     }
     uint32_t e[CPW];
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) e[q] = (k[q] != KIND_CLIENT && sh[q] < n_shapes) ? dep_ep[sh[q]] : NONE;
+    for (int q = 0; q < CPW; ++q) e[q] = dep_ep[sh[q] < n_shapes ? sh[q] : 0];
+#pragma unroll
+    for (int q = 0; q < CPW; ++q)
+      if (k[q] == KIND_CLIENT || sh[q] >= n_shapes || !n_shapes) e[q] = NONE;
 #pragma unroll
     for (int q = 0; q < CPW; ++q) {
       const uint32_t jl = q * CTT + threadIdx.x;
@@ -221,41 +205,69 @@ __global__ void __launch_bounds__(CTT, 4) k4_chain(const uint8_t *__restrict__ k
     }
   }
   __syncthreads();
-  // hash every needed ancestry (LDS only)
+  // hash every needed ancestry (Horner over s, a1, ..., aD, walked in LDS):
+  //   acc = ((elem(s) M + elem(a1)) M + ...) M + elem(aD),  sig = final(acc, D)
+  // lsig first holds every slot's element hash, then the finished sigs.
+  const bool hash_on = !(ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
 #pragma unroll
   for (int q = 0; q < CPW; ++q) {
     const uint32_t jl = q * CTT + threadIdx.x;
-    if (jl >= wn || !lneed[jl]) continue;
-    if (ablate & (1u << 16)) {  // diagnostic: no hashing / probing / inserting
-      lst[jl] = S_DONE;
-      continue;
+    if (jl < wn && lneed[jl]) lsig[jl] = sig_elem(lep[jl], lkind[jl] == KIND_SERVER, seed);
+  }
+  __syncthreads();
+  {
+    uint64_t sg[CPW];
+    uint32_t dd[CPW];
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const uint32_t jl = q * CTT + threadIdx.x;
+      sg[q] = 0;
+      dd[q] = 0;
+      if (jl >= wn || !lneed[jl]) continue;
+      if (!hash_on) {
+        lst[jl] = S_DONE;
+        continue;
+      }
+      if (lep[jl] >= n_ep && (lkind[jl] == KIND_SERVER || lanc[jl])) flags |= F_RANGE;
+      uint64_t acc = lsig[jl];
+      uint32_t d = 0, a = lcp[jl];
+      while (a < CW && d < WIN_DEPTH) {
+        acc = acc * SIG_M + lsig[a];
+        ++d;
+        a = lcp[a];
+      }
+      if (a != W_NONE) {  // W_OUT: leaves the window or deeper than WIN_DEPTH; W_CYC: CLIENT loop
+        if (a == W_CYC) flags |= F_CYCLE;
+        lst[jl] = S_PEND;
+        continue;
+      }
+      sg[q] = sig_final(acc, d, seed);
+      dd[q] = d;
+      lst[jl] = (ablate & (1u << 17)) ? S_DONE : S_PUT;  // diagnostic knob: hash only
     }
-    const bool on = lkind[jl] == KIND_SERVER;
-    if (lep[jl] >= n_ep && (on || lanc[jl])) flags |= F_RANGE;
-    uint64_t sg;
-    uint32_t d;
-    const uint32_t top = ancestry_sig(lcp, lkind, lep, jl, seed, &sg, &d);
-    if (top != W_NONE) {  // W_OUT: ancestry leaves the window or is too deep; W_CYC: CLIENT loop
-      if (top == W_CYC) flags |= F_CYCLE;
-      lst[jl] = S_PEND;
-      continue;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const uint32_t jl = q * CTT + threadIdx.x;
+      if (jl < wn && lneed[jl] && lst[jl] != S_PEND) {
+        lsig[jl] = sg[q];
+        ldep[jl] = (uint16_t)dd[q];
+      }
     }
-    lsig[jl] = sg;
-    ldep[jl] = (uint16_t)d;
-    lst[jl] = (ablate & (1u << 17)) ? S_DONE : S_PUT;  // diagnostic knob: hash only
   }
   __syncthreads();
   // one round of probes, all in flight; a found entry is checked against the
   // span's own (parent sig, endpoint, kind)
   {
     ulonglong2 w01[CPW], w23[CPW];  // (sig, parent sig), (endpoint/kind, -)
-    uint64_t pos[CPW];
+    uint64_t pos[CPW], sgq[CPW];
     bool pr[CPW];
 #pragma unroll
     for (int q = 0; q < CPW; ++q) {
       const uint32_t jl = q * CTT + threadIdx.x;
       pr[q] = jl < wn && lst[jl] == S_PUT;
-      pos[q] = pr[q] ? slot_of(lsig[jl], ccap) : 0;
+      sgq[q] = pr[q] ? lsig[jl] : 0;
+      pos[q] = pr[q] ? slot_of(sgq[q], ccap) : 0;
       const ulonglong2 *e = reinterpret_cast<const ulonglong2 *>(ctab + 4 * pos[q]);
       w01[q] = pr[q] ? e[0] : make_ulonglong2(0, 0);
       w23[q] = pr[q] ? e[1] : make_ulonglong2(0, 0);
@@ -264,7 +276,7 @@ __global__ void __launch_bounds__(CTT, 4) k4_chain(const uint8_t *__restrict__ k
     for (int q = 0; q < CPW; ++q) {
       if (!pr[q]) continue;
       const uint32_t jl = q * CTT + threadIdx.x;
-      const uint64_t sg = lsig[jl];
+      const uint64_t sg = sgq[q];
       for (uint32_t z = 0; w01[q].x != sg && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
         pos[q] = pos[q] + 1 == ccap ? 0 : pos[q] + 1;
         const ulonglong2 *e = reinterpret_cast<const ulonglong2 *>(ctab + 4 * pos[q]);
@@ -461,8 +473,8 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     const uint32_t es = sh < n_shapes ? dep_ep[sh] : NONE;
     const bool on = ki == KIND_SERVER;
     if (es >= n_ep && on) flags |= F_RANGE;
-    // hashes of the span's ancestry and of its parent's (suffix) ancestry
-    uint64_t acc = sig_elem(es, on, seed), mul = SIG_M, pacc = 0, pmul = 1;
+    // Horner hashes of the span's ancestry and of its parent's (suffix) ancestry
+    uint64_t acc = sig_elem(es, on, seed), pacc = 0;
     uint32_t d = 0;
     bool bad = false;
     const uint32_t a = cparent[i];
@@ -475,10 +487,8 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
       const uint32_t sa = shape[cur];
       const uint32_t ea = sa < n_shapes ? dep_ep[sa] : NONE;
       const uint64_t el = sig_elem(ea, kind[cur] == KIND_SERVER, seed);
-      acc += el * mul;
-      mul *= SIG_M;
-      pacc += el * pmul;
-      pmul *= SIG_M;
+      acc = acc * SIG_M + el;
+      pacc = d == 1 ? el : pacc * SIG_M + el;
     }
     if (bad) continue;
     const uint64_t sg = sig_final(acc, d, seed), psig = a == NONE ? ROOT_SIG : sig_final(pacc, d - 1, seed);
