@@ -54,7 +54,7 @@ struct kmz_ctx {
   DevBuf synth_cnt, synth_off, dur_table;
   DevBuf k3pool, k3dir, k3part, tile_tmp, sgrp;
   DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
-  DevBuf ctab, plist;                                 // K4 chain interning
+  DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n;  // K4 chain interning
   int path = 0;             // kmz_info.path of the last dependency run
   bool sstats = false;      // shape-level K3 partials computed in this run
   bool chain_ran = false;   // this run's dependency graph came from k4_chain
@@ -243,7 +243,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->stats64,   &c->scratch,
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
-                    &c->mval, &c->ctab, &c->plist};
+                    &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->own_stream) hipStreamDestroy(c->stream);
@@ -482,8 +482,13 @@ static int run_deps(kmz_ctx *c, bool links) {
     // unique span ids: rows are the SERVER spans; chain interning (kmz_chain.hip)
     if (!c->sstats && (r = run_shape_stats(c))) return r;
     const uint32_t nt = chain_tiles(n);
+    // per persistent workgroup: staged keys of candidate new chains and
+    // deferred chain checks (overflow is handled in place, just slower)
+    const uint32_t scap = 1u << 16, dcap = 1u << 14, ng = chain_grid(n);
     if (ensure(c, c->ctab, c->ccap * 32) || ensure(c, c->tile_tmp, (size_t)nt * 16) ||
-        ensure(c, c->plist, (size_t)(n + 1) * 4))
+        ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, (size_t)ng * scap * 8) ||
+        ensure(c, c->kstage_n, (size_t)ng * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 32) ||
+        ensure(c, c->kdefer_n, (size_t)ng * 4))
       return KMZ_E_HIP;
     {
       Timed t(c, KMZ_K_MEMSET);
@@ -495,7 +500,9 @@ static int run_deps(kmz_ctx *c, bool links) {
       launch_chain(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
                    c->n_shapes, c->n_dep, c->index_base, c->sig_seed, c->ctab.p, c->ccap,
                    P<unsigned long long>(c->trip), c->tcap, epp, links ? P<unsigned long long>(c->rowpos) : nullptr,
-                   P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->tile_tmp), st, c->ablate);
+                   P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->tile_tmp), st, P<unsigned long long>(c->kstage),
+                   scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
+                   c->ablate);
     }
     {  // ancestries that left their window: one pass, sized on the device (no host round trip)
       Timed t(c, KMZ_K_PEND);

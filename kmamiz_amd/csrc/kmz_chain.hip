@@ -8,7 +8,7 @@
 // ancestors only.  That sequence -- the row's *chain* -- is interned in a
 // global open-addressing table of 32-byte entries
 //
-//     { sig(chain), sig(parent chain) (0 at a root), endpoint, kind == SERVER }
+//     { sig(chain), sig(parent chain) (ROOT_SIG at a root), endpoint, kind == SERVER }
 //
 // Rows that share a chain (most of them: the 100M-span mesh has ~0.5M distinct
 // chains) produce identical edge keys, so only the workgroup that inserts a new
@@ -20,17 +20,23 @@
 // the hash: an entry records the exact recursive definition (parent chain,
 // endpoint, kind) and every span checks the entry it found or joined against
 // its own.  The table holds one entry per sig, so by induction from the roots
-// (parent sig 0) equal sigs are equal chains; a failed check (a 64-bit
-// collision) raises F_SIG and the run is repeated with another hash seed.
+// equal sigs are equal chains; a failed check (a 64-bit collision) raises F_SIG
+// and the run is repeated with another hash seed.
 //
-//   k4_chain       2048-span tile + 512-span halo per side in LDS (contracted
-//                  parent, kind, endpoint).  Marks the tile's spans and their
-//                  in-window ancestors, hashes the ancestries (a Horner walk
-//                  over LDS element hashes), probes, inserts
-//                  the new chains (one leader per distinct chain per
-//                  workgroup), then emits the new chains' keys with the whole
+//   k4_chain       persistent workgroups over 1536-span tiles + a 256-span halo
+//                  per side in LDS (contracted parent, kind, endpoint, element
+//                  hash).  Per tile: hash every non-CLIENT ancestry in the
+//                  window (a Horner walk over the LDS element hashes), probe
+//                  the tile's, check what the probes found, elect one leader
+//                  per distinct unknown chain in the workgroup; a leader
+//                  stages its chain's keys and claims the probed slot with one
+//                  CAS, publishing if it won and deferring a check to
+//                  k_chain_settle otherwise -- nothing waits on another
 //                  workgroup.  Ancestries that leave the window (or are deeper
-//                  than WIN_DEPTH inside it) go to a pending list.
+//                  than WIN_DEPTH inside it) go to a pending list.  The next
+//                  tile's window is loaded into registers while a tile computes.
+//   k_chain_settle the staged keys -> the global edge set; the deferred chain
+//                  checks (join + verify, or insert).
 //   k4_chain_pend  the pending spans, one pass, hashing over the global
 //                  contracted parents (rare).
 //
@@ -45,20 +51,25 @@
 
 namespace kmz {
 
-constexpr uint32_t CT = 2048, CH = 512, CW = CT + 2 * CH;
+constexpr uint32_t CT = 1536, CH = 256, CW = CT + 2 * CH;
 constexpr int CTT = 512;
-constexpr int CPT = CT / CTT;  // tile spans per thread
-constexpr int CPW = CW / CTT;  // window spans per thread
-static_assert(CW % CTT == 0 && CT % CTT == 0 && CH % CTT == 0, "window slots must map to fixed threads");
+constexpr int CPW = CW / CTT;  // window slots per thread (slot jl = q * CTT + thread)
+static_assert(CW % CTT == 0, "window slots must split evenly over the threads");
 constexpr uint16_t W_NONE = 0xFFFF, W_CYC = 0xFFFE, W_OUT = 0xFFFD;
 constexpr uint32_t WIN_DEPTH = 255;  // deeper in-window ancestries take the pending path
 constexpr uint32_t PROBE_MAX = 512;
-constexpr uint32_t IMAP = 512;  // LDS map: one inserting leader per distinct new chain
-constexpr uint32_t WAIT_ROUNDS = 256;
-constexpr uint32_t FMAX = CT;   // new SERVER chains per tile whose keys the workgroup emits
+constexpr uint32_t IMAP = 256;  // LDS map: one inserting leader per distinct new chain
+#ifndef KMZ_CHAIN_WAVES
+#define KMZ_CHAIN_WAVES 4
+#endif
+constexpr int CHAIN_WAVES = KMZ_CHAIN_WAVES;  // waves per SIMD: 4 -> 2 workgroups per CU (<= 128 VGPRs), 6 -> 3
+constexpr uint32_t CHAIN_WG = 256 * (CHAIN_WAVES / 2);  // persistent workgroups
 constexpr uint64_t SIG_M = 0xD6E8FEB86659FD93ull;
-// lst: per window slot
+// per-slot byte: kind in bits 0-1, state in bits 2-3 (state written only by the slot's owner)
 constexpr uint8_t S_NONE = 0, S_DONE = 1, S_PUT = 2, S_PEND = 3;
+__device__ __forceinline__ uint8_t kf_kind(uint8_t b) { return b & 3; }
+__device__ __forceinline__ uint8_t kf_st(uint8_t b) { return b >> 2; }
+__device__ __forceinline__ uint8_t kf_make(uint8_t kind, uint8_t st) { return (uint8_t)(kind | (st << 2)); }
 
 __device__ __forceinline__ uint64_t sig_elem(uint32_t ep, bool on, uint64_t seed) {
   return mix64((((uint64_t)ep << 1) | (on ? 1ull : 0ull)) ^ seed);
@@ -122,312 +133,284 @@ __device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, 
   return -1;
 }
 
-__device__ unsigned long long g_chain_dbg[8];  // diagnostic counters (KMZ_ABLATE bit 21 only)
+__device__ unsigned long long g_chain_dbg[8];  // diagnostic phase clocks (KMZ_ABLATE bit 22 only)
 
-__global__ void __launch_bounds__(CTT, 4) k4_chain(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
-                                                   const int64_t *__restrict__ ts,
-                                                   const uint32_t *__restrict__ cparent, uint32_t n,
-                                                   const uint32_t *__restrict__ dep_ep, uint32_t n_shapes,
-                                                   uint32_t n_ep, uint64_t index_base, uint64_t seed,
-                                                   unsigned long long *__restrict__ ctab, uint64_t ccap,
-                                                   unsigned long long *__restrict__ trip, uint64_t tcap,
-                                                   unsigned long long *__restrict__ ep_ts,
-                                                   unsigned long long *__restrict__ rowpos_out,
-                                                   uint32_t *__restrict__ plist, uint32_t pcap,
-                                                   unsigned int *__restrict__ counters,
-                                                   uint32_t *__restrict__ tile_stats, uint32_t ablate) {
-  __shared__ unsigned long long lsig[CW];
+__global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
+    const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape, const int64_t *__restrict__ ts,
+    const uint32_t *__restrict__ cparent, uint32_t n, const uint32_t *__restrict__ dep_ep, uint32_t n_shapes,
+    uint32_t n_ep, uint64_t index_base, uint64_t seed, unsigned long long *__restrict__ ctab, uint64_t ccap,
+    unsigned long long *__restrict__ trip, uint64_t tcap, unsigned long long *__restrict__ ep_ts,
+    unsigned long long *__restrict__ rowpos_out, uint32_t *__restrict__ plist, uint32_t pcap,
+    unsigned int *__restrict__ counters, uint32_t *__restrict__ wg_stats, unsigned long long *__restrict__ stage,
+    uint32_t scap, uint32_t *__restrict__ stage_n, unsigned long long *__restrict__ defer, uint32_t dcap,
+    uint32_t *__restrict__ defer_n, uint32_t nt, uint32_t ablate) {
+  __shared__ unsigned long long lsig[CW];  // element hashes, then the finished sigs
   __shared__ uint32_t lep[CW];
-  __shared__ uint16_t lcp[CW], ldep[CW];
-  __shared__ uint8_t lkind[CW], lneed[CW], lanc[CW], lst[CW];
-  __shared__ unsigned long long imap_sig[IMAP];
-  __shared__ uint32_t imap_state[IMAP];  // 0 open, 1 leader working, 2 leader done
-  __shared__ uint16_t fresh[FMAX];
-  __shared__ uint32_t foff[FMAX + 1];
-  __shared__ uint32_t nfresh;
+  __shared__ uint16_t lcp[CW];
+  __shared__ uint8_t lkf[CW], ldep[CW];
+  __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP], imap_epon[IMAP];
+  __shared__ uint32_t scnt, dcnt;  // keys staged for k_chain_settle, records deferred to k_chain_settle
   __shared__ uint32_t red[CTT / 64][4];
-  const uint32_t tile = blockIdx.x, t0 = tile * CT, t1 = min(n, t0 + CT);
-  const uint32_t w0 = t0 > CH ? t0 - CH : 0, w1 = min(n, t1 + CH), wn = w1 - w0;
-  {  // window -> LDS; every global load of a thread in flight together
-    uint32_t c[CPW], sh[CPW];
-    uint8_t k[CPW];
+  // diagnostic phase clock (KMZ_ABLATE bit 22 only): s_memtime deltas by thread 0
+  const bool dbg_t = (ablate & (1u << 22)) != 0;
+  unsigned long long tprev = 0, tacc[7] = {0, 0, 0, 0, 0, 0, 0};
+#define KMZ_STAMP(k)                                            \
+  if (dbg_t) {                                                  \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && tprev) tacc[k] += t_ - tprev;       \
+    tprev = t_;                                                 \
+  }
+  // persistent: this workgroup walks tiles blockIdx.x, +gridDim.x, ...; the
+  // next tile's window is loaded into registers while the current one computes
+  uint32_t c[CPW], sh[CPW], e[CPW];
+  uint8_t k[CPW];
+  auto fetch = [&](uint32_t tl) {
+    const uint32_t tb = tl * CT, wb = tb > CH ? tb - CH : 0;
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {  // clamped, unconditional: no branch between the loads
-      const uint32_t j = min(w0 + q * CTT + threadIdx.x, n - 1);
+    for (int q = 0; q < CPW; ++q) {  // clamped, unconditional: every load in flight together
+      const uint32_t j = min(wb + q * CTT + threadIdx.x, n - 1);
       c[q] = cparent[j];
       k[q] = kind[j];
       sh[q] = shape[j];
     }
-    uint32_t e[CPW];
+  };
+  auto gather_ep = [&]() {
 #pragma unroll
     for (int q = 0; q < CPW; ++q) e[q] = dep_ep[sh[q] < n_shapes ? sh[q] : 0];
-#pragma unroll
-    for (int q = 0; q < CPW; ++q)
-      if (k[q] == KIND_CLIENT || sh[q] >= n_shapes || !n_shapes) e[q] = NONE;
+  };
+  if (threadIdx.x == 0) scnt = dcnt = 0;
+  if (blockIdx.x < nt) {
+    fetch(blockIdx.x);
+    gather_ep();
+  }
+  uint32_t rows = 0, rel = 0, maxd = 0, fresh_n = 0, flags = 0;
+  for (uint32_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {
+    KMZ_STAMP(0);
+    const uint32_t t0 = tile * CT, t1 = min(n, t0 + CT);
+    const uint32_t w0 = t0 > CH ? t0 - CH : 0, w1 = min(n, t1 + CH), wn = w1 - w0;
+    // window -> LDS, with every non-CLIENT slot's element hash
 #pragma unroll
     for (int q = 0; q < CPW; ++q) {
       const uint32_t jl = q * CTT + threadIdx.x;
+      const bool client = k[q] == KIND_CLIENT;
+      const uint32_t ep = (client || sh[q] >= n_shapes) ? NONE : e[q];
       if (jl < wn) {
-        lkind[jl] = k[q];
-        lep[jl] = e[q];
+        lkf[jl] = kf_make(k[q] & 3, S_NONE);
+        lep[jl] = ep;
         lcp[jl] = c[q] == NONE ? W_NONE
                                : (c[q] == CYC ? W_CYC : ((c[q] >= w0 && c[q] < w1) ? (uint16_t)(c[q] - w0) : W_OUT));
+        if (!client) lsig[jl] = sig_elem(ep, k[q] == KIND_SERVER, seed);
       }
-      lneed[jl] = 0;
-      lanc[jl] = 0;
-      lst[jl] = S_NONE;
     }
-    for (uint32_t x = threadIdx.x; x < IMAP; x += CTT) {
-      imap_sig[x] = 0;
-      imap_state[x] = 0;
-    }
-    if (threadIdx.x == 0) nfresh = 0;
-  }
-  __syncthreads();
-  // mark: the tile's non-CLIENT spans need their chain, and so do their
-  // in-window ancestors (lanc: ancestor of a tile row, for non-SERVER
-  // lastUsage).  Every store writes 1, so concurrent marking loses nothing.
-  uint32_t flags = 0;
-#pragma unroll
-  for (int q = 0; q < CPT; ++q) {
-    const uint32_t i = t0 + q * CTT + threadIdx.x;
-    if (i >= t1) continue;
-    const uint32_t jl = i - w0;
-    const uint8_t kj = lkind[jl];
-    if (kj == KIND_CLIENT) continue;
-    const bool row = kj == KIND_SERVER;
-    lneed[jl] = 1;
-    for (uint32_t a = lcp[jl], steps = 0; a < CW && steps < CW; ++steps) {
-      if (lneed[a] && (!row || lanc[a])) break;  // marked from here up already
-      lneed[a] = 1;
-      if (row) lanc[a] = 1;
-      a = lcp[a];
-    }
-  }
-  __syncthreads();
-  // hash every needed ancestry (Horner over s, a1, ..., aD, walked in LDS):
-  //   acc = ((elem(s) M + elem(a1)) M + ...) M + elem(aD),  sig = final(acc, D)
-  // lsig first holds every slot's element hash, then the finished sigs.
-  const bool hash_on = !(ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
-#pragma unroll
-  for (int q = 0; q < CPW; ++q) {
-    const uint32_t jl = q * CTT + threadIdx.x;
-    if (jl < wn && lneed[jl]) lsig[jl] = sig_elem(lep[jl], lkind[jl] == KIND_SERVER, seed);
-  }
-  __syncthreads();
-  {
+    for (uint32_t x = threadIdx.x; x < IMAP; x += CTT) imap_sig[x] = 0;
+    __syncthreads();
+    KMZ_STAMP(1);
+    const bool more = tile + gridDim.x < nt;
+    if (more) fetch(tile + gridDim.x);  // lands while this tile computes
+    // hash every non-CLIENT ancestry of the window (Horner over s, a1, ..., aD,
+    // walked in LDS; halo slots are hashed as parents of tile slots):
+    //   acc = ((elem(s) M + elem(a1)) M + ...) M + elem(aD),  sig = final(acc, D)
+    // and issue the tile slots' probes at once.  A tile row's walk also gives
+    // its non-SERVER ancestors (not rows) their lastUsage.
     uint64_t sg[CPW];
     uint32_t dd[CPW];
+    const bool hash_on = !(ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
 #pragma unroll
     for (int q = 0; q < CPW; ++q) {
-      const uint32_t jl = q * CTT + threadIdx.x;
+      const uint32_t jl = q * CTT + threadIdx.x, i = w0 + jl;
       sg[q] = 0;
       dd[q] = 0;
-      if (jl >= wn || !lneed[jl]) continue;
+      if (jl >= wn) continue;
+      const uint8_t kj = kf_kind(lkf[jl]);
+      if (kj == KIND_CLIENT) continue;
+      const bool mine = i >= t0 && i < t1, row = mine && kj == KIND_SERVER;
       if (!hash_on) {
-        lst[jl] = S_DONE;
+        if (mine) lkf[jl] = kf_make(kj, S_DONE);
         continue;
       }
-      if (lep[jl] >= n_ep && (lkind[jl] == KIND_SERVER || lanc[jl])) flags |= F_RANGE;
+      if (row && lep[jl] >= n_ep) flags |= F_RANGE;
       uint64_t acc = lsig[jl];
       uint32_t d = 0, a = lcp[jl];
       while (a < CW && d < WIN_DEPTH) {
         acc = acc * SIG_M + lsig[a];
+        if (row && kf_kind(lkf[a]) != KIND_SERVER) {  // (rare) a non-SERVER ancestor of a row
+          if (lep[a] < n_ep)
+            atomicMax(&ep_ts[lep[a]], (unsigned long long)((uint64_t)ts[w0 + a] ^ TS_BIAS));
+          else
+            flags |= F_RANGE;
+        }
         ++d;
         a = lcp[a];
       }
       if (a != W_NONE) {  // W_OUT: leaves the window or deeper than WIN_DEPTH; W_CYC: CLIENT loop
-        if (a == W_CYC) flags |= F_CYCLE;
-        lst[jl] = S_PEND;
+        if (mine) {
+          if (a == W_CYC) flags |= F_CYCLE;
+          lkf[jl] = kf_make(kj, S_PEND);
+        }
         continue;
       }
       sg[q] = sig_final(acc, d, seed);
       dd[q] = d;
-      lst[jl] = (ablate & (1u << 17)) ? S_DONE : S_PUT;  // diagnostic knob: hash only
+      if (mine) lkf[jl] = kf_make(kj, (ablate & (1u << 17)) ? S_DONE : S_PUT);  // diagnostic knob: hash only
+    }
+    ulonglong2 w01[CPW];  // (sig, parent sig) of the probed slot
+    uint64_t w2[CPW];     // its endpoint/kind word
+    uint64_t pos[CPW];
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const uint32_t jl = q * CTT + threadIdx.x, i = w0 + jl;
+      const bool pr = sg[q] && i >= t0 && i < t1 && !(ablate & (1u << 17));
+      pos[q] = pr ? slot_of(sg[q], ccap) : 0;
+      const unsigned long long *en = ctab + 4 * pos[q];
+      w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(en) : make_ulonglong2(0, 0);
+      w2[q] = pr ? en[2] : 0;
+    }
+    __syncthreads();  // every walk is done reading element hashes
+    KMZ_STAMP(2);
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const uint32_t jl = q * CTT + threadIdx.x;
+      if (sg[q]) {
+        lsig[jl] = sg[q];
+        ldep[jl] = (uint8_t)dd[q];
+      }
     }
     __syncthreads();
+    KMZ_STAMP(3);
+    // check what the probes found against (parent sig, endpoint, kind); a
+    // chain not found (or not yet published) elects one leader per distinct
+    // sig in this workgroup
+    uint32_t hslot[CPW];
 #pragma unroll
     for (int q = 0; q < CPW; ++q) {
       const uint32_t jl = q * CTT + threadIdx.x;
-      if (jl < wn && lneed[jl] && lst[jl] != S_PEND) {
-        lsig[jl] = sg[q];
-        ldep[jl] = (uint16_t)dd[q];
-      }
-    }
-  }
-  __syncthreads();
-  // one round of probes, all in flight; a found entry is checked against the
-  // span's own (parent sig, endpoint, kind)
-  {
-    ulonglong2 w01[CPW], w23[CPW];  // (sig, parent sig), (endpoint/kind, -)
-    uint64_t pos[CPW], sgq[CPW];
-    bool pr[CPW];
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const uint32_t jl = q * CTT + threadIdx.x;
-      pr[q] = jl < wn && lst[jl] == S_PUT;
-      sgq[q] = pr[q] ? lsig[jl] : 0;
-      pos[q] = pr[q] ? slot_of(sgq[q], ccap) : 0;
-      const ulonglong2 *e = reinterpret_cast<const ulonglong2 *>(ctab + 4 * pos[q]);
-      w01[q] = pr[q] ? e[0] : make_ulonglong2(0, 0);
-      w23[q] = pr[q] ? e[1] : make_ulonglong2(0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      if (!pr[q]) continue;
-      const uint32_t jl = q * CTT + threadIdx.x;
-      const uint64_t sg = sgq[q];
-      for (uint32_t z = 0; w01[q].x != sg && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
+      hslot[q] = IMAP + 1;  // not an insert
+      if (!sg[q] || jl >= wn || kf_st(lkf[jl]) != S_PUT) continue;
+      for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
         pos[q] = pos[q] + 1 == ccap ? 0 : pos[q] + 1;
-        const ulonglong2 *e = reinterpret_cast<const ulonglong2 *>(ctab + 4 * pos[q]);
-        w01[q] = e[0];
-        w23[q] = e[1];
+        const unsigned long long *en = ctab + 4 * pos[q];
+        w01[q] = *reinterpret_cast<const ulonglong2 *>(en);
+        w2[q] = en[2];
       }
-      if (w01[q].x == sg && w01[q].y != 0 && w23[q].x != 0) {
-        const uint32_t p = lcp[jl];
-        const uint64_t psig = p == W_NONE ? ROOT_SIG : lsig[p];
-        if (w23[q].x != epon_of(lep[jl], lkind[jl] == KIND_SERVER) || w01[q].y != psig) flags |= F_SIG;
-        lst[jl] = S_DONE;
-      }
-    }
-  }
-  // chains not in the table: insert (no ordering among them: an entry names
-  // its parent by sig), one leader per distinct chain in this workgroup
-  uint32_t fresh_n = 0, dbg_put = 0, dbg_r[3] = {0, 0, 0}, dbg_rounds = 0;
-  if (ablate & (1u << 21))
-    for (uint32_t jl = threadIdx.x; jl < wn; jl += CTT) dbg_put += lst[jl] == S_PUT;
-  if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
-    for (uint32_t jl = threadIdx.x; jl < wn; jl += CTT)
-      if (lst[jl] == S_PUT) lst[jl] = S_DONE;
-  __syncthreads();
-  for (uint32_t round = 0;; ++round) {
-    bool prog = false, waiting = false;
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const uint32_t jl = q * CTT + threadIdx.x;
-      if (jl >= wn || lst[jl] != S_PUT) continue;
-      const uint64_t sg = lsig[jl];
       const uint32_t p = lcp[jl];
       const uint64_t psig = p == W_NONE ? ROOT_SIG : lsig[p];
-      const bool on = lkind[jl] == KIND_SERVER;
-      const uint64_t epon = epon_of(lep[jl], on);
-      uint32_t h = (uint32_t)(sg >> 32) & (IMAP - 1), slot = IMAP;
-      bool leader = true;
+      const uint8_t kj = kf_kind(lkf[jl]);
+      const uint64_t epon = epon_of(lep[jl], kj == KIND_SERVER);
+      if (w01[q].x == sg[q] && w01[q].y != 0 && w2[q] != 0) {
+        if (w2[q] != epon || w01[q].y != psig) flags |= F_SIG;
+        lkf[jl] = kf_make(kj, S_DONE);
+        continue;
+      }
+      uint32_t h = (uint32_t)(sg[q] >> 32) & (IMAP - 1);
+      hslot[q] = IMAP;  // a leader without a map slot (map full)
       for (uint32_t t = 0; t < 8; ++t) {
-        unsigned long long k = imap_sig[h];
-        if (k == 0) k = atomicCAS(&imap_sig[h], 0ull, (unsigned long long)sg);
-        if (k == 0 || k == sg) {  // this sig's slot: lead it if nobody does
-          slot = h;
-          leader = atomicCAS(&imap_state[h], 0u, 1u) == 0u;
+        const unsigned long long kk = atomicCAS(&imap_sig[h], 0ull, (unsigned long long)sg[q]);
+        if (kk == 0) {  // leader: publish what the followers compare against
+          imap_psig[h] = psig;
+          imap_epon[h] = epon;
+          hslot[q] = h;
+          break;
+        }
+        if (kk == sg[q]) {  // follower
+          hslot[q] = h | 0x80000000u;
           break;
         }
         h = (h + 1) & (IMAP - 1);
       }
-      if (!leader) {  // the leader's check covers this span too: same sig => same entry
-        if (imap_state[slot] == 2) {
-          lst[jl] = S_DONE;
-          prog = true;
-        } else {
-          waiting = true;
-        }
-        continue;
-      }
-      const int r = chain_put(ctab, ccap, sg, psig, epon, &flags);
-      if (r >= 0) ++dbg_r[r];
-      if (r == 0) {  // another workgroup inserted it and has not published yet
-        if (slot < IMAP) imap_state[slot] = 0;  // reopen the leadership for the next round
-        waiting = true;
-        continue;
-      }
-      prog = true;
-      lst[jl] = r < 0 ? S_PEND : S_DONE;
-      if (slot < IMAP) imap_state[slot] = r < 0 ? 0u : 2u;
-      if (r == 1) {
-        ++fresh_n;
-        if (on && ldep[jl]) {  // a new chain: its keys are emitted below
-          const uint32_t f = atomicAdd(&nfresh, 1u);
-          if (f < FMAX)
-            fresh[f] = (uint16_t)jl;
-          else
-            flags |= F_TRIPLE_OVERFLOW;  // cannot happen: FMAX covers every tile span
-        }
-      }
     }
-    ++dbg_rounds;
-    if (!__syncthreads_or(prog || (waiting && round < ((ablate & (1u << 20)) ? 0u : WAIT_ROUNDS)))) break;
-  }
-  if (ablate & (1u << 21)) {
-    atomicAdd(&g_chain_dbg[0], (unsigned long long)dbg_put);
-    atomicAdd(&g_chain_dbg[1], (unsigned long long)dbg_r[0]);
-    atomicAdd(&g_chain_dbg[2], (unsigned long long)dbg_r[1]);
-    atomicAdd(&g_chain_dbg[3], (unsigned long long)dbg_r[2]);
-    if (threadIdx.x == 0) {
-      atomicAdd(&g_chain_dbg[4], (unsigned long long)dbg_rounds);
-      atomicAdd(&g_chain_dbg[5], 1ull);
-    }
-  }
-  // the new chains' keys: (ancestor k, chain, k) work items over the workgroup
-  const uint32_t nf = (ablate & (1u << 19)) ? 0 : min(nfresh, FMAX);  // diagnostic knob: no emission
-  if (nf) {
-    if (threadIdx.x == 0) {
-      uint32_t acc = 0;
-      for (uint32_t f = 0; f < nf; ++f) {
-        foff[f] = acc;
-        acc += ldep[fresh[f]];
-      }
-      foff[nf] = acc;
-    }
+    if (more) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
+    if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
+#pragma unroll
+      for (int q = 0; q < CPW; ++q) hslot[q] = IMAP + 1;
     __syncthreads();
-    const uint32_t total = foff[nf];
-    for (uint32_t it = threadIdx.x; it < total; it += CTT) {
-      uint32_t lo = 0, hi = nf;  // last f with foff[f] <= it
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (foff[mid] <= it)
-          lo = mid;
-        else
-          hi = mid;
-      }
-      const uint32_t jl = fresh[lo], k = it - foff[lo] + 1;
-      uint32_t a = lcp[jl];
-      for (uint32_t t = 1; t < k; ++t) a = lcp[a];
-      edge_insert(edge_key(lep[a], lep[jl], k, lkind[a] == KIND_SERVER), trip, tcap, &flags);
-    }
-  }
-  // per tile: rows, relations, max depth; pending spans
-  uint32_t rows = 0, rel = 0, maxd = 0;
+    KMZ_STAMP(4);
+    // followers compare with their leader; leaders claim the slot the probe
+    // ended on (one CAS), publish if they won, and defer a final check to
+    // k_chain_settle otherwise.  Keys of a leader's chain are staged whether
+    // or not it is new (duplicates are harmless in the edge set), so nothing
+    // here waits on another workgroup.
 #pragma unroll
-  for (int q = 0; q < CPT; ++q) {
-    const uint32_t i = t0 + q * CTT + threadIdx.x;
-    if (i >= t1) continue;
-    const uint32_t jl = i - w0;
-    const uint8_t kj = lkind[jl];
-    uint64_t rp = NONE64;
-    if (kj != KIND_CLIENT) {
-      const bool pending = lst[jl] != S_DONE;  // S_PUT left over: a starved wait
-      if (kj == KIND_SERVER) {
-        rp = index_base + i;
-        if (!pending) {
-          const uint32_t d = ldep[jl];
-          ++rows;
-          rel += d;
-          maxd = max(maxd, d);
+    for (int q = 0; q < CPW; ++q) {
+      if (hslot[q] > IMAP) {
+        if (hslot[q] != IMAP + 1) {  // follower
+          const uint32_t jl = q * CTT + threadIdx.x, h = hslot[q] & (IMAP - 1);
+          const uint32_t p = lcp[jl];
+          const uint8_t kj = kf_kind(lkf[jl]);
+          if (imap_psig[h] != (p == W_NONE ? ROOT_SIG : lsig[p]) || imap_epon[h] != epon_of(lep[jl], kj == KIND_SERVER))
+            flags |= F_SIG;
+          lkf[jl] = kf_make(kj, S_DONE);
+        }
+        continue;
+      }
+      const uint32_t jl = q * CTT + threadIdx.x;
+      const uint32_t p = lcp[jl];
+      const uint8_t kj = kf_kind(lkf[jl]);
+      const bool on = kj == KIND_SERVER;
+      const uint64_t psig = p == W_NONE ? ROOT_SIG : lsig[p], epon = epon_of(lep[jl], on);
+      unsigned long long *en = ctab + 4 * pos[q];
+      const unsigned long long cv = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
+      const uint32_t d = dd[q];
+      if (on && d && !(ablate & (1u << 19))) {  // stage the chain's keys (knob 19: diagnostic, none)
+        const uint32_t es = lep[jl];
+        const uint32_t base = atomicAdd(&scnt, d);
+        uint32_t a = p;
+        for (uint32_t kk = 1; kk <= d; ++kk) {
+          const uint64_t key = edge_key(lep[a], es, kk, kf_kind(lkf[a]) == KIND_SERVER);
+          if (base + d <= scap)
+            stage[(uint64_t)blockIdx.x * scap + base + kk - 1] = key;  // inserted by k_chain_settle
+          else
+            edge_insert(key, trip, tcap, &flags);  // staging region full: insert here
+          a = lcp[a];
         }
       }
-      if (pending) {
-        const uint32_t x = atomicAdd(&counters[C_PLIST], 1u);
-        if (x < pcap) plist[x] = i;
+      if (cv == 0) {  // won the slot: publish
+        atomicExch(&en[1], (unsigned long long)psig);
+        atomicExch(&en[2], (unsigned long long)epon);
+        ++fresh_n;
+      } else {  // joined an unpublished entry, or lost the slot to another chain
+        const uint32_t x = atomicAdd(&dcnt, 1u);
+        if (x < dcap) {
+          unsigned long long *r = defer + 4 * ((uint64_t)blockIdx.x * dcap + x);
+          r[0] = sg[q];
+          r[1] = psig;
+          r[2] = epon;
+        } else {
+          int rr = 0;
+          for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t) rr = chain_put(ctab, ccap, sg[q], psig, epon, &flags);
+          fresh_n += rr == 1;
+        }
       }
+      lkf[jl] = kf_make(kj, S_DONE);
     }
-    if (rowpos_out) rowpos_out[i] = rp;
-  }
-  // non-SERVER ancestors of rows are not rows: their use counts for lastUsage
+    KMZ_STAMP(5);
+    // per span of the tile: row counts, pending list, rowpos
 #pragma unroll
-  for (int q = 0; q < CPW; ++q) {
-    const uint32_t jl = q * CTT + threadIdx.x;
-    if (jl < wn && lanc[jl] && lkind[jl] != KIND_SERVER && lep[jl] < n_ep)
-      atomicMax(&ep_ts[lep[jl]], (unsigned long long)((uint64_t)ts[w0 + jl] ^ TS_BIAS));
+    for (int q = 0; q < CPW; ++q) {
+      const uint32_t jl = q * CTT + threadIdx.x, i = w0 + jl;
+      if (jl >= wn || i < t0 || i >= t1) continue;
+      const uint8_t b = lkf[jl], kj = kf_kind(b);
+      uint64_t rp = NONE64;
+      if (kj != KIND_CLIENT) {
+        const bool pending = kf_st(b) != S_DONE;
+        if (kj == KIND_SERVER) {
+          rp = index_base + i;
+          if (!pending) {
+            ++rows;
+            rel += dd[q];
+            maxd = max(maxd, dd[q]);
+          }
+        }
+        if (pending) {
+          const uint32_t x = atomicAdd(&counters[C_PLIST], 1u);
+          if (x < pcap) plist[x] = i;
+        }
+      }
+      if (rowpos_out) rowpos_out[i] = rp;
+    }
+    __syncthreads();  // LDS is rewritten by the next tile
+    KMZ_STAMP(6);
   }
+  // per workgroup: rows, relations, max depth, new chains
   if (flags) atomicOr(&counters[C_FLAGS], flags);
   for (int o = 32; o > 0; o >>= 1) {
     fresh_n += __shfl_xor(fresh_n, o, 64);
@@ -445,8 +428,44 @@ __global__ void __launch_bounds__(CTT, 4) k4_chain(const uint8_t *__restrict__ k
   if (threadIdx.x < 4) {
     uint32_t a = 0;
     for (int w = 0; w < CTT / 64; ++w) a = threadIdx.x == 2 ? max(a, red[w][2]) : a + red[w][threadIdx.x];
-    tile_stats[(uint64_t)tile * 4 + threadIdx.x] = a;
+    wg_stats[(uint64_t)blockIdx.x * 4 + threadIdx.x] = a;
   }
+  if (threadIdx.x == 0) {
+    stage_n[blockIdx.x] = min(scnt, scap);
+    defer_n[blockIdx.x] = min(dcnt, dcap);
+  }
+  if (dbg_t && threadIdx.x == 0)
+    for (int kk = 0; kk < 7; ++kk) atomicAdd(&g_chain_dbg[kk], tacc[kk]);
+#undef KMZ_STAMP
+}
+
+// keys of the chains the tile kernel staged, per workgroup -> the edge set;
+// and the deferred chain checks: every entry the tile kernel claimed is
+// published by now, so each deferred (sig, parent sig, endpoint/kind) is
+// joined and checked, or inserted if its slot was lost to another chain
+__global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *__restrict__ stage, uint32_t scap,
+                                                      const uint32_t *__restrict__ stage_n,
+                                                      const unsigned long long *__restrict__ defer, uint32_t dcap,
+                                                      const uint32_t *__restrict__ defer_n, uint32_t nwg,
+                                                      unsigned long long *__restrict__ trip, uint64_t tcap,
+                                                      unsigned long long *__restrict__ ctab, uint64_t ccap,
+                                                      unsigned int *__restrict__ counters,
+                                                      unsigned long long *__restrict__ stats64) {
+  uint32_t flags = 0, fresh = 0;
+  for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
+    const uint32_t m = stage_n[w];
+    for (uint32_t x = threadIdx.x; x < m; x += blockDim.x) edge_insert(stage[(uint64_t)w * scap + x], trip, tcap, &flags);
+    const uint32_t md = defer_n[w];
+    for (uint32_t x = threadIdx.x; x < md; x += blockDim.x) {
+      const unsigned long long *r = defer + 4 * ((uint64_t)w * dcap + x);
+      int rr = 0;
+      for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t) rr = chain_put(ctab, ccap, r[0], r[1], r[2], &flags);
+      fresh += rr == 1;
+    }
+  }
+  if (flags) atomicOr(&counters[C_FLAGS], flags);
+  for (int o = 32; o > 0; o >>= 1) fresh += __shfl_xor(fresh, o, 64);
+  if ((threadIdx.x & 63) == 0 && fresh) atomicAdd(&stats64[S_CHAINS], (unsigned long long)fresh);
 }
 
 // The pending spans (ancestry outside their LDS window), one pass: each hashes
@@ -496,9 +515,9 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     for (uint32_t t = 0; t < 1u << 20 && r == 0; ++t) r = chain_put(ctab, ccap, sg, psig, epon_of(es, on), &flags);
     if (r <= 0) continue;
     if (on) {  // a row: its relations, keys (new chain) and non-SERVER ancestors
-      uint32_t k = 0;
+      uint32_t kk = 0;
       for (uint32_t cur = a; cur != NONE; cur = cparent[cur]) {
-        ++k;
+        ++kk;
         const uint8_t ka = kind[cur];
         const uint32_t sa = shape[cur];
         const uint32_t ea = sa < n_shapes ? dep_ep[sa] : NONE;
@@ -506,7 +525,7 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
           flags |= F_RANGE;
           break;
         }
-        if (r == 1) edge_insert(edge_key(ea, es, k, ka == KIND_SERVER), trip, tcap, &flags);
+        if (r == 1) edge_insert(edge_key(ea, es, kk, ka == KIND_SERVER), trip, tcap, &flags);
         if (ka != KIND_SERVER) atomicMax(&ep_ts[ea], (unsigned long long)((uint64_t)ts[cur] ^ TS_BIAS));
       }
       atomicAdd(&stats64[S_ROWS], 1ull);
@@ -530,18 +549,26 @@ extern "C" int kmz__debug_chain(unsigned long long *out, int reset) {
 }
 namespace kmz {
 
+uint32_t chain_grid(uint32_t n) { return std::min<uint32_t>(chain_tiles(n), CHAIN_WG); }
+
 void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
                   const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
                   uint64_t index_base, uint64_t seed, void *ctab, uint64_t ccap, unsigned long long *trip,
                   uint64_t tcap, unsigned long long *ep_ts, unsigned long long *rowpos, uint32_t *plist,
-                  uint32_t pcap, unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64,
-                  uint32_t ablate) {
+                  uint32_t pcap, unsigned int *counters, uint32_t *wg_stats, unsigned long long *stats64,
+                  unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
+                  uint32_t dcap, uint32_t *defer_n, uint32_t ablate) {
   const uint32_t nt = chain_tiles(n);
   if (!nt) return;
-  hipLaunchKernelGGL(k4_chain, dim3(nt), dim3(CTT), 0, s, kind, shape, ts, cparent, n, dep_ep, n_shapes, n_ep,
-                     index_base, seed, reinterpret_cast<unsigned long long *>(ctab), ccap, trip, tcap, ep_ts, rowpos,
-                     plist, pcap, counters, tile_stats, ablate);
-  launch_tile_sum(s, tile_stats, nt, 4u, 4u, stats64 + S_ROWS, 2u);  // rows, rel, maxd, chains
+  const uint32_t g = chain_grid(n);
+  unsigned long long *tab = reinterpret_cast<unsigned long long *>(ctab);
+  hipLaunchKernelGGL(k4_chain, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, dep_ep, n_shapes, n_ep,
+                     index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
+                     scap, stage_n, defer, dcap, defer_n, nt, ablate);
+  hipLaunchKernelGGL(k_chain_settle, dim3(g), dim3(256), 0, s, (const unsigned long long *)stage, scap,
+                     (const uint32_t *)stage_n, (const unsigned long long *)defer, dcap, (const uint32_t *)defer_n, g,
+                     trip, tcap, tab, ccap, counters, stats64);
+  launch_tile_sum(s, wg_stats, g, 4u, 4u, stats64 + S_ROWS, 2u);  // rows, rel, maxd, chains
 }
 
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,

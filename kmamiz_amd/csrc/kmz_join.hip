@@ -124,13 +124,18 @@ __global__ void __launch_bounds__(JTT) k_join_window(const uint64_t *__restrict_
   uint64_t s[PW], p[PW];
   uint8_t k[PW];
 #pragma unroll
-  for (int q = 0; q < PW; ++q) {
-    const uint32_t j = w0 + q * JTT + threadIdx.x;
-    const bool ok = j < w1;
-    s[q] = ok ? sid[j] : 0;
-    p[q] = ok ? pid[j] : 0;
-    k[q] = ok ? kind[j] : 0;
+  for (int q = 0; q < PW; ++q) {  // clamped and unconditional: no branch between the loads
+    const uint32_t j = w0 + q * JTT + threadIdx.x, jj = min(j, n - 1);
+    s[q] = sid[jj];
+    p[q] = pid[jj];
+    k[q] = kind[jj];
   }
+#pragma unroll
+  for (int q = 0; q < PW; ++q)
+    if (w0 + q * JTT + threadIdx.x >= w1) {
+      s[q] = p[q] = 0;
+      k[q] = 0;
+    }
   uint64_t hs[PW];
 #pragma unroll
   for (int q = 0; q < PW; ++q) {

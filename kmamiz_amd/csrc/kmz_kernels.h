@@ -78,7 +78,9 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint64_t index_base, uint64_t seed, void *ctab, uint64_t ccap, unsigned long long *trip,
                   uint64_t tcap, unsigned long long *ep_ts, unsigned long long *rowpos, uint32_t *plist,
                   uint32_t pcap, unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64,
-                  uint32_t ablate = 0);
+                  unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
+                  uint32_t dcap, uint32_t *defer_n, uint32_t ablate = 0);
+uint32_t chain_grid(uint32_t n);
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,
                        const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,

@@ -1,0 +1,24 @@
+"""Diagnostic: k4_chain phase clocks (KMZ_ABLATE bit 22), summed over workgroups."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["KMZ_ABLATE"] = str(1 << 22)
+from kmamiz_amd import Engine, synth  # noqa: E402
+from kmamiz_amd import _lib as L  # noqa: E402
+
+ntr = int(sys.argv[1]) if len(sys.argv) > 1 else 3650000
+e = Engine(0)
+e.load_synthetic(synth.MESH, synth.SEED, 0, ntr)
+buf = (C.c_ulonglong * 8)()
+e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+names = ["loop/next", "fill", "hash+probe-issue", "sig-write", "check+elect", "leaders", "stats"]
+for k in range(2):
+    L.lib().kmz__debug_chain(buf, 1)
+    e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    L.lib().kmz__debug_chain(buf, 1)
+    v = list(buf)[:7]
+    tot = max(1, sum(v))
+    print("run", k, " ".join(f"{nm}={x / tot * 100:.1f}%" for nm, x in zip(names, v)), "total", tot, flush=True)
