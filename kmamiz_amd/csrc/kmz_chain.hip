@@ -54,6 +54,8 @@ namespace kmz {
 constexpr uint32_t CT = 1536, CH = 256, CW = CT + 2 * CH;
 constexpr int CTT = 512;
 constexpr int CPW = CW / CTT;  // window slots per thread (slot jl = q * CTT + thread)
+constexpr int TPW = CT / CTT;  // tile slots per thread
+static_assert(CT % CTT == 0, "tile slots must split evenly over the threads");
 static_assert(CW % CTT == 0, "window slots must split evenly over the threads");
 constexpr uint16_t W_NONE = 0xFFFF, W_CYC = 0xFFFE, W_OUT = 0xFFFD;
 constexpr uint32_t WIN_DEPTH = 255;  // deeper in-window ancestries take the pending path
@@ -144,16 +146,16 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     unsigned int *__restrict__ counters, uint32_t *__restrict__ wg_stats, unsigned long long *__restrict__ stage,
     uint32_t scap, uint32_t *__restrict__ stage_n, unsigned long long *__restrict__ defer, uint32_t dcap,
     uint32_t *__restrict__ defer_n, uint32_t nt, uint32_t ablate) {
-  __shared__ unsigned long long lsig[CW];  // element hashes, then the finished sigs
-  __shared__ uint32_t lep[CW];
-  __shared__ uint16_t lcp[CW];
-  __shared__ uint8_t lkf[CW], ldep[CW];
+  // one 16-byte record per window slot: element hash (x, y), endpoint (z),
+  // contracted parent | kind << 16 (w) -- a walk step is one LDS read
+  __shared__ uint4 lrec[CW];
+  __shared__ unsigned long long lpow[WIN_DEPTH + 1];  // SIG_M^d
   __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP], imap_epon[IMAP];
   __shared__ uint32_t scnt, dcnt;  // keys staged for k_chain_settle, records deferred to k_chain_settle
   __shared__ uint32_t red[CTT / 64][4];
   // diagnostic phase clock (KMZ_ABLATE bit 22 only): s_memtime deltas by thread 0
   const bool dbg_t = (ablate & (1u << 22)) != 0;
-  unsigned long long tprev = 0, tacc[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = 0, tacc[6] = {0, 0, 0, 0, 0, 0};
 #define KMZ_STAMP(k)                                            \
   if (dbg_t) {                                                  \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -179,6 +181,12 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     for (int q = 0; q < CPW; ++q) e[q] = dep_ep[sh[q] < n_shapes ? sh[q] : 0];
   };
   if (threadIdx.x == 0) scnt = dcnt = 0;
+  if (threadIdx.x <= WIN_DEPTH) {
+    uint64_t r = 1, b = SIG_M;
+    for (uint32_t x = threadIdx.x; x; x >>= 1, b *= b)
+      if (x & 1) r *= b;
+    lpow[threadIdx.x] = r;
+  }
   if (blockIdx.x < nt) {
     fetch(blockIdx.x);
     gather_ep();
@@ -194,111 +202,119 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       const uint32_t jl = q * CTT + threadIdx.x;
       const bool client = k[q] == KIND_CLIENT;
       const uint32_t ep = (client || sh[q] >= n_shapes) ? NONE : e[q];
-      if (jl < wn) {
-        lkf[jl] = kf_make(k[q] & 3, S_NONE);
-        lep[jl] = ep;
-        lcp[jl] = c[q] == NONE ? W_NONE
-                               : (c[q] == CYC ? W_CYC : ((c[q] >= w0 && c[q] < w1) ? (uint16_t)(c[q] - w0) : W_OUT));
-        if (!client) lsig[jl] = sig_elem(ep, k[q] == KIND_SERVER, seed);
-      }
+      const uint32_t cp =
+          c[q] == NONE ? W_NONE : (c[q] == CYC ? W_CYC : ((c[q] >= w0 && c[q] < w1) ? c[q] - w0 : W_OUT));
+      const uint64_t el = client ? 0 : sig_elem(ep, k[q] == KIND_SERVER, seed);
+      if (jl < wn) lrec[jl] = make_uint4((uint32_t)el, (uint32_t)(el >> 32), ep, cp | ((uint32_t)(k[q] & 3) << 16));
     }
     for (uint32_t x = threadIdx.x; x < IMAP; x += CTT) imap_sig[x] = 0;
     __syncthreads();
     KMZ_STAMP(1);
     const bool more = tile + gridDim.x < nt;
     if (more) fetch(tile + gridDim.x);  // lands while this tile computes
-    // hash every non-CLIENT ancestry of the window (Horner over s, a1, ..., aD,
-    // walked in LDS; halo slots are hashed as parents of tile slots):
-    //   acc = ((elem(s) M + elem(a1)) M + ...) M + elem(aD),  sig = final(acc, D)
-    // and issue the tile slots' probes at once.  A tile row's walk also gives
-    // its non-SERVER ancestors (not rows) their lastUsage.
-    uint64_t sg[CPW];
-    uint32_t dd[CPW];
+    // hash the ancestry of every non-CLIENT span of the tile by a Horner walk
+    // over the LDS element hashes of its ancestors a1..aD:
+    //   pacc = (elem(a1) M + elem(a2)) M + ... + elem(aD)
+    //   sig  = final(elem(s) M^D + pacc, D),  parent sig = final(pacc, D-1)
+    // (the parent's own sig, so halo spans need no walk), and issue the probes
+    // at once.  A row's walk also gives its non-SERVER ancestors (not rows)
+    // their lastUsage.
+    const uint32_t toff = t0 - w0;
+    uint64_t sg[TPW], ps[TPW], acc[TPW];
+    uint32_t dd[TPW], wa[TPW], myep[TPW];
+    uint8_t st[TPW], kq[TPW];
     const bool hash_on = !(ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const uint32_t jl = q * CTT + threadIdx.x, i = w0 + jl;
-      sg[q] = 0;
+    for (int q = 0; q < TPW; ++q) {
+      const uint32_t jl = toff + q * CTT + threadIdx.x;
+      const uint4 r = lrec[min(jl, CW - 1)];
+      kq[q] = (r.w >> 16) & 3;
+      myep[q] = r.z;
+      sg[q] = (uint64_t)r.y << 32 | r.x;  // the element hash until the walk is done
+      acc[q] = 0;
       dd[q] = 0;
-      if (jl >= wn) continue;
-      const uint8_t kj = kf_kind(lkf[jl]);
-      if (kj == KIND_CLIENT) continue;
-      const bool mine = i >= t0 && i < t1, row = mine && kj == KIND_SERVER;
-      if (!hash_on) {
-        if (mine) lkf[jl] = kf_make(kj, S_DONE);
-        continue;
-      }
-      if (row && lep[jl] >= n_ep) flags |= F_RANGE;
-      uint64_t acc = lsig[jl];
-      uint32_t d = 0, a = lcp[jl];
-      while (a < CW && d < WIN_DEPTH) {
-        acc = acc * SIG_M + lsig[a];
-        if (row && kf_kind(lkf[a]) != KIND_SERVER) {  // (rare) a non-SERVER ancestor of a row
-          if (lep[a] < n_ep)
-            atomicMax(&ep_ts[lep[a]], (unsigned long long)((uint64_t)ts[w0 + a] ^ TS_BIAS));
-          else
-            flags |= F_RANGE;
-        }
-        ++d;
-        a = lcp[a];
-      }
-      if (a != W_NONE) {  // W_OUT: leaves the window or deeper than WIN_DEPTH; W_CYC: CLIENT loop
-        if (mine) {
-          if (a == W_CYC) flags |= F_CYCLE;
-          lkf[jl] = kf_make(kj, S_PEND);
-        }
-        continue;
-      }
-      sg[q] = sig_final(acc, d, seed);
-      dd[q] = d;
-      if (mine) lkf[jl] = kf_make(kj, (ablate & (1u << 17)) ? S_DONE : S_PUT);  // diagnostic knob: hash only
+      wa[q] = W_NONE;
+      st[q] = S_NONE;
+      if (w0 + jl >= t1 || kq[q] == KIND_CLIENT) continue;
+      st[q] = S_DONE;
+      if (!hash_on) continue;
+      if (kq[q] == KIND_SERVER && r.z >= n_ep) flags |= F_RANGE;
+      wa[q] = r.w & 0xFFFF;
     }
-    ulonglong2 w01[CPW];  // (sig, parent sig) of the probed slot
-    uint64_t w2[CPW];     // its endpoint/kind word
-    uint64_t pos[CPW];
+    // the TPW walks of a thread step together: TPW independent LDS reads in
+    // flight per step
+    for (;;) {
+      bool go = false;
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const uint32_t jl = q * CTT + threadIdx.x, i = w0 + jl;
-      const bool pr = sg[q] && i >= t0 && i < t1 && !(ablate & (1u << 17));
+      for (int q = 0; q < TPW; ++q) go |= wa[q] < CW && dd[q] < WIN_DEPTH;
+      if (!go) break;
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) {
+        const bool act = wa[q] < CW && dd[q] < WIN_DEPTH;
+        const uint32_t a = act ? wa[q] : 0;
+        const uint4 r = lrec[a];
+        if (act) {
+          acc[q] = acc[q] * SIG_M + ((uint64_t)r.y << 32 | r.x);
+          if (kq[q] == KIND_SERVER && ((r.w >> 16) & 3) != KIND_SERVER) {  // (rare) a non-SERVER ancestor of a row
+            if (r.z < n_ep)
+              atomicMax(&ep_ts[r.z], (unsigned long long)((uint64_t)ts[w0 + a] ^ TS_BIAS));
+            else
+              flags |= F_RANGE;
+          }
+          ++dd[q];
+          wa[q] = r.w & 0xFFFF;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+      if (st[q] != S_DONE || !hash_on) {
+        sg[q] = 0;
+        continue;
+      }
+      if (wa[q] != W_NONE) {  // W_OUT: leaves the window or deeper than WIN_DEPTH; W_CYC: CLIENT loop
+        if (wa[q] == W_CYC) flags |= F_CYCLE;
+        st[q] = S_PEND;
+        sg[q] = 0;
+        continue;
+      }
+      const uint32_t d = dd[q];
+      ps[q] = d ? sig_final(acc[q], d - 1, seed) : ROOT_SIG;
+      sg[q] = sig_final(sg[q] * lpow[d] + acc[q], d, seed);
+      if (!(ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
+    }
+    ulonglong2 w01[TPW];  // (sig, parent sig) of the probed slot
+    uint64_t w2[TPW];     // its endpoint/kind word
+    uint64_t pos[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+      const bool pr = st[q] == S_PUT;
       pos[q] = pr ? slot_of(sg[q], ccap) : 0;
       const unsigned long long *en = ctab + 4 * pos[q];
       w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(en) : make_ulonglong2(0, 0);
       w2[q] = pr ? en[2] : 0;
     }
-    __syncthreads();  // every walk is done reading element hashes
     KMZ_STAMP(2);
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const uint32_t jl = q * CTT + threadIdx.x;
-      if (sg[q]) {
-        lsig[jl] = sg[q];
-        ldep[jl] = (uint8_t)dd[q];
-      }
-    }
-    __syncthreads();
-    KMZ_STAMP(3);
     // check what the probes found against (parent sig, endpoint, kind); a
     // chain not found (or not yet published) elects one leader per distinct
     // sig in this workgroup
-    uint32_t hslot[CPW];
+    uint32_t hslot[TPW];
+    uint64_t epon[TPW];
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const uint32_t jl = q * CTT + threadIdx.x;
+    for (int q = 0; q < TPW; ++q) {
       hslot[q] = IMAP + 1;  // not an insert
-      if (!sg[q] || jl >= wn || kf_st(lkf[jl]) != S_PUT) continue;
+      epon[q] = 0;
+      if (st[q] != S_PUT) continue;
       for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
         pos[q] = pos[q] + 1 == ccap ? 0 : pos[q] + 1;
         const unsigned long long *en = ctab + 4 * pos[q];
         w01[q] = *reinterpret_cast<const ulonglong2 *>(en);
         w2[q] = en[2];
       }
-      const uint32_t p = lcp[jl];
-      const uint64_t psig = p == W_NONE ? ROOT_SIG : lsig[p];
-      const uint8_t kj = kf_kind(lkf[jl]);
-      const uint64_t epon = epon_of(lep[jl], kj == KIND_SERVER);
+      epon[q] = epon_of(myep[q], kq[q] == KIND_SERVER);
+      st[q] = S_DONE;
       if (w01[q].x == sg[q] && w01[q].y != 0 && w2[q] != 0) {
-        if (w2[q] != epon || w01[q].y != psig) flags |= F_SIG;
-        lkf[jl] = kf_make(kj, S_DONE);
+        if (w2[q] != epon[q] || w01[q].y != ps[q]) flags |= F_SIG;
         continue;
       }
       uint32_t h = (uint32_t)(sg[q] >> 32) & (IMAP - 1);
@@ -306,8 +322,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       for (uint32_t t = 0; t < 8; ++t) {
         const unsigned long long kk = atomicCAS(&imap_sig[h], 0ull, (unsigned long long)sg[q]);
         if (kk == 0) {  // leader: publish what the followers compare against
-          imap_psig[h] = psig;
-          imap_epon[h] = epon;
+          imap_psig[h] = ps[q];
+          imap_epon[h] = epon[q];
           hslot[q] = h;
           break;
         }
@@ -321,77 +337,69 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     if (more) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
     if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
 #pragma unroll
-      for (int q = 0; q < CPW; ++q) hslot[q] = IMAP + 1;
+      for (int q = 0; q < TPW; ++q) hslot[q] = IMAP + 1;
     __syncthreads();
-    KMZ_STAMP(4);
+    KMZ_STAMP(3);
     // followers compare with their leader; leaders claim the slot the probe
     // ended on (one CAS), publish if they won, and defer a final check to
     // k_chain_settle otherwise.  Keys of a leader's chain are staged whether
     // or not it is new (duplicates are harmless in the edge set), so nothing
     // here waits on another workgroup.
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {
+    for (int q = 0; q < TPW; ++q) {
       if (hslot[q] > IMAP) {
         if (hslot[q] != IMAP + 1) {  // follower
-          const uint32_t jl = q * CTT + threadIdx.x, h = hslot[q] & (IMAP - 1);
-          const uint32_t p = lcp[jl];
-          const uint8_t kj = kf_kind(lkf[jl]);
-          if (imap_psig[h] != (p == W_NONE ? ROOT_SIG : lsig[p]) || imap_epon[h] != epon_of(lep[jl], kj == KIND_SERVER))
-            flags |= F_SIG;
-          lkf[jl] = kf_make(kj, S_DONE);
+          const uint32_t h = hslot[q] & (IMAP - 1);
+          if (imap_psig[h] != ps[q] || imap_epon[h] != epon[q]) flags |= F_SIG;
         }
         continue;
       }
-      const uint32_t jl = q * CTT + threadIdx.x;
-      const uint32_t p = lcp[jl];
-      const uint8_t kj = kf_kind(lkf[jl]);
-      const bool on = kj == KIND_SERVER;
-      const uint64_t psig = p == W_NONE ? ROOT_SIG : lsig[p], epon = epon_of(lep[jl], on);
+      const uint32_t jl = toff + q * CTT + threadIdx.x;
       unsigned long long *en = ctab + 4 * pos[q];
       const unsigned long long cv = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
       const uint32_t d = dd[q];
-      if (on && d && !(ablate & (1u << 19))) {  // stage the chain's keys (knob 19: diagnostic, none)
-        const uint32_t es = lep[jl];
+      if ((epon[q] & 1) && d && !(ablate & (1u << 19))) {  // a row: stage its keys (knob 19: diagnostic, none)
+        const uint32_t es = myep[q];
         const uint32_t base = atomicAdd(&scnt, d);
-        uint32_t a = p;
+        uint32_t a = lrec[jl].w & 0xFFFF;
         for (uint32_t kk = 1; kk <= d; ++kk) {
-          const uint64_t key = edge_key(lep[a], es, kk, kf_kind(lkf[a]) == KIND_SERVER);
+          const uint4 r = lrec[a];
+          const uint64_t key = edge_key(r.z, es, kk, ((r.w >> 16) & 3) == KIND_SERVER);
           if (base + d <= scap)
             stage[(uint64_t)blockIdx.x * scap + base + kk - 1] = key;  // inserted by k_chain_settle
           else
             edge_insert(key, trip, tcap, &flags);  // staging region full: insert here
-          a = lcp[a];
+          a = r.w & 0xFFFF;
         }
       }
       if (cv == 0) {  // won the slot: publish
-        atomicExch(&en[1], (unsigned long long)psig);
-        atomicExch(&en[2], (unsigned long long)epon);
+        atomicExch(&en[1], (unsigned long long)ps[q]);
+        atomicExch(&en[2], (unsigned long long)epon[q]);
         ++fresh_n;
       } else {  // joined an unpublished entry, or lost the slot to another chain
         const uint32_t x = atomicAdd(&dcnt, 1u);
         if (x < dcap) {
           unsigned long long *r = defer + 4 * ((uint64_t)blockIdx.x * dcap + x);
           r[0] = sg[q];
-          r[1] = psig;
-          r[2] = epon;
+          r[1] = ps[q];
+          r[2] = epon[q];
         } else {
           int rr = 0;
-          for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t) rr = chain_put(ctab, ccap, sg[q], psig, epon, &flags);
+          for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t) rr = chain_put(ctab, ccap, sg[q], ps[q], epon[q], &flags);
           fresh_n += rr == 1;
         }
       }
-      lkf[jl] = kf_make(kj, S_DONE);
     }
-    KMZ_STAMP(5);
+    KMZ_STAMP(4);
     // per span of the tile: row counts, pending list, rowpos
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const uint32_t jl = q * CTT + threadIdx.x, i = w0 + jl;
-      if (jl >= wn || i < t0 || i >= t1) continue;
-      const uint8_t b = lkf[jl], kj = kf_kind(b);
+    for (int q = 0; q < TPW; ++q) {
+      const uint32_t jl = toff + q * CTT + threadIdx.x, i = w0 + jl;
+      if (i >= t1) continue;
+      const uint8_t kj = kq[q];
       uint64_t rp = NONE64;
       if (kj != KIND_CLIENT) {
-        const bool pending = kf_st(b) != S_DONE;
+        const bool pending = st[q] == S_PEND;
         if (kj == KIND_SERVER) {
           rp = index_base + i;
           if (!pending) {
@@ -408,7 +416,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       if (rowpos_out) rowpos_out[i] = rp;
     }
     __syncthreads();  // LDS is rewritten by the next tile
-    KMZ_STAMP(6);
+    KMZ_STAMP(5);
   }
   // per workgroup: rows, relations, max depth, new chains
   if (flags) atomicOr(&counters[C_FLAGS], flags);
@@ -435,7 +443,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     defer_n[blockIdx.x] = min(dcnt, dcap);
   }
   if (dbg_t && threadIdx.x == 0)
-    for (int kk = 0; kk < 7; ++kk) atomicAdd(&g_chain_dbg[kk], tacc[kk]);
+    for (int kk = 0; kk < 6; ++kk) atomicAdd(&g_chain_dbg[kk], tacc[kk]);
 #undef KMZ_STAMP
 }
 

@@ -14,11 +14,11 @@ e = Engine(0)
 e.load_synthetic(synth.MESH, synth.SEED, 0, ntr)
 buf = (C.c_ulonglong * 8)()
 e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
-names = ["loop/next", "fill", "hash+probe-issue", "sig-write", "check+elect", "leaders", "stats"]
+names = ["loop/next", "fill", "hash+probe-issue", "check+elect", "leaders", "stats"]
 for k in range(2):
     L.lib().kmz__debug_chain(buf, 1)
     e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
     L.lib().kmz__debug_chain(buf, 1)
-    v = list(buf)[:7]
+    v = list(buf)[:6]
     tot = max(1, sum(v))
     print("run", k, " ".join(f"{nm}={x / tot * 100:.1f}%" for nm, x in zip(names, v)), "total", tot, flush=True)
