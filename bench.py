@@ -137,9 +137,9 @@ def main():
             eng.import_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
             eng.finalize()
             state["keys"] = keys.cpu() if not args.no_fetch else keys
-        elif not args.no_fetch:
-            state["keys"] = eng.triples(sort=False, copy=False)
-        if not args.no_fetch:
+        elif not args.no_fetch:  # the three result sets, one synchronisation
+            state["groups"], state["keys"], state["endpoints"] = eng.fetch()
+        if world > 1 and not args.no_fetch:
             state["groups"] = eng.groups(copy=False)
             state["endpoints"] = eng.endpoints()
 

@@ -161,6 +161,14 @@ int kmz_get_triples(kmz_ctx *ctx, uint64_t *out, uint64_t cap, uint64_t *n_out);
 /* per span: first non-CLIENT ancestor (KMZ_NONE if none) and, for rows, the
  * row's global first-occurrence index (KMZ_NONE if the span is not a row) */
 int kmz_get_span_links(kmz_ctx *ctx, uint32_t *cparent, uint64_t *rowpos, uint64_t cap);
+/* The three result sets of the last run in one call (one stream
+ * synchronisation): what a binding returns from Traces.toRealTimeData()
+ * .toCombinedRealtimeData() (Traces.ts:27-106, RealtimeDataList.ts:22-97) and
+ * Traces.toEndpointDependencies() (Traces.ts:112-211).  Any pointer may be
+ * NULL to skip that set; *n_triples receives the edge-key count either way.
+ * Pinned (page-locked) output buffers copy fastest. */
+int kmz_fetch(kmz_ctx *ctx, kmz_group *groups, uint64_t groups_cap, uint64_t *triples, uint64_t triples_cap,
+              uint64_t *n_triples, kmz_endpoint *endpoints, uint64_t endpoints_cap);
 
 /* ---- multi-GPU partials (traceId-sharded batches) ------------------------ */
 /* Raw group partials: 6 arrays of n_groups u64, in this order:

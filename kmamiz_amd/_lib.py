@@ -113,6 +113,7 @@ SIGNATURES = [
     ("kmz_get_endpoints", C.c_int, [_P, _P, C.c_uint64]),
     ("kmz_get_triples", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("kmz_get_span_links", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("kmz_fetch", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64]),
     ("kmz_group_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_endpoint_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_partials_size", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),

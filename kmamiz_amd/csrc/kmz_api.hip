@@ -61,6 +61,12 @@ struct kmz_ctx {
   uint64_t cap = 0, tcap = 1ull << 16, ccap = 1ull << 20;
   uint64_t sig_seed = 0x4B4D5A5349470001ull;  // K4 ancestry-hash seed (changed after a collision)
   uint32_t dcap = 1024;
+  uint32_t mcap = 1u << 16;   // window-join miss table slots (grown on F_MISS_OVERFLOW)
+  bool table_hint = false;    // the loaded batch failed the uniqueness certificate: go to the table path
+  void *hpin = nullptr;       // pinned host copy of counters + stats64 (one read-back per run)
+  bool hpin_valid = false;    // hpin holds the last completed run's values
+  void *hep = nullptr;        // pinned staging for the endpoint partials
+  size_t hep_bytes = 0;
 
   // last run
   uint32_t ran = 0;
@@ -117,7 +123,9 @@ hipEvent_t ev_get(kmz_ctx *c) {
     return e;
   }
   hipEvent_t e = nullptr;
-  hipEventCreate(&e);
+  // device-scope timing events: no system-scope fence (and no pipeline bubble
+  // for one) between the kernels they bracket
+  hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   return e;
 }
 
@@ -246,6 +254,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
+  if (c->hpin) hipHostFree(c->hpin);
+  if (c->hep) hipHostFree(c->hep);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -289,6 +299,8 @@ int kmz_load(kmz_ctx *c, const kmz_spans *s, const kmz_shapes *sh, int where) {
   c->n = s->n;
   c->index_base = s->index_base;
   c->ran = 0;
+  c->table_hint = false;
+  c->hpin_valid = false;
   if (where == KMZ_MEM_DEVICE) {
     c->sid = s->span_id;
     c->pid = s->parent_id;
@@ -332,7 +344,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
   const uint32_t n = (uint32_t)c->n;
   *ok = false;
   CertPlan pl;
-  if (n == 0 || !cert_plan(n, &pl) || (c->ablate & 32)) return KMZ_OK;
+  if (n == 0 || !cert_plan(n, &pl) || c->table_hint || (c->ablate & 32)) return KMZ_OK;
   const size_t nsub = (size_t)cert_bins() << pl.B2;
   if (ensure(c, c->dp, (size_t)(n + 1) * 4) || ensure(c, c->cpool1, cert_pool1_words(n) * 8) ||
       ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) ||
@@ -341,6 +353,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
   HIPCHK(c, hipMemsetAsync(cur2, 0, nsub * 4, c->stream));
+  if (ensure(c, c->mkey, (size_t)c->mcap * 8) || ensure(c, c->mval, (size_t)c->mcap * 4)) return KMZ_E_HIP;
   {
     Timed t(c, KMZ_K_JOIN);
     launch_join(c->stream, c->sid, c->pid, c->kind, n, P<uint32_t>(c->cparent), P<uint32_t>(c->dp),
@@ -355,24 +368,17 @@ static int run_join(kmz_ctx *c, bool *ok) {
     Timed t(c, KMZ_K_CHECK);
     launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
   }
-  unsigned int h[C_COUNT];
-  HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (h[C_CERT]) {
-    HIPCHK(c, hipMemsetAsync(cnt + C_MISS, 0, 3 * 4, c->stream));
-    return KMZ_OK;
-  }
-  if (h[C_MISS] || h[C_PEND]) {
+  {
+    // parents outside the window / chains leaving it: these kernels read the
+    // join's counters and return at once when there is nothing to do, so the
+    // host never waits here.  The certificate is read after the run: if an id
+    // repeats, kmz_run discards the run and takes the table path.
     Timed t(c, KMZ_K_RESOLVE);
-    if (h[C_MISS]) {
-      uint32_t mcap = (uint32_t)std::min<uint64_t>(2ull * h[C_MISS] + 64, 0xFFFFFFF0ull);
-      if (ensure(c, c->mkey, (size_t)mcap * 8) || ensure(c, c->mval, (size_t)mcap * 4)) return KMZ_E_HIP;
-      HIPCHK(c, hipMemsetAsync(c->mkey.p, 0, (size_t)mcap * 8, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->mval.p, 0xFF, (size_t)mcap * 4, c->stream));
-      launch_miss(c->stream, c->sid, c->pid, P<uint32_t>(c->dp), n, P<unsigned long long>(c->mkey),
-                  P<uint32_t>(c->mval), mcap);
-    }
-    if (h[C_PEND]) launch_pend(c->stream, c->kind, P<uint32_t>(c->dp), n, P<uint32_t>(c->cparent));
+    HIPCHK(c, hipMemsetAsync(c->mkey.p, 0, (size_t)c->mcap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->mval.p, 0xFF, (size_t)c->mcap * 4, c->stream));  // ids not in the batch: NONE
+    launch_miss(c->stream, c->sid, c->pid, P<uint32_t>(c->dp), n, P<unsigned long long>(c->mkey),
+                P<uint32_t>(c->mval), c->mcap, cnt);
+    launch_pend(c->stream, c->kind, P<uint32_t>(c->dp), n, P<uint32_t>(c->cparent), cnt);
   }
   *ok = true;
   return KMZ_OK;
@@ -507,7 +513,7 @@ static int run_deps(kmz_ctx *c, bool links) {
     {  // ancestries that left their window: one pass, sized on the device (no host round trip)
       Timed t(c, KMZ_K_PEND);
       launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent),
-                        P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
+                        n, P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
                         P<unsigned long long>(c->trip), c->tcap, epp, cnt, st);
     }
     {
@@ -574,6 +580,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
   if (smode == (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG)) return fail(c, KMZ_E_ARG, "choose one stats identity per run");
   const bool links = (flags & KMZ_RUN_SPAN_LINKS) != 0;
   hipSetDevice(c->device);
+  c->hpin_valid = false;
   for (int attempt = 0; attempt < 8; ++attempt) {
     c->sstats = false;
     c->chain_ran = false;
@@ -582,18 +589,30 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     int r;
     if (smode && (r = run_stats(c, smode))) return r;
     if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, links))) return r;
-    unsigned int h[C_COUNT];
-    HIPCHK(c, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    // one read-back per run: counters + statistics into pinned host memory
+    if (!c->hpin && hipHostMalloc(&c->hpin, C_COUNT * 4 + S_COUNT * 8, hipHostMallocDefault) != hipSuccess) {
+      c->hpin = nullptr;
+      return fail(c, KMZ_E_HIP, "hipHostMalloc (run read-back)");
+    }
+    unsigned int *h = reinterpret_cast<unsigned int *>(c->hpin);
+    unsigned long long *s64 = reinterpret_cast<unsigned long long *>(h + C_COUNT);
+    HIPCHK(c, hipMemcpyAsync(h, c->counters.p, C_COUNT * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(s64, c->stats64.p, S_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
-    {  // hash-table load factors: grow for the next run (correctness never
-       // depends on it: an overfull probe raises the overflow flags below)
-      unsigned long long s64[S_COUNT];
-      HIPCHK(c, hipMemcpy(s64, c->stats64.p, sizeof(s64), hipMemcpyDeviceToHost));
-      if (c->chain_ran && s64[S_CHAINS] * 2 > c->ccap && c->ccap < (1ull << 31)) c->ccap *= 2;
-      if ((flags & KMZ_RUN_DEPS) && s64[S_TRIP_OUT] * 2 > c->tcap) c->tcap *= 2;
+    if ((flags & KMZ_RUN_DEPS) && (c->path & 1) && h[C_CERT]) {  // a repeated span id: the table path, same run
+      c->table_hint = true;
+      continue;
     }
+    // hash-table load factors: grow for the next run (correctness never
+    // depends on it: an overfull probe raises the overflow flags below)
+    if (c->chain_ran && s64[S_CHAINS] * 2 > c->ccap && c->ccap < (1ull << 31)) c->ccap *= 2;
+    if ((flags & KMZ_RUN_DEPS) && s64[S_TRIP_OUT] * 2 > c->tcap) c->tcap *= 2;
     bool retry = false;
+    if (h[C_FLAGS] & F_MISS_OVERFLOW) {
+      c->mcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * c->mcap, 2ull * h[C_MISS] + 64), 0xFFFFFFF0ull);
+      retry = true;
+    }
     if (h[C_FLAGS] & F_TRIPLE_OVERFLOW) {
       c->tcap *= 4;
       retry = true;
@@ -616,6 +635,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
       if (e) return e;
       c->ran = flags;
       c->links = links;
+      c->hpin_valid = true;
       return KMZ_OK;
     }
   }
@@ -624,11 +644,18 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
 
 int kmz_get_info(kmz_ctx *c, kmz_info *out) {
   if (!c || !out) return KMZ_E_ARG;
-  unsigned int h[C_COUNT];
-  unsigned long long s[S_COUNT];
-  HIPCHK(c, hipMemcpyAsync(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  unsigned int hb[C_COUNT];
+  unsigned long long sb[S_COUNT];
+  const unsigned int *h = hb;
+  const unsigned long long *s = sb;
+  if (c->hpin_valid) {  // the last run's read-back (nothing has run since)
+    h = reinterpret_cast<const unsigned int *>(c->hpin);
+    s = reinterpret_cast<const unsigned long long *>(h + C_COUNT);
+  } else {
+    HIPCHK(c, hipMemcpyAsync(hb, c->counters.p, sizeof(hb), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(sb, c->stats64.p, sizeof(sb), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   memset(out, 0, sizeof(*out));
   out->n_spans = c->n;
   out->n_server = s[S_SERVER];
@@ -653,35 +680,70 @@ int kmz_get_groups(kmz_ctx *c, kmz_group *out, uint64_t cap) {
 }
 
 int kmz_get_endpoints(kmz_ctx *c, kmz_endpoint *out, uint64_t cap) {
-  if (!c) return KMZ_E_ARG;
-  if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
-  if (cap < c->n_dep) return fail(c, KMZ_E_ARG, "output too small");
-  std::vector<uint64_t> h((size_t)c->n_dep * 2 + 1);
-  if (c->n_dep)
-    HIPCHK(c, hipMemcpyAsync(h.data(), c->epp.p, (size_t)c->n_dep * 16, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  for (uint32_t e = 0; e < c->n_dep; ++e) {
-    uint64_t tsx = h[e], f = h[c->n_dep + e];
-    out[e].last_ts = tsx == 0 ? INT64_MIN : (int64_t)(tsx ^ TS_BIAS);
-    out[e].has_row = f != ~0ull;
-    out[e].first_row = f == ~0ull ? ~0ull : (f >> 1);
-    out[e].external = f == ~0ull ? 0u : (uint32_t)((f & 1) == 0);
-  }
-  return KMZ_OK;
+  return kmz_fetch(c, nullptr, 0, nullptr, 0, nullptr, out, cap);
 }
 
 int kmz_get_triples(kmz_ctx *c, uint64_t *out, uint64_t cap, uint64_t *n_out) {
   if (!c || !n_out) return KMZ_E_ARG;
-  if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
-  unsigned long long s[S_COUNT];
-  HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  *n_out = s[S_TRIP_OUT];
-  if (!out) return KMZ_OK;
-  if (cap < s[S_TRIP_OUT]) return fail(c, KMZ_E_ARG, "output too small");
-  if (s[S_TRIP_OUT])
-    HIPCHK(c, hipMemcpyAsync(out, c->trip_out.p, s[S_TRIP_OUT] * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return kmz_fetch(c, nullptr, 0, out, cap, n_out, nullptr, 0);
+}
+
+int kmz_fetch(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint64_t tcap, uint64_t *n_trip,
+              kmz_endpoint *eps, uint64_t ecap) {
+  if (!c) return KMZ_E_ARG;
+  const bool want_deps = trip || n_trip || eps;
+  if (groups && !(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
+  if (want_deps && !(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+  if (groups && gcap < c->G) return fail(c, KMZ_E_ARG, "output too small");
+  if (eps && ecap < c->n_dep) return fail(c, KMZ_E_ARG, "output too small");
+  uint64_t nt = 0;
+  if (want_deps) {
+    if (c->hpin_valid) {
+      nt = reinterpret_cast<const unsigned long long *>(reinterpret_cast<const unsigned int *>(c->hpin) + C_COUNT)[S_TRIP_OUT];
+    } else {
+      unsigned long long s[S_COUNT];
+      HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      nt = s[S_TRIP_OUT];
+    }
+    if (n_trip) *n_trip = nt;
+    if (trip && tcap < nt) return fail(c, KMZ_E_ARG, "output too small");
+  }
+  bool any = false;
+  if (groups && c->G) {
+    HIPCHK(c, hipMemcpyAsync(groups, c->grp_final.p, (size_t)c->G * sizeof(kmz_group), hipMemcpyDeviceToHost, c->stream));
+    any = true;
+  }
+  if (trip && nt) {
+    HIPCHK(c, hipMemcpyAsync(trip, c->trip_out.p, nt * 8, hipMemcpyDeviceToHost, c->stream));
+    any = true;
+  }
+  const size_t eb = (size_t)c->n_dep * 16;
+  if (eps && c->n_dep) {
+    if (c->hep_bytes < eb) {
+      if (c->hep) hipHostFree(c->hep);
+      c->hep = nullptr;
+      c->hep_bytes = 0;
+      if (hipHostMalloc(&c->hep, eb, hipHostMallocDefault) != hipSuccess) {
+        c->hep = nullptr;
+        return fail(c, KMZ_E_HIP, "hipHostMalloc (endpoint staging)");
+      }
+      c->hep_bytes = eb;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->hep, c->epp.p, eb, hipMemcpyDeviceToHost, c->stream));
+    any = true;
+  }
+  if (any) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (eps) {
+    const uint64_t *h = reinterpret_cast<const uint64_t *>(c->hep);
+    for (uint32_t e = 0; e < c->n_dep; ++e) {
+      const uint64_t tsx = h[e], f = h[c->n_dep + e];
+      eps[e].last_ts = tsx == 0 ? INT64_MIN : (int64_t)(tsx ^ TS_BIAS);
+      eps[e].has_row = f != ~0ull;
+      eps[e].first_row = f == ~0ull ? ~0ull : (f >> 1);
+      eps[e].external = f == ~0ull ? 0u : (uint32_t)((f & 1) == 0);
+    }
+  }
   return KMZ_OK;
 }
 
@@ -786,6 +848,10 @@ void kmz_host_free(void *p) {
 int kmz_set_profiling(kmz_ctx *c, int on) {
   if (!c) return KMZ_E_ARG;
   c->prof = on != 0;
+  // create the timing events now, not inside the first timed run
+  std::vector<hipEvent_t> tmp;
+  while (c->prof && c->pool.size() + tmp.size() < 4 * KMZ_K_COUNT) tmp.push_back(ev_get(c));
+  for (auto e : tmp) c->pool.push_back(e);
   return KMZ_OK;
 }
 
@@ -895,6 +961,8 @@ int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t 
   c->ts = o.timestamp;
   c->loaded = true;
   c->ran = 0;
+  c->table_hint = false;
+  c->hpin_valid = false;
   if (n_out) *n_out = n;
   return KMZ_OK;
 }

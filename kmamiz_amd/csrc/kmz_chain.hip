@@ -483,7 +483,7 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
                                                      const uint8_t *__restrict__ kind,
                                                      const uint32_t *__restrict__ shape,
                                                      const int64_t *__restrict__ ts,
-                                                     const uint32_t *__restrict__ cparent,
+                                                     const uint32_t *__restrict__ cparent, uint32_t n,
                                                      const uint32_t *__restrict__ dep_ep, uint32_t n_shapes,
                                                      uint32_t n_ep, uint64_t seed,
                                                      unsigned long long *__restrict__ ctab, uint64_t ccap,
@@ -506,7 +506,13 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     bool bad = false;
     const uint32_t a = cparent[i];
     for (uint32_t cur = a; cur != NONE; cur = cparent[cur]) {
-      if (cur == CYC || ++d > MAX_DEPTH) {
+      if (cur >= n) {  // CYC (a CLIENT loop); never another value (k_pend/k_resolve leave indices < n)
+        if (cur == CYC) flags |= F_CYCLE;
+        else flags |= F_RANGE;
+        bad = true;
+        break;
+      }
+      if (++d > MAX_DEPTH) {
         flags |= F_CYCLE;
         bad = true;
         break;
@@ -580,11 +586,12 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
 }
 
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,
-                       const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, const uint32_t *dep_ep,
+                       const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, uint32_t n,
+                       const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
                        unsigned long long *stats64) {
-  hipLaunchKernelGGL(k4_chain_pend, dim3(1024), dim3(256), 0, s, plist, pcap, kind, shape, ts, cparent, dep_ep,
+  hipLaunchKernelGGL(k4_chain_pend, dim3(1024), dim3(256), 0, s, plist, pcap, kind, shape, ts, cparent, n, dep_ep,
                      n_shapes, n_ep, seed, reinterpret_cast<unsigned long long *>(ctab), ccap, trip, tcap, ep_ts,
                      counters, stats64);
 }

@@ -479,8 +479,25 @@ __global__ void __launch_bounds__(1024) k_cert_check(const unsigned long long *_
 // ---- MISS parents: semi-join of the missing parent ids against all span ids
 __device__ __forceinline__ uint64_t mslot(uint64_t key, uint32_t mcap) { return slot_of(key ^ 0x7F4A7C159E3779B9ull, mcap); }
 
+// The MISS/PEND kernels are launched on every join run without a host round
+// trip; they read the join's counters first and return when there is nothing
+// to do (or when the miss table is too small: the host grows it and runs
+// again).  They run even when the certificate failed, so that cparent is
+// always well formed (indices < n, NONE or CYC) for the kernels after them.
+__device__ __forceinline__ bool miss_skip(const unsigned int *counters, uint32_t mcap) {
+  const uint32_t m = counters[C_MISS];
+  if (m == 0) return true;
+  if ((uint64_t)m * 2 > mcap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(const_cast<unsigned int *>(counters) + C_FLAGS, F_MISS_OVERFLOW);
+    return true;
+  }
+  return false;
+}
+
 __global__ void __launch_bounds__(256) k_miss_insert(const uint64_t *__restrict__ pid, const uint32_t *__restrict__ dp,
-                                                     uint32_t n, unsigned long long *__restrict__ mkey, uint32_t mcap) {
+                                                     uint32_t n, unsigned long long *__restrict__ mkey, uint32_t mcap,
+                                                     const unsigned int *counters) {
+  if (miss_skip(counters, mcap)) return;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     if (dp[i] != MISSV) continue;
     const uint64_t key = pid[i];
@@ -495,7 +512,9 @@ __global__ void __launch_bounds__(256) k_miss_insert(const uint64_t *__restrict_
 
 __global__ void __launch_bounds__(256) k_miss_probe(const uint64_t *__restrict__ sid, uint32_t n,
                                                     const unsigned long long *__restrict__ mkey,
-                                                    uint32_t *__restrict__ mval, uint32_t mcap) {
+                                                    uint32_t *__restrict__ mval, uint32_t mcap,
+                                                    const unsigned int *counters) {
+  if (miss_skip(counters, mcap)) return;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
     const uint64_t key = sid[j];
     if (key == 0) continue;
@@ -514,7 +533,9 @@ __global__ void __launch_bounds__(256) k_miss_probe(const uint64_t *__restrict__
 
 __global__ void __launch_bounds__(256) k_miss_fix(const uint64_t *__restrict__ pid, uint32_t *__restrict__ dp,
                                                   uint32_t n, const unsigned long long *__restrict__ mkey,
-                                                  const uint32_t *__restrict__ mval, uint32_t mcap) {
+                                                  const uint32_t *__restrict__ mval, uint32_t mcap,
+                                                  const unsigned int *counters) {
+  if (miss_skip(counters, mcap)) return;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     if (dp[i] != MISSV) continue;
     const uint64_t key = pid[i];
@@ -534,7 +555,9 @@ __global__ void __launch_bounds__(256) k_miss_fix(const uint64_t *__restrict__ p
 
 // PEND chains over the global dp array
 __global__ void __launch_bounds__(256) k_pend(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ dp,
-                                              uint32_t n, uint32_t *__restrict__ cparent) {
+                                              uint32_t n, uint32_t *__restrict__ cparent,
+                                              const unsigned int *counters) {
+  if (counters[C_PEND] == 0) return;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     if (cparent[i] != PEND) continue;
     uint32_t j = dp[i], hops = 0, cp;
@@ -596,18 +619,19 @@ void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsi
 }
 
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,
-                 unsigned long long *mkey, uint32_t *mval, uint32_t mcap) {
+                 unsigned long long *mkey, uint32_t *mval, uint32_t mcap, const unsigned int *counters) {
   if (!n) return;
   const uint32_t g = std::min<uint32_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_miss_insert, dim3(g), dim3(256), 0, s, pid, dp, n, mkey, mcap);
-  hipLaunchKernelGGL(k_miss_probe, dim3(g), dim3(256), 0, s, sid, n, mkey, mval, mcap);
-  hipLaunchKernelGGL(k_miss_fix, dim3(g), dim3(256), 0, s, pid, dp, n, mkey, mval, mcap);
+  hipLaunchKernelGGL(k_miss_insert, dim3(g), dim3(256), 0, s, pid, dp, n, mkey, mcap, counters);
+  hipLaunchKernelGGL(k_miss_probe, dim3(g), dim3(256), 0, s, sid, n, mkey, mval, mcap, counters);
+  hipLaunchKernelGGL(k_miss_fix, dim3(g), dim3(256), 0, s, pid, dp, n, mkey, mval, mcap, counters);
 }
 
-void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent) {
+void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent,
+                 const unsigned int *counters) {
   if (!n) return;
   const uint32_t g = std::min<uint32_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_pend, dim3(g), dim3(256), 0, s, kind, dp, n, cparent);
+  hipLaunchKernelGGL(k_pend, dim3(g), dim3(256), 0, s, kind, dp, n, cparent, counters);
 }
 
 }  // namespace kmz

@@ -82,7 +82,8 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint32_t dcap, uint32_t *defer_n, uint32_t ablate = 0);
 uint32_t chain_grid(uint32_t n);
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,
-                       const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, const uint32_t *dep_ep,
+                       const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, uint32_t n,
+                       const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
                        unsigned long long *stats64);
@@ -110,7 +111,8 @@ void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
                        const unsigned int *cur2, unsigned int *counters);
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,
-                 unsigned long long *mkey, uint32_t *mval, uint32_t mcap);
-void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent);
+                 unsigned long long *mkey, uint32_t *mval, uint32_t mcap, const unsigned int *counters);
+void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent,
+                 const unsigned int *counters);
 
 }  // namespace kmz

@@ -183,7 +183,7 @@ class Engine:
 
     def triples(self, sort: bool = True, copy: bool = True) -> np.ndarray:
         n = C.c_uint64()
-        L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, None, 0, C.byref(n)))
+        L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, None, 0, C.byref(n)))  # no sync after a run
         out = self._pinned_array("triples", n.value, np.uint64)
         L.check(self.ctx, self._lib.kmz_get_triples(self.ctx, L.ptr(out), n.value, C.byref(n)))
         if copy or sort:
@@ -191,6 +191,22 @@ class Engine:
         if sort:
             out.sort()
         return out
+
+    def fetch(self, groups: bool = True, deps: bool = True):
+        """All result sets of the last run with one stream synchronisation
+        (kmz_fetch).  Returns (groups, triples, endpoints); groups and triples
+        are views of reused pinned buffers (valid until the next fetch),
+        triples unordered."""
+        info = self.info()  # the run's cached read-back: no device round trip
+        g = self._pinned_array("groups", info["n_groups"], L.GROUP_DTYPE) if groups else None
+        t = self._pinned_array("triples", info["n_triples"], np.uint64) if deps else None
+        e = np.zeros(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE) if deps else None
+        n = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_fetch(self.ctx, L.ptr(g) if groups else None, len(g) if groups else 0,
+                                              L.ptr(t) if deps else None, len(t) if deps else 0,
+                                              C.byref(n) if deps else None, L.ptr(e) if deps else None,
+                                              len(e) if deps else 0))
+        return g, t, e
 
     def span_links(self):
         cp = np.zeros(self.n, dtype=np.uint32)

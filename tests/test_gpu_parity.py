@@ -297,6 +297,11 @@ def test_full_size_properties(engine, config, ntr):
     edges = set(zip(a.tolist(), d.tolist(), dist.tolist(), on.tolist()))
     assert edges == {(0, 1, 1, True), (0, 2, 1, True), (0, 3, 1, True), (0, 4, 1, True), (3, 5, 1, True),
                      (4, 5, 1, True), (0, 5, 2, True)}
+    # kmz_fetch (one synchronisation) returns the same three result sets
+    g2, k2, e2 = engine.fetch()
+    assert g2.tobytes() == g1.tobytes()
+    assert np.array_equal(np.sort(k2), k1)
+    assert e2.tobytes() == e1.tobytes()
 
 
 def test_hot_descendant_falls_back_to_global_edge_set(engine):

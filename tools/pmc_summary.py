@@ -1,17 +1,17 @@
-"""Summarise rocprofv3 --pmc counter CSVs: mean counter value per kernel."""
-import csv
+"""Summarise a rocprofv3 --pmc sqlite result: per kernel, counter sums per dispatch (averaged)."""
+import collections
+import sqlite3
 import sys
-from collections import defaultdict
 
-acc = defaultdict(lambda: defaultdict(list))
-for path in sys.argv[1:]:
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            name = r["Kernel_Name"].split("(")[0][:48]
-            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            acc[name]["_ns"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-for k, d in sorted(acc.items()):
-    if "copyBuffer" in k or "fill" in k.lower() and "synth" not in k:
-        continue
-    row = {c: sum(v) / len(v) for c, v in d.items()}
-    print(k, {c: (f"{x:.4g}") for c, x in sorted(row.items())})
+c = sqlite3.connect(sys.argv[1])
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for name, ctr, disp, val in c.execute("select kernel_name, counter_name, dispatch_id, value from counters_collection"):
+    acc[name.split("(")[0]][ctr].append((disp, val))
+for k, d in acc.items():
+    print(k)
+    for ctr, v in sorted(d.items()):
+        per = collections.defaultdict(float)
+        for disp, x in v:
+            per[disp] += x
+        vals = list(per.values())
+        print(f"  {ctr:28s} {sum(vals) / len(vals):16.4g}  (dispatches {len(vals)})")
