@@ -392,85 +392,46 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
 }
 
-// pass 3: exact duplicate check of one sub-bin.  Two-choice buckets of eight
-// 64-bit hashed ids (+ a small stash); after all inserts, every id counts its
-// equals in its two buckets and the stash (an id that occurs twice finds two).
-// No CAS loops.
-constexpr uint32_t CB = CERT_SET / 8, CSTASH = 64;
-__device__ __forceinline__ uint32_t count_eq(const ulonglong2 *b, uint64_t h) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const ulonglong2 v = b[t];
-    c += (v.x == h) + (v.y == h);
-  }
-  return c;
-}
-
-__global__ void __launch_bounds__(1024) k_cert_check(const unsigned long long *__restrict__ pool, uint32_t cap,
-                                                    const unsigned int *__restrict__ cur, uint32_t cur_stride,
-                                                    unsigned int *__restrict__ counters) {
-  __shared__ ulonglong2 set2[CB * 4];  // bucket b = set2[4b .. 4b+3]
-  __shared__ uint32_t cnt[CB];
-  __shared__ uint64_t stash[CSTASH];
-  __shared__ uint32_t nstash;
+// pass 3: exact duplicate check of one sub-bin: every hashed id is inserted
+// into an LDS open-addressing set with one 64-bit compare-and-swap per probe;
+// a CAS that returns the id itself is a repeated id.  cert_plan keeps every
+// sub-bin at or below 3/4 of the set (typically ~0.4), so probing ends.
+constexpr uint32_t CSLOTS = CERT_SET;
+constexpr int CCT = 512;  // threads per pass-3 workgroup (two per CU with the 64 KB set)
+__global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__restrict__ pool, uint32_t cap,
+                                                   const unsigned int *__restrict__ cur, uint32_t cur_stride,
+                                                   unsigned int *__restrict__ counters) {
+  __shared__ ulonglong2 set2[CSLOTS / 2];
   const uint32_t sb = blockIdx.x;
   const uint32_t m = min(cur[(uint64_t)sb * cur_stride], cap);
   if (m == 0) return;
-  for (uint32_t k = threadIdx.x; k < CB * 4; k += blockDim.x) set2[k] = make_ulonglong2(0, 0);
-  for (uint32_t k = threadIdx.x; k < CB; k += blockDim.x) cnt[k] = 0;
-  if (threadIdx.x == 0) nstash = 0;
-  __syncthreads();
-  unsigned long long *set = reinterpret_cast<unsigned long long *>(set2);
   const unsigned long long *src = pool + (uint64_t)sb * cap;
-  bool bad = false;
-  for (uint32_t e0 = 0; e0 < m; e0 += 8 * 1024) {
+  unsigned long long *set = reinterpret_cast<unsigned long long *>(set2);
+  bool dup = false;
+  for (uint32_t e0 = 0; e0 < m; e0 += 8 * CCT) {
     uint64_t h[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint32_t e = e0 + q * 1024 + threadIdx.x;
+    for (int q = 0; q < 8; ++q) {  // (the first batch is in flight while the set is cleared)
+      const uint32_t e = e0 + q * CCT + threadIdx.x;
       h[q] = e < m ? src[e] : 0;
+    }
+    if (e0 == 0) {
+      for (uint32_t k = threadIdx.x; k < CSLOTS / 2; k += CCT) set2[k] = make_ulonglong2(0, 0);
+      __syncthreads();
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       if (h[q] == 0) continue;  // mix64(0) == 0: span id 0, reported as F_ZERO_ID
-      const uint32_t b1 = (uint32_t)h[q] & (CB - 1), b2 = (uint32_t)(h[q] >> 10) & (CB - 1);
-      uint32_t b = cnt[b1] <= cnt[b2] ? b1 : b2;
-      uint32_t slot = atomicAdd(&cnt[b], 1u);
-      if (slot >= 8) {
-        b = b ^ b1 ^ b2;
-        slot = atomicAdd(&cnt[b], 1u);
+      uint32_t pos = (uint32_t)h[q] & (CSLOTS - 1);
+      for (uint32_t z = 0; z < CSLOTS; ++z) {
+        const unsigned long long c = atomicCAS(&set[pos], 0ull, (unsigned long long)h[q]);
+        if (c == 0) break;
+        if (c == h[q]) {
+          dup = true;
+          break;
+        }
+        pos = (pos + 1) & (CSLOTS - 1);
       }
-      if (slot < 8) {
-        set[8 * b + slot] = h[q];
-      } else {
-        const uint32_t t = atomicAdd(&nstash, 1u);
-        if (t < CSTASH)
-          stash[t] = h[q];
-        else
-          bad = true;  // no verdict for this sub-bin
-      }
-    }
-  }
-  if (bad) atomicOr(&counters[C_CERT], CERT_OVF);
-  __syncthreads();
-  const uint32_t ns = min(nstash, CSTASH);
-  bool dup = false;
-  for (uint32_t e0 = 0; e0 < m; e0 += 8 * 1024) {
-    uint64_t h[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint32_t e = e0 + q * 1024 + threadIdx.x;
-      h[q] = e < m ? src[e] : 0;
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if (h[q] == 0) continue;
-      const uint32_t b1 = (uint32_t)h[q] & (CB - 1), b2 = (uint32_t)(h[q] >> 10) & (CB - 1);
-      uint32_t c = count_eq(&set2[4 * b1], h[q]);
-      if (b2 != b1) c += count_eq(&set2[4 * b2], h[q]);
-      for (uint32_t t = 0; t < ns; ++t) c += stash[t] == h[q];
-      dup |= c > 1;
     }
   }
   if (dup) atomicOr(&counters[C_CERT], CERT_DUP);
@@ -615,7 +576,7 @@ void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
                        const unsigned int *cur2, unsigned int *counters) {
   if (!n) return;
-  hipLaunchKernelGGL(k_cert_check, dim3(CERT_BINS << pl.B2), dim3(1024), 0, s, pool2, pl.cap2, cur2, 1u, counters);
+  hipLaunchKernelGGL(k_cert_check, dim3(CERT_BINS << pl.B2), dim3(CCT), 0, s, pool2, pl.cap2, cur2, 1u, counters);
 }
 
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,

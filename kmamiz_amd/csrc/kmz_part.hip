@@ -57,18 +57,18 @@ __device__ __forceinline__ uint32_t block_excl_scan_pairs(const uint32_t *cnt, u
 // ===========================================================================
 // K3P
 // ===========================================================================
-struct __align__(8) Rec {
+// one SERVER span's record: 16 bytes
+struct __align__(16) Rec {
   uint64_t tsx;  // timestamp ^ 2^63
-  uint32_t i;    // local span index
   uint32_t d;    // duration (us)
-  uint32_t kl;   // group within the partition
-  uint32_t pad;
+  uint32_t w;    // group within the partition (10 bits) | span index within the tile << 10 (11 bits)
 };
 
 constexpr uint32_t K3T = 2048;     // spans per tile
 constexpr uint32_t K3R = 1024;     // groups per partition
 constexpr uint32_t K3PMAX = 1024;  // partitions (G <= 1M)
 constexpr int K3PT = 512;          // producer threads
+static_assert(K3R <= 1024 && K3T <= 2048, "record word: 10 group bits, 11 index bits");
 
 __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
                                                    const uint16_t *__restrict__ status, const uint32_t *__restrict__ dur,
@@ -82,34 +82,46 @@ __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ k
   __shared__ uint32_t wave_tot[K3PT / 64 + 1];
   __shared__ Rec stage[K3T];
   const uint32_t tile = blockIdx.x, t0 = tile * K3T;
-  for (uint32_t p = threadIdx.x; p < P; p += K3PT) cnt[p] = 0;
-  __syncthreads();
   constexpr int PER = K3T / K3PT;
-  uint32_t pp[PER], rr[PER];
-  Rec rec[PER];
-  uint32_t servers = 0;
+  // every column of the tile in flight at once (clamped, unconditional loads)
+  uint8_t kd[PER];
+  uint32_t sh[PER], du[PER];
+  uint16_t st[PER];
+  int64_t tv[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    uint32_t i = t0 + k * K3PT + threadIdx.x;
+    const uint32_t i = min(t0 + k * K3PT + threadIdx.x, n - 1);
+    kd[k] = kind[i];
+    sh[k] = shape[i];
+    st[k] = status[i];
+    du[k] = dur[i];
+    tv[k] = ts[i];
+  }
+  for (uint32_t p = threadIdx.x; p < P; p += K3PT) cnt[p] = 0;
+  __syncthreads();
+  uint32_t pp[PER], rr[PER];
+  Rec rec[PER];
+  uint32_t servers = 0, flags = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t li = k * K3PT + threadIdx.x;
     pp[k] = NONE;
-    if (i < n && kind[i] == KIND_SERVER) {
+    if (t0 + li < n && kd[k] == KIND_SERVER) {
       ++servers;
-      uint32_t sh = shape[i], st = status[i];
-      uint32_t ep = sh < n_shapes ? (ep_of_shape ? ep_of_shape[sh] : sh) : NONE;  // null map: group by shape
-      if (ep >= n_ep || st >= n_status) {
-        atomicOr(&counters[C_FLAGS], F_RANGE);
+      const uint32_t ep = sh[k] < n_shapes ? (ep_of_shape ? ep_of_shape[sh[k]] : sh[k]) : NONE;  // null map: by shape
+      if (ep >= n_ep || st[k] >= n_status) {
+        flags |= F_RANGE;
         continue;
       }
-      uint32_t g = ep * n_status + st;
+      const uint32_t g = ep * n_status + st[k];
       pp[k] = g / K3R;
-      rec[k].kl = g % K3R;
-      rec[k].d = dur[i];
-      rec[k].i = i;
-      rec[k].tsx = (uint64_t)ts[i] ^ TS_BIAS;
-      rec[k].pad = 0;
+      rec[k].tsx = (uint64_t)tv[k] ^ TS_BIAS;
+      rec[k].d = du[k];
+      rec[k].w = (g % K3R) | (li << 10);
       rr[k] = atomicAdd(&cnt[pp[k]], 1u);
     }
   }
+  if (flags) atomicOr(&counters[C_FLAGS], flags);
   __syncthreads();
   uint32_t total = block_excl_scan_pairs<K3PT>(cnt, off, P, wave_tot);
   for (uint32_t p = threadIdx.x; p < P; p += K3PT) dir[(uint64_t)p * ntiles + tile] = (off[p] << 16) | cnt[p];
@@ -118,9 +130,9 @@ __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ k
     if (pp[k] != NONE) stage[off[pp[k]] + rr[k]] = rec[k];
   __syncthreads();
   // coalesced copy of the partition-sorted tile into its region
-  const uint64_t *src = reinterpret_cast<const uint64_t *>(stage);
-  uint64_t *dst = reinterpret_cast<uint64_t *>(pool + (uint64_t)tile * K3T);
-  for (uint32_t w = threadIdx.x; w < total * 3; w += K3PT) dst[w] = src[w];
+  const uint4 *src = reinterpret_cast<const uint4 *>(stage);
+  uint4 *dst = reinterpret_cast<uint4 *>(pool + (uint64_t)tile * K3T);
+  for (uint32_t w = threadIdx.x; w < total; w += K3PT) dst[w] = src[w];
   // realtime-row count: per tile, summed later (no same-address atomics)
   for (int o = 32; o > 0; o >>= 1) servers += __shfl_xor(servers, o, 64);
   if ((threadIdx.x & 63) == 0) wave_tot[threadIdx.x >> 6] = servers;
@@ -164,36 +176,53 @@ __global__ void __launch_bounds__(1024) k_tile_sum(const uint32_t *__restrict__ 
 
 static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32_t>(64, (ntiles + 1023) / 1024 + 0); }
 
-// slice s of partition p: tiles s, s+S, ...  -> part[(s*6 + f) * G + g]
-__global__ void __launch_bounds__(256) k3_reduce(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
-                                                 uint32_t ntiles, uint32_t S, uint32_t G, uint64_t index_base,
-                                                 unsigned long long *__restrict__ part) {
+// slice s of partition p: tiles s, s+S, ...  -> part[(s*6 + f) * G + g].
+// Each wave takes four of the slice's tiles at a time and spreads the
+// concatenation of their record runs over its lanes (coalesced 16-byte reads).
+constexpr int K3RT = 256;
+__global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
+                                                  uint32_t ntiles, uint32_t S, uint32_t G, uint64_t index_base,
+                                                  unsigned long long *__restrict__ part) {
   __shared__ unsigned long long a_cnt[K3R], a_s1[K3R], a_s2a[K3R], a_s2b[K3R], a_tsx[K3R], a_fst[K3R];
   const uint32_t s = blockIdx.x, p = blockIdx.y;
-  for (uint32_t k = threadIdx.x; k < K3R; k += blockDim.x) {
+  for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
     a_cnt[k] = a_s1[k] = a_s2a[k] = a_s2b[k] = a_tsx[k] = 0;
     a_fst[k] = ~0ull;
   }
   __syncthreads();
   const uint32_t *row = dir + (uint64_t)p * ntiles;
-  for (uint64_t k = (uint64_t)s + (uint64_t)threadIdx.x * S; k < ntiles; k += (uint64_t)blockDim.x * S) {
-    uint32_t w = row[k];
-    uint32_t off = w >> 16, c = w & 0xFFFF;
-    if (off + c > K3T) continue;  // cannot happen for a well-formed directory; never read past the tile
-    const Rec *r = pool + k * K3T + off;
-    for (uint32_t q = 0; q < c; ++q) {
-      Rec x = r[q];
-      uint64_t d = x.d, dd = d * d;
-      atomicAdd(&a_cnt[x.kl], 1ull);
-      atomicAdd(&a_s1[x.kl], (unsigned long long)d);
-      atomicAdd(&a_s2a[x.kl], (unsigned long long)(dd & 0xFFFFFFFFull));
-      atomicAdd(&a_s2b[x.kl], (unsigned long long)(dd >> 32));
-      atomicMax(&a_tsx[x.kl], (unsigned long long)x.tsx);
-      atomicMin(&a_fst[x.kl], (unsigned long long)(index_base + x.i));
+  constexpr uint32_t NW = K3RT / 64, B = 4;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t step = (uint64_t)S * NW;  // consecutive tiles of this wave
+  for (uint64_t k0 = (uint64_t)s + (uint64_t)w * S; k0 < ntiles; k0 += step * B) {
+    uint32_t c[B], o[B], pre[B + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < B; ++j) {
+      const uint64_t k = k0 + j * step;
+      const uint32_t x = k < ntiles ? row[k] : 0;
+      o[j] = x >> 16;
+      c[j] = (o[j] + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;  // a well-formed directory never exceeds the tile
+      pre[j + 1] = pre[j] + c[j];
+    }
+    for (uint32_t q = lane; q < pre[B]; q += 64) {
+      uint32_t j = 0;
+#pragma unroll
+      for (uint32_t t = 1; t < B; ++t) j += q >= pre[t];
+      const uint64_t k = k0 + j * step;
+      const Rec x = pool[k * K3T + o[j] + (q - pre[j])];
+      const uint32_t kl = x.w & (K3R - 1);
+      const uint64_t d = x.d, dd = d * d;
+      atomicAdd(&a_cnt[kl], 1ull);
+      atomicAdd(&a_s1[kl], (unsigned long long)d);
+      atomicAdd(&a_s2a[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
+      atomicAdd(&a_s2b[kl], (unsigned long long)(dd >> 32));
+      atomicMax(&a_tsx[kl], (unsigned long long)x.tsx);
+      atomicMin(&a_fst[kl], (unsigned long long)(index_base + k * K3T + (x.w >> 10)));
     }
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < K3R; k += blockDim.x) {
+  for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
     uint64_t g = (uint64_t)p * K3R + k;
     if (g >= G) break;
     unsigned long long *b = part + (uint64_t)s * 6 * G + g;
@@ -244,7 +273,7 @@ void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base
                       const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp) {
   if (!n || !G) return;
   const uint32_t P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
-  hipLaunchKernelGGL(k3_reduce, dim3(S, P), dim3(256), 0, s, (const Rec *)pool, dir, ntiles, S, G, index_base, part);
+  hipLaunchKernelGGL(k3_reduce, dim3(S, P), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, S, G, index_base, part);
   hipLaunchKernelGGL(k3_combine, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part, S, G,
                      grp);
 }
