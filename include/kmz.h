@@ -132,6 +132,7 @@ typedef struct kmz_info {
   uint32_t flags;       /* internal error bits                             */
   uint32_t path;        /* last dependency run: bit 0 window join (else global span table),
                            bit 1 chain-interning walk (else per-relation global walk) */
+  uint64_t n_chains;    /* distinct interned ancestor chains (chain-interning path) */
 } kmz_info;
 
 /* ---- lifecycle ---------------------------------------------------------- */

@@ -181,6 +181,7 @@ static napi_value js_info(napi_env env, napi_callback_info info) {
   set_u64(env, out, "n_dups", i.n_dups);
   set_u64(env, out, "max_depth", i.max_depth);
   set_u64(env, out, "n_groups", i.n_groups);
+  set_u64(env, out, "n_chains", i.n_chains);
   return out;
 }
 

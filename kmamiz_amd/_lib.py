@@ -86,6 +86,7 @@ class Info(C.Structure):
         ("n_groups", C.c_uint64),
         ("flags", C.c_uint32),
         ("path", C.c_uint32),
+        ("n_chains", C.c_uint64),
     ]
 
 

@@ -606,7 +606,12 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     }
     // hash-table load factors: grow for the next run (correctness never
     // depends on it: an overfull probe raises the overflow flags below)
-    if (c->chain_ran && s64[S_CHAINS] * 2 > c->ccap && c->ccap < (1ull << 31)) c->ccap *= 2;
+    // chain table at load factor <= 1/8 while it fits the 256 MB MALL, else
+    // <= 1/4: a found chain is then almost always at its home slot (each
+    // extra slot is another dependent probe round trip)
+    while (c->chain_ran && c->ccap < (1ull << 31) &&
+           (s64[S_CHAINS] * 4 > c->ccap || (s64[S_CHAINS] * 8 > c->ccap && c->ccap * 32 < (256ull << 20))))
+      c->ccap *= 2;
     if ((flags & KMZ_RUN_DEPS) && s64[S_TRIP_OUT] * 2 > c->tcap) c->tcap *= 2;
     bool retry = false;
     if (h[C_FLAGS] & F_MISS_OVERFLOW) {
@@ -667,6 +672,7 @@ int kmz_get_info(kmz_ctx *c, kmz_info *out) {
   out->n_groups = c->G;
   out->flags = h[C_FLAGS];
   out->path = (uint32_t)c->path;
+  out->n_chains = c->chain_ran ? s[S_CHAINS] : 0;
   return KMZ_OK;
 }
 

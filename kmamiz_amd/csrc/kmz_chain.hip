@@ -197,6 +197,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     const uint32_t t0 = tile * CT, t1 = min(n, t0 + CT);
     const uint32_t w0 = t0 > CH ? t0 - CH : 0, w1 = min(n, t1 + CH), wn = w1 - w0;
     // window -> LDS, with every non-CLIENT slot's element hash
+    bool other = false;  // a span neither SERVER nor CLIENT in the window (rows' lastUsage path)
 #pragma unroll
     for (int q = 0; q < CPW; ++q) {
       const uint32_t jl = q * CTT + threadIdx.x;
@@ -206,9 +207,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           c[q] == NONE ? W_NONE : (c[q] == CYC ? W_CYC : ((c[q] >= w0 && c[q] < w1) ? c[q] - w0 : W_OUT));
       const uint64_t el = client ? 0 : sig_elem(ep, k[q] == KIND_SERVER, seed);
       if (jl < wn) lrec[jl] = make_uint4((uint32_t)el, (uint32_t)(el >> 32), ep, cp | ((uint32_t)(k[q] & 3) << 16));
+      other |= jl < wn && (k[q] & 3) != KIND_SERVER && !client;
     }
     for (uint32_t x = threadIdx.x; x < IMAP; x += CTT) imap_sig[x] = 0;
-    __syncthreads();
+    const bool any_other = __syncthreads_or(other);
     KMZ_STAMP(1);
     const bool more = tile + gridDim.x < nt;
     if (more) fetch(tile + gridDim.x);  // lands while this tile computes
@@ -248,22 +250,25 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
 #pragma unroll
       for (int q = 0; q < TPW; ++q) go |= wa[q] < CW && dd[q] < WIN_DEPTH;
       if (!go) break;
+      // all TPW reads first, then branch-free updates (selects), so the reads
+      // stay in flight together
+      uint4 r[TPW];
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) r[q] = lrec[wa[q] < CW ? wa[q] : 0];
 #pragma unroll
       for (int q = 0; q < TPW; ++q) {
         const bool act = wa[q] < CW && dd[q] < WIN_DEPTH;
-        const uint32_t a = act ? wa[q] : 0;
-        const uint4 r = lrec[a];
-        if (act) {
-          acc[q] = acc[q] * SIG_M + ((uint64_t)r.y << 32 | r.x);
-          if (kq[q] == KIND_SERVER && ((r.w >> 16) & 3) != KIND_SERVER) {  // (rare) a non-SERVER ancestor of a row
-            if (r.z < n_ep)
-              atomicMax(&ep_ts[r.z], (unsigned long long)((uint64_t)ts[w0 + a] ^ TS_BIAS));
-            else
-              flags |= F_RANGE;
-          }
-          ++dd[q];
-          wa[q] = r.w & 0xFFFF;
+        const uint64_t nacc = acc[q] * SIG_M + ((uint64_t)r[q].y << 32 | r[q].x);
+        if (any_other && act && kq[q] == KIND_SERVER && ((r[q].w >> 16) & 3) != KIND_SERVER) {
+          // (rare) a non-SERVER ancestor of a row
+          if (r[q].z < n_ep)
+            atomicMax(&ep_ts[r[q].z], (unsigned long long)((uint64_t)ts[w0 + wa[q]] ^ TS_BIAS));
+          else
+            flags |= F_RANGE;
         }
+        acc[q] = act ? nacc : acc[q];
+        dd[q] += act ? 1u : 0u;
+        wa[q] = act ? (r[q].w & 0xFFFF) : wa[q];
       }
     }
 #pragma unroll
