@@ -490,7 +490,7 @@ static int run_deps(kmz_ctx *c, bool links) {
     const uint32_t nt = chain_tiles(n);
     // per persistent workgroup: staged keys of candidate new chains and
     // deferred chain checks (overflow is handled in place, just slower)
-    const uint32_t scap = 1u << 16, dcap = 1u << 14, ng = chain_grid(n);
+    const uint32_t scap = 1u << 15, dcap = 1u << 12, ng = chain_grid(n);
     if (ensure(c, c->ctab, c->ccap * 32) || ensure(c, c->tile_tmp, (size_t)nt * 16) ||
         ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, (size_t)ng * scap * 8) ||
         ensure(c, c->kstage_n, (size_t)ng * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 32) ||

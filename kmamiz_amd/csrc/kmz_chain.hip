@@ -23,7 +23,7 @@
 // equal sigs are equal chains; a failed check (a 64-bit collision) raises F_SIG
 // and the run is repeated with another hash seed.
 //
-//   k4_chain       persistent workgroups over 1536-span tiles + a 256-span halo
+//   k4_chain       persistent workgroups over 768-span tiles + a 128-span halo
 //                  per side in LDS (contracted parent, kind, endpoint, element
 //                  hash).  Per tile: hash every non-CLIENT ancestry in the
 //                  window (a Horner walk over the LDS element hashes), probe
@@ -51,8 +51,8 @@
 
 namespace kmz {
 
-constexpr uint32_t CT = 1536, CH = 256, CW = CT + 2 * CH;
-constexpr int CTT = 512;
+constexpr uint32_t CT = 768, CH = 128, CW = CT + 2 * CH;
+constexpr int CTT = 256;
 constexpr int CPW = CW / CTT;  // window slots per thread (slot jl = q * CTT + thread)
 constexpr int TPW = CT / CTT;  // tile slots per thread
 static_assert(CT % CTT == 0, "tile slots must split evenly over the threads");
@@ -65,7 +65,7 @@ constexpr uint32_t IMAP = 256;  // LDS map: one inserting leader per distinct ne
 #define KMZ_CHAIN_WAVES 4
 #endif
 constexpr int CHAIN_WAVES = KMZ_CHAIN_WAVES;  // waves per SIMD: 4 -> 2 workgroups per CU (<= 128 VGPRs), 6 -> 3
-constexpr uint32_t CHAIN_WG = 256 * (CHAIN_WAVES / 2);  // persistent workgroups
+constexpr uint32_t CHAIN_WG = 256 * CHAIN_WAVES * 4 / (CTT / 64);  // persistent workgroups (fill the CUs)
 constexpr uint64_t SIG_M = 0xD6E8FEB86659FD93ull;
 // per-slot byte: kind in bits 0-1, state in bits 2-3 (state written only by the slot's owner)
 constexpr uint8_t S_NONE = 0, S_DONE = 1, S_PUT = 2, S_PEND = 3;
