@@ -31,12 +31,12 @@
 
 namespace kmz {
 
-constexpr uint32_t JT = 2048, JH = 512, JW = JT + 2 * JH, JTT = 1024;
+constexpr uint32_t JT = 1024, JH = 256, JW = JT + 2 * JH, JTT = 256;
 static_assert(JW < 4096, "local index + 1 must fit an entry's 12 bits");
 constexpr uint16_t L_NONE = 0xFFFF, L_MISS = 0xFFFE;
 constexpr uint32_t CERT_B1 = 6, CERT_BINS = 1u << CERT_B1;
 constexpr uint32_t CERT_CHUNK = 8192;  // records per pass-2 workgroup (LDS staging)
-constexpr uint32_t CERT_TPC = 192;     // tiles per pass-2 workgroup: ~6144 records of one bin
+constexpr uint32_t CERT_TPC = 384;     // tiles per pass-2 workgroup: ~6144 records of one bin
 constexpr uint32_t CERT_SET = 8192;    // pass-3 LDS set (u64), sub-bins <= 6144 records
 
 
@@ -80,7 +80,8 @@ __device__ void block_scan_lds(uint32_t *a, uint32_t m, uint32_t *wsum) {
 // fingerprint hit reads the 64-bit id.  Entries that find both buckets full go
 // to a small stash that lookups scan (broadcast reads) when it is not empty.
 // No probe loops: constant work per span, no wave waiting on its unluckiest lane.
-constexpr uint32_t JB = 2048;     // buckets (16384 entries, load <= 0.19)
+constexpr uint32_t JB = 512;      // buckets (4096 entries, load <= 0.375)
+static_assert(JB * 16 >= JT * 8, "the buckets double as the tile's certificate staging");
 constexpr uint32_t JSTASH = 64;
 __device__ __forceinline__ uint32_t jb1(uint64_t h) { return (uint32_t)h & (JB - 1); }
 __device__ __forceinline__ uint32_t jb2(uint64_t h) { return (uint32_t)(h >> 11) & (JB - 1); }
@@ -97,7 +98,7 @@ __device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
   return m;
 }
 
-__global__ void __launch_bounds__(JTT) k_join_window(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
+__global__ void __launch_bounds__(JTT, 5) k_join_window(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
                                                      const uint8_t *__restrict__ kind, uint32_t n,
                                                      uint32_t *__restrict__ cparent, uint32_t *__restrict__ dp,
                                                      unsigned long long *__restrict__ pool1,
@@ -306,7 +307,7 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
                                                      uint32_t cap2, unsigned int *__restrict__ cur2,
                                                      unsigned int *__restrict__ counters) {
   extern __shared__ uint64_t dyn[];
-  __shared__ uint32_t wsum[16], tcnt[CERT_TPC], toff[CERT_TPC], ttot;
+  __shared__ uint32_t wsum[16], tcnt[CERT_TPC], toff[CERT_TPC];
   uint64_t *stg = dyn;
   const uint32_t M = 1u << B2;
   uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn + CERT_CHUNK), *base = cnt + M;
@@ -328,37 +329,32 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
     toff[threadIdx.x] = o;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (uint32_t t = 0; t < CERT_TPC; ++t) {
-      const uint32_t c = tcnt[t];
-      tcnt[t] = acc;  // tcnt := position of the tile's run in the chunk
-      acc += c;
-      if (t + 1 == CERT_TPC) ttot = acc;
-    }
-  }
-  __syncthreads();
-  const uint32_t cn = ttot;
+  const uint32_t last = tcnt[CERT_TPC - 1];
+  block_scan_lds(tcnt, CERT_TPC, wsum);  // tcnt := position of the tile's run in the chunk
+  const uint32_t cn = tcnt[CERT_TPC - 1] + last;
   if (cn > CERT_CHUNK) {  // cannot happen for hashed ids short of ~20 sigma
     if (threadIdx.x == 0) atomicOr(&counters[C_CERT], CERT_OVF);
     return;
   }
-  {  // gather: one wave per tile run
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (uint32_t t = w; t < nt; t += blockDim.x / 64) {
-      const uint32_t beg = tcnt[t], end = t + 1 < CERT_TPC ? tcnt[t + 1] : cn;
-      const unsigned long long *src = pool1 + (uint64_t)(T0 + t) * JT + toff[t];
-      for (uint32_t l = lane; l < end - beg; l += 64) stg[beg + l] = src[l];
-    }
-  }
-  __syncthreads();
+  // gather the chunk's records straight into registers: record e belongs to
+  // the last tile whose run starts at or before e (binary search in LDS);
+  // every load is in flight before any is used
   constexpr int PQ = CERT_CHUNK / 1024;
   uint64_t h[PQ];
   uint32_t rk[PQ];
 #pragma unroll
   for (int q = 0; q < PQ; ++q) {
     const uint32_t e = q * 1024 + threadIdx.x;
-    h[q] = e < cn ? stg[e] : 0;
+    h[q] = 0;
+    if (e < cn) {
+      uint32_t lo = 0, hi = nt;  // tcnt[lo] <= e < tcnt[hi] (tcnt[nt] = cn)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tcnt[mid] <= e) lo = mid;
+        else hi = mid;
+      }
+      h[q] = pool1[(uint64_t)(T0 + lo) * JT + toff[lo] + (e - tcnt[lo])];
+    }
   }
   const uint32_t sh = 64 - CERT_B1 - B2;
 #pragma unroll
