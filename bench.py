@@ -38,6 +38,19 @@ def alg_bytes(kernel, n, n_server, relations):
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic_mesh100M.json")
+
+
+def traffic_of(kernel, config, n_local):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE), when this run is the
+    workload they were measured on (mesh, ~1e8 spans); else None."""
+    from kmamiz_amd import synth
+
+    if config != synth.MESH or abs(n_local - 1e8) > 2e6 or not os.path.exists(TRAFFIC_FILE):
+        return None
+    k = json.load(open(TRAFFIC_FILE)).get("kernels", {}).get(kernel)
+    return k["traffic_bytes"] if k else None
 
 
 def parse():
@@ -191,6 +204,8 @@ def main():
     d = per_kernel[dom]
     kern_ms = sum(v["ms_per_step"] for v in per_kernel.values())
     pipe_bytes = sum(v["alg_bytes"] for v in per_kernel.values() if v["alg_bytes"])
+    kname = {"join": "k_join_window", "stats": "k3_produce" if "reduce" in per_kernel else "k_stats",
+             "reduce": "k3_reduce", "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check"}[dom]
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0:
@@ -221,14 +236,12 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": {"join": "k_join_window", "stats": "k3_produce" if "reduce" in per_kernel else "k_stats",
-                           "reduce": "k3_reduce",
-                           "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check"}[dom],
+                "kernel": kname,
                 "achieved": d["gbs"],
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(d["gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic_of(kname, config, n_local),
                 "pipeline_gbs": round(pipe_bytes / (kern_ms * 1e-3) / 1e9, 1),
                 "kernel_ms_per_step": round(kern_ms, 4),
                 "kernels": per_kernel,

@@ -207,14 +207,15 @@ void kmz_host_free(void *p);
 #define KMZ_K_FIXUP 2    /* K1 duplicate-id fixup (repeated ids only)            */
 #define KMZ_K_RESOLVE 3  /* K2 table resolve / window-join MISS + PEND fix-ups    */
 #define KMZ_K_STATS 4    /* K3 k3_produce (or the one-pass LDS k_stats)           */
-#define KMZ_K_WALK 5     /* K4 k4_chain (or the global k_walk for repeated ids)   */
+#define KMZ_K_WALK 5     /* K4 k4_chain alone (or the global k_walk for repeated ids) */
 #define KMZ_K_FINAL 6    /* finalise, collapse, edge-set compaction               */
 #define KMZ_K_JOIN 7     /* K2 k_join_window: parent join + CLIENT contraction    */
 #define KMZ_K_CERT 8     /* uniqueness certificate pass 2 (k_cert_split)          */
 #define KMZ_K_REDUCE 9   /* K3 k3_reduce + k3_combine                             */
 #define KMZ_K_PEND 10    /* K4 chains whose ancestry leaves the LDS window        */
 #define KMZ_K_CHECK 11   /* uniqueness certificate pass 3 (k_cert_check)          */
-#define KMZ_K_COUNT 12
+#define KMZ_K_SETTLE 12  /* K4 k_chain_settle: staged keys + deferred chain checks */
+#define KMZ_K_COUNT 13
 int kmz_set_profiling(kmz_ctx *ctx, int on);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);

@@ -32,7 +32,8 @@ ERRORS = {
     -8: "KMZ_E_RCCL",
 }
 
-KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final", "join", "cert", "reduce", "pend", "check"]
+KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final", "join", "cert", "reduce", "pend", "check",
+           "settle"]
 SYNTH_BOOKINFO, SYNTH_MESH = 2, 3
 PART_GROUPS, PART_ENDPOINTS, PART_TRIPLES = 0, 1, 2
 

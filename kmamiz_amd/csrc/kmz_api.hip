@@ -510,6 +510,12 @@ static int run_deps(kmz_ctx *c, bool links) {
                    scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
                    c->ablate);
     }
+    {
+      Timed t(c, KMZ_K_SETTLE);
+      launch_chain_settle(c->stream, n, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
+                          P<uint32_t>(c->tile_tmp), st, P<unsigned long long>(c->kstage), scap,
+                          P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n));
+    }
     {  // ancestries that left their window: one pass, sized on the device (no host round trip)
       Timed t(c, KMZ_K_PEND);
       launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent),

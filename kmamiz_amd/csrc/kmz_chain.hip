@@ -584,9 +584,16 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
   hipLaunchKernelGGL(k4_chain, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, dep_ep, n_shapes, n_ep,
                      index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
                      scap, stage_n, defer, dcap, defer_n, nt, ablate);
-  hipLaunchKernelGGL(k_chain_settle, dim3(g), dim3(256), 0, s, (const unsigned long long *)stage, scap,
-                     (const uint32_t *)stage_n, (const unsigned long long *)defer, dcap, (const uint32_t *)defer_n, g,
-                     trip, tcap, tab, ccap, counters, stats64);
+}
+
+void launch_chain_settle(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip, uint64_t tcap,
+                         unsigned int *counters, const uint32_t *wg_stats, unsigned long long *stats64,
+                         const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
+                         const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n) {
+  if (!chain_tiles(n)) return;
+  const uint32_t g = chain_grid(n);
+  hipLaunchKernelGGL(k_chain_settle, dim3(g), dim3(256), 0, s, stage, scap, stage_n, defer, dcap, defer_n, g, trip,
+                     tcap, reinterpret_cast<unsigned long long *>(ctab), ccap, counters, stats64);
   launch_tile_sum(s, wg_stats, g, 4u, 4u, stats64 + S_ROWS, 2u);  // rows, rel, maxd, chains
 }
 
