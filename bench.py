@@ -167,14 +167,15 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
+    marks = []
     for _ in range(args.steps):
         step()
-    ev1.record(stream)
+        marks.append(time.perf_counter())
     barrier()
     t1 = time.perf_counter()
+    if os.environ.get("KMZ_BENCH_TRACE"):  # diagnostic: per-step wall times
+        print("step ms:", [round((b - a) * 1e3, 3) for a, b in zip([t0] + marks, marks + [t1])], file=sys.stderr)
     eng.set_profiling(False)
     ktimes = eng.kernel_times(reset=True)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if world > 1 else "cpu")

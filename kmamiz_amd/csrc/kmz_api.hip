@@ -860,10 +860,17 @@ void kmz_host_free(void *p) {
 int kmz_set_profiling(kmz_ctx *c, int on) {
   if (!c) return KMZ_E_ARG;
   c->prof = on != 0;
-  // create the timing events now, not inside the first timed run
+  // create the timing events now, and record each once (the first record of
+  // an event allocates its completion signal: ~0.5 ms, not inside a timed run)
   std::vector<hipEvent_t> tmp;
   while (c->prof && c->pool.size() + tmp.size() < 4 * KMZ_K_COUNT) tmp.push_back(ev_get(c));
   for (auto e : tmp) c->pool.push_back(e);
+  if (c->prof) {
+    for (auto e : c->pool) HIPCHK(c, hipEventRecord(e, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float t = 0.f;  // and the elapsed-time path once per pair
+    for (size_t k = 0; k + 1 < c->pool.size(); k += 2) hipEventElapsedTime(&t, c->pool[k], c->pool[k + 1]);
+  }
   return KMZ_OK;
 }
 
