@@ -363,7 +363,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       unsigned long long *en = ctab + 4 * pos[q];
       const unsigned long long cv = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
       const uint32_t d = dd[q];
-      if ((epon[q] & 1) && d && !(ablate & (1u << 19))) {  // a row: stage its keys (knob 19: diagnostic, none)
+      // a row whose chain this leader inserted (or lost to another chain: the
+      // deferred check may insert it) stages its keys; one that joined the
+      // same chain leaves them to the winner (knob 19: diagnostic, none)
+      if ((epon[q] & 1) && d && cv != sg[q] && !(ablate & (1u << 19))) {
         const uint32_t es = myep[q];
         const uint32_t base = atomicAdd(&scnt, d);
         uint32_t a = lrec[jl].w & 0xFFFF;
