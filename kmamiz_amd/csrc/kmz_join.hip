@@ -83,9 +83,15 @@ __device__ void block_scan_lds(uint32_t *a, uint32_t m, uint32_t *wsum) {
 constexpr uint32_t JB = 512;      // buckets (4096 entries, load <= 0.375)
 static_assert(JB * 16 >= JT * 8, "the buckets double as the tile's certificate staging");
 constexpr uint32_t JSTASH = 64;
-__device__ __forceinline__ uint32_t jb1(uint64_t h) { return (uint32_t)h & (JB - 1); }
-__device__ __forceinline__ uint32_t jb2(uint64_t h) { return (uint32_t)(h >> 11) & (JB - 1); }
-__device__ __forceinline__ uint32_t jfp(uint64_t h) { return (uint32_t)(h >> 22) & 0xF; }
+// Window-hash placement: two 32-bit multiplicative hashes of the folded id.
+// Placement quality only affects speed (an overfull bucket pair goes to the
+// stash, a full stash to the table path); exactness comes from comparing the
+// full 64-bit ids, and the certificate keeps its own bijective mix64.
+static_assert(JB == 512, "bucket indices are the top 9 bits of the 32-bit hashes");
+__device__ __forceinline__ uint32_t jfold(uint64_t id) { return (uint32_t)id ^ (uint32_t)(id >> 32); }
+__device__ __forceinline__ uint32_t jb1(uint32_t x) { return (x * 0x9E3779B1u) >> 23; }
+__device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >> 23; }
+__device__ __forceinline__ uint32_t jfp(uint32_t x) { return ((x * 0x9E3779B1u) >> 19) & 0xF; }
 
 // lanes of this wave whose `v` (6 bits) equals mine, among `valid` lanes
 __device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
@@ -137,11 +143,11 @@ __global__ void __launch_bounds__(JTT, 5) k_join_window(const uint64_t *__restri
       s[q] = p[q] = 0;
       k[q] = 0;
     }
-  uint64_t hs[PW];
+  uint32_t hs[PW];
 #pragma unroll
   for (int q = 0; q < PW; ++q) {
     const uint32_t jl = q * JTT + threadIdx.x;
-    hs[q] = mix64(s[q]);
+    hs[q] = jfold(s[q]);
     if (w0 + jl < w1) {
       lsid[jl] = s[q];
       lkind[jl] = k[q];
@@ -183,14 +189,28 @@ __global__ void __launch_bounds__(JTT, 5) k_join_window(const uint64_t *__restri
     uint32_t r = L_NONE;
     if (p[q] != 0 && ((j >= t0 && j < t1) || k[q] == KIND_CLIENT) && !(ablate & 512)) {
       r = L_MISS;
-      const uint64_t h = mix64(p[q]);
-      const uint32_t f = jfp(h);
-      const uint4 x = lbkt[jb1(h)], y = lbkt[jb2(h)];
+      const uint32_t h = jfold(p[q]);
+      const uint32_t f = jfp(h), pb1 = jb1(h), pb2 = jb2(h);
+      const uint4 x = lbkt[pb1], y = lbkt[pb2];
       const uint32_t c[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+      // candidates: occupied entries with the fingerprint (two per word, SWAR)
+      const uint32_t pat = (f << 12) | (f << 28);
+      uint32_t cand = 0;
 #pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        const uint32_t en = (c[t >> 1] >> (16 * (t & 1))) & 0xFFFF;
-        if (en && (en >> 12) == f && lsid[(en & 4095) - 1] == p[q]) r = (en & 4095) - 1;
+      for (int t = 0; t < 8; ++t) {
+        const uint32_t v = c[t], z = v ^ pat;
+        cand |= (((z & 0xF000u) == 0 && (v & 0xFFFFu) != 0) ? 1u : 0u) << (2 * t);
+        cand |= (((z & 0xF0000000u) == 0 && (v >> 16) != 0) ? 1u : 0u) << (2 * t + 1);
+      }
+      while (cand) {  // usually one candidate: the parent
+        const uint32_t t = __builtin_ctz(cand);
+        cand &= cand - 1;
+        // (re-read the entry from LDS: no dynamic indexing of registers)
+        const uint32_t en = reinterpret_cast<const uint16_t *>(&lbkt[t < 8 ? pb1 : pb2])[t & 7] & 0xFFF;
+        if (lsid[en - 1] == p[q]) {
+          r = en - 1;
+          break;
+        }
       }
       for (uint32_t t = 0; t < ns; ++t) {
         const uint32_t en = stash[t];
