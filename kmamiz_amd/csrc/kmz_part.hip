@@ -177,8 +177,9 @@ __global__ void __launch_bounds__(1024) k_tile_sum(const uint32_t *__restrict__ 
 static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32_t>(64, (ntiles + 1023) / 1024 + 0); }
 
 // slice s of partition p: tiles s, s+S, ...  -> part[(s*6 + f) * G + g].
-// Each wave takes four of the slice's tiles at a time and spreads the
-// concatenation of their record runs over its lanes (coalesced 16-byte reads).
+// Each wave takes sixteen of the slice's tiles at a time and spreads the
+// concatenation of their record runs over its lanes (coalesced 16-byte reads,
+// four per lane in flight).
 constexpr int K3RT = 256;
 __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
                                                   uint32_t ntiles, uint32_t S, uint32_t G, uint64_t index_base,
@@ -191,34 +192,54 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
   }
   __syncthreads();
   const uint32_t *row = dir + (uint64_t)p * ntiles;
-  constexpr uint32_t NW = K3RT / 64, B = 4;
+  constexpr uint32_t NW = K3RT / 64, B = 16, U = 4;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t step = (uint64_t)S * NW;  // consecutive tiles of this wave
   for (uint64_t k0 = (uint64_t)s + (uint64_t)w * S; k0 < ntiles; k0 += step * B) {
-    uint32_t c[B], o[B], pre[B + 1];
+    // the batch's B directory words (wave-uniform) and their run prefix
+    uint32_t o[B], pre[B + 1];
     pre[0] = 0;
 #pragma unroll
     for (uint32_t j = 0; j < B; ++j) {
       const uint64_t k = k0 + j * step;
       const uint32_t x = k < ntiles ? row[k] : 0;
       o[j] = x >> 16;
-      c[j] = (o[j] + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;  // a well-formed directory never exceeds the tile
-      pre[j + 1] = pre[j] + c[j];
+      const uint32_t c = (o[j] + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;  // a well-formed directory never exceeds the tile
+      pre[j + 1] = pre[j] + c;
     }
-    for (uint32_t q = lane; q < pre[B]; q += 64) {
-      uint32_t j = 0;
+    // the batch's records spread over the lanes, U loads in flight per lane
+    for (uint32_t q0 = 0; q0 < pre[B]; q0 += 64 * U) {
+      Rec x[U];
+      uint64_t kk[U];
+      bool v[U];
 #pragma unroll
-      for (uint32_t t = 1; t < B; ++t) j += q >= pre[t];
-      const uint64_t k = k0 + j * step;
-      const Rec x = pool[k * K3T + o[j] + (q - pre[j])];
-      const uint32_t kl = x.w & (K3R - 1);
-      const uint64_t d = x.d, dd = d * d;
-      atomicAdd(&a_cnt[kl], 1ull);
-      atomicAdd(&a_s1[kl], (unsigned long long)d);
-      atomicAdd(&a_s2a[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
-      atomicAdd(&a_s2b[kl], (unsigned long long)(dd >> 32));
-      atomicMax(&a_tsx[kl], (unsigned long long)x.tsx);
-      atomicMin(&a_fst[kl], (unsigned long long)(index_base + k * K3T + (x.w >> 10)));
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t q = q0 + u * 64 + lane;
+        v[u] = q < pre[B];
+        uint32_t ob = o[0], pb = 0;
+        uint64_t kb = k0;
+#pragma unroll
+        for (uint32_t t = 1; t < B; ++t)  // the run holding record q (selects, no indexing)
+          if (q >= pre[t]) {
+            ob = o[t];
+            pb = pre[t];
+            kb = k0 + t * step;
+          }
+        kk[u] = kb;
+        x[u] = pool[v[u] ? kb * K3T + ob + (q - pb) : 0];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        if (!v[u]) continue;
+        const uint32_t kl = x[u].w & (K3R - 1);
+        const uint64_t d = x[u].d, dd = d * d;
+        atomicAdd(&a_cnt[kl], 1ull);
+        atomicAdd(&a_s1[kl], (unsigned long long)d);
+        atomicAdd(&a_s2a[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
+        atomicAdd(&a_s2b[kl], (unsigned long long)(dd >> 32));
+        atomicMax(&a_tsx[kl], (unsigned long long)x[u].tsx);
+        atomicMin(&a_fst[kl], (unsigned long long)(index_base + kk[u] * K3T + (x[u].w >> 10)));
+      }
     }
   }
   __syncthreads();
