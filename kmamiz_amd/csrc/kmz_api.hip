@@ -28,6 +28,8 @@ struct EventPair {
 
 }  // namespace
 
+constexpr uint64_t SIG_SEED0 = 0x4B4D5A5349470001ull;  // the K4 ancestry-hash seed of a fresh context
+
 struct kmz_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -59,7 +61,7 @@ struct kmz_ctx {
   bool sstats = false;      // shape-level K3 partials computed in this run
   bool chain_ran = false;   // this run's dependency graph came from k4_chain
   uint64_t cap = 0, tcap = 1ull << 16, ccap = 1ull << 20;
-  uint64_t sig_seed = 0x4B4D5A5349470001ull;  // K4 ancestry-hash seed (changed after a collision)
+  uint64_t sig_seed = SIG_SEED0;  // K4 ancestry-hash seed (changed after a collision)
   uint32_t dcap = 1024;
   uint32_t mcap = 1u << 16;   // window-join miss table slots (grown on F_MISS_OVERFLOW)
   bool table_hint = false;    // the loaded batch failed the uniqueness certificate: go to the table path
@@ -508,7 +510,8 @@ static int run_deps(kmz_ctx *c, bool links) {
                    P<unsigned long long>(c->trip), c->tcap, epp, links ? P<unsigned long long>(c->rowpos) : nullptr,
                    P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->tile_tmp), st, P<unsigned long long>(c->kstage),
                    scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
-                   c->ablate);
+                   // (test knob 24 forces sig collisions on the first seed only)
+                   c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)));
     }
     {
       Timed t(c, KMZ_K_SETTLE);

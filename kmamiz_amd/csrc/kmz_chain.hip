@@ -286,6 +286,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       const uint32_t d = dd[q];
       ps[q] = d ? sig_final(acc[q], d - 1, seed) : ROOT_SIG;
       sg[q] = sig_final(sg[q] * lpow[d] + acc[q], d, seed);
+      if (ablate & (1u << 24)) {  // test knob: 4-bit sigs, i.e. collisions (F_SIG, then a retry with another seed)
+        sg[q] = (sg[q] & 0xF) + 2;
+        ps[q] = d ? (ps[q] & 0xF) + 2 : ROOT_SIG;
+      }
       if (!(ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
     ulonglong2 w01[TPW];  // (sig, parent sig) of the probed slot

@@ -238,7 +238,7 @@ def _compare_synth(engine, batch, table):
     return info
 
 
-@pytest.mark.parametrize("config,ntr", [(2, 30000), (3, 4000)])
+@pytest.mark.parametrize("config,ntr", [(2, 30000), (3, 4000), (3, 40000)])
 def test_synthetic_vs_c_oracle(engine, config, ntr):
     from kmamiz_amd import synth
 
@@ -400,3 +400,66 @@ def test_window_join_matches_span_table(engine):
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
     assert a[3].tobytes() == b[3].tobytes()
     assert {k: v for k, v in a[4].items() if k != "path"} == {k: v for k, v in b[4].items() if k != "path"}
+
+
+# ---------------------------------------------------------------------------
+# K4 chain interning: hash collisions, deep chains (kmz_chain.hip)
+# ---------------------------------------------------------------------------
+def test_sig_collision_is_detected_and_retried(engine):
+    """KMZ_ABLATE bit 24 truncates the ancestry sigs to 4 bits on the first
+    seed: different chains share sigs, the exact entry checks raise F_SIG, and
+    the run repeats with another seed.  The result must equal a normal run."""
+    import os
+
+    from kmamiz_amd import Engine
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    def run(e):
+        e.load_synthetic(3, synth.SEED, 0, 20000)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        return e.triples(), e.endpoints(), e.info()
+
+    a = run(engine)
+    os.environ["KMZ_ABLATE"] = str(1 << 24)
+    try:
+        e2 = Engine(0)
+    finally:
+        del os.environ["KMZ_ABLATE"]
+    try:
+        b = run(e2)
+    finally:
+        e2.close()
+    assert np.array_equal(a[0], b[0])
+    assert a[1].tobytes() == b[1].tobytes()
+    assert a[2] == b[2]
+
+
+def test_deep_chain_takes_the_pending_path(engine):
+    """A 300-deep SERVER/CLIENT chain is deeper than the LDS window and
+    WIN_DEPTH: its spans hash over the global contracted parents."""
+    from kmamiz_amd import Traces
+
+    def span(i, kind, parent, svc):
+        tags = {"http.url": f"http://{svc}/x", "http.method": "GET", "istio.canonical_revision": "v1",
+                "http.status_code": "200"}
+        d = {"id": f"{i + 1:016x}", "kind": kind, "name": f"{svc}.ns.svc.cluster.local:80/x", "timestamp": 1000 + i,
+             "duration": 10 + i % 7, "tags": tags}
+        if parent is not None:
+            d["parentId"] = f"{parent + 1:016x}"
+        return d
+
+    trace, prev, i = [], None, 0
+    for level in range(300):
+        svc = f"s{level % 5}"
+        if prev is not None:
+            trace.append(span(i, "CLIENT", prev, svc))
+            i += 1
+            prev = i - 1
+        trace.append(span(i, "SERVER", prev, svc))
+        prev = i
+        i += 1
+    # a short normal trace in front, so the deep one also crosses tiles
+    ours = Traces([trace[:1], trace], engine=engine)
+    exp = O.strip_undef(O.Traces([trace[:1], trace]).toEndpointDependencies(max_depth=10000).toJSON())
+    assert ours.toEndpointDependencies().toJSON() == exp
