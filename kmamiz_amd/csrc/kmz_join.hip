@@ -31,12 +31,12 @@
 
 namespace kmz {
 
-constexpr uint32_t JT = 1024, JH = 256, JW = JT + 2 * JH, JTT = 256;
+constexpr uint32_t JT = 2048, JH = 256, JW = JT + 2 * JH, JTT = 512;
 static_assert(JW < 4096, "local index + 1 must fit an entry's 12 bits");
 constexpr uint16_t L_NONE = 0xFFFF, L_MISS = 0xFFFE;
 constexpr uint32_t CERT_B1 = 6, CERT_BINS = 1u << CERT_B1;
 constexpr uint32_t CERT_CHUNK = 8192;  // records per pass-2 workgroup (LDS staging)
-constexpr uint32_t CERT_TPC = 384;     // tiles per pass-2 workgroup: ~6144 records of one bin
+constexpr uint32_t CERT_TPC = 192;     // tiles per pass-2 workgroup: ~6144 records of one bin
 constexpr uint32_t CERT_SET = 8192;    // pass-3 LDS set (u64), sub-bins <= 6144 records
 
 
@@ -80,18 +80,18 @@ __device__ void block_scan_lds(uint32_t *a, uint32_t m, uint32_t *wsum) {
 // fingerprint hit reads the 64-bit id.  Entries that find both buckets full go
 // to a small stash that lookups scan (broadcast reads) when it is not empty.
 // No probe loops: constant work per span, no wave waiting on its unluckiest lane.
-constexpr uint32_t JB = 512;      // buckets (4096 entries, load <= 0.375)
+constexpr uint32_t JB = 1024;     // buckets (8192 entries, load <= 0.31)
 static_assert(JB * 16 >= JT * 8, "the buckets double as the tile's certificate staging");
 constexpr uint32_t JSTASH = 64;
 // Window-hash placement: two 32-bit multiplicative hashes of the folded id.
 // Placement quality only affects speed (an overfull bucket pair goes to the
 // stash, a full stash to the table path); exactness comes from comparing the
 // full 64-bit ids, and the certificate keeps its own bijective mix64.
-static_assert(JB == 512, "bucket indices are the top 9 bits of the 32-bit hashes");
+static_assert(JB == 1024, "bucket indices are the top 10 bits of the 32-bit hashes");
 __device__ __forceinline__ uint32_t jfold(uint64_t id) { return (uint32_t)id ^ (uint32_t)(id >> 32); }
-__device__ __forceinline__ uint32_t jb1(uint32_t x) { return (x * 0x9E3779B1u) >> 23; }
-__device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >> 23; }
-__device__ __forceinline__ uint32_t jfp(uint32_t x) { return ((x * 0x9E3779B1u) >> 19) & 0xF; }
+__device__ __forceinline__ uint32_t jb1(uint32_t x) { return (x * 0x9E3779B1u) >> 22; }
+__device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >> 22; }
+__device__ __forceinline__ uint32_t jfp(uint32_t x) { return ((x * 0x9E3779B1u) >> 18) & 0xF; }
 
 // lanes of this wave whose `v` (6 bits) equals mine, among `valid` lanes
 __device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
@@ -104,7 +104,7 @@ __device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
   return m;
 }
 
-__global__ void __launch_bounds__(JTT, 5) k_join_window(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
+__global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
                                                      const uint8_t *__restrict__ kind, uint32_t n,
                                                      uint32_t *__restrict__ cparent, uint32_t *__restrict__ dp,
                                                      unsigned long long *__restrict__ pool1,
