@@ -145,16 +145,14 @@ def main():
             eng.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, True)
             kdist.merge_group_partials(g, gw // 6)
             kdist.merge_endpoint_partials(e, ew // 2)
-            keys = kdist.merge_edge_keys(t[:tw])
+            kdist.merge_edge_keys_into(eng, t[:tw])  # union in the engine's device edge set
             eng.import_partials(L.PART_GROUPS, g.data_ptr(), gw, True)
             eng.import_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
             eng.finalize()
-            state["keys"] = keys.cpu() if not args.no_fetch else keys
+            if not args.no_fetch:
+                state["groups"], state["keys"], state["endpoints"] = eng.fetch()
         elif not args.no_fetch:  # the three result sets, one synchronisation
             state["groups"], state["keys"], state["endpoints"] = eng.fetch()
-        if world > 1 and not args.no_fetch:
-            state["groups"] = eng.groups(copy=False)
-            state["endpoints"] = eng.endpoints()
 
     for _ in range(args.warmup):
         step()

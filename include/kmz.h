@@ -190,6 +190,12 @@ int kmz_endpoint_partials(kmz_ctx *ctx, void **dev_ptr, uint64_t *n_ep);
 #define KMZ_PART_TRIPLES 2
 int kmz_partials_size(kmz_ctx *ctx, int which, uint64_t *words);
 int kmz_partials_copy(kmz_ctx *ctx, int which, void *buf, uint64_t words, int mem, int direction);
+/* Union of edge-key sets across traceId shards (the dependency half of
+ * EndpointDependencies.combineWith, EndpointDependencies.ts:91-112, over the
+ * reduced form): inserts n keys (0 = padding, skipped; host or device memory
+ * per `mem`) into this context's edge set after a KMZ_RUN_DEPS run;
+ * kmz_get_triples / kmz_fetch / KMZ_PART_TRIPLES then return the union. */
+int kmz_merge_triples(kmz_ctx *ctx, const uint64_t *keys, uint64_t n, int mem);
 /* re-finalise the groups after the partials were reduced in place */
 int kmz_finalize(kmz_ctx *ctx);
 /* host-side finalisation of one partial (same arithmetic as the device) */

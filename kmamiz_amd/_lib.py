@@ -120,6 +120,7 @@ SIGNATURES = [
     ("kmz_endpoint_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_partials_size", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
     ("kmz_partials_copy", C.c_int, [_P, C.c_int, _P, C.c_uint64, C.c_int, C.c_int]),
+    ("kmz_merge_triples", C.c_int, [_P, _P, C.c_uint64, C.c_int]),
     ("kmz_finalize", C.c_int, [_P]),
     ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
     ("kmz_host_alloc", _P, [C.c_uint64]),

@@ -57,6 +57,7 @@ struct kmz_ctx {
   DevBuf k3pool, k3dir, k3part, tile_tmp, sgrp;
   DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n;  // K4 chain interning
+  DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   int path = 0;             // kmz_info.path of the last dependency run
   bool sstats = false;      // shape-level K3 partials computed in this run
   bool chain_ran = false;   // this run's dependency graph came from k4_chain
@@ -253,7 +254,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->stats64,   &c->scratch,
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
-                    &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n};
+                    &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
+                    &c->mkeys_in, &c->mtab};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->hpin) hipHostFree(c->hpin);
@@ -800,10 +802,14 @@ int kmz_partials_size(kmz_ctx *c, int which, uint64_t *words) {
     *words = 2ull * c->n_dep;
   } else if (which == KMZ_PART_TRIPLES) {
     if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
-    unsigned long long s[S_COUNT];
-    HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    *words = s[S_TRIP_OUT];
+    if (c->hpin_valid) {
+      *words = reinterpret_cast<const unsigned long long *>(reinterpret_cast<const unsigned int *>(c->hpin) + C_COUNT)[S_TRIP_OUT];
+    } else {
+      unsigned long long s[S_COUNT];
+      HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      *words = s[S_TRIP_OUT];
+    }
   } else {
     return fail(c, KMZ_E_ARG, "unknown partial");
   }
@@ -826,6 +832,59 @@ int kmz_partials_copy(kmz_ctx *c, int which, void *buf, uint64_t words, int mem,
       HIPCHK(c, hipMemcpyAsync(buf, mine, need * 8, k, c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_merge_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, int mem) {
+  if (!c || (n && !keys)) return KMZ_E_ARG;
+  if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+  uint64_t nl = 0;
+  int r = kmz_partials_size(c, KMZ_PART_TRIPLES, &nl);
+  if (r) return r;
+  const unsigned long long *src = reinterpret_cast<const unsigned long long *>(keys);
+  if (n && mem == KMZ_MEM_HOST) {
+    if (ensure(c, c->mkeys_in, n * 8)) return KMZ_E_HIP;
+    HIPCHK(c, hipMemcpyAsync(c->mkeys_in.p, keys, n * 8, hipMemcpyHostToDevice, c->stream));
+    src = P<unsigned long long>(c->mkeys_in);
+  }
+  unsigned int *cnt = P<unsigned int>(c->counters);
+  unsigned long long *st = P<unsigned long long>(c->stats64);
+  // the run's edge set is intact: insert the incoming keys into it (they are
+  // mostly already there), then compact again
+  HIPCHK(c, hipMemsetAsync(cnt + C_FLAGS, 0, 4, c->stream));
+  {
+    Timed t(c, KMZ_K_FINAL);
+    launch_key_insert(c->stream, src, n, P<unsigned long long>(c->trip), c->tcap, cnt);
+  }
+  unsigned int fl = 0;
+  HIPCHK(c, hipMemcpyAsync(&fl, cnt + C_FLAGS, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  unsigned long long *tab = P<unsigned long long>(c->trip);
+  uint64_t cap = c->tcap;
+  if (fl & F_TRIPLE_OVERFLOW) {  // the union outgrew the set: a fresh one, large enough for every key
+    cap = 1ull << 16;
+    while (cap < 2 * (nl + n) + 64) cap *= 2;
+    if (ensure(c, c->mtab, cap * 8)) return KMZ_E_HIP;
+    tab = P<unsigned long long>(c->mtab);
+    HIPCHK(c, hipMemsetAsync(tab, 0, cap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(cnt + C_FLAGS, 0, 4, c->stream));
+    launch_key_insert(c->stream, P<unsigned long long>(c->trip_out), nl, tab, cap, cnt);  // this rank's keys
+    launch_key_insert(c->stream, src, n, tab, cap, cnt);
+    HIPCHK(c, hipMemcpyAsync(&fl, cnt + C_FLAGS, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (fl & F_TRIPLE_OVERFLOW) return fail(c, KMZ_E_OVERFLOW, "edge-key union overflow");
+    if (ensure(c, c->trip_out, cap * 8)) return KMZ_E_HIP;
+  }
+  HIPCHK(c, hipMemsetAsync(st + S_TRIP_OUT, 0, 8, c->stream));
+  {
+    Timed t(c, KMZ_K_FINAL);
+    launch_compact(c->stream, tab, cap, P<unsigned long long>(c->trip_out), st + S_TRIP_OUT);
+  }
+  unsigned long long nt = 0;
+  HIPCHK(c, hipMemcpyAsync(&nt, st + S_TRIP_OUT, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->hpin_valid)
+    reinterpret_cast<unsigned long long *>(reinterpret_cast<unsigned int *>(c->hpin) + C_COUNT)[S_TRIP_OUT] = nt;
   return KMZ_OK;
 }
 

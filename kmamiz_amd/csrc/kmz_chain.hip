@@ -563,6 +563,25 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
   if (flags) atomicOr(&counters[C_FLAGS], flags);
 }
 
+// multi-GPU union of edge-key sets: other ranks' keys into this context's set
+__global__ void __launch_bounds__(256) k_key_insert(const unsigned long long *__restrict__ keys, uint64_t n,
+                                                    unsigned long long *__restrict__ trip, uint64_t tcap,
+                                                    unsigned int *__restrict__ counters) {
+  uint32_t flags = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const unsigned long long k = keys[i];
+    if (k) edge_insert(k, trip, tcap, &flags);  // 0: padding
+  }
+  if (flags) atomicOr(&counters[C_FLAGS], flags);
+}
+
+void launch_key_insert(hipStream_t s, const unsigned long long *keys, uint64_t n, unsigned long long *trip,
+                       uint64_t tcap, unsigned int *counters) {
+  if (!n) return;
+  const uint32_t g = (uint32_t)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_key_insert, dim3(g), dim3(256), 0, s, keys, n, trip, tcap, counters);
+}
+
 uint32_t chain_tiles(uint32_t n) { return (n + CT - 1) / CT; }
 }  // namespace kmz
 extern "C" int kmz__debug_chain(unsigned long long *out, int reset) {

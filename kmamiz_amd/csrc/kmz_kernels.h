@@ -81,6 +81,8 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
                   uint32_t dcap, uint32_t *defer_n, uint32_t ablate = 0);
 uint32_t chain_grid(uint32_t n);
+void launch_key_insert(hipStream_t s, const unsigned long long *keys, uint64_t n, unsigned long long *trip,
+                       uint64_t tcap, unsigned int *counters);
 void launch_chain_settle(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip, uint64_t tcap,
                          unsigned int *counters, const uint32_t *wg_stats, unsigned long long *stats64,
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,

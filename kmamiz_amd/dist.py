@@ -8,7 +8,9 @@ partials then merge with collectives over the default process group:
                     [max timestamp]                                all_reduce MAX
                     [min first index]                              all_reduce MIN
 * endpoint partials [max timestamp] MAX, [min first_row<<1|!external] MIN
-* edge keys         size all_reduce MAX, padded all_gather, unique
+* edge keys         size all_reduce MAX, padded all_gather, then a union:
+                    into the engine's own device edge set (kmz_merge_triples,
+                    ``merge_edge_keys_into``) or ``torch.unique`` (CPU tensors)
 
 Integer moments make the merge exact: the merged groups are bit-identical to a
 single-GPU run over the whole batch (the reference's pooled-variance formula,
@@ -72,3 +74,26 @@ def merge_edge_keys(keys: torch.Tensor) -> torch.Tensor:
     dist.all_gather(parts, pad)
     allk = torch.unique(torch.cat(parts))
     return allk[allk != 0]
+
+
+def merge_edge_keys_into(engine, keys: torch.Tensor) -> None:
+    """Union every rank's edge keys into ``engine``'s device edge set
+    (kmz_merge_triples: hash inserts into the run's set, no sort).  ``keys``:
+    this rank's unique keys, int64 view, on the engine's GPU (RCCL) or on the
+    CPU (gloo)."""
+    if dist.get_world_size() == 1:
+        return
+    n = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX)
+    m = int(n.item())
+    pad = torch.zeros(m, dtype=torch.int64, device=keys.device)
+    pad[: keys.numel()] = keys
+    if keys.is_cuda:
+        allk = torch.empty(m * dist.get_world_size(), dtype=torch.int64, device=keys.device)
+        dist.all_gather_into_tensor(allk, pad)
+        torch.cuda.current_stream(keys.device).synchronize()  # the engine's stream may not be torch's
+    else:
+        parts = [torch.empty_like(pad) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, pad)
+        allk = torch.cat(parts)
+    engine.merge_triples(allk.data_ptr(), allk.numel(), keys.is_cuda)

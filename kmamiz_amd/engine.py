@@ -241,6 +241,11 @@ class Engine:
     def finalize(self):
         L.check(self.ctx, self._lib.kmz_finalize(self.ctx))
 
+    def merge_triples(self, src_ptr: int, n: int, device: bool):
+        """Union other shards' edge keys (u64, 0 = padding) into this run's set."""
+        L.check(self.ctx, self._lib.kmz_merge_triples(self.ctx, C.c_void_p(src_ptr), n,
+                                                      L.MEM_DEVICE if device else L.MEM_HOST))
+
     # ---- profiling -------------------------------------------------------------
     def set_profiling(self, on: bool):
         L.check(self.ctx, self._lib.kmz_set_profiling(self.ctx, 1 if on else 0))

@@ -1,0 +1,88 @@
+"""The bench's multi-GPU merge sequence on real engines: two ranks (gloo, CPU
+tensors) share the one GPU, each runs its traceId shard, and the partials and
+edge keys merge through kmamiz_amd.dist (kmz_partials_copy, kmz_merge_triples,
+kmz_finalize).  Both ranks must end with the single-engine result over the
+whole batch, bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kmamiz_amd import Engine
+        from kmamiz_amd import _lib as L
+        from kmamiz_amd import dist as kdist
+        from kmamiz_amd import synth
+
+        e = Engine(0)
+        cut = [0, 1500, 4000]
+        e.load_synthetic(synth.MESH, synth.SEED, cut[rank], cut[rank + 1])
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        gw, ew, tw = (e.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
+        g = torch.zeros(gw, dtype=torch.int64)
+        ep = torch.zeros(ew, dtype=torch.int64)
+        t = torch.zeros(max(1, tw), dtype=torch.int64)
+        e.export_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
+        e.export_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
+        e.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, False)
+        kdist.merge_group_partials(g, gw // 6)
+        kdist.merge_endpoint_partials(ep, ew // 2)
+        kdist.merge_edge_keys_into(e, t[:tw])
+        e.import_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
+        e.import_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
+        e.finalize()
+        groups, keys, eps = e.fetch()
+        q.put((rank, groups.tobytes(), np.sort(keys).tobytes(), eps.tobytes()))
+        e.close()
+    except Exception as ex:  # surfaced by the parent
+        q.put((rank, "error", repr(ex), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_merge_equals_single_engine():
+    from kmamiz_amd import Engine
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r[2]
+    e = Engine(0)
+    try:
+        e.load_synthetic(synth.MESH, synth.SEED, 0, 4000)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        g, k, ep = e.fetch()
+        exp = (g.tobytes(), np.sort(k).tobytes(), ep.tobytes())
+    finally:
+        e.close()
+    for r in res:
+        assert r[1] == exp[0]
+        assert r[2] == exp[1]
+        assert r[3] == exp[2]

@@ -463,3 +463,36 @@ def test_deep_chain_takes_the_pending_path(engine):
     ours = Traces([trace[:1], trace], engine=engine)
     exp = O.strip_undef(O.Traces([trace[:1], trace]).toEndpointDependencies(max_depth=10000).toJSON())
     assert ours.toEndpointDependencies().toJSON() == exp
+
+
+def test_merge_triples_is_the_union_of_shards(engine):
+    """kmz_merge_triples: shard B's edge keys unioned into shard A's device set
+    equal the edge set of one run over both shards; a union that outgrows the
+    set (many foreign keys, host memory) takes the fresh-table path."""
+    from kmamiz_amd import Engine
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    F = L.RUN_STATS_TAG | L.RUN_DEPS
+    engine.load_synthetic(3, synth.SEED, 0, 4000)
+    engine.run(F)
+    full = engine.triples()
+    b = Engine(0)
+    try:
+        b.load_synthetic(3, synth.SEED, 2000, 4000)
+        b.run(F)
+        kb = b.triples()
+    finally:
+        b.close()
+    engine.load_synthetic(3, synth.SEED, 0, 2000)
+    engine.run(F)
+    ka = engine.triples()
+    assert len(ka) < len(full) and len(kb) < len(full)
+    pad = np.concatenate([kb, np.zeros(17, np.uint64)])  # zeros: padding, skipped
+    engine.merge_triples(pad.ctypes.data, len(pad), False)
+    assert np.array_equal(engine.triples(), full)
+    assert engine.info()["n_triples"] == len(full)
+    rng = np.random.default_rng(3)
+    foreign = np.unique(rng.integers(1, 2**62, size=300000, dtype=np.uint64))
+    engine.merge_triples(foreign.ctypes.data, len(foreign), False)
+    assert np.array_equal(engine.triples(), np.union1d(full, foreign))
