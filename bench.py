@@ -5,7 +5,7 @@ K1 build + K2 resolve + K4 walk (dependency graph) and K3 (combined stats),
 finalisation, the multi-GPU merge (N > 1, RCCL via torch.distributed) and the
 download of the results (groups, endpoint records, edge keys) to the host.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config mesh|bookinfo]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config mesh|bookinfo|power]
 
 Weak scaling: every rank owns a fixed shard of whole traces (config 3's
 100M-span 500-service mesh per GPU by default; N=8 is config 4's ~1B-span
@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["mesh", "bookinfo"], default="mesh")
+    ap.add_argument("--config", choices=["mesh", "bookinfo", "power"], default="mesh")
     ap.add_argument("--spans", type=float, default=None, help="spans per GPU (default: 1e8 mesh, 1e6 bookinfo)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-fetch", action="store_true", help="leave results on the device")
@@ -117,8 +117,8 @@ def main():
     from kmamiz_amd import dist as kdist
     from kmamiz_amd import synth
 
-    config = synth.MESH if args.config == "mesh" else synth.BOOKINFO
-    target = int(args.spans or (1e8 if args.config == "mesh" else 1e6))
+    config = {"mesh": synth.MESH, "bookinfo": synth.BOOKINFO, "power": synth.POWER}[args.config]
+    target = int(args.spans or (1e6 if args.config == "bookinfo" else 1e8))
     sample_tr = 20000
     per_trace = synth.count_spans(config, 0, sample_tr) / sample_tr
     traces_per_gpu = max(1, int(round(target / per_trace)))
@@ -223,8 +223,10 @@ def main():
             "dtype": "int64+f64",
             "data": "synthetic (device-generated, seed 0x4B4D414D495A)",
             "config": {
-                "workload": ("config3: 500-service/20k-endpoint mesh, depth-8 chains, "
-                             if config == synth.MESH else "config2: Bookinfo-shaped mesh, ")
+                "workload": {synth.MESH: "config3: 500-service/20k-endpoint mesh, depth-8 chains, ",
+                             synth.BOOKINFO: "config2: Bookinfo-shaped mesh, ",
+                             synth.POWER: "config5: power-law fan-out mesh, 50k endpoints, depth-16 chains, "
+                                          "hot endpoints, "}[config]
                 + f"{n_local} spans/GPU ({traces_per_gpu} traces/GPU)"
                 + (", sharded by whole traces (config 4 at N=8)" if config == synth.MESH else ""),
                 "spans_per_gpu": n_local,

@@ -229,6 +229,7 @@ int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);
 /* ---- synthetic workload (BASELINE.json configs 2-5), generated in HBM ---- */
 #define KMZ_SYNTH_BOOKINFO 2
 #define KMZ_SYNTH_MESH 3
+#define KMZ_SYNTH_POWER 5 /* power-law fan-out mesh, 50k endpoints, depth-16 chains, hot endpoints */
 typedef struct kmz_synth_desc {
   uint32_t n_shapes, n_status;
   uint32_t n_endpoints;

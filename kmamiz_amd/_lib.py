@@ -34,7 +34,7 @@ ERRORS = {
 
 KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final", "join", "cert", "reduce", "pend", "check",
            "settle"]
-SYNTH_BOOKINFO, SYNTH_MESH = 2, 3
+SYNTH_BOOKINFO, SYNTH_MESH, SYNTH_POWER = 2, 3, 5
 PART_GROUPS, PART_ENDPOINTS, PART_TRIPLES = 0, 1, 2
 
 

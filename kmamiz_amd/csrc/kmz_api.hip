@@ -958,6 +958,8 @@ int kmz_synth_describe(int config, kmz_synth_desc *out) {
     out->n_shapes = out->n_endpoints = BOOK_EPS;
   } else if (config == KMZ_SYNTH_MESH) {
     out->n_shapes = out->n_endpoints = MESH_EPS;
+  } else if (config == KMZ_SYNTH_POWER) {
+    out->n_shapes = out->n_endpoints = PL_EPS;
   } else {
     return KMZ_E_ARG;
   }
@@ -1051,23 +1053,23 @@ int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t 
 int kmz_synth_host(int config, uint64_t seed, uint64_t t0, uint64_t t1, uint64_t cap, uint64_t *span_id,
                    uint64_t *parent_id, uint8_t *kind, uint32_t *shape, uint16_t *status, uint32_t *duration,
                    int64_t *timestamp, uint64_t *trace_off, uint64_t *n_out) {
-  if (t1 < t0 || (config != KMZ_SYNTH_BOOKINFO && config != KMZ_SYNTH_MESH)) return KMZ_E_ARG;
+  if (t1 < t0 || (config != KMZ_SYNTH_BOOKINFO && config != KMZ_SYNTH_MESH && config != KMZ_SYNTH_POWER))
+    return KMZ_E_ARG;
   const auto &dt = dur_table_host();
+  auto gen = [&](uint64_t t, uint64_t gbase, uint64_t lbase, const uint32_t *tab, const SynthOut *o) -> uint32_t {
+    if (config == KMZ_SYNTH_BOOKINFO) return synth_trace<2>(seed, t, gbase, lbase, tab, o);
+    if (config == KMZ_SYNTH_POWER) return synth_trace<5>(seed, t, gbase, lbase, tab, o);
+    return synth_trace<3>(seed, t, gbase, lbase, tab, o);
+  };
   uint64_t base = 0;
-  for (uint64_t t = 0; t < t0; ++t)
-    base += config == 2 ? synth_trace<2>(seed, t, 0, 0, nullptr, nullptr) : synth_trace<3>(seed, t, 0, 0, nullptr, nullptr);
+  for (uint64_t t = 0; t < t0; ++t) base += gen(t, 0, 0, nullptr, nullptr);
   SynthOut o{span_id, parent_id, kind, shape, status, duration, timestamp};
   uint64_t off = 0;
   for (uint64_t t = t0; t < t1; ++t) {
-    uint32_t cnt = config == 2 ? synth_trace<2>(seed, t, 0, 0, nullptr, nullptr) : synth_trace<3>(seed, t, 0, 0, nullptr, nullptr);
+    const uint32_t cnt = gen(t, 0, 0, nullptr, nullptr);
     if (trace_off) trace_off[t - t0] = off;
     if (span_id && off + cnt > cap) return KMZ_E_ARG;
-    if (span_id) {
-      if (config == 2)
-        synth_trace<2>(seed, t, base + off, off, dt.data(), &o);
-      else
-        synth_trace<3>(seed, t, base + off, off, dt.data(), &o);
-    }
+    if (span_id) gen(t, base + off, off, dt.data(), &o);
     off += cnt;
   }
   if (trace_off) trace_off[t1 - t0] = off;

@@ -771,6 +771,8 @@ void launch_synth_count(hipStream_t s, int config, uint64_t seed, uint64_t t0, u
   if (!nt) return;
   if (config == 2)
     hipLaunchKernelGGL(k_synth_count<2>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, cnt);
+  else if (config == 5)
+    hipLaunchKernelGGL(k_synth_count<5>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, cnt);
   else
     hipLaunchKernelGGL(k_synth_count<3>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, cnt);
 }
@@ -780,6 +782,8 @@ void launch_synth_fill(hipStream_t s, int config, uint64_t seed, uint64_t t0, ui
   if (!nt) return;
   if (config == 2)
     hipLaunchKernelGGL(k_synth_fill<2>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, off, gbase, dur_table, out);
+  else if (config == 5)
+    hipLaunchKernelGGL(k_synth_fill<5>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, off, gbase, dur_table, out);
   else
     hipLaunchKernelGGL(k_synth_fill<3>, dim3(grid_for(nt)), dim3(256), 0, s, seed, t0, nt, off, gbase, dur_table, out);
 }

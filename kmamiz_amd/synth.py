@@ -1,4 +1,4 @@
-"""Synthetic Zipkin workloads of BASELINE.json (configs 2 and 3).
+"""Synthetic Zipkin workloads of BASELINE.json (configs 2, 3 and 5).
 
 The same C generator (``kmz_synth.h``) runs on the device
 (``Engine.load_synthetic``) and on the host (:func:`host_batch`), so tests can
@@ -16,7 +16,7 @@ import numpy as np
 from . import _lib as L
 from .engine import ShapeTable, SpanBatch
 
-BOOKINFO, MESH = L.SYNTH_BOOKINFO, L.SYNTH_MESH
+BOOKINFO, MESH, POWER = L.SYNTH_BOOKINFO, L.SYNTH_MESH, L.SYNTH_POWER
 SEED = 0x4B4D414D495A  # "KMAMIZ"
 STATUSES = ["200", "404", "500"]
 

@@ -78,6 +78,17 @@ def deps(batch, dep_ep: np.ndarray, n_ep: int):
         n, _p(batch.span_id), _p(batch.parent_id), _p(batch.kind), _p(batch.shape), _p(batch.timestamp), _p(ep),
         n_ep, cap, _p(keys), C.byref(nk), _p(last), _p(first), _p(ext), _p(counts),
     )
+    if rc == -4:  # more unique keys than 2n (deep chains): once more with the size it reported
+        cap = nk.value
+        keys = np.zeros(cap, np.uint64)
+        last[:] = 0
+        first[:] = 0
+        ext[:] = 0
+        counts[:] = 0
+        rc = lib().oracle_deps(
+            n, _p(batch.span_id), _p(batch.parent_id), _p(batch.kind), _p(batch.shape), _p(batch.timestamp), _p(ep),
+            n_ep, cap, _p(keys), C.byref(nk), _p(last), _p(first), _p(ext), _p(counts),
+        )
     if rc == -3:
         raise RuntimeError("cyclic parent chain")
     assert rc == 0, rc

@@ -273,7 +273,11 @@ int oracle_deps(uint64_t n, const uint64_t *sid, const uint64_t *pid, const uint
   for (uint64_t x = 0; x < nk; ++x)
     if (u == 0 || kk[x] != kk[u - 1]) kk[u++] = kk[x];
   if (keys) {
-    if (u > max_keys) return -1;
+    if (u > max_keys) {  /* the caller's key buffer is too small: report the size needed */
+      *n_keys = u;
+      free(kk);
+      return -4;
+    }
     memcpy(keys, kk, u * 8);
   }
   *n_keys = u;

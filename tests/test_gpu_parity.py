@@ -238,7 +238,7 @@ def _compare_synth(engine, batch, table):
     return info
 
 
-@pytest.mark.parametrize("config,ntr", [(2, 30000), (3, 4000), (3, 40000)])
+@pytest.mark.parametrize("config,ntr", [(2, 30000), (3, 4000), (3, 40000), (5, 2000), (5, 20000)])
 def test_synthetic_vs_c_oracle(engine, config, ntr):
     from kmamiz_amd import synth
 
@@ -260,7 +260,7 @@ def test_device_generation_equals_host(engine):
     from kmamiz_amd import _lib as L
     from kmamiz_amd import synth
 
-    for config, (t0, t1) in ((2, (5, 20000)), (3, (17, 3000))):
+    for config, (t0, t1) in ((2, (5, 20000)), (3, (17, 3000)), (5, (11, 2000))):
         batch, _ = synth.host_batch(config, t0, t1)
         table = synth.shape_table(config)
         engine.load(batch, table)
