@@ -58,6 +58,8 @@ struct kmz_ctx {
   DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
+  DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
+  bool ctab_dirty = true;  // the chain table holds entries no list records (new, or a list overflowed)
   int path = 0;             // kmz_info.path of the last dependency run
   bool sstats = false;      // shape-level K3 partials computed in this run
   bool chain_ran = false;   // this run's dependency graph came from k4_chain
@@ -255,7 +257,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->mkeys_in, &c->mtab};
+                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->hpin) hipHostFree(c->hpin);
@@ -494,17 +496,26 @@ static int run_deps(kmz_ctx *c, bool links) {
     const uint32_t nt = chain_tiles(n);
     // per persistent workgroup: staged keys of candidate new chains and
     // deferred chain checks (overflow is handled in place, just slower)
-    const uint32_t scap = 1u << 15, dcap = 1u << 12, ng = chain_grid(n);
+    // and the slots each workgroup claims in the chain table (wcap each; the
+    // run's global list of wcap more follows them)
+    const uint32_t scap = 1u << 15, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
+    void *old_ctab = c->ctab.p;
     if (ensure(c, c->ctab, c->ccap * 32) || ensure(c, c->tile_tmp, (size_t)nt * 16) ||
         ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, (size_t)ng * scap * 8) ||
         ensure(c, c->kstage_n, (size_t)ng * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 32) ||
-        ensure(c, c->kdefer_n, (size_t)ng * 4))
+        ensure(c, c->kdefer_n, (size_t)ng * 4) || ensure(c, c->kwpos, ((size_t)ng + 1) * wcap * 4) ||
+        ensure(c, c->kwpos_n, (size_t)ng * 4))
       return KMZ_E_HIP;
+    if (c->ctab.p != old_ctab) c->ctab_dirty = true;
+    uint32_t *wpos = P<uint32_t>(c->kwpos), *gpos = wpos + (size_t)ng * wcap;
     {
       Timed t(c, KMZ_K_MEMSET);
-      HIPCHK(c, hipMemsetAsync(c->ctab.p, 0, c->ccap * 32, c->stream));
+      // the chain table is cleared entry by entry after each run; a full
+      // memset only when it is new or a list overflowed
+      if (c->ctab_dirty) HIPCHK(c, hipMemsetAsync(c->ctab.p, 0, c->ccap * 32, c->stream));
       HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
     }
+    c->ctab_dirty = true;  // until this run's slots are cleared below
     {
       Timed t(c, KMZ_K_WALK);
       launch_chain(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
@@ -512,6 +523,7 @@ static int run_deps(kmz_ctx *c, bool links) {
                    P<unsigned long long>(c->trip), c->tcap, epp, links ? P<unsigned long long>(c->rowpos) : nullptr,
                    P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->tile_tmp), st, P<unsigned long long>(c->kstage),
                    scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
+                   wpos, wcap, P<uint32_t>(c->kwpos_n),
                    // (test knob 24 forces sig collisions on the first seed only)
                    c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)));
     }
@@ -519,13 +531,14 @@ static int run_deps(kmz_ctx *c, bool links) {
       Timed t(c, KMZ_K_SETTLE);
       launch_chain_settle(c->stream, n, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
                           P<uint32_t>(c->tile_tmp), st, P<unsigned long long>(c->kstage), scap,
-                          P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n));
+                          P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
+                          gpos, wcap);
     }
     {  // ancestries that left their window: one pass, sized on the device (no host round trip)
       Timed t(c, KMZ_K_PEND);
       launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent),
                         n, P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
-                        P<unsigned long long>(c->trip), c->tcap, epp, cnt, st);
+                        P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, wcap);
     }
     {
       Timed t(c, KMZ_K_FINAL);
@@ -534,7 +547,9 @@ static int run_deps(kmz_ctx *c, bool links) {
       launch_collapse_endpoints(c->stream, P<unsigned long long>(c->sgrp), c->n_shapes, c->n_status,
                                 P<uint32_t>(c->d_dep), c->n_dep, P<uint32_t>(c->cparent), c->index_base, epp,
                                 epp + c->n_dep, cnt);
+      launch_chain_clear(c->stream, n, c->ctab.p, wpos, wcap, P<uint32_t>(c->kwpos_n), gpos, wcap, cnt);
     }
+    c->ctab_dirty = false;  // (set again after the run if a list overflowed: F_CTAB_DIRTY)
     c->path = (joined ? 1 : 0) | 2;
     c->chain_ran = true;
     return KMZ_OK;
@@ -611,6 +626,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     HIPCHK(c, hipMemcpyAsync(s64, c->stats64.p, S_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
+    if (h[C_FLAGS] & F_CTAB_DIRTY) c->ctab_dirty = true;
     if ((flags & KMZ_RUN_DEPS) && (c->path & 1) && h[C_CERT]) {  // a repeated span id: the table path, same run
       c->table_hint = true;
       continue;

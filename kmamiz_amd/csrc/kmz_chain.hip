@@ -112,8 +112,11 @@ __device__ __forceinline__ void edge_insert(uint64_t key, unsigned long long *__
 // once all three are nonzero.
 // Insert (or join) the chain `sig`.  Returns 1 inserted, 2 found (and
 // checked), 0 not yet decidable (the winner has not published), -1 probe bound.
+// A slot this call claims is appended to the run's written list (gpos, counted
+// in counters[C_WPOS]) so that it can be cleared after the run.
 __device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, uint64_t ccap, uint64_t sig,
-                                         uint64_t psig, uint64_t epon, uint32_t *flags) {
+                                         uint64_t psig, uint64_t epon, uint32_t *flags, uint32_t *__restrict__ gpos,
+                                         uint32_t gcap, unsigned int *__restrict__ counters) {
   uint64_t pos = slot_of(sig, ccap);
   for (uint32_t z = 0; z < PROBE_MAX; ++z) {
     unsigned long long *e = ctab + 4 * pos;
@@ -121,6 +124,11 @@ __device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, 
     if (c == 0) {
       atomicExch(&e[1], (unsigned long long)psig);
       atomicExch(&e[2], (unsigned long long)epon);
+      const uint32_t x = atomicAdd(&counters[C_WPOS], 1u);  // (rare paths only)
+      if (x < gcap)
+        gpos[x] = (uint32_t)pos;
+      else
+        *flags |= F_CTAB_DIRTY;
       return 1;
     }
     if (c == sig) {
@@ -145,13 +153,15 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     unsigned long long *__restrict__ rowpos_out, uint32_t *__restrict__ plist, uint32_t pcap,
     unsigned int *__restrict__ counters, uint32_t *__restrict__ wg_stats, unsigned long long *__restrict__ stage,
     uint32_t scap, uint32_t *__restrict__ stage_n, unsigned long long *__restrict__ defer, uint32_t dcap,
-    uint32_t *__restrict__ defer_n, uint32_t nt, uint32_t ablate) {
+    uint32_t *__restrict__ defer_n, uint32_t *__restrict__ wpos, uint32_t wcap, uint32_t *__restrict__ wpos_n,
+    uint32_t nt, uint32_t ablate) {
   // one 16-byte record per window slot: element hash (x, y), endpoint (z),
   // contracted parent | kind << 16 (w) -- a walk step is one LDS read
   __shared__ uint4 lrec[CW];
   __shared__ unsigned long long lpow[WIN_DEPTH + 1];  // SIG_M^d
   __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP], imap_epon[IMAP];
   __shared__ uint32_t scnt, dcnt;  // keys staged for k_chain_settle, records deferred to k_chain_settle
+  __shared__ uint32_t wcnt;        // chain-table slots this workgroup claimed (cleared after the run)
   __shared__ uint32_t red[CTT / 64][4];
   // diagnostic phase clock (KMZ_ABLATE bit 22 only): s_memtime deltas by thread 0
   const bool dbg_t = (ablate & (1u << 22)) != 0;
@@ -180,7 +190,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
 #pragma unroll
     for (int q = 0; q < CPW; ++q) e[q] = dep_ep[sh[q] < n_shapes ? sh[q] : 0];
   };
-  if (threadIdx.x == 0) scnt = dcnt = 0;
+  if (threadIdx.x == 0) scnt = dcnt = wcnt = 0;
   if (threadIdx.x <= WIN_DEPTH) {
     uint64_t r = 1, b = SIG_M;
     for (uint32_t x = threadIdx.x; x; x >>= 1, b *= b)
@@ -388,6 +398,11 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         atomicExch(&en[1], (unsigned long long)ps[q]);
         atomicExch(&en[2], (unsigned long long)epon[q]);
         ++fresh_n;
+        const uint32_t x = atomicAdd(&wcnt, 1u);
+        if (x < wcap)
+          wpos[(uint64_t)blockIdx.x * wcap + x] = (uint32_t)pos[q];
+        else
+          flags |= F_CTAB_DIRTY;
       } else {  // joined an unpublished entry, or lost the slot to another chain
         const uint32_t x = atomicAdd(&dcnt, 1u);
         if (x < dcap) {
@@ -397,7 +412,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           r[2] = epon[q];
         } else {
           int rr = 0;
-          for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t) rr = chain_put(ctab, ccap, sg[q], ps[q], epon[q], &flags);
+          for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t)
+            rr = chain_put(ctab, ccap, sg[q], ps[q], epon[q], &flags, wpos + (uint64_t)gridDim.x * wcap, wcap,
+                           counters);  // (the run's global written list follows the per-workgroup ones)
           fresh_n += rr == 1;
         }
       }
@@ -453,6 +470,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   if (threadIdx.x == 0) {
     stage_n[blockIdx.x] = min(scnt, scap);
     defer_n[blockIdx.x] = min(dcnt, dcap);
+    wpos_n[blockIdx.x] = min(wcnt, wcap);
   }
   if (dbg_t && threadIdx.x == 0)
     for (int kk = 0; kk < 6; ++kk) atomicAdd(&g_chain_dbg[kk], tacc[kk]);
@@ -470,7 +488,8 @@ __global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *
                                                       unsigned long long *__restrict__ trip, uint64_t tcap,
                                                       unsigned long long *__restrict__ ctab, uint64_t ccap,
                                                       unsigned int *__restrict__ counters,
-                                                      unsigned long long *__restrict__ stats64) {
+                                                      unsigned long long *__restrict__ stats64,
+                                                      uint32_t *__restrict__ gpos, uint32_t gcap) {
   uint32_t flags = 0, fresh = 0;
   for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
     const uint32_t m = stage_n[w];
@@ -479,7 +498,8 @@ __global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *
     for (uint32_t x = threadIdx.x; x < md; x += blockDim.x) {
       const unsigned long long *r = defer + 4 * ((uint64_t)w * dcap + x);
       int rr = 0;
-      for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t) rr = chain_put(ctab, ccap, r[0], r[1], r[2], &flags);
+      for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t)
+        rr = chain_put(ctab, ccap, r[0], r[1], r[2], &flags, gpos, gcap, counters);
       fresh += rr == 1;
     }
   }
@@ -502,7 +522,8 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
                                                      unsigned long long *__restrict__ trip, uint64_t tcap,
                                                      unsigned long long *__restrict__ ep_ts,
                                                      unsigned int *__restrict__ counters,
-                                                     unsigned long long *__restrict__ stats64) {
+                                                     unsigned long long *__restrict__ stats64,
+                                                     uint32_t *__restrict__ gpos, uint32_t gcap) {
   const uint32_t m = min(counters[C_PLIST], pcap);
   uint32_t flags = 0;
   for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
@@ -538,7 +559,8 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     if (bad) continue;
     const uint64_t sg = sig_final(acc, d, seed), psig = a == NONE ? ROOT_SIG : sig_final(pacc, d - 1, seed);
     int r = 0;
-    for (uint32_t t = 0; t < 1u << 20 && r == 0; ++t) r = chain_put(ctab, ccap, sg, psig, epon_of(es, on), &flags);
+    for (uint32_t t = 0; t < 1u << 20 && r == 0; ++t)
+      r = chain_put(ctab, ccap, sg, psig, epon_of(es, on), &flags, gpos, gcap, counters);
     if (r <= 0) continue;
     if (on) {  // a row: its relations, keys (new chain) and non-SERVER ancestors
       uint32_t kk = 0;
@@ -602,25 +624,55 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint64_t tcap, unsigned long long *ep_ts, unsigned long long *rowpos, uint32_t *plist,
                   uint32_t pcap, unsigned int *counters, uint32_t *wg_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
-                  uint32_t dcap, uint32_t *defer_n, uint32_t ablate) {
+                  uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
+                  uint32_t ablate) {
   const uint32_t nt = chain_tiles(n);
   if (!nt) return;
   const uint32_t g = chain_grid(n);
   unsigned long long *tab = reinterpret_cast<unsigned long long *>(ctab);
   hipLaunchKernelGGL(k4_chain, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, dep_ep, n_shapes, n_ep,
                      index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
-                     scap, stage_n, defer, dcap, defer_n, nt, ablate);
+                     scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, ablate);
 }
 
 void launch_chain_settle(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip, uint64_t tcap,
                          unsigned int *counters, const uint32_t *wg_stats, unsigned long long *stats64,
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
-                         const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n) {
+                         const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
+                         uint32_t gcap) {
   if (!chain_tiles(n)) return;
   const uint32_t g = chain_grid(n);
   hipLaunchKernelGGL(k_chain_settle, dim3(g), dim3(256), 0, s, stage, scap, stage_n, defer, dcap, defer_n, g, trip,
-                     tcap, reinterpret_cast<unsigned long long *>(ctab), ccap, counters, stats64);
+                     tcap, reinterpret_cast<unsigned long long *>(ctab), ccap, counters, stats64, gpos, gcap);
   launch_tile_sum(s, wg_stats, g, 4u, 4u, stats64 + S_ROWS, 2u);  // rows, rel, maxd, chains
+}
+
+// zero the chain-table entries this run wrote: the per-workgroup lists of the
+// tile kernel and the run's global list (settle / pending / inline inserts)
+__global__ void __launch_bounds__(256) k_chain_clear(unsigned long long *__restrict__ ctab,
+                                                     const uint32_t *__restrict__ wpos, uint32_t wcap,
+                                                     const uint32_t *__restrict__ wpos_n, uint32_t nwg,
+                                                     const uint32_t *__restrict__ gpos, uint32_t gcap,
+                                                     const unsigned int *__restrict__ counters) {
+  auto clear = [&](uint32_t p) {
+    ulonglong2 *e = reinterpret_cast<ulonglong2 *>(ctab + 4 * (uint64_t)p);
+    e[0] = make_ulonglong2(0, 0);
+    e[1] = make_ulonglong2(0, 0);
+  };
+  for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
+    const uint32_t m = wpos_n[w];
+    for (uint32_t x = threadIdx.x; x < m; x += 256) clear(wpos[(uint64_t)w * wcap + x]);
+  }
+  const uint32_t mg = min(counters[C_WPOS], gcap);
+  for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < mg; x += gridDim.x * 256) clear(gpos[x]);
+}
+
+void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
+                        const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters) {
+  if (!chain_tiles(n)) return;
+  const uint32_t g = chain_grid(n);
+  hipLaunchKernelGGL(k_chain_clear, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long *>(ctab), wpos,
+                     wcap, wpos_n, g, gpos, gcap, counters);
 }
 
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,
@@ -628,10 +680,10 @@ void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, cons
                        const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
-                       unsigned long long *stats64) {
+                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap) {
   hipLaunchKernelGGL(k4_chain_pend, dim3(1024), dim3(256), 0, s, plist, pcap, kind, shape, ts, cparent, n, dep_ep,
                      n_shapes, n_ep, seed, reinterpret_cast<unsigned long long *>(ctab), ccap, trip, tcap, ep_ts,
-                     counters, stats64);
+                     counters, stats64, gpos, gcap);
 }
 
 }  // namespace kmz

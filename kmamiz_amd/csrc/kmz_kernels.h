@@ -21,6 +21,7 @@ enum {
   C_PEND = 4,
   C_CERT = 5,
   C_PLIST = 6,  // K4 spans whose ancestry leaves their LDS window (pending list length)
+  C_WPOS = 7,   // K4 chain-table slots written outside the tile kernel (cleared after the run)
   C_COUNT = 8
 };
 // C_CERT bits: the window join's answers cannot be used (global table path)
@@ -79,20 +80,25 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint64_t tcap, unsigned long long *ep_ts, unsigned long long *rowpos, uint32_t *plist,
                   uint32_t pcap, unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
-                  uint32_t dcap, uint32_t *defer_n, uint32_t ablate = 0);
+                  uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
+                  uint32_t ablate = 0);
 uint32_t chain_grid(uint32_t n);
 void launch_key_insert(hipStream_t s, const unsigned long long *keys, uint64_t n, unsigned long long *trip,
                        uint64_t tcap, unsigned int *counters);
 void launch_chain_settle(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip, uint64_t tcap,
                          unsigned int *counters, const uint32_t *wg_stats, unsigned long long *stats64,
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
-                         const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n);
+                         const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
+                         uint32_t gcap);
+// zero the chain-table entries this run wrote (instead of a memset of the table)
+void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
+                        const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,
                        const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, uint32_t n,
                        const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
-                       unsigned long long *stats64);
+                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap);
 // shape-level K3 partials -> endpoint groups / dependency-endpoint records
 void launch_collapse_groups(hipStream_t s, const unsigned long long *sg, uint32_t n_shapes, uint32_t S,
                             const uint32_t *map, uint32_t n_ep, unsigned long long *grp, unsigned int *counters);
