@@ -16,4 +16,5 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KR" -d g
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KR" -d gpurun_out/pmcw_$TAG -o pmc -- python3 bench.py --steps 2 --warmup 1 --cpu-seconds 0 > gpurun_out/pmcw_$TAG.log 2>&1 || exit 1
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-seconds ${CPU_SECONDS:-0} > gpurun_out/bench_mesh_$TAG.json 2>gpurun_out/bench_mesh_$TAG.err || exit 1
 timeout -k 10 200 python bench.py --config bookinfo --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/bench_book_$TAG.json 2>gpurun_out/bench_book_$TAG.err || exit 1
+timeout -k 10 300 python bench.py --config power --steps 10 --warmup 3 --cpu-seconds 0 > gpurun_out/bench_power_$TAG.json 2>gpurun_out/bench_power_$TAG.err || exit 1
 echo DONE
