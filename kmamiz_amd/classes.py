@@ -361,8 +361,84 @@ class CombinedRealtimeDataList:
             )
         return CombinedRealtimeDataList(out)
 
-    def toHistoricalData(self, *a, **k):
-        raise NotImplementedError("minute bucketing / history is SURVEY.md 8f item 4 (next)")
+    def toHistoricalData(self, serviceDependencies: List[dict], replicas: Optional[List[dict]] = None,
+                         labelMap: Optional[Dict[str, str]] = None) -> List[dict]:
+        """CombinedRealtimeDataList.ts:26-150, host side:
+        the combined rows (one per endpoint x status, already reduced on the
+        GPU) are bucketed by the UTC minute of their latestTimestamp
+        (Utils.BelongsToMinuteTimestamp, Utils.ts:135-141); each minute gets its
+        endpoint and service summaries and RiskAnalyzer.RealtimeRisk
+        (RiskAnalyzer.ts:10-49).  ``date`` is the ISO string of the JSON form."""
+        import datetime
+
+        from .risk import realtime_risk
+
+        def minute(ts_ms: float) -> int:
+            return (math.trunc(ts_ms) // 60000) * 60000  # Date truncates, the ISO minute floors
+
+        def iso(ms: int) -> str:
+            d = datetime.datetime(1970, 1, 1) + datetime.timedelta(milliseconds=ms)
+            return d.strftime("%Y-%m-%dT%H:%M:%S.") + f"{ms % 1000:03d}Z"
+
+        def mean_of(rows, ok) -> float:
+            vals = [r["latency"]["mean"] for r in rows if ok(r["latency"].get("mean"))]
+            if not vals:
+                return 0
+            acc = 0.0
+            for v in vals:  # left-to-right, as Array.reduce
+                acc += v
+            m = acc / len(vals)
+            return m if math.isfinite(m) else 0
+
+        buckets: Dict[int, List[dict]] = {}
+        for r in self._data:
+            buckets.setdefault(minute(r["latestTimestamp"] / 1000), []).append(r)
+        out = []
+        for t, rows in buckets.items():
+            risks = {x["uniqueServiceName"]: x for x in reversed(realtime_risk(rows, serviceDependencies, replicas or []))}
+            by_ep: Dict[str, List[dict]] = {}
+            by_svc: Dict[str, List[dict]] = {}
+            for r in rows:
+                by_ep.setdefault(r["uniqueEndpointName"], []).append(r)
+                by_svc.setdefault(r["uniqueServiceName"], []).append(r)
+            endpoints = []
+            for uen, rs in by_ep.items():
+                svc, ns, ver, method = (uen.split("\t") + [None] * 4)[:4]
+                e = {
+                    "latencyMean": mean_of(rs, lambda m: m is not None),
+                    "latencyCV": max((r["latency"].get("cv") or 0) for r in rs),
+                    "method": method,
+                    "requestErrors": sum(r["combined"] for r in rs if str(r["status"]).startswith("4")),
+                    "requests": sum(r["combined"] for r in rs),
+                    "serverErrors": sum(r["combined"] for r in rs if str(r["status"]).startswith("5")),
+                    "uniqueEndpointName": uen,
+                    "uniqueServiceName": f"{svc}\t{ns}\t{ver}",
+                }
+                if labelMap and uen in labelMap:
+                    e["labelName"] = labelMap[uen]
+                endpoints.append(e)
+            services = []
+            for usn, rs in by_svc.items():
+                svc, ns, ver = (usn.split("\t") + [None] * 3)[:3]
+                mine = [e for e in endpoints if e["uniqueServiceName"] == usn]
+                svc_info = {
+                    "date": iso(t),
+                    "endpoints": mine,
+                    "service": svc,
+                    "namespace": ns,
+                    "version": ver,
+                    "requests": sum(e["requests"] for e in mine),
+                    "requestErrors": sum(e["requestErrors"] for e in mine),
+                    "serverErrors": sum(e["serverErrors"] for e in mine),
+                    "latencyMean": mean_of(rs, lambda m: isinstance(m, (int, float)) and math.isfinite(m)),
+                    "latencyCV": max((r["latency"].get("cv") or 0) for r in rs),
+                    "uniqueServiceName": usn,
+                }
+                if "norm" in risks[usn]:  # (BetweenFixedNumber of equal risks gives one value: Normalizer.ts:22)
+                    svc_info["risk"] = risks[usn]["norm"]
+                services.append(svc_info)
+            out.append({"date": iso(t), "services": services})
+        return out
 
     def extractEndpointDataType(self, *a, **k):
         raise NotImplementedError("endpoint schema inference is out of scope (SURVEY.md 2)")

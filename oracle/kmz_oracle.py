@@ -100,6 +100,21 @@ def js_round(x: float) -> float:
     return float(r)
 
 
+def belongs_to_minute(ts_ms: float) -> int:
+    """Utils.BelongsToMinuteTimestamp (Utils.ts:135-141): new Date(ts) truncates
+    the time value toward zero; the ISO string then names its UTC minute."""
+    ms = math.trunc(ts_ms)
+    return (ms // 60000) * 60000
+
+
+def iso_minute(ms: int) -> str:
+    """Date.prototype.toISOString of a whole-minute time value."""
+    import datetime
+
+    d = datetime.datetime(1970, 1, 1) + datetime.timedelta(milliseconds=ms)
+    return d.strftime("%Y-%m-%dT%H:%M:%S.") + f"{ms % 1000:03d}Z"
+
+
 def to_precise(num: float) -> float:
     """Utils.ToPrecise (Utils.ts:311-313)."""
     return js_round((num + EPSILON) * 1e14) / 1e14
@@ -497,6 +512,84 @@ class CombinedRealtimeDataList:
 
     def adjustTimestamp(self, to):
         return CombinedRealtimeDataList([{**r, "latestTimestamp": to * 1000} for r in self._data])
+
+    def toHistoricalData(self, serviceDependencies, replicas=None, labelMap=None):
+        """CombinedRealtimeDataList.ts:26-150: rows bucketed by the minute of their
+        latestTimestamp (Utils.BelongsToMinuteTimestamp, Utils.ts:135-141), then
+        per minute the endpoint and service summaries and RiskAnalyzer.RealtimeRisk.
+        Dates are given as the ISO strings their JSON form has."""
+        replicas = replicas or []
+        dates: Dict[int, List[dict]] = {}
+        for r in self._data:
+            dates.setdefault(belongs_to_minute(r["latestTimestamp"] / 1000), []).append(r)
+        out = []
+        for time, daily in dates.items():
+            risks = RiskAnalyzer.RealtimeRisk(daily, serviceDependencies, replicas)
+            emap: Dict[str, List[dict]] = {}
+            smap: Dict[str, List[dict]] = {}
+            for r in daily:
+                emap.setdefault(r["uniqueEndpointName"], []).append(r)
+                smap.setdefault(r["uniqueServiceName"], []).append(r)
+            eps = []
+            for uen, rows in emap.items():
+                tok = uen.split("\t")
+                req = rerr = serr = 0
+                for c in rows:
+                    req += c["combined"]
+                    if str(c["status"]).startswith("4"):
+                        rerr += c["combined"]
+                    if str(c["status"]).startswith("5"):
+                        serr += c["combined"]
+                valid = [c for c in rows if get(c["latency"], "mean") is not UNDEF and c["latency"].get("mean") is not None]
+                tot = 0.0
+                for c in valid:
+                    tot = tot + c["latency"]["mean"]
+                mean = tot / len(valid) if valid else math.nan
+                e = {
+                    "latencyMean": mean if math.isfinite(mean) else 0,
+                    "latencyCV": max((c["latency"].get("cv") or 0) for c in rows),
+                    "method": tok[3] if len(tok) > 3 else UNDEF,
+                    "requestErrors": rerr,
+                    "requests": req,
+                    "serverErrors": serr,
+                    "uniqueEndpointName": uen,
+                    "uniqueServiceName": "\t".join(tok[:3]) if len(tok) >= 3 else UNDEF,
+                }
+                if labelMap is not None and uen in labelMap:
+                    e["labelName"] = labelMap[uen]
+                eps.append(strip_undef(e))
+            svcs = []
+            for usn, rows in smap.items():
+                tok = usn.split("\t")
+                mine = [e for e in eps if e.get("uniqueServiceName") == usn]
+                req = rerr = serr = 0
+                for e in mine:
+                    rerr += e["requestErrors"]
+                    serr += e["serverErrors"]
+                    req += e["requests"]
+                valid = [c for c in rows if isinstance(c["latency"].get("mean"), (int, float))
+                         and math.isfinite(c["latency"]["mean"])]
+                tot = 0.0
+                for c in valid:
+                    tot = tot + c["latency"]["mean"]
+                mean = tot / len(valid) if valid else math.nan
+                risk = next(x for x in risks if x["uniqueServiceName"] == usn)
+                svcs.append(strip_undef({
+                    "date": iso_minute(time),
+                    "endpoints": mine,
+                    "service": tok[0],
+                    "namespace": tok[1] if len(tok) > 1 else UNDEF,
+                    "version": tok[2] if len(tok) > 2 else UNDEF,
+                    "requests": req,
+                    "requestErrors": rerr,
+                    "serverErrors": serr,
+                    "latencyMean": mean if math.isfinite(mean) else 0,
+                    "latencyCV": max((c["latency"].get("cv") or 0) for c in rows),
+                    "uniqueServiceName": usn,
+                    "risk": risk.get("norm", UNDEF),
+                }))
+            out.append({"date": iso_minute(time), "services": svcs})
+        return out
 
     def combineWith(self, other: "CombinedRealtimeDataList"):
         """CombinedRealtimeDataList.ts:183-263 (body/schema merge out of scope)."""

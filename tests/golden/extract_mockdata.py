@@ -9,7 +9,7 @@ The reference keeps its fixtures as TypeScript object literals in
 literal out of the file, drops the ``: Type[]`` annotation of its ``const``
 line, and lets the local Node (v12) evaluate the literal with the few free
 identifiers it references bound to fixed stand-ins (``Yesterday``/``Today`` are
-pinned to constants so the output is deterministic).  Only the resulting JSON
+pinned to constants, and so is ``Date.now``, so the output is deterministic).  Only the resulting JSON
 *data* is committed under ``tests/fixtures/``; no reference source is kept.
 Properties whose value is ``undefined`` are dropped, exactly as Jest's
 ``toEqual`` ignores them.
@@ -28,6 +28,7 @@ TODAY = 1700000000000
 YESTERDAY = TODAY - 86400000
 
 PRELUDE = f"""
+Date.now = () => {TODAY};
 const Today = {TODAY};
 const Yesterday = {YESTERDAY};
 const Service = "srv";
@@ -54,6 +55,7 @@ WANT = {
         "MockReplicas",
         "MockDependencies",
         "MockEndpointInfoPDAS1",
+        "MockHistoricalData",
     ],
     "MockData2.ts": ["traces"],
 }

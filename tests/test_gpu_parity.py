@@ -496,3 +496,35 @@ def test_merge_triples_is_the_union_of_shards(engine):
     foreign = np.unique(rng.integers(1, 2**62, size=300000, dtype=np.uint64))
     engine.merge_triples(foreign.ctypes.data, len(foreign), False)
     assert np.array_equal(engine.triples(), np.union1d(full, foreign))
+
+
+@pytest.mark.parametrize("fx", ["MockTracePDAS", "MockTrace", "MockData2_traces"])
+def test_fixture_historical_data_vs_oracle(engine, fx):
+    """The whole worker step of ServiceOperator.ts:153-160 on the fixtures:
+    GPU stats + GPU dependency graph -> service dependencies ->
+    CombinedRealtimeDataList.toHistoricalData (host)."""
+    traces = fixture(fx)
+    if fx != "MockTrace":
+        traces = [traces]
+    ours, ref = _run_both(traces)
+    reps = [{"uniqueServiceName": "details\tbook\tv1", "replicas": 3}]
+    sdep = ours.toEndpointDependencies().toServiceDependencies()
+    got = ours.combineLogsToRealtimeData([], reps).toCombinedRealtimeData().toHistoricalData(sdep, reps)
+    rsdep = ref.toEndpointDependencies().toServiceDependencies()
+    exp = ref.combineLogsToRealtimeData([], reps).toCombinedRealtimeData().toHistoricalData(rsdep, reps)
+    exp = O.strip_undef(exp)
+    assert len(got) == len(exp)
+    for g, e in zip(got, exp):
+        assert g["date"] == e["date"]
+        assert len(g["services"]) == len(e["services"])
+        for gs, es in zip(g["services"], e["services"]):
+            for k in ("service", "namespace", "version", "requests", "requestErrors", "serverErrors",
+                      "uniqueServiceName", "date"):
+                assert gs.get(k) == es.get(k), k
+            assert ("risk" in gs) == ("risk" in es)
+            if "risk" in es:
+                assert gs["risk"] == pytest.approx(es["risk"], rel=REL, abs=1e-13)
+            assert gs["latencyMean"] == pytest.approx(es["latencyMean"], rel=REL, abs=0)
+            assert gs["latencyCV"] == pytest.approx(es["latencyCV"], rel=REL, abs=1e-13)
+            assert [x["uniqueEndpointName"] for x in gs["endpoints"]] == [x["uniqueEndpointName"]
+                                                                           for x in es["endpoints"]]

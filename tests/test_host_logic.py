@@ -178,3 +178,61 @@ def test_product_risk_matches_oracle():
            [(r["uniqueServiceName"], r["norm"], r["risk"]) for r in exp]
     assert risk.Normalizer.Strategy.BetweenFixedNumber([1, 2, 3]) == [0.1, 0.55, 1]
     assert risk.Normalizer.Strategy.Linear([1, 2, 3]) == [0.4, 0.7, 1]
+
+
+# ---------------------------------------------------------------------------
+# CombinedRealtimeDataList.toHistoricalData
+# ---------------------------------------------------------------------------
+def _fx(name):
+    import json
+    import os
+
+    return json.load(open(os.path.join(os.path.dirname(__file__), "fixtures", f"{name}.json")))
+
+
+def test_historical_data_oracle_matches_reference_fixture():
+    """CombinedRealtimeDataList.test.ts:14-18 (MockHistoricalData)."""
+    from oracle import kmz_oracle as O
+
+    got = O.CombinedRealtimeDataList(_fx("MockBaseCrlData1")).toHistoricalData(_fx("MockDependencies"),
+                                                                               _fx("MockReplicas"))
+    assert got == _fx("MockHistoricalData")
+
+
+def test_historical_data_mirror_matches_reference_fixture():
+    from kmamiz_amd.classes import CombinedRealtimeDataList
+
+    got = CombinedRealtimeDataList(_fx("MockBaseCrlData1")).toHistoricalData(_fx("MockDependencies"),
+                                                                             _fx("MockReplicas"))
+    assert got == _fx("MockHistoricalData")
+
+
+def test_historical_data_mirror_matches_oracle_on_many_minutes():
+    """Rows spread over several minutes and services, with 4xx/5xx statuses and
+    a missing mean: the mirror and the oracle agree exactly."""
+    import copy
+    import random
+
+    from kmamiz_amd.classes import CombinedRealtimeDataList
+    from oracle import kmz_oracle as O
+
+    rng = random.Random(5)
+    base = _fx("MockBaseCrlData1")[0]
+    rows = []
+    for i in range(300):
+        r = copy.deepcopy(base)
+        svc = f"s{rng.randrange(6)}"
+        r["service"], r["uniqueServiceName"] = svc, f"{svc}\tns\tlatest"
+        r["uniqueEndpointName"] = f"{svc}\tns\tlatest\tGET\thttp://{svc}/api/{rng.randrange(4)}"
+        r["status"] = rng.choice(["200", "404", "500", "201"])
+        r["combined"] = rng.randrange(1, 50)
+        r["latestTimestamp"] = (1700000000000 + rng.randrange(0, 5 * 60000)) * 1000 + rng.randrange(1000)
+        r["latency"] = {"mean": rng.random() * 100, "cv": rng.random()}
+        if i % 37 == 0:
+            del r["latency"]["mean"]
+        rows.append(r)
+    deps = _fx("MockDependencies")
+    exp = O.CombinedRealtimeDataList(copy.deepcopy(rows)).toHistoricalData(deps, _fx("MockReplicas"))
+    got = CombinedRealtimeDataList(copy.deepcopy(rows)).toHistoricalData(deps, _fx("MockReplicas"))
+    assert len(got) >= 5  # (the range starts 20 s into a minute)
+    assert got == exp
