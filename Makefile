@@ -4,7 +4,7 @@ ARCH ?= gfx950
 HIPFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
 SRC = kmamiz_amd/csrc/kmz_kernels.hip kmamiz_amd/csrc/kmz_part.hip kmamiz_amd/csrc/kmz_join.hip kmamiz_amd/csrc/kmz_chain.hip kmamiz_amd/csrc/kmz_api.hip
 HDR = include/kmz.h kmamiz_amd/csrc/kmz_common.h kmamiz_amd/csrc/kmz_synth.h kmamiz_amd/csrc/kmz_kernels.h
-OBJ = build/kmz_kernels.o build/kmz_part.o build/kmz_join.o build/kmz_chain.o build/kmz_api.o
+OBJ = build/kmz_kernels.o build/kmz_part.o build/kmz_join.o build/kmz_chain.o build/kmz_api.o build/kmz_ingest.o
 
 all: kmamiz_amd/libkmz.so oracle addon
 
@@ -12,8 +12,13 @@ build/%.o: kmamiz_amd/csrc/%.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# host-only sources (the Zipkin JSON ingest)
+build/%.o: kmamiz_amd/csrc/%.cpp include/kmz.h
+	@mkdir -p build
+	g++ -O3 -std=c++17 -fPIC -Wall -pthread -c $< -o $@
+
 kmamiz_amd/libkmz.so: $(OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -pthread -o $@ $(OBJ)
 
 oracle:
 	$(MAKE) -C oracle

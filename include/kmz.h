@@ -67,6 +67,7 @@ extern "C" {
 #define KMZ_E_OVERFLOW -6 /* internal table overflow (retried internally; surfaced if persistent) */
 #define KMZ_E_STATE -7    /* call order (e.g. kmz_get_* before kmz_run) */
 #define KMZ_E_RCCL -8     /* collective failed */
+#define KMZ_E_UNSUPPORTED -9 /* input outside a fast path's domain: the caller takes the general path */
 
 /* kmz_run flags */
 #define KMZ_RUN_STATS_RT 1u  /* group by toRealTimeData identity (Traces.ts:32-46) */
@@ -134,6 +135,34 @@ typedef struct kmz_info {
                            bit 1 chain-interning walk (else per-relation global walk) */
   uint64_t n_chains;    /* distinct interned ancestor chains (chain-interning path) */
 } kmz_info;
+
+/* ---- host ingest: Zipkin JSON -> kmz_spans columns ---- */
+/* Parses the Trace[][] JSON that ZipkinService.getTraceListFromZipkinByServiceName
+ * returns (ZipkinService.ts:44-57; span shape Trace.ts:1-38) in flatten order
+ * (Traces.ts:29).  Shapes are interned by the raw JSON text of `name` and the
+ * six identity tags, statuses by that of tags["http.status_code"]; each comes
+ * back as (byte offset, length) slices into `json` (length KMZ_JSON_ABSENT:
+ * the property is missing), for the caller's once-per-shape identity rules.
+ * Returns KMZ_E_UNSUPPORTED (nothing parsed) for input outside the fast path:
+ * ids that are not 16 lowercase hex digits, non-integer or out-of-range
+ * duration/timestamp, escaped keys or kinds, non-object tags.  threads <= 0:
+ * all hardware threads. */
+#define KMZ_JSON_ABSENT 0xFFFFFFFFFFFFFFFFull
+typedef struct kmz_zipkin_batch {
+  uint64_t n;
+  uint64_t *span_id, *parent_id; /* parent 0: absent, "" or null (falsy)        */
+  uint8_t *kind;
+  uint32_t *shape, *status;      /* ids into shape_fields / status_fields       */
+  uint32_t *duration;
+  int64_t *timestamp;
+  uint32_t n_shapes, n_statuses;
+  uint64_t *shape_fields;  /* [n_shapes][7][offset, length]: name, http.method, http.url,
+                              istio.canonical_revision, istio.canonical_service,
+                              istio.namespace, istio.mesh_id */
+  uint64_t *status_fields; /* [n_statuses][offset, length] */
+} kmz_zipkin_batch;
+int kmz_parse_zipkin(const char *json, uint64_t len, int threads, kmz_zipkin_batch **out);
+void kmz_zipkin_free(kmz_zipkin_batch *batch);
 
 /* ---- lifecycle ---------------------------------------------------------- */
 int kmz_abi_version(void);

@@ -100,6 +100,27 @@ GROUP_DTYPE = np.dtype(
 )
 ENDPOINT_DTYPE = np.dtype([("last_ts", "<i8"), ("first_row", "<u8"), ("external", "<u4"), ("has_row", "<u4")])
 
+class ZipkinBatch(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64),
+        ("span_id", C.POINTER(C.c_uint64)),
+        ("parent_id", C.POINTER(C.c_uint64)),
+        ("kind", C.POINTER(C.c_uint8)),
+        ("shape", C.POINTER(C.c_uint32)),
+        ("status", C.POINTER(C.c_uint32)),
+        ("duration", C.POINTER(C.c_uint32)),
+        ("timestamp", C.POINTER(C.c_int64)),
+        ("n_shapes", C.c_uint32),
+        ("n_statuses", C.c_uint32),
+        ("shape_fields", C.POINTER(C.c_uint64)),
+        ("status_fields", C.POINTER(C.c_uint64)),
+    ]
+
+
+E_UNSUPPORTED = -9
+JSON_ABSENT = 0xFFFFFFFFFFFFFFFF
+
+
 # (name, restype, argtypes) for every symbol declared in include/kmz.h
 _P = C.c_void_p
 SIGNATURES = [
@@ -121,6 +142,8 @@ SIGNATURES = [
     ("kmz_partials_size", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
     ("kmz_partials_copy", C.c_int, [_P, C.c_int, _P, C.c_uint64, C.c_int, C.c_int]),
     ("kmz_merge_triples", C.c_int, [_P, _P, C.c_uint64, C.c_int]),
+    ("kmz_parse_zipkin", C.c_int, [C.c_char_p, C.c_uint64, C.c_int, C.POINTER(C.POINTER(ZipkinBatch))]),
+    ("kmz_zipkin_free", None, [C.POINTER(ZipkinBatch)]),
     ("kmz_finalize", C.c_int, [_P]),
     ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
     ("kmz_host_alloc", _P, [C.c_uint64]),

@@ -22,7 +22,8 @@ import numpy as np
 
 from . import _lib as L
 from .engine import Engine
-from .ingest import UNDEFINED, Dictionary, dep_identity, explode_url, ingest_rows, ingest_traces, js_truthy, tpl
+from .ingest import (UNDEFINED, Dictionary, dep_identity, explode_url, ingest_json, ingest_rows, ingest_traces,
+                     js_truthy, tpl)
 
 _engines: Dict[int, Engine] = {}
 
@@ -42,11 +43,55 @@ def _clean(d: dict) -> dict:
 # ------------------------------------------------------------------------------
 # Traces
 # ------------------------------------------------------------------------------
+class _LazyFlat:
+    """The flattened span dicts of a Traces built from raw JSON, parsed only if
+    a per-span object is ever materialised (small batches)."""
+
+    def __init__(self, owner: "Traces"):
+        self._owner = owner
+        self._flat = None
+
+    def _get(self):
+        if self._flat is None:
+            self._flat = [s for t in self._owner._traces for s in t]
+        return self._flat
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __len__(self):
+        return len(self._get())
+
+
 class Traces:
     def __init__(self, traces, engine: Optional[Engine] = None):
-        self._traces = traces
+        self._traces_v = traces
+        self._raw = None
         self._engine = engine
         self._ingested = None
+
+    @classmethod
+    def from_json(cls, data: bytes, engine: Optional[Engine] = None, threads: int = 0) -> "Traces":
+        """Traces of a raw Zipkin response (Trace[][] JSON bytes, as
+        ZipkinService.ts:44-57 receives it): columns come from the native
+        parser (kmz_parse_zipkin) without building span
+        objects; the JSON is parsed into objects only if a per-span result is
+        materialised, or if the batch is outside the parser's fast path."""
+        t = cls(None, engine)
+        t._raw = bytes(data)
+        t._threads = threads
+        return t
+
+    @property
+    def _traces(self):
+        if self._traces_v is None and self._raw is not None:
+            import json
+
+            self._traces_v = json.loads(self._raw)
+        return self._traces_v
 
     def toJSON(self):
         return self._traces
@@ -54,7 +99,8 @@ class Traces:
     # -- plumbing -------------------------------------------------------------
     def _ingest(self):
         if self._ingested is None:
-            self._ingested = ingest_traces(self._traces)
+            r = ingest_json(self._raw, threads=self._threads) if self._raw is not None else None
+            self._ingested = (r[0], r[1], _LazyFlat(self)) if r is not None else ingest_traces(self._traces)
         return self._ingested
 
     def _load(self) -> Engine:

@@ -374,3 +374,57 @@ def ingest_rows(rows: Sequence[dict]):
     n_ids = np.arange(1, n + 1, dtype=np.uint64)
     batch = SpanBatch(n_ids, np.zeros(n, np.uint64), kind, shape, status, dur, ts, 0)
     return batch, table, d, first_row
+
+
+def ingest_json(data: bytes, index_base: int = 0, threads: int = 0):
+    """Zipkin Trace[][] JSON bytes -> (SpanBatch, Dictionary) through the native
+    parser (kmz_parse_zipkin), or None when the batch is
+    outside its fast path (the caller then parses it the general way).  The
+    identity rules run once per distinct shape, on json.loads of the raw
+    field slices the parser returns."""
+    import ctypes as C
+    import json
+
+    from . import _lib as L
+
+    out = C.POINTER(L.ZipkinBatch)()
+    rc = L.lib().kmz_parse_zipkin(data, len(data), threads, C.byref(out))
+    if rc == L.E_UNSUPPORTED:
+        return None
+    L.check(None, rc)
+    try:
+        b = out.contents
+        n = int(b.n)
+
+        def col(ptr, dtype):
+            return np.ctypeslib.as_array(ptr, shape=(max(1, n),))[:n].astype(dtype, copy=True)
+
+        sid, pid = col(b.span_id, np.uint64), col(b.parent_id, np.uint64)
+        kind, dur, ts = col(b.kind, np.uint8), col(b.duration, np.uint32), col(b.timestamp, np.int64)
+        shp, sts = col(b.shape, np.uint32), col(b.status, np.uint32)
+        absent = L.JSON_ABSENT
+        ns, nt = int(b.n_shapes), int(b.n_statuses)
+        sf = np.ctypeslib.as_array(b.shape_fields, shape=(max(1, ns) * 14,))[: ns * 14].reshape(ns * 7, 2)
+        tf = np.ctypeslib.as_array(b.status_fields, shape=(max(1, nt) * 2,))[: nt * 2].reshape(nt, 2)
+        # every raw field slice decoded by one json.loads of "[s0,s1,...]"
+        fields = np.concatenate([sf, tf]).tolist()
+        present = [ln != absent for _, ln in fields]
+        dec = iter(json.loads(b"[" + b",".join(data[o:o + ln] for (o, ln), p in zip(fields, present) if p) + b"]"))
+        vals = [next(dec) if p else UNDEFINED for p in present]
+
+        d = Dictionary()
+        smap = np.zeros(max(1, ns), dtype=np.uint32)
+        for i in range(ns):
+            v = vals[7 * i:7 * i + 7]
+            tags = {t: x for t, x in zip(SHAPE_TAGS, v[1:]) if x is not UNDEFINED}
+            smap[i] = d.shape_id(v[0], tags)
+        tmap = np.zeros(max(1, nt), dtype=np.uint32)
+        for i in range(nt):
+            tmap[i] = d.status_id(vals[7 * ns + i])
+    finally:
+        L.lib().kmz_zipkin_free(out)
+    if len(d.statuses) > 65535:
+        raise ValueError("more than 65535 distinct status strings")
+    batch = SpanBatch(sid, pid, kind, smap[shp] if n else shp, (tmap[sts] if n else sts).astype(np.uint16), dur,
+                      ts, index_base)
+    return batch, d

@@ -528,3 +528,27 @@ def test_fixture_historical_data_vs_oracle(engine, fx):
             assert gs["latencyCV"] == pytest.approx(es["latencyCV"], rel=REL, abs=1e-13)
             assert [x["uniqueEndpointName"] for x in gs["endpoints"]] == [x["uniqueEndpointName"]
                                                                            for x in es["endpoints"]]
+
+
+@pytest.mark.parametrize("src", ["MockTracePDAS", "MockTrace", "MockData2_traces", "mesh"])
+def test_from_json_equals_object_ingest(engine, src):
+    """Traces.from_json (native JSON parser) gives the
+    same realtime rows, combined stats and dependency graph as Traces over
+    the parsed objects."""
+    import json
+
+    from kmamiz_amd import Traces, synth
+
+    if src == "mesh":
+        batch, off = synth.host_batch(3, 0, 2000)
+        traces = synth.to_traces(3, batch, off)
+    else:
+        traces = fixture(src)
+        if src != "MockTrace":
+            traces = [traces]
+    data = json.dumps(traces).encode()
+    a, b = Traces.from_json(data, engine=engine), Traces(traces, engine=engine)
+    assert a.toRealTimeData().toJSON() == b.toRealTimeData().toJSON()
+    assert (a.combineLogsToRealtimeData([]).toCombinedRealtimeData().toJSON()
+            == b.combineLogsToRealtimeData([]).toCombinedRealtimeData().toJSON())
+    assert a.toEndpointDependencies().toJSON() == b.toEndpointDependencies().toJSON()
