@@ -146,7 +146,7 @@ typedef struct kmz_info {
  * Returns KMZ_E_UNSUPPORTED (nothing parsed) for input outside the fast path:
  * ids that are not 16 lowercase hex digits, non-integer or out-of-range
  * duration/timestamp, escaped keys or kinds, non-object tags.  threads <= 0:
- * all hardware threads. */
+ * the hardware threads, at most 16. */
 #define KMZ_JSON_ABSENT 0xFFFFFFFFFFFFFFFFull
 typedef struct kmz_zipkin_batch {
   uint64_t n;

@@ -173,7 +173,14 @@ function ingest(traces) {
   }
   for (const [i, v] of pendSid) sid[i] = other.get(v);
   for (const [i, v] of pendPid) pid[i] = other.get(v);
-  // identities per shape and rule (errors kept, raised only when used)
+  return Object.assign(
+    { flat, spans: { span_id: sid, parent_id: pid, kind, shape, status, duration, timestamp, index_base: 0 } },
+    identities(shapes, statuses)
+  );
+}
+
+// identities per shape and rule (errors kept, raised only when used)
+function identities(shapes, statuses) {
   const ident = {}, epOf = {}, epNames = {}, poison = {};
   for (const rule of ["rt", "tag", "dep"]) {
     const names = new Map();
@@ -206,8 +213,6 @@ function ingest(traces) {
     });
   }
   return {
-    flat,
-    spans: { span_id: sid, parent_id: pid, kind, shape, status, duration, timestamp, index_base: 0 },
     shapesTable: {
       rt_ep: epOf.rt,
       tag_ep: epOf.tag,
@@ -221,6 +226,86 @@ function ingest(traces) {
     ident,
     poison,
   };
+}
+
+// Raw Zipkin response bytes (a Buffer of Trace[][] JSON) -> the same batch as
+// ingest(JSON.parse(buf)), through the native parser (kmz_parse_zipkin,
+// SURVEY.md 8f row 1); null when the batch is outside its fast path.  Span
+// objects are parsed only if a per-span result needs them (`flat`).
+function ingestJSON(buf, threads) {
+  const r = addon.parseZipkin(buf, threads || 0);
+  if (r === null) return null;
+  const n = r.n;
+  // every raw field slice decoded by one JSON.parse
+  const sf = r.shapeFields, tf = r.statusFields;
+  const parts = [];
+  const collect = (f) => {
+    for (let i = 0; i < f.length; i += 2) if (f[i + 1] >= 0) parts.push(buf.toString("utf8", f[i], f[i] + f[i + 1]));
+  };
+  collect(sf);
+  collect(tf);
+  const dec = JSON.parse("[" + parts.join(",") + "]");
+  let k = 0;
+  const next = (f, i) => (f[2 * i + 1] >= 0 ? dec[k++] : undefined);
+  // raw shapes -> shapes by content, in first-occurrence order (as ingest numbers them)
+  const nRaw = sf.length / 14, smap = new Uint32Array(nRaw);
+  const shapeIndex = new Map(), shapes = [];
+  for (let i = 0; i < nRaw; i++) {
+    const key = [];
+    for (let j = 0; j < 7; j++) key.push(next(sf, 7 * i + j));
+    const hk = JSON.stringify(key.map((v) => (v === undefined ? { u: 1 } : v)));
+    let si = shapeIndex.get(hk);
+    if (si === undefined) {
+      si = shapes.length;
+      shapeIndex.set(hk, si);
+      shapes.push(key);
+    }
+    smap[i] = si;
+  }
+  const nRawSt = tf.length / 2, tmap = new Uint32Array(nRawSt);
+  const statusIndex = new Map(), statuses = [];
+  for (let i = 0; i < nRawSt; i++) {
+    const st = next(tf, i);
+    let si = statusIndex.get(st);
+    if (si === undefined) {
+      si = statuses.length;
+      statusIndex.set(st, si);
+      statuses.push(st);
+    }
+    tmap[i] = si;
+  }
+  if (statuses.length > 65535) throw new RangeError("more than 65535 distinct status strings");
+  const shape = new Uint32Array(n), status = new Uint16Array(n);
+  for (let i = 0; i < n; i++) {
+    shape[i] = smap[r.shape[i]];
+    status[i] = tmap[r.status[i]];
+  }
+  const out = Object.assign(
+    {
+      spans: {
+        span_id: r.span_id,
+        parent_id: r.parent_id,
+        kind: r.kind,
+        shape,
+        status,
+        duration: r.duration,
+        timestamp: r.timestamp,
+        index_base: 0,
+      },
+    },
+    identities(shapes, statuses)
+  );
+  let flat = null;
+  Object.defineProperty(out, "flat", {
+    get() {
+      if (!flat) {
+        flat = [];
+        for (const t of JSON.parse(buf.toString("utf8"))) for (const s of t) flat.push(s);
+      }
+      return flat;
+    },
+  });
+  return out;
 }
 
 function strip(o) {
@@ -237,16 +322,30 @@ function replicaOf(replicas, usn) {
 
 class NativeTraces {
   constructor(traces, device) {
-    this._traces = traces;
+    this._tv = traces;
     this._device = device || 0;
     this._b = null;
     this._ctx = null;
+    this._raw = null;
+  }
+  // Traces of a raw Zipkin response (Buffer of Trace[][] JSON, as
+  // ZipkinService.ts:44-57 receives it when asked for the bytes): the columns
+  // come from the native parser; objects are built only when needed.
+  static fromJSON(buf, device, threads) {
+    const t = new NativeTraces(null, device);
+    t._raw = buf;
+    t._threads = threads || 0;
+    return t;
+  }
+  get _traces() {
+    if (this._tv === null && this._raw) this._tv = JSON.parse(this._raw.toString("utf8"));
+    return this._tv;
   }
   toJSON() {
     return this._traces;
   }
   _batch() {
-    if (!this._b) this._b = ingest(this._traces);
+    if (!this._b) this._b = (this._raw && ingestJSON(this._raw, this._threads)) || ingest(this._traces);
     return this._b;
   }
   _engine() {
@@ -269,7 +368,7 @@ class NativeTraces {
     const b = this._batch();
     const ctx = this._engine();
     addon.run(ctx, addon.RUN_DEPS | addon.RUN_SPAN_LINKS);
-    const n = b.flat.length;
+    const n = b.spans.span_id.length;
     const links = addon.spanLinks(ctx, n);
     const E = b.shapesTable.n_dep_ep;
     const ep = new DataView(addon.endpoints(ctx, E));
@@ -277,7 +376,7 @@ class NativeTraces {
     const info = (i) => {
       const f = b.ident.dep[b.spans.shape[i]];
       if (!f) throw b.poison.dep.get(dep[b.spans.shape[i]]);
-      return strip(Object.assign({}, f, { timestamp: b.flat[i].timestamp / 1000 }));
+      return strip(Object.assign({}, f, { timestamp: Number(b.spans.timestamp[i]) / 1000 }));
     };
     const rows = [];
     for (let i = 0; i < n; i++) if (links.rowpos[i] !== NONE64) rows.push(i);
@@ -325,25 +424,26 @@ class NativeRealtimeDataList {
   toJSON() {
     const b = this._t._batch();
     const out = [];
-    b.flat.forEach((s, i) => {
-      if (b.spans.kind[i] !== KIND_SERVER) return;
+    const sp = b.spans, n = sp.span_id.length;
+    for (let i = 0; i < n; i++) {
+      if (sp.kind[i] !== KIND_SERVER) continue;
       const f = b.ident[this._rule][b.spans.shape[i]];
       if (!f) throw b.poison[this._rule].get(b.shapesTable[this._rule + "_ep"][b.spans.shape[i]]);
       out.push(
         strip({
-          timestamp: s.timestamp,
+          timestamp: Number(sp.timestamp[i]),
           service: f.service,
           namespace: f.namespace,
           version: f.version,
           method: f.method,
-          latency: s.duration / 1000,
-          status: (s.tags || {})["http.status_code"],
+          latency: sp.duration[i] / 1000,
+          status: b.statuses[sp.status[i]],
           uniqueServiceName: f.uniqueServiceName,
           uniqueEndpointName: f.uniqueEndpointName,
           replica: replicaOf(this._replicas, f.uniqueServiceName),
         })
       );
-    });
+    }
     return out;
   }
   toCombinedRealtimeData() {
@@ -387,4 +487,4 @@ class NativeRealtimeDataList {
   }
 }
 
-module.exports = { NativeTraces, NativeRealtimeDataList, explodeUrl, ingest, addon };
+module.exports = { NativeTraces, NativeRealtimeDataList, explodeUrl, ingest, ingestJSON, addon };

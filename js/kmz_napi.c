@@ -33,6 +33,7 @@ static const char *code_name(int rc) {
     case KMZ_E_RANGE: return "KMZ_E_RANGE";
     case KMZ_E_OVERFLOW: return "KMZ_E_OVERFLOW";
     case KMZ_E_STATE: return "KMZ_E_STATE";
+    case KMZ_E_UNSUPPORTED: return "KMZ_E_UNSUPPORTED";
     default: return "KMZ_E";
   }
 }
@@ -268,6 +269,85 @@ static napi_value js_span_links(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* copy n elements of `bytes` each into a fresh typed array */
+static napi_value copy_typed(napi_env env, napi_typedarray_type t, const void *src, size_t n, size_t bytes) {
+  void *d;
+  napi_value ab, out;
+  if (!(ab = new_buffer(env, n * bytes, &d))) return NULL;
+  if (n) memcpy(d, src, n * bytes);
+  if (napi_create_typedarray(env, t, n, ab, 0, &out) != napi_ok) return NULL;
+  return out;
+}
+
+/* (offset, length) pairs -> Float64Array, an absent property as length -1 */
+static napi_value field_pairs(napi_env env, const uint64_t *f, size_t pairs) {
+  void *d;
+  napi_value ab, out;
+  if (!(ab = new_buffer(env, pairs * 16, &d))) return NULL;
+  double *x = (double *)d;
+  for (size_t i = 0; i < pairs; ++i) {
+    x[2 * i] = (double)f[2 * i];
+    x[2 * i + 1] = f[2 * i + 1] == KMZ_JSON_ABSENT ? -1.0 : (double)f[2 * i + 1];
+  }
+  if (napi_create_typedarray(env, napi_float64_array, pairs * 2, ab, 0, &out) != napi_ok) return NULL;
+  return out;
+}
+
+/* parseZipkin(buffer, threads) -> null (outside the fast path: parse it the
+ * general way) or {n, span_id, parent_id, kind, shape, status, duration,
+ * timestamp, shapeFields, statusFields}: kmz_parse_zipkin's columns, shape and
+ * status indices into the raw-slice tables (7 and 1 (offset, length) pairs). */
+static napi_value js_parse_zipkin(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2], out, v;
+  int32_t threads = 0;
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void *data = NULL;
+  size_t len = 0;
+  bool is_buf = false;
+  if (argc < 1 || napi_is_buffer(env, argv[0], &is_buf) != napi_ok || !is_buf ||
+      napi_get_buffer_info(env, argv[0], &data, &len) != napi_ok) {
+    napi_throw_type_error(env, "KMZ_E_ARG", "parseZipkin: expected a Buffer");
+    return NULL;
+  }
+  if (argc > 1) napi_get_value_int32(env, argv[1], &threads);
+  kmz_zipkin_batch *b = NULL;
+  int rc = kmz_parse_zipkin((const char *)data, len, threads, &b);
+  if (rc == KMZ_E_UNSUPPORTED) {
+    CHECK(napi_get_null(env, &out));
+    return out;
+  }
+  if (rc) {
+    napi_throw_error(env, code_name(rc), "kmz_parse_zipkin failed (allocation)");
+    return NULL;
+  }
+  const size_t n = b->n;
+  napi_value cols[9];
+  cols[0] = copy_typed(env, napi_biguint64_array, b->span_id, n, 8);
+  cols[1] = copy_typed(env, napi_biguint64_array, b->parent_id, n, 8);
+  cols[2] = copy_typed(env, napi_uint8_array, b->kind, n, 1);
+  cols[3] = copy_typed(env, napi_uint32_array, b->shape, n, 4);
+  cols[4] = copy_typed(env, napi_uint32_array, b->status, n, 4);
+  cols[5] = copy_typed(env, napi_uint32_array, b->duration, n, 4);
+  cols[6] = copy_typed(env, napi_bigint64_array, b->timestamp, n, 8);
+  cols[7] = field_pairs(env, b->shape_fields, (size_t)b->n_shapes * 7);
+  cols[8] = field_pairs(env, b->status_fields, b->n_statuses);
+  kmz_zipkin_free(b);
+  static const char *names[9] = {"span_id", "parent_id", "kind",     "shape",       "status",
+                                 "duration", "timestamp", "shapeFields", "statusFields"};
+  CHECK(napi_create_object(env, &out));
+  for (int i = 0; i < 9; ++i) {
+    if (!cols[i]) {
+      napi_throw_error(env, "KMZ_NAPI", "parseZipkin: allocation failed");
+      return NULL;
+    }
+    napi_set_named_property(env, out, names[i], cols[i]);
+  }
+  CHECK(napi_create_double(env, (double)n, &v));
+  napi_set_named_property(env, out, "n", v);
+  return out;
+}
+
 static void export_fn(napi_env env, napi_value exports, const char *name, napi_callback fn) {
   napi_value f;
   napi_create_function(env, name, NAPI_AUTO_LENGTH, fn, NULL, &f);
@@ -289,6 +369,7 @@ NAPI_MODULE_INIT() {
   export_fn(env, exports, "endpoints", js_endpoints);
   export_fn(env, exports, "triples", js_triples);
   export_fn(env, exports, "spanLinks", js_span_links);
+  export_fn(env, exports, "parseZipkin", js_parse_zipkin);
   export_u32(env, exports, "RUN_STATS_RT", KMZ_RUN_STATS_RT);
   export_u32(env, exports, "RUN_STATS_TAG", KMZ_RUN_STATS_TAG);
   export_u32(env, exports, "RUN_DEPS", KMZ_RUN_DEPS);

@@ -470,7 +470,7 @@ int kmz_parse_zipkin(const char *json, uint64_t len, int threads, kmz_zipkin_bat
   // the batch on one thread.
   std::vector<const char *> starts{c.p};
   const uint64_t bytes = (uint64_t)(e - c.p);
-  int T = threads <= 0 ? (int)std::thread::hardware_concurrency() : threads;
+  int T = threads <= 0 ? std::min(16, (int)std::thread::hardware_concurrency()) : threads;
   T = std::max(1, std::min<int>(T, (int)(bytes >> 20)));  // >= 1 MiB a thread
   if (empty) T = 0;
   for (int t = 1; t < T; ++t) {

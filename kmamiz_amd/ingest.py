@@ -114,6 +114,13 @@ class Identity:
         self.error = error
 
 
+# The identity rules are pure functions of a shape, and a realtime worker sees
+# the same endpoints batch after batch: their results are kept across batches
+# (read-only Identity objects, keyed by the typed shape tuple).
+_IDENT_CACHE: Dict[Tuple, Tuple] = {}
+_IDENT_CACHE_MAX = 1 << 20
+
+
 class Dictionary:
     """Interned strings of one batch: shapes, statuses, endpoint names."""
 
@@ -138,7 +145,7 @@ class Dictionary:
             i = len(self.shapes)
             self.shape_index[hk] = i
             self.shapes.append(key)
-            self._add_identities(key)
+            self._add_identities(key, hk)
         return i
 
     def status_id(self, v) -> int:
@@ -164,12 +171,19 @@ class Dictionary:
             self.ep_names[rule].append(name)
         return eid
 
-    def _add_identities(self, key: Tuple):
-        for rule, fn in (("rt", rt_identity), ("tag", tag_identity), ("dep", dep_identity)):
-            try:
-                ident = Identity(fn(key))
-            except TypeError as e:  # reference raises when it evaluates this shape
-                ident = Identity(error=e)
+    def _add_identities(self, key: Tuple, hk: Tuple):
+        idents = _IDENT_CACHE.get(hk)
+        if idents is None:
+            idents = []
+            for fn in (rt_identity, tag_identity, dep_identity):
+                try:
+                    idents.append(Identity(fn(key)))
+                except TypeError as e:  # reference raises when it evaluates this shape
+                    idents.append(Identity(error=e))
+            if len(_IDENT_CACHE) >= _IDENT_CACHE_MAX:
+                _IDENT_CACHE.clear()
+            _IDENT_CACHE[hk] = idents = tuple(idents)
+        for rule, ident in zip(("rt", "tag", "dep"), idents):
             self.shape_ident[rule].append(ident)
             self.shape_ep[rule].append(self._ep(rule, ident))
 

@@ -51,15 +51,53 @@ def test_js_explode_url_and_endpoint_info():
     assert info == [O.strip_undef(O.Traces.ToEndpointInfo(s)) for tr in traces for s in tr]
 
 
+_SAME_BATCH_JS = """
+const {ingest, ingestJSON} = require('./js/kmamiz_native'); const fs = require('fs');
+const raw = fs.readFileSync(process.argv[1]);
+const a = ingestJSON(raw, Number(process.argv[2])), b = ingest(JSON.parse(raw.toString('utf8')));
+const out = {};
+for (const k of ['span_id', 'parent_id', 'kind', 'shape', 'status', 'duration', 'timestamp'])
+  out[k] = a.spans[k].length === b.spans[k].length && a.spans[k].every((x, i) => x === b.spans[k][i]);
+out.table = JSON.stringify(Object.keys(b.shapesTable).map(k => Array.from(a.shapesTable[k].length !== undefined
+  ? a.shapesTable[k] : [a.shapesTable[k]]))) === JSON.stringify(Object.keys(b.shapesTable).map(k =>
+  Array.from(b.shapesTable[k].length !== undefined ? b.shapesTable[k] : [b.shapesTable[k]])));
+out.statuses = JSON.stringify(a.statuses) === JSON.stringify(b.statuses);
+out.ident = JSON.stringify(a.ident) === JSON.stringify(b.ident);
+out.n = a.spans.span_id.length;
+process.stdout.write(JSON.stringify(out));
+"""
+
+
+@pytest.mark.parametrize("src", ["MockTracePDAS", "MockTrace", "MockData2_traces", "mesh"])
+def test_js_ingest_json_equals_object_ingest(src, tmp_path):
+    """NativeTraces.fromJSON's batch (native parser through parseZipkin) is
+    the batch the object ingest builds: columns, identity tables, statuses."""
+    if src == "mesh":
+        from kmamiz_amd import synth
+
+        batch, off = synth.host_batch(3, 0, 3000)
+        traces = synth.to_traces(3, batch, off)
+    else:
+        traces = fixture(src)
+        if src != "MockTrace":
+            traces = [traces]
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(traces))
+    out = node(_SAME_BATCH_JS, str(p), "4")
+    assert out.pop("n") == sum(len(t) for t in traces)
+    assert all(out.values()), out
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fx", ["MockTracePDAS", "MockTrace", "MockData2_traces"])
-def test_node_path_vs_oracle(fx, tmp_path):
+@pytest.mark.parametrize("mode", ["objects", "json"])
+def test_node_path_vs_oracle(fx, mode, tmp_path):
     traces = fixture(fx)
     if fx != "MockTrace":
         traces = [traces]
     p = tmp_path / "t.json"
     p.write_text(json.dumps(traces))
-    r = subprocess.run([NODE, "js/run_fixture.js", str(p)], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([NODE, "js/run_fixture.js", str(p), mode], cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     ref = O.Traces(traces)

@@ -5,7 +5,10 @@ kmz_spans columns, native parser (kmz_parse_zipkin) vs the general path
 usage: python tools/bench_ingest.py [traces] [config]   -> one JSON line"""
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -29,7 +32,7 @@ def best(fn, reps=3):
     return t
 
 
-cores = os.cpu_count()
+cores = min(16, os.cpu_count())
 
 
 def parse_only(threads):
@@ -47,6 +50,14 @@ tpn = best(lambda: parse_only(0))
 t1 = best(lambda: ingest_json(data, threads=1))
 tn = best(lambda: ingest_json(data, threads=0))
 tg = best(lambda: ingest_traces(json.loads(data)), reps=1)
+node = {}
+if shutil.which("node") and os.path.exists(os.path.join(ROOT, "js", "kmz.node")):
+    with tempfile.NamedTemporaryFile(suffix=".json") as f:
+        f.write(data)
+        f.flush()
+        r = subprocess.run(["node", os.path.join(ROOT, "tools", "bench_ingest_node.js"), f.name],
+                           capture_output=True, text=True, timeout=600)
+        node = json.loads(r.stdout) if r.returncode == 0 else {"node_error": r.stderr[-300:]}
 print(json.dumps({
     "workload": f"config{config} synthetic, {ntr} traces, {n} spans, {len(data) / n:.0f} B/span of JSON",
     "native_1thread_spans_per_s": round(n / t1), "native_all_threads_spans_per_s": round(n / tn),
@@ -54,4 +65,5 @@ print(json.dumps({
     "native_GB_per_s_1thread": round(len(data) / t1 / 1e9, 3),
     "parse_only_GB_per_s_1thread": round(len(data) / tp1 / 1e9, 3),
     "parse_only_GB_per_s_all_threads": round(len(data) / tpn / 1e9, 3), "speedup_1thread": round(tg / t1, 1),
+    **node,
 }))
