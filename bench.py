@@ -62,6 +62,8 @@ def parse():
     ap.add_argument("--spans", type=float, default=None, help="spans per GPU (default: 1e8 mesh, 1e6 bookinfo)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-fetch", action="store_true", help="leave results on the device")
+    ap.add_argument("--tail", choices=["auto", "on", "off"], default="auto",
+                    help="service-level tail (instability/coupling/cohesion/risk) in every step; auto = config 5")
     return ap.parse_args()
 
 
@@ -107,10 +109,6 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        dist.init_process_group("gloo", rank=0, world_size=1)
 
     from kmamiz_amd import Engine
     from kmamiz_amd import _lib as L
@@ -130,6 +128,35 @@ def main():
     flags = L.RUN_STATS_TAG | L.RUN_DEPS
     dev = torch.device("cuda", local)
     state = {}
+    tail_on = args.tail == "on" or (args.tail == "auto" and config == synth.POWER)
+    if tail_on:  # interned service names of the synthetic shapes (static per config, built once)
+        import numpy as np
+
+        from kmamiz_amd.ingest import SHAPE_TAGS, UNDEFINED, tag_identity
+        from kmamiz_amd.tail import maps_for_synth, realtime_risk_arrays, run_tail
+
+        args.no_fetch = False
+        tmaps = maps_for_synth(config)
+        n_shapes, n_status, _ = synth.describe(config)
+        sid_of, sid_names = {}, []
+        tag_sid = np.zeros(n_shapes, dtype=np.int64)
+        for sh in range(n_shapes):
+            name, tags = synth.shape_tags(config, sh)
+            usn = tag_identity((name,) + tuple(tags.get(t, UNDEFINED) for t in SHAPE_TAGS))["uniqueServiceName"]
+            if usn not in sid_of:
+                sid_of[usn] = len(sid_names)
+                sid_names.append(usn)
+            tag_sid[sh] = sid_of[usn]
+        is_5xx = np.array([str(x).startswith("5") for x in synth.STATUSES[:n_status]], dtype=bool)
+
+    def service_tail():
+        g, _, e = state["groups"], state["keys"], state["endpoints"]
+        t = run_tail(eng, tmaps, e)
+        state["metrics"] = t.metrics()
+        used = np.nonzero(g["combined"] > 0)[0]
+        used = used[np.argsort(g["first"][used], kind="stable")]
+        state["risk"] = realtime_risk_arrays(t, tag_sid[used // n_status], sid_names, g["combined"][used],
+                                             g["cv"][used], is_5xx[used % n_status])
 
     def step():
         eng.run(flags)
@@ -153,6 +180,8 @@ def main():
                 state["groups"], state["keys"], state["endpoints"] = eng.fetch()
         elif not args.no_fetch:  # the three result sets, one synchronisation
             state["groups"], state["keys"], state["endpoints"] = eng.fetch()
+        if tail_on:
+            service_tail()
 
     for _ in range(args.warmup):
         step()
@@ -161,7 +190,8 @@ def main():
     eng.set_profiling(True)
 
     def barrier():
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
 
     barrier()
@@ -228,12 +258,14 @@ def main():
                              synth.POWER: "config5: power-law fan-out mesh, 50k endpoints, depth-16 chains, "
                                           "hot endpoints, "}[config]
                 + f"{n_local} spans/GPU ({traces_per_gpu} traces/GPU)"
-                + (", sharded by whole traces (config 4 at N=8)" if config == synth.MESH else ""),
+                + (", sharded by whole traces (config 4 at N=8)" if config == synth.MESH else "")
+                + (", + service tail (instability/coupling/cohesion/risk) per step" if tail_on else ""),
                 "spans_per_gpu": n_local,
                 "spans_total": n_total,
                 "relations_per_gpu": A,
                 "edge_keys": info["n_triples"],
                 "parallelism": f"traceId-shard x{world}",
+                "service_tail": tail_on,
             },
             "roofline": {
                 "bound": "hbm",
@@ -251,7 +283,8 @@ def main():
         }
         print(json.dumps(line))
     eng.close()
-    dist.destroy_process_group()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -230,6 +230,44 @@ int kmz_finalize(kmz_ctx *ctx);
 /* host-side finalisation of one partial (same arithmetic as the device) */
 void kmz_finalize_host(const uint64_t *partials, uint64_t n_groups, kmz_group *out);
 
+/* ---- service-level tail over the reduced edge set ---- */
+/* Replaces the per-row scans of EndpointDependencies.toServiceDependencies
+ * (EndpointDependencies.ts:369-470), whose link counts feed toServiceInstability
+ * (614-641), toServiceCoupling / RiskAnalyzer.AbsoluteCriticalityOfServices
+ * (643-657, RiskAnalyzer.ts:145-169), RiskAnalyzer.RelyingFactor (124-137) and
+ * toServiceEndpointCohesion (565-612).  The host interns the strings:
+ *   svc[e]   uniqueServiceName of dependency endpoint e (rows are grouped by it;
+ *            also the consumer service of cohesion)
+ *   cls[e]   the link identity of e: uniqueServiceName, method, labelName
+ *            (EndpointDependencies.ts:419-421; labels from the host's label map)
+ *   lsvc[c]  the linked service of link class c (the key's first three fields)
+ * All ids < 2^24. */
+typedef struct kmz_tail_map {
+  const uint32_t *svc;  /* [n_ep] */
+  const uint32_t *cls;  /* [n_ep] */
+  const uint32_t *lsvc; /* [n_cls] */
+  uint32_t n_ep, n_svc, n_cls, n_lsvc;
+} kmz_tail_map;
+/* one link detail of toServiceDependencies: service svc, linked service lsvc,
+ * distance -> count / dependingBy / dependingOn (EndpointDependencies.ts:427-447) */
+typedef struct kmz_tail_detail {
+  uint32_t svc, lsvc, distance, count, depending_by, depending_on;
+} kmz_tail_detail;
+/* cohesion: service svc has `consumes` distinct endpoints that consumer
+ * service `consumer` calls at distance 1 (EndpointDependencies.ts:569-596) */
+typedef struct kmz_tail_pair {
+  uint32_t svc, consumer, consumes;
+} kmz_tail_pair;
+/* upload the maps (host memory; kept until replaced) */
+int kmz_tail_map_set(kmz_ctx *ctx, const kmz_tail_map *map);
+/* run the tail over the context's current edge set (after KMZ_RUN_DEPS and
+ * any kmz_merge_triples); synchronous, returns the result sizes */
+int kmz_tail_run(kmz_ctx *ctx, uint64_t *n_details, uint64_t *n_pairs);
+/* copy the results: details and pairs in no particular order; has_in[e] = 1
+ * when endpoint e's merged row has a non-empty dependingBy */
+int kmz_tail_get(kmz_ctx *ctx, kmz_tail_detail *details, uint64_t dcap, kmz_tail_pair *pairs, uint64_t pcap,
+                 uint8_t *has_in, uint64_t hcap);
+
 /* ---- pinned host memory for result buffers (fast D2H) ---------------------- */
 void *kmz_host_alloc(uint64_t bytes);
 void kmz_host_free(void *p);
@@ -250,7 +288,8 @@ void kmz_host_free(void *p);
 #define KMZ_K_PEND 10    /* K4 chains whose ancestry leaves the LDS window        */
 #define KMZ_K_CHECK 11   /* uniqueness certificate pass 3 (k_cert_check)          */
 #define KMZ_K_SETTLE 12  /* K4 k_chain_settle: staged keys + deferred chain checks */
-#define KMZ_K_COUNT 13
+#define KMZ_K_TAIL 13    /* service tail: k_tail_links + k_tail_compact           */
+#define KMZ_K_COUNT 14
 int kmz_set_profiling(kmz_ctx *ctx, int on);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);

@@ -33,7 +33,7 @@ ERRORS = {
 }
 
 KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final", "join", "cert", "reduce", "pend", "check",
-           "settle"]
+           "settle", "tail"]
 SYNTH_BOOKINFO, SYNTH_MESH, SYNTH_POWER = 2, 3, 5
 PART_GROUPS, PART_ENDPOINTS, PART_TRIPLES = 0, 1, 2
 
@@ -99,6 +99,22 @@ GROUP_DTYPE = np.dtype(
     [("combined", "<u8"), ("first", "<u8"), ("latest_timestamp", "<i8"), ("mean", "<f8"), ("cv", "<f8")]
 )
 ENDPOINT_DTYPE = np.dtype([("last_ts", "<i8"), ("first_row", "<u8"), ("external", "<u4"), ("has_row", "<u4")])
+TAIL_DETAIL_DTYPE = np.dtype([("svc", "<u4"), ("lsvc", "<u4"), ("distance", "<u4"), ("count", "<u4"),
+                              ("depending_by", "<u4"), ("depending_on", "<u4")])
+TAIL_PAIR_DTYPE = np.dtype([("svc", "<u4"), ("consumer", "<u4"), ("consumes", "<u4")])
+
+
+class TailMap(C.Structure):
+    _fields_ = [
+        ("svc", C.c_void_p),
+        ("cls", C.c_void_p),
+        ("lsvc", C.c_void_p),
+        ("n_ep", C.c_uint32),
+        ("n_svc", C.c_uint32),
+        ("n_cls", C.c_uint32),
+        ("n_lsvc", C.c_uint32),
+    ]
+
 
 class ZipkinBatch(C.Structure):
     _fields_ = [
@@ -144,6 +160,9 @@ SIGNATURES = [
     ("kmz_merge_triples", C.c_int, [_P, _P, C.c_uint64, C.c_int]),
     ("kmz_parse_zipkin", C.c_int, [C.c_char_p, C.c_uint64, C.c_int, C.POINTER(C.POINTER(ZipkinBatch))]),
     ("kmz_zipkin_free", None, [C.POINTER(ZipkinBatch)]),
+    ("kmz_tail_map_set", C.c_int, [_P, C.POINTER(TailMap)]),
+    ("kmz_tail_run", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("kmz_tail_get", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, _P, C.c_uint64]),
     ("kmz_finalize", C.c_int, [_P]),
     ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
     ("kmz_host_alloc", _P, [C.c_uint64]),

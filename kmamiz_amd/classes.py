@@ -498,6 +498,7 @@ class _DepResult:
 
     def __init__(self, traces: Traces, eng: Engine):
         batch, d, flat = traces._ingest()
+        self.traces = traces
         self.batch, self.dict, self.flat = batch, d, flat
         self.cparent, self.rowpos = eng.span_links()
         self.endpoints = eng.endpoints()
@@ -587,6 +588,19 @@ class EndpointDependencies:
         if self._native is None:
             raise ValueError("reduced() needs an engine-backed result")
         return self._native.triples, self._native.endpoints
+
+    def service_tail(self, labelMap: Optional[Dict[str, str]] = None):
+        """Scale form of the service-level tail (tail.ServiceTail) of the
+        reduced graph ``EndpointDependencies([]).combineWith(self).trim()``,
+        computed on the GPU from the edge keys (kmz_tail_run)."""
+        from .tail import maps_from_dictionary, run_tail
+
+        if self._native is None:
+            raise ValueError("service_tail() needs an engine-backed result")
+        traces = self._native.traces
+        eng = traces._load()
+        eng.run(L.RUN_DEPS)
+        return run_tail(eng, maps_from_dictionary(self._native.dict, labelMap), eng.endpoints())
 
     def trim(self):
         """EndpointDependencies.ts:91-112."""

@@ -59,6 +59,12 @@ struct kmz_ctx {
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
+  // service tail (kmz_tail.hip): maps, link set, detail table, pair set, pair table, outputs
+  DevBuf tl_svc, tl_cls, tl_lsvc, tl_lset, tl_akey, tl_aval, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs,
+      tl_cnt;
+  uint32_t tl_n_ep = 0, tl_n_cls = 0;
+  bool tl_map = false, tl_ran = false;
+  uint64_t tl_acap = 0, tl_pacap = 0, tl_nd = 0, tl_np = 0;
   bool ctab_dirty = true;  // the chain table holds entries no list records (new, or a list overflowed)
   int path = 0;             // kmz_info.path of the last dependency run
   bool sstats = false;      // shape-level K3 partials computed in this run
@@ -257,7 +263,9 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n};
+                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
+                    &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->hpin) hipHostFree(c->hpin);
@@ -901,6 +909,122 @@ int kmz_merge_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, int mem) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->hpin_valid)
     reinterpret_cast<unsigned long long *>(reinterpret_cast<unsigned int *>(c->hpin) + C_COUNT)[S_TRIP_OUT] = nt;
+  return KMZ_OK;
+}
+
+static uint64_t pow2_at_least(uint64_t x) {
+  uint64_t c = 1024;
+  while (c < x) c *= 2;
+  return c;
+}
+
+int kmz_tail_map_set(kmz_ctx *c, const kmz_tail_map *m) {
+  if (!c || !m || !m->svc || !m->cls || (m->n_cls && !m->lsvc)) return KMZ_E_ARG;
+  const uint32_t lim = 1u << 24;
+  if (m->n_svc >= lim || m->n_cls >= lim || m->n_lsvc >= lim || m->n_ep >= lim) return fail(c, KMZ_E_ARG, "tail ids must be < 2^24");
+  for (uint32_t e = 0; e < m->n_ep; ++e)
+    if (m->svc[e] >= m->n_svc || m->cls[e] >= m->n_cls) return fail(c, KMZ_E_RANGE, "tail map id out of range");
+  for (uint32_t k = 0; k < m->n_cls; ++k)
+    if (m->lsvc[k] >= m->n_lsvc) return fail(c, KMZ_E_RANGE, "tail link-class id out of range");
+  if (ensure(c, c->tl_svc, (size_t)m->n_ep * 4) || ensure(c, c->tl_cls, (size_t)m->n_ep * 4) ||
+      ensure(c, c->tl_lsvc, (size_t)m->n_cls * 4) || ensure(c, c->tl_hasin, m->n_ep) || ensure(c, c->tl_cnt, 32))
+    return KMZ_E_HIP;
+  if (m->n_ep) {
+    HIPCHK(c, hipMemcpyAsync(c->tl_svc.p, m->svc, (size_t)m->n_ep * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->tl_cls.p, m->cls, (size_t)m->n_ep * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  if (m->n_cls) HIPCHK(c, hipMemcpyAsync(c->tl_lsvc.p, m->lsvc, (size_t)m->n_cls * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->tl_n_ep = m->n_ep;
+  c->tl_n_cls = m->n_cls;
+  c->tl_map = true;
+  c->tl_ran = false;
+  return KMZ_OK;
+}
+
+int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
+  if (!c) return KMZ_E_ARG;
+  if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+  if (!c->tl_map) return fail(c, KMZ_E_STATE, "kmz_tail_map_set first");
+  if (c->tl_n_ep != c->n_dep) return fail(c, KMZ_E_ARG, "tail map size differs from the dependency endpoints");
+  unsigned long long *st = P<unsigned long long>(c->stats64);
+  uint64_t nt = 0;
+  if (c->hpin_valid) {
+    nt = reinterpret_cast<const unsigned long long *>(reinterpret_cast<const unsigned int *>(c->hpin) + C_COUNT)[S_TRIP_OUT];
+  } else {
+    unsigned long long s[S_COUNT];
+    HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    nt = s[S_TRIP_OUT];
+  }
+  // link keys <= 2 per edge key (load <= 1/2); pairs <= 1 per edge key; the
+  // detail / pair tables start smaller and grow on overflow
+  const uint64_t lcap = pow2_at_least(4 * nt + 64), pcap = pow2_at_least(2 * nt + 64);
+  if (!c->tl_acap) c->tl_acap = pow2_at_least(nt / 2 + 4096);
+  if (!c->tl_pacap) c->tl_pacap = pow2_at_least(nt / 4 + 4096);
+  for (int attempt = 0;; ++attempt) {
+    const uint64_t acap = c->tl_acap, pacap = c->tl_pacap;
+    if (ensure(c, c->tl_lset, lcap * 8) || ensure(c, c->tl_akey, acap * 8) || ensure(c, c->tl_aval, acap * 16) ||
+        ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
+        ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)))
+      return KMZ_E_HIP;
+    {
+      Timed t(c, KMZ_K_MEMSET);
+      HIPCHK(c, hipMemsetAsync(c->tl_lset.p, 0, lcap * 8, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_akey.p, 0, acap * 8, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_aval.p, 0, acap * 16, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_pset.p, 0, pcap * 8, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_pkey.p, 0, pacap * 8, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_pval.p, 0, pacap * 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_hasin.p, 0, c->tl_n_ep ? c->tl_n_ep : 1, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_cnt.p, 0, 32, c->stream));
+    }
+    unsigned long long *cnt64 = P<unsigned long long>(c->tl_cnt);  // [0] flags (u32), [1] details, [2] pairs
+    {
+      Timed t(c, KMZ_K_TAIL);
+      launch_tail(c->stream, P<unsigned long long>(c->trip_out), st + S_TRIP_OUT, nt, P<uint32_t>(c->tl_svc),
+                  P<uint32_t>(c->tl_cls), P<uint32_t>(c->tl_lsvc), P<uint32_t>(c->tl_svc), c->tl_n_ep, c->tl_n_cls,
+                  P<unsigned long long>(c->tl_lset), lcap, P<unsigned long long>(c->tl_akey), P<uint32_t>(c->tl_aval),
+                  acap, P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey),
+                  P<uint32_t>(c->tl_pval), pacap, P<uint8_t>(c->tl_hasin), P<unsigned int>(c->tl_cnt),
+                  P<uint32_t>(c->tl_det), P<uint32_t>(c->tl_pairs), cnt64 + 1);
+    }
+    unsigned long long h[3];
+    HIPCHK(c, hipMemcpyAsync(h, c->tl_cnt.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    harvest(c);
+    const uint32_t fl = (uint32_t)h[0];
+    if (fl & F_RANGE) return fail(c, KMZ_E_RANGE, "edge key endpoint outside the tail map");
+    if (fl & F_TRIPLE_OVERFLOW) {
+      if (attempt >= 3) return fail(c, KMZ_E_OVERFLOW, "service tail table overflow");
+      c->tl_acap *= 4;
+      c->tl_pacap *= 4;
+      continue;
+    }
+    // keep the detail / pair tables at load <= 1/2 for the next run
+    while (h[1] * 2 > c->tl_acap) c->tl_acap *= 2;
+    while (h[2] * 2 > c->tl_pacap) c->tl_pacap *= 2;
+    c->tl_nd = h[1];
+    c->tl_np = h[2];
+    c->tl_ran = true;
+    if (n_details) *n_details = h[1];
+    if (n_pairs) *n_pairs = h[2];
+    return KMZ_OK;
+  }
+}
+
+int kmz_tail_get(kmz_ctx *c, kmz_tail_detail *det, uint64_t dcap, kmz_tail_pair *pairs, uint64_t pcap,
+                 uint8_t *has_in, uint64_t hcap) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
+  if ((det && dcap < c->tl_nd) || (pairs && pcap < c->tl_np) || (has_in && hcap < c->tl_n_ep))
+    return fail(c, KMZ_E_ARG, "output too small");
+  if (det && c->tl_nd)
+    HIPCHK(c, hipMemcpyAsync(det, c->tl_det.p, c->tl_nd * sizeof(kmz_tail_detail), hipMemcpyDeviceToHost, c->stream));
+  if (pairs && c->tl_np)
+    HIPCHK(c, hipMemcpyAsync(pairs, c->tl_pairs.p, c->tl_np * sizeof(kmz_tail_pair), hipMemcpyDeviceToHost, c->stream));
+  if (has_in && c->tl_n_ep) HIPCHK(c, hipMemcpyAsync(has_in, c->tl_hasin.p, c->tl_n_ep, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return KMZ_OK;
 }
 

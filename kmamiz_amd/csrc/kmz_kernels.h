@@ -106,6 +106,14 @@ void launch_collapse_endpoints(hipStream_t s, const unsigned long long *sg, uint
                                const uint32_t *dep_map, uint32_t n_dep, const uint32_t *cparent, uint64_t index_base,
                                unsigned long long *ep_ts, unsigned long long *ep_first, unsigned int *counters);
 
+// service-level tail over the compacted edge keys (kmz_tail.hip)
+void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned long long *n_keys, uint64_t n_max,
+                 const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
+                 uint32_t n_ep, uint32_t n_cls, unsigned long long *lset, uint64_t lcap, unsigned long long *akey,
+                 uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
+                 uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned int *counters, uint32_t *links_out,
+                 uint32_t *pairs_out, unsigned long long *out_counts);
+
 // window parent join + uniqueness certificate (kmz_join.hip)
 struct CertPlan {
   uint32_t B2, cap2, chunks;

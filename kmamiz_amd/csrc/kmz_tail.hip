@@ -1,0 +1,182 @@
+// kmz_tail.hip -- the service-level tail over the reduced edge set (SURVEY.md
+// 8a row a8; config 5's "service risk/instability/coupling recompute").
+//
+// The reference derives every service metric from the endpoint rows of
+// EndpointDependencies.toServiceDependencies (EndpointDependencies.ts:369-470):
+// per service (the rows' uniqueServiceName) it collects the distinct link keys
+//
+//     linked usn \t method \t labelName \t type \t distance          (419-421)
+//
+// over the dependingOn (type SERVER) and dependingBy (type CLIENT) entries of
+// its rows, then counts them per linked service (the key's first three
+// fields) and distance (427-466).  Instability (614-641), ACS / coupling
+// (643-657, RiskAnalyzer.ts:145-169), the relying factor (RiskAnalyzer.ts:
+// 124-137) and cohesion (565-612) are small functions of those counts.
+//
+// On the reduced form a row's entries are the run's edge keys
+// (anc, desc, distance, on): desc's row has (anc, distance) in dependingBy,
+// and anc's row -- when the ancestor occurrence is a SERVER span (on) -- has
+// (desc, distance) in dependingOn.  So one pass over the edge keys produces
+// every link key of every service:
+//
+//     (svc[desc], cls[anc], CLIENT, d)              always
+//     (svc[anc],  cls[desc], SERVER, d)             if on
+//
+// where cls = interned (uniqueServiceName, method, labelName) and svc =
+// interned uniqueServiceName of an endpoint (host-supplied maps: the label map
+// is the host's, as in EndpointDependencies.label()).  A link key that wins its
+// slot in the link set adds itself to its (svc, lsvc(cls), d) detail counters
+// in the same step (count, dependingBy, dependingOn), so duplicates cost one
+// probe and no second pass runs.  Cohesion needs, per service, the distinct
+// (consumer service, consumed endpoint) pairs at distance 1: the pair set
+// (desc, usn[anc]) does the same on its own winners.  `hasin` marks rows with
+// a non-empty dependingBy (a service with a row without one is a gateway,
+// RiskAnalyzer.ts:155-158).
+//
+// Everything is integer; the fp64 metrics are finished on the host over at
+// most services x linked services x distances detail rows.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kmz_kernels.h"
+
+namespace kmz {
+
+constexpr uint32_t TAIL_PROBE_MAX = 1024;
+
+// insert `key` (nonzero) into an open-addressing set; true if this call put it there
+__device__ __forceinline__ bool tail_set_put(unsigned long long *__restrict__ set, uint64_t cap, uint64_t key,
+                                             uint32_t *flags) {
+  uint64_t pos = slot_of(key, cap);
+  for (uint32_t z = 0; z < TAIL_PROBE_MAX; ++z) {
+    unsigned long long cur = set[pos];
+    if (cur == key) return false;
+    if (cur == 0) {
+      cur = atomicCAS(&set[pos], 0ull, (unsigned long long)key);
+      if (cur == 0) return true;
+      if (cur == key) return false;
+    }
+    pos = pos + 1 == cap ? 0 : pos + 1;
+  }
+  *flags |= F_TRIPLE_OVERFLOW;
+  return false;
+}
+
+// the slot of `key` in an aggregation table (inserted if new), or cap on overflow
+__device__ __forceinline__ uint64_t tail_agg_slot(unsigned long long *__restrict__ akey, uint64_t cap, uint64_t key,
+                                                  uint32_t *flags) {
+  uint64_t pos = slot_of(key, cap);
+  for (uint32_t z = 0; z < TAIL_PROBE_MAX; ++z) {
+    unsigned long long cur = akey[pos];
+    if (cur == key) return pos;
+    if (cur == 0) {
+      cur = atomicCAS(&akey[pos], 0ull, (unsigned long long)key);
+      if (cur == 0 || cur == key) return pos;
+    }
+    pos = pos + 1 == cap ? 0 : pos + 1;
+  }
+  *flags |= F_TRIPLE_OVERFLOW;
+  return cap;
+}
+
+// link key: svc << 40 | cls << 16 | type << 15 | d   (type 1 = SERVER / dependingOn)
+// detail key: svc << 40 | lsvc << 16 | d
+// pair key: (desc + 1) << 32 | consumer usn;  pair detail key: (svc + 1) << 32 | consumer usn
+__global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__restrict__ keys,
+                                                    const unsigned long long *__restrict__ n_keys,
+                                                    const uint32_t *__restrict__ svc, const uint32_t *__restrict__ cls,
+                                                    const uint32_t *__restrict__ lsvc_of_cls,
+                                                    const uint32_t *__restrict__ usn, uint32_t n_ep, uint32_t n_cls,
+                                                    unsigned long long *__restrict__ lset, uint64_t lcap,
+                                                    unsigned long long *__restrict__ akey, uint32_t *__restrict__ aval,
+                                                    uint64_t acap, unsigned long long *__restrict__ pset,
+                                                    uint64_t pcap, unsigned long long *__restrict__ pkey,
+                                                    uint32_t *__restrict__ pval, uint64_t pacap,
+                                                    uint8_t *__restrict__ hasin, unsigned int *__restrict__ counters) {
+  const uint64_t n = *n_keys;
+  uint32_t flags = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    const uint32_t a = (uint32_t)(k >> 40), s = (uint32_t)(k >> 16) & 0xFFFFFFu, d = (uint32_t)(k >> 1) & 0x7FFFu;
+    const bool on = (k & 1) != 0;
+    if (a >= n_ep || s >= n_ep || cls[a] >= n_cls || cls[s] >= n_cls) {
+      flags |= F_RANGE;
+      continue;
+    }
+    hasin[s] = 1;
+    // desc's row: (anc, d) in dependingBy
+    uint32_t side = 0;
+    uint64_t lk[2];
+    lk[side++] = ((uint64_t)svc[s] << 40) | ((uint64_t)cls[a] << 16) | d;
+    if (on) lk[side++] = ((uint64_t)svc[a] << 40) | ((uint64_t)cls[s] << 16) | (1u << 15) | d;
+    for (uint32_t t = 0; t < side; ++t) {
+      if (!tail_set_put(lset, lcap, lk[t], &flags)) continue;
+      const uint32_t c = (uint32_t)(lk[t] >> 16) & 0xFFFFFFu;
+      const uint64_t dk = (lk[t] & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
+      const uint64_t p = tail_agg_slot(akey, acap, dk, &flags);
+      if (p == acap) continue;
+      atomicAdd(&aval[4 * p + 0], 1u);                      // count
+      atomicAdd(&aval[4 * p + 1 + ((lk[t] >> 15) & 1)], 1u);  // dependingBy (CLIENT) / dependingOn (SERVER)
+    }
+    // cohesion: (consumer service, consumed endpoint) at distance 1
+    if (d == 1 && tail_set_put(pset, pcap, ((uint64_t)(s + 1) << 32) | usn[a], &flags)) {
+      const uint64_t p = tail_agg_slot(pkey, pacap, ((uint64_t)(svc[s] + 1) << 32) | usn[a], &flags);
+      if (p != pacap) atomicAdd(&pval[p], 1u);
+    }
+  }
+  if (flags) atomicOr(&counters[C_FLAGS], flags);
+}
+
+// aggregation tables -> dense kmz_tail_detail (MODE 0) / kmz_tail_pair (MODE 1)
+// records, wave-aggregated output positions
+template <int MODE>
+__global__ void __launch_bounds__(256) k_tail_compact(const unsigned long long *__restrict__ akey,
+                                                      const uint32_t *__restrict__ aval, uint64_t cap,
+                                                      uint32_t *__restrict__ out,
+                                                      unsigned long long *__restrict__ count) {
+  constexpr uint32_t W = MODE == 0 ? 6 : 3;  // record words
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < cap; p0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t p = p0 + threadIdx.x;
+    const unsigned long long k = p < cap ? akey[p] : 0;
+    const uint64_t m = __ballot(k != 0);
+    if (!m) continue;
+    const int lead = __ffsll((long long)m) - 1;
+    unsigned long long base = 0;
+    if ((int)lane == lead) base = atomicAdd(count, (unsigned long long)__popcll(m));
+    base = __shfl(base, lead, 64);
+    if (k) {
+      uint32_t *r = out + (uint64_t)W * (base + __popcll(m & ((1ull << lane) - 1)));
+      if (MODE == 0) {  // detail key svc << 40 | lsvc << 16 | d
+        r[0] = (uint32_t)(k >> 40);
+        r[1] = (uint32_t)(k >> 16) & 0xFFFFFFu;
+        r[2] = (uint32_t)k & 0xFFFFu;
+        r[3] = aval[4 * p + 0];
+        r[4] = aval[4 * p + 1];
+        r[5] = aval[4 * p + 2];
+      } else {  // pair detail key (svc + 1) << 32 | consumer
+        r[0] = (uint32_t)(k >> 32) - 1;
+        r[1] = (uint32_t)k;
+        r[2] = aval[p];
+      }
+    }
+  }
+}
+
+void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned long long *n_keys, uint64_t n_max,
+                 const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
+                 uint32_t n_ep, uint32_t n_cls, unsigned long long *lset, uint64_t lcap, unsigned long long *akey,
+                 uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
+                 uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned int *counters, uint32_t *links_out,
+                 uint32_t *pairs_out, unsigned long long *out_counts) {
+  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_tail_links, dim3(g), dim3(256), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls,
+                     lset, lcap, akey, aval, acap, pset, pcap, pkey, pval, pacap, hasin, counters);
+  const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((acap + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_tail_compact<0>, dim3(ga), dim3(256), 0, s, akey, aval, acap, links_out, out_counts);
+  const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pacap + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_tail_compact<1>, dim3(gp), dim3(256), 0, s, pkey, pval, pacap, pairs_out, out_counts + 1);
+}
+
+}  // namespace kmz

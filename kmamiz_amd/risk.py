@@ -58,6 +58,8 @@ class Normalizer:
 
 
 def _gateway(dep) -> bool:
+    if "gateway" in dep:  # the compact form of tail.ServiceTail.service_deps_compact()
+        return dep["gateway"]
     return any(len(d["dependingBy"]) == 0 for d in dep["dependency"])
 
 

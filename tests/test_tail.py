@@ -1,0 +1,195 @@
+"""Service-level tail at scale: kmz_tail_run + the host
+finish (kmamiz_amd/tail.py) against the Python oracle's tail over the reduced
+form ``EndpointDependencies([]).combineWith(deps).trim()``
+(EndpointDependencies.ts:369-657, RiskAnalyzer.ts:10-248).
+
+* CPU: a numpy restatement of the kernel's reduction over the C oracle's edge
+  keys feeds the same host finish (checks the edge-key -> link-detail algebra);
+* GPU: the kernel through the C ABI, on the reference fixtures, synthetic
+  configs 2/3/5, with and without a label map.
+"""
+import numpy as np
+import pytest
+
+from conftest import fixture
+from oracle import kmz_oracle as O
+
+REL = 1e-9
+
+
+def _oracle(traces, label_map=None, replicas=None):
+    ref = O.Traces(traces)
+    red = O.EndpointDependencies([]).combineWith(ref.toEndpointDependencies()).trim().toJSON()
+    od = O.EndpointDependencies(O.strip_undef(red))
+    if label_map is not None:
+        od = O.EndpointDependencies(od.label(label_map))
+    data = ref.toRealTimeData(replicas).toCombinedRealtimeData().toJSON()
+    data = [d for d in O.strip_undef(data) if d.get("uniqueServiceName") is not None]
+    risk = O.strip_undef(O.RiskAnalyzer.RealtimeRisk(data, od.toServiceDependencies(), replicas or []))
+    return od, data, risk
+
+
+def _compare(tail, od, data=None, risk=None):
+    exp_i = od.toServiceInstability()
+    assert tail.instability() == exp_i
+    assert tail.coupling() == od.toServiceCoupling()
+    got_c, exp_c = tail.cohesion(), od.toServiceEndpointCohesion()
+    assert [c["uniqueServiceName"] for c in got_c] == [c["uniqueServiceName"] for c in exp_c]
+    for g, e in zip(got_c, exp_c):
+        assert g["totalEndpoints"] == e["totalEndpoints"]
+        key = lambda c: c["uniqueServiceName"]  # noqa: E731
+        assert sorted(g["consumers"], key=key) == sorted(e["consumers"], key=key)
+        assert g["endpointUsageCohesion"] == pytest.approx(e["endpointUsageCohesion"], rel=REL)
+    # relying factor / ACS through the compact service-deps form
+    from kmamiz_amd import risk as R
+
+    sd = od.toServiceDependencies()
+    comp = tail.service_deps_compact()
+    assert [s["uniqueServiceName"] for s in comp] == [s["uniqueServiceName"] for s in sd]
+    assert R.absolute_criticality(comp) == R.absolute_criticality(sd)
+    for a, b in zip(R.relying_factor(comp), R.relying_factor(sd)):
+        assert a["uniqueServiceName"] == b["uniqueServiceName"]
+        assert a["factor"] == pytest.approx(b["factor"], rel=REL)
+    if risk is not None:
+        from kmamiz_amd.tail import realtime_risk_arrays
+
+        names = list(dict.fromkeys(d["uniqueServiceName"] for d in data))
+        ids = {u: i for i, u in enumerate(names)}
+        got = realtime_risk_arrays(tail, np.array([ids[d["uniqueServiceName"]] for d in data]), names,
+                                   np.array([d["combined"] for d in data]),
+                                   np.array([d["latency"]["cv"] for d in data]),
+                                   np.array([str(d["status"]).startswith("5") for d in data]))
+        assert [r["uniqueServiceName"] for r in got] == [r["uniqueServiceName"] for r in risk]
+        for g, e in zip(got, risk):
+            for k in ("risk", "impact", "probability", "norm"):
+                assert (k in g) == (k in e)
+                if k in g:
+                    assert g[k] == pytest.approx(e[k], rel=REL, abs=1e-15), k
+
+
+# ---------------------------------------------------------------------------
+# CPU: numpy restatement of k_tail_links over the C oracle's edge keys
+# ---------------------------------------------------------------------------
+def _tail_np(keys, maps, endpoints_has_row, first_row):
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd.engine import decode_triples
+    from kmamiz_amd.tail import ServiceTail
+
+    a, s, d, on = decode_triples(keys)
+    svc, cls, lsvc = maps.svc.astype(np.int64), maps.cls.astype(np.int64), maps.lsvc.astype(np.int64)
+    # link keys (svc, cls, type, d), unique
+    lk = np.concatenate([np.stack([svc[s], cls[a], np.zeros_like(d), d], 1),
+                         np.stack([svc[a[on]], cls[s[on]], np.ones(on.sum(), dtype=np.int64), d[on]], 1)])
+    lk = np.unique(lk, axis=0)
+    dk = np.stack([lk[:, 0], lsvc[lk[:, 1]], lk[:, 3]], 1)
+    u, inv = np.unique(dk, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    det = np.zeros(len(u), dtype=L.TAIL_DETAIL_DTYPE)
+    det["svc"], det["lsvc"], det["distance"] = u[:, 0], u[:, 1], u[:, 2]
+    det["count"] = np.bincount(inv, minlength=len(u))
+    det["depending_by"] = np.bincount(inv, weights=lk[:, 2] == 0, minlength=len(u))
+    det["depending_on"] = np.bincount(inv, weights=lk[:, 2] == 1, minlength=len(u))
+    one = d == 1
+    pk = np.unique(np.stack([s[one], svc[a[one]]], 1), axis=0)
+    pv = np.stack([svc[pk[:, 0]], pk[:, 1]], 1)
+    pu, pinv = np.unique(pv, axis=0, return_inverse=True)
+    pairs = np.zeros(len(pu), dtype=L.TAIL_PAIR_DTYPE)
+    pairs["svc"], pairs["consumer"] = pu[:, 0], pu[:, 1]
+    pairs["consumes"] = np.bincount(pinv.reshape(-1), minlength=len(pu))
+    hasin = np.zeros(maps.n_ep, dtype=np.uint8)
+    hasin[s] = 1
+    ep = np.zeros(maps.n_ep, dtype=L.ENDPOINT_DTYPE)
+    ep["has_row"] = endpoints_has_row
+    ep["first_row"] = first_row
+    return ServiceTail(maps, det, pairs, hasin, ep)
+
+
+@pytest.mark.parametrize("config,ntr", [(2, 300), (3, 120), (5, 150)])
+def test_tail_restatement_vs_oracle_cpu(config, ntr):
+    from kmamiz_amd import synth
+    from kmamiz_amd.tail import maps_for_synth
+    from oracle import c_oracle
+
+    batch, off = synth.host_batch(config, 0, ntr)
+    table = synth.shape_table(config)
+    keys, oep, _ = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    first = np.where(oep["has_row"], oep["first"], np.iinfo(np.uint64).max).astype(np.uint64)
+    tail = _tail_np(keys, maps_for_synth(config), oep["has_row"], first)
+    od, data, risk = _oracle(synth.to_traces(config, batch, off))
+    _compare(tail, od, data, risk)
+    m = tail.metrics()
+    coh = {c["uniqueServiceName"]: c for c in od.toServiceEndpointCohesion()}
+    for i, c in enumerate(tail.coupling()):
+        assert m["acs"][i] == c["acs"]
+        assert m["cohesion"][i] == pytest.approx(coh[c["uniqueServiceName"]]["endpointUsageCohesion"], rel=REL)
+    assert list(m["instability"]) == [x["instability"] for x in od.toServiceInstability()]
+
+
+# ---------------------------------------------------------------------------
+# GPU: the kernel through the C ABI
+# ---------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("fx", ["MockTrace", "MockTracePDAS", "MockData2_traces"])
+def test_tail_fixtures_gpu(engine, fx):
+    from kmamiz_amd import Traces
+
+    traces = fixture(fx)
+    if fx != "MockTrace":
+        traces = [traces]
+    tail = Traces(traces, engine=engine).toEndpointDependencies().service_tail()
+    od, data, risk = _oracle(traces)
+    _compare(tail, od, data, risk)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,ntr", [(2, 2000), (3, 300), (5, 400)])
+def test_tail_synthetic_gpu(engine, config, ntr):
+    from kmamiz_amd import Traces, synth
+
+    batch, off = synth.host_batch(config, 0, ntr)
+    traces = synth.to_traces(config, batch, off)
+    tail = Traces(traces, engine=engine).toEndpointDependencies().service_tail()
+    od, data, risk = _oracle(traces)
+    _compare(tail, od, data, risk)
+
+
+@pytest.mark.gpu
+def test_tail_label_map_gpu(engine):
+    """Labels collapse or split link keys (EndpointDependencies.ts:419-421)."""
+    from kmamiz_amd import Traces, synth
+
+    batch, off = synth.host_batch(3, 0, 200)
+    traces = synth.to_traces(3, batch, off)
+    names = sorted({s["name"] for t in traces for s in t})
+    deps = Traces(traces, engine=engine).toEndpointDependencies()
+    lm = {}
+    for r in deps.toJSON():
+        u = r["endpoint"]["uniqueEndpointName"]
+        lm.setdefault(u, "/api/L%d" % (len(lm) % 3))
+    assert names
+    tail = deps.service_tail(lm)
+    od, _, _ = _oracle(traces, label_map=lm)
+    _compare(tail, od)
+
+
+@pytest.mark.gpu
+def test_tail_full_size_matches_restatement(engine):
+    """Config 5 at 2e6 spans on the device: the kernel equals the numpy
+    restatement over the engine's own edge keys (a size the oracle cannot
+    reach)."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+    from kmamiz_amd.tail import maps_for_synth, run_tail
+
+    engine.load_synthetic(5, synth.SEED, 0, 60000)
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    maps = maps_for_synth(5)
+    ep = engine.endpoints()
+    tail = run_tail(engine, maps, ep)
+    ref = _tail_np(engine.triples(), maps, ep["has_row"], ep["first_row"])
+    for f in tail.details.dtype.names:
+        assert np.array_equal(tail.details[f], ref.details[f]), f
+    for f in tail.pairs.dtype.names:
+        assert np.array_equal(tail.pairs[f], ref.pairs[f]), f
+    assert np.array_equal(tail.gateway, ref.gateway)
+    assert tail.instability() == ref.instability()
