@@ -154,9 +154,8 @@ def main():
         t = run_tail(eng, tmaps, e)
         state["metrics"] = t.metrics()
         used = np.nonzero(g["combined"] > 0)[0]
-        used = used[np.argsort(g["first"][used], kind="stable")]
         state["risk"] = realtime_risk_arrays(t, tag_sid[used // n_status], sid_names, g["combined"][used],
-                                             g["cv"][used], is_5xx[used % n_status])
+                                             g["cv"][used], is_5xx[used % n_status], first=g["first"][used])
 
     def step():
         eng.run(flags)

@@ -263,6 +263,18 @@ int kmz_tail_map_set(kmz_ctx *ctx, const kmz_tail_map *map);
 /* run the tail over the context's current edge set (after KMZ_RUN_DEPS and
  * any kmz_merge_triples); synchronous, returns the result sizes */
 int kmz_tail_run(kmz_ctx *ctx, uint64_t *n_details, uint64_t *n_pairs);
+/* per-service counters of the last tail run, 8 u32 per service id:
+ *   [0] linked services with dependingBy > 0, [1] with dependingOn > 0
+ *       (toServiceInstability, EndpointDependencies.ts:618-628)
+ *   [2] distance-1 details with dependingBy > 0 (AIS without the gateway +1),
+ *   [3] distance-1 details with dependingOn > 0 (ADS)   (RiskAnalyzer.ts:150-166)
+ *   [4] distance-1 consumer services, [5] sum of their consumes
+ *       (toServiceEndpointCohesion, EndpointDependencies.ts:569-596)
+ * and by_dist[svc * n_dist + d] = sum of dependingBy at distance d
+ * (RelyingFactor, RiskAnalyzer.ts:124-137).  *n_dist = 0 when some distance
+ * exceeded the dense table (the caller then sums the details). */
+int kmz_tail_service_stats(kmz_ctx *ctx, uint32_t *stats, uint64_t scap, uint32_t *by_dist, uint64_t dcap,
+                           uint32_t *n_dist);
 /* copy the results: details and pairs in no particular order; has_in[e] = 1
  * when endpoint e's merged row has a non-empty dependingBy */
 int kmz_tail_get(kmz_ctx *ctx, kmz_tail_detail *details, uint64_t dcap, kmz_tail_pair *pairs, uint64_t pcap,

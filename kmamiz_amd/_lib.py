@@ -163,6 +163,7 @@ SIGNATURES = [
     ("kmz_tail_map_set", C.c_int, [_P, C.POINTER(TailMap)]),
     ("kmz_tail_run", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("kmz_tail_get", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, _P, C.c_uint64]),
+    ("kmz_tail_service_stats", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint32)]),
     ("kmz_finalize", C.c_int, [_P]),
     ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
     ("kmz_host_alloc", _P, [C.c_uint64]),

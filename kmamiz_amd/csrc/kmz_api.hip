@@ -61,8 +61,9 @@ struct kmz_ctx {
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
   // service tail (kmz_tail.hip): maps, link set, detail table, pair set, pair table, outputs
   DevBuf tl_svc, tl_cls, tl_lsvc, tl_lset, tl_akey, tl_aval, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs,
-      tl_cnt;
-  uint32_t tl_n_ep = 0, tl_n_cls = 0;
+      tl_cnt, tl_fkey, tl_fval, tl_sstat, tl_rel;
+  uint32_t tl_n_ep = 0, tl_n_cls = 0, tl_n_svc = 0, tl_n_dist = 64, tl_deep = 0;
+  uint32_t tl_rel_dist = 0;  // distances in the last run's relying table (0: not complete, use the details)
   bool tl_map = false, tl_ran = false;
   uint64_t tl_acap = 0, tl_pacap = 0, tl_nd = 0, tl_np = 0;
   bool ctab_dirty = true;  // the chain table holds entries no list records (new, or a list overflowed)
@@ -265,7 +266,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
                     &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
-                    &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt};
+                    &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
+                    &c->tl_sstat, &c->tl_rel};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->hpin) hipHostFree(c->hpin);
@@ -937,6 +939,7 @@ int kmz_tail_map_set(kmz_ctx *c, const kmz_tail_map *m) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->tl_n_ep = m->n_ep;
   c->tl_n_cls = m->n_cls;
+  c->tl_n_svc = m->n_svc;
   c->tl_map = true;
   c->tl_ran = false;
   return KMZ_OK;
@@ -966,7 +969,9 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
     const uint64_t acap = c->tl_acap, pacap = c->tl_pacap;
     if (ensure(c, c->tl_lset, lcap * 8) || ensure(c, c->tl_akey, acap * 8) || ensure(c, c->tl_aval, acap * 16) ||
         ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
-        ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)))
+        ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
+        ensure(c, c->tl_fkey, acap * 8) || ensure(c, c->tl_fval, acap * 4) ||
+        ensure(c, c->tl_sstat, (size_t)c->tl_n_svc * 32) || ensure(c, c->tl_rel, (size_t)c->tl_n_svc * c->tl_n_dist * 4))
       return KMZ_E_HIP;
     {
       Timed t(c, KMZ_K_MEMSET);
@@ -978,6 +983,10 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       HIPCHK(c, hipMemsetAsync(c->tl_pval.p, 0, pacap * 4, c->stream));
       HIPCHK(c, hipMemsetAsync(c->tl_hasin.p, 0, c->tl_n_ep ? c->tl_n_ep : 1, c->stream));
       HIPCHK(c, hipMemsetAsync(c->tl_cnt.p, 0, 32, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_fkey.p, 0, acap * 8, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_fval.p, 0, acap * 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_sstat.p, 0, (size_t)c->tl_n_svc * 32 + 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_rel.p, 0, (size_t)c->tl_n_svc * c->tl_n_dist * 4 + 4, c->stream));
     }
     unsigned long long *cnt64 = P<unsigned long long>(c->tl_cnt);  // [0] flags (u32), [1] details, [2] pairs
     {
@@ -986,10 +995,11 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
                   P<uint32_t>(c->tl_cls), P<uint32_t>(c->tl_lsvc), P<uint32_t>(c->tl_svc), c->tl_n_ep, c->tl_n_cls,
                   P<unsigned long long>(c->tl_lset), lcap, P<unsigned long long>(c->tl_akey), P<uint32_t>(c->tl_aval),
                   acap, P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey),
-                  P<uint32_t>(c->tl_pval), pacap, P<uint8_t>(c->tl_hasin), P<unsigned int>(c->tl_cnt),
-                  P<uint32_t>(c->tl_det), P<uint32_t>(c->tl_pairs), cnt64 + 1);
+                  P<uint32_t>(c->tl_pval), pacap, P<uint8_t>(c->tl_hasin), P<unsigned long long>(c->tl_fkey),
+                  P<uint32_t>(c->tl_fval), acap, P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), c->tl_n_dist,
+                  P<unsigned int>(c->tl_cnt), P<uint32_t>(c->tl_det), P<uint32_t>(c->tl_pairs), cnt64 + 1, true);
     }
-    unsigned long long h[3];
+    unsigned long long h[4];
     HIPCHK(c, hipMemcpyAsync(h, c->tl_cnt.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
@@ -1006,11 +1016,30 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
     while (h[2] * 2 > c->tl_pacap) c->tl_pacap *= 2;
     c->tl_nd = h[1];
     c->tl_np = h[2];
+    // relying-factor distances beyond the dense table: reported, and the
+    // table grows for the next run (the host takes them from the details)
+    c->tl_deep = (uint32_t)h[3];
+    if (c->tl_deep >= c->tl_n_dist && (uint64_t)c->tl_n_svc * (c->tl_deep + 1) <= (1ull << 26))
+      c->tl_n_dist = c->tl_deep + 1;
+    c->tl_rel_dist = c->tl_deep ? 0 : c->tl_n_dist;
     c->tl_ran = true;
     if (n_details) *n_details = h[1];
     if (n_pairs) *n_pairs = h[2];
     return KMZ_OK;
   }
+}
+
+int kmz_tail_service_stats(kmz_ctx *c, uint32_t *stats, uint64_t scap, uint32_t *by_dist, uint64_t dcap,
+                           uint32_t *n_dist) {
+  if (!c || !n_dist) return KMZ_E_ARG;
+  if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
+  *n_dist = c->tl_rel_dist;
+  const uint64_t ns = (uint64_t)c->tl_n_svc * 8, nd = (uint64_t)c->tl_n_svc * c->tl_rel_dist;
+  if ((stats && scap < ns) || (by_dist && dcap < nd)) return fail(c, KMZ_E_ARG, "output too small");
+  if (stats && ns) HIPCHK(c, hipMemcpyAsync(stats, c->tl_sstat.p, ns * 4, hipMemcpyDeviceToHost, c->stream));
+  if (by_dist && nd) HIPCHK(c, hipMemcpyAsync(by_dist, c->tl_rel.p, nd * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
 }
 
 int kmz_tail_get(kmz_ctx *c, kmz_tail_detail *det, uint64_t dcap, kmz_tail_pair *pairs, uint64_t pcap,

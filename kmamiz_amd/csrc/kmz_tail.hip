@@ -44,6 +44,9 @@
 namespace kmz {
 
 constexpr uint32_t TAIL_PROBE_MAX = 1024;
+// per-service counters (8 u32 per service, kmz_tail_service_stats)
+constexpr uint32_t TS_NBY = 0, TS_NON = 1, TS_AIS = 2, TS_ADS = 3, TS_CONSUMERS = 4, TS_CONSUMES = 5;
+static_assert(TS_NON == TS_NBY + 1 && TS_ADS == TS_AIS + 1, "the link type (0 CLIENT, 1 SERVER) selects the counter");
 
 // insert `key` (nonzero) into an open-addressing set; true if this call put it there
 __device__ __forceinline__ bool tail_set_put(unsigned long long *__restrict__ set, uint64_t cap, uint64_t key,
@@ -93,7 +96,10 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
                                                     uint64_t acap, unsigned long long *__restrict__ pset,
                                                     uint64_t pcap, unsigned long long *__restrict__ pkey,
                                                     uint32_t *__restrict__ pval, uint64_t pacap,
-                                                    uint8_t *__restrict__ hasin, unsigned int *__restrict__ counters) {
+                                                    uint8_t *__restrict__ hasin, unsigned long long *__restrict__ fkey,
+                                                    uint32_t *__restrict__ fval, uint64_t fcap,
+                                                    uint32_t *__restrict__ sstat, uint32_t *__restrict__ rel,
+                                                    uint32_t n_dist, unsigned int *__restrict__ counters) {
   const uint64_t n = *n_keys;
   uint32_t flags = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -116,13 +122,33 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
       const uint64_t dk = (lk[t] & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
       const uint64_t p = tail_agg_slot(akey, acap, dk, &flags);
       if (p == acap) continue;
-      atomicAdd(&aval[4 * p + 0], 1u);                      // count
-      atomicAdd(&aval[4 * p + 1 + ((lk[t] >> 15) & 1)], 1u);  // dependingBy (CLIENT) / dependingOn (SERVER)
+      const uint32_t ty = (uint32_t)(lk[t] >> 15) & 1u, sv = (uint32_t)(lk[t] >> 40);
+      atomicAdd(&aval[4 * p + 0], 1u);                              // count
+      const uint32_t old = atomicAdd(&aval[4 * p + 1 + ty], 1u);    // dependingBy (CLIENT) / dependingOn (SERVER)
+      if (ty == 0) {  // RelyingFactor: sum of dependingBy / distance (RiskAnalyzer.ts:124-137)
+        if (d < n_dist)
+          atomicAdd(&rel[(uint64_t)sv * n_dist + d], 1u);
+        else
+          atomicMax(&counters[6], d);  // deeper than the dense table: the host uses the details
+      }
+      if (old) continue;
+      // first type-`ty` link of this (service, linked service, distance):
+      // ACS counts distance-1 details with dependingBy / dependingOn > 0
+      // (RiskAnalyzer.ts:150-166), instability linked services with any
+      // (EndpointDependencies.ts:618-628)
+      if (d == 1) atomicAdd(&sstat[8 * sv + TS_AIS + ty], 1u);
+      const uint64_t q = tail_agg_slot(fkey, fcap, (dk >> 16) + 1, &flags);  // (svc, lsvc)
+      if (q == fcap) continue;
+      const uint32_t was = atomicOr(&fval[q], 1u << ty);
+      if (!(was & (1u << ty))) atomicAdd(&sstat[8 * sv + TS_NBY + ty], 1u);
     }
     // cohesion: (consumer service, consumed endpoint) at distance 1
     if (d == 1 && tail_set_put(pset, pcap, ((uint64_t)(s + 1) << 32) | usn[a], &flags)) {
       const uint64_t p = tail_agg_slot(pkey, pacap, ((uint64_t)(svc[s] + 1) << 32) | usn[a], &flags);
-      if (p != pacap) atomicAdd(&pval[p], 1u);
+      if (p != pacap) {
+        atomicAdd(&sstat[8 * svc[s] + TS_CONSUMES], 1u);
+        if (atomicAdd(&pval[p], 1u) == 0) atomicAdd(&sstat[8 * svc[s] + TS_CONSUMERS], 1u);
+      }
     }
   }
   if (flags) atomicOr(&counters[C_FLAGS], flags);
@@ -168,11 +194,14 @@ void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned l
                  const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
                  uint32_t n_ep, uint32_t n_cls, unsigned long long *lset, uint64_t lcap, unsigned long long *akey,
                  uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
-                 uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned int *counters, uint32_t *links_out,
-                 uint32_t *pairs_out, unsigned long long *out_counts) {
+                 uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned long long *fkey, uint32_t *fval,
+                 uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
+                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts, bool compact) {
   const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + 255) / 256, 8192));
   hipLaunchKernelGGL(k_tail_links, dim3(g), dim3(256), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls,
-                     lset, lcap, akey, aval, acap, pset, pcap, pkey, pval, pacap, hasin, counters);
+                     lset, lcap, akey, aval, acap, pset, pcap, pkey, pval, pacap, hasin, fkey, fval, fcap, sstat, rel,
+                     n_dist, counters);
+  if (!compact) return;
   const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((acap + 255) / 256, 4096));
   hipLaunchKernelGGL(k_tail_compact<0>, dim3(ga), dim3(256), 0, s, akey, aval, acap, links_out, out_counts);
   const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pacap + 255) / 256, 4096));

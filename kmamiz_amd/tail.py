@@ -71,6 +71,21 @@ class TailMaps:
         self.lsvc_names = list(lsvc_idx)
         self.n_ep = len(fields)
 
+    def rank(self, kind: str) -> np.ndarray:
+        """Rank of every service name in RiskAnalyzer's sort orders, cached:
+        ``locale`` (localeCompare, RiskAnalyzer.ts:63-70) or ``code`` (the
+        default Array.sort code-unit order, RiskAnalyzer.ts:72)."""
+        cache = self.__dict__.setdefault("_ranks", {})
+        if kind not in cache:
+            from .risk import _collation_key
+
+            key = _collation_key if kind == "locale" else (lambda x: x)
+            order = sorted(range(len(self.svc_names)), key=lambda i: key(self.svc_names[i]))
+            r = np.empty(len(order), dtype=np.int64)
+            r[order] = np.arange(len(order))
+            cache[kind] = r
+        return cache[kind]
+
     def c_struct(self) -> L.TailMap:
         return L.TailMap(L.ptr(self.svc), L.ptr(self.cls), L.ptr(self.lsvc), self.n_ep, len(self.svc_names),
                          len(self.lsvc), len(self.lsvc_names))
@@ -100,7 +115,9 @@ def maps_for_synth(config: int, label_map: Optional[Dict[str, str]] = None) -> T
 
 def run_tail(eng, maps: TailMaps, endpoints: np.ndarray) -> "ServiceTail":
     """kmz_tail_run over the engine's current edge set (after a dependency run
-    and any multi-GPU merge), then the host finish."""
+    and any multi-GPU merge).  Only the per-service counters come back to the
+    host; the link details and cohesion pairs are copied when a list output
+    needs them."""
     lib = L.lib()
     if getattr(eng, "_tail_maps", None) is not maps:
         m = maps.c_struct()
@@ -108,23 +125,48 @@ def run_tail(eng, maps: TailMaps, endpoints: np.ndarray) -> "ServiceTail":
         eng._tail_maps = maps
     nd, npairs = C.c_uint64(), C.c_uint64()
     L.check(eng.ctx, lib.kmz_tail_run(eng.ctx, C.byref(nd), C.byref(npairs)))
-    det = np.empty(nd.value, dtype=L.TAIL_DETAIL_DTYPE)
-    pairs = np.empty(npairs.value, dtype=L.TAIL_PAIR_DTYPE)
+    n_svc = len(maps.svc_names)
+    nd_, npairs_ = nd.value, npairs.value
+    dist = C.c_uint32()
+    L.check(eng.ctx, lib.kmz_tail_service_stats(eng.ctx, None, 0, None, 0, C.byref(dist)))
+    stats = np.empty((n_svc, 8), dtype=np.uint32)
+    by_dist = np.empty((n_svc, dist.value), dtype=np.uint32)
+    L.check(eng.ctx, lib.kmz_tail_service_stats(eng.ctx, L.ptr(stats), stats.size, L.ptr(by_dist), by_dist.size,
+                                                  C.byref(dist)))
     hasin = np.empty(maps.n_ep, dtype=np.uint8)
-    L.check(eng.ctx, lib.kmz_tail_get(eng.ctx, L.ptr(det), len(det), L.ptr(pairs), len(pairs), L.ptr(hasin),
-                                      len(hasin)))
-    return ServiceTail(maps, det, pairs, hasin, endpoints)
+    L.check(eng.ctx, lib.kmz_tail_get(eng.ctx, None, 0, None, 0, L.ptr(hasin), len(hasin)))
+
+    def fetch():
+        det = np.empty(nd_, dtype=L.TAIL_DETAIL_DTYPE)
+        pairs = np.empty(npairs_, dtype=L.TAIL_PAIR_DTYPE)
+        L.check(eng.ctx, lib.kmz_tail_get(eng.ctx, L.ptr(det), len(det), L.ptr(pairs), len(pairs), None, 0))
+        return det, pairs
+
+    if dist.value == 0:  # a distance beyond the dense relying table: sum the details instead
+        det, pairs = fetch()
+        return ServiceTail.from_details(maps, det, pairs, hasin, endpoints)
+    return ServiceTail(maps, stats, by_dist, hasin, endpoints, fetch)
+
+
+def _by(n, idx, w=None):
+    return np.bincount(np.asarray(idx, dtype=np.int64), weights=w, minlength=n)
 
 
 class ServiceTail:
-    """Service metrics of the reduced dependency graph."""
+    """Service metrics of the reduced dependency graph.
 
-    def __init__(self, maps: TailMaps, details: np.ndarray, pairs: np.ndarray, hasin: np.ndarray,
-                 endpoints: np.ndarray):
+    ``stats[svc]`` are kmz_tail_service_stats' counters (linked services with
+    dependingBy / dependingOn, distance-1 AIS/ADS details, cohesion consumers
+    and consumes), ``by_dist[svc, d]`` the dependingBy sums per distance."""
+
+    def __init__(self, maps: TailMaps, stats: np.ndarray, by_dist: np.ndarray, hasin: np.ndarray,
+                 endpoints: np.ndarray, fetch=None, details: Optional[np.ndarray] = None,
+                 pairs: Optional[np.ndarray] = None):
         self.maps = maps
-        order = np.lexsort((details["distance"], details["lsvc"], details["svc"]))
-        self.details = details[order]
-        self.pairs = pairs[np.lexsort((pairs["consumer"], pairs["svc"]))]
+        self.stats = stats.astype(np.int64)
+        self.by_dist = by_dist
+        self._fetch = fetch
+        self._details, self._pairs = details, pairs
         n_svc = len(maps.svc_names)
         rows = np.nonzero(endpoints["has_row"] != 0)[0]
         rsvc = maps.svc[rows].astype(np.int64)
@@ -137,38 +179,69 @@ class ServiceTail:
         present = np.nonzero(self.total > 0)[0]
         self.services = present[np.argsort(first[present], kind="stable")]  # first-row order (EndpointDependencies.ts:372-384)
 
-    # -- per service (svc id) ----------------------------------------------------
-    def _link_sides(self):
-        """(svc, lsvc) -> (sum dependingBy, sum dependingOn) over distances."""
-        d = self.details
+    @classmethod
+    def from_details(cls, maps: TailMaps, details: np.ndarray, pairs: np.ndarray, hasin: np.ndarray,
+                     endpoints: np.ndarray) -> "ServiceTail":
+        """The same counters summed from the link details and pairs (the path
+        for distances beyond the dense table, and the CPU restatement's)."""
+        n = len(maps.svc_names)
+        d = details
+        stats = np.zeros((n, 8), dtype=np.int64)
         key = d["svc"].astype(np.int64) * (1 << 24) + d["lsvc"]
         uk, inv = np.unique(key, return_inverse=True)
         by = np.bincount(inv, weights=d["depending_by"], minlength=len(uk))
         on = np.bincount(inv, weights=d["depending_on"], minlength=len(uk))
-        return (uk >> 24).astype(np.int64), by, on
+        s = uk >> 24
+        stats[:, 0] = _by(n, s, by > 0)
+        stats[:, 1] = _by(n, s, on > 0)
+        one = d["distance"] == 1
+        stats[:, 2] = _by(n, d["svc"][one], d["depending_by"][one] > 0)
+        stats[:, 3] = _by(n, d["svc"][one], d["depending_on"][one] > 0)
+        stats[:, 4] = _by(n, pairs["svc"])
+        stats[:, 5] = _by(n, pairs["svc"], pairs["consumes"])
+        nd = int(d["distance"].max()) + 1 if len(d) else 1
+        by_dist = np.zeros((n, nd), dtype=np.int64)
+        np.add.at(by_dist, (d["svc"].astype(np.int64), d["distance"].astype(np.int64)), d["depending_by"])
+        return cls(maps, stats, by_dist, hasin, endpoints, None, details, pairs)
+
+    # -- lists (copied from the device on demand) ----------------------------------
+    def _lists(self):
+        if self._details is None:
+            det, pairs = self._fetch()
+            self._details, self._pairs = det, pairs
+        return self._details, self._pairs
+
+    @property
+    def details(self) -> np.ndarray:
+        d = self._lists()[0]
+        return d[np.lexsort((d["distance"], d["lsvc"], d["svc"]))]
+
+    @property
+    def pairs(self) -> np.ndarray:
+        p = self._lists()[1]
+        return p[np.lexsort((p["consumer"], p["svc"]))]
+
+    # -- per service (svc id) ----------------------------------------------------
+    def _acs(self):
+        return self.stats[:, 2] + self.gateway, self.stats[:, 3]
+
+    def relying_factor(self) -> np.ndarray:
+        """RiskAnalyzer.ts:124-137: sum of dependingBy / distance (+1 gateway)."""
+        bd = self.by_dist
+        if bd.shape[1] <= 1:
+            return self.gateway.astype(np.float64)
+        return (bd[:, 1:] / np.arange(1, bd.shape[1], dtype=np.float64)).sum(axis=1) + self.gateway
 
     def instability(self) -> List[dict]:
         """EndpointDependencies.ts:614-641."""
-        n_svc = len(self.maps.svc_names)
-        s, by, on = self._link_sides()
-        nby = np.bincount(s, weights=(by > 0), minlength=n_svc).astype(np.int64)
-        non = np.bincount(s, weights=(on > 0), minlength=n_svc).astype(np.int64)
         out = []
         for v in self.services.tolist():
             usn = self.maps.svc_names[v]
             sv, ns, ver = _split3(usn)
-            b, o = int(nby[v]), int(non[v])
+            b, o = int(self.stats[v, 0]), int(self.stats[v, 1])
             out.append({"uniqueServiceName": usn, "name": f"{tpl(sv)}.{tpl(ns)} ({tpl(ver)})", "dependingBy": b,
                         "dependingOn": o, "instability": 0 if o + b == 0 else o / (o + b)})
         return out
-
-    def _acs(self):
-        n_svc = len(self.maps.svc_names)
-        d = self.details[self.details["distance"] == 1]
-        s = d["svc"].astype(np.int64)
-        ais = np.bincount(s, weights=d["depending_by"] > 0, minlength=n_svc).astype(np.int64) + self.gateway
-        ads = np.bincount(s, weights=d["depending_on"] > 0, minlength=n_svc).astype(np.int64)
-        return ais, ads
 
     def coupling(self) -> List[dict]:
         """EndpointDependencies.ts:643-657 (RiskAnalyzer.ts:145-169)."""
@@ -181,15 +254,8 @@ class ServiceTail:
                         "acs": int(ais[v] * ads[v])})
         return out
 
-    def relying_factor(self) -> np.ndarray:
-        """RiskAnalyzer.ts:124-137: sum of dependingBy / distance (+1 gateway)."""
-        d = self.details
-        f = np.zeros(len(self.maps.svc_names), dtype=np.float64)
-        np.add.at(f, d["svc"].astype(np.int64), d["depending_by"] / d["distance"])
-        return f + self.gateway
-
     def cohesion(self) -> List[dict]:
-        """EndpointDependencies.ts:565-612."""
+        """EndpointDependencies.ts:565-612 (consumer lists from the pairs)."""
         p = self.pairs
         starts = np.searchsorted(p["svc"], self.services)
         ends = np.searchsorted(p["svc"], self.services, side="right")
@@ -210,25 +276,19 @@ class ServiceTail:
 
     def metrics(self) -> Dict[str, np.ndarray]:
         """Every per-service scalar at once, as arrays over ``self.services``
-        (instability counts, AIS/ADS/ACS, relying factor, cohesion); the
-        cohesion mean is summed in consumer-id order."""
-        n_svc = len(self.maps.svc_names)
-        s, by, on = self._link_sides()
-        nby = np.bincount(s, weights=(by > 0), minlength=n_svc)
-        non = np.bincount(s, weights=(on > 0), minlength=n_svc)
+        (no list output: nothing but the counters crosses from the device)."""
+        st = self.stats
+        nby, non = st[:, 0], st[:, 1]
         tot = nby + non
-        inst = np.divide(non, tot, out=np.zeros(n_svc), where=tot > 0)
+        inst = np.divide(non, tot, out=np.zeros(len(tot)), where=tot > 0)
         ais, ads = self._acs()
-        p = self.pairs
-        ps = p["svc"].astype(np.int64)
-        share = p["consumes"] / np.maximum(self.total[ps], 1)
-        ncons = np.bincount(ps, minlength=n_svc)
-        coh = np.divide(np.bincount(ps, weights=share, minlength=n_svc), ncons, out=np.zeros(n_svc),
+        ncons, cons = st[:, 4], st[:, 5]
+        coh = np.divide(cons / np.maximum(self.total, 1), ncons, out=np.zeros(len(tot)),
                         where=(ncons > 0) & (self.total > 0))
         v = self.services
-        return {"depending_by": nby[v].astype(np.int64), "depending_on": non[v].astype(np.int64),
-                "instability": inst[v], "ais": ais[v], "ads": ads[v], "acs": (ais * ads)[v],
-                "relying": self.relying_factor()[v], "cohesion": coh[v], "total_endpoints": self.total[v]}
+        return {"depending_by": nby[v], "depending_on": non[v], "instability": inst[v], "ais": ais[v],
+                "ads": ads[v], "acs": (ais * ads)[v], "relying": self.relying_factor()[v], "cohesion": coh[v],
+                "total_endpoints": self.total[v]}
 
     def service_deps_compact(self) -> List[dict]:
         """What RiskAnalyzer reads from toServiceDependencies(): per service its
@@ -247,25 +307,32 @@ class ServiceTail:
 
 # -- risk over column arrays (RiskAnalyzer.ts:10-122, 171-248) -------------------
 def realtime_risk_arrays(tail: ServiceTail, data_sid: np.ndarray, sid_names: Sequence[str], combined: np.ndarray,
-                         cv: np.ndarray, is_5xx: np.ndarray, replicas: Optional[List[dict]] = None) -> List[dict]:
-    """RiskAnalyzer.RealtimeRisk over the combined rows as columns (in row
-    order): ``data_sid[i]`` indexes ``sid_names`` (the row's
-    uniqueServiceName).  Same arithmetic as ``risk.realtime_risk``, which
+                         cv: np.ndarray, is_5xx: np.ndarray, replicas: Optional[List[dict]] = None,
+                         first: Optional[np.ndarray] = None) -> List[dict]:
+    """RiskAnalyzer.RealtimeRisk over the combined rows as columns:
+    ``data_sid[i]`` indexes ``sid_names`` (row i's uniqueServiceName).  Rows
+    are in toCombinedRealtimeData order, or in any order with ``first`` (each
+    row's first span index), which orders services by first occurrence
+    (RiskAnalyzer.ts:18).  Same arithmetic as ``risk.realtime_risk``, which
     takes row dicts and the full service dependencies."""
-    from .risk import MINIMUM_PROB, Normalizer, _collation_key
+    from .risk import MINIMUM_PROB, Normalizer
 
     sid = np.asarray(data_sid, dtype=np.int64)
-    # services in first-occurrence order of their rows
-    uniq, first = np.unique(sid, return_index=True)
-    order_ids = uniq[np.argsort(first, kind="stable")]
+    if first is None:
+        uniq, pos = np.unique(sid, return_index=True)
+        order_ids = uniq[np.argsort(pos, kind="stable")]
+    else:
+        mn = np.full(len(sid_names), np.iinfo(np.uint64).max, dtype=np.uint64)
+        np.minimum.at(mn, sid, np.asarray(first, dtype=np.uint64))
+        uniq = np.nonzero(mn != np.iinfo(np.uint64).max)[0]
+        order_ids = uniq[np.argsort(mn[uniq], kind="stable")]
     remap = np.full(len(sid_names), -1, dtype=np.int64)
     remap[order_ids] = np.arange(len(order_ids))
     r = remap[sid]
     k = len(order_ids)
     comb = np.asarray(combined, dtype=np.float64)
     # latency CV per service weighted by request count (RiskAnalyzer.ts:228-248)
-    wsum = np.zeros(k)
-    np.add.at(wsum, r, np.asarray(cv, dtype=np.float64) * comb)
+    wsum = np.bincount(r, weights=np.asarray(cv, dtype=np.float64) * comb, minlength=k)
     cnt = np.bincount(r, weights=comb, minlength=k)
     err = np.bincount(r, weights=comb * np.asarray(is_5xx, dtype=bool), minlength=k)
     rel_norm = Normalizer.Strategy.SigmoidAdj([wsum[i] / cnt[i] if cnt[i] else math.nan for i in range(k)])
@@ -275,19 +342,21 @@ def realtime_risk_arrays(tail: ServiceTail, data_sid: np.ndarray, sid_names: Seq
     base = Normalizer.Strategy.Linear([p * nerr[i] for i, p in enumerate(npro)], MINIMUM_PROB)
     prob = [(rel_norm[i] * (MINIMUM_PROB if base[i] < MINIMUM_PROB else base[i])) * (1 - MINIMUM_PROB) + MINIMUM_PROB
             for i in range(k)]
-    # impact (RiskAnalyzer.ts:51-85)
-    svc_names = [tail.maps.svc_names[v] for v in tail.services.tolist()]
-    rf = tail.relying_factor()[tail.services]
+    # impact (RiskAnalyzer.ts:51-85): factors sorted by localeCompare, zipped
+    # with the names in code-unit order
+    sv = tail.services
+    rf = tail.relying_factor()[sv]
     ais, ads = tail._acs()
-    acs = (ais * ads)[tail.services]
-    order = sorted(range(len(svc_names)), key=lambda i: _collation_key(svc_names[i]))
-    nrf = Normalizer.Strategy.FixedRatio([float(rf[i]) for i in order])
-    nacs = Normalizer.Strategy.FixedRatio([float(acs[i]) for i in order])
+    acs = (ais * ads)[sv]
+    by_locale = np.argsort(tail.maps.rank("locale")[sv], kind="stable")
+    nrf = Normalizer.Strategy.FixedRatio([float(x) for x in rf[by_locale]])
+    nacs = Normalizer.Strategy.FixedRatio([float(x) for x in acs[by_locale]])
+    names_sorted = [tail.maps.svc_names[v] for v in sv[np.argsort(tail.maps.rank("code")[sv], kind="stable")]]
     rep = {}
     for x in replicas or []:
         rep.setdefault(x["uniqueServiceName"], x.get("replicas"))
     raw = []
-    for i, usn in enumerate(sorted(svc_names)):
+    for i, usn in enumerate(names_sorted):
         div = rep.get(usn) or 1
         raw.append((usn, (nrf[i] + nacs[i]) / div))
     ni = Normalizer.Strategy.Linear([x[1] for x in raw])

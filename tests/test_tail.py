@@ -101,7 +101,7 @@ def _tail_np(keys, maps, endpoints_has_row, first_row):
     ep = np.zeros(maps.n_ep, dtype=L.ENDPOINT_DTYPE)
     ep["has_row"] = endpoints_has_row
     ep["first_row"] = first_row
-    return ServiceTail(maps, det, pairs, hasin, ep)
+    return ServiceTail.from_details(maps, det, pairs, hasin, ep)
 
 
 @pytest.mark.parametrize("config,ntr", [(2, 300), (3, 120), (5, 150)])
@@ -192,4 +192,34 @@ def test_tail_full_size_matches_restatement(engine):
     for f in tail.pairs.dtype.names:
         assert np.array_equal(tail.pairs[f], ref.pairs[f]), f
     assert np.array_equal(tail.gateway, ref.gateway)
+    assert np.array_equal(tail.stats, ref.stats)
+    nd = min(tail.by_dist.shape[1], ref.by_dist.shape[1])
+    assert np.array_equal(tail.by_dist[:, :nd], ref.by_dist[:, :nd])
+    assert not tail.by_dist[:, nd:].any() and not ref.by_dist[:, nd:].any()
     assert tail.instability() == ref.instability()
+    assert tail.coupling() == ref.coupling()
+
+
+def test_risk_arrays_row_order_free():
+    """realtime_risk_arrays with ``first`` gives the same answer on shuffled rows."""
+    from kmamiz_amd import synth
+    from kmamiz_amd.tail import maps_for_synth, realtime_risk_arrays
+    from oracle import c_oracle
+
+    batch, off = synth.host_batch(5, 0, 150)
+    table = synth.shape_table(5)
+    keys, oep, _ = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    first = np.where(oep["has_row"], oep["first"], np.iinfo(np.uint64).max).astype(np.uint64)
+    tail = _tail_np(keys, maps_for_synth(5), oep["has_row"], first)
+    od, data, risk = _oracle(synth.to_traces(5, batch, off))
+    names = list(dict.fromkeys(d["uniqueServiceName"] for d in data))
+    ids = {u: i for i, u in enumerate(names)}
+    perm = np.random.default_rng(1).permutation(len(data))
+    rows = [data[i] for i in perm]
+    got = realtime_risk_arrays(tail, np.array([ids[d["uniqueServiceName"]] for d in rows]), names,
+                               np.array([d["combined"] for d in rows]), np.array([d["latency"]["cv"] for d in rows]),
+                               np.array([str(d["status"]).startswith("5") for d in rows]),
+                               first=perm.astype(np.uint64))
+    assert [r["uniqueServiceName"] for r in got] == [r["uniqueServiceName"] for r in risk]
+    for g, e in zip(got, risk):
+        assert g["risk"] == pytest.approx(e["risk"], rel=REL, abs=1e-15)
