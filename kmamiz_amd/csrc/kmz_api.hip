@@ -985,8 +985,10 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       HIPCHK(c, hipMemsetAsync(c->tl_cnt.p, 0, 32, c->stream));
       HIPCHK(c, hipMemsetAsync(c->tl_fkey.p, 0, acap * 8, c->stream));
       HIPCHK(c, hipMemsetAsync(c->tl_fval.p, 0, acap * 4, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_sstat.p, 0, (size_t)c->tl_n_svc * 32 + 4, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_rel.p, 0, (size_t)c->tl_n_svc * c->tl_n_dist * 4 + 4, c->stream));
+      if (c->tl_n_svc) {
+        HIPCHK(c, hipMemsetAsync(c->tl_sstat.p, 0, (size_t)c->tl_n_svc * 32, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->tl_rel.p, 0, (size_t)c->tl_n_svc * c->tl_n_dist * 4, c->stream));
+      }
     }
     unsigned long long *cnt64 = P<unsigned long long>(c->tl_cnt);  // [0] flags (u32), [1] details, [2] pairs
     {
