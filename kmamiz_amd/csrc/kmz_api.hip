@@ -58,6 +58,7 @@ struct kmz_ctx {
   DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
+  DevBuf ctile;           // K4 per-workgroup stats (apart from K3's tile_tmp: the two run concurrently)
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
   // service tail (kmz_tail.hip): maps, link set, detail table, pair set, pair table, outputs
   DevBuf tl_svc, tl_cls, tl_lsvc, tl_lset, tl_akey, tl_aval, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs,
@@ -87,6 +88,12 @@ struct kmz_ctx {
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
 
+  // side stream: K3 and the uniqueness certificate run beside the join and the
+  // chain walk (they share no buffers; fork/join by events)
+  hipStream_t main = nullptr, side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_k3 = nullptr, ev_join = nullptr, ev_done = nullptr;
+  bool overlap = false;  // this run uses the side stream
+
   // profiling
   bool prof = false;
   std::vector<EventPair> pending;
@@ -111,8 +118,10 @@ int fail(kmz_ctx *c, int code, const std::string &msg) {
 int ensure(kmz_ctx *c, DevBuf &b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.bytes >= bytes) return 0;
-  if (b.p) {
+  if (b.p) {  // (both streams may still use it)
     hipStreamSynchronize(c->stream);
+    if (c->side) hipStreamSynchronize(c->side);
+    if (c->main && c->main != c->stream) hipStreamSynchronize(c->main);
     hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
@@ -243,6 +252,14 @@ kmz_ctx *kmz_create(int device, void *stream) {
     }
     c->own_stream = true;
   }
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_k3, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
   if (const char *a = getenv("KMZ_ABLATE")) c->ablate = (uint32_t)strtoul(a, nullptr, 0);
   if (ensure(c, c->counters, C_COUNT * 4) || ensure(c, c->stats64, S_COUNT * 8)) {
     delete c;
@@ -264,7 +281,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
                     &c->tl_sstat, &c->tl_rel};
@@ -272,6 +289,12 @@ void kmz_destroy(kmz_ctx *c) {
     if (b->p) hipFree(b->p);
   if (c->hpin) hipHostFree(c->hpin);
   if (c->hep) hipHostFree(c->hep);
+  if (c->side) {
+    hipStreamSynchronize(c->side);
+    hipStreamDestroy(c->side);
+  }
+  for (hipEvent_t e : {c->ev_fork, c->ev_k3, c->ev_join, c->ev_done})
+    if (e) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -375,6 +398,16 @@ static int run_join(kmz_ctx *c, bool *ok) {
     launch_join(c->stream, c->sid, c->pid, c->kind, n, P<uint32_t>(c->cparent), P<uint32_t>(c->dp),
                 P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, c->ablate);
   }
+  // ... only while the chain table fits the 256 MB MALL: then the walk's
+  // probes leave HBM to the certificate (measured: mesh 5.21 -> 5.12 ms,
+  // Bookinfo 0.385 -> 0.323 ms); a chain table in HBM (config 5, 4 GB) and
+  // the certificate slow each other down (19.3 -> 25.7 ms)
+  const bool cert_side = c->overlap && !(c->ablate & (1u << 26)) && c->ccap * 32 <= (256ull << 20);
+  if (cert_side) {  // the certificate checks the join's ids beside the chain walk (read after the run)
+    HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
+    c->stream = c->side;
+  }
   {
     Timed t(c, KMZ_K_CERT);
     launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
@@ -384,6 +417,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
     Timed t(c, KMZ_K_CHECK);
     launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
   }
+  c->stream = c->main;
   {
     // parents outside the window / chains leaving it: these kernels read the
     // join's counters and return at once when there is nothing to do, so the
@@ -510,7 +544,7 @@ static int run_deps(kmz_ctx *c, bool links) {
     // run's global list of wcap more follows them)
     const uint32_t scap = 1u << 15, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
     void *old_ctab = c->ctab.p;
-    if (ensure(c, c->ctab, c->ccap * 32) || ensure(c, c->tile_tmp, (size_t)nt * 16) ||
+    if (ensure(c, c->ctab, c->ccap * 32) || ensure(c, c->ctile, (size_t)nt * 16) ||
         ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, (size_t)ng * scap * 8) ||
         ensure(c, c->kstage_n, (size_t)ng * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 32) ||
         ensure(c, c->kdefer_n, (size_t)ng * 4) || ensure(c, c->kwpos, ((size_t)ng + 1) * wcap * 4) ||
@@ -531,7 +565,7 @@ static int run_deps(kmz_ctx *c, bool links) {
       launch_chain(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
                    c->n_shapes, c->n_dep, c->index_base, c->sig_seed, c->ctab.p, c->ccap,
                    P<unsigned long long>(c->trip), c->tcap, epp, links ? P<unsigned long long>(c->rowpos) : nullptr,
-                   P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->tile_tmp), st, P<unsigned long long>(c->kstage),
+                   P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage),
                    scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
                    wpos, wcap, P<uint32_t>(c->kwpos_n),
                    // (test knob 24 forces sig collisions on the first seed only)
@@ -540,7 +574,7 @@ static int run_deps(kmz_ctx *c, bool links) {
     {
       Timed t(c, KMZ_K_SETTLE);
       launch_chain_settle(c->stream, n, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
-                          P<uint32_t>(c->tile_tmp), st, P<unsigned long long>(c->kstage), scap,
+                          P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), scap,
                           P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
                           gpos, wcap);
     }
@@ -550,6 +584,7 @@ static int run_deps(kmz_ctx *c, bool links) {
                         n, P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
                         P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, wcap);
     }
+    if (c->overlap) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_k3, 0));  // the shape-level K3 partials
     {
       Timed t(c, KMZ_K_FINAL);
       launch_compact(c->stream, P<unsigned long long>(c->trip), c->tcap, P<unsigned long long>(c->trip_out),
@@ -623,8 +658,30 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4, c->stream));
     HIPCHK(c, hipMemsetAsync(c->stats64.p, 0, S_COUNT * 8, c->stream));
     int r;
-    if (smode && (r = run_stats(c, smode))) return r;
-    if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, links))) return r;
+    c->main = c->stream;
+    // K3 (+ the certificate, see run_join) on the side stream while the main
+    // stream joins and walks (KMZ_ABLATE bit 25: serial, for comparison)
+    c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25));
+    if (c->overlap) {
+      HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      c->stream = c->side;
+    }
+    r = smode ? run_stats(c, smode) : 0;
+    if (c->overlap) {
+      c->stream = c->main;
+      HIPCHK(c, hipEventRecord(c->ev_k3, c->side));
+    }
+    if (r) return r;
+    if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, links))) {
+      c->stream = c->main;
+      if (c->overlap) hipStreamSynchronize(c->side);
+      return r;
+    }
+    if (c->overlap) {  // everything queued on the side stream, before the read-back
+      HIPCHK(c, hipEventRecord(c->ev_done, c->side));
+      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
+    }
     // one read-back per run: counters + statistics into pinned host memory
     if (!c->hpin && hipHostMalloc(&c->hpin, C_COUNT * 4 + S_COUNT * 8, hipHostMallocDefault) != hipSuccess) {
       c->hpin = nullptr;
