@@ -661,7 +661,13 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     c->main = c->stream;
     // K3 (+ the certificate, see run_join) on the side stream while the main
     // stream joins and walks (KMZ_ABLATE bit 25: serial, for comparison)
-    c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25));
+    // Only small batches (< 2^23 spans) overlap: they are launch- and
+    // latency-bound (Bookinfo 1M: 0.369 -> 0.323 ms/step).  At 10^8 spans every
+    // kernel fills the GPU by itself, overlap buys <= 3 % (mesh 5.29 -> 5.12 ms)
+    // or loses (config 5: 19.6 -> 25.7 ms), and it blurs the per-kernel
+    // roofline accounting (profiles/r01_overlap_ab/).  KMZ_ABLATE bit 27 forces it.
+    c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25)) &&
+                 (c->n < (1ull << 23) || (c->ablate & (1u << 27)));
     if (c->overlap) {
       HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
       HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
