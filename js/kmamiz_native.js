@@ -408,6 +408,74 @@ class NativeTraces {
       };
     });
   }
+  // Service-level tail of the reduced graph (EndpointDependencies([]).combineWith(deps).trim()),
+  // from the GPU's per-service counters (kmz_tail_run): toServiceInstability
+  // (EndpointDependencies.ts:614-641), toServiceCoupling (643-657, RiskAnalyzer.ts:145-169),
+  // the relying factor (RiskAnalyzer.ts:124-137) and cohesion's numbers (565-612), services
+  // in first-row order.  labelMap: uniqueEndpointName -> labelName (EndpointDependencies.label()).
+  serviceTail(labelMap) {
+    const b = this._batch();
+    const ctx = this._engine();
+    addon.run(ctx, addon.RUN_DEPS);
+    const E = b.shapesTable.n_dep_ep;
+    const fields = new Array(E).fill(null);
+    b.shapesTable.dep_ep.forEach((e, sh) => {
+      if (b.ident.dep[sh]) fields[e] = b.ident.dep[sh];
+    });
+    const svcIdx = new Map(), clsIdx = new Map(), lsvcIdx = new Map(), lsvcOfCls = [];
+    const svc = new Uint32Array(E), cls = new Uint32Array(E);
+    const str = (x) => (x === undefined ? "undefined" : `${x}`);
+    fields.forEach((f, e) => {
+      const usn = f ? f.uniqueServiceName : "";
+      const label = labelMap && f ? labelMap[f.uniqueEndpointName] : undefined;
+      if (!svcIdx.has(usn)) svcIdx.set(usn, svcIdx.size);
+      svc[e] = svcIdx.get(usn);
+      const ck = `${usn}\t${str(f ? f.method : undefined)}\t${str(label)}`;
+      if (!clsIdx.has(ck)) {
+        clsIdx.set(ck, clsIdx.size);
+        const l3 = usn.split("\t").slice(0, 3).join("\t");
+        if (!lsvcIdx.has(l3)) lsvcIdx.set(l3, lsvcIdx.size);
+        lsvcOfCls.push(lsvcIdx.get(l3));
+      }
+      cls[e] = clsIdx.get(ck);
+    });
+    const r = addon.serviceTail(ctx, { svc, cls, lsvc: Uint32Array.from(lsvcOfCls), n_svc: svcIdx.size,
+                                       n_lsvc: lsvcIdx.size });
+    const names = [...svcIdx.keys()];
+    const ep = new DataView(addon.endpoints(ctx, E));
+    const first = new Map(), total = new Array(names.length).fill(0), gateway = new Array(names.length).fill(false);
+    for (let e = 0; e < E; e++) {
+      if (!ep.getUint32(e * 24 + 20, true)) continue;  // has_row
+      const v = svc[e], fr = ep.getBigUint64(e * 24 + 8, true);
+      if (!first.has(v) || fr < first.get(v)) first.set(v, fr);
+      total[v]++;
+      if (!r.hasIn[e]) gateway[v] = true;
+    }
+    const order = [...first.keys()].sort((a, c) => (first.get(a) < first.get(c) ? -1 : 1));
+    const st = (v, k) => r.stats[v * 8 + k];
+    return order.map((v) => {
+      const usn = names[v];
+      const [s, n, ver] = usn.split("\t");
+      const by = st(v, 0), on = st(v, 1), ais = st(v, 2) + (gateway[v] ? 1 : 0), ads = st(v, 3);
+      let relying = gateway[v] ? 1 : 0;
+      for (let d = 1; d < r.nDist; d++) relying += r.byDist[v * r.nDist + d] / d;
+      const ncons = st(v, 4);
+      return {
+        uniqueServiceName: usn,
+        name: `${s}.${n} (${ver})`,
+        dependingBy: by,
+        dependingOn: on,
+        instability: on + by === 0 ? 0 : on / (on + by),
+        ais,
+        ads,
+        acs: ais * ads,
+        relyingFactor: relying,
+        totalEndpoints: total[v],
+        consumers: ncons,
+        endpointUsageCohesion: ncons && total[v] ? st(v, 5) / total[v] / ncons : 0,
+      };
+    });
+  }
   static ToEndpointInfo(trace) {
     const tags = trace.tags || {};
     const key = [trace.name].concat(SHAPE_TAGS.map((k) => tags[k]));

@@ -247,6 +247,52 @@ static napi_value js_triples(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* serviceTail(ctx, {svc: Uint32Array, cls: Uint32Array, lsvc: Uint32Array,
+ * n_svc, n_lsvc}) -> {stats: Uint32Array(n_svc * 8), byDist: Uint32Array,
+ * nDist, hasIn: Uint8Array(n_ep)}: kmz_tail_map_set + kmz_tail_run +
+ * kmz_tail_service_stats (the counters behind EndpointDependencies.
+ * toServiceInstability / toServiceCoupling / toServiceEndpointCohesion and
+ * RiskAnalyzer's relying factor, include/kmz.h) */
+static napi_value js_service_tail(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2], out, v;
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  kmz_ctx *c = get_ctx(env, argv[0]);
+  if (!c) return NULL;
+  void *svc, *cls, *lsvc;
+  size_t n_ep, n_ep2, n_cls;
+  if (argc < 2 || typed_prop(env, argv[1], "svc", napi_uint32_array, &svc, &n_ep) ||
+      typed_prop(env, argv[1], "cls", napi_uint32_array, &cls, &n_ep2) ||
+      typed_prop(env, argv[1], "lsvc", napi_uint32_array, &lsvc, &n_cls) || n_ep != n_ep2) {
+    napi_throw_type_error(env, "KMZ_E_ARG", "serviceTail: {svc, cls, lsvc} Uint32Arrays expected");
+    return NULL;
+  }
+  kmz_tail_map m = {(const uint32_t *)svc, (const uint32_t *)cls, (const uint32_t *)lsvc, (uint32_t)n_ep,
+                    u32_prop(env, argv[1], "n_svc"), (uint32_t)n_cls, u32_prop(env, argv[1], "n_lsvc")};
+  int rc = kmz_tail_map_set(c, &m);
+  if (!rc) rc = kmz_tail_run(c, NULL, NULL);
+  uint32_t nd = 0;
+  if (!rc) rc = kmz_tail_service_stats(c, NULL, 0, NULL, 0, &nd);
+  if (rc) return throw_rc(env, c, rc);
+  void *ds, *dd, *dh;
+  napi_value abs = new_buffer(env, (size_t)m.n_svc * 32, &ds), abd = new_buffer(env, (size_t)m.n_svc * nd * 4, &dd),
+             abh = new_buffer(env, n_ep, &dh);
+  if (!abs || !abd || !abh) return NULL;
+  rc = kmz_tail_service_stats(c, (uint32_t *)ds, (uint64_t)m.n_svc * 8, (uint32_t *)dd, (uint64_t)m.n_svc * nd, &nd);
+  if (!rc) rc = kmz_tail_get(c, NULL, 0, NULL, 0, (uint8_t *)dh, n_ep);
+  if (rc) return throw_rc(env, c, rc);
+  CHECK(napi_create_object(env, &out));
+  CHECK(napi_create_typedarray(env, napi_uint32_array, (size_t)m.n_svc * 8, abs, 0, &v));
+  CHECK(napi_set_named_property(env, out, "stats", v));
+  CHECK(napi_create_typedarray(env, napi_uint32_array, (size_t)m.n_svc * nd, abd, 0, &v));
+  CHECK(napi_set_named_property(env, out, "byDist", v));
+  CHECK(napi_create_typedarray(env, napi_uint8_array, n_ep, abh, 0, &v));
+  CHECK(napi_set_named_property(env, out, "hasIn", v));
+  CHECK(napi_create_uint32(env, nd, &v));
+  CHECK(napi_set_named_property(env, out, "nDist", v));
+  return out;
+}
+
 /* spanLinks(ctx, n) -> {cparent: Uint32Array, rowpos: BigUint64Array} */
 static napi_value js_span_links(napi_env env, napi_callback_info info) {
   size_t argc = 2;
@@ -370,6 +416,7 @@ NAPI_MODULE_INIT() {
   export_fn(env, exports, "triples", js_triples);
   export_fn(env, exports, "spanLinks", js_span_links);
   export_fn(env, exports, "parseZipkin", js_parse_zipkin);
+  export_fn(env, exports, "serviceTail", js_service_tail);
   export_u32(env, exports, "RUN_STATS_RT", KMZ_RUN_STATS_RT);
   export_u32(env, exports, "RUN_STATS_TAG", KMZ_RUN_STATS_TAG);
   export_u32(env, exports, "RUN_DEPS", KMZ_RUN_DEPS);

@@ -113,3 +113,49 @@ def test_node_path_vs_oracle(fx, mode, tmp_path):
         for a, b in zip(g, e):
             assert a["latency"]["mean"] == pytest.approx(b["latency"]["mean"], rel=1e-9)
             assert a["latency"]["cv"] == pytest.approx(b["latency"]["cv"], rel=1e-9, abs=1e-13)
+
+
+_TAIL_JS = """
+const {NativeTraces} = require('./js/kmamiz_native'); const fs = require('fs');
+const t = new NativeTraces(JSON.parse(fs.readFileSync(process.argv[1])));
+const lm = process.argv[2] ? JSON.parse(process.argv[2]) : undefined;
+process.stdout.write(JSON.stringify(t.serviceTail(lm)));
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src", ["MockTrace", "MockTracePDAS", "mesh", "power", "mesh-labels"])
+def test_node_service_tail_vs_oracle(src, tmp_path):
+    """NativeTraces.serviceTail (addon serviceTail -> kmz_tail_run) against
+    the oracle's tail of the reduced graph (EndpointDependencies.ts:565-657,
+    RiskAnalyzer.ts:124-169)."""
+    lm = None
+    if src in ("mesh", "power", "mesh-labels"):
+        from kmamiz_amd import synth
+
+        cfg = 5 if src == "power" else 3
+        batch, off = synth.host_batch(cfg, 0, 200)
+        traces = synth.to_traces(cfg, batch, off)
+    else:
+        traces = fixture(src)
+        if src != "MockTrace":
+            traces = [traces]
+    ref = O.Traces(traces)
+    red = O.strip_undef(O.EndpointDependencies([]).combineWith(ref.toEndpointDependencies()).trim().toJSON())
+    od = O.EndpointDependencies(red)
+    if src == "mesh-labels":
+        lm = {r["endpoint"]["uniqueEndpointName"]: "/L%d" % (i % 3) for i, r in enumerate(red)}
+        od = O.EndpointDependencies(od.label(lm))
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(traces))
+    got = node(_TAIL_JS, str(p), json.dumps(lm) if lm else "")
+    inst, coup, coh = od.toServiceInstability(), od.toServiceCoupling(), od.toServiceEndpointCohesion()
+    rf = {x["uniqueServiceName"]: x["factor"] for x in O.RiskAnalyzer.RelyingFactor(od.toServiceDependencies())}
+    assert [g["uniqueServiceName"] for g in got] == [x["uniqueServiceName"] for x in inst]
+    for g, i, c, h in zip(got, inst, coup, coh):
+        assert (g["name"], g["dependingBy"], g["dependingOn"]) == (i["name"], i["dependingBy"], i["dependingOn"])
+        assert g["instability"] == pytest.approx(i["instability"], rel=1e-12)
+        assert (g["ais"], g["ads"], g["acs"]) == (c["ais"], c["ads"], c["acs"])
+        assert (g["totalEndpoints"], g["consumers"]) == (h["totalEndpoints"], len(h["consumers"]))
+        assert g["endpointUsageCohesion"] == pytest.approx(h["endpointUsageCohesion"], rel=1e-9)
+        assert g["relyingFactor"] == pytest.approx(rf[g["uniqueServiceName"]], rel=1e-9)
