@@ -118,7 +118,7 @@ def test_node_path_vs_oracle(fx, mode, tmp_path):
 _TAIL_JS = """
 const {NativeTraces} = require('./js/kmamiz_native'); const fs = require('fs');
 const t = new NativeTraces(JSON.parse(fs.readFileSync(process.argv[1])));
-const lm = process.argv[2] ? JSON.parse(process.argv[2]) : undefined;
+const lm = process.argv[2] ? JSON.parse(fs.readFileSync(process.argv[2])) : undefined;
 process.stdout.write(JSON.stringify(t.serviceTail(lm)));
 """
 
@@ -148,7 +148,9 @@ def test_node_service_tail_vs_oracle(src, tmp_path):
         od = O.EndpointDependencies(od.label(lm))
     p = tmp_path / "t.json"
     p.write_text(json.dumps(traces))
-    got = node(_TAIL_JS, str(p), json.dumps(lm) if lm else "")
+    q = tmp_path / "labels.json"
+    q.write_text(json.dumps(lm))
+    got = node(_TAIL_JS, str(p), str(q) if lm else "")
     inst, coup, coh = od.toServiceInstability(), od.toServiceCoupling(), od.toServiceEndpointCohesion()
     rf = {x["uniqueServiceName"]: x["factor"] for x in O.RiskAnalyzer.RelyingFactor(od.toServiceDependencies())}
     assert [g["uniqueServiceName"] for g in got] == [x["uniqueServiceName"] for x in inst]
