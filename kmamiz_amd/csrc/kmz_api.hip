@@ -74,6 +74,7 @@ struct kmz_ctx {
   uint64_t cap = 0, tcap = 1ull << 16, ccap = 1ull << 20;
   uint64_t sig_seed = SIG_SEED0;  // K4 ancestry-hash seed (changed after a collision)
   uint32_t dcap = 1024;
+  uint32_t scap = 1u << 15;  // K4 staged keys per persistent workgroup (grown when it overflows)
   uint32_t mcap = 1u << 16;   // window-join miss table slots (grown on F_MISS_OVERFLOW)
   bool table_hint = false;    // the loaded batch failed the uniqueness certificate: go to the table path
   void *hpin = nullptr;       // pinned host copy of counters + stats64 (one read-back per run)
@@ -542,7 +543,7 @@ static int run_deps(kmz_ctx *c, bool links) {
     // deferred chain checks (overflow is handled in place, just slower)
     // and the slots each workgroup claims in the chain table (wcap each; the
     // run's global list of wcap more follows them)
-    const uint32_t scap = 1u << 15, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
+    const uint32_t scap = c->scap, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
     void *old_ctab = c->ctab.p;
     if (ensure(c, c->ctab, c->ccap * 32) || ensure(c, c->ctile, (size_t)nt * 16) ||
         ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, (size_t)ng * scap * 8) ||
@@ -700,6 +701,11 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
     if (h[C_FLAGS] & F_CTAB_DIRTY) c->ctab_dirty = true;
+    // staged keys overflowed (low chain reuse, config 5): the overflow was
+    // inserted in place, correct but serial per leader; stage more next time
+    // (<= 8 GB of staging)
+    if ((h[C_FLAGS] & F_STAGE_FULL) && (uint64_t)chain_grid((uint32_t)c->n) * c->scap * 4 * 8 <= (8ull << 30))
+      c->scap *= 4;
     if ((flags & KMZ_RUN_DEPS) && (c->path & 1) && h[C_CERT]) {  // a repeated span id: the table path, same run
       c->table_hint = true;
       continue;

@@ -389,8 +389,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           const uint64_t key = edge_key(r.z, es, kk, ((r.w >> 16) & 3) == KIND_SERVER);
           if (base + d <= scap)
             stage[(uint64_t)blockIdx.x * scap + base + kk - 1] = key;  // inserted by k_chain_settle
-          else
-            edge_insert(key, trip, tcap, &flags);  // staging region full: insert here
+          else {
+            edge_insert(key, trip, tcap, &flags);  // staging region full: insert here (slow: one lane per chain)
+            flags |= F_STAGE_FULL;
+          }
           a = r.w & 0xFFFF;
         }
       }

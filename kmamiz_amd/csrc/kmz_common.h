@@ -25,6 +25,7 @@ constexpr uint32_t F_TRIPLE_OVERFLOW = 16u;
 constexpr uint32_t F_TABLE_FULL = 32u;
 constexpr uint32_t F_CHAIN_OVERFLOW = 64u;
 constexpr uint32_t F_CTAB_DIRTY = 512u;     // (informational) the chain table could not be cleared by list
+constexpr uint32_t F_STAGE_FULL = 1024u;    // (informational) K4 key staging overflowed: keys went straight to the edge set
 constexpr uint32_t F_MISS_OVERFLOW = 256u;  // the window join's miss table is too small (grown, run again)
 constexpr uint32_t F_SIG = 128u;  // a 64-bit ancestry hash collision (K4 retries with another seed)
 

@@ -10,8 +10,9 @@ from kmamiz_amd import Engine, synth  # noqa: E402
 from kmamiz_amd import _lib as L  # noqa: E402
 
 ntr = int(sys.argv[1]) if len(sys.argv) > 1 else 3650000
+cfg = int(sys.argv[2]) if len(sys.argv) > 2 else synth.MESH
 e = Engine(0)
-e.load_synthetic(synth.MESH, synth.SEED, 0, ntr)
+e.load_synthetic(cfg, synth.SEED, 0, ntr)
 buf = (C.c_ulonglong * 8)()
 e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
 names = ["loop/next", "fill", "hash+probe-issue", "check+elect", "leaders", "stats"]
