@@ -262,6 +262,7 @@ kmz_ctx *kmz_create(int device, void *stream) {
     return nullptr;
   }
   if (const char *a = getenv("KMZ_ABLATE")) c->ablate = (uint32_t)strtoul(a, nullptr, 0);
+  if (c->ablate & (1u << 30)) c->scap = 256;  // test knob: tiny key staging (overflow + growth paths)
   if (ensure(c, c->counters, C_COUNT * 4) || ensure(c, c->stats64, S_COUNT * 8)) {
     delete c;
     return nullptr;

@@ -552,3 +552,35 @@ def test_from_json_equals_object_ingest(engine, src):
     assert (a.combineLogsToRealtimeData([]).toCombinedRealtimeData().toJSON()
             == b.combineLogsToRealtimeData([]).toCombinedRealtimeData().toJSON())
     assert a.toEndpointDependencies().toJSON() == b.toEndpointDependencies().toJSON()
+
+
+@pytest.mark.parametrize("knob", [1 << 30])
+def test_key_staging_paths_equal(engine, knob):
+    """K4's staged edge keys reach the edge set through k_chain_settle, or in
+    place when a workgroup's staging overflows (KMZ_ABLATE bit 30: 256 slots;
+    the staging then grows run by run).  Same graph either way."""
+    import os
+
+    from kmamiz_amd import Engine
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    def run(e):
+        e.load_synthetic(5, synth.SEED, 0, 20000)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        return e.triples(), e.endpoints(), e.info()
+
+    a = run(engine)
+    os.environ["KMZ_ABLATE"] = str(knob)
+    try:
+        e2 = Engine(0)
+    finally:
+        del os.environ["KMZ_ABLATE"]
+    try:
+        for _ in range(3):  # overflow, then grown staging
+            b = run(e2)
+            assert np.array_equal(a[0], b[0])
+            assert a[1].tobytes() == b[1].tobytes()
+            assert {k: v for k, v in a[2].items() if k != "flags"} == {k: v for k, v in b[2].items() if k != "flags"}
+    finally:
+        e2.close()
