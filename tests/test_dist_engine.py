@@ -2,7 +2,9 @@
 tensors) share the one GPU, each runs its traceId shard, and the partials and
 edge keys merge through kmamiz_amd.dist (kmz_partials_copy, kmz_merge_triples,
 kmz_finalize).  Both ranks must end with the single-engine result over the
-whole batch, bit for bit."""
+whole batch, bit for bit -- including the service tail run on the merged edge
+set (kmz_tail_run: the north_star's "edge sets merge ... before the
+service-level instability, coupling/cohesion and risk computation")."""
 import os
 import socket
 
@@ -49,10 +51,14 @@ def _worker(rank, world, port, q):
         e.import_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
         e.finalize()
         groups, keys, eps = e.fetch()
-        q.put((rank, groups.tobytes(), np.sort(keys).tobytes(), eps.tobytes()))
+        from kmamiz_amd.tail import maps_for_synth, run_tail
+
+        tl = run_tail(e, maps_for_synth(synth.MESH), eps)
+        q.put((rank, groups.tobytes(), np.sort(keys).tobytes(), eps.tobytes(),
+               (tl.stats.tobytes(), tl.by_dist.tobytes(), tl.gateway.tobytes(), tl.services.tobytes())))
         e.close()
     except Exception as ex:  # surfaced by the parent
-        q.put((rank, "error", repr(ex), None))
+        q.put((rank, "error", repr(ex), None, None))
     finally:
         dist.destroy_process_group()
 
@@ -80,9 +86,14 @@ def test_two_rank_merge_equals_single_engine():
         e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
         g, k, ep = e.fetch()
         exp = (g.tobytes(), np.sort(k).tobytes(), ep.tobytes())
+        from kmamiz_amd.tail import maps_for_synth, run_tail
+
+        tl = run_tail(e, maps_for_synth(synth.MESH), ep)
+        exp_tail = (tl.stats.tobytes(), tl.by_dist.tobytes(), tl.gateway.tobytes(), tl.services.tobytes())
     finally:
         e.close()
     for r in res:
         assert r[1] == exp[0]
         assert r[2] == exp[1]
         assert r[3] == exp[2]
+        assert r[4] == exp_tail
