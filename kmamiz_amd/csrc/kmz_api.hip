@@ -66,7 +66,7 @@ struct kmz_ctx {
   uint32_t tl_n_ep = 0, tl_n_cls = 0, tl_n_svc = 0, tl_n_dist = 64, tl_deep = 0;
   uint32_t tl_rel_dist = 0;  // distances in the last run's relying table (0: not complete, use the details)
   bool tl_map = false, tl_ran = false;
-  uint64_t tl_acap = 0, tl_pacap = 0, tl_nd = 0, tl_np = 0;
+  uint64_t tl_acap = 0, tl_pacap = 0, tl_lcap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0;
   bool ctab_dirty = true;  // the chain table holds entries no list records (new, or a list overflowed)
   int path = 0;             // kmz_info.path of the last dependency run
   bool sstats = false;      // shape-level K3 partials computed in this run
@@ -999,7 +999,7 @@ int kmz_tail_map_set(kmz_ctx *c, const kmz_tail_map *m) {
   for (uint32_t k = 0; k < m->n_cls; ++k)
     if (m->lsvc[k] >= m->n_lsvc) return fail(c, KMZ_E_RANGE, "tail link-class id out of range");
   if (ensure(c, c->tl_svc, (size_t)m->n_ep * 4) || ensure(c, c->tl_cls, (size_t)m->n_ep * 4) ||
-      ensure(c, c->tl_lsvc, (size_t)m->n_cls * 4) || ensure(c, c->tl_hasin, m->n_ep) || ensure(c, c->tl_cnt, 32))
+      ensure(c, c->tl_lsvc, (size_t)m->n_cls * 4) || ensure(c, c->tl_hasin, m->n_ep) || ensure(c, c->tl_cnt, 64))
     return KMZ_E_HIP;
   if (m->n_ep) {
     HIPCHK(c, hipMemcpyAsync(c->tl_svc.p, m->svc, (size_t)m->n_ep * 4, hipMemcpyHostToDevice, c->stream));
@@ -1032,11 +1032,15 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
   }
   // link keys <= 2 per edge key (load <= 1/2); pairs <= 1 per edge key; the
   // detail / pair tables start smaller and grow on overflow
-  const uint64_t lcap = pow2_at_least(4 * nt + 64), pcap = pow2_at_least(2 * nt + 64);
+  // link / pair sets: sized by the previous run's first occurrences (load
+  // <= 1/2, cache-resident when the keys repeat), or by the worst case (two
+  // link keys and one pair per edge key) on the first run; grown on overflow
+  if (!c->tl_lcap) c->tl_lcap = pow2_at_least(4 * nt + 64);
+  if (!c->tl_pcap) c->tl_pcap = pow2_at_least(2 * nt + 64);
   if (!c->tl_acap) c->tl_acap = pow2_at_least(nt / 2 + 4096);
   if (!c->tl_pacap) c->tl_pacap = pow2_at_least(nt / 4 + 4096);
   for (int attempt = 0;; ++attempt) {
-    const uint64_t acap = c->tl_acap, pacap = c->tl_pacap;
+    const uint64_t acap = c->tl_acap, pacap = c->tl_pacap, lcap = c->tl_lcap, pcap = c->tl_pcap;
     if (ensure(c, c->tl_lset, lcap * 8) || ensure(c, c->tl_akey, acap * 8) || ensure(c, c->tl_aval, acap * 16) ||
         ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
         ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
@@ -1052,7 +1056,7 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       HIPCHK(c, hipMemsetAsync(c->tl_pkey.p, 0, pacap * 8, c->stream));
       HIPCHK(c, hipMemsetAsync(c->tl_pval.p, 0, pacap * 4, c->stream));
       HIPCHK(c, hipMemsetAsync(c->tl_hasin.p, 0, c->tl_n_ep ? c->tl_n_ep : 1, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_cnt.p, 0, 32, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->tl_cnt.p, 0, 64, c->stream));
       HIPCHK(c, hipMemsetAsync(c->tl_fkey.p, 0, acap * 8, c->stream));
       HIPCHK(c, hipMemsetAsync(c->tl_fval.p, 0, acap * 4, c->stream));
       if (c->tl_n_svc) {
@@ -1069,9 +1073,9 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
                   acap, P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey),
                   P<uint32_t>(c->tl_pval), pacap, P<uint8_t>(c->tl_hasin), P<unsigned long long>(c->tl_fkey),
                   P<uint32_t>(c->tl_fval), acap, P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), c->tl_n_dist,
-                  P<unsigned int>(c->tl_cnt), P<uint32_t>(c->tl_det), P<uint32_t>(c->tl_pairs), cnt64 + 1, true);
+                  P<unsigned int>(c->tl_cnt), P<uint32_t>(c->tl_det), P<uint32_t>(c->tl_pairs), cnt64 + 1);
     }
-    unsigned long long h[4];
+    unsigned long long h[5];
     HIPCHK(c, hipMemcpyAsync(h, c->tl_cnt.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
@@ -1081,8 +1085,13 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       if (attempt >= 3) return fail(c, KMZ_E_OVERFLOW, "service tail table overflow");
       c->tl_acap *= 4;
       c->tl_pacap *= 4;
+      c->tl_lcap = std::max(c->tl_lcap * 4, pow2_at_least(4 * nt + 64));
+      c->tl_pcap = std::max(c->tl_pcap * 4, pow2_at_least(2 * nt + 64));
       continue;
     }
+    const uint64_t won_l = (uint32_t)h[4], won_p = (uint32_t)(h[4] >> 32);
+    c->tl_lcap = pow2_at_least(2 * won_l + 4096);  // the next run's sets (this run's keys at load <= 1/2)
+    c->tl_pcap = pow2_at_least(2 * won_p + 4096);
     // keep the detail / pair tables at load <= 1/2 for the next run
     while (h[1] * 2 > c->tl_acap) c->tl_acap *= 2;
     while (h[2] * 2 > c->tl_pacap) c->tl_pacap *= 2;

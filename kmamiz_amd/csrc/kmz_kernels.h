@@ -113,7 +113,7 @@ void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned l
                  uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
                  uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned long long *fkey, uint32_t *fval,
                  uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
-                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts, bool compact);
+                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts);
 
 // window parent join + uniqueness certificate (kmz_join.hip)
 struct CertPlan {

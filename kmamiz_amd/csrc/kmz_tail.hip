@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
                                                     uint32_t *__restrict__ sstat, uint32_t *__restrict__ rel,
                                                     uint32_t n_dist, unsigned int *__restrict__ counters) {
   const uint64_t n = *n_keys;
-  uint32_t flags = 0;
+  uint32_t flags = 0, won_l = 0, won_p = 0;  // first occurrences in the link / pair sets (sizes the next run's sets)
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = keys[i];
     const uint32_t a = (uint32_t)(k >> 40), s = (uint32_t)(k >> 16) & 0xFFFFFFu, d = (uint32_t)(k >> 1) & 0x7FFFu;
@@ -118,6 +118,7 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
     if (on) lk[side++] = ((uint64_t)svc[a] << 40) | ((uint64_t)cls[s] << 16) | (1u << 15) | d;
     for (uint32_t t = 0; t < side; ++t) {
       if (!tail_set_put(lset, lcap, lk[t], &flags)) continue;
+      ++won_l;
       const uint32_t c = (uint32_t)(lk[t] >> 16) & 0xFFFFFFu;
       const uint64_t dk = (lk[t] & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
       const uint64_t p = tail_agg_slot(akey, acap, dk, &flags);
@@ -125,12 +126,6 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
       const uint32_t ty = (uint32_t)(lk[t] >> 15) & 1u, sv = (uint32_t)(lk[t] >> 40);
       atomicAdd(&aval[4 * p + 0], 1u);                              // count
       const uint32_t old = atomicAdd(&aval[4 * p + 1 + ty], 1u);    // dependingBy (CLIENT) / dependingOn (SERVER)
-      if (ty == 0) {  // RelyingFactor: sum of dependingBy / distance (RiskAnalyzer.ts:124-137)
-        if (d < n_dist)
-          atomicAdd(&rel[(uint64_t)sv * n_dist + d], 1u);
-        else
-          atomicMax(&counters[6], d);  // deeper than the dense table: the host uses the details
-      }
       if (old) continue;
       // first type-`ty` link of this (service, linked service, distance):
       // ACS counts distance-1 details with dependingBy / dependingOn > 0
@@ -144,6 +139,7 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
     }
     // cohesion: (consumer service, consumed endpoint) at distance 1
     if (d == 1 && tail_set_put(pset, pcap, ((uint64_t)(s + 1) << 32) | usn[a], &flags)) {
+      ++won_p;
       const uint64_t p = tail_agg_slot(pkey, pacap, ((uint64_t)(svc[s] + 1) << 32) | usn[a], &flags);
       if (p != pacap) {
         atomicAdd(&sstat[8 * svc[s] + TS_CONSUMES], 1u);
@@ -152,6 +148,14 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
     }
   }
   if (flags) atomicOr(&counters[C_FLAGS], flags);
+  for (int o = 32; o > 0; o >>= 1) {
+    won_l += __shfl_xor(won_l, o, 64);
+    won_p += __shfl_xor(won_p, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && (won_l | won_p)) {
+    atomicAdd(&counters[8], won_l);  // (u32 words 8 and 9 of the tail's counter block)
+    atomicAdd(&counters[9], won_p);
+  }
 }
 
 // aggregation tables -> dense kmz_tail_detail (MODE 0) / kmz_tail_pair (MODE 1)
@@ -160,7 +164,9 @@ template <int MODE>
 __global__ void __launch_bounds__(256) k_tail_compact(const unsigned long long *__restrict__ akey,
                                                       const uint32_t *__restrict__ aval, uint64_t cap,
                                                       uint32_t *__restrict__ out,
-                                                      unsigned long long *__restrict__ count) {
+                                                      unsigned long long *__restrict__ count,
+                                                      uint32_t *__restrict__ rel, uint32_t n_dist,
+                                                      unsigned int *__restrict__ counters) {
   constexpr uint32_t W = MODE == 0 ? 6 : 3;  // record words
   const uint32_t lane = threadIdx.x & 63;
   for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < cap; p0 += (uint64_t)gridDim.x * blockDim.x) {
@@ -181,6 +187,15 @@ __global__ void __launch_bounds__(256) k_tail_compact(const unsigned long long *
         r[3] = aval[4 * p + 0];
         r[4] = aval[4 * p + 1];
         r[5] = aval[4 * p + 2];
+        // RelyingFactor: sum of dependingBy / distance (RiskAnalyzer.ts:124-137),
+        // per (service, distance) -- one add per detail, not per link key
+        const uint32_t d = (uint32_t)k & 0xFFFFu;
+        if (r[4]) {
+          if (d < n_dist)
+            atomicAdd(&rel[(uint64_t)r[0] * n_dist + d], r[4]);
+          else
+            atomicMax(&counters[6], d);  // deeper than the dense table: the host uses the details
+        }
       } else {  // pair detail key (svc + 1) << 32 | consumer
         r[0] = (uint32_t)(k >> 32) - 1;
         r[1] = (uint32_t)k;
@@ -196,16 +211,17 @@ void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned l
                  uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
                  uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned long long *fkey, uint32_t *fval,
                  uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
-                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts, bool compact) {
+                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts) {
   const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + 255) / 256, 8192));
   hipLaunchKernelGGL(k_tail_links, dim3(g), dim3(256), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls,
                      lset, lcap, akey, aval, acap, pset, pcap, pkey, pval, pacap, hasin, fkey, fval, fcap, sstat, rel,
                      n_dist, counters);
-  if (!compact) return;
   const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((acap + 255) / 256, 4096));
-  hipLaunchKernelGGL(k_tail_compact<0>, dim3(ga), dim3(256), 0, s, akey, aval, acap, links_out, out_counts);
+  hipLaunchKernelGGL(k_tail_compact<0>, dim3(ga), dim3(256), 0, s, akey, aval, acap, links_out, out_counts, rel, n_dist,
+                     counters);
   const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pacap + 255) / 256, 4096));
-  hipLaunchKernelGGL(k_tail_compact<1>, dim3(gp), dim3(256), 0, s, pkey, pval, pacap, pairs_out, out_counts + 1);
+  hipLaunchKernelGGL(k_tail_compact<1>, dim3(gp), dim3(256), 0, s, pkey, pval, pacap, pairs_out, out_counts + 1, rel,
+                     n_dist, counters);
 }
 
 }  // namespace kmz
