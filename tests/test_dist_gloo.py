@@ -3,7 +3,9 @@
 Each rank takes half of the traces of a synthetic batch (whole traces, global
 indices via index_base), forms the engine's partial layout for its shard, and
 merges through the same functions the GPU path uses over RCCL.  The merged
-result must equal the single-batch oracle exactly (integers) / within 1e-9."""
+result must equal the single-batch oracle exactly (integers) / within 1e-9,
+and so must the service tail computed over the merged edge set (its kernel's
+numpy restatement, tests/test_tail.py, pinned there against the oracle)."""
 import os
 import socket
 
@@ -84,6 +86,19 @@ def _worker(rank, world, port, q):
             ok &= bool(np.array_equal(has, oep["has_row"]))
             ok &= bool(np.array_equal(ev[E:][has] >> U64(1), oep["first"][has]))
             ok &= bool(np.array_equal((ev[E:][has] & U64(1)) == 0, oep["external"][has]))
+            # the service tail over the merged edge set = over the single batch
+            from test_tail import _tail_np
+
+            from kmamiz_amd.tail import maps_for_synth
+
+            maps = maps_for_synth(cfg)
+            first = np.where(has, ev[E:] >> U64(1), U64(0xFFFFFFFFFFFFFFFF))
+            got = _tail_np(np.sort(merged_keys.numpy().view(U64)), maps, has, first)
+            ofirst = np.where(oep["has_row"], oep["first"], np.iinfo(np.uint64).max).astype(U64)
+            exp = _tail_np(okeys, maps, oep["has_row"], ofirst)
+            ok &= bool(np.array_equal(got.stats, exp.stats) and np.array_equal(got.by_dist, exp.by_dist))
+            ok &= bool(np.array_equal(got.gateway, exp.gateway) and np.array_equal(got.services, exp.services))
+            ok &= got.instability() == exp.instability() and got.coupling() == exp.coupling()
             q.put(ok)
     finally:
         dist.destroy_process_group()
