@@ -169,9 +169,9 @@ def main():
             eng.export_partials(L.PART_GROUPS, g.data_ptr(), gw, True)
             eng.export_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
             eng.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, True)
-            kdist.merge_group_partials(g, gw // 6)
-            kdist.merge_endpoint_partials(e, ew // 2)
-            kdist.merge_edge_keys_into(eng, t[:tw])  # union in the engine's device edge set
+            # three collectives: SUM moments, MAX of max / negated min fields
+            # + key count, all-gather of the keys (union in the engine's set)
+            kdist.merge_all(g, gw // 6, e, ew // 2, t[:tw], engine=eng)
             eng.import_partials(L.PART_GROUPS, g.data_ptr(), gw, True)
             eng.import_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
             eng.finalize()

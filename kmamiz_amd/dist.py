@@ -62,6 +62,53 @@ def merge_endpoint_partials(e: torch.Tensor, n_ep: int) -> torch.Tensor:
     return e
 
 
+def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: torch.Tensor, engine=None):
+    """The whole per-step merge in three collectives (the bench's N > 1 path):
+    one SUM all-reduce of the group moments, one MAX all-reduce that carries
+    every max field and every min field negated (min x = -max -x in signed
+    order) plus the edge-key count, and one all-gather of the padded keys.
+    Same results as merge_group_partials + merge_endpoint_partials +
+    merge_edge_keys(_into); returns the merged keys when ``engine`` is None."""
+    if dist.get_world_size() == 1:
+        return None if engine is not None else torch.unique(keys)
+    G, E = n_groups, n_ep
+    if G:
+        dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM)  # modular: exact for u64
+    dev = p.device
+    ming = p[5 * G :]
+    mine = e[E:]
+    mx = torch.cat([
+        _as_signed_order(p[4 * G : 5 * G]),
+        _as_signed_order(e[:E]),
+        -torch.where(ming == -1, torch.full_like(ming, _I64_MAX), ming),
+        -torch.where(mine == -1, torch.full_like(mine, _I64_MAX), mine),
+        torch.tensor([keys.numel()], dtype=torch.int64, device=dev),
+    ])
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    p[4 * G : 5 * G] = _as_signed_order(mx[:G])
+    e[:E] = _as_signed_order(mx[G : G + E])
+    fg = -mx[G + E : 2 * G + E]
+    fe = -mx[2 * G + E : 2 * G + 2 * E]
+    p[5 * G :] = torch.where(fg == _I64_MAX, torch.full_like(fg, -1), fg)
+    e[E:] = torch.where(fe == _I64_MAX, torch.full_like(fe, -1), fe)
+    m = int(mx[-1].item())
+    pad = torch.zeros(m, dtype=torch.int64, device=keys.device)
+    pad[: keys.numel()] = keys
+    if keys.is_cuda:
+        allk = torch.empty(m * dist.get_world_size(), dtype=torch.int64, device=keys.device)
+        dist.all_gather_into_tensor(allk, pad)
+        torch.cuda.current_stream(keys.device).synchronize()  # the engine's stream may not be torch's
+    else:
+        parts = [torch.empty_like(pad) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, pad)
+        allk = torch.cat(parts)
+    if engine is not None:
+        engine.merge_triples(allk.data_ptr(), allk.numel(), keys.is_cuda)
+        return None
+    u = torch.unique(allk)
+    return u[u != 0]
+
+
 def merge_edge_keys(keys: torch.Tensor) -> torch.Tensor:
     """Union of every rank's unique edge keys (int64 view, keys are > 0)."""
     if dist.get_world_size() == 1:

@@ -1,6 +1,6 @@
 """The bench's multi-GPU merge sequence on real engines: two ranks (gloo, CPU
 tensors) share the one GPU, each runs its traceId shard, and the partials and
-edge keys merge through kmamiz_amd.dist (kmz_partials_copy, kmz_merge_triples,
+edge keys merge through kmamiz_amd.dist.merge_all (kmz_partials_copy, kmz_merge_triples,
 kmz_finalize).  Both ranks must end with the single-engine result over the
 whole batch, bit for bit -- including the service tail run on the merged edge
 set (kmz_tail_run: the north_star's "edge sets merge ... before the
@@ -44,9 +44,7 @@ def _worker(rank, world, port, q):
         e.export_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
         e.export_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
         e.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, False)
-        kdist.merge_group_partials(g, gw // 6)
-        kdist.merge_endpoint_partials(ep, ew // 2)
-        kdist.merge_edge_keys_into(e, t[:tw])
+        kdist.merge_all(g, gw // 6, ep, ew // 2, t[:tw], engine=e)  # bench.py's three-collective merge
         e.import_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
         e.import_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
         e.finalize()

@@ -65,11 +65,17 @@ def _worker(rank, world, port, q):
         G = table.n_tag_ep * table.n_status
         pt = torch.from_numpy(p.view(np.int64).copy())
         et = torch.from_numpy(e.view(np.int64).copy())
+        kt = torch.from_numpy(keys.view(np.int64).copy())
+        # the fused three-collective merge (bench.py) equals the separate ones
+        pf, ef = pt.clone(), et.clone()
+        fused_keys = kdist.merge_all(pf, G, ef, table.n_dep_ep, kt)
         kdist.merge_group_partials(pt, G)
         kdist.merge_endpoint_partials(et, table.n_dep_ep)
-        merged_keys = kdist.merge_edge_keys(torch.from_numpy(keys.view(np.int64).copy()))
+        merged_keys = kdist.merge_edge_keys(kt)
+        fused_ok = bool(torch.equal(pf, pt) and torch.equal(ef, et) and torch.equal(fused_keys, merged_keys))
         if rank == 0:
             full, _ = synth.host_batch(cfg, 0, ntr)
+            assert fused_ok
             groups = finalize_host(pt.numpy().view(U64), G)
             o = c_oracle.stats(full, table.tag_ep, table.n_tag_ep, table.n_status)
             ok = bool(np.array_equal(groups["combined"], o["combined"]))
