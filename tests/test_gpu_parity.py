@@ -176,6 +176,13 @@ def test_messy_batches_vs_oracle(engine, seed):
         return
     ours = Traces(traces, engine=engine)
     assert ours.toEndpointDependencies().toJSON() == exp_deps
+    # the service tail at scale over the same batch (kmz_tail_run) vs the
+    # oracle's tail of the reduced graph (duplicate ids, non-SERVER ancestors,
+    # tag-fallback identities)
+    from test_tail import _compare
+
+    red = O.strip_undef(O.EndpointDependencies([]).combineWith(O.EndpointDependencies(exp_deps)).trim().toJSON())
+    _compare(ours.toEndpointDependencies().service_tail(), O.EndpointDependencies(red))
     for rule in ("rt", "tag"):
         try:
             exp = (ref.toRealTimeData() if rule == "rt" else ref.combineLogsToRealtimeData([])).toCombinedRealtimeData()
@@ -192,6 +199,8 @@ def test_empty_batch(engine):
 
     t = Traces([], engine=engine)
     assert t.toEndpointDependencies().toJSON() == []
+    tail = t.toEndpointDependencies().service_tail()
+    assert tail.instability() == [] and tail.coupling() == [] and tail.cohesion() == []
     assert t.toRealTimeData().toCombinedRealtimeData().toJSON() == []
 
 
