@@ -593,3 +593,33 @@ def test_key_staging_paths_equal(engine, knob):
             assert {k: v for k, v in a[2].items() if k != "flags"} == {k: v for k, v in b[2].items() if k != "flags"}
     finally:
         e2.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_side_stream_run_equals_separate_runs(engine, seed):
+    """A stats + dependency run of a small batch uses the side stream (K3 and
+    the certificate beside the join and the walk); with repeated span ids the
+    certificate fails and the run is redone on the table path.  Either way the
+    results equal a stats-only run followed by a dependency-only run (both
+    serial)."""
+    from kmamiz_amd import CycleError
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd.ingest import ingest_traces
+
+    rng = random.Random(1000 + seed)
+    traces = messy_batch(rng, 60, rng.choice([8, 64, 4096]))
+    batch, d, _ = ingest_traces(traces)
+    engine.load(batch, d.shape_table())
+    engine._loaded_token = None
+    try:
+        engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    except CycleError:
+        return
+    g1, k1, e1 = engine.groups(), engine.triples(), engine.endpoints()
+    engine.run(L.RUN_STATS_TAG)
+    g2 = engine.groups()
+    engine.run(L.RUN_DEPS)
+    k2, e2 = engine.triples(), engine.endpoints()
+    assert g1.tobytes() == g2.tobytes()
+    assert np.array_equal(k1, k2)
+    assert e1.tobytes() == e2.tobytes()
