@@ -32,9 +32,11 @@ sys.path.insert(0, ROOT)
 #   cert   k_cert_split   uniqueness certificate: one radix split of the
 #                         8-B hashed span id (read + write)      16 B/span
 #   check  k_cert_check   certificate check: one read of it       8 B/span
-def alg_bytes(kernel, n, n_server, relations):
+#   tail   k_tail_links   service tail: one read of each edge key  8 B/key
+#          (+ k_tail_compact; config 5 only)
+def alg_bytes(kernel, n, n_server, relations, n_keys=0):
     return {"join": 57 * n, "stats": 19 * n, "reduce": 16 * n_server, "walk": 12 * relations,
-            "cert": 16 * n, "check": 8 * n}.get(kernel, 0)
+            "cert": 16 * n, "check": 8 * n, "tail": 8 * n_keys}.get(kernel, 0)
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -224,7 +226,7 @@ def main():
         if not calls:
             continue
         avg = ms / calls
-        alg = alg_bytes(k, n_local, info["n_server"], A) if calls == args.steps else 0
+        alg = alg_bytes(k, n_local, info["n_server"], A, info["n_triples"]) if calls == args.steps else 0
         per_kernel[k] = {"ms_per_step": round(ms / args.steps, 4), "calls_per_step": round(calls / args.steps, 2),
                          "avg_ms": round(avg, 4), "alg_bytes": alg,
                          "gbs": round(alg / (avg * 1e-3) / 1e9, 1) if alg else None}
@@ -233,7 +235,8 @@ def main():
     kern_ms = sum(v["ms_per_step"] for v in per_kernel.values())
     pipe_bytes = sum(v["alg_bytes"] for v in per_kernel.values() if v["alg_bytes"])
     kname = {"join": "k_join_window", "stats": "k3_produce" if "reduce" in per_kernel else "k_stats",
-             "reduce": "k3_reduce", "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check"}[dom]
+             "reduce": "k3_reduce", "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check",
+             "tail": "k_tail_links"}[dom]
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0:
