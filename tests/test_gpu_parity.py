@@ -623,3 +623,34 @@ def test_side_stream_run_equals_separate_runs(engine, seed):
     assert g1.tobytes() == g2.tobytes()
     assert np.array_equal(k1, k2)
     assert e1.tobytes() == e2.tobytes()
+
+
+def test_certificate_at_scale_finds_one_repeated_id(engine):
+    """At 10^7 spans the certificate has 4096 sub-bins, more than the
+    persistent check kernel has workgroups, so each workgroup checks many
+    sub-bins over one LDS set.  A clean batch must pass (window path); the
+    same batch with one span id repeated far away must fail it and take the
+    table path, with the reference's duplicate-id semantics."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(3, 0, 370000)
+    assert len(batch) > 10_000_000
+    table = synth.shape_table(3)
+    engine.load(batch, table)
+    engine._loaded_token = None
+    engine.run(L.RUN_DEPS)
+    info = engine.info()
+    assert info["path"] & 1 and info["n_dups"] == 0
+    rng = np.random.default_rng(7)
+    for _ in range(5):  # one repeated id at a time, in different sub-bins
+        i, j = int(rng.integers(0, len(batch) // 2)), int(rng.integers(len(batch) // 2, len(batch)))
+        keep = batch.span_id[j].copy()
+        batch.span_id[j] = batch.span_id[i]
+        engine.load(batch, table)
+        engine._loaded_token = None
+        engine.run(L.RUN_DEPS)
+        info = engine.info()
+        batch.span_id[j] = keep
+        assert not (info["path"] & 1), "the certificate missed a repeated span id"
+        assert info["n_dups"] == 1
