@@ -359,10 +359,10 @@ class NativeTraces {
   toRealTimeData(replicas) {
     return new NativeRealtimeDataList(this, "rt", replicas);
   }
+  // Traces.ts:55-106: stats from the engine; the Envoy-log join (59-84) adds
+  // bodies and content types on the host (SURVEY.md 8f row 3)
   combineLogsToRealtimeData(structuredLogs, replicas) {
-    if ((structuredLogs || []).some((l) => l.traces.length))
-      throw new Error("Envoy log bodies (SURVEY.md 8f item 3) are not handled by the engine yet");
-    return new NativeRealtimeDataList(this, "tag", replicas);
+    return new NativeRealtimeDataList(this, "tag", replicas, logMap(structuredLogs));
   }
   toEndpointDependencies() {
     const b = this._batch();
@@ -483,11 +483,47 @@ class NativeTraces {
   }
 }
 
+// traceId -> spanId -> structured log trace (Traces.ts:59-67)
+function logMap(structuredLogs) {
+  const m = new Map();
+  (structuredLogs || []).forEach((l) => {
+    if (l.traces.length === 0) return;
+    const { traceId } = l.traces[0];
+    if (!m.has(traceId)) m.set(traceId, new Map());
+    l.traces.forEach((t) => m.get(traceId).set(t.spanId, t));
+  });
+  return m.size ? m : null;
+}
+
+const JSON_CT = "application/json";
+
 class NativeRealtimeDataList {
-  constructor(traces, rule, replicas) {
+  constructor(traces, rule, replicas, logs) {
     this._t = traces;
     this._rule = rule;
     this._replicas = replicas;
+    this._logs = logs || null;
+  }
+  // the log the reference picks for flat span i (Traces.ts:80-84)
+  _log(i) {
+    if (!this._logs) return undefined;
+    if (!this._flat) this._flat = [].concat(...this._t._traces);
+    const s = this._flat[i];
+    const lm = this._logs.get(s.traceId);
+    let log = lm ? lm.get(s.id) : undefined;
+    if ((!log || log.isFallback) && s.parentId) log = lm ? lm.get(s.parentId) : undefined;
+    return log;
+  }
+  // the body fields of a row (Traces.ts:94-97; `log?.response.body` throws without a response)
+  _logFields(i) {
+    const log = this._log(i);
+    if (!log) return {};
+    return {
+      responseBody: log.response.body,
+      responseContentType: log.response.contentType,
+      requestBody: log.request.body,
+      requestContentType: log.request.contentType,
+    };
   }
   toJSON() {
     const b = this._t._batch();
@@ -506,6 +542,7 @@ class NativeRealtimeDataList {
           method: f.method,
           latency: sp.duration[i] / 1000,
           status: b.statuses[sp.status[i]],
+          ...this._logFields(i),
           uniqueServiceName: f.uniqueServiceName,
           uniqueEndpointName: f.uniqueEndpointName,
           replica: replicaOf(this._replicas, f.uniqueServiceName),
@@ -533,11 +570,16 @@ class NativeRealtimeDataList {
       used.push({ g, e, n, first });
     }
     used.sort((a, c) => epFirst.get(a.e) - epFirst.get(c.e) || a.first - c.first);
-    return used.map(({ g, e, n }) => {
+    return used.map(({ g, e, n, first }) => {
       const i = epFirst.get(e);
       const f = b.ident[this._rule][b.spans.shape[i]];
       if (!f) throw b.poison[this._rule].get(e);
       const r = replicaOf(this._replicas, f.uniqueServiceName);
+      // with logs: the first row's content types (RealtimeDataList.ts:53-89);
+      // JSON bodies need json-to-ts schemas (120-155), which this build lacks
+      const lf = this._logs ? this._logFields(first) : {};
+      if (lf.requestContentType === JSON_CT || lf.responseContentType === JSON_CT)
+        throw new Error("application/json bodies need json-to-ts schemas (SURVEY.md 8f row 3)");
       return strip({
         uniqueServiceName: f.uniqueServiceName,
         uniqueEndpointName: f.uniqueEndpointName,
@@ -550,6 +592,8 @@ class NativeRealtimeDataList {
         avgReplica: r ? (r * n) / n : undefined,
         latestTimestamp: Number(v.getBigInt64(g * 40 + 16, true)),
         latency: { mean: v.getFloat64(g * 40 + 24, true), cv: v.getFloat64(g * 40 + 32, true) },
+        requestContentType: lf.requestContentType,
+        responseContentType: lf.responseContentType,
       });
     });
   }

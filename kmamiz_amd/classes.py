@@ -117,11 +117,24 @@ class Traces:
         return RealtimeDataList(_native=(self, "rt", replicas))
 
     def combineLogsToRealtimeData(self, structuredLogs=(), replicas=None) -> "RealtimeDataList":
-        """Traces.ts:55-106.  The Envoy-log body join (59-84, 94-97) only feeds
-        request/response bodies; it is SURVEY.md 8f item 3 and not built yet."""
-        if any(len(l.get("traces", [])) for l in structuredLogs or ()):
-            raise NotImplementedError("Envoy log bodies (SURVEY.md 8f item 3) are not handled by the engine yet")
-        return RealtimeDataList(_native=(self, "tag", replicas))
+        """Traces.ts:55-106.  The stats come from the engine (K3); the Envoy-log
+        join (59-84: per SERVER span the log of (traceId, id), or of (traceId,
+        parentId) when that is missing or a fallback) only adds request /
+        response bodies and content types, host-side."""
+        logs = _log_map(structuredLogs)
+        return RealtimeDataList(_native=(self, "tag", replicas, logs))
+
+    def _span_log(self, logs, i: int):
+        """The log entry the reference picks for flat span i (Traces.ts:80-84)."""
+        if not logs:
+            return None
+        s = self._ingest()[2][i]
+        lm = logs.get(s.get("traceId", UNDEFINED))
+        log = lm.get(s.get("id", UNDEFINED)) if lm is not None else None
+        # (a log object is truthy in JS even when empty)
+        if (log is None or js_truthy(log.get("isFallback", UNDEFINED))) and js_truthy(s.get("parentId", UNDEFINED)):
+            log = lm.get(s["parentId"]) if lm is not None else None
+        return log
 
     def extractContainingNamespaces(self):
         """Traces.ts:108-110."""
@@ -145,6 +158,34 @@ class Traces:
         info = dict(dep_identity(key))
         info["timestamp"] = trace["timestamp"] / 1000
         return _clean(info)
+
+
+def _log_map(structuredLogs):
+    """traceId -> spanId -> TStructuredEnvoyLogTrace (Traces.ts:59-67); a log
+    with no traces is skipped, the last entry of a spanId wins."""
+    m: Dict = {}
+    for l in structuredLogs or ():
+        trs = l.get("traces", [])
+        if len(trs) == 0:
+            continue
+        d = m.setdefault(trs[0]["traceId"], {})
+        for t in trs:
+            d[t["spanId"]] = t
+    return m
+
+
+def _log_fields(log) -> dict:
+    """The body fields of a realtime row (Traces.ts:94-97)."""
+    if log is None:
+        return {}
+    req, res = log.get("request"), log.get("response")
+    if req is None or res is None:  # `log?.response.body` throws in the reference
+        raise TypeError("Cannot read properties of undefined (reading 'body')")
+    return {"responseBody": res.get("body", UNDEFINED), "responseContentType": res.get("contentType", UNDEFINED),
+            "requestBody": req.get("body", UNDEFINED), "requestContentType": req.get("contentType", UNDEFINED)}
+
+
+JSON_CT = "application/json"
 
 
 def _replica_lookup(replicas, usn):
@@ -173,7 +214,7 @@ class RealtimeDataList:
         return set(r.get("namespace") for r in self.toJSON())
 
     def _materialize_rows(self):
-        traces, rule, replicas = self._native
+        traces, rule, replicas, logs = (tuple(self._native) + (None,))[:4]
         batch, d, flat = traces._ingest()
         out = []
         idx = np.nonzero(batch.kind == L.KIND_SERVER)[0]
@@ -196,6 +237,7 @@ class RealtimeDataList:
                         "uniqueServiceName": f["uniqueServiceName"],
                         "uniqueEndpointName": f["uniqueEndpointName"],
                         "replica": _replica_lookup(replicas, f["uniqueServiceName"]),
+                        **_log_fields(traces._span_log(logs, int(i))),
                     }
                 )
             )
@@ -204,11 +246,12 @@ class RealtimeDataList:
     def toCombinedRealtimeData(self) -> "CombinedRealtimeDataList":
         """RealtimeDataList.ts:22-97 on the GPU (K3 + finalisation)."""
         if self._native is not None:
-            traces, rule, replicas = self._native
+            traces, rule, replicas, logs = (tuple(self._native) + (None,))[:4]
             eng = traces._load()
             eng.run(L.RUN_STATS_RT if rule == "rt" else L.RUN_STATS_TAG)
             batch, d, _ = traces._ingest()
-            return CombinedRealtimeDataList(_combine_native(eng.groups(), eng.index_base, batch, d, rule, replicas))
+            return CombinedRealtimeDataList(_combine_native(eng.groups(), eng.index_base, batch, d, rule, replicas,
+                                                            traces if logs else None, logs))
         rows = self._rows or []
         batch, table, d, first_row = ingest_rows(rows)
         eng = default_engine()
@@ -234,9 +277,20 @@ def _ordered_groups(groups: np.ndarray, n_status: int):
     return [(int(used[k]), int(ep[k]), ep_first[int(ep[k])]) for k in order]
 
 
-def _combine_native(groups, index_base, batch, d: Dictionary, rule, replicas):
+def _combine_native(groups, index_base, batch, d: Dictionary, rule, replicas, traces=None, logs=None):
     n_status = max(1, len(d.statuses))
     out = []
+    # with Envoy logs: reduce() keeps the first row's content types
+    # (RealtimeDataList.ts:53-67); bodies reach the output only for
+    # application/json, where the reference also infers a schema with
+    # json-to-ts (RealtimeDataList.ts:120-155) -- absent here, so refused
+    firsts = None
+    if logs:
+        firsts = {}
+        srv = np.nonzero(batch.kind == L.KIND_SERVER)[0]
+        gid = np.asarray(d.shape_ep[rule], dtype=np.int64)[batch.shape[srv]] * n_status + batch.status[srv]
+        for i, g in zip(srv.tolist(), gid.tolist()):
+            firsts.setdefault(g, i)
     for g, e, ep_first in _ordered_groups(groups, n_status):
         if e in d.poison[rule]:
             # the reference throws while building the realtime rows (Utils.ts:90)
@@ -263,10 +317,21 @@ def _combine_native(groups, index_base, batch, d: Dictionary, rule, replicas):
                     "avgReplica": avg,
                     "latestTimestamp": int(rec["latest_timestamp"]),
                     "latency": {"mean": float(rec["mean"]), "cv": float(rec["cv"])},
+                    **_group_content_types(traces, logs, firsts, g),
                 }
             )
         )
     return out
+
+
+def _group_content_types(traces, logs, firsts, g) -> dict:
+    if firsts is None:
+        return {}
+    f = _log_fields(traces._span_log(logs, firsts[g]))
+    ct = {k: f[k] for k in ("requestContentType", "responseContentType") if k in f}
+    if JSON_CT in ct.values():
+        raise NotImplementedError("application/json bodies need json-to-ts schemas (SURVEY.md 8f row 3)")
+    return ct
 
 
 def _seq_sum(r, n):

@@ -266,6 +266,10 @@ class Traces:
                 log = lm.get(tr["parentId"], UNDEF) if lm is not None else UNDEF
             req = get(log, "request") if truthy(log) else UNDEF
             res = get(log, "response") if truthy(log) else UNDEF
+            if truthy(log) and (res is UNDEF or res is None or req is UNDEF or req is None):
+                # `log?.response.body` (Traces.ts:94-97): a log without request /
+                # response throws a TypeError in the reference
+                raise TypeError("Cannot read properties of undefined (reading 'body')")
             out.append(
                 {
                     "timestamp": tr["timestamp"],
