@@ -230,6 +230,17 @@ int kmz_finalize(kmz_ctx *ctx);
 /* host-side finalisation of one partial (same arithmetic as the device) */
 void kmz_finalize_host(const uint64_t *partials, uint64_t n_groups, kmz_group *out);
 
+/* ---- multi-GPU sharding guard ---------------------------- */
+/* Sharding by whole traces equals the reference's global span map
+ * (Traces.ts:117-123) only if no parent link crosses shards.  After a
+ * KMZ_RUN_DEPS run on the window-join path: the parent ids of this batch's
+ * spans whose parent is not in the batch (ids == NULL: count only; `mem`
+ * says where ids lives).  KMZ_E_UNSUPPORTED on the span-table path (repeated
+ * ids: sharding is not exact there anyway). */
+int kmz_unresolved_parents(kmz_ctx *ctx, uint64_t *ids, uint64_t cap, uint64_t *n_out, int mem);
+/* how many of the given ids (0 = padding) are span ids of the loaded batch */
+int kmz_count_ids(kmz_ctx *ctx, const uint64_t *ids, uint64_t n, int mem, uint64_t *found);
+
 /* ---- service-level tail over the reduced edge set ---- */
 /* Replaces the per-row scans of EndpointDependencies.toServiceDependencies
  * (EndpointDependencies.ts:369-470), whose link counts feed toServiceInstability

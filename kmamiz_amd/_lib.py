@@ -160,6 +160,8 @@ SIGNATURES = [
     ("kmz_merge_triples", C.c_int, [_P, _P, C.c_uint64, C.c_int]),
     ("kmz_parse_zipkin", C.c_int, [C.c_char_p, C.c_uint64, C.c_int, C.POINTER(C.POINTER(ZipkinBatch))]),
     ("kmz_zipkin_free", None, [C.POINTER(ZipkinBatch)]),
+    ("kmz_unresolved_parents", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64), C.c_int]),
+    ("kmz_count_ids", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.POINTER(C.c_uint64)]),
     ("kmz_tail_map_set", C.c_int, [_P, C.POINTER(TailMap)]),
     ("kmz_tail_run", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("kmz_tail_get", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, _P, C.c_uint64]),

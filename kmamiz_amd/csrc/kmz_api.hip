@@ -58,6 +58,7 @@ struct kmz_ctx {
   DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
+  DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
   DevBuf ctile;           // K4 per-workgroup stats (apart from K3's tile_tmp: the two run concurrently)
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
   // service tail (kmz_tail.hip): maps, link set, detail table, pair set, pair table, outputs
@@ -283,7 +284,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
                     &c->tl_sstat, &c->tl_rel};
@@ -1135,6 +1136,62 @@ int kmz_tail_get(kmz_ctx *c, kmz_tail_detail *det, uint64_t dcap, kmz_tail_pair 
     HIPCHK(c, hipMemcpyAsync(pairs, c->tl_pairs.p, c->tl_np * sizeof(kmz_tail_pair), hipMemcpyDeviceToHost, c->stream));
   if (has_in && c->tl_n_ep) HIPCHK(c, hipMemcpyAsync(has_in, c->tl_hasin.p, c->tl_n_ep, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_unresolved_parents(kmz_ctx *c, uint64_t *ids, uint64_t cap, uint64_t *n_out, int mem) {
+  if (!c || !n_out) return KMZ_E_ARG;
+  if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
+  if (!(c->path & 1)) return fail(c, KMZ_E_UNSUPPORTED, "span-table path: no per-span parent resolution to export");
+  if (c->hpin_valid && reinterpret_cast<const unsigned int *>(c->hpin)[C_MISS] == 0) {
+    *n_out = 0;  // every parent was found in its own window: nothing is unresolved (no scan)
+    return KMZ_OK;
+  }
+  if (ensure(c, c->gd_cnt, 16)) return KMZ_E_HIP;
+  unsigned long long *cnt = P<unsigned long long>(c->gd_cnt);
+  HIPCHK(c, hipMemsetAsync(cnt, 0, 8, c->stream));
+  unsigned long long *out = nullptr;
+  if (ids && cap) {
+    if (mem == KMZ_MEM_DEVICE) {
+      out = reinterpret_cast<unsigned long long *>(ids);
+    } else {
+      if (ensure(c, c->gd_out, cap * 8)) return KMZ_E_HIP;
+      out = P<unsigned long long>(c->gd_out);
+    }
+  }
+  launch_unresolved(c->stream, c->pid, P<uint32_t>(c->dp), (uint32_t)c->n, out, out ? cap : 0, cnt);
+  unsigned long long n = 0;
+  HIPCHK(c, hipMemcpyAsync(&n, cnt, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *n_out = n;
+  if (out && n > cap) return fail(c, KMZ_E_ARG, "output too small");
+  if (out && mem != KMZ_MEM_DEVICE && n) {
+    HIPCHK(c, hipMemcpyAsync(ids, out, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return KMZ_OK;
+}
+
+int kmz_count_ids(kmz_ctx *c, const uint64_t *ids, uint64_t n, int mem, uint64_t *found) {
+  if (!c || !found || (n && !ids)) return KMZ_E_ARG;
+  if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_count_ids before kmz_load");
+  uint64_t cap = 1024;
+  while (cap < 2 * n + 64) cap *= 2;
+  if (ensure(c, c->gd_set, cap * 8) || ensure(c, c->gd_cnt, 16)) return KMZ_E_HIP;
+  const unsigned long long *src = reinterpret_cast<const unsigned long long *>(ids);
+  if (n && mem == KMZ_MEM_HOST) {
+    if (ensure(c, c->gd_in, n * 8)) return KMZ_E_HIP;
+    HIPCHK(c, hipMemcpyAsync(c->gd_in.p, ids, n * 8, hipMemcpyHostToDevice, c->stream));
+    src = P<unsigned long long>(c->gd_in);
+  }
+  unsigned long long *cnt = P<unsigned long long>(c->gd_cnt);
+  HIPCHK(c, hipMemsetAsync(c->gd_set.p, 0, cap * 8, c->stream));
+  HIPCHK(c, hipMemsetAsync(cnt + 1, 0, 8, c->stream));
+  launch_ids_count(c->stream, src, n, P<unsigned long long>(c->gd_set), cap, c->sid, (uint32_t)c->n, cnt + 1);
+  unsigned long long f = 0;
+  HIPCHK(c, hipMemcpyAsync(&f, cnt + 1, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *found = f;
   return KMZ_OK;
 }
 

@@ -115,6 +115,12 @@ void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned l
                  uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
                  uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts);
 
+// multi-GPU sharding guard (kmz_guard.hip)
+void launch_unresolved(hipStream_t s, const uint64_t *pid, const uint32_t *dp, uint32_t n, unsigned long long *out,
+                       uint64_t cap, unsigned long long *count);
+void launch_ids_count(hipStream_t s, const unsigned long long *ids, uint64_t m, unsigned long long *set, uint64_t cap,
+                      const uint64_t *sid, uint32_t n, unsigned long long *found);
+
 // window parent join + uniqueness certificate (kmz_join.hip)
 struct CertPlan {
   uint32_t B2, cap2, chunks;

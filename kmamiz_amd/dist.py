@@ -75,6 +75,8 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
     if G:
         dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM)  # modular: exact for u64
     dev = p.device
+    # sharding guard: this rank's parent ids that are not in its shard
+    nu = _unresolved(engine) if engine is not None else 0
     ming = p[5 * G :]
     mine = e[E:]
     mx = torch.cat([
@@ -82,9 +84,11 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
         _as_signed_order(e[:E]),
         -torch.where(ming == -1, torch.full_like(ming, _I64_MAX), ming),
         -torch.where(mine == -1, torch.full_like(mine, _I64_MAX), mine),
-        torch.tensor([keys.numel()], dtype=torch.int64, device=dev),
+        torch.tensor([nu, keys.numel()], dtype=torch.int64, device=dev),
     ])
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    if int(mx[-2].item()) > 0:
+        _check_shards(engine, nu, int(mx[-2].item()), dev)
     p[4 * G : 5 * G] = _as_signed_order(mx[:G])
     e[:E] = _as_signed_order(mx[G : G + E])
     fg = -mx[G + E : 2 * G + E]
@@ -107,6 +111,43 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
         return None
     u = torch.unique(allk)
     return u[u != 0]
+
+
+class ShardingError(RuntimeError):
+    """A parent link crosses shards: the sharded result would differ from the
+    reference's global span map (Traces.ts:117-123); run unsharded."""
+
+
+def _unresolved(engine) -> int:
+    from ._lib import KmzError
+
+    try:
+        return engine.unresolved_parents()
+    except KmzError as e:
+        if e.code == -9:  # KMZ_E_UNSUPPORTED: the span-table path (repeated span ids in a shard)
+            raise ShardingError("repeated span ids in a shard: sharding is not exact, run unsharded") from e
+        raise
+
+
+def _check_shards(engine, nu: int, mu: int, dev) -> None:
+    """Exchange the unresolved parent ids (padded to the largest list) and
+    count, on every rank, how many of them are span ids of its own shard."""
+    mine = torch.zeros(mu, dtype=torch.int64, device=dev)
+    if nu:
+        engine.unresolved_parents(mine.data_ptr(), mu, mine.is_cuda)
+    if mine.is_cuda:
+        allu = torch.empty(mu * dist.get_world_size(), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allu, mine)
+        torch.cuda.current_stream(dev).synchronize()
+    else:
+        parts = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, mine)
+        allu = torch.cat(parts)
+    found = torch.tensor([engine.count_ids(allu.data_ptr(), allu.numel(), allu.is_cuda)], dtype=torch.int64,
+                         device=dev)
+    dist.all_reduce(found, op=dist.ReduceOp.SUM)
+    if int(found.item()):
+        raise ShardingError(f"{int(found.item())} parent ids of one shard are spans of another: shard by whole traces")
 
 
 def merge_edge_keys(keys: torch.Tensor) -> torch.Tensor:

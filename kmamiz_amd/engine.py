@@ -246,6 +246,22 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_merge_triples(self.ctx, C.c_void_p(src_ptr), n,
                                                       L.MEM_DEVICE if device else L.MEM_HOST))
 
+    # ---- multi-GPU sharding guard (kmz_guard.hip) -------------------------------
+    def unresolved_parents(self, dst_ptr: int = 0, cap: int = 0, device: bool = False) -> int:
+        """Count (and with dst_ptr, copy) the parent ids missing from this
+        batch; raises KmzError(KMZ_E_UNSUPPORTED) on the span-table path."""
+        n = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_unresolved_parents(self.ctx, C.c_void_p(dst_ptr) if dst_ptr else None, cap,
+                                                           C.byref(n), L.MEM_DEVICE if device else L.MEM_HOST))
+        return n.value
+
+    def count_ids(self, src_ptr: int, n: int, device: bool) -> int:
+        """How many of the given ids (0 = padding) are span ids of this batch."""
+        f = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_count_ids(self.ctx, C.c_void_p(src_ptr) if n else None, n,
+                                                  L.MEM_DEVICE if device else L.MEM_HOST, C.byref(f)))
+        return f.value
+
     # ---- profiling -------------------------------------------------------------
     def set_profiling(self, on: bool):
         L.check(self.ctx, self._lib.kmz_set_profiling(self.ctx, 1 if on else 0))

@@ -95,3 +95,63 @@ def test_two_rank_merge_equals_single_engine():
         assert r[2] == exp[1]
         assert r[3] == exp[2]
         assert r[4] == exp_tail
+
+
+def _cross_worker(rank, world, port, q):
+    """Rank 1's batch has a span whose parentId is a span of rank 0's shard."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kmamiz_amd import Engine
+        from kmamiz_amd import _lib as L
+        from kmamiz_amd import dist as kdist
+        from kmamiz_amd import synth
+
+        cut = [0, 300, 700]
+        table = synth.shape_table(synth.MESH)
+        b0, _ = synth.host_batch(synth.MESH, cut[0], cut[1])
+        batch, _ = synth.host_batch(synth.MESH, cut[rank], cut[rank + 1])
+        if rank == 1:
+            roots = np.nonzero(batch.parent_id == 0)[0]
+            batch.parent_id[roots[3]] = b0.span_id[10]  # a parent on the other shard
+        e = Engine(0)
+        e.load(batch, table)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        gw, ew, tw = (e.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
+        g = torch.zeros(gw, dtype=torch.int64)
+        ep = torch.zeros(ew, dtype=torch.int64)
+        t = torch.zeros(max(1, tw), dtype=torch.int64)
+        e.export_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
+        e.export_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
+        e.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, False)
+        nu = e.unresolved_parents()
+        try:
+            kdist.merge_all(g, gw // 6, ep, ew // 2, t[:tw], engine=e)
+            q.put((rank, nu, "merged"))
+        except kdist.ShardingError:
+            q.put((rank, nu, "refused"))
+        e.close()
+    except Exception as ex:  # surfaced by the parent
+        q.put((rank, -1, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_cross_shard_parent_is_refused():
+    """a parent link across shards would be joined by the
+    reference's global span map; merge_all's guard finds it on both ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_cross_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0] == (0, 0, "refused"), res
+    assert res[1] == (1, 1, "refused"), res
