@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
       flags |= F_RANGE;
       continue;
     }
-    hasin[s] = 1;
+    if (!hasin[s]) hasin[s] = 1;  // (read first: ~10^7 keys share ~10^4 bytes)
     // desc's row: (anc, d) in dependingBy
     uint32_t side = 0;
     uint64_t lk[2];
