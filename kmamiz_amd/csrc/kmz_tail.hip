@@ -83,6 +83,32 @@ __device__ __forceinline__ uint64_t tail_agg_slot(unsigned long long *__restrict
   return cap;
 }
 
+// add (count, dependingBy, dependingOn) to the detail dk in the global table;
+// the first link of a type there also counts into the service's ACS
+// (distance 1, RiskAnalyzer.ts:150-166) and instability (any distance,
+// EndpointDependencies.ts:618-628) counters
+__device__ __forceinline__ void detail_add(uint64_t dk, uint32_t cnt, uint32_t by, uint32_t on,
+                                           unsigned long long *__restrict__ akey, uint32_t *__restrict__ aval,
+                                           uint64_t acap, unsigned long long *__restrict__ fkey,
+                                           uint32_t *__restrict__ fval, uint64_t fcap, uint32_t *__restrict__ sstat,
+                                           uint32_t *flags) {
+  const uint64_t p = tail_agg_slot(akey, acap, dk, flags);
+  if (p == acap) return;
+  const uint32_t sv = (uint32_t)(dk >> 40), d = (uint32_t)dk & 0xFFFFu;
+  atomicAdd(&aval[4 * p + 0], cnt);
+  for (uint32_t ty = 0; ty < 2; ++ty) {
+    const uint32_t v = ty ? on : by;
+    if (!v || atomicAdd(&aval[4 * p + 1 + ty], v)) continue;
+    if (d == 1) atomicAdd(&sstat[8 * sv + TS_AIS + ty], 1u);
+    const uint64_t q = tail_agg_slot(fkey, fcap, (dk >> 16) + 1, flags);  // (svc, lsvc)
+    if (q == fcap) continue;
+    const uint32_t was = atomicOr(&fval[q], 1u << ty);
+    if (!(was & (1u << ty))) atomicAdd(&sstat[8 * sv + TS_NBY + ty], 1u);
+  }
+}
+
+constexpr uint32_t TAIL_LAGG = 2048;  // per-workgroup LDS detail slots (40 KB)
+
 // link key: svc << 40 | cls << 16 | type << 15 | d   (type 1 = SERVER / dependingOn)
 // detail key: svc << 40 | lsvc << 16 | d
 // pair key: (desc + 1) << 32 | consumer usn;  pair detail key: (svc + 1) << 32 | consumer usn
@@ -102,6 +128,15 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
                                                     uint32_t n_dist, unsigned int *__restrict__ counters) {
   const uint64_t n = *n_keys;
   uint32_t flags = 0, won_l = 0, won_p = 0;  // first occurrences in the link / pair sets (sizes the next run's sets)
+  // winners' details are summed in LDS first (hot (service, linked service,
+  // distance) entries see one global update per workgroup, not one per link)
+  __shared__ unsigned long long lkey[TAIL_LAGG];
+  __shared__ uint32_t lval[TAIL_LAGG][3];
+  for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += blockDim.x) {
+    lkey[x] = 0;
+    lval[x][0] = lval[x][1] = lval[x][2] = 0;
+  }
+  __syncthreads();
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = keys[i];
     const uint32_t a = (uint32_t)(k >> 40), s = (uint32_t)(k >> 16) & 0xFFFFFFu, d = (uint32_t)(k >> 1) & 0x7FFFu;
@@ -121,21 +156,20 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
       ++won_l;
       const uint32_t c = (uint32_t)(lk[t] >> 16) & 0xFFFFFFu;
       const uint64_t dk = (lk[t] & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
-      const uint64_t p = tail_agg_slot(akey, acap, dk, &flags);
-      if (p == acap) continue;
-      const uint32_t ty = (uint32_t)(lk[t] >> 15) & 1u, sv = (uint32_t)(lk[t] >> 40);
-      atomicAdd(&aval[4 * p + 0], 1u);                              // count
-      const uint32_t old = atomicAdd(&aval[4 * p + 1 + ty], 1u);    // dependingBy (CLIENT) / dependingOn (SERVER)
-      if (old) continue;
-      // first type-`ty` link of this (service, linked service, distance):
-      // ACS counts distance-1 details with dependingBy / dependingOn > 0
-      // (RiskAnalyzer.ts:150-166), instability linked services with any
-      // (EndpointDependencies.ts:618-628)
-      if (d == 1) atomicAdd(&sstat[8 * sv + TS_AIS + ty], 1u);
-      const uint64_t q = tail_agg_slot(fkey, fcap, (dk >> 16) + 1, &flags);  // (svc, lsvc)
-      if (q == fcap) continue;
-      const uint32_t was = atomicOr(&fval[q], 1u << ty);
-      if (!(was & (1u << ty))) atomicAdd(&sstat[8 * sv + TS_NBY + ty], 1u);
+      const uint32_t ty = (uint32_t)(lk[t] >> 15) & 1u;  // dependingBy (CLIENT) / dependingOn (SERVER)
+      uint32_t h = (uint32_t)(mix64(dk) & (TAIL_LAGG - 1));
+      bool done = false;
+      for (uint32_t z = 0; z < 16; ++z) {
+        const unsigned long long cur = atomicCAS(&lkey[h], 0ull, (unsigned long long)dk);
+        if (cur == 0 || cur == dk) {
+          atomicAdd(&lval[h][0], 1u);
+          atomicAdd(&lval[h][1 + ty], 1u);
+          done = true;
+          break;
+        }
+        h = (h + 1) & (TAIL_LAGG - 1);
+      }
+      if (!done) detail_add(dk, 1u, ty == 0, ty == 1, akey, aval, acap, fkey, fval, fcap, sstat, &flags);
     }
     // cohesion: (consumer service, consumed endpoint) at distance 1
     if (d == 1 && tail_set_put(pset, pcap, ((uint64_t)(s + 1) << 32) | usn[a], &flags)) {
@@ -147,6 +181,10 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
       }
     }
   }
+  __syncthreads();  // this workgroup's details -> the global table
+  for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += blockDim.x)
+    if (lkey[x]) detail_add(lkey[x], lval[x][0], lval[x][1], lval[x][2], akey, aval, acap, fkey, fval, fcap, sstat,
+                            &flags);
   if (flags) atomicOr(&counters[C_FLAGS], flags);
   for (int o = 32; o > 0; o >>= 1) {
     won_l += __shfl_xor(won_l, o, 64);
@@ -212,7 +250,7 @@ void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned l
                  uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned long long *fkey, uint32_t *fval,
                  uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
                  uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts) {
-  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + 255) / 256, 8192));
+  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + 255) / 256, 1024));
   hipLaunchKernelGGL(k_tail_links, dim3(g), dim3(256), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls,
                      lset, lcap, akey, aval, acap, pset, pcap, pkey, pval, pacap, hasin, fkey, fval, fcap, sstat, rel,
                      n_dist, counters);
