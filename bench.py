@@ -7,9 +7,11 @@ download of the results (groups, endpoint records, edge keys) to the host.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config mesh|bookinfo|power]
 
-Weak scaling: every rank owns a fixed shard of whole traces (config 3's
-100M-span 500-service mesh per GPU by default; N=8 is config 4's ~1B-span
-mesh).  Rank 0 prints one JSON line.
+Workloads: one GPU runs config 3 (the 500-service mesh, 1e8 spans); N > 1
+GPUs run config 4: 1e9 spans of the same mesh, sharded by h(traceId) mod N
+(kmz_synth_load_shard), so the total work is fixed as N grows
+(strong scaling, over N = 2/4/8).  --spans / --scaling override.  Rank 0
+prints one JSON line.
 """
 from __future__ import annotations
 
@@ -61,7 +63,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=["mesh", "bookinfo", "power"], default="mesh")
-    ap.add_argument("--spans", type=float, default=None, help="spans per GPU (default: 1e8 mesh, 1e6 bookinfo)")
+    ap.add_argument("--spans", type=float, default=None,
+                    help="spans of the whole job (default: mesh 1e8 on one GPU = config 3, 1e9 on N > 1 GPUs = "
+                         "config 4; bookinfo 1e6; power 1e8)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: --spans is the job's total, sharded by h(traceId) mod N; weak: --spans per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-fetch", action="store_true", help="leave results on the device")
     ap.add_argument("--tail", choices=["auto", "on", "off"], default="auto",
@@ -118,15 +124,21 @@ def main():
     from kmamiz_amd import synth
 
     config = {"mesh": synth.MESH, "bookinfo": synth.BOOKINFO, "power": synth.POWER}[args.config]
-    target = int(args.spans or (1e6 if args.config == "bookinfo" else 1e8))
+    if args.spans:
+        target = int(args.spans) * (world if args.scaling == "weak" else 1)
+    else:  # config 3 on one GPU, config 4 (1e9 spans over the node) on several
+        target = int(1e6 if args.config == "bookinfo" else (1e9 if world > 1 and args.config == "mesh" else 1e8))
     sample_tr = 20000
     per_trace = synth.count_spans(config, 0, sample_tr) / sample_tr
-    traces_per_gpu = max(1, int(round(target / per_trace)))
-    t_begin, t_end = rank * traces_per_gpu, (rank + 1) * traces_per_gpu
+    n_traces = max(1, int(round(target / per_trace)))
 
     stream = torch.cuda.current_stream()
     eng = Engine(local, stream=stream.cuda_stream)
-    n_local = eng.load_synthetic(config, synth.SEED, t_begin, t_end)
+    if world > 1:  # this rank's traces: shard(traceId) == rank, global flatten indices
+        n_local = eng.load_synthetic_shard(config, synth.SEED, 0, n_traces, world, rank)
+    else:
+        n_local = eng.load_synthetic(config, synth.SEED, 0, n_traces)
+    digest = synth.table_digest(config)  # every rank indexes partials by the same synthetic id tables
     flags = L.RUN_STATS_TAG | L.RUN_DEPS
     dev = torch.device("cuda", local)
     state = {}
@@ -173,7 +185,7 @@ def main():
             eng.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, True)
             # three collectives: SUM moments, MAX of max / negated min fields
             # + key count, all-gather of the keys (union in the engine's set)
-            kdist.merge_all(g, gw // 6, e, ew // 2, t[:tw], engine=eng)
+            kdist.merge_all(g, gw // 6, e, ew // 2, t[:tw], engine=eng, digest=digest)
             eng.import_partials(L.PART_GROUPS, g.data_ptr(), gw, True)
             eng.import_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
             eng.finalize()
@@ -250,7 +262,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(secs / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int64+f64",
             "data": "synthetic (device-generated, seed 0x4B4D414D495A)",
@@ -259,14 +271,15 @@ def main():
                              synth.BOOKINFO: "config2: Bookinfo-shaped mesh, ",
                              synth.POWER: "config5: power-law fan-out mesh, 50k endpoints, depth-16 chains, "
                                           "hot endpoints, "}[config]
-                + f"{n_local} spans/GPU ({traces_per_gpu} traces/GPU)"
-                + (", sharded by whole traces (config 4 at N=8)" if config == synth.MESH else "")
+                + f"{n_total} spans ({n_traces} traces)"
+                + (f", sharded by h(traceId) mod {world} ({n_local} spans on rank 0)" if world > 1 else "")
+                + (" = config 4" if config == synth.MESH and world > 1 and n_total >= 9e8 else "")
                 + (", + service tail (instability/coupling/cohesion/risk) per step" if tail_on else ""),
                 "spans_per_gpu": n_local,
                 "spans_total": n_total,
                 "relations_per_gpu": A,
                 "edge_keys": info["n_triples"],
-                "parallelism": f"traceId-shard x{world}",
+                "parallelism": f"traceId-shard x{world}" if world > 1 else "single GPU",
                 "service_tail": tail_on,
             },
             "roofline": {

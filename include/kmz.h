@@ -241,6 +241,21 @@ int kmz_unresolved_parents(kmz_ctx *ctx, uint64_t *ids, uint64_t cap, uint64_t *
 /* how many of the given ids (0 = padding) are span ids of the loaded batch */
 int kmz_count_ids(kmz_ctx *ctx, const uint64_t *ids, uint64_t n, int mem, uint64_t *found);
 
+/* ---- traceId sharding (shard = h(traceId) mod G) ------------ */
+/* The shard of a trace, from its traceId string (the reference dedups and
+ * groups traces by t[0].traceId, RealtimeWorkerImpl.ts:17-27): canonical
+ * 16/32-digit lowercase hex ids hash by value, any other string by its bytes. */
+uint32_t kmz_trace_shard(const char *trace_id, uint64_t len, uint32_t world);
+/* A shard that is not one contiguous range of the global flatten order
+ * (Traces.ts:29): after kmz_load, give the runs of the local batch, local
+ * index local_start[k] being global index global_start[k] (local_start
+ * non-decreasing, local_start[0] = 0; an index maps through the last run
+ * whose start is <= it, so empty runs may repeat a start).  Every index a
+ * result reports (kmz_group.first, kmz_endpoint.first_row, the partials,
+ * span links) is then global; index_base is ignored.  n_runs = 0: contiguous
+ * again.  kmz_load resets it. */
+int kmz_set_index_map(kmz_ctx *ctx, const uint64_t *local_start, const uint64_t *global_start, uint64_t n_runs);
+
 /* ---- service-level tail over the reduced edge set ---- */
 /* Replaces the per-row scans of EndpointDependencies.toServiceDependencies
  * (EndpointDependencies.ts:369-470), whose link counts feed toServiceInstability
@@ -331,6 +346,11 @@ int kmz_synth_describe(int config, kmz_synth_desc *out);
  * before trace_begin (computed by the call). Returns the span count. */
 int kmz_synth_load(kmz_ctx *ctx, int config, uint64_t seed, uint64_t trace_begin, uint64_t trace_end,
                    uint64_t *n_spans_out);
+/* The traces of [trace_begin, trace_end) whose synthetic traceId (the 128-bit
+ * t * 0x9E3779B97F4A7C15) has kmz_trace_shard == rank, with their global
+ * flatten indices (the index map is set by the call). */
+int kmz_synth_load_shard(kmz_ctx *ctx, int config, uint64_t seed, uint64_t trace_begin, uint64_t trace_end,
+                         uint32_t world, uint32_t rank, uint64_t *n_spans_out);
 /* Host-side generation of the same traces into caller arrays (cap spans);
  * trace_off receives trace_end-trace_begin+1 offsets. */
 int kmz_synth_host(int config, uint64_t seed, uint64_t trace_begin, uint64_t trace_end, uint64_t cap,

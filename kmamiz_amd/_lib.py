@@ -162,6 +162,8 @@ SIGNATURES = [
     ("kmz_zipkin_free", None, [C.POINTER(ZipkinBatch)]),
     ("kmz_unresolved_parents", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64), C.c_int]),
     ("kmz_count_ids", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.POINTER(C.c_uint64)]),
+    ("kmz_trace_shard", C.c_uint32, [C.c_char_p, C.c_uint64, C.c_uint32]),
+    ("kmz_set_index_map", C.c_int, [_P, _P, _P, C.c_uint64]),
     ("kmz_tail_map_set", C.c_int, [_P, C.POINTER(TailMap)]),
     ("kmz_tail_run", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("kmz_tail_get", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, _P, C.c_uint64]),
@@ -174,6 +176,8 @@ SIGNATURES = [
     ("kmz_kernel_times", C.c_int, [_P, _P, _P, C.c_int]),
     ("kmz_synth_describe", C.c_int, [C.c_int, C.POINTER(SynthDesc)]),
     ("kmz_synth_load", C.c_int, [_P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("kmz_synth_load_shard", C.c_int,
+     [_P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
     (
         "kmz_synth_host",
         C.c_int,

@@ -59,6 +59,8 @@ struct kmz_ctx {
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
+  DevBuf imap_l, imap_g;  // local -> global flatten-index runs of a non-contiguous shard (kmz_shard.hip)
+  uint64_t imap_n = 0;     // 0: contiguous batch (index_base + i)
   DevBuf ctile;           // K4 per-workgroup stats (apart from K3's tile_tmp: the two run concurrently)
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
   // service tail (kmz_tail.hip): maps, link set, detail table, pair set, pair table, outputs
@@ -284,7 +286,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
                     &c->tl_sstat, &c->tl_rel};
@@ -340,6 +342,7 @@ int kmz_load(kmz_ctx *c, const kmz_spans *s, const kmz_shapes *sh, int where) {
   if (r) return r;
   c->n = s->n;
   c->index_base = s->index_base;
+  c->imap_n = 0;
   c->ran = 0;
   c->table_hint = false;
   c->hpin_valid = false;
@@ -647,6 +650,68 @@ static int run_stats(kmz_ctx *c, uint32_t mode) {
   return KMZ_OK;
 }
 
+// A non-contiguous shard (kmz_set_index_map): the run used local flatten
+// indices; map the order keys it reports to global ones (kmz_shard.hip).
+static int remap_results(kmz_ctx *c, uint32_t flags, bool links) {
+  const uint64_t *ls = P<uint64_t>(c->imap_l), *gs = P<uint64_t>(c->imap_g);
+  if (flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG)) {
+    launch_remap_index(c->stream, P<unsigned long long>(c->grp) + 5ull * c->G, c->G, 1, 0, ls, gs, c->imap_n);
+    launch_remap_index(c->stream, P<unsigned long long>(c->grp_final) + 1, c->G, sizeof(kmz_group) / 8, 0, ls, gs,
+                       c->imap_n);
+  }
+  if (flags & KMZ_RUN_DEPS) {
+    launch_remap_index(c->stream, P<unsigned long long>(c->epp) + c->n_dep, c->n_dep, 1, 1, ls, gs, c->imap_n);
+    if (links) launch_remap_index(c->stream, P<unsigned long long>(c->rowpos), c->n, 1, 0, ls, gs, c->imap_n);
+  }
+  HIPCHK(c, hipGetLastError());
+  return KMZ_OK;
+}
+
+int kmz_set_index_map(kmz_ctx *c, const uint64_t *local_start, const uint64_t *global_start, uint64_t n_runs) {
+  if (!c || (n_runs && (!local_start || !global_start))) return KMZ_E_ARG;
+  if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_set_index_map before kmz_load");
+  if (n_runs == 0) {
+    c->imap_n = 0;
+    return KMZ_OK;
+  }
+  if (local_start[0] != 0) return fail(c, KMZ_E_ARG, "the first run must start at local index 0");
+  for (uint64_t k = 1; k < n_runs; ++k)
+    if (local_start[k] < local_start[k - 1] || (local_start[k] > local_start[k - 1] &&
+                                                global_start[k] < global_start[k - 1] + (local_start[k] - local_start[k - 1])))
+      return fail(c, KMZ_E_ARG, "index map runs must be ordered and non-overlapping");
+  if (ensure(c, c->imap_l, n_runs * 8) || ensure(c, c->imap_g, n_runs * 8)) return KMZ_E_HIP;
+  HIPCHK(c, hipMemcpyAsync(c->imap_l.p, local_start, n_runs * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->imap_g.p, global_start, n_runs * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->imap_n = n_runs;
+  c->index_base = 0;  // the run works on local indices; results are mapped
+  c->ran = 0;
+  c->hpin_valid = false;
+  return KMZ_OK;
+}
+
+uint32_t kmz_trace_shard(const char *trace_id, uint64_t len, uint32_t world) {
+  if (world <= 1) return 0;
+  uint64_t hi = 0, lo = 0;
+  bool hex = trace_id && (len == 16 || len == 32);
+  for (uint64_t i = 0; hex && i < len; ++i) {
+    const char ch = trace_id[i];
+    const uint64_t v = ch >= '0' && ch <= '9' ? (uint64_t)(ch - '0') : (ch >= 'a' && ch <= 'f' ? (uint64_t)(ch - 'a' + 10) : 16);
+    if (v == 16) {
+      hex = false;
+      break;
+    }
+    hi = (hi << 4) | (lo >> 60);
+    lo = (lo << 4) | v;
+  }
+  if (!hex) {  // any other traceId string: FNV-1a of its bytes
+    hi = ~0ull;
+    lo = 0xcbf29ce484222325ull;
+    for (uint64_t i = 0; trace_id && i < len; ++i) lo = (lo ^ (uint8_t)trace_id[i]) * 0x100000001b3ull;
+  }
+  return shard_of(hi, lo, world);
+}
+
 int kmz_run(kmz_ctx *c, uint32_t flags) {
   if (!c) return KMZ_E_ARG;
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_run before kmz_load");
@@ -746,6 +811,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     if (!retry) {
       int e = check_flags(c, h[C_FLAGS]);
       if (e) return e;
+      if (c->imap_n && (e = remap_results(c, flags, links))) return e;
       c->ran = flags;
       c->links = links;
       c->hpin_valid = true;
@@ -1286,6 +1352,24 @@ int kmz_synth_shape_ids(int config, uint32_t *rt, uint32_t *tag, uint32_t *dep, 
   return KMZ_OK;
 }
 
+// spans of the synthetic traces [0, t0): the global flatten index of trace t0's first span
+static int synth_base(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t *base) {
+  *base = 0;
+  if (!t0) return KMZ_OK;
+  size_t tmp_bytes = 0;
+  if (t0 >= (1ull << 31)) return fail(c, KMZ_E_ARG, "trace range too large");
+  if (ensure(c, c->synth_cnt, t0 * 8) || ensure(c, c->synth_off, 16)) return KMZ_E_HIP;
+  launch_synth_count(c->stream, config, seed, 0, t0, P<uint64_t>(c->synth_cnt));
+  HIPCHK(c, hipcub::DeviceReduce::Sum(nullptr, tmp_bytes, P<uint64_t>(c->synth_cnt), P<uint64_t>(c->synth_off),
+                                       (int)t0, c->stream));
+  if (ensure(c, c->scratch, tmp_bytes)) return KMZ_E_HIP;
+  HIPCHK(c, hipcub::DeviceReduce::Sum(c->scratch.p, tmp_bytes, P<uint64_t>(c->synth_cnt), P<uint64_t>(c->synth_off),
+                                       (int)t0, c->stream));
+  HIPCHK(c, hipMemcpyAsync(base, c->synth_off.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
 int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t t1, uint64_t *n_out) {
   if (!c || t1 < t0) return KMZ_E_ARG;
   kmz_synth_desc d;
@@ -1295,20 +1379,10 @@ int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t 
   if (ensure(c, c->dur_table, dt.size() * 4)) return KMZ_E_HIP;
   HIPCHK(c, hipMemcpyAsync(c->dur_table.p, dt.data(), dt.size() * 4, hipMemcpyHostToDevice, c->stream));
   uint64_t nt = t1 - t0;
-  // spans before t0 (global flatten index of the first generated span)
   uint64_t base = 0;
+  int rb = synth_base(c, config, seed, t0, &base);
+  if (rb) return rb;
   size_t tmp_bytes = 0;
-  if (t0) {
-    if (ensure(c, c->synth_cnt, t0 * 8) || ensure(c, c->synth_off, 16)) return KMZ_E_HIP;
-    launch_synth_count(c->stream, config, seed, 0, t0, P<uint64_t>(c->synth_cnt));
-    HIPCHK(c, hipcub::DeviceReduce::Sum(nullptr, tmp_bytes, P<uint64_t>(c->synth_cnt), P<uint64_t>(c->synth_off),
-                                         (int)t0, c->stream));
-    if (ensure(c, c->scratch, tmp_bytes)) return KMZ_E_HIP;
-    HIPCHK(c, hipcub::DeviceReduce::Sum(c->scratch.p, tmp_bytes, P<uint64_t>(c->synth_cnt), P<uint64_t>(c->synth_off),
-                                         (int)t0, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&base, c->synth_off.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
   if (ensure(c, c->synth_cnt, (nt + 1) * 8) || ensure(c, c->synth_off, (nt + 1) * 8)) return KMZ_E_HIP;
   launch_synth_count(c->stream, config, seed, t0, nt, P<uint64_t>(c->synth_cnt));
   tmp_bytes = 0;
@@ -1342,6 +1416,79 @@ int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t 
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->n = n;
   c->index_base = base;
+  c->imap_n = 0;
+  c->sid = o.span_id;
+  c->pid = o.parent_id;
+  c->kind = o.kind;
+  c->shape = o.shape;
+  c->status = o.status;
+  c->dur = o.duration;
+  c->ts = o.timestamp;
+  c->loaded = true;
+  c->ran = 0;
+  c->table_hint = false;
+  c->hpin_valid = false;
+  if (n_out) *n_out = n;
+  return KMZ_OK;
+}
+
+int kmz_synth_load_shard(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t t1, uint32_t world,
+                         uint32_t rank, uint64_t *n_out) {
+  if (!c || t1 < t0 || world == 0 || rank >= world) return KMZ_E_ARG;
+  kmz_synth_desc d;
+  if (kmz_synth_describe(config, &d)) return fail(c, KMZ_E_ARG, "unknown synthetic config");
+  hipSetDevice(c->device);
+  const uint64_t nt = t1 - t0;
+  if (nt >= (1ull << 31)) return fail(c, KMZ_E_ARG, "trace range too large");
+  const auto &dt = dur_table_host();
+  if (ensure(c, c->dur_table, dt.size() * 4)) return KMZ_E_HIP;
+  HIPCHK(c, hipMemcpyAsync(c->dur_table.p, dt.data(), dt.size() * 4, hipMemcpyHostToDevice, c->stream));
+  uint64_t base = 0;
+  int rb = synth_base(c, config, seed, t0, &base);
+  if (rb) return rb;
+  // per trace: spans (cnt), spans if it is this rank's (sel); their exclusive
+  // sums are the global (imap_g) and local (imap_l) starts of every trace
+  if (ensure(c, c->synth_cnt, (nt + 1) * 8) || ensure(c, c->synth_off, (nt + 1) * 8) ||
+      ensure(c, c->imap_l, (nt + 1) * 8) || ensure(c, c->imap_g, (nt + 1) * 8))
+    return KMZ_E_HIP;
+  uint64_t *cnt = P<uint64_t>(c->synth_cnt), *sel = P<uint64_t>(c->synth_off);
+  uint64_t *loff = P<uint64_t>(c->imap_l), *goff = P<uint64_t>(c->imap_g);
+  launch_synth_count(c->stream, config, seed, t0, nt, cnt);
+  launch_shard_select(c->stream, t0, nt, world, rank, cnt, sel);
+  size_t tmp_bytes = 0;
+  HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, goff, (int)nt, c->stream));
+  if (ensure(c, c->scratch, tmp_bytes)) return KMZ_E_HIP;
+  if (nt) {
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scratch.p, tmp_bytes, cnt, goff, (int)nt, c->stream));
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scratch.p, tmp_bytes, sel, loff, (int)nt, c->stream));
+  }
+  uint64_t last_off = 0, last_cnt = 0;
+  if (nt) {
+    HIPCHK(c, hipMemcpyAsync(&last_off, loff + nt - 1, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&last_cnt, sel + nt - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t n = last_off + last_cnt;
+  if (n >= 0xFFFFFFFFull) return fail(c, KMZ_E_ARG, "synthetic shard too large for one context");
+  if (ensure(c, c->in_sid, n * 8) || ensure(c, c->in_pid, n * 8) || ensure(c, c->in_kind, n) ||
+      ensure(c, c->in_shape, n * 4) || ensure(c, c->in_status, n * 2) || ensure(c, c->in_dur, n * 4) ||
+      ensure(c, c->in_ts, n * 8))
+    return KMZ_E_HIP;
+  SynthOut o{P<uint64_t>(c->in_sid), P<uint64_t>(c->in_pid), P<uint8_t>(c->in_kind), P<uint32_t>(c->in_shape),
+             P<uint16_t>(c->in_status), P<uint32_t>(c->in_dur), P<int64_t>(c->in_ts)};
+  launch_synth_fill_shard(c->stream, config, seed, t0, nt, world, rank, goff, loff, base, P<uint32_t>(c->dur_table), o);
+  launch_add_base(c->stream, goff, nt, base);
+  HIPCHK(c, hipGetLastError());
+  std::vector<uint32_t> ids(d.n_shapes);
+  kmz_synth_shape_ids(config, ids.data(), nullptr, nullptr, d.n_shapes);
+  kmz_shapes sh{d.n_shapes, ids.data(), ids.data(), ids.data(), d.n_endpoints, d.n_endpoints, d.n_endpoints,
+                d.n_status};
+  int r = load_shapes(c, &sh);
+  if (r) return r;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->n = n;
+  c->index_base = 0;
+  c->imap_n = nt;  // one run per trace (foreign traces repeat a local start: skipped by the map)
   c->sid = o.span_id;
   c->pid = o.parent_id;
   c->kind = o.kind;

@@ -44,6 +44,15 @@ KMZ_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
 #endif
 }
 
+// traceId -> shard (shard = h(traceId) mod G).  (hi, lo) is the
+// 128-bit value of a canonical lowercase-hex traceId (hi = 0 for 16-digit
+// ids; other strings are hashed by kmz_trace_shard).  A multiply-shift range
+// reduction instead of a modulo: uniform for any world size.
+KMZ_HD uint64_t shard_hash(uint64_t hi, uint64_t lo) { return mix64(hi ^ mix64(lo ^ 0x4B4D5A5348415244ull)); }
+KMZ_HD uint32_t shard_of(uint64_t hi, uint64_t lo, uint32_t world) {
+  return (uint32_t)mulhi64(shard_hash(hi, lo), world);
+}
+
 // position of key k in a table of `cap` slots (any cap, no pow2 rounding)
 KMZ_HD uint64_t slot_of(uint64_t k, uint64_t cap) { return mulhi64(mix64(k ^ 0x5bd1e9955bd1e995ull), cap); }
 KMZ_HD uint32_t tag_of(uint64_t k) { return (uint32_t)(mix64(k + 0x9e3779b97f4a7c15ull) >> 32); }

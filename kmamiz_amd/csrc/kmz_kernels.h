@@ -121,6 +121,16 @@ void launch_unresolved(hipStream_t s, const uint64_t *pid, const uint32_t *dp, u
 void launch_ids_count(hipStream_t s, const unsigned long long *ids, uint64_t m, unsigned long long *set, uint64_t cap,
                       const uint64_t *sid, uint32_t n, unsigned long long *found);
 
+// traceId sharding + local -> global index map (kmz_shard.hip)
+void launch_shard_select(hipStream_t s, uint64_t t0, uint64_t nt, uint32_t world, uint32_t rank, const uint64_t *cnt,
+                         uint64_t *sel);
+void launch_synth_fill_shard(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, uint32_t world,
+                             uint32_t rank, const uint64_t *goff, const uint64_t *loff, uint64_t gbase,
+                             const uint32_t *dur_table, SynthOut out);
+void launch_add_base(hipStream_t s, uint64_t *v, uint64_t n, uint64_t base);
+void launch_remap_index(hipStream_t s, unsigned long long *v, uint64_t n, uint32_t stride, uint32_t shift,
+                        const uint64_t *lstart, const uint64_t *gstart, uint64_t nruns);
+
 // window parent join + uniqueness certificate (kmz_join.hip)
 struct CertPlan {
   uint32_t B2, cap2, chunks;

@@ -62,55 +62,69 @@ def merge_endpoint_partials(e: torch.Tensor, n_ep: int) -> torch.Tensor:
     return e
 
 
-def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: torch.Tensor, engine=None):
+def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: torch.Tensor, engine=None,
+              digest: int = 0, group=None):
     """The whole per-step merge in three collectives (the bench's N > 1 path):
     one SUM all-reduce of the group moments, one MAX all-reduce that carries
     every max field and every min field negated (min x = -max -x in signed
-    order) plus the edge-key count, and one all-gather of the padded keys.
-    Same results as merge_group_partials + merge_endpoint_partials +
-    merge_edge_keys(_into); returns the merged keys when ``engine`` is None."""
-    if dist.get_world_size() == 1:
+    order) plus the edge-key count and the id-table digest, and one
+    all-gather of the padded keys.  Same results as merge_group_partials +
+    merge_endpoint_partials + merge_edge_keys(_into); returns the merged keys
+    when ``engine`` is None.
+
+    The same collective calls run on device tensors (RCCL) and on CPU tensors
+    (gloo), so the CPU tests exercise the production sequence.  ``digest``:
+    a digest of the endpoint/status id tables this rank's partials are indexed
+    by (shard.exchange_tables); ranks that disagree raise ShardingError."""
+    world = dist.get_world_size(group)
+    if world == 1:
         return None if engine is not None else torch.unique(keys)
     G, E = n_groups, n_ep
     if G:
-        dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM)  # modular: exact for u64
+        dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM, group=group)  # modular: exact for u64
     dev = p.device
     # sharding guard: this rank's parent ids that are not in its shard
     nu = _unresolved(engine) if engine is not None else 0
-    ming = p[5 * G :]
-    mine = e[E:]
+    ming = p[5 * G : 6 * G]
+    mine = e[E : 2 * E]
+    dg = int(digest) & ((1 << 62) - 1)
     mx = torch.cat([
         _as_signed_order(p[4 * G : 5 * G]),
         _as_signed_order(e[:E]),
         -torch.where(ming == -1, torch.full_like(ming, _I64_MAX), ming),
         -torch.where(mine == -1, torch.full_like(mine, _I64_MAX), mine),
-        torch.tensor([nu, keys.numel()], dtype=torch.int64, device=dev),
+        torch.tensor([nu, keys.numel(), dg, -dg, G, -G, E, -E], dtype=torch.int64, device=dev),
     ])
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    if int(mx[-2].item()) > 0:
-        _check_shards(engine, nu, int(mx[-2].item()), dev)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+    tail = mx[-8:].tolist()
+    if tail[2] != -tail[3] or tail[4] != -tail[5] or tail[6] != -tail[7]:
+        raise ShardingError("ranks merged partials over different endpoint/status id tables "
+                            "(assign global ids with shard.exchange_tables)")
+    if tail[0] > 0:
+        _check_shards(engine, nu, int(tail[0]), dev, group)
     p[4 * G : 5 * G] = _as_signed_order(mx[:G])
     e[:E] = _as_signed_order(mx[G : G + E])
     fg = -mx[G + E : 2 * G + E]
     fe = -mx[2 * G + E : 2 * G + 2 * E]
-    p[5 * G :] = torch.where(fg == _I64_MAX, torch.full_like(fg, -1), fg)
-    e[E:] = torch.where(fe == _I64_MAX, torch.full_like(fe, -1), fe)
-    m = int(mx[-1].item())
-    pad = torch.zeros(m, dtype=torch.int64, device=keys.device)
-    pad[: keys.numel()] = keys
-    if keys.is_cuda:
-        allk = torch.empty(m * dist.get_world_size(), dtype=torch.int64, device=keys.device)
-        dist.all_gather_into_tensor(allk, pad)
-        torch.cuda.current_stream(keys.device).synchronize()  # the engine's stream may not be torch's
-    else:
-        parts = [torch.empty_like(pad) for _ in range(dist.get_world_size())]
-        dist.all_gather(parts, pad)
-        allk = torch.cat(parts)
+    p[5 * G : 6 * G] = torch.where(fg == _I64_MAX, torch.full_like(fg, -1), fg)
+    e[E : 2 * E] = torch.where(fe == _I64_MAX, torch.full_like(fe, -1), fe)
+    allk = _gather_padded(keys, int(tail[1]), world, group)
     if engine is not None:
         engine.merge_triples(allk.data_ptr(), allk.numel(), keys.is_cuda)
         return None
     u = torch.unique(allk)
     return u[u != 0]
+
+
+def _gather_padded(x: torch.Tensor, m: int, world: int, group=None) -> torch.Tensor:
+    """All-gather of every rank's int64 list, each padded with 0 to m."""
+    pad = torch.zeros(max(1, m), dtype=torch.int64, device=x.device)
+    pad[: x.numel()] = x
+    out = torch.empty(pad.numel() * world, dtype=torch.int64, device=x.device)
+    dist.all_gather_into_tensor(out, pad, group=group)
+    if x.is_cuda:
+        torch.cuda.current_stream(x.device).synchronize()  # the engine's stream may not be torch's
+    return out
 
 
 class ShardingError(RuntimeError):
@@ -129,59 +143,38 @@ def _unresolved(engine) -> int:
         raise
 
 
-def _check_shards(engine, nu: int, mu: int, dev) -> None:
+def _check_shards(engine, nu: int, mu: int, dev, group=None) -> None:
     """Exchange the unresolved parent ids (padded to the largest list) and
     count, on every rank, how many of them are span ids of its own shard."""
     mine = torch.zeros(mu, dtype=torch.int64, device=dev)
     if nu:
         engine.unresolved_parents(mine.data_ptr(), mu, mine.is_cuda)
-    if mine.is_cuda:
-        allu = torch.empty(mu * dist.get_world_size(), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(allu, mine)
-        torch.cuda.current_stream(dev).synchronize()
-    else:
-        parts = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
-        dist.all_gather(parts, mine)
-        allu = torch.cat(parts)
+    allu = _gather_padded(mine, mu, dist.get_world_size(group), group)
     found = torch.tensor([engine.count_ids(allu.data_ptr(), allu.numel(), allu.is_cuda)], dtype=torch.int64,
                          device=dev)
-    dist.all_reduce(found, op=dist.ReduceOp.SUM)
+    dist.all_reduce(found, op=dist.ReduceOp.SUM, group=group)
     if int(found.item()):
         raise ShardingError(f"{int(found.item())} parent ids of one shard are spans of another: shard by whole traces")
 
 
-def merge_edge_keys(keys: torch.Tensor) -> torch.Tensor:
+def merge_edge_keys(keys: torch.Tensor, group=None) -> torch.Tensor:
     """Union of every rank's unique edge keys (int64 view, keys are > 0)."""
-    if dist.get_world_size() == 1:
+    if dist.get_world_size(group) == 1:
         return torch.unique(keys)
     n = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
-    dist.all_reduce(n, op=dist.ReduceOp.MAX)
-    pad = torch.zeros(int(n.item()), dtype=torch.int64, device=keys.device)
-    pad[: keys.numel()] = keys
-    parts = [torch.empty_like(pad) for _ in range(dist.get_world_size())]
-    dist.all_gather(parts, pad)
-    allk = torch.unique(torch.cat(parts))
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    allk = torch.unique(_gather_padded(keys, int(n.item()), dist.get_world_size(group), group))
     return allk[allk != 0]
 
 
-def merge_edge_keys_into(engine, keys: torch.Tensor) -> None:
+def merge_edge_keys_into(engine, keys: torch.Tensor, group=None) -> None:
     """Union every rank's edge keys into ``engine``'s device edge set
     (kmz_merge_triples: hash inserts into the run's set, no sort).  ``keys``:
     this rank's unique keys, int64 view, on the engine's GPU (RCCL) or on the
     CPU (gloo)."""
-    if dist.get_world_size() == 1:
+    if dist.get_world_size(group) == 1:
         return
     n = torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device)
-    dist.all_reduce(n, op=dist.ReduceOp.MAX)
-    m = int(n.item())
-    pad = torch.zeros(m, dtype=torch.int64, device=keys.device)
-    pad[: keys.numel()] = keys
-    if keys.is_cuda:
-        allk = torch.empty(m * dist.get_world_size(), dtype=torch.int64, device=keys.device)
-        dist.all_gather_into_tensor(allk, pad)
-        torch.cuda.current_stream(keys.device).synchronize()  # the engine's stream may not be torch's
-    else:
-        parts = [torch.empty_like(pad) for _ in range(dist.get_world_size())]
-        dist.all_gather(parts, pad)
-        allk = torch.cat(parts)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    allk = _gather_padded(keys, int(n.item()), dist.get_world_size(group), group)
     engine.merge_triples(allk.data_ptr(), allk.numel(), keys.is_cuda)

@@ -156,6 +156,31 @@ class Engine:
         self.n_status = d.n_status
         return self.n
 
+    def load_synthetic_shard(self, config: int, seed: int, trace_begin: int, trace_end: int, world: int,
+                             rank: int) -> int:
+        """The traces of [trace_begin, trace_end) with shard(traceId) == rank
+        (kmz_synth_load_shard), with their global flatten indices."""
+        n = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_synth_load_shard(self.ctx, config, seed, trace_begin, trace_end, world, rank,
+                                                         C.byref(n)))
+        d = L.SynthDesc()
+        self._lib.kmz_synth_describe(config, C.byref(d))
+        self.n = n.value
+        self.index_base = 0
+        self.n_dep_ep = d.n_endpoints
+        self.n_status = d.n_status
+        return self.n
+
+    def set_index_map(self, local_start: np.ndarray, global_start: np.ndarray):
+        """Local -> global flatten-index runs of a non-contiguous shard
+        (kmz_set_index_map): results then report global indices."""
+        ls = np.ascontiguousarray(local_start, dtype=np.uint64)
+        gs = np.ascontiguousarray(global_start, dtype=np.uint64)
+        if len(ls) != len(gs):
+            raise ValueError("local_start and global_start differ in length")
+        L.check(self.ctx, self._lib.kmz_set_index_map(self.ctx, L.ptr(ls), L.ptr(gs), len(ls)))
+        self.index_base = 0
+
     # ---- compute -------------------------------------------------------------
     def run(self, flags: int):
         L.check(self.ctx, self._lib.kmz_run(self.ctx, flags))

@@ -64,6 +64,16 @@ def shape_table(config: int) -> ShapeTable:
     return ShapeTable(ids, ids, ids, n_ep, n_ep, n_ep, n_status)
 
 
+def table_digest(config: int) -> int:
+    """Digest of a synthetic config's id tables (merge_all's guard): every
+    rank of a synthetic run indexes its partials by the same static tables."""
+    import hashlib
+
+    n_shapes, n_status, n_ep = describe(config)
+    h = hashlib.blake2b(f"kmz-synth:{config}:{n_shapes}:{n_status}:{n_ep}".encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little") & ((1 << 62) - 1)
+
+
 def count_spans(config: int, trace_begin: int, trace_end: int, seed: int = SEED) -> int:
     n = C.c_uint64()
     L.check(

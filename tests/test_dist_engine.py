@@ -155,3 +155,73 @@ def test_cross_shard_parent_is_refused():
         p.join(timeout=60)
     assert res[0] == (0, 0, "refused"), res
     assert res[1] == (1, 1, "refused"), res
+
+
+# ---------------------------------------------------------------------------
+# traceId sharding with different JSON shards (SURVEY.md 8e, config 4's merge)
+# ---------------------------------------------------------------------------
+def _json_shard_worker(rank, world, port, q, n_mesh):
+    import json
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from shard_util import endpoints_by_name, groups_by_name, mixed_traces
+
+        from kmamiz_amd import Engine
+        from kmamiz_amd import _lib as L
+        from kmamiz_amd.ingest import ingest_json
+        from kmamiz_amd.shard import gather_names, run_sharded, shard_traces
+
+        plan = shard_traces(mixed_traces(n_mesh), world)[rank]
+        batch, d = ingest_json(json.dumps(plan.traces).encode())  # this rank's own Zipkin response bytes
+        e = Engine(0)
+        r1 = run_sharded(e, batch, d, plan.local_start, plan.global_start, L.RUN_STATS_TAG | L.RUN_DEPS)
+        r2 = run_sharded(e, batch, d, plan.local_start, plan.global_start, L.RUN_STATS_RT)
+        tag, rt, dep = (gather_names(r1.tables, d, x) for x in ("tag", "rt", "dep"))
+        from shard_util import _edges
+
+        q.put((rank, groups_by_name(r1.groups, tag, r1.tables.statuses), _edges(r1.keys, dep),
+               endpoints_by_name(r1.endpoints, dep), groups_by_name(r2.groups, rt, r2.tables.statuses),
+               len(d.shapes), len(batch)))
+        e.close()
+    except Exception:
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc(), None, None, None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_json_shards_merge_equals_c_oracle(world):
+    """Config 4's merge on real engines: each rank parses its own JSON shard
+    (different shape sets), ids are made global by shard.exchange_tables, first
+    indices by the index map; the merged groups (both identity rules), edges
+    and endpoints equal the C oracle over the whole batch, on every rank."""
+    from shard_util import assert_groups_equal, mixed_traces, oracle_by_name
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_json_shard_worker, args=(r, world, port, q, 400)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] != "error", r[2]
+    traces = mixed_traces(400)
+    exp_g, exp_k, exp_e = oracle_by_name(traces, "tag")
+    exp_rt, _, _ = oracle_by_name(traces, "rt")
+    assert len({r[5] for r in res}) > 1  # the shards' shape tables differ
+    assert sum(r[6] for r in res) == sum(len(t) for t in traces)
+    for r in res:
+        assert_groups_equal(r[1], exp_g)
+        assert r[2] == exp_k
+        assert r[3] == exp_e
+        assert_groups_equal(r[4], exp_rt)

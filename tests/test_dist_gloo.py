@@ -18,10 +18,13 @@ import torch.multiprocessing as mp
 U64 = np.uint64
 
 
-def shard_partials(batch, ep_of_shape, n_ep, n_status, dep_ep, n_dep):
+def shard_partials(batch, ep_of_shape, n_ep, n_status, dep_ep, n_dep, gidx=None):
     """Engine partial layout for one shard (test-side restatement of K3/K4's
-    accumulators: integer moments, biased max timestamp, min first index)."""
+    accumulators: integer moments, biased max timestamp, min first index).
+    gidx: global flatten index of every local span (default index_base + i)."""
     G = n_ep * n_status
+    if gidx is None:
+        gidx = np.arange(len(batch), dtype=np.int64) + batch.index_base
     p = np.zeros(6 * G, dtype=U64)
     p[4 * G : 5 * G] = 0
     p[5 * G :] = U64(0xFFFFFFFFFFFFFFFF)
@@ -35,7 +38,7 @@ def shard_partials(batch, ep_of_shape, n_ep, n_status, dep_ep, n_dep):
     np.add.at(p, 3 * G + g, dd >> U64(32))
     tsx = batch.timestamp[srv].astype(np.int64).view(U64) ^ U64(1 << 63)
     np.maximum.at(p, 4 * G + g, tsx)
-    np.minimum.at(p, 5 * G + g, (srv + batch.index_base).astype(U64))
+    np.minimum.at(p, 5 * G + g, gidx[srv].astype(U64))
     # endpoint partials: rows = SERVER spans (unique ids in the synthetic data)
     e = np.zeros(2 * n_dep, dtype=U64)
     e[n_dep:] = U64(0xFFFFFFFFFFFFFFFF)
@@ -44,7 +47,7 @@ def shard_partials(batch, ep_of_shape, n_ep, n_status, dep_ep, n_dep):
     idx = {int(s): i for i, s in enumerate(batch.span_id.tolist())}
     ext = np.array([0 if (batch.parent_id[i] and batch.kind[idx[int(batch.parent_id[i])]] == 2 and
                           batch.parent_id[idx[int(batch.parent_id[i])]] != 0) else 1 for i in srv], dtype=U64)
-    np.minimum.at(e, n_dep + es, ((srv + batch.index_base).astype(U64) << U64(1)) | (U64(1) - ext))
+    np.minimum.at(e, n_dep + es, (gidx[srv].astype(U64) << U64(1)) | (U64(1) - ext))
     return p, e
 
 

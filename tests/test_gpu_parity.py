@@ -654,3 +654,84 @@ def test_certificate_at_scale_finds_one_repeated_id(engine):
         batch.span_id[j] = keep
         assert not (info["path"] & 1), "the certificate missed a repeated span id"
         assert info["n_dups"] == 1
+
+
+# ---------------------------------------------------------------------------
+# traceId sharding: device shard generation + index map
+# ---------------------------------------------------------------------------
+def _host_shard(config, t0, t1, world, rank):
+    """The traces of [t0, t1) with kmz_trace_shard(traceId) == rank, generated
+    on the host, with the index-map runs of their global positions."""
+    from kmamiz_amd import SpanBatch, synth
+    from kmamiz_amd.shard import trace_shard
+
+    batch, off = synth.host_batch(config, t0, t1)
+    sel, ls, gs, loc = [], [], [], 0
+    for t in range(t1 - t0):
+        if trace_shard(f"{(t0 + t) * 0x9E3779B97F4A7C15 % (1 << 128):032x}", world) != rank:
+            continue
+        a, b = int(off[t]), int(off[t + 1])
+        sel.append(np.arange(a, b))
+        ls.append(loc)
+        gs.append(batch.index_base + a)
+        loc += b - a
+    idx = np.concatenate(sel) if sel else np.zeros(0, np.int64)
+    cols = {f: getattr(batch, f)[idx] for f in ("span_id", "parent_id", "kind", "shape", "status", "duration",
+                                                 "timestamp")}
+    return SpanBatch(index_base=0, **cols), np.array(ls or [0], np.uint64), np.array(gs or [0], np.uint64)
+
+
+@pytest.mark.parametrize("config,t0,t1,world", [(3, 0, 3000, 3), (5, 7, 1500, 2), (2, 0, 20000, 4)])
+def test_shard_generation_and_index_map(engine, config, t0, t1, world):
+    """kmz_synth_load_shard == the host selection of the same traces through
+    kmz_set_index_map; the shards' partials, summed / max'ed / min'ed as
+    merge_all does, finalise to the single run over [t0, t1) bit for bit."""
+    from kmamiz_amd import Engine, synth
+    from kmamiz_amd import _lib as L
+
+    table = synth.shape_table(config)
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS
+    parts = []
+    total = 0
+    for rank in range(world):
+        n = engine.load_synthetic_shard(config, synth.SEED, t0, t1, world, rank)
+        engine.run(flags)
+        dev = engine.fetch()
+        dev = (dev[0].copy(), np.sort(dev[1]), dev[2])
+        hb, ls, gs = _host_shard(config, t0, t1, world, rank)
+        assert n == len(hb)
+        total += n
+        engine.load(hb, table)
+        engine.set_index_map(ls, gs)
+        engine.run(flags)
+        host = engine.fetch()
+        assert dev[0].tobytes() == host[0].tobytes()
+        assert np.array_equal(dev[1], np.sort(host[1]))
+        assert dev[2].tobytes() == host[2].tobytes()
+        gw, ew, tw = (engine.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
+        g, e, k = np.zeros(gw, np.uint64), np.zeros(ew, np.uint64), np.zeros(max(1, tw), np.uint64)
+        engine.export_partials(L.PART_GROUPS, g.ctypes.data, gw, False)
+        engine.export_partials(L.PART_ENDPOINTS, e.ctypes.data, ew, False)
+        engine.export_partials(L.PART_TRIPLES, k.ctypes.data, tw, False)
+        parts.append((g, e, k[:tw]))
+    G, E = len(parts[0][0]) // 6, len(parts[0][1]) // 2
+    g = parts[0][0].copy()
+    e = parts[0][1].copy()
+    for pg, pe, _ in parts[1:]:
+        g[: 4 * G] += pg[: 4 * G]
+        g[4 * G: 5 * G] = np.maximum(g[4 * G: 5 * G], pg[4 * G: 5 * G])
+        g[5 * G:] = np.minimum(g[5 * G:], pg[5 * G:])
+        e[:E] = np.maximum(e[:E], pe[:E])
+        e[E:] = np.minimum(e[E:], pe[E:])
+    keys = np.unique(np.concatenate([k for _, _, k in parts]))
+    n = engine.load_synthetic(config, synth.SEED, t0, t1)
+    assert n == total
+    engine.run(flags)
+    whole = engine.fetch()
+    assert np.array_equal(np.sort(whole[1]), keys)
+    gw, ew = engine.partials_words(L.PART_GROUPS), engine.partials_words(L.PART_ENDPOINTS)
+    wg, we = np.zeros(gw, np.uint64), np.zeros(ew, np.uint64)
+    engine.export_partials(L.PART_GROUPS, wg.ctypes.data, gw, False)
+    engine.export_partials(L.PART_ENDPOINTS, we.ctypes.data, ew, False)
+    assert np.array_equal(wg, g)
+    assert np.array_equal(we, e)
