@@ -217,7 +217,7 @@ def test_cycle_is_reported(engine):
 # ---------------------------------------------------------------------------
 # synthetic configs vs the C oracle
 # ---------------------------------------------------------------------------
-def _compare_synth(engine, batch, table):
+def _compare_synth(engine, batch, table, odeps=None):
     from kmamiz_amd import _lib as L
 
     engine.load(batch, table)
@@ -233,7 +233,7 @@ def _compare_synth(engine, batch, table):
     keys = engine.triples()
     ep = engine.endpoints()
     info = engine.info()
-    okeys, oep, ocnt = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    okeys, oep, ocnt = odeps or c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
     assert np.array_equal(keys, okeys)
     assert np.array_equal(ep["has_row"].astype(bool), oep["has_row"])
     assert np.array_equal(ep["first_row"][oep["has_row"]], oep["first"][oep["has_row"]])
@@ -247,7 +247,7 @@ def _compare_synth(engine, batch, table):
     return info
 
 
-@pytest.mark.parametrize("config,ntr", [(2, 30000), (3, 4000), (3, 40000), (5, 2000), (5, 20000)])
+@pytest.mark.parametrize("config,ntr", [(2, 30000), (3, 4000), (3, 40000), (3, 366000), (5, 2000), (5, 20000)])
 def test_synthetic_vs_c_oracle(engine, config, ntr):
     from kmamiz_amd import synth
 
@@ -735,3 +735,87 @@ def test_shard_generation_and_index_map(engine, config, t0, t1, world):
     engine.export_partials(L.PART_ENDPOINTS, we.ctypes.data, ew, False)
     assert np.array_equal(wg, g)
     assert np.array_equal(we, e)
+
+
+def test_headline_size_config3_properties(engine):
+    """Config 3 at its BASELINE size (1e8 spans, beyond the oracle): every
+    SERVER span is one row and one group member; a second run is byte-equal;
+    the edge set / groups / endpoints equal the merge of two traceId shards of
+    the same batch (kmz_synth_load_shard + the index map)."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    ntr = 3657845  # bench.py's config-3 batch (100 071 364 spans)
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS
+    n = engine.load_synthetic(3, synth.SEED, 0, ntr)
+    assert n > 1e8
+    engine.run(flags)
+    i1 = engine.info()
+    g1, k1, e1 = (x.copy() for x in engine.fetch())
+    k1.sort()
+    assert int(g1["combined"].sum()) == i1["n_server"] == i1["n_rows"]
+    assert i1["n_dups"] == 0 and i1["max_depth"] == 7  # 8 levels: 7 hops to the root service
+    # every endpoint with a row is first used by its first row; external rows are roots' children
+    assert np.all(e1["first_row"][e1["has_row"] == 1] < n)
+    engine.run(flags)
+    g2, k2, e2 = engine.fetch()
+    assert g2.tobytes() == g1.tobytes() and e2.tobytes() == e1.tobytes()
+    assert np.array_equal(np.sort(k2), k1)
+    # two shards by traceId, merged as merge_all does
+    G = len(g1)
+    parts = []
+    for rank in range(2):
+        engine.load_synthetic_shard(3, synth.SEED, 0, ntr, 2, rank)
+        engine.run(flags)
+        gw, ew, tw = (engine.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
+        g, e, k = np.zeros(gw, np.uint64), np.zeros(ew, np.uint64), np.zeros(max(1, tw), np.uint64)
+        engine.export_partials(L.PART_GROUPS, g.ctypes.data, gw, False)
+        engine.export_partials(L.PART_ENDPOINTS, e.ctypes.data, ew, False)
+        engine.export_partials(L.PART_TRIPLES, k.ctypes.data, tw, False)
+        parts.append((g, e, k[:tw]))
+    (ga, ea, ka), (gb, eb, kb) = parts
+    E = len(ea) // 2
+    g = np.concatenate([ga[:4 * G] + gb[:4 * G], np.maximum(ga[4 * G:5 * G], gb[4 * G:5 * G]),
+                        np.minimum(ga[5 * G:], gb[5 * G:])])
+    e = np.concatenate([np.maximum(ea[:E], eb[:E]), np.minimum(ea[E:], eb[E:])])
+    from kmamiz_amd import finalize_host
+
+    assert finalize_host(g, G).tobytes() == g1.tobytes()
+    assert np.array_equal(e[E:] >> np.uint64(1), np.where(e1["has_row"] == 1, e1["first_row"], e[E:] >> np.uint64(1)))
+    assert np.array_equal(np.union1d(ka, kb), k1)
+
+
+def test_headline_config5_vs_c_oracle_and_tail():
+    """Config 5 at 1e7 spans: groups, edges and endpoints vs the C oracle, and
+    the service tail kernel vs the numpy restatement over the ORACLE's edge
+    keys and endpoint records (so the tail is pinned to the oracle at scale)."""
+    from test_tail import _tail_np
+
+    from kmamiz_amd import Engine, synth
+    from kmamiz_amd.tail import maps_for_synth, run_tail
+
+    batch, _ = synth.host_batch(5, 0, 175000)
+    assert len(batch) > 9.9e6
+    table = synth.shape_table(5)
+    e = Engine(0)
+    try:
+        odeps = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+        okeys, oep, _ = odeps
+        _compare_synth(e, batch, table, odeps)  # groups / edges / endpoints vs the C oracle
+        maps = maps_for_synth(5)
+        tail = run_tail(e, maps, e.endpoints())
+        first = np.where(oep["has_row"], oep["first"], np.iinfo(np.uint64).max).astype(np.uint64)
+        ref = _tail_np(okeys, maps, oep["has_row"], first)
+        for f in tail.details.dtype.names:
+            assert np.array_equal(tail.details[f], ref.details[f]), f
+        for f in tail.pairs.dtype.names:
+            assert np.array_equal(tail.pairs[f], ref.pairs[f]), f
+        assert np.array_equal(tail.gateway, ref.gateway)
+        assert np.array_equal(tail.stats, ref.stats)
+        assert tail.instability() == ref.instability()
+        assert tail.coupling() == ref.coupling()
+        mt, mr = tail.metrics(), ref.metrics()
+        for k in mt:
+            np.testing.assert_allclose(np.asarray(mt[k], dtype=float), np.asarray(mr[k], dtype=float), rtol=REL)
+    finally:
+        e.close()

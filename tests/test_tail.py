@@ -77,24 +77,34 @@ def _tail_np(keys, maps, endpoints_has_row, first_row):
 
     a, s, d, on = decode_triples(keys)
     svc, cls, lsvc = maps.svc.astype(np.int64), maps.cls.astype(np.int64), maps.lsvc.astype(np.int64)
-    # link keys (svc, cls, type, d), unique
-    lk = np.concatenate([np.stack([svc[s], cls[a], np.zeros_like(d), d], 1),
-                         np.stack([svc[a[on]], cls[s[on]], np.ones(on.sum(), dtype=np.int64), d[on]], 1)])
-    lk = np.unique(lk, axis=0)
-    dk = np.stack([lk[:, 0], lsvc[lk[:, 1]], lk[:, 3]], 1)
-    u, inv = np.unique(dk, axis=0, return_inverse=True)
+    U = np.uint64
+    M24 = (1 << 24) - 1
+    # link keys (svc, cls, type, d), unique -- packed 24 | 24 | 1 | 15 bits
+    def pack(*f):
+        k = np.zeros(len(f[0][0]), dtype=U)
+        for v, bits in f:
+            k = (k << U(bits)) | np.asarray(v, dtype=np.int64).astype(U)
+        return k
+    lk = np.unique(np.concatenate([pack((svc[s], 24), (cls[a], 24), (np.zeros_like(d), 1), (d, 15)),
+                                   pack((svc[a[on]], 24), (cls[s[on]], 24), (np.ones(int(on.sum()), np.int64), 1),
+                                        (d[on], 15))]))
+    l_svc = (lk >> U(40)).astype(np.int64)
+    l_cls = ((lk >> U(16)) & U(M24)).astype(np.int64)
+    l_typ = ((lk >> U(15)) & U(1)).astype(np.int64)
+    l_d = (lk & U(0x7FFF)).astype(np.int64)
+    u, inv = np.unique(pack((l_svc, 24), (lsvc[l_cls], 24), (l_d, 15)), return_inverse=True)
     inv = inv.reshape(-1)
     det = np.zeros(len(u), dtype=L.TAIL_DETAIL_DTYPE)
-    det["svc"], det["lsvc"], det["distance"] = u[:, 0], u[:, 1], u[:, 2]
+    det["svc"], det["lsvc"], det["distance"] = u >> U(39), (u >> U(15)) & U(M24), u & U(0x7FFF)
     det["count"] = np.bincount(inv, minlength=len(u))
-    det["depending_by"] = np.bincount(inv, weights=lk[:, 2] == 0, minlength=len(u))
-    det["depending_on"] = np.bincount(inv, weights=lk[:, 2] == 1, minlength=len(u))
+    det["depending_by"] = np.bincount(inv, weights=l_typ == 0, minlength=len(u))
+    det["depending_on"] = np.bincount(inv, weights=l_typ == 1, minlength=len(u))
     one = d == 1
-    pk = np.unique(np.stack([s[one], svc[a[one]]], 1), axis=0)
-    pv = np.stack([svc[pk[:, 0]], pk[:, 1]], 1)
-    pu, pinv = np.unique(pv, axis=0, return_inverse=True)
+    pk = np.unique(pack((s[one], 24), (svc[a[one]], 24)))
+    pu, pinv = np.unique(pack((svc[(pk >> U(24)).astype(np.int64)], 24), ((pk & U(M24)).astype(np.int64), 24)),
+                         return_inverse=True)
     pairs = np.zeros(len(pu), dtype=L.TAIL_PAIR_DTYPE)
-    pairs["svc"], pairs["consumer"] = pu[:, 0], pu[:, 1]
+    pairs["svc"], pairs["consumer"] = pu >> U(24), pu & U(M24)
     pairs["consumes"] = np.bincount(pinv.reshape(-1), minlength=len(pu))
     hasin = np.zeros(maps.n_ep, dtype=np.uint8)
     hasin[s] = 1
