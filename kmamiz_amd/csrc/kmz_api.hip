@@ -56,7 +56,7 @@ struct kmz_ctx {
   DevBuf synth_cnt, synth_off, dur_table;
   DevBuf k3pool, k3dir, k3part, tile_tmp, sgrp;
   DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
-  DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n;  // K4 chain interning
+  DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n, cetab;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
   DevBuf imap_l, imap_g;  // local -> global flatten-index runs of a non-contiguous shard (kmz_shard.hip)
@@ -285,7 +285,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->stats64,   &c->scratch,
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
-                    &c->mval, &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
+                    &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
                     &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
@@ -408,7 +408,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
   // probes leave HBM to the certificate (measured: mesh 5.21 -> 5.12 ms,
   // Bookinfo 0.385 -> 0.323 ms); a chain table in HBM (config 5, 4 GB) and
   // the certificate slow each other down (19.3 -> 25.7 ms)
-  const bool cert_side = c->overlap && !(c->ablate & (1u << 26)) && c->ccap * 32 <= (256ull << 20);
+  const bool cert_side = c->overlap && !(c->ablate & (1u << 26)) && c->ccap * CHAIN_ENTRY_BYTES <= (256ull << 20);
   if (cert_side) {  // the certificate checks the join's ids beside the chain walk (read after the run)
     HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
@@ -550,11 +550,11 @@ static int run_deps(kmz_ctx *c, bool links) {
     // run's global list of wcap more follows them)
     const uint32_t scap = c->scap, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
     void *old_ctab = c->ctab.p;
-    if (ensure(c, c->ctab, c->ccap * 32) || ensure(c, c->ctile, (size_t)nt * 16) ||
+    if (ensure(c, c->ctab, c->ccap * CHAIN_ENTRY_BYTES) || ensure(c, c->ctile, (size_t)nt * 16) ||
         ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, (size_t)ng * scap * 8) ||
-        ensure(c, c->kstage_n, (size_t)ng * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 32) ||
+        ensure(c, c->kstage_n, (size_t)ng * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 16) ||
         ensure(c, c->kdefer_n, (size_t)ng * 4) || ensure(c, c->kwpos, ((size_t)ng + 1) * wcap * 4) ||
-        ensure(c, c->kwpos_n, (size_t)ng * 4))
+        ensure(c, c->kwpos_n, (size_t)ng * 4) || ensure(c, c->cetab, ((size_t)c->n_shapes + 1) * 16))
       return KMZ_E_HIP;
     if (c->ctab.p != old_ctab) c->ctab_dirty = true;
     uint32_t *wpos = P<uint32_t>(c->kwpos), *gpos = wpos + (size_t)ng * wcap;
@@ -562,7 +562,7 @@ static int run_deps(kmz_ctx *c, bool links) {
       Timed t(c, KMZ_K_MEMSET);
       // the chain table is cleared entry by entry after each run; a full
       // memset only when it is new or a list overflowed
-      if (c->ctab_dirty) HIPCHK(c, hipMemsetAsync(c->ctab.p, 0, c->ccap * 32, c->stream));
+      if (c->ctab_dirty) HIPCHK(c, hipMemsetAsync(c->ctab.p, 0, c->ccap * CHAIN_ENTRY_BYTES, c->stream));
       HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
     }
     c->ctab_dirty = true;  // until this run's slots are cleared below
@@ -573,7 +573,7 @@ static int run_deps(kmz_ctx *c, bool links) {
                    P<unsigned long long>(c->trip), c->tcap, epp, links ? P<unsigned long long>(c->rowpos) : nullptr,
                    P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage),
                    scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
-                   wpos, wcap, P<uint32_t>(c->kwpos_n),
+                   wpos, wcap, P<uint32_t>(c->kwpos_n), P<uint4>(c->cetab),
                    // (test knob 24 forces sig collisions on the first seed only)
                    c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)));
     }
@@ -783,7 +783,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     // <= 1/4: a found chain is then almost always at its home slot (each
     // extra slot is another dependent probe round trip)
     while (c->chain_ran && c->ccap < (1ull << 31) &&
-           (s64[S_CHAINS] * 4 > c->ccap || (s64[S_CHAINS] * 8 > c->ccap && c->ccap * 32 < (256ull << 20))))
+           (s64[S_CHAINS] * 4 > c->ccap || (s64[S_CHAINS] * 8 > c->ccap && c->ccap * CHAIN_ENTRY_BYTES < (256ull << 20))))
       c->ccap *= 2;
     if ((flags & KMZ_RUN_DEPS) && s64[S_TRIP_OUT] * 2 > c->tcap) c->tcap *= 2;
     bool retry = false;

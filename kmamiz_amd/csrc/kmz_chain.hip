@@ -8,20 +8,23 @@
 // ancestors only.  That sequence -- the row's *chain* -- is interned in a
 // global open-addressing table of 32-byte entries
 //
-//     { sig(chain), sig(parent chain) (ROOT_SIG at a root), endpoint, kind == SERVER }
+//     { sig(chain), sig(parent chain) (ROOT_SIG at a root) }
 //
 // Rows that share a chain (most of them: the 100M-span mesh has ~0.5M distinct
 // chains) produce identical edge keys, so only the workgroup that inserts a new
 // chain emits its keys; nothing per relation is written to HBM.
 //
-// `sig` is a 64-bit polynomial hash of the whole ancestry, computed by walking
-// the ancestors in LDS, so every span probes the table once, in one round, with
-// no dependency on its parent's probe or insert.  Exactness does not rest on
-// the hash: an entry records the exact recursive definition (parent chain,
-// endpoint, kind) and every span checks the entry it found or joined against
-// its own.  The table holds one entry per sig, so by induction from the roots
-// equal sigs are equal chains; a failed check (a 64-bit collision) raises F_SIG
-// and the run is repeated with another hash seed.
+// `sig` is a 64-bit hash of the whole ancestry (a rotate-xor fold of the
+// ancestors' element hashes, finished by the mix64 bijection), computed by
+// walking the ancestors in LDS, so every span probes the table once, in one
+// round, with no dependency on its parent's probe or insert.  Exactness does
+// not rest on the hash: every span checks the entry it found or joined against
+// its own parent sig.  The table holds one entry per sig, so by induction from
+// the roots a checked parent sig names one exact parent chain; for that parent
+// the fold, the finish and the element hash are all bijective in the span's
+// own (endpoint, kind), so an equal sig is an equal chain.  (The two values the
+// finish may not produce, 0 and ROOT_SIG, raise F_SIG like a failed check: the
+// run is repeated with another hash seed.)  An entry is 16 bytes.
 //
 //   k4_chain       persistent workgroups over 768-span tiles + a 128-span halo
 //                  per side in LDS (contracted parent, kind, endpoint, element
@@ -66,24 +69,35 @@ constexpr uint32_t IMAP = 256;  // LDS map: one inserting leader per distinct ne
 #endif
 constexpr int CHAIN_WAVES = KMZ_CHAIN_WAVES;  // waves per SIMD: 4 -> 2 workgroups per CU (<= 128 VGPRs), 6 -> 3
 constexpr uint32_t CHAIN_WG = 256 * CHAIN_WAVES * 4 / (CTT / 64);  // persistent workgroups (fill the CUs)
-constexpr uint64_t SIG_M = 0xD6E8FEB86659FD93ull;
+constexpr uint32_t SIG_R = 21;  // fold rotation (odd: x ^ rotl(x, R) is 2-to-1 only on {x, ~x})
 // per-slot byte: kind in bits 0-1, state in bits 2-3 (state written only by the slot's owner)
 constexpr uint8_t S_NONE = 0, S_DONE = 1, S_PUT = 2, S_PEND = 3;
 __device__ __forceinline__ uint8_t kf_kind(uint8_t b) { return b & 3; }
 __device__ __forceinline__ uint8_t kf_st(uint8_t b) { return b >> 2; }
 __device__ __forceinline__ uint8_t kf_make(uint8_t kind, uint8_t st) { return (uint8_t)(kind | (st << 2)); }
 
-__device__ __forceinline__ uint64_t sig_elem(uint32_t ep, bool on, uint64_t seed) {
+__host__ __device__ __forceinline__ uint64_t sig_elem(uint32_t ep, bool on, uint64_t seed) {
   return mix64((((uint64_t)ep << 1) | (on ? 1ull : 0ull)) ^ seed);
 }
 constexpr uint64_t ROOT_SIG = ~0ull;  // the "parent sig" of a root
-__device__ __forceinline__ uint64_t sig_final(uint64_t acc, uint32_t d, uint64_t seed) {
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, uint32_t r) {
+  r &= 63;
+  return r ? (x << r) | (x >> (64 - r)) : x;
+}
+// one fold step: the ancestors a1 (nearest) .. aD give
+//   acc = rotl^(D-1)(e(a1)) ^ ... ^ rotl(e(aD-1)) ^ e(aD)
+__device__ __forceinline__ uint64_t sig_step(uint64_t acc, uint64_t el) {
+  return ((acc << SIG_R) | (acc >> (64 - SIG_R))) ^ el;
+}
+// 0 marks an unwritten word and ROOT_SIG a root's parent: a sig equal to
+// either is treated as a collision (another seed)
+__device__ __forceinline__ uint64_t sig_final(uint64_t acc, uint32_t d, uint64_t seed, uint32_t *flags) {
   const uint64_t z = mix64(acc ^ ((uint64_t)d * 0x632BE59BD9B4E019ull) ^ (seed << 1));
-  return (z == 0 || z == ROOT_SIG) ? 1 : z;  // 0 marks an unwritten word, ROOT_SIG a root's parent
+  if (z == 0 || z == ROOT_SIG) *flags |= F_SIG;
+  return z;
 }
-__device__ __forceinline__ uint64_t epon_of(uint32_t ep, bool on) {
-  return (1ull << 63) | ((uint64_t)ep << 1) | (on ? 1ull : 0ull);  // never 0 (0 = unpublished)
-}
+// the sig is already a mix64 output: its high bits place it
+__device__ __forceinline__ uint64_t cslot(uint64_t sig, uint64_t ccap) { return mulhi64(sig, ccap); }
 
 __device__ __forceinline__ uint64_t edge_key(uint32_t ea, uint32_t es, uint32_t d, bool on) {
   return ((uint64_t)ea << 40) | ((uint64_t)es << 16) | ((uint64_t)d << 1) | (on ? 1ull : 0ull);
@@ -106,24 +120,22 @@ __device__ __forceinline__ void edge_insert(uint64_t key, unsigned long long *__
   *flags |= F_TRIPLE_OVERFLOW;
 }
 
-// Chain table entry words: [0] sig, [1] parent sig (ROOT_SIG at a root),
-// [2] endpoint/kind, [3] unused.  Every word is written once with a nonzero
-// value, so a reader needs no ordering between them: an entry is published
-// once all three are nonzero.
+// Chain table entry words: [0] sig, [1] parent sig (ROOT_SIG at a root).
+// Both are written once with a nonzero value, so a reader needs no ordering
+// between them: an entry is published once both are nonzero.
 // Insert (or join) the chain `sig`.  Returns 1 inserted, 2 found (and
 // checked), 0 not yet decidable (the winner has not published), -1 probe bound.
 // A slot this call claims is appended to the run's written list (gpos, counted
 // in counters[C_WPOS]) so that it can be cleared after the run.
 __device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, uint64_t ccap, uint64_t sig,
-                                         uint64_t psig, uint64_t epon, uint32_t *flags, uint32_t *__restrict__ gpos,
+                                         uint64_t psig, uint32_t *flags, uint32_t *__restrict__ gpos,
                                          uint32_t gcap, unsigned int *__restrict__ counters) {
-  uint64_t pos = slot_of(sig, ccap);
+  uint64_t pos = cslot(sig, ccap);
   for (uint32_t z = 0; z < PROBE_MAX; ++z) {
-    unsigned long long *e = ctab + 4 * pos;
+    unsigned long long *e = ctab + 2 * pos;
     const unsigned long long c = atomicCAS(&e[0], 0ull, (unsigned long long)sig);
     if (c == 0) {
       atomicExch(&e[1], (unsigned long long)psig);
-      atomicExch(&e[2], (unsigned long long)epon);
       const uint32_t x = atomicAdd(&counters[C_WPOS], 1u);  // (rare paths only)
       if (x < gcap)
         gpos[x] = (uint32_t)pos;
@@ -132,9 +144,9 @@ __device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, 
       return 1;
     }
     if (c == sig) {
-      const unsigned long long ps = atomicAdd(&e[1], 0ull), w = atomicAdd(&e[2], 0ull);  // memory-side reads
-      if (w == 0 || ps == 0) return 0;
-      if (w != epon || ps != psig) *flags |= F_SIG;
+      const unsigned long long ps = atomicAdd(&e[1], 0ull);  // memory-side read
+      if (ps == 0) return 0;
+      if (ps != psig) *flags |= F_SIG;
       return 2;
     }
     pos = pos + 1 == ccap ? 0 : pos + 1;
@@ -147,7 +159,7 @@ __device__ unsigned long long g_chain_dbg[8];  // diagnostic phase clocks (KMZ_A
 
 __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape, const int64_t *__restrict__ ts,
-    const uint32_t *__restrict__ cparent, uint32_t n, const uint32_t *__restrict__ dep_ep, uint32_t n_shapes,
+    const uint32_t *__restrict__ cparent, uint32_t n, const uint4 *__restrict__ etab, uint32_t n_shapes,
     uint32_t n_ep, uint64_t index_base, uint64_t seed, unsigned long long *__restrict__ ctab, uint64_t ccap,
     unsigned long long *__restrict__ trip, uint64_t tcap, unsigned long long *__restrict__ ep_ts,
     unsigned long long *__restrict__ rowpos_out, uint32_t *__restrict__ plist, uint32_t pcap,
@@ -158,8 +170,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   // one 16-byte record per window slot: element hash (x, y), endpoint (z),
   // contracted parent | kind << 16 (w) -- a walk step is one LDS read
   __shared__ uint4 lrec[CW];
-  __shared__ unsigned long long lpow[WIN_DEPTH + 1];  // SIG_M^d
-  __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP], imap_epon[IMAP];
+  __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP];
   __shared__ uint32_t scnt, dcnt;  // keys staged for k_chain_settle, records deferred to k_chain_settle
   __shared__ uint32_t wcnt;        // chain-table slots this workgroup claimed (cleared after the run)
   __shared__ uint32_t red[CTT / 64][4];
@@ -174,7 +185,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   }
   // persistent: this workgroup walks tiles blockIdx.x, +gridDim.x, ...; the
   // next tile's window is loaded into registers while the current one computes
-  uint32_t c[CPW], sh[CPW], e[CPW];
+  uint32_t c[CPW], sh[CPW];
+  uint4 e[CPW];  // the slot's shape: endpoint, SERVER element hash (k_chain_etab)
   uint8_t k[CPW];
   auto fetch = [&](uint32_t tl) {
     const uint32_t tb = tl * CT, wb = tb > CH ? tb - CH : 0;
@@ -188,15 +200,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   };
   auto gather_ep = [&]() {
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) e[q] = dep_ep[sh[q] < n_shapes ? sh[q] : 0];
+    for (int q = 0; q < CPW; ++q) e[q] = etab[sh[q] < n_shapes ? sh[q] : 0];
   };
   if (threadIdx.x == 0) scnt = dcnt = wcnt = 0;
-  if (threadIdx.x <= WIN_DEPTH) {
-    uint64_t r = 1, b = SIG_M;
-    for (uint32_t x = threadIdx.x; x; x >>= 1, b *= b)
-      if (x & 1) r *= b;
-    lpow[threadIdx.x] = r;
-  }
   if (blockIdx.x < nt) {
     fetch(blockIdx.x);
     gather_ep();
@@ -212,10 +218,12 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     for (int q = 0; q < CPW; ++q) {
       const uint32_t jl = q * CTT + threadIdx.x;
       const bool client = k[q] == KIND_CLIENT;
-      const uint32_t ep = (client || sh[q] >= n_shapes) ? NONE : e[q];
+      const uint32_t ep = (client || sh[q] >= n_shapes) ? NONE : e[q].x;
       const uint32_t cp =
           c[q] == NONE ? W_NONE : (c[q] == CYC ? W_CYC : ((c[q] >= w0 && c[q] < w1) ? c[q] - w0 : W_OUT));
-      const uint64_t el = client ? 0 : sig_elem(ep, k[q] == KIND_SERVER, seed);
+      uint64_t el = ((uint64_t)e[q].z << 32) | e[q].y;  // SERVER
+      if (client) el = 0;
+      else if ((k[q] & 3) != KIND_SERVER || sh[q] >= n_shapes) el = sig_elem(ep, k[q] == KIND_SERVER, seed);  // (rare)
       if (jl < wn) lrec[jl] = make_uint4((uint32_t)el, (uint32_t)(el >> 32), ep, cp | ((uint32_t)(k[q] & 3) << 16));
       other |= jl < wn && (k[q] & 3) != KIND_SERVER && !client;
     }
@@ -224,10 +232,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     KMZ_STAMP(1);
     const bool more = tile + gridDim.x < nt;
     if (more) fetch(tile + gridDim.x);  // lands while this tile computes
-    // hash the ancestry of every non-CLIENT span of the tile by a Horner walk
+    // hash the ancestry of every non-CLIENT span of the tile by a fold walk
     // over the LDS element hashes of its ancestors a1..aD:
-    //   pacc = (elem(a1) M + elem(a2)) M + ... + elem(aD)
-    //   sig  = final(elem(s) M^D + pacc, D),  parent sig = final(pacc, D-1)
+    //   pacc = rotl^(D-1)(elem(a1)) ^ ... ^ elem(aD)
+    //   sig  = final(rotl^D(elem(s)) ^ pacc, D),  parent sig = final(pacc, D-1)
     // (the parent's own sig, so halo spans need no walk), and issue the probes
     // at once.  A row's walk also gives its non-SERVER ancestors (not rows)
     // their lastUsage.
@@ -268,7 +276,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
 #pragma unroll
       for (int q = 0; q < TPW; ++q) {
         const bool act = wa[q] < CW && dd[q] < WIN_DEPTH;
-        const uint64_t nacc = acc[q] * SIG_M + ((uint64_t)r[q].y << 32 | r[q].x);
+        const uint64_t nacc = sig_step(acc[q], (uint64_t)r[q].y << 32 | r[q].x);
         if (any_other && act && kq[q] == KIND_SERVER && ((r[q].w >> 16) & 3) != KIND_SERVER) {
           // (rare) a non-SERVER ancestor of a row
           if (r[q].z < n_ep)
@@ -294,8 +302,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         continue;
       }
       const uint32_t d = dd[q];
-      ps[q] = d ? sig_final(acc[q], d - 1, seed) : ROOT_SIG;
-      sg[q] = sig_final(sg[q] * lpow[d] + acc[q], d, seed);
+      ps[q] = d ? sig_final(acc[q], d - 1, seed, &flags) : ROOT_SIG;
+      sg[q] = sig_final(rotl64(sg[q], SIG_R * d) ^ acc[q], d, seed, &flags);
       if (ablate & (1u << 24)) {  // test knob: 4-bit sigs, i.e. collisions (F_SIG, then a retry with another seed)
         sg[q] = (sg[q] & 0xF) + 2;
         ps[q] = d ? (ps[q] & 0xF) + 2 : ROOT_SIG;
@@ -303,37 +311,30 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       if (!(ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
     ulonglong2 w01[TPW];  // (sig, parent sig) of the probed slot
-    uint64_t w2[TPW];     // its endpoint/kind word
     uint64_t pos[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
       const bool pr = st[q] == S_PUT;
-      pos[q] = pr ? slot_of(sg[q], ccap) : 0;
-      const unsigned long long *en = ctab + 4 * pos[q];
+      pos[q] = pr ? cslot(sg[q], ccap) : 0;
+      const unsigned long long *en = ctab + 2 * pos[q];
       w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(en) : make_ulonglong2(0, 0);
-      w2[q] = pr ? en[2] : 0;
     }
     KMZ_STAMP(2);
     // check what the probes found against (parent sig, endpoint, kind); a
     // chain not found (or not yet published) elects one leader per distinct
     // sig in this workgroup
     uint32_t hslot[TPW];
-    uint64_t epon[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
       hslot[q] = IMAP + 1;  // not an insert
-      epon[q] = 0;
       if (st[q] != S_PUT) continue;
       for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
         pos[q] = pos[q] + 1 == ccap ? 0 : pos[q] + 1;
-        const unsigned long long *en = ctab + 4 * pos[q];
-        w01[q] = *reinterpret_cast<const ulonglong2 *>(en);
-        w2[q] = en[2];
+        w01[q] = *reinterpret_cast<const ulonglong2 *>(ctab + 2 * pos[q]);
       }
-      epon[q] = epon_of(myep[q], kq[q] == KIND_SERVER);
       st[q] = S_DONE;
-      if (w01[q].x == sg[q] && w01[q].y != 0 && w2[q] != 0) {
-        if (w2[q] != epon[q] || w01[q].y != ps[q]) flags |= F_SIG;
+      if (w01[q].x == sg[q] && w01[q].y != 0) {
+        if (w01[q].y != ps[q]) flags |= F_SIG;
         continue;
       }
       uint32_t h = (uint32_t)(sg[q] >> 32) & (IMAP - 1);
@@ -342,7 +343,6 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         const unsigned long long kk = atomicCAS(&imap_sig[h], 0ull, (unsigned long long)sg[q]);
         if (kk == 0) {  // leader: publish what the followers compare against
           imap_psig[h] = ps[q];
-          imap_epon[h] = epon[q];
           hslot[q] = h;
           break;
         }
@@ -369,18 +369,18 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       if (hslot[q] > IMAP) {
         if (hslot[q] != IMAP + 1) {  // follower
           const uint32_t h = hslot[q] & (IMAP - 1);
-          if (imap_psig[h] != ps[q] || imap_epon[h] != epon[q]) flags |= F_SIG;
+          if (imap_psig[h] != ps[q]) flags |= F_SIG;
         }
         continue;
       }
       const uint32_t jl = toff + q * CTT + threadIdx.x;
-      unsigned long long *en = ctab + 4 * pos[q];
+      unsigned long long *en = ctab + 2 * pos[q];
       const unsigned long long cv = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
       const uint32_t d = dd[q];
       // a row whose chain this leader inserted (or lost to another chain: the
       // deferred check may insert it) stages its keys; one that joined the
       // same chain leaves them to the winner (knob 19: diagnostic, none)
-      if ((epon[q] & 1) && d && cv != sg[q] && !(ablate & (1u << 19))) {
+      if (kq[q] == KIND_SERVER && d && cv != sg[q] && !(ablate & (1u << 19))) {
         const uint32_t es = myep[q];
         const uint32_t base = atomicAdd(&scnt, d);
         uint32_t a = lrec[jl].w & 0xFFFF;
@@ -398,7 +398,6 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       }
       if (cv == 0) {  // won the slot: publish
         atomicExch(&en[1], (unsigned long long)ps[q]);
-        atomicExch(&en[2], (unsigned long long)epon[q]);
         ++fresh_n;
         const uint32_t x = atomicAdd(&wcnt, 1u);
         if (x < wcap)
@@ -408,14 +407,11 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       } else {  // joined an unpublished entry, or lost the slot to another chain
         const uint32_t x = atomicAdd(&dcnt, 1u);
         if (x < dcap) {
-          unsigned long long *r = defer + 4 * ((uint64_t)blockIdx.x * dcap + x);
-          r[0] = sg[q];
-          r[1] = ps[q];
-          r[2] = epon[q];
+          *reinterpret_cast<ulonglong2 *>(defer + 2 * ((uint64_t)blockIdx.x * dcap + x)) = make_ulonglong2(sg[q], ps[q]);
         } else {
           int rr = 0;
           for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t)
-            rr = chain_put(ctab, ccap, sg[q], ps[q], epon[q], &flags, wpos + (uint64_t)gridDim.x * wcap, wcap,
+            rr = chain_put(ctab, ccap, sg[q], ps[q], &flags, wpos + (uint64_t)gridDim.x * wcap, wcap,
                            counters);  // (the run's global written list follows the per-workgroup ones)
           fresh_n += rr == 1;
         }
@@ -498,10 +494,10 @@ __global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *
     for (uint32_t x = threadIdx.x; x < m; x += blockDim.x) edge_insert(stage[(uint64_t)w * scap + x], trip, tcap, &flags);
     const uint32_t md = defer_n[w];
     for (uint32_t x = threadIdx.x; x < md; x += blockDim.x) {
-      const unsigned long long *r = defer + 4 * ((uint64_t)w * dcap + x);
+      const unsigned long long *r = defer + 2 * ((uint64_t)w * dcap + x);
       int rr = 0;
       for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t)
-        rr = chain_put(ctab, ccap, r[0], r[1], r[2], &flags, gpos, gcap, counters);
+        rr = chain_put(ctab, ccap, r[0], r[1], &flags, gpos, gcap, counters);
       fresh += rr == 1;
     }
   }
@@ -535,7 +531,7 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     const uint32_t es = sh < n_shapes ? dep_ep[sh] : NONE;
     const bool on = ki == KIND_SERVER;
     if (es >= n_ep && on) flags |= F_RANGE;
-    // Horner hashes of the span's ancestry and of its parent's (suffix) ancestry
+    // fold hashes of the span's ancestry and of its parent's (suffix) ancestry
     uint64_t acc = sig_elem(es, on, seed), pacc = 0;
     uint32_t d = 0;
     bool bad = false;
@@ -555,14 +551,14 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
       const uint32_t sa = shape[cur];
       const uint32_t ea = sa < n_shapes ? dep_ep[sa] : NONE;
       const uint64_t el = sig_elem(ea, kind[cur] == KIND_SERVER, seed);
-      acc = acc * SIG_M + el;
-      pacc = d == 1 ? el : pacc * SIG_M + el;
+      acc = sig_step(acc, el);
+      pacc = d == 1 ? el : sig_step(pacc, el);
     }
     if (bad) continue;
-    const uint64_t sg = sig_final(acc, d, seed), psig = a == NONE ? ROOT_SIG : sig_final(pacc, d - 1, seed);
+    const uint64_t sg = sig_final(acc, d, seed, &flags), psig = a == NONE ? ROOT_SIG : sig_final(pacc, d - 1, seed, &flags);
     int r = 0;
     for (uint32_t t = 0; t < 1u << 20 && r == 0; ++t)
-      r = chain_put(ctab, ccap, sg, psig, epon_of(es, on), &flags, gpos, gcap, counters);
+      r = chain_put(ctab, ccap, sg, psig, &flags, gpos, gcap, counters);
     if (r <= 0) continue;
     if (on) {  // a row: its relations, keys (new chain) and non-SERVER ancestors
       uint32_t kk = 0;
@@ -620,6 +616,17 @@ namespace kmz {
 
 uint32_t chain_grid(uint32_t n) { return std::min<uint32_t>(chain_tiles(n), CHAIN_WG); }
 
+// per shape: its dependency endpoint and the element hash of a SERVER span of
+// it under this run's seed (the walk's per-slot hash is then one gather)
+__global__ void __launch_bounds__(256) k_chain_etab(const uint32_t *__restrict__ dep_ep, uint32_t n_shapes,
+                                                    uint64_t seed, uint4 *__restrict__ etab) {
+  for (uint32_t s = blockIdx.x * 256 + threadIdx.x; s < n_shapes; s += gridDim.x * 256) {
+    const uint32_t ep = dep_ep[s];
+    const uint64_t el = sig_elem(ep, true, seed);
+    etab[s] = make_uint4(ep, (uint32_t)el, (uint32_t)(el >> 32), 0);
+  }
+}
+
 void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
                   const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
                   uint64_t index_base, uint64_t seed, void *ctab, uint64_t ccap, unsigned long long *trip,
@@ -627,12 +634,14 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint32_t pcap, unsigned int *counters, uint32_t *wg_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
                   uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
-                  uint32_t ablate) {
+                  uint4 *etab, uint32_t ablate) {
   const uint32_t nt = chain_tiles(n);
   if (!nt) return;
   const uint32_t g = chain_grid(n);
   unsigned long long *tab = reinterpret_cast<unsigned long long *>(ctab);
-  hipLaunchKernelGGL(k4_chain, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, dep_ep, n_shapes, n_ep,
+  hipLaunchKernelGGL(k_chain_etab, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_shapes + 255) / 256, 1024))),
+                     dim3(256), 0, s, dep_ep, n_shapes, seed, etab);
+  hipLaunchKernelGGL(k4_chain, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, etab, n_shapes, n_ep,
                      index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
                      scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, ablate);
 }
@@ -656,11 +665,7 @@ __global__ void __launch_bounds__(256) k_chain_clear(unsigned long long *__restr
                                                      const uint32_t *__restrict__ wpos_n, uint32_t nwg,
                                                      const uint32_t *__restrict__ gpos, uint32_t gcap,
                                                      const unsigned int *__restrict__ counters) {
-  auto clear = [&](uint32_t p) {
-    ulonglong2 *e = reinterpret_cast<ulonglong2 *>(ctab + 4 * (uint64_t)p);
-    e[0] = make_ulonglong2(0, 0);
-    e[1] = make_ulonglong2(0, 0);
-  };
+  auto clear = [&](uint32_t p) { *reinterpret_cast<ulonglong2 *>(ctab + 2 * (uint64_t)p) = make_ulonglong2(0, 0); };
   for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
     const uint32_t m = wpos_n[w];
     for (uint32_t x = threadIdx.x; x < m; x += 256) clear(wpos[(uint64_t)w * wcap + x]);

@@ -408,49 +408,81 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
 }
 
-// pass 3: exact duplicate check of one sub-bin: every hashed id is inserted
-// into an LDS open-addressing set with one 64-bit compare-and-swap per probe;
-// a CAS that returns the id itself is a repeated id.  cert_plan keeps every
-// sub-bin at or below 3/4 of the set (typically ~0.4), so probing ends.
-constexpr uint32_t CSLOTS = CERT_SET;
-constexpr int CCT = 512;  // threads per pass-3 workgroup (two per CU with the 64 KB set)
+// pass 3: exact duplicate check of one sub-bin, without probe loops.  Every
+// hashed id goes to bucket (low bits of the hash) of an LDS table of 8-slot
+// buckets: one returning LDS add gives its slot, one store places it; ids
+// past a bucket's 8 slots go to an overflow list.  Equal ids share a bucket,
+// so after one barrier each thread compares the pairs of its buckets' slots,
+// and each overflow id its bucket's slots and the other overflow ids.
+// cert_plan keeps a sub-bin at ~3 ids per bucket (a handful overflow).
+constexpr uint32_t CK_NB = 1024, CK_S = 8;  // buckets, slots per bucket (64 KB)
+constexpr uint32_t CK_OVF = 1024;           // overflow ids (8 KB)
+constexpr int CCT = 512;                    // threads per pass-3 workgroup (two per CU)
+constexpr int CK_PER = 12;                  // ids per thread: sub-bins <= CCT * CK_PER = 6144 (cert_plan)
+static_assert(CCT * CK_PER >= CERT_SET * 3 / 4, "a sub-bin must fit the workgroup's registers");
 __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__restrict__ pool, uint32_t cap,
                                                    const unsigned int *__restrict__ cur, uint32_t cur_stride,
                                                    unsigned int *__restrict__ counters) {
-  __shared__ ulonglong2 set2[CSLOTS / 2];
+  __shared__ ulonglong2 bkt2[CK_NB * CK_S / 2];
+  __shared__ uint32_t bcnt[CK_NB];
+  __shared__ unsigned long long ovf[CK_OVF];
+  __shared__ uint32_t novf;
+  unsigned long long *bkt = reinterpret_cast<unsigned long long *>(bkt2);
   const uint32_t sb = blockIdx.x;
   const uint32_t m = min(cur[(uint64_t)sb * cur_stride], cap);
   if (m == 0) return;
   const unsigned long long *src = pool + (uint64_t)sb * cap;
-  unsigned long long *set = reinterpret_cast<unsigned long long *>(set2);
-  bool dup = false;
-  for (uint32_t e0 = 0; e0 < m; e0 += 8 * CCT) {
-    uint64_t h[8];
+  uint64_t h[CK_PER];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {  // (the first batch is in flight while the set is cleared)
-      const uint32_t e = e0 + q * CCT + threadIdx.x;
-      h[q] = e < m ? src[e] : 0;
-    }
-    if (e0 == 0) {
-      for (uint32_t k = threadIdx.x; k < CSLOTS / 2; k += CCT) set2[k] = make_ulonglong2(0, 0);
-      __syncthreads();
-    }
+  for (int q = 0; q < CK_PER; ++q) {  // every load in flight while the counters are cleared
+    const uint32_t e = q * CCT + threadIdx.x;
+    h[q] = e < m ? src[e] : 0;
+  }
+  for (uint32_t k = threadIdx.x; k < CK_NB; k += CCT) bcnt[k] = 0;
+  if (threadIdx.x == 0) novf = 0;
+  __syncthreads();
+  bool lost = false;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if (h[q] == 0) continue;  // mix64(0) == 0: span id 0, reported as F_ZERO_ID
-      uint32_t pos = (uint32_t)h[q] & (CSLOTS - 1);
-      for (uint32_t z = 0; z < CSLOTS; ++z) {
-        const unsigned long long c = atomicCAS(&set[pos], 0ull, (unsigned long long)h[q]);
-        if (c == 0) break;
-        if (c == h[q]) {
-          dup = true;
-          break;
-        }
-        pos = (pos + 1) & (CSLOTS - 1);
-      }
+  for (int q = 0; q < CK_PER; ++q) {
+    if (h[q] == 0) continue;  // padding (and mix64(0) == 0: span id 0, reported as F_ZERO_ID)
+    const uint32_t b = (uint32_t)h[q] & (CK_NB - 1);
+    const uint32_t slot = atomicAdd(&bcnt[b], 1u);
+    if (slot < CK_S) {
+      bkt[b * CK_S + slot] = h[q];
+    } else {
+      const uint32_t o = atomicAdd(&novf, 1u);
+      if (o < CK_OVF) ovf[o] = h[q];
+      else lost = true;
     }
   }
+  __syncthreads();
+  bool dup = false;
+  // pairs within each bucket's slots
+  for (uint32_t b = threadIdx.x; b < CK_NB; b += CCT) {
+    const uint32_t c = min(bcnt[b], CK_S);
+    uint64_t x[CK_S];
+#pragma unroll
+    for (uint32_t j = 0; j < CK_S; j += 2) {
+      const ulonglong2 v = bkt2[(b * CK_S + j) / 2];
+      x[j] = v.x;
+      x[j + 1] = v.y;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < CK_S; ++i)
+#pragma unroll
+      for (uint32_t j = i + 1; j < CK_S; ++j) dup |= j < c && x[i] == x[j];
+  }
+  // overflow ids: against their bucket's slots and the later overflow ids
+  const uint32_t no = min(novf, CK_OVF);
+  for (uint32_t o = threadIdx.x; o < no; o += CCT) {
+    const uint64_t v = ovf[o];
+    const uint32_t b = (uint32_t)v & (CK_NB - 1);
+#pragma unroll
+    for (uint32_t j = 0; j < CK_S; ++j) dup |= bkt[b * CK_S + j] == v;  // (a full bucket: all 8 slots written)
+    for (uint32_t t = o + 1; t < no; ++t) dup |= ovf[t] == v;
+  }
   if (dup) atomicOr(&counters[C_CERT], CERT_DUP);
+  if (lost) atomicOr(&counters[C_CERT], CERT_OVF);
 }
 
 // ---- MISS parents: semi-join of the missing parent ids against all span ids

@@ -81,8 +81,9 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint32_t pcap, unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
                   uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
-                  uint32_t ablate = 0);
+                  uint4 *etab, uint32_t ablate = 0);
 uint32_t chain_grid(uint32_t n);
+constexpr uint64_t CHAIN_ENTRY_BYTES = 16;  // {sig, parent sig}
 void launch_key_insert(hipStream_t s, const unsigned long long *keys, uint64_t n, unsigned long long *trip,
                        uint64_t tcap, unsigned int *counters);
 void launch_chain_settle(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip, uint64_t tcap,
