@@ -503,6 +503,12 @@ static int run_shape_stats(kmz_ctx *c) {
       launch_k3_reduce(c->stream, n, (uint32_t)Gs, c->index_base, c->k3pool.p, P<uint32_t>(c->k3dir),
                        P<unsigned long long>(c->k3part), S, sg);
     }
+  } else if (Gs <= 1024 && !(c->ablate & 8)) {
+    const uint32_t nb = k3_small_blocks(n);
+    if (ensure(c, c->k3part, (size_t)nb * 6 * Gs * 8) || ensure(c, c->tile_tmp, (size_t)nb * 16)) return KMZ_E_HIP;
+    Timed t(c, KMZ_K_STATS);
+    launch_k3_small(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_shapes,
+                    c->n_status, c->index_base, cnt, nsrv, P<unsigned long long>(c->k3part), P<uint32_t>(c->tile_tmp), sg);
   } else {
     Timed t(c, KMZ_K_STATS);
     launch_stats(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_shapes,

@@ -65,6 +65,13 @@ void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape
                        unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp);
 void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
                       const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp);
+// small key spaces (G <= 1024): per-chunk LDS partials, part = [k3_small_blocks(n)][6][G] u64
+uint32_t k3_small_blocks(uint32_t n);
+void launch_k3_small(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
+                     const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
+                     uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint64_t index_base,
+                     unsigned int *counters, unsigned long long *n_server, unsigned long long *part,
+                     uint32_t *tile_tmp, unsigned long long *grp);
 uint32_t k3_partitions(uint32_t G);
 uint32_t k3_pmax();
 uint64_t k3_pool_bytes(uint32_t n);

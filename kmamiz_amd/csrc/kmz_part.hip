@@ -177,14 +177,19 @@ __global__ void __launch_bounds__(1024) k_tile_sum(const uint32_t *__restrict__ 
 static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32_t>(64, (ntiles + 1023) / 1024 + 0); }
 
 // slice s of partition p: tiles s, s+S, ...  -> part[(s*6 + f) * G + g].
-// Each wave takes sixteen of the slice's tiles at a time and spreads the
-// concatenation of their record runs over its lanes (coalesced 16-byte reads,
-// four per lane in flight).
+// Each wave takes 64 of the slice's tiles at a time (one directory word per
+// lane), scans their run lengths across the lanes, and spreads the
+// concatenation of the runs over its lanes (coalesced 16-byte reads, four per
+// lane in flight); a record finds its run by a binary search over the wave's
+// 64 run starts in LDS.
 constexpr int K3RT = 256;
+constexpr uint32_t K3RB = 64;  // runs per wave batch (one per lane)
 __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
                                                   uint32_t ntiles, uint32_t S, uint32_t G, uint64_t index_base,
                                                   unsigned long long *__restrict__ part) {
   __shared__ unsigned long long a_cnt[K3R], a_s1[K3R], a_s2a[K3R], a_s2b[K3R], a_tsx[K3R], a_fst[K3R];
+  constexpr uint32_t NW = K3RT / 64;
+  __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB];  // per wave: run starts in the batch, pool offsets
   const uint32_t s = blockIdx.x, p = blockIdx.y;
   for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
     a_cnt[k] = a_s1[k] = a_s2a[k] = a_s2b[k] = a_tsx[k] = 0;
@@ -192,55 +197,55 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
   }
   __syncthreads();
   const uint32_t *row = dir + (uint64_t)p * ntiles;
-  constexpr uint32_t NW = K3RT / 64, B = 16, U = 4;
+  constexpr uint32_t U = 4;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t step = (uint64_t)S * NW;  // consecutive tiles of this wave
-  for (uint64_t k0 = (uint64_t)s + (uint64_t)w * S; k0 < ntiles; k0 += step * B) {
-    // the batch's B directory words (wave-uniform) and their run prefix
-    uint32_t o[B], pre[B + 1];
-    pre[0] = 0;
+  for (uint64_t k0 = (uint64_t)s + (uint64_t)w * S; k0 < ntiles; k0 += step * K3RB) {
+    // this lane's run: tile k0 + lane * step
+    const uint64_t k = k0 + lane * step;
+    const uint32_t x = k < ntiles ? row[k] : 0;
+    const uint32_t o = x >> 16;
+    const uint32_t c = (o + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;  // a well-formed directory never exceeds the tile
+    uint32_t incl = c;
 #pragma unroll
-    for (uint32_t j = 0; j < B; ++j) {
-      const uint64_t k = k0 + j * step;
-      const uint32_t x = k < ntiles ? row[k] : 0;
-      o[j] = x >> 16;
-      const uint32_t c = (o[j] + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;  // a well-formed directory never exceeds the tile
-      pre[j + 1] = pre[j] + c;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
     }
-    // the batch's records spread over the lanes, U loads in flight per lane
-    for (uint32_t q0 = 0; q0 < pre[B]; q0 += 64 * U) {
-      Rec x[U];
-      uint64_t kk[U];
+    const uint32_t total = __shfl(incl, 63, 64);
+    r_pre[w][lane] = incl - c;
+    r_off[w][lane] = (uint32_t)(k < ntiles ? k : 0) * K3T + o;  // (ntiles * K3T < 2^32: n < 2^32)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    for (uint32_t q0 = 0; q0 < total; q0 += 64 * U) {
+      Rec xr[U];
+      uint32_t run[U];
       bool v[U];
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
         const uint32_t q = q0 + u * 64 + lane;
-        v[u] = q < pre[B];
-        uint32_t ob = o[0], pb = 0;
-        uint64_t kb = k0;
+        v[u] = q < total;
+        uint32_t j = 0;  // the last run starting at or before q
 #pragma unroll
-        for (uint32_t t = 1; t < B; ++t)  // the run holding record q (selects, no indexing)
-          if (q >= pre[t]) {
-            ob = o[t];
-            pb = pre[t];
-            kb = k0 + t * step;
-          }
-        kk[u] = kb;
-        x[u] = pool[v[u] ? kb * K3T + ob + (q - pb) : 0];
+        for (uint32_t b = 32; b; b >>= 1)
+          if (r_pre[w][j + b] <= q) j += b;
+        run[u] = j;
+        xr[u] = pool[v[u] ? r_off[w][j] + (q - r_pre[w][j]) : 0];
       }
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
         if (!v[u]) continue;
-        const uint32_t kl = x[u].w & (K3R - 1);
-        const uint64_t d = x[u].d, dd = d * d;
+        const uint32_t kl = xr[u].w & (K3R - 1);
+        const uint64_t d = xr[u].d, dd = d * d;
         atomicAdd(&a_cnt[kl], 1ull);
         atomicAdd(&a_s1[kl], (unsigned long long)d);
         atomicAdd(&a_s2a[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
         atomicAdd(&a_s2b[kl], (unsigned long long)(dd >> 32));
-        atomicMax(&a_tsx[kl], (unsigned long long)x[u].tsx);
-        atomicMin(&a_fst[kl], (unsigned long long)(index_base + kk[u] * K3T + (x[u].w >> 10)));
+        atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
+        atomicMin(&a_fst[kl], (unsigned long long)(index_base + (k0 + run[u] * step) * K3T + (xr[u].w >> 10)));
       }
     }
+    __builtin_amdgcn_wave_barrier();  // r_pre / r_off are rewritten by the next batch
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
@@ -276,6 +281,117 @@ __global__ void __launch_bounds__(256) k3_combine(const unsigned long long *__re
     grp[4ull * G + g] = tsx;
     grp[5ull * G + g] = fst;
   }
+}
+
+// ===========================================================================
+// K3S: (endpoint x status) reduction for small key spaces (G <= 1024, e.g.
+// Bookinfo's 18 groups): every workgroup reduces one contiguous chunk in LDS
+// (one copy of the accumulators per wave while G <= 256, so lanes only
+// contend within their wave) and writes its partials; no global atomics, no
+// shared counter (a per-wave atomic on one n_server word serialises ~4k
+// waves).  k3_combine_small folds the chunks: one workgroup per group.
+// ===========================================================================
+constexpr int KS_T = 256;
+__global__ void __launch_bounds__(KS_T) k3_small(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
+                                                 const uint16_t *__restrict__ status, const uint32_t *__restrict__ dur,
+                                                 const int64_t *__restrict__ ts, uint32_t n, uint32_t chunk,
+                                                 const uint32_t *__restrict__ ep_of_shape, uint32_t n_shapes,
+                                                 uint32_t n_ep, uint32_t n_status, uint64_t index_base,
+                                                 uint32_t copies, unsigned int *__restrict__ counters,
+                                                 unsigned long long *__restrict__ part,
+                                                 uint32_t *__restrict__ wg_servers) {
+  extern __shared__ unsigned long long sm[];
+  __shared__ uint32_t wsrv[KS_T / 64];
+  const uint32_t G = n_ep * n_status;
+  for (uint32_t k = threadIdx.x; k < copies * 6 * G; k += KS_T) sm[k] = (k / G) % 6 == 5 ? ~0ull : 0ull;
+  __syncthreads();
+  unsigned long long *a = sm + (copies > 1 ? (threadIdx.x >> 6) : 0) * 6 * G;
+  const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+  const uint32_t end = (uint32_t)min<uint64_t>(c0 + chunk, n);
+  uint32_t servers = 0, flags = 0;
+  for (uint32_t i = (uint32_t)c0 + threadIdx.x; i < end; i += KS_T) {
+    if (kind[i] != KIND_SERVER) continue;
+    ++servers;
+    const uint32_t sh = shape[i], st = status[i];
+    const uint32_t ep = sh < n_shapes ? (ep_of_shape ? ep_of_shape[sh] : sh) : NONE;  // null map: by shape
+    if (ep >= n_ep || st >= n_status) {
+      flags |= F_RANGE;
+      continue;
+    }
+    const uint32_t g = ep * n_status + st;
+    const uint64_t d = dur[i], dd = d * d;
+    atomicAdd(&a[g], 1ull);
+    atomicAdd(&a[G + g], (unsigned long long)d);
+    atomicAdd(&a[2 * G + g], (unsigned long long)(dd & 0xFFFFFFFFull));
+    atomicAdd(&a[3 * G + g], (unsigned long long)(dd >> 32));
+    atomicMax(&a[4 * G + g], (unsigned long long)((uint64_t)ts[i] ^ TS_BIAS));
+    atomicMin(&a[5 * G + g], (unsigned long long)(index_base + i));
+  }
+  if (flags) atomicOr(&counters[C_FLAGS], flags);
+  for (int o = 32; o > 0; o >>= 1) servers += __shfl_xor(servers, o, 64);
+  if ((threadIdx.x & 63) == 0) wsrv[threadIdx.x >> 6] = servers;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < KS_T / 64; ++w) t += wsrv[w];
+    wg_servers[blockIdx.x] = t;
+  }
+  for (uint32_t k = threadIdx.x; k < 6 * G; k += KS_T) {
+    const uint32_t f = k / G;
+    unsigned long long v = sm[k];
+    for (uint32_t c = 1; c < copies; ++c) {
+      const unsigned long long x = sm[c * 6 * G + k];
+      v = f < 4 ? v + x : (f == 4 ? max(v, x) : min(v, x));
+    }
+    part[(uint64_t)blockIdx.x * 6 * G + k] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) k3_combine_small(const unsigned long long *__restrict__ part, uint32_t S,
+                                                        uint32_t G, unsigned long long *__restrict__ grp) {
+  __shared__ unsigned long long red[4][6];
+  const uint32_t g = blockIdx.x;
+  unsigned long long v[6] = {0, 0, 0, 0, 0, ~0ull};
+  for (uint32_t s = threadIdx.x; s < S; s += 256) {
+    const unsigned long long *b = part + (uint64_t)s * 6 * G + g;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) v[f] += b[(uint64_t)f * G];
+    v[4] = max(v[4], b[4ull * G]);
+    v[5] = min(v[5], b[5ull * G]);
+  }
+#pragma unroll
+  for (int f = 0; f < 6; ++f)
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long y = __shfl_xor(v[f], o, 64);
+      v[f] = f < 4 ? v[f] + y : (f == 4 ? max(v[f], y) : min(v[f], y));
+    }
+  if ((threadIdx.x & 63) == 0)
+    for (int f = 0; f < 6; ++f) red[threadIdx.x >> 6][f] = v[f];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int f = threadIdx.x;
+    unsigned long long r = red[0][f];
+    for (int w = 1; w < 4; ++w) r = f < 4 ? r + red[w][f] : (f == 4 ? max(r, red[w][f]) : min(r, red[w][f]));
+    grp[(uint64_t)f * G + g] = r;
+  }
+}
+
+uint32_t k3_small_blocks(uint32_t n) { return std::max<uint32_t>(1, std::min<uint32_t>(1024, (n + 1023) / 1024)); }
+
+void launch_k3_small(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
+                     const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
+                     uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint64_t index_base,
+                     unsigned int *counters, unsigned long long *n_server, unsigned long long *part,
+                     uint32_t *tile_tmp, unsigned long long *grp) {
+  const uint32_t G = n_ep * n_status;
+  if (!n || !G) return;
+  const uint32_t nb = k3_small_blocks(n), chunk = (n + nb - 1) / nb;
+  const uint32_t copies = G <= 256 ? KS_T / 64 : 1;
+  hipLaunchKernelGGL(k3_small, dim3(nb), dim3(KS_T), (size_t)copies * 6 * G * 8, s, kind, shape, status, dur, ts, n,
+                     chunk, ep_of_shape, n_shapes, n_ep, n_status, index_base, copies, counters, part, tile_tmp);
+  hipLaunchKernelGGL(k3_combine_small, dim3(G), dim3(256), 0, s, part, nb, G, grp);
+  hipLaunchKernelGGL(k_tile_sum, dim3(std::max<uint32_t>(1, tile_sum_blocks(nb))), dim3(1024), 0, s, tile_tmp, nb, 1u, 1u,
+                     n_server, 99u);
 }
 
 void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
