@@ -13,6 +13,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkmz.so")
+if os.environ.get("KMZ_LIB_VARIANT"):  # diagnostic A/B builds (tools/variant.sh): libkmz_<variant>.so, in-tree
+    LIB_PATH = os.path.join(_HERE, "libkmz_%s.so" % os.environ["KMZ_LIB_VARIANT"])
 
 KIND_OTHER, KIND_SERVER, KIND_CLIENT = 0, 1, 2
 NONE32 = 0xFFFFFFFF

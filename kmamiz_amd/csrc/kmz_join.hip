@@ -35,8 +35,10 @@ constexpr uint32_t JT = 2048, JH = 256, JW = JT + 2 * JH, JTT = 512;
 static_assert(JW < 4096, "local index + 1 must fit an entry's 12 bits");
 constexpr uint16_t L_NONE = 0xFFFF, L_MISS = 0xFFFE;
 constexpr uint32_t CERT_B1 = 6, CERT_BINS = 1u << CERT_B1;
-constexpr uint32_t CERT_CHUNK = 8192;  // records per pass-2 workgroup (LDS staging)
-constexpr uint32_t CERT_TPC = 192;     // tiles per pass-2 workgroup: ~6144 records of one bin
+#ifndef KMZ_CERT_PQ
+#define KMZ_CERT_PQ 8
+#endif
+constexpr uint32_t CERT_PQ = KMZ_CERT_PQ;  // pass 2: records per thread (chunks of PQ * 1024 records of one bin)
 constexpr uint32_t CERT_SET = 8192;    // pass-3 LDS set (u64), sub-bins <= 6144 records
 
 
@@ -319,13 +321,16 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) pool1[(uint64_t)t0 + e] = stg[e];
 }
 
-// pass 2: for one bin, the runs of CERT_TPC tiles -> 2^B2 sub-bins (dynamic
-// LDS: CERT_CHUNK u64 staging + 2 * 2^B2 u32)
+// pass 2: for one bin, the runs of TPC tiles -> 2^B2 sub-bins (dynamic LDS:
+// PQ * 1024 u64 staging + 2 * 2^B2 u32).  (PQ = 16, i.e. runs twice as long
+// per sub-bin, measured slower: 0.59 against 0.55 ms on config 3.)
+template <int PQ>
 __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *__restrict__ pool1,
                                                      const uint16_t *__restrict__ jdir, uint32_t n, uint32_t chunks,
                                                      uint32_t B2, unsigned long long *__restrict__ pool2,
                                                      uint32_t cap2, unsigned int *__restrict__ cur2,
                                                      unsigned int *__restrict__ counters) {
+  constexpr uint32_t CERT_CHUNK = PQ * 1024, CERT_TPC = PQ * 24;  // ~32 ids per tile run at 64 bins
   extern __shared__ uint64_t dyn[];
   __shared__ uint32_t wsum[16], tcnt[CERT_TPC], toff[CERT_TPC];
   uint64_t *stg = dyn;
@@ -359,7 +364,6 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   // gather the chunk's records straight into registers: record e belongs to
   // the last tile whose run starts at or before e (binary search in LDS);
   // every load is in flight before any is used
-  constexpr int PQ = CERT_CHUNK / 1024;
   uint64_t h[PQ];
   uint32_t rk[PQ];
 #pragma unroll
@@ -597,7 +601,7 @@ bool cert_plan(uint32_t n, CertPlan *pl) {
   const double mean2 = (double)n / ((uint64_t)CERT_BINS << B2);
   pl->B2 = B2;
   pl->cap2 = (uint32_t)(mean2 * 1.15) + 256;
-  pl->chunks = (join_tiles(n) + CERT_TPC - 1) / CERT_TPC;
+  pl->chunks = (join_tiles(n) + CERT_PQ * 24 - 1) / (CERT_PQ * 24);
   return pl->cap2 <= CERT_SET * 3 / 4;
 }
 
@@ -616,9 +620,9 @@ void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const 
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
                        const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters) {
   if (!n) return;
-  const size_t lds = CERT_CHUNK * 8 + (size_t)2 * (1u << pl.B2) * 4;
-  hipLaunchKernelGGL(k_cert_split, dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n, pl.chunks, pl.B2,
-                     pool2, pl.cap2, cur2, counters);
+  const size_t lds = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B2) * 4;
+  hipLaunchKernelGGL(k_cert_split<CERT_PQ>, dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n, pl.chunks,
+                     pl.B2, pool2, pl.cap2, cur2, counters);
 }
 
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
