@@ -106,6 +106,16 @@ __device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
   return m;
 }
 
+__device__ unsigned long long g_join_dbg[16];  // diagnostic phase clocks (KMZ_ABLATE bit 23 only)
+#define KMZ_JSTAMP(k)                                           \
+  if (dbg_t) {                                                  \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && tprev) tacc[k] += t_ - tprev;       \
+    tprev = t_;                                                 \
+  }
+
+// (A persistent form of this kernel, the next tile's window loaded while the
+// current tile contracts and bins, measured 1.62 against 1.18 ms on config 3.)
 __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
                                                      const uint8_t *__restrict__ kind, uint32_t n,
                                                      uint32_t *__restrict__ cparent, uint32_t *__restrict__ dp,
@@ -124,6 +134,9 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   constexpr int PW = JW / JTT, PT = JT / JTT;
   const uint32_t t0 = blockIdx.x * JT, t1 = min(n, t0 + JT);
   const uint32_t w0 = t0 > JH ? t0 - JH : 0, w1 = min(n, t1 + JH);
+  const bool dbg_t = (ablate & (1u << 23)) != 0;
+  unsigned long long tprev = 0, tacc[6] = {0, 0, 0, 0, 0, 0};
+  KMZ_JSTAMP(0);
   for (uint32_t k = threadIdx.x; k < JB; k += JTT) {
     lbkt[k] = make_uint4(0, 0, 0, 0);
     lcnt[k] = 0;
@@ -156,6 +169,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
     }
   }
   __syncthreads();
+  KMZ_JSTAMP(0);
   bool ovf = false;
   if (!(ablate & 256)) {  // insert: the emptier of the two buckets, else the other, else the stash
 #pragma unroll
@@ -182,6 +196,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
     }
   }
   __syncthreads();
+  KMZ_JSTAMP(1);
   const uint32_t ns = min(nstash, JSTASH);
   // window parents: tile spans, and CLIENT spans of the halo (chains pass through them)
 #pragma unroll
@@ -223,6 +238,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   }
   if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
   __syncthreads();
+  KMZ_JSTAMP(2);
   // tile: CLIENT contraction inside the window (Traces.ts:131-137), lockstep
   uint32_t miss = 0, pend = 0, zero = 0;
   uint64_t hv[PT];
@@ -287,6 +303,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
     if (pend) atomicAdd(&counters[C_PEND], pend);
     if (zero) atomicOr(&counters[C_FLAGS], F_ZERO_ID);
   }
+  KMZ_JSTAMP(3);
   if (ablate & 64) return;  // diagnostic: no certificate pass 1
   // certificate pass 1: the tile's hashed ids into 64 bins.  Ranks come from
   // wave ballots and per-wave counters (no LDS atomics on 64 hot words).
@@ -319,6 +336,9 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   }
   __syncthreads();
   for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) pool1[(uint64_t)t0 + e] = stg[e];
+  KMZ_JSTAMP(4);
+  if (dbg_t && threadIdx.x == 0)
+    for (int kk = 0; kk < 5; ++kk) atomicAdd(&g_join_dbg[kk], tacc[kk]);
 }
 
 // pass 2: for one bin, the runs of TPC tiles -> 2^B2 sub-bins (dynamic LDS:
@@ -648,3 +668,12 @@ void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_
 }
 
 }  // namespace kmz
+
+extern "C" int kmz__debug_join(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmz::g_join_dbg), sizeof(kmz::g_join_dbg)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(kmz::g_join_dbg), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
