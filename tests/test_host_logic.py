@@ -236,3 +236,27 @@ def test_historical_data_mirror_matches_oracle_on_many_minutes():
     got = CombinedRealtimeDataList(copy.deepcopy(rows)).toHistoricalData(deps, _fx("MockReplicas"))
     assert len(got) >= 5  # (the range starts 20 s into a minute)
     assert got == exp
+
+
+@pytest.mark.parametrize("config,ntr", [(2, 3000), (3, 800), (5, 600)])
+def test_openmp_baseline_matches_sequential_oracle(config, ntr):
+    """oracle/kmz_cpu_omp.c (bench.py's all-core cpu_baseline) computes the
+    same results as the sequential C oracle: integers exactly, latency
+    statistics within the north_star's 1e-9."""
+    from kmamiz_amd import synth
+    from oracle import c_oracle
+
+    b, _ = synth.host_batch(config, 5, 5 + ntr)
+    t = synth.shape_table(config)
+    o = c_oracle.stats(b, t.tag_ep, t.n_tag_ep, t.n_status)
+    p = c_oracle.omp_stats(b, t.tag_ep, t.n_tag_ep, t.n_status)
+    for k in ("combined", "first", "latest_timestamp"):
+        assert np.array_equal(o[k], p[k]), k
+    used = o["combined"] > 0
+    np.testing.assert_allclose(p["mean"][used], o["mean"][used], rtol=1e-9, atol=0)
+    np.testing.assert_allclose(p["cv"][used], o["cv"][used], rtol=1e-9, atol=1e-13)
+    k1, e1, c1 = c_oracle.deps(b, t.dep_ep, t.n_dep_ep)
+    k2, e2, c2 = c_oracle.omp_deps(b, t.dep_ep, t.n_dep_ep)
+    assert np.array_equal(k1, k2) and c1 == c2
+    for k in e1:
+        assert np.array_equal(e1[k], e2[k]), k
