@@ -42,19 +42,41 @@ def alg_bytes(kernel, n, n_server, relations, n_keys=0):
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-TRAFFIC_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic_mesh100M.json")
+PROFILES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+
+
+def build_id() -> str:
+    """Digest of the engine's sources (kernels, ABI, headers): which build a
+    committed PMC traffic figure was measured on."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha1()
+    root = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(root, "kmamiz_amd", "csrc", "*")) + [os.path.join(root, "include", "kmz.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:12]
 
 
 def traffic_of(kernel, config, n_local):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
-    (tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE), when this run is the
-    workload they were measured on (mesh, ~1e8 spans); else None."""
-    from kmamiz_amd import synth
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC pass
+    (tools/traffic.sh -> profiles/traffic_*.json: 2 x FETCH_SIZE + WRITE_SIZE)
+    of THIS build on this workload; else None (never a stale build's figure)."""
+    import glob
 
-    if config != synth.MESH or abs(n_local - 1e8) > 2e6 or not os.path.exists(TRAFFIC_FILE):
-        return None
-    k = json.load(open(TRAFFIC_FILE)).get("kernels", {}).get(kernel)
-    return k["traffic_bytes"] if k else None
+    bid = build_id()
+    for f in sorted(glob.glob(os.path.join(PROFILES, "traffic_*.json")), reverse=True):
+        try:
+            t = json.load(open(f))
+        except Exception:
+            continue
+        if t.get("build") != bid or t.get("config") != config or abs(t.get("n_spans", 0) - n_local) > 0.02 * n_local:
+            continue
+        k = t.get("kernels", {}).get(kernel)
+        return (k["traffic_bytes"], os.path.basename(f)) if k else None
+    return None
 
 
 def parse():
@@ -70,6 +92,7 @@ def parse():
                     help="strong: --spans is the job's total, sharded by h(traceId) mod N; weak: --spans per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-fetch", action="store_true", help="leave results on the device")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the host-to-device copy timing of the batch")
     ap.add_argument("--tail", choices=["auto", "on", "off"], default="auto",
                     help="service-level tail (instability/coupling/cohesion/risk) in every step; auto = config 5")
     return ap.parse_args()
@@ -251,6 +274,27 @@ def main():
     kname = {"join": "k_join_window", "stats": "k3_produce" if "reduce" in per_kernel else "k_stats",
              "reduce": "k3_reduce", "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check",
              "tail": "k_tail_links"}[dom]
+    tr = traffic_of(kname, config, n_local)
+    h2d = None
+    if rank == 0 and not args.no_h2d:
+        # the kmz_spans columns (35 B/span) from pinned host memory, as kmz_load
+        # copies a host-parsed batch: reported beside the device-resident rate
+        nbytes = 35 * n_local
+        host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        devb = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        devb.copy_(host, non_blocking=True)
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        devb.copy_(host, non_blocking=True)
+        ev1.record()
+        torch.cuda.synchronize()
+        h2d_ms = ev0.elapsed_time(ev1)
+        step_ms = secs / args.steps * 1e3
+        h2d = {"bytes": nbytes, "ms": round(h2d_ms, 3), "GB_per_s": round(nbytes / (h2d_ms * 1e-3) / 1e9, 1),
+               "pcie_inclusive_spans_per_s": round(n_local / ((h2d_ms + step_ms) * 1e-3), 1),
+               "note": "35 B/span kmz_spans columns, pinned host -> HBM, one GPU; not part of `value`"}
+        del host, devb
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0:
@@ -291,12 +335,15 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(d["gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": traffic_of(kname, config, n_local),
+                "traffic": (tr[0] if tr else None),
+                "traffic_source": (f"profiles/{tr[1]} (build {build_id()})" if tr else
+                                   f"no PMC pass of build {build_id()} on this workload committed"),
                 "pipeline_gbs": round(pipe_bytes / (kern_ms * 1e-3) / 1e9, 1),
                 "kernel_ms_per_step": round(kern_ms, 4),
                 "kernels": per_kernel,
             },
             "cpu_baseline": cpu,
+            "h2d": h2d,
         }
         print(json.dumps(line))
     eng.close()
