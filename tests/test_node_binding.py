@@ -161,3 +161,49 @@ def test_node_service_tail_vs_oracle(src, tmp_path):
         assert (g["totalEndpoints"], g["consumers"]) == (h["totalEndpoints"], len(h["consumers"]))
         assert g["endpointUsageCohesion"] == pytest.approx(h["endpointUsageCohesion"], rel=1e-9)
         assert g["relyingFactor"] == pytest.approx(rf[g["uniqueServiceName"]], rel=1e-9)
+
+
+def test_addon_loads_in_worker_threads():
+    """The realtime step runs in a worker_threads Worker in the reference
+    (RealtimeWorkerImpl.ts:29-84, ServiceOperator.ts:57-64): the addon must be
+    context-aware.  Four Workers load kmz.node (through js/realtime_worker.js)
+    at once."""
+    r = subprocess.run([NODE, "js/worker_seam_run.js", os.path.join(FIX, "MockTrace.json"), "4", "load"], cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout) == {"loaded": 4}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src", ["MockTrace", "mesh"])
+def test_worker_threads_run_the_path_concurrently(src, tmp_path):
+    """Two (and four) Workers, each with its own engine context on the GPU,
+    run the worker step on the same batch at the same time (half from
+    objects, half from the raw JSON bytes); every answer equals the oracle."""
+    if src == "mesh":
+        from kmamiz_amd import synth
+
+        batch, off = synth.host_batch(3, 0, 300)
+        traces = synth.to_traces(3, batch, off)
+    else:
+        traces = fixture(src)
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(traces))
+    ref = O.Traces(traces)
+    exp_deps = O.strip_undef(ref.toEndpointDependencies().toJSON())
+    exp_rl = O.strip_undef(ref.combineLogsToRealtimeData([]).toCombinedRealtimeData().toJSON())
+    for nw in (2, 4):
+        r = subprocess.run([NODE, "js/worker_seam_run.js", str(p), str(nw), "gpu"], cwd=ROOT, capture_output=True,
+                           text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        res = json.loads(r.stdout)["results"]
+        assert len(res) == nw
+        for x in res:
+            assert "error" not in x, x.get("error")
+            assert x["dependencies"] == exp_deps
+            got = x["rlDataList"]
+            assert [(g["uniqueEndpointName"], g["status"], g["combined"], g["latestTimestamp"]) for g in got] == \
+                [(e["uniqueEndpointName"], e["status"], e["combined"], e["latestTimestamp"]) for e in exp_rl]
+            for a, b in zip(got, exp_rl):
+                assert a["latency"]["mean"] == pytest.approx(b["latency"]["mean"], rel=1e-9)
+                assert a["latency"]["cv"] == pytest.approx(b["latency"]["cv"], rel=1e-9, abs=1e-13)
