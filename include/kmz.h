@@ -74,6 +74,7 @@ extern "C" {
 #define KMZ_RUN_STATS_TAG 2u /* group by combineLogsToRealtimeData identity (Traces.ts:73-99) */
 #define KMZ_RUN_DEPS 4u      /* dependency graph (Traces.ts:112-211) */
 #define KMZ_RUN_SPAN_LINKS 8u/* keep per-span links for kmz_get_span_links */
+#define KMZ_RUN_DEP_ORDER 16u /* with DEPS: the entry order of the reduced graph (kmz_get_dep_entries) */
 
 /* where a kmz_load buffer lives */
 #define KMZ_MEM_HOST 0
@@ -199,6 +200,35 @@ int kmz_get_span_links(kmz_ctx *ctx, uint32_t *cparent, uint64_t *rowpos, uint64
  * Pinned (page-locked) output buffers copy fastest. */
 int kmz_fetch(kmz_ctx *ctx, kmz_group *groups, uint64_t groups_cap, uint64_t *triples, uint64_t triples_cap,
               uint64_t *n_triples, kmz_endpoint *endpoints, uint64_t endpoints_cap);
+
+/* ---- reduced graph in exact order ------------------- */
+/* The cache layer holds EndpointDependencies reduced to one merged row per
+ * endpoint: EndpointDependencies([]).combineWith(traces.toEndpointDependencies())
+ * .trim() (EndpointDependencies.ts:91-112, 499-542; Initializer.ts:92,
+ * RealtimeWorkerImpl.ts:68-70, Cacheable/CEndpointDependencies.ts:46-48).
+ * After kmz_run(KMZ_RUN_DEPS | KMZ_RUN_DEP_ORDER), one record per entry of it:
+ *   key   anc_ep<<40 | desc_ep<<16 | distance<<1 | side
+ *         side 0: a dependingBy entry of desc_ep's merged row (type CLIENT),
+ *         side 1: a dependingOn entry of anc_ep's merged row (type SERVER)
+ *   row   global first-occurrence index of the row that brought the entry
+ *         into the merged row (the endpoint's first row having it)
+ *   pos   its place in that row's list: side 1 the first descendant row's
+ *         index (lowerMap insertion order); side 0 = row (upperMap is in
+ *         distance order)
+ *   span  global index of the span whose ToEndpointInfo the entry carries
+ *         (side 0: the ancestor; side 1: the LAST descendant with the key)
+ *   ts / shape of that span
+ * A merged row lists its entries by (row, pos) for side 1 and (row, distance)
+ * for side 0.  row_ts / row_shape[e]: the span of endpoint e's first row
+ * (the merged row's `endpoint`; INT64_MIN / KMZ_NONE without a row).
+ * out == NULL: *n_out only.  Records come in no particular order. */
+typedef struct kmz_dep_entry {
+  uint64_t key, row, span, pos;
+  int64_t ts;
+  uint32_t shape, pad;
+} kmz_dep_entry;
+int kmz_get_dep_entries(kmz_ctx *ctx, kmz_dep_entry *out, uint64_t cap, uint64_t *n_out, int64_t *row_ts,
+                        uint32_t *row_shape, uint64_t row_cap);
 
 /* ---- multi-GPU partials (traceId-sharded batches) ------------------------ */
 /* Raw group partials: 6 arrays of n_groups u64, in this order:
@@ -327,7 +357,8 @@ void kmz_host_free(void *p);
 #define KMZ_K_CHECK 11   /* uniqueness certificate pass 3 (k_cert_check)          */
 #define KMZ_K_SETTLE 12  /* K4 k_chain_settle: staged keys + deferred chain checks */
 #define KMZ_K_TAIL 13    /* service tail: k_tail_links + k_tail_compact           */
-#define KMZ_K_COUNT 14
+#define KMZ_K_ORDER 14   /* entry order of the reduced graph (KMZ_RUN_DEP_ORDER)  */
+#define KMZ_K_COUNT 15
 int kmz_set_profiling(kmz_ctx *ctx, int on);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);

@@ -20,7 +20,7 @@ KIND_OTHER, KIND_SERVER, KIND_CLIENT = 0, 1, 2
 NONE32 = 0xFFFFFFFF
 NONE64 = 0xFFFFFFFFFFFFFFFF
 
-RUN_STATS_RT, RUN_STATS_TAG, RUN_DEPS, RUN_SPAN_LINKS = 1, 2, 4, 8
+RUN_STATS_RT, RUN_STATS_TAG, RUN_DEPS, RUN_SPAN_LINKS, RUN_DEP_ORDER = 1, 2, 4, 8, 16
 MEM_HOST, MEM_DEVICE = 0, 1
 
 ERRORS = {
@@ -35,7 +35,7 @@ ERRORS = {
 }
 
 KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final", "join", "cert", "reduce", "pend", "check",
-           "settle", "tail"]
+           "settle", "tail", "order"]
 SYNTH_BOOKINFO, SYNTH_MESH, SYNTH_POWER = 2, 3, 5
 PART_GROUPS, PART_ENDPOINTS, PART_TRIPLES = 0, 1, 2
 
@@ -101,6 +101,9 @@ GROUP_DTYPE = np.dtype(
     [("combined", "<u8"), ("first", "<u8"), ("latest_timestamp", "<i8"), ("mean", "<f8"), ("cv", "<f8")]
 )
 ENDPOINT_DTYPE = np.dtype([("last_ts", "<i8"), ("first_row", "<u8"), ("external", "<u4"), ("has_row", "<u4")])
+# kmz_dep_entry: one entry of the reduced graph with its order (kmz.h)
+DEP_ENTRY_DTYPE = np.dtype([("key", "<u8"), ("row", "<u8"), ("span", "<u8"), ("pos", "<u8"), ("ts", "<i8"),
+                            ("shape", "<u4"), ("pad", "<u4")])
 TAIL_DETAIL_DTYPE = np.dtype([("svc", "<u4"), ("lsvc", "<u4"), ("distance", "<u4"), ("count", "<u4"),
                               ("depending_by", "<u4"), ("depending_on", "<u4")])
 TAIL_PAIR_DTYPE = np.dtype([("svc", "<u4"), ("consumer", "<u4"), ("consumes", "<u4")])
@@ -154,6 +157,7 @@ SIGNATURES = [
     ("kmz_get_endpoints", C.c_int, [_P, _P, C.c_uint64]),
     ("kmz_get_triples", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("kmz_get_span_links", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("kmz_get_dep_entries", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, _P, C.c_uint64]),
     ("kmz_fetch", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64]),
     ("kmz_group_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_endpoint_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),

@@ -145,7 +145,7 @@ class Traces:
     def toEndpointDependencies(self) -> "EndpointDependencies":
         """Traces.ts:112-211 on the GPU; objects are materialised lazily."""
         eng = self._load()
-        eng.run(L.RUN_DEPS | L.RUN_SPAN_LINKS)
+        eng.run(L.RUN_DEPS | L.RUN_SPAN_LINKS | L.RUN_DEP_ORDER)
         return EndpointDependencies(_native=_DepResult(self, eng))
 
     @staticmethod
@@ -402,7 +402,8 @@ def _pooled(n1, m1, c1, n2, m2, c2):
     sa, sb = c1 * a, c2 * b
     tot = n1 + n2
     mt = (n1 * a + n2 * b) / tot
-    pv = (n1 * sa ** 2 + n2 * sb ** 2 + n1 * (a - mt) ** 2 + n2 * (b - mt) ** 2) / tot
+    da, db = a - mt, b - mt  # (x ** 2 is Math.pow(x, 2) = x * x in V8's fdlibm pow)
+    pv = (n1 * (sa * sa) + n2 * (sb * sb) + n1 * (da * da) + n2 * (db * db)) / tot
     return mt * scale, (0 if mt == 0 else math.sqrt(pv) / mt)
 
 
@@ -570,6 +571,7 @@ class _DepResult:
         self.triples = eng.triples()
         self.info = eng.info()
         self.index_base = eng.index_base
+        self.order = eng.dep_entries()
         for e in d.poison["dep"]:
             if self.endpoints["has_row"][e] or np.any((self.triples >> np.uint64(40)) == np.uint64(e)):
                 raise self._poison_error(e)
@@ -580,6 +582,16 @@ class _DepResult:
             if d.shape_ep["dep"][b.shape[i]] == e:
                 return d.shape_ident["dep"][b.shape[i]].error
         return TypeError("ExplodeUrl failed")
+
+    def reduced_graph(self, reg=None):
+        """cache.ReducedDependencies of EndpointDependencies([]).combineWith(rows).trim()
+        from the engine's entry order (kmz_get_dep_entries), no per-span work."""
+        from .cache import ReducedDependencies
+
+        entries, rts, rsh = self.order
+        idents = self.dict.shape_ident["dep"]
+        return ReducedDependencies.from_window(entries, rts, rsh, self.endpoints, self.dict.ep_names["dep"],
+                                               lambda s: idents[s].fields, reg)
 
     def info_of(self, i: int) -> dict:
         f = self.dict.shape_ident["dep"][self.batch.shape[i]].fields
@@ -666,6 +678,15 @@ class EndpointDependencies:
         eng = traces._load()
         eng.run(L.RUN_DEPS)
         return run_tail(eng, maps_from_dictionary(self._native.dict, labelMap), eng.endpoints())
+
+    def toReduced(self, reg=None):
+        """Columns of ``EndpointDependencies([]).combineWith(self).trim()``
+        (cache.ReducedDependencies, the form the dependency cache keeps)."""
+        from .cache import ReducedDependencies
+
+        if self._native is not None and self._deps is None:
+            return self._native.reduced_graph(reg)
+        return ReducedDependencies.from_json(self._list(), merge_rows=True, reg=reg)
 
     def trim(self):
         """EndpointDependencies.ts:91-112."""

@@ -59,6 +59,8 @@ struct kmz_ctx {
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n, cetab;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
+  DevBuf o_key, o_a, o_b, o_val, o_out, o_rts, o_rsh;  // reduced-graph entry order (kmz_order.hip)
+  uint64_t o_n = 0;
   DevBuf imap_l, imap_g;  // local -> global flatten-index runs of a non-contiguous shard (kmz_shard.hip)
   uint64_t imap_n = 0;     // 0: contiguous batch (index_base + i)
   DevBuf ctile;           // K4 per-workgroup stats (apart from K3's tile_tmp: the two run concurrently)
@@ -289,7 +291,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
-                    &c->tl_sstat, &c->tl_rel};
+                    &c->tl_sstat, &c->tl_rel, &c->o_key, &c->o_a, &c->o_b, &c->o_val, &c->o_out,
+                    &c->o_rts, &c->o_rsh};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->hpin) hipHostFree(c->hpin);
@@ -656,6 +659,67 @@ static int run_stats(kmz_ctx *c, uint32_t mode) {
   return KMZ_OK;
 }
 
+// Entry order of the reduced graph (kmz_order.hip): after a successful
+// dependency run with span links; synchronous (the record count sizes the
+// index remap of a non-contiguous shard).
+static int run_dep_order(kmz_ctx *c, uint64_t n_keys, bool dups) {
+  const uint32_t n = (uint32_t)c->n;
+  // by-entries and on-entries are each at most one per edge key: load <= 1/2
+  uint64_t ecap = 1024;
+  while (ecap < 4 * n_keys + 64) ecap *= 2;
+  const uint64_t ocap = 2 * n_keys + 1;
+  if (ensure(c, c->o_key, ecap * 8) || ensure(c, c->o_a, ecap * 8) || ensure(c, c->o_b, ecap * 8) ||
+      ensure(c, c->o_out, ocap * sizeof(kmz_dep_entry)) || ensure(c, c->o_rts, ((size_t)c->n_dep + 1) * 8) ||
+      ensure(c, c->o_rsh, ((size_t)c->n_dep + 1) * 4) || (dups && ensure(c, c->o_val, ((size_t)n + 1) * 4)))
+    return KMZ_E_HIP;
+  unsigned long long *cnt = P<unsigned long long>(c->stats64) + S_DEPENT;
+  {
+    Timed t(c, KMZ_K_ORDER);
+    HIPCHK(c, hipMemsetAsync(c->o_key.p, 0, ecap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->o_a.p, 0xFF, ecap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->o_b.p, 0xFF, ecap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(cnt, 0, 8, c->stream));
+    launch_dep_order(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), P<unsigned long long>(c->rowpos),
+                     n, P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->index_base, P<unsigned long long>(c->o_key),
+                     P<unsigned long long>(c->o_a), P<unsigned long long>(c->o_b), ecap,
+                     dups ? P<uint32_t>(c->o_val) : nullptr, P<unsigned long long>(c->epp) + c->n_dep,
+                     P<kmz_dep_entry>(c->o_out), cnt, P<int64_t>(c->o_rts), P<uint32_t>(c->o_rsh),
+                     P<unsigned int>(c->counters));
+  }
+  HIPCHK(c, hipGetLastError());
+  unsigned long long m = 0;
+  unsigned int fl = 0;
+  HIPCHK(c, hipMemcpyAsync(&m, cnt, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&fl, P<unsigned int>(c->counters) + C_FLAGS, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((fl & F_TABLE_FULL) || m > ocap) return fail(c, KMZ_E_OVERFLOW, "entry-order table overflow");
+  c->o_n = m;
+  if (c->imap_n && m) {
+    const uint64_t *ls = P<uint64_t>(c->imap_l), *gs = P<uint64_t>(c->imap_g);
+    unsigned long long *o = P<unsigned long long>(c->o_out);
+    for (int col = 1; col <= 3; ++col)  // row, span, pos
+      launch_remap_index(c->stream, o + col, m, sizeof(kmz_dep_entry) / 8, 0, ls, gs, c->imap_n);
+    HIPCHK(c, hipGetLastError());
+  }
+  return KMZ_OK;
+}
+
+int kmz_get_dep_entries(kmz_ctx *c, kmz_dep_entry *out, uint64_t cap, uint64_t *n_out, int64_t *row_ts,
+                        uint32_t *row_shape, uint64_t row_cap) {
+  if (!c || !n_out) return KMZ_E_ARG;
+  if (!(c->ran & KMZ_RUN_DEP_ORDER)) return fail(c, KMZ_E_STATE, "run with KMZ_RUN_DEPS|KMZ_RUN_DEP_ORDER first");
+  *n_out = c->o_n;
+  if (out && cap < c->o_n) return fail(c, KMZ_E_ARG, "output too small");
+  if ((row_ts || row_shape) && row_cap < c->n_dep) return fail(c, KMZ_E_ARG, "output too small");
+  if (out && c->o_n)
+    HIPCHK(c, hipMemcpyAsync(out, c->o_out.p, c->o_n * sizeof(kmz_dep_entry), hipMemcpyDeviceToHost, c->stream));
+  if (row_ts && c->n_dep) HIPCHK(c, hipMemcpyAsync(row_ts, c->o_rts.p, (size_t)c->n_dep * 8, hipMemcpyDeviceToHost, c->stream));
+  if (row_shape && c->n_dep)
+    HIPCHK(c, hipMemcpyAsync(row_shape, c->o_rsh.p, (size_t)c->n_dep * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
 // A non-contiguous shard (kmz_set_index_map): the run used local flatten
 // indices; map the order keys it reports to global ones (kmz_shard.hip).
 static int remap_results(kmz_ctx *c, uint32_t flags, bool links) {
@@ -723,7 +787,8 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_run before kmz_load");
   uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
   if (smode == (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG)) return fail(c, KMZ_E_ARG, "choose one stats identity per run");
-  const bool links = (flags & KMZ_RUN_SPAN_LINKS) != 0;
+  if ((flags & KMZ_RUN_DEP_ORDER) && !(flags & KMZ_RUN_DEPS)) return fail(c, KMZ_E_ARG, "KMZ_RUN_DEP_ORDER needs KMZ_RUN_DEPS");
+  const bool links = (flags & (KMZ_RUN_SPAN_LINKS | KMZ_RUN_DEP_ORDER)) != 0;
   hipSetDevice(c->device);
   c->hpin_valid = false;
   for (int attempt = 0; attempt < 8; ++attempt) {
@@ -817,6 +882,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     if (!retry) {
       int e = check_flags(c, h[C_FLAGS]);
       if (e) return e;
+      if ((flags & KMZ_RUN_DEP_ORDER) && (e = run_dep_order(c, s64[S_TRIP_OUT], h[C_DUPS] != 0))) return e;
       if (c->imap_n && (e = remap_results(c, flags, links))) return e;
       c->ran = flags;
       c->links = links;

@@ -29,7 +29,7 @@ constexpr uint32_t CERT_DUP = 1u, CERT_OVF = 2u;
 constexpr uint32_t MISSV = 0xFFFFFFFDu;  // dp: parent id not in the span's window
 constexpr uint32_t PEND = 0xFFFFFFFCu;   // cparent: CLIENT chain leaves the window
 // u64 device statistics
-enum { S_ROWS = 0, S_REL = 1, S_MAXD = 2, S_CHAINS = 3, S_SERVER = 4, S_TRIP_OUT = 5, S_COUNT = 8 };
+enum { S_ROWS = 0, S_REL = 1, S_MAXD = 2, S_CHAINS = 3, S_SERVER = 4, S_TRIP_OUT = 5, S_DEPENT = 6, S_COUNT = 8 };
 
 struct DupEntry {
   uint32_t pos, idx, winner, pad;
@@ -159,5 +159,13 @@ void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32
                  unsigned long long *mkey, uint32_t *mval, uint32_t mcap, const unsigned int *counters);
 void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent,
                  const unsigned int *counters);
+
+// entry order of the reduced dependency graph (kmz_order.hip)
+void launch_dep_order(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
+                      const uint32_t *cparent, const unsigned long long *rowpos, uint32_t n, const uint32_t *dep_ep,
+                      uint32_t n_shapes, uint32_t n_ep, uint64_t index_base, unsigned long long *ekey,
+                      unsigned long long *ea, unsigned long long *eb, uint64_t ecap, uint32_t *val,
+                      const unsigned long long *ep_first, kmz_dep_entry *out, unsigned long long *count,
+                      int64_t *row_ts, uint32_t *row_shape, unsigned int *counters);
 
 }  // namespace kmz

@@ -239,6 +239,18 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_get_span_links(self.ctx, L.ptr(cp), L.ptr(rp), self.n))
         return cp, rp
 
+    def dep_entries(self):
+        """-> (entries DEP_ENTRY_DTYPE, row_ts int64[n_dep], row_shape uint32[n_dep]) of the last
+        run with RUN_DEPS | RUN_DEP_ORDER (kmz_get_dep_entries)."""
+        m = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_get_dep_entries(self.ctx, None, 0, C.byref(m), None, None, 0))
+        out = np.zeros(m.value, dtype=L.DEP_ENTRY_DTYPE)
+        rts = np.zeros(self.n_dep_ep, dtype=np.int64)
+        rsh = np.zeros(self.n_dep_ep, dtype=np.uint32)
+        L.check(self.ctx, self._lib.kmz_get_dep_entries(self.ctx, L.ptr(out), m.value, C.byref(m), L.ptr(rts),
+                                                        L.ptr(rsh), self.n_dep_ep))
+        return out, rts, rsh
+
     # ---- multi-GPU partials ----------------------------------------------------
     def group_partials_ptr(self):
         p, g = C.c_void_p(), C.c_uint64()

@@ -33,6 +33,8 @@ def lib():
         L.oracle_stats.argtypes = [C.c_uint64, P, P, P, P, P, P, C.c_uint32, C.c_uint32, P, P, P, P, P]
         L.oracle_deps.restype = C.c_int
         L.oracle_deps.argtypes = [C.c_uint64, P, P, P, P, P, P, C.c_uint32, C.c_uint64, P, P, P, P, P, P]
+        L.oracle_dep_entries.restype = C.c_int
+        L.oracle_dep_entries.argtypes = [C.c_uint64, P, P, P, P, P, P, C.c_uint32, C.c_uint64, P, P, P, P]
         L.oracle_to_precise.restype = C.c_double
         L.oracle_to_precise.argtypes = [C.c_double]
         _lib = L
@@ -101,6 +103,41 @@ def deps(batch, dep_ep: np.ndarray, n_ep: int):
         dict(last=last[:n_ep], first=first[:n_ep], external=ext[:n_ep].astype(bool), has_row=has[:n_ep]),
         dict(rows=int(counts[0]), relations=int(counts[1]), max_depth=int(counts[2]), keys=int(counts[3])),
     )
+
+
+ENTRY_DTYPE = np.dtype([("key", "<u8"), ("row", "<u8"), ("span", "<u8"), ("pos", "<u8"), ("ts", "<i8"),
+                        ("shape", "<u4"), ("pad", "<u4")])
+
+
+def dep_entries(batch, dep_ep: np.ndarray, n_ep: int):
+    """oracle_dep_entries: the entry records of the reduced graph
+    EndpointDependencies([]).combineWith(deps).trim(), sorted by key, plus the
+    (timestamp, shape) of each endpoint's first row.  Indices are global."""
+    n = len(batch)
+    ep = np.ascontiguousarray(dep_ep, dtype=np.uint32)
+    row_ts = np.zeros(max(1, n_ep), np.int64)
+    row_shape = np.zeros(max(1, n_ep), np.uint32)
+    cap = max(64, n // 4)
+    while True:
+        out = np.zeros(cap, ENTRY_DTYPE)
+        m = C.c_uint64()
+        rc = lib().oracle_dep_entries(
+            n, _p(batch.span_id), _p(batch.parent_id), _p(batch.kind), _p(batch.shape), _p(batch.timestamp), _p(ep),
+            n_ep, cap, _p(out), C.byref(m), _p(row_ts), _p(row_shape),
+        )
+        if rc == -4:
+            cap = m.value
+            continue
+        if rc == -3:
+            raise RuntimeError("cyclic parent chain")
+        assert rc == 0, rc
+        break
+    out = out[: m.value]
+    base = np.uint64(batch.index_base)
+    for f in ("row", "span", "pos"):
+        out[f] += base
+    out = out[np.argsort(out["key"], kind="stable")]
+    return out, row_ts[:n_ep], row_shape[:n_ep]
 
 
 # ---- all-core OpenMP restatement (kmz_cpu_omp.c): the bench's cpu_baseline ----

@@ -316,3 +316,120 @@ int oracle_deps(uint64_t n, const uint64_t *sid, const uint64_t *pid, const uint
   map_free(&ids);
   return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* entry order of the reduced graph                                          */
+/* ------------------------------------------------------------------------ */
+/* EndpointDependencies([]).combineWith(traces.toEndpointDependencies()).trim()
+ * in columnar form (EndpointDependencies.ts:91-112, 499-542 over the per-row
+ * lists of Traces.ts:145-190).  The merged row of endpoint e is e's first row
+ * with, appended in row order, every entry of e's later rows whose
+ * (endpoint name, distance) it has not seen; within one row:
+ *   dependingBy = the walk's ancestors in distance order (upperMap),
+ *   dependingOn = the rows whose walk reached it, in row order, deduplicated
+ *                 by (name, distance): first position, LAST value (lowerMap).
+ * One record per entry of the merged graph (sequential first-seen rules):
+ *   key   = anc_ep<<40 | desc_ep<<16 | distance<<1 | side
+ *           (side 0: dependingBy entry of desc_ep's row, 1: dependingOn entry
+ *            of anc_ep's row)
+ *   row   = position of the row that contributed it (the first row of the
+ *           merged row's endpoint having that entry)
+ *   pos   = side 0: = row; side 1: position of the first descendant row
+ *   span  = the span whose ToEndpointInfo the entry carries (side 0: the
+ *           ancestor at `distance` in that row's walk; side 1: the last
+ *           descendant row with the entry's key in that row's lowerMap)
+ *   ts, shape of `span`
+ * row_ts[e] / row_shape[e]: the value span of e's first row (INT64_MIN /
+ * UINT32_MAX without a row).  Records come out in no particular order
+ * (n_out = count; -4 when cap is too small, with the count needed). */
+int oracle_dep_entries(uint64_t n, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind,
+                       const uint32_t *shape, const int64_t *ts, const uint32_t *dep_ep, uint32_t n_ep, uint64_t cap,
+                       uint64_t *out /* [cap][6] */, uint64_t *n_out, int64_t *row_ts, uint32_t *row_shape) {
+  u64map ids;
+  if (map_init(&ids, n)) return -1;
+  int nw;
+  for (uint64_t i = 0; i < n; ++i) map_set(&ids, sid[i], i, &nw);
+  /* rows in map order: positions sorted, value span per position */
+  uint64_t *val = (uint64_t *)malloc((n ? n : 1) * 8);
+  uint8_t *isrow = (uint8_t *)calloc(n ? n : 1, 1);
+  if (!val || !isrow) return -1;
+  for (uint64_t p = 0; p < ids.cap; ++p)
+    if (ids.key[p] && kind[ids.v1[p]] == KIND_SERVER) {
+      val[ids.v0[p]] = ids.v1[p];
+      isrow[ids.v0[p]] = 1;
+    }
+  for (uint32_t e = 0; e < n_ep; ++e) {
+    row_ts[e] = INT64_MIN;
+    row_shape[e] = UINT32_MAX;
+  }
+  u64map ent; /* entry key -> record index */
+  if (map_init(&ent, 1024)) return -1;
+  uint64_t m = 0;
+  int rc = 0;
+  for (uint64_t r = 0; r < n && rc == 0; ++r) {
+    if (!isrow[r]) continue;
+    uint64_t s = val[r];
+    uint32_t d = dep_ep[shape[s]];
+    if (row_shape[d] == UINT32_MAX) {
+      row_ts[d] = ts[s];
+      row_shape[d] = shape[s];
+    }
+    uint64_t p = pid[s], depth = 1, steps = 0;
+    while (p) {
+      if (++steps > (1u << 20)) {
+        rc = -3;
+        break;
+      }
+      uint64_t slot = map_find(&ids, p);
+      if (slot == UINT64_MAX) break;
+      uint64_t q = ids.v1[slot];
+      if (kind[q] == KIND_CLIENT) {
+        p = pid[q];
+        continue;
+      }
+      uint64_t base = ((uint64_t)dep_ep[shape[q]] << 40) | ((uint64_t)d << 16) | (depth << 1);
+      for (int side = 0; side < 2; ++side) {
+        if (side == 1 && kind[q] != KIND_SERVER) break;
+        uint64_t key = base | (uint64_t)side;
+        uint64_t row = side ? ids.v0[slot] : r; /* the row the entry belongs to */
+        uint64_t span = side ? s : q;
+        uint64_t es = map_find(&ent, key), x;
+        if (es == UINT64_MAX) {
+          if (m < cap) {
+            x = m;
+            out[6 * x + 0] = key;
+            out[6 * x + 1] = row;
+            out[6 * x + 2] = span;
+            out[6 * x + 3] = r; /* side 0: = row (== r); side 1: first descendant */
+          }
+          map_set(&ent, key, m, &nw);
+          m++;
+          continue;
+        }
+        x = ent.v1[es];
+        if (x >= cap) continue;
+        if (row < out[6 * x + 1]) { /* an earlier row of the same endpoint has it */
+          out[6 * x + 1] = row;
+          out[6 * x + 2] = span;
+          out[6 * x + 3] = r;
+        } else if (side && row == out[6 * x + 1]) {
+          out[6 * x + 2] = span; /* lowerMap: last value */
+        }
+      }
+      p = pid[q];
+      depth++;
+    }
+  }
+  for (uint64_t x = 0; x < m && x < cap; ++x) {
+    uint64_t sp = out[6 * x + 2];
+    out[6 * x + 4] = (uint64_t)ts[sp];
+    out[6 * x + 5] = shape[sp];
+  }
+  *n_out = m;
+  map_free(&ent);
+  map_free(&ids);
+  free(val);
+  free(isrow);
+  if (rc) return rc;
+  return m > cap ? -4 : 0;
+}

@@ -496,9 +496,13 @@ def combine_latency_cv_and_mean(n1, mean1, cv1, n2, mean2, cv2):
     std2s = cv2 * mean2s
     total = n1 + n2
     mean_total = (n1 * mean1s + n2 * mean2s) / total
-    var1 = std1s ** 2
-    var2 = std2s ** 2
-    pooled = (n1 * var1 + n2 * var2 + n1 * (mean1s - mean_total) ** 2 + n2 * (mean2s - mean_total) ** 2) / total
+    # JS `x ** 2` is Math.pow(x, 2), whose fdlibm core returns x * x for y == 2
+    # (V8 base/ieee754 pow); C pow(x, 2.0) is only within 0.52 ulp of it
+    var1 = std1s * std1s
+    var2 = std2s * std2s
+    d1 = mean1s - mean_total
+    d2 = mean2s - mean_total
+    pooled = (n1 * var1 + n2 * var2 + n1 * (d1 * d1) + n2 * (d2 * d2)) / total
     std_total = math.sqrt(pooled)
     cv_total = 0 if mean_total == 0 else std_total / mean_total
     return mean_total * scale, cv_total
