@@ -43,21 +43,25 @@ def _freeze(fields: dict):
 
 class _Registry:
     """uniqueEndpointName -> stable id, and interned ToEndpointInfo field sets
-    (everything of an endpoint info but its timestamp)."""
+    (everything of an endpoint info but its timestamp).  Append-only, so every
+    cache state and window built on one registry shares it: ids never change."""
 
     def __init__(self):
         self.names: List[str] = []
         self.index: Dict[str, int] = {}
         self.infos: List[dict] = []
         self.info_index: Dict[tuple, int] = {}
+        self._by_obj: Dict[int, tuple] = {}  # id(fields dict) -> (dict, info id)
 
-    def copy(self) -> "_Registry":
-        r = _Registry()
-        r.names = list(self.names)
-        r.index = dict(self.index)
-        r.infos = list(self.infos)
-        r.info_index = dict(self.info_index)
-        return r
+    def info_of_obj(self, fields: dict) -> int:
+        """info_id of a long-lived fields dict (the ingest's per-shape Identity
+        objects are cached across batches): interned once per object."""
+        hit = self._by_obj.get(id(fields))
+        if hit is not None and hit[0] is fields:
+            return hit[1]
+        i = self.info_id(fields)
+        self._by_obj[id(fields)] = (fields, i)
+        return i
 
     def name_id(self, name: str) -> int:
         i = self.index.get(name)
@@ -116,15 +120,16 @@ class ReducedDependencies:
     @classmethod
     def from_columns(cls, entries, row_ts, row_shape, first_row, has_row, external, last_ms, last_none, names,
                      shape_fields, reg: Optional[_Registry] = None) -> "ReducedDependencies":
-        out = cls(reg.copy() if reg is not None else None)
+        out = cls(reg)
         R = out.reg
         emap = np.array([R.name_id(n) if n is not None else -1 for n in names] or [-1], dtype=np.int64)
         has = np.nonzero(has_row)[0]
         has = has[np.argsort(first_row[has], kind="stable")]
-        shapes = np.unique(np.concatenate([entries["shape"], row_shape[has]]))
+        used = np.concatenate([entries["shape"], row_shape[has]])
+        shapes = np.nonzero(np.bincount(used))[0] if len(used) else used  # distinct shapes, O(n)
         smap = np.full(int(shapes.max()) + 1 if len(shapes) else 1, -1, np.int64)
         for s in shapes.tolist():
-            smap[s] = R.info_id(shape_fields(s))
+            smap[s] = R.info_of_obj(shape_fields(s))
         out.row_ep = emap[has]
         out.row_info = smap[row_shape[has]]
         out.row_ts = row_ts[has] / 1000
@@ -141,12 +146,18 @@ class ReducedDependencies:
         out.e_ep = emap[np.where(side == 1, d, a)]
         out.e_info = smap[entries["shape"]]
         out.e_ts = entries["ts"] / 1000
-        # within a merged row: by the contributing row, then the row's own order
+        # within a merged row: by the contributing row, then the row's own
+        # order (side 1: the first descendant's index; side 0: the distance).
+        # Both are flatten indices < 2^31, so (row, within) packs into one
+        # order-preserving int64 and no sort is needed here.
         within = np.where(side == 1, entries["pos"], out.e_dist.astype(np.uint64))
-        o = np.lexsort((within, entries["row"]))
-        out.e_ord = np.empty(len(o), np.int64)
-        out.e_ord[o] = np.arange(len(o), dtype=np.int64)
-        out.next_ord = len(o)
+        if len(k) and (int(entries["row"].max()) >= 1 << 31 or int(within.max()) >= 1 << 32):
+            o = np.lexsort((within, entries["row"]))
+            out.e_ord = np.empty(len(o), np.int64)
+            out.e_ord[o] = np.arange(len(o), dtype=np.int64)
+        else:
+            out.e_ord = ((entries["row"] << _U(32)) | within).astype(np.int64)
+        out.next_ord = int(out.e_ord.max()) + 1 if len(k) else 0
         return out
 
     @classmethod
@@ -158,7 +169,7 @@ class ReducedDependencies:
         position: Map.set, EndpointDependencies.ts:508-513); ``True`` as its
         argument (later rows append their unseen entries, 514-535).  Each row's
         lists are deduplicated as trim() does (first position, last value)."""
-        out = cls(reg.copy() if reg is not None else None)
+        out = cls(reg)
         R = out.reg
         order: List[int] = []
         by_ep: Dict[int, list] = {}
@@ -236,20 +247,24 @@ class ReducedDependencies:
         if not isinstance(other, ReducedDependencies):
             other = other.toReduced() if hasattr(other, "toReduced") else ReducedDependencies.from_json(
                 other.toJSON(), merge_rows=True)
-        out = ReducedDependencies(self.reg.copy())
+        out = ReducedDependencies(self.reg)
         R = out.reg
-        bmap = np.array([R.name_id(n) for n in other.reg.names], dtype=np.int64)
-        imap = np.array([R.info_id(f) for f in other.reg.infos], dtype=np.int64)
-        b_row = bmap[other.row_ep] if len(other.row_ep) else other.row_ep
+        if other.reg is R:  # one registry: ids already agree
+            bmap = imap = None
+        else:
+            bmap = np.array([R.name_id(n) for n in other.reg.names] or [0], dtype=np.int64)
+            imap = np.array([R.info_id(f) for f in other.reg.infos] or [0], dtype=np.int64)
+        b_row = bmap[other.row_ep] if bmap is not None else other.row_ep
         new = ~np.isin(b_row, self.row_ep)
         out.row_ep = np.concatenate([self.row_ep, b_row[new]])
-        out.row_info = np.concatenate([self.row_info, imap[other.row_info[new]] if new.any() else other.row_info[new]])
+        out.row_info = np.concatenate([self.row_info, imap[other.row_info[new]] if imap is not None else
+                                       other.row_info[new]])
         out.row_ts = np.concatenate([self.row_ts, other.row_ts[new]])
         out.row_last = np.concatenate([self.row_last, other.row_last[new]])
         out.row_last_int = np.concatenate([self.row_last_int, other.row_last_int[new]])
         out.row_ext = np.concatenate([self.row_ext, other.row_ext[new]])
         if len(other.e_row):
-            br, be = bmap[other.e_row], bmap[other.e_ep]
+            br, be = (bmap[other.e_row], bmap[other.e_ep]) if bmap is not None else (other.e_row, other.e_ep)
             bck = self._ck(br, other.e_side, be, other.e_dist)
             fresh = ~np.isin(bck, self._ck(self.e_row, self.e_side, self.e_ep, self.e_dist))
         else:
@@ -261,7 +276,8 @@ class ReducedDependencies:
         out.e_side = np.concatenate([self.e_side, other.e_side[fresh]])
         out.e_ep = np.concatenate([self.e_ep, be[fresh]])
         out.e_dist = np.concatenate([self.e_dist, other.e_dist[fresh]])
-        out.e_info = np.concatenate([self.e_info, imap[other.e_info[fresh]] if len(rank) else other.e_info[fresh]])
+        out.e_info = np.concatenate([self.e_info, imap[other.e_info[fresh]] if imap is not None else
+                                     other.e_info[fresh]])
         out.e_ts = np.concatenate([self.e_ts, other.e_ts[fresh]])
         out.e_ord = np.concatenate([self.e_ord, self.next_ord + rank])
         out.next_ord = self.next_ord + len(rank)
@@ -419,15 +435,40 @@ def to_precise(x: np.ndarray) -> np.ndarray:
     return r / 1e14
 
 
+class _CombinedTables:
+    """Interned group keys (``uniqueEndpointName\tstatus``) and sample metas of
+    combined rows; append-only, shared by every cache state built on it."""
+
+    def __init__(self):
+        self.keys: Dict[str, int] = {}
+        self.metas: List[dict] = []
+        self.meta_index: Dict[tuple, int] = {}
+        self.memo: Dict[tuple, tuple] = {}  # (id(endpoint fields), status text) -> (key id, meta id)
+        self._hold: List[dict] = []  # keeps the memo's field dicts alive
+
+    def key_id(self, k: str) -> int:
+        i = self.keys.get(k)
+        if i is None:
+            i = self.keys[k] = len(self.keys)
+        return i
+
+    def meta_id(self, m: dict) -> int:
+        f = _freeze(m)
+        i = self.meta_index.get(f)
+        if i is None:
+            i = self.meta_index[f] = len(self.metas)
+            self.metas.append(m)
+        return i
+
+
 class CombinedColumns:
     """CombinedRealtimeDataList as columns: one row per (endpoint, status),
-    ``key`` the interned ``uniqueEndpointName\\tstatus`` (CombinedRealtimeDataList
+    ``key`` the interned ``uniqueEndpointName\tstatus`` (CombinedRealtimeDataList
     .ts:188-190), ``meta`` the row's sample fields (uniqueEndpointName, status,
     and _BASE), ``combined`` / ``latest`` / ``mean`` / ``cv``."""
 
-    def __init__(self, keys: Optional[Dict[str, int]] = None, metas: Optional[List[dict]] = None):
-        self.keys = keys if keys is not None else {}
-        self.metas = metas if metas is not None else []
+    def __init__(self, tab: Optional[_CombinedTables] = None):
+        self.tab = tab or _CombinedTables()
         self.key = np.zeros(0, np.int64)
         self.meta = np.zeros(0, np.int64)
         self.combined = np.zeros(0, np.int64)
@@ -438,26 +479,14 @@ class CombinedColumns:
 
     @classmethod
     def from_json(cls, rows: Sequence[dict], like: Optional["CombinedColumns"] = None) -> "CombinedColumns":
-        out = cls(dict(like.keys) if like else None, list(like.metas) if like else None)
-        meta_index = {}
-        for i, m in enumerate(out.metas):
-            meta_index[_freeze(m)] = i
+        out = cls(like.tab if like else None)
+        T = out.tab
         key, meta, comb, lat, lint, mean, cv = [], [], [], [], [], [], []
         for r in rows:
             if any(k in r for k in ("requestBody", "responseBody", "requestSchema", "responseSchema")):
                 raise NotImplementedError("body / schema merge (Utils.Merge, json-to-ts) is not columnar")
-            k = f"{r['uniqueEndpointName']}\t{tpl(r.get('status', UNDEFINED))}"
-            kid = out.keys.get(k)
-            if kid is None:
-                kid = out.keys[k] = len(out.keys)
-            m = {f: r.get(f, UNDEFINED) for f in ("uniqueEndpointName", "status") + _BASE}
-            fm = _freeze(m)
-            mid = meta_index.get(fm)
-            if mid is None:
-                mid = meta_index[fm] = len(out.metas)
-                out.metas.append(m)
-            key.append(kid)
-            meta.append(mid)
+            key.append(T.key_id(f"{r['uniqueEndpointName']}\t{tpl(r.get('status', UNDEFINED))}"))
+            meta.append(T.meta_id({f: r.get(f, UNDEFINED) for f in ("uniqueEndpointName", "status") + _BASE}))
             comb.append(int(r["combined"]))
             lat.append(r["latestTimestamp"])
             lint.append(type(r["latestTimestamp"]) is int)
@@ -472,33 +501,70 @@ class CombinedColumns:
         out.cv = np.array(cv, np.float64)
         return out
 
+    @classmethod
+    def from_groups(cls, groups: np.ndarray, n_status: int, ep_fields, statuses: Sequence,
+                    like: Optional["CombinedColumns"] = None) -> "CombinedColumns":
+        """Columns of RealtimeDataList.toCombinedRealtimeData() straight from the
+        engine's dense groups (kmz_get_groups, [n_ep * n_status]): used groups
+        ordered by their endpoint's first row, then their own first row
+        (RealtimeDataList.ts:22-45).  ep_fields(e): the row fields of endpoint e
+        (Traces.ts:73-99; long-lived dicts, memoised by identity); statuses[s]:
+        the interned status values.  No Envoy logs here (no content types)."""
+        out = cls(like.tab if like else None)
+        T = out.tab
+        used = np.nonzero(groups["combined"] > 0)[0]
+        ep, st = used // n_status, used % n_status
+        first = groups["first"][used]
+        if len(used):
+            epf = np.full(int(ep.max()) + 1, np.iinfo(np.uint64).max, np.uint64)
+            np.minimum.at(epf, ep, first)
+            o = np.lexsort((first, epf[ep]))
+            used, ep, st = used[o], ep[o], st[o]
+        st_txt = [tpl(v) for v in statuses]
+        keys, metas = [], []
+        for e, s in zip(ep.tolist(), st.tolist()):
+            f = ep_fields(e)
+            hit = T.memo.get((id(f), st_txt[s]))
+            if hit is None:
+                T._hold.append(f)
+                sv = statuses[s]
+                hit = T.memo[(id(f), st_txt[s])] = (
+                    T.key_id(f"{f['uniqueEndpointName']}\t{st_txt[s]}"),
+                    T.meta_id({"uniqueEndpointName": f["uniqueEndpointName"], "status": sv,
+                               **{b: f.get(b, UNDEFINED) for b in _BASE}}))
+            keys.append(hit[0])
+            metas.append(hit[1])
+        out.key = np.array(keys, np.int64)
+        out.meta = np.array(metas, np.int64)
+        out.combined = groups["combined"][used].astype(np.int64)
+        out.latest = groups["latest_timestamp"][used].astype(np.float64)
+        out.latest_int = np.ones(len(used), bool)
+        out.mean = groups["mean"][used].astype(np.float64)
+        out.cv = groups["cv"][used].astype(np.float64)
+        return out
+
     def _adopt(self, other: "CombinedColumns"):
-        """other's key / meta ids in this's tables."""
-        kinv = [None] * len(other.keys)
-        for k, i in other.keys.items():
+        """other's key / meta ids in this's tables (identity when shared)."""
+        if other.tab is self.tab:
+            return None, None
+        kinv = [None] * len(other.tab.keys)
+        for k, i in other.tab.keys.items():
             kinv[i] = k
-        kmap = np.array([self.keys.setdefault(k, len(self.keys)) for k in kinv] or [0], np.int64)
-        mi = {_freeze(m): i for i, m in enumerate(self.metas)}
-        mm = []
-        for m in other.metas:
-            f = _freeze(m)
-            if f not in mi:
-                mi[f] = len(self.metas)
-                self.metas.append(m)
-            mm.append(mi[f])
-        return kmap, np.array(mm or [0], np.int64)
+        kmap = np.array([self.tab.key_id(k) for k in kinv] or [0], np.int64)
+        mmap = np.array([self.tab.meta_id(m) for m in other.tab.metas] or [0], np.int64)
+        return kmap, mmap
 
     def filter_service(self) -> "CombinedColumns":
         """``update.toJSON().filter((rl) => rl.service)`` (CCombinedRealtimeData.ts:48-50)."""
-        ok = np.array([js_truthy(m.get("service", UNDEFINED)) for m in self.metas] or [False])
+        ok = np.array([js_truthy(m.get("service", UNDEFINED)) for m in self.tab.metas] or [False])
         return self._take(ok[self.meta] if len(self.meta) else np.zeros(0, bool))
 
     def filter_namespace(self, namespace: str) -> "CombinedColumns":
-        ok = np.array([m.get("namespace", UNDEFINED) == namespace for m in self.metas] or [False])
+        ok = np.array([m.get("namespace", UNDEFINED) == namespace for m in self.tab.metas] or [False])
         return self._take(ok[self.meta] if len(self.meta) else np.zeros(0, bool))
 
     def _take(self, sel) -> "CombinedColumns":
-        out = CombinedColumns(self.keys, self.metas)
+        out = CombinedColumns(self.tab)
         for f in ("key", "meta", "combined", "latest", "latest_int", "mean", "cv"):
             setattr(out, f, getattr(self, f)[sel])
         return out
@@ -508,10 +574,10 @@ class CombinedColumns:
         first-appearance order of this + other; the sample (and its meta) is the
         group's first row; the latency fold starts from (0, 0, 0) and takes the
         rows in list order, one rank of rows per step."""
-        out = CombinedColumns(dict(self.keys), list(self.metas))
+        out = CombinedColumns(self.tab)
         kmap, mmap = out._adopt(other)
-        key = np.concatenate([self.key, kmap[other.key] if len(other.key) else other.key])
-        meta = np.concatenate([self.meta, mmap[other.meta] if len(other.meta) else other.meta])
+        key = np.concatenate([self.key, kmap[other.key] if kmap is not None else other.key])
+        meta = np.concatenate([self.meta, mmap[other.meta] if mmap is not None else other.meta])
         comb = np.concatenate([self.combined, other.combined])
         lat = np.concatenate([self.latest, other.latest])
         lint = np.concatenate([self.latest_int, other.latest_int])
@@ -561,7 +627,7 @@ class CombinedColumns:
         out = []
         for mi, n, lt, li, mu, cv in zip(self.meta.tolist(), self.combined.tolist(), self.latest.tolist(),
                                          self.latest_int.tolist(), self.mean.tolist(), self.cv.tolist()):
-            m = self.metas[mi]
+            m = self.tab.metas[mi]
             out.append(_clean({
                 "uniqueEndpointName": m["uniqueEndpointName"],
                 "uniqueServiceName": m["uniqueServiceName"],
@@ -589,7 +655,7 @@ class CCombinedRealtimeData:
 
     def setData(self, update) -> None:
         if not isinstance(update, CombinedColumns):
-            update = CombinedColumns.from_json(update.toJSON())
+            update = CombinedColumns.from_json(update.toJSON(), like=self._data)
         update = update.filter_service()
         self._data = self._data.combineWith(update) if self._data is not None else update
 

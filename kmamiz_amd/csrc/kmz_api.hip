@@ -59,7 +59,7 @@ struct kmz_ctx {
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n, cetab;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
-  DevBuf o_key, o_a, o_b, o_val, o_out, o_rts, o_rsh;  // reduced-graph entry order (kmz_order.hip)
+  DevBuf o_key, o_val, o_out, o_rts, o_rsh;  // reduced-graph entry order (kmz_order.hip; o_key = the slot table)
   uint64_t o_n = 0;
   DevBuf imap_l, imap_g;  // local -> global flatten-index runs of a non-contiguous shard (kmz_shard.hip)
   uint64_t imap_n = 0;     // 0: contiguous batch (index_base + i)
@@ -291,7 +291,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
-                    &c->tl_sstat, &c->tl_rel, &c->o_key, &c->o_a, &c->o_b, &c->o_val, &c->o_out,
+                    &c->tl_sstat, &c->tl_rel, &c->o_key, &c->o_val, &c->o_out,
                     &c->o_rts, &c->o_rsh};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
@@ -668,20 +668,17 @@ static int run_dep_order(kmz_ctx *c, uint64_t n_keys, bool dups) {
   uint64_t ecap = 1024;
   while (ecap < 4 * n_keys + 64) ecap *= 2;
   const uint64_t ocap = 2 * n_keys + 1;
-  if (ensure(c, c->o_key, ecap * 8) || ensure(c, c->o_a, ecap * 8) || ensure(c, c->o_b, ecap * 8) ||
-      ensure(c, c->o_out, ocap * sizeof(kmz_dep_entry)) || ensure(c, c->o_rts, ((size_t)c->n_dep + 1) * 8) ||
-      ensure(c, c->o_rsh, ((size_t)c->n_dep + 1) * 4) || (dups && ensure(c, c->o_val, ((size_t)n + 1) * 4)))
+  if (ensure(c, c->o_key, ecap * dep_order_slot_bytes()) || ensure(c, c->o_out, ocap * sizeof(kmz_dep_entry)) ||
+      ensure(c, c->o_rts, ((size_t)c->n_dep + 1) * 8) || ensure(c, c->o_rsh, ((size_t)c->n_dep + 1) * 4) ||
+      (dups && ensure(c, c->o_val, ((size_t)n + 1) * 4)))
     return KMZ_E_HIP;
   unsigned long long *cnt = P<unsigned long long>(c->stats64) + S_DEPENT;
   {
     Timed t(c, KMZ_K_ORDER);
-    HIPCHK(c, hipMemsetAsync(c->o_key.p, 0, ecap * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->o_a.p, 0xFF, ecap * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->o_b.p, 0xFF, ecap * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->o_key.p, 0xFF, ecap * dep_order_slot_bytes(), c->stream));
     HIPCHK(c, hipMemsetAsync(cnt, 0, 8, c->stream));
     launch_dep_order(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), P<unsigned long long>(c->rowpos),
-                     n, P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->index_base, P<unsigned long long>(c->o_key),
-                     P<unsigned long long>(c->o_a), P<unsigned long long>(c->o_b), ecap,
+                     n, P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->index_base, c->o_key.p, ecap,
                      dups ? P<uint32_t>(c->o_val) : nullptr, P<unsigned long long>(c->epp) + c->n_dep,
                      P<kmz_dep_entry>(c->o_out), cnt, P<int64_t>(c->o_rts), P<uint32_t>(c->o_rsh),
                      P<unsigned int>(c->counters));

@@ -163,9 +163,9 @@ void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_
 // entry order of the reduced dependency graph (kmz_order.hip)
 void launch_dep_order(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
                       const uint32_t *cparent, const unsigned long long *rowpos, uint32_t n, const uint32_t *dep_ep,
-                      uint32_t n_shapes, uint32_t n_ep, uint64_t index_base, unsigned long long *ekey,
-                      unsigned long long *ea, unsigned long long *eb, uint64_t ecap, uint32_t *val,
+                      uint32_t n_shapes, uint32_t n_ep, uint64_t index_base, void *tab, uint64_t ecap, uint32_t *val,
                       const unsigned long long *ep_first, kmz_dep_entry *out, unsigned long long *count,
                       int64_t *row_ts, uint32_t *row_shape, unsigned int *counters);
+uint64_t dep_order_slot_bytes();
 
 }  // namespace kmz

@@ -64,6 +64,23 @@ def shape_table(config: int) -> ShapeTable:
     return ShapeTable(ids, ids, ids, n_ep, n_ep, n_ep, n_status)
 
 
+def dictionary(config: int):
+    """The host Dictionary of a synthetic config's shapes and statuses, interned
+    in id order (so its endpoint ids are the device tables' identity ids)."""
+    from .ingest import Dictionary
+
+    n_shapes, n_status, _ = describe(config)
+    d = Dictionary()
+    for s in range(n_shapes):
+        assert d.shape_id(*shape_tags(config, s)) == s
+    for st in STATUSES[:n_status]:
+        d.status_id(st)
+    for rule in ("rt", "tag", "dep"):
+        if d.shape_ep[rule] != list(range(n_shapes)):
+            raise ValueError(f"synthetic config {config}: {rule} endpoints are not one per shape")
+    return d
+
+
 def table_digest(config: int) -> int:
     """Digest of a synthetic config's id tables (merge_all's guard): every
     rank of a synthetic run indexes its partials by the same static tables."""

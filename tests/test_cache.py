@@ -214,3 +214,39 @@ def test_pooled_matches_scalar_fold():
         em, ec = O.combine_latency_cv_and_mean(int(n1[k]), float(m1[k]), float(c1[k]), int(n2[k]), float(m2[k]),
                                                float(c2[k]))
         assert gm[k] == em and gc[k] == ec, k
+
+
+def test_combined_columns_from_engine_groups():
+    """CombinedColumns.from_groups (the engine's dense groups -> columns) equals
+    the drop-in rows built from the same groups (classes._combine_native), on
+    the C oracle's groups of a mixed batch; and merges like them."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd.cache import CombinedColumns
+    from kmamiz_amd.classes import CombinedRealtimeDataList, _combine_native
+    from kmamiz_amd.ingest import ingest_traces
+
+    def groups_of(traces):
+        batch, d, _ = ingest_traces(traces)
+        t = d.shape_table()
+        o = c_oracle.stats(batch, t.tag_ep, t.n_tag_ep, t.n_status)
+        g = np.zeros(len(o["combined"]), L.GROUP_DTYPE)
+        for f in L.GROUP_DTYPE.names:
+            g[f] = o[f]
+        return g, batch, d, t
+
+    traces = mixed_traces(160)
+    parts = []
+    for w in (traces[:70], traces[50:]):
+        g, batch, d, t = groups_of(copy.deepcopy(w))
+        rows = _combine_native(g, 0, batch, d, "tag", None)
+        idents = d.shape_ident["tag"]
+        first_shape = {}
+        for sh, e in enumerate(d.shape_ep["tag"]):
+            first_shape.setdefault(e, sh)
+        cols = CombinedColumns.from_groups(g, t.n_status, lambda e: idents[first_shape[e]].fields, d.statuses)
+        assert cols.toJSON() == rows
+        parts.append((cols, rows))
+    got = parts[0][0].combineWith(parts[1][0]).toJSON()
+    exp = CombinedRealtimeDataList(copy.deepcopy(parts[0][1])).combineWith(
+        CombinedRealtimeDataList(copy.deepcopy(parts[1][1]))).toJSON()
+    assert got == exp
