@@ -88,8 +88,47 @@ def cut_literal(text, name):
         j += 1
 
 
+def cut_expression(text, name):
+    """`const NAME = <expression>;` for a non-literal expression (MockLogsPDAS
+    is a template string split into lines, MockData.ts:3933-3941)."""
+    m = re.search(r"^const %s\s*=\s*" % re.escape(name), text, re.M)
+    if not m:
+        raise KeyError(name)
+    i = m.end()
+    j, in_str, quote, depth = i, False, "", 0
+    while True:
+        c = text[j]
+        if in_str:
+            if c == "\\":
+                j += 2
+                continue
+            if c == quote:
+                in_str = False
+        elif c in "\"'`":
+            in_str, quote = True, c
+        elif c in "([{":
+            depth += 1
+        elif c in ")]}":
+            depth -= 1
+        elif c == ";" and depth == 0:
+            return text[i:j]
+        j += 1
+
+
+EXPRESSIONS = {"MockData.ts": ["MockLogsPDAS"]}
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    for fname, names in EXPRESSIONS.items():
+        text = open(os.path.join(REF, fname)).read()
+        for name in names:
+            js = "const __v = " + cut_expression(text, name) + ";\nprocess.stdout.write(JSON.stringify(__v));\n"
+            out = subprocess.run(["node", "-e", js], check=True, capture_output=True, text=True).stdout
+            dst = os.path.join(OUT, f"{name}.json")
+            with open(dst, "w") as f:
+                json.dump(json.loads(out), f, indent=1, ensure_ascii=False)
+            print("wrote", dst, file=sys.stderr)
     for fname, names in WANT.items():
         text = open(os.path.join(REF, fname)).read()
         # MockBaseCrlData2 needs divBaseData2 (MockData.ts:4501-4504)
