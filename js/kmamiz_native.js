@@ -497,6 +497,98 @@ function logMap(structuredLogs) {
 
 const JSON_CT = "application/json";
 
+// Utils.Merge / MergeStringBody (Utils.ts:279-309), restated in the same language
+function mergeValues(a, b) {
+  if (Array.isArray(a) && Array.isArray(b)) return [...a.slice(0, 10), ...b.slice(0, 10)];
+  if (!Array.isArray(a) && !Array.isArray(b)) return { ...a, ...b };
+  return a || b;
+}
+function mergeStringBody(a, b) {
+  if (a && b) {
+    let pa, pb;
+    try { pa = JSON.parse(a); } catch (e) {}
+    try { pb = JSON.parse(b); } catch (e) {}
+    if (pa && pb) return JSON.stringify(mergeValues(pa, pb));
+    return JSON.stringify(pa || pb);
+  }
+  return a || b;
+}
+// Utils.ObjectToInterfaceString (Utils.ts:14-75).  Its json-to-ts dependency
+// is taken from the host application when it has one (the reference's own
+// node_modules); otherwise the single-interface outputs fixed by the
+// reference's tests are restated (a flat object, an array of one flat shape)
+// and anything nested throws.
+let jsonToTs = null;
+try { jsonToTs = require("json-to-ts"); jsonToTs = jsonToTs.default || jsonToTs; } catch (e) {}
+const isPrimitive = (o) => o !== Object(o);
+function sortObject(obj) {
+  if (Array.isArray(obj)) return obj.every(isPrimitive) ? obj : obj.filter((o) => !isPrimitive(o)).map(sortObject);
+  return Object.keys(obj).sort().reduce((prev, curr) => {
+    let o = obj[curr];
+    if (typeof o === "object") {
+      if (Array.isArray(o) && o.length > 0) {
+        if (o.every((i) => typeof i === "object" && i !== null && !Array.isArray(i))) o = o.map(sortObject);
+      } else if (!Array.isArray(o)) o = o ? sortObject(o) : null;
+    }
+    prev[curr] = o;
+    return prev;
+  }, {});
+}
+function flatMembers(o) {
+  let s = "";
+  for (const [k, v] of Object.entries(o)) {
+    if (!/^[a-zA-Z_][a-zA-Z\d_]*$/.test(k) || (v !== null && typeof v === "object")) return null;
+    s += v === null ? `  ${k}?: any;\n` : `  ${k}: ${typeof v};\n`;
+  }
+  return s;
+}
+function toTS(obj, rootName) {
+  if (jsonToTs) return jsonToTs(obj, { rootName });
+  let m = null;
+  if (!Array.isArray(obj)) m = flatMembers(obj);
+  else if (obj.length && obj.every((o) => o && typeof o === "object" && !Array.isArray(o))) {
+    const all = obj.map(flatMembers);
+    if (all.every((x) => x !== null && x === all[0])) m = all[0];
+  }
+  if (m === null) {
+    const err = new Error("ObjectToInterfaceString needs json-to-ts for nested objects (not installed)");
+    err.missingJsonToTs = true;
+    throw err;
+  }
+  return [`interface ${rootName} {\n${m}}`];
+}
+function objectToInterfaceString(object, name = "Root") {
+  if (isPrimitive(object)) return typeof object;
+  const sorted = sortObject(object);
+  if (Array.isArray(sorted)) {
+    let arrayType = "Array<any>{}", appending = "";
+    if (object.length > 0) {
+      if (isPrimitive(object[0])) arrayType = `Array<${typeof object[0]}>{}`;
+      else {
+        arrayType = "Array<ArrayItem>{}\n";
+        appending = toTS(sorted, "ArrayItem").join("\n");
+      }
+    }
+    return `interface ${name} extends ${arrayType}${appending}`;
+  }
+  return toTS(sorted, name).join("\n");
+}
+// RealtimeDataList.parseRequestResponseBody (RealtimeDataList.ts:120-155)
+function parseBodies(d) {
+  const r = {};
+  for (const side of ["request", "response"]) {
+    if (d[side + "ContentType"] !== JSON_CT) continue;
+    try {
+      r[side + "Body"] = JSON.parse(d[side + "Body"]);
+      r[side + "Schema"] = objectToInterfaceString(r[side + "Body"]);
+    } catch (e) {
+      if (e && e.missingJsonToTs) throw e;  // (a missing dependency is not a body the reference skips)
+      r[side + "Body"] = r[side + "Schema"] = undefined;
+    }
+  }
+  return r;
+}
+
 class NativeRealtimeDataList {
   constructor(traces, rule, replicas, logs) {
     this._t = traces;
@@ -570,16 +662,43 @@ class NativeRealtimeDataList {
       used.push({ g, e, n, first });
     }
     used.sort((a, c) => epFirst.get(a.e) - epFirst.get(c.e) || a.first - c.first);
+    // groups whose first row is application/json fold every row's bodies
+    // (RealtimeDataList.ts:53-67): their rows in flatten order
+    const rowsOf = new Map();
+    if (this._logs) {
+      for (const { g, first } of used) {
+        const lf = this._logFields(first);
+        if (lf.requestContentType === JSON_CT || lf.responseContentType === JSON_CT) rowsOf.set(g, []);
+      }
+      if (rowsOf.size) {
+        const epOf = b.shapesTable[this._rule + "_ep"], sp = b.spans;
+        for (let i = 0; i < sp.span_id.length; i++) {
+          if (sp.kind[i] !== KIND_SERVER) continue;
+          const g = epOf[sp.shape[i]] * S + sp.status[i];
+          if (rowsOf.has(g)) rowsOf.get(g).push(i);
+        }
+      }
+    }
     return used.map(({ g, e, n, first }) => {
       const i = epFirst.get(e);
       const f = b.ident[this._rule][b.spans.shape[i]];
       if (!f) throw b.poison[this._rule].get(e);
       const r = replicaOf(this._replicas, f.uniqueServiceName);
-      // with logs: the first row's content types (RealtimeDataList.ts:53-89);
-      // JSON bodies need json-to-ts schemas (120-155), which this build lacks
+      // with logs: the first row's content types (RealtimeDataList.ts:53-89),
+      // and for application/json the folded, parsed bodies (120-155)
       const lf = this._logs ? this._logFields(first) : {};
-      if (lf.requestContentType === JSON_CT || lf.responseContentType === JSON_CT)
-        throw new Error("application/json bodies need json-to-ts schemas (SURVEY.md 8f row 3)");
+      let bodies = {};
+      if (rowsOf.has(g)) {
+        const rows = rowsOf.get(g);
+        let req = lf.requestBody, res = lf.responseBody;
+        for (let k = 1; k < rows.length; k++) {
+          const f = this._logFields(rows[k]);
+          req = mergeStringBody(req, f.requestBody);
+          res = mergeStringBody(res, f.responseBody);
+        }
+        bodies = parseBodies({ requestContentType: lf.requestContentType, responseContentType: lf.responseContentType,
+                               requestBody: req, responseBody: res });
+      }
       return strip({
         uniqueServiceName: f.uniqueServiceName,
         uniqueEndpointName: f.uniqueEndpointName,
@@ -594,9 +713,11 @@ class NativeRealtimeDataList {
         latency: { mean: v.getFloat64(g * 40 + 24, true), cv: v.getFloat64(g * 40 + 32, true) },
         requestContentType: lf.requestContentType,
         responseContentType: lf.responseContentType,
+        ...bodies,
       });
     });
   }
 }
 
-module.exports = { NativeTraces, NativeRealtimeDataList, explodeUrl, ingest, ingestJSON, addon };
+module.exports = { NativeTraces, NativeRealtimeDataList, explodeUrl, ingest, ingestJSON, addon, mergeStringBody,
+                   objectToInterfaceString };

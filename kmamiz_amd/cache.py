@@ -401,6 +401,55 @@ _BASE = ("uniqueServiceName", "service", "namespace", "version", "method", "requ
          "responseContentType")
 
 
+_BODY_FIELDS = ("requestBody", "requestSchema", "responseBody", "responseSchema")
+
+
+def _undef_col(n: int) -> np.ndarray:
+    c = np.empty(n, dtype=object)
+    c[:] = [UNDEFINED] * n
+    return c
+
+
+def _merge_bodies(body: Dict[str, np.ndarray], g: np.ndarray, rank: np.ndarray, head: np.ndarray, G: int):
+    """The body half of combineWith's reduce (CombinedRealtimeDataList.ts:
+    204-226): a group of one row keeps its row's bodies and schemas; a longer
+    group folds Utils.Merge over its rows from the first and re-derives the
+    schema of each truthy result.  Rows without bodies (or with {}) merge to {}
+    whose schema is one constant: that case is vectorised, the rest loops."""
+    from .envoy import merge, object_to_interface_string
+
+    out = {f: body[f][head].copy() for f in _BODY_FIELDS}
+    size = np.bincount(g, minlength=G)
+    multi = size > 1
+    if not multi.any():
+        return out
+    for side in ("request", "response"):
+        b = body[side + "Body"]
+        plain = np.array([v is UNDEFINED or (isinstance(v, dict) and not v) for v in b.tolist()], bool)
+        all_plain = np.ones(G, bool)
+        np.logical_and.at(all_plain, g, plain)
+        fast = np.nonzero(multi & all_plain)[0]
+        schema = object_to_interface_string({}) if len(fast) else None
+        for k in fast.tolist():
+            out[side + "Body"][k] = {}
+            out[side + "Schema"][k] = schema
+        slow = np.nonzero(multi & ~all_plain)[0]
+        if len(slow):
+            members = np.lexsort((rank, g))
+            starts = np.searchsorted(g[members], np.arange(G + 1))
+            sch = body[side + "Schema"]
+            for k in slow.tolist():
+                idx = members[starts[k]:starts[k + 1]]
+                acc, sc = b[idx[0]], sch[idx[0]]
+                for r in idx[1:].tolist():
+                    acc = merge(acc, b[r])
+                    if js_truthy(acc):
+                        sc = object_to_interface_string(acc)
+                out[side + "Body"][k] = acc
+                out[side + "Schema"][k] = sc
+    return out
+
+
 def _safe_log10_floor(x: np.ndarray) -> np.ndarray:
     """Math.floor(Math.log10(x)) for x > 0, else 0 (CombinedRealtimeDataList.ts:322-330)."""
     u, inv = np.unique(x, return_inverse=True)
@@ -476,15 +525,19 @@ class CombinedColumns:
         self.latest_int = np.zeros(0, bool)
         self.mean = np.zeros(0)
         self.cv = np.zeros(0)
+        # parsed bodies and their schemas (Envoy logs; Python objects, UNDEFINED = absent)
+        self.body = {f: _undef_col(0) for f in _BODY_FIELDS}
 
     @classmethod
     def from_json(cls, rows: Sequence[dict], like: Optional["CombinedColumns"] = None) -> "CombinedColumns":
         out = cls(like.tab if like else None)
         T = out.tab
         key, meta, comb, lat, lint, mean, cv = [], [], [], [], [], [], []
-        for r in rows:
-            if any(k in r for k in ("requestBody", "responseBody", "requestSchema", "responseSchema")):
-                raise NotImplementedError("body / schema merge (Utils.Merge, json-to-ts) is not columnar")
+        body = {f: _undef_col(len(rows)) for f in _BODY_FIELDS}
+        for j, r in enumerate(rows):
+            for f in _BODY_FIELDS:
+                if f in r:
+                    body[f][j] = r[f]
             key.append(T.key_id(f"{r['uniqueEndpointName']}\t{tpl(r.get('status', UNDEFINED))}"))
             meta.append(T.meta_id({f: r.get(f, UNDEFINED) for f in ("uniqueEndpointName", "status") + _BASE}))
             comb.append(int(r["combined"]))
@@ -499,6 +552,7 @@ class CombinedColumns:
         out.latest_int = np.array(lint, bool)
         out.mean = np.array(mean, np.float64)
         out.cv = np.array(cv, np.float64)
+        out.body = body
         return out
 
     @classmethod
@@ -541,6 +595,7 @@ class CombinedColumns:
         out.latest_int = np.ones(len(used), bool)
         out.mean = groups["mean"][used].astype(np.float64)
         out.cv = groups["cv"][used].astype(np.float64)
+        out.body = {f: _undef_col(len(used)) for f in _BODY_FIELDS}
         return out
 
     def _adopt(self, other: "CombinedColumns"):
@@ -567,6 +622,7 @@ class CombinedColumns:
         out = CombinedColumns(self.tab)
         for f in ("key", "meta", "combined", "latest", "latest_int", "mean", "cv"):
             setattr(out, f, getattr(self, f)[sel])
+        out.body = {f: v[sel] for f, v in self.body.items()}
         return out
 
     def combineWith(self, other: "CombinedColumns") -> "CombinedColumns":
@@ -611,6 +667,8 @@ class CombinedColumns:
                 up = lat[rows] > best[gg]  # Math.max(prev, curr) (keeps prev on ties)
                 best[gg[up]] = lat[rows][up]
                 best_int[gg[up]] = lint[rows][up]
+        out.body = _merge_bodies({f: np.concatenate([self.body[f], other.body[f]]) for f in _BODY_FIELDS}, g, rank,
+                                 head, G)
         out.key = key[head]
         out.meta = meta[head]
         out.combined = n
@@ -625,8 +683,9 @@ class CombinedColumns:
 
     def toJSON(self) -> List[dict]:
         out = []
-        for mi, n, lt, li, mu, cv in zip(self.meta.tolist(), self.combined.tolist(), self.latest.tolist(),
-                                         self.latest_int.tolist(), self.mean.tolist(), self.cv.tolist()):
+        bodies = [self.body[f].tolist() for f in _BODY_FIELDS]
+        for j, (mi, n, lt, li, mu, cv) in enumerate(zip(self.meta.tolist(), self.combined.tolist(), self.latest.tolist(),
+                                                        self.latest_int.tolist(), self.mean.tolist(), self.cv.tolist())):
             m = self.tab.metas[mi]
             out.append(_clean({
                 "uniqueEndpointName": m["uniqueEndpointName"],
@@ -640,6 +699,7 @@ class CombinedColumns:
                 "requestContentType": m["requestContentType"],
                 "responseContentType": m["responseContentType"],
                 "latestTimestamp": int(lt) if li else lt,
+                **{f: bodies[k][j] for k, f in enumerate(_BODY_FIELDS)},
                 "latency": {"mean": mu, "cv": cv},
             }))
         return out

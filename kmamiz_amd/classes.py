@@ -22,6 +22,7 @@ import numpy as np
 
 from . import _lib as L
 from .engine import Engine
+from .envoy import merge, merge_string_body, object_to_interface_string, parse_request_response_body
 from .ingest import (UNDEFINED, Dictionary, dep_identity, explode_url, ingest_json, ingest_rows, ingest_traces,
                      js_truthy, tpl)
 
@@ -284,13 +285,23 @@ def _combine_native(groups, index_base, batch, d: Dictionary, rule, replicas, tr
     # (RealtimeDataList.ts:53-67); bodies reach the output only for
     # application/json, where the reference also infers a schema with
     # json-to-ts (RealtimeDataList.ts:120-155) -- absent here, so refused
-    firsts = None
+    firsts = rows_of = None
     if logs:
         firsts = {}
         srv = np.nonzero(batch.kind == L.KIND_SERVER)[0]
         gid = np.asarray(d.shape_ep[rule], dtype=np.int64)[batch.shape[srv]] * n_status + batch.status[srv]
         for i, g in zip(srv.tolist(), gid.tolist()):
             firsts.setdefault(g, i)
+        # groups whose first row is application/json fold every row's bodies
+        rows_of = {}
+        for g, i in firsts.items():
+            f = _log_fields(traces._span_log(logs, i))
+            if JSON_CT in (f.get("requestContentType"), f.get("responseContentType")):
+                rows_of[g] = []
+        if rows_of:
+            for i, g in zip(srv.tolist(), gid.tolist()):
+                if g in rows_of:
+                    rows_of[g].append(i)
     for g, e, ep_first in _ordered_groups(groups, n_status):
         if e in d.poison[rule]:
             # the reference throws while building the realtime rows (Utils.ts:90)
@@ -317,21 +328,30 @@ def _combine_native(groups, index_base, batch, d: Dictionary, rule, replicas, tr
                     "avgReplica": avg,
                     "latestTimestamp": int(rec["latest_timestamp"]),
                     "latency": {"mean": float(rec["mean"]), "cv": float(rec["cv"])},
-                    **_group_content_types(traces, logs, firsts, g),
+                    **_group_log_fields(traces, logs, firsts, rows_of, g),
                 }
             )
         )
     return out
 
 
-def _group_content_types(traces, logs, firsts, g) -> dict:
+def _group_log_fields(traces, logs, firsts, rows_of, g) -> dict:
+    """The group's content types (its first row's: the reduce starts from it,
+    RealtimeDataList.ts:53-67) and, for application/json, the bodies folded
+    with Utils.MergeStringBody over the group's rows in order, parsed, with
+    their schemas (parseRequestResponseBody, RealtimeDataList.ts:120-155)."""
     if firsts is None:
         return {}
     f = _log_fields(traces._span_log(logs, firsts[g]))
-    ct = {k: f[k] for k in ("requestContentType", "responseContentType") if k in f}
-    if JSON_CT in ct.values():
-        raise NotImplementedError("application/json bodies need json-to-ts schemas (SURVEY.md 8f row 3)")
-    return ct
+    ct = {k: f[k] for k in ("requestContentType", "responseContentType") if f.get(k, UNDEFINED) is not UNDEFINED}
+    if g not in rows_of:
+        return ct
+    req, res = f.get("requestBody", UNDEFINED), f.get("responseBody", UNDEFINED)
+    for i in rows_of[g][1:]:
+        fi = _log_fields(traces._span_log(logs, i))
+        req = merge_string_body(req, fi.get("requestBody", UNDEFINED))
+        res = merge_string_body(res, fi.get("responseBody", UNDEFINED))
+    return {**ct, **parse_request_response_body({**ct, "requestBody": req, "responseBody": res})}
 
 
 def _seq_sum(r, n):
@@ -350,8 +370,11 @@ def _combine_rows(groups, rows, d: Dictionary, n_status):
         first = rows[int(rec["first"])]
         st = d.statuses[g % n_status]
         acc = first.get("replica", UNDEFINED)
-        if js_truthy(acc):
+        cts = (first.get("requestContentType", UNDEFINED), first.get("responseContentType", UNDEFINED))
+        bodies = {}
+        if js_truthy(acc) or JSON_CT in cts:
             uen = sample["uniqueEndpointName"]
+            req, res = first.get("requestBody", UNDEFINED), first.get("responseBody", UNDEFINED)
             seen_first = False
             for r in rows:
                 if r["uniqueEndpointName"] != uen or r.get("status", UNDEFINED) != st:
@@ -362,6 +385,11 @@ def _combine_rows(groups, rows, d: Dictionary, n_status):
                 cur = r.get("replica", UNDEFINED)
                 if js_truthy(acc) and js_truthy(cur):
                     acc = acc + cur
+                req = merge_string_body(req, r.get("requestBody", UNDEFINED))
+                res = merge_string_body(res, r.get("responseBody", UNDEFINED))
+            if JSON_CT in cts:
+                bodies = parse_request_response_body({"requestContentType": cts[0], "responseContentType": cts[1],
+                                                      "requestBody": req, "responseBody": res})
         n = int(rec["combined"])
         out.append(
             _clean(
@@ -379,6 +407,7 @@ def _combine_rows(groups, rows, d: Dictionary, n_status):
                     "latency": {"mean": float(rec["mean"]), "cv": float(rec["cv"])},
                     "requestContentType": first.get("requestContentType", UNDEFINED),
                     "responseContentType": first.get("responseContentType", UNDEFINED),
+                    **bodies,
                 }
             )
         )
@@ -430,8 +459,8 @@ class CombinedRealtimeDataList:
 
     def combineWith(self, rlData: "CombinedRealtimeDataList") -> "CombinedRealtimeDataList":
         """CombinedRealtimeDataList.ts:183-263: group by endpoint+status, sum
-        counts, max timestamps, fold (n, mean, cv) pairwise in list order.
-        (Body/schema merging belongs to SURVEY.md 8f item 3.)"""
+        counts, max timestamps, Utils.Merge the bodies (+ their schemas), fold
+        (n, mean, cv) pairwise in list order."""
         by_key: Dict[str, List[dict]] = {}
         for r in list(self._data) + list(rlData._data):
             by_key.setdefault(f"{r['uniqueEndpointName']}\t{tpl(r.get('status', UNDEFINED))}", []).append(r)
@@ -446,6 +475,13 @@ class CombinedRealtimeDataList:
                 if js_truthy(avg) and js_truthy(xa):
                     avg = avg + xa
                 latest = max(latest, x["latestTimestamp"])
+                # Utils.Merge of the parsed bodies (two absent ones merge to {}),
+                # and the schema of a truthy result (CombinedRealtimeDataList.ts:212-223)
+                for side in ("request", "response"):
+                    b = merge(s.get(side + "Body", UNDEFINED), x.get(side + "Body", UNDEFINED))
+                    s[side + "Body"] = b
+                    if js_truthy(b):
+                        s[side + "Schema"] = object_to_interface_string(b)
             if js_truthy(avg) and "avgReplica" in s:
                 s["avgReplica"] = avg  # the reduce mutates group[0] (208-210)
             s["latestTimestamp"] = latest
@@ -467,6 +503,10 @@ class CombinedRealtimeDataList:
                         "requestContentType": s.get("requestContentType", UNDEFINED),
                         "responseContentType": s.get("responseContentType", UNDEFINED),
                         "latestTimestamp": latest,
+                        "requestBody": s.get("requestBody", UNDEFINED),
+                        "requestSchema": s.get("requestSchema", UNDEFINED),
+                        "responseBody": s.get("responseBody", UNDEFINED),
+                        "responseSchema": s.get("responseSchema", UNDEFINED),
                         "latency": {"mean": _to_precise(m), "cv": _to_precise(c)},
                     }
                 )

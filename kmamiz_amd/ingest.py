@@ -61,7 +61,8 @@ def tpl(v) -> str:
 
 
 def js_truthy(v) -> bool:
-    return not (v is UNDEFINED or v is None or v is False or v == "" or (isinstance(v, (int, float)) and v == 0))
+    return not (v is UNDEFINED or v is None or v is False or v == "" or
+                (isinstance(v, (int, float)) and (v == 0 or v != v)))  # (NaN is falsy)
 
 
 def explode_url(url, service: bool = False) -> List[Any]:

@@ -15,6 +15,11 @@ TypeScript on V8 builtins:
 * ``src/classes/EndpointDependencies.ts:40-657``       -> EndpointDependencies
 * ``src/utils/RiskAnalyzer.ts:10-248``                 -> RiskAnalyzer
 * ``src/utils/Normalizer.ts:17-70``                    -> Normalizer
+* ``src/classes/EnvoyLog.ts:7-149``, ``services/KubernetesService.ts:201-242``
+                                                       -> EnvoyLogs, parse_envoy_logs
+* ``src/utils/Utils.ts:14-75, 279-309`` (Merge, MergeStringBody,
+  ObjectToInterfaceString without json-to-ts)          -> js_merge, merge_string_body,
+                                                          object_to_interface_string
 
 JS semantics reproduced:
 * ``Map``/``Set`` keep the position of the first insertion and the value of the
@@ -36,6 +41,7 @@ fixtures and the synthetic generator (zero padded, so both orders agree).
 """
 from __future__ import annotations
 
+import json
 import math
 import re
 from typing import Any, Dict, List, Optional
@@ -87,6 +93,8 @@ def truthy(v) -> bool:
         return False
     if isinstance(v, float) and math.isnan(v):
         return False
+    if isinstance(v, (dict, list)):
+        return True  # every object is truthy in JS, {} and [] included
     return bool(v)
 
 
@@ -452,10 +460,13 @@ class RealtimeDataList:
                 acc = dict(sub[0])
                 for cur in sub[1:]:
                     acc = dict(acc)
+                    acc["requestBody"] = merge_string_body(get(acc, "requestBody"), get(cur, "requestBody"))
+                    acc["responseBody"] = merge_string_body(get(acc, "responseBody"), get(cur, "responseBody"))
                     acc["timestamp"] = acc["timestamp"] if acc["timestamp"] > cur["timestamp"] else cur["timestamp"]
                     ar, cr = get(acc, "replica"), get(cur, "replica")
                     if truthy(ar) and truthy(cr):
                         acc["replica"] = ar + cr
+                bodies = parse_bodies(acc)
                 rep = get(acc, "replica")
                 combined.append(
                     {
@@ -467,6 +478,7 @@ class RealtimeDataList:
                         "latency": {"mean": to_precise(mean), "cv": to_precise(cv)},
                         "requestContentType": get(acc, "requestContentType"),
                         "responseContentType": get(acc, "responseContentType"),
+                        **bodies,
                     }
                 )
         return CombinedRealtimeDataList(combined)
@@ -615,6 +627,12 @@ class CombinedRealtimeDataList:
                 if truthy(get(prev, "avgReplica")) and truthy(get(cur, "avgReplica")):
                     prev["avgReplica"] = prev["avgReplica"] + cur["avgReplica"]
                 prev["latestTimestamp"] = js_max([prev["latestTimestamp"], cur["latestTimestamp"]])
+                prev["requestBody"] = js_merge(get(prev, "requestBody"), get(cur, "requestBody"))
+                prev["responseBody"] = js_merge(get(prev, "responseBody"), get(cur, "responseBody"))
+                if truthy(prev["requestBody"]):
+                    prev["requestSchema"] = object_to_interface_string(prev["requestBody"])
+                if truthy(prev["responseBody"]):
+                    prev["responseSchema"] = object_to_interface_string(prev["responseBody"])
             acc = {"mean": 0.0, "cv": 0.0, "n": 0}
             for cur in group:
                 m, c = combine_latency_cv_and_mean(
@@ -634,6 +652,10 @@ class CombinedRealtimeDataList:
                     "requestContentType": get(sample, "requestContentType"),
                     "responseContentType": get(sample, "responseContentType"),
                     "latestTimestamp": prev["latestTimestamp"],
+                    "requestBody": get(prev, "requestBody"),
+                    "requestSchema": get(prev, "requestSchema"),
+                    "responseBody": get(prev, "responseBody"),
+                    "responseSchema": get(prev, "responseSchema"),
                     "latency": {"mean": to_precise(acc["mean"]), "cv": to_precise(acc["cv"])},
                 }
             )
@@ -1110,3 +1132,307 @@ class RiskAnalyzer:
                 total += d["combined"]
             out.append({"uniqueServiceName": usn, "metric": ssum / total if total else math.nan})
         return out
+
+
+# --------------------------------------------------------------------------
+# bodies: Utils.Merge / MergeStringBody / ObjectToInterfaceString
+# --------------------------------------------------------------------------
+def js_parse(text):
+    """JSON.parse (SyntaxError -> ValueError).  JS numbers are doubles."""
+    if not isinstance(text, str):
+        raise ValueError("JSON.parse of a non-string")
+
+    def num(tok):
+        v = int(tok)
+        return v if -(2 ** 53) < v < 2 ** 53 else float(tok)
+
+    def bad(tok):
+        raise ValueError(tok)
+
+    return json.loads(text, parse_int=num, parse_constant=bad)
+
+
+def js_stringify(v):
+    """JSON.stringify of a parsed JSON value.  Only ever re-parsed here, so
+    Python's float spelling (1e+16 for 10000000000000000) is equivalent."""
+    if v is UNDEF:
+        return UNDEF
+    return json.dumps(v, ensure_ascii=False, separators=(",", ":"), allow_nan=False)
+
+
+def _spread(x) -> dict:
+    if isinstance(x, dict):
+        return dict(x)
+    if isinstance(x, str):
+        units = x.encode("utf-16-le", "surrogatepass")
+        return {str(k // 2): units[k:k + 2].decode("utf-16-le", "surrogatepass") for k in range(0, len(units), 2)}
+    return {}
+
+
+def js_merge(a, b):
+    """Utils.Merge (Utils.ts:279-291)."""
+    if isinstance(a, list) and isinstance(b, list):
+        return a[:10] + b[:10]
+    if not isinstance(a, list) and not isinstance(b, list):
+        out = _spread(a)
+        out.update(_spread(b))
+        return out
+    return a if truthy(a) else b
+
+
+def merge_string_body(a, b):
+    """Utils.MergeStringBody (Utils.ts:293-309)."""
+    if not (truthy(a) and truthy(b)):
+        return a if truthy(a) else b
+    pa = pb = UNDEF
+    try:
+        pa = js_parse(a)
+    except ValueError:
+        pass
+    try:
+        pb = js_parse(b)
+    except ValueError:
+        pass
+    if truthy(pa) and truthy(pb):
+        return js_stringify(js_merge(pa, pb))
+    return js_stringify(pa if truthy(pa) else pb)
+
+
+JSON_TO_TS = None  # a json-to-ts restatement (obj, rootName) -> [interface strings]; absent
+
+
+def _primitive(v):
+    return not isinstance(v, (dict, list))
+
+
+def _js_typeof(v):
+    if v is None:
+        return "object"
+    if v is UNDEF:
+        return "undefined"
+    if v is True or v is False:
+        return "boolean"
+    return {int: "number", float: "number", str: "string"}.get(type(v), "object")
+
+
+def _sort_obj(o):
+    if isinstance(o, list):
+        return o if all(_primitive(x) for x in o) else [_sort_obj(x) for x in o if not _primitive(x)]
+    out = {}
+    for k in sorted(o, key=lambda t: [ord(c) for c in t.encode("utf-16-be", "surrogatepass").decode("latin-1")]):
+        v = o[k]
+        if isinstance(v, list):
+            if v and all(isinstance(x, dict) for x in v):
+                v = [_sort_obj(x) for x in v]
+        elif isinstance(v, dict):
+            v = _sort_obj(v)
+        out[k] = v
+    return out
+
+
+def _members(o):
+    out = ""
+    for k in o:
+        v = o[k]
+        if not re.match(r"^[A-Za-z_][A-Za-z0-9_]*$", k) or isinstance(v, (dict, list)):
+            return None
+        out += "  %s?: any;\n" % k if v is None else "  %s: %s;\n" % (k, _js_typeof(v))
+    return out
+
+
+def _to_ts(o, root):
+    """JsonToTS (json-to-ts 1.7) for single-interface shapes only (the format
+    of tests/Utils.test.ts:17-30,58-69): a flat object, or a non-empty array
+    of flat objects that all give the same members."""
+    body = None
+    if isinstance(o, dict):
+        body = _members(o)
+    elif isinstance(o, list) and o and all(isinstance(x, dict) for x in o):
+        each = [_members(x) for x in o]
+        body = each[0] if None not in each and len(set(each)) == 1 else None
+    if body is not None:
+        return ["interface %s {\n%s}" % (root, body)]
+    if JSON_TO_TS is None:
+        raise NotImplementedError("json-to-ts")
+    return list(JSON_TO_TS(o, root))
+
+
+def object_to_interface_string(o, name="Root"):
+    """Utils.ObjectToInterfaceString (Utils.ts:14-36)."""
+    if _primitive(o):
+        return _js_typeof(o)
+    so = _sort_obj(o)
+    if isinstance(so, list):
+        if len(o) == 0:
+            return "interface %s extends Array<any>{}" % name
+        if _primitive(o[0]):
+            return "interface %s extends Array<%s>{}" % (name, _js_typeof(o[0]))
+        return "interface %s extends Array<ArrayItem>{}\n" % name + "\n".join(_to_ts(so, "ArrayItem"))
+    return "\n".join(_to_ts(so, name))
+
+
+def parse_bodies(acc):
+    """RealtimeDataList.parseRequestResponseBody (RealtimeDataList.ts:120-155)."""
+    out = {}
+    for side in ("request", "response"):
+        if get(acc, side + "ContentType") != "application/json":
+            continue
+        try:
+            body = js_parse(get(acc, side + "Body"))
+        except ValueError:
+            continue
+        out[side + "Body"] = body
+        out[side + "Schema"] = object_to_interface_string(body)
+    return out
+
+
+# --------------------------------------------------------------------------
+# Envoy logs: KubernetesService.ParseEnvoyLogs + classes/EnvoyLog.ts
+# --------------------------------------------------------------------------
+class Date:
+    """new Date(iso) -> getTime() in ms (NaN if unparsable), fraction truncated."""
+
+    def __init__(self, text):
+        self.text = text
+        m = re.match(r"^(\d{4})-(\d\d)-(\d\d)T(\d\d):(\d\d):(\d\d)(?:\.(\d+))?(Z|[+-]\d\d:\d\d)?$", text or "")
+        if not m:
+            self.t = float("nan")
+            return
+        import datetime
+
+        y, mo, d, h, mi, se, fr, tz = m.groups()
+        try:
+            dt = datetime.datetime(int(y), int(mo), int(d), int(h), int(mi), int(se), tzinfo=datetime.timezone.utc)
+        except ValueError:
+            self.t = float("nan")
+            return
+        ms = int(dt.timestamp()) * 1000 + int(((fr or "") + "000")[:3])
+        if tz and tz != "Z":
+            off = (int(tz[1:3]) * 60 + int(tz[4:6])) * 60000
+            ms = ms - off if tz[0] == "+" else ms + off
+        self.t = float(ms)
+
+    def getTime(self):
+        return self.t
+
+
+def parse_envoy_logs(lines, namespace, pod):
+    """KubernetesService.ParseEnvoyLogs (KubernetesService.ts:201-242)."""
+    term = "\n\r\u2028\u2029"
+    first_trace = {}
+    logs = []
+    for line in lines:
+        cols = line.split("\t")
+        if len(cols) < 2:
+            raise TypeError("log is undefined")
+        t, log = cols[0], cols[1]
+        h = re.search(r"\[(Request|Response) ([A-Za-z0-9_\-]+)/([A-Za-z0-9_]+)/([A-Za-z0-9_]+)/([A-Za-z0-9_]+)\]", log)
+        if not h or not h.group(2):
+            continue
+        typ, rid, tid, sid, pid = h.groups()
+        st = re.search(r"\[Status\] ([0-9]+)", log)
+        mp = re.search(r"(GET|POST|PUT|DELETE|PATCH|HEAD|OPTIONS) ([^\]]+)", log)
+        ct = re.search(r"\[ContentType ([^\]]*)\]", log)
+        bd = re.search("\\[Body\\] ([^" + term + "]*)", log)
+        if rid not in first_trace and tid != "NO_ID":
+            first_trace[rid] = tid
+        e = {"timestamp": Date(t), "type": typ, "requestId": rid, "traceId": tid, "spanId": sid,
+             "parentSpanId": pid, "namespace": namespace, "podName": pod}
+        if mp:
+            e["method"], e["path"] = mp.group(1), mp.group(2)
+        if st:
+            e["status"] = st.group(1)
+        if bd:
+            e["body"] = bd.group(1)
+        if ct:
+            e["contentType"] = ct.group(1)
+        logs.append(e)
+    for e in logs:
+        e["traceId"] = first_trace.get(e["requestId"]) or "NO_ID"
+    return EnvoyLogs(logs)
+
+
+class EnvoyLogs:
+    def __init__(self, logs):
+        self.logs = logs
+
+    def toJSON(self):
+        return self.logs
+
+    def toStructured(self):
+        if not self.logs:
+            return []
+        by_id: Dict[str, Dict[str, dict]] = {}
+        for e in self.logs:
+            by_id.setdefault(js_str(get(e, "requestId")) + "/" + js_str(get(e, "traceId")), {})[get(e, "spanId")] = e
+        if any("NO_ID" in m for m in by_id.values()):
+            return self.toStructuredFallback()
+        res = []
+        for key, spans in by_id.items():
+            parts = key.split("/")
+            traces = []
+            for sid, e in spans.items():
+                par = spans.get(get(e, "parentSpanId"))
+                if get(e, "type") == "Response" and par is not None and get(par, "type") == "Request":
+                    traces.append({"traceId": parts[1], "spanId": sid, "parentSpanId": get(e, "parentSpanId"),
+                                   "request": par, "response": e, "isFallback": False})
+            res.append({"requestId": parts[0], "traces": traces})
+        return res
+
+    def toStructuredFallback(self):
+        if not self.logs:
+            return []
+        groups: Dict[str, List[dict]] = {}
+        for e in self.logs:
+            if truthy(get(e, "requestId")):
+                groups.setdefault(js_str(e["requestId"]) + "/" + js_str(get(e, "traceId")), []).append(e)
+        res = []
+        for key, logs in groups.items():
+            parts = key.split("/")
+            open_reqs = []
+            by_span: Dict[Any, dict] = {}
+            for e in logs:
+                if get(e, "type") == "Request":
+                    open_reqs.append(e)
+                if get(e, "type") == "Response":
+                    if not open_reqs:
+                        continue
+                    q = open_reqs.pop()
+                    by_span[get(q, "spanId")] = {"traceId": parts[1], "request": q, "response": e,
+                                                 "spanId": get(q, "spanId"), "parentSpanId": get(q, "parentSpanId"),
+                                                 "isFallback": True}
+            res.append({"requestId": parts[0], "traces": list(by_span.values())})
+        return res
+
+    @staticmethod
+    def CombineToStructuredEnvoyLogs(all_logs):
+        return EnvoyLogs.FillMissingId(EnvoyLogs.CombineStructuredEnvoyLogs([l.toStructured() for l in all_logs]))
+
+    @staticmethod
+    def CombineStructuredEnvoyLogs(structured):
+        merged: Dict[str, list] = {}
+        for per_service in structured:
+            for l in per_service:
+                merged[l["requestId"]] = merged.get(l["requestId"], []) + l["traces"]
+        out = []
+        for rid, traces in merged.items():
+            times = [t["request"]["timestamp"].getTime() if isinstance(t["request"].get("timestamp"), Date)
+                     else float("nan") for t in traces]
+            if any(x < 0 for x in times):
+                raise NotImplementedError("sort with pre-1970 request times")
+            out.append({"requestId": rid, "traces": traces})  # (comparator >= 0 or NaN: order kept)
+        return out
+
+    @staticmethod
+    def FillMissingId(logs):
+        parents = {}
+        for l in logs:
+            for t in l["traces"]:
+                p = get(t, "parentSpanId")
+                if truthy(p) and p != "NO_ID":
+                    parents[js_str(l["requestId"]) + "/" + js_str(get(t, "spanId"))] = p
+        for l in logs:
+            for t in l["traces"]:
+                p = parents.get(js_str(l["requestId"]) + "/" + js_str(get(t, "spanId")))
+                t["parentSpanId"] = p if truthy(p) else get(t, "parentSpanId")
+        return logs

@@ -3,8 +3,8 @@
 missing or fallback logs) adds request/response bodies and content types to
 the realtime rows; toCombinedRealtimeData keeps the first row's content types
 (RealtimeDataList.ts:53-89).  Rows and combined data must equal the oracle's.
-application/json bodies need json-to-ts schemas (RealtimeDataList.ts:120-155),
-which this build does not have: the mirror refuses them."""
+application/json bodies (MergeStringBody, JSON.parse, schemas) are covered by
+test_envoy_structuring.py."""
 import random
 
 import pytest
@@ -69,16 +69,6 @@ def test_combined_with_logs_equal_oracle(engine, seed):
     for a, b in zip(got, exp):
         for k in ("requestContentType", "responseContentType"):
             assert a.get(k) == b.get(k), k
-
-
-@pytest.mark.gpu
-def test_json_bodies_are_refused(engine):
-    from kmamiz_amd import Traces
-
-    traces = [fixture("MockTracePDAS")]
-    logs = make_logs(traces, random.Random(0), ["application/json"])
-    with pytest.raises(NotImplementedError):
-        Traces(traces, engine=engine).combineLogsToRealtimeData(logs).toCombinedRealtimeData()
 
 
 def test_log_without_response_raises_like_the_reference():
@@ -150,3 +140,25 @@ def test_node_combined_with_logs_equal_oracle(tmp_path):
                  x.get("responseContentType")) for x in rows]
 
     assert key(out["combined"]) == key(exp)
+
+
+@pytest.mark.gpu
+def test_node_combined_with_json_bodies_equal_oracle(tmp_path):
+    """The Node mirror folds application/json bodies (MergeStringBody, JSON.parse,
+    ObjectToInterfaceString) like the oracle; bodies whose schema needs
+    json-to-ts's nested naming are left out (not restated)."""
+    from kmamiz_amd import synth
+    from test_envoy_structuring import JSON_BODIES, json_logs
+
+    batch, off = synth.host_batch(2, 0, 120)
+    traces = synth.to_traces(2, batch, off)
+    logs = json_logs(traces, random.Random(9), [b for b in JSON_BODIES if "deep" not in b])
+    out = _node(tmp_path, traces, logs, True)
+    ref = O.Traces(traces).combineLogsToRealtimeData(logs)
+    assert out["rows"] == O.strip_undef(ref.toJSON())
+    exp = O.strip_undef(ref.toCombinedRealtimeData().toJSON())
+    assert len(out["combined"]) == len(exp)
+    for a, b in zip(out["combined"], exp):
+        for k in ("uniqueEndpointName", "status", "combined", "requestContentType", "responseContentType",
+                  "requestBody", "requestSchema", "responseBody", "responseSchema"):
+            assert a.get(k) == b.get(k), k
