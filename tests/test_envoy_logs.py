@@ -146,13 +146,15 @@ def test_node_combined_with_logs_equal_oracle(tmp_path):
 def test_node_combined_with_json_bodies_equal_oracle(tmp_path):
     """The Node mirror folds application/json bodies (MergeStringBody, JSON.parse,
     ObjectToInterfaceString) like the oracle; bodies whose schema needs
-    json-to-ts's nested naming are left out (not restated)."""
+    json-to-ts's nested naming or quoted members are left out (not restated)."""
     from kmamiz_amd import synth
     from test_envoy_structuring import JSON_BODIES, json_logs
 
     batch, off = synth.host_batch(2, 0, 120)
     traces = synth.to_traces(2, batch, off)
-    logs = json_logs(traces, random.Random(9), [b for b in JSON_BODIES if "deep" not in b])
+    # (a string body spread into an object gives "0", "1", ... members, whose
+    # interface json-to-ts quotes: not restated either)
+    logs = json_logs(traces, random.Random(9), [b for b in JSON_BODIES if "deep" not in b and b != '"str"'])
     out = _node(tmp_path, traces, logs, True)
     ref = O.Traces(traces).combineLogsToRealtimeData(logs)
     assert out["rows"] == O.strip_undef(ref.toJSON())
