@@ -165,6 +165,28 @@ typedef struct kmz_zipkin_batch {
 int kmz_parse_zipkin(const char *json, uint64_t len, int threads, kmz_zipkin_batch **out);
 void kmz_zipkin_free(kmz_zipkin_batch *batch);
 
+/* ---- device ingest: Zipkin JSON -> columns on the GPU ---- */
+/* The same fast path as kmz_parse_zipkin, on the device: the JSON bytes
+ * (host memory: copied to HBM; device memory: read in place, kept valid until
+ * kmz_json_load) are scanned for the span objects and every span is parsed by
+ * its own thread; span ids, parent ids, kinds, durations and timestamps land
+ * in the context's columns.  Shapes and statuses are interned by the raw text
+ * of their fields (hash + byte verification) in first-occurrence order, exactly
+ * as kmz_parse_zipkin numbers them.  KMZ_E_UNSUPPORTED (nothing loaded) for
+ * input outside the fast path, as kmz_parse_zipkin, or on a hash collision
+ * between two distinct shapes: the caller then parses on the host. */
+int kmz_json_parse(kmz_ctx *ctx, const char *json, uint64_t len, int mem, uint64_t *n_spans, uint32_t *n_shapes,
+                   uint32_t *n_statuses);
+/* the distinct raw shapes / statuses of the last kmz_json_parse, in the
+ * kmz_zipkin_batch layout: [n_shapes][7][offset, length], [n_statuses][offset,
+ * length] (length KMZ_JSON_ABSENT: property missing) */
+int kmz_json_fields(kmz_ctx *ctx, uint64_t *shape_fields, uint64_t *status_fields);
+/* make the parsed spans the loaded batch (as kmz_load): raw shape k becomes
+ * shape_of_raw[k], raw status k status_of_raw[k] (< 65536); the identity
+ * tables as kmz_load takes them */
+int kmz_json_load(kmz_ctx *ctx, const uint32_t *shape_of_raw, const uint32_t *status_of_raw, const kmz_shapes *shapes,
+                  uint64_t index_base);
+
 /* ---- lifecycle ---------------------------------------------------------- */
 int kmz_abi_version(void);
 /* stream: hipStream_t to launch on (NULL = the context creates its own). */
@@ -189,6 +211,10 @@ int kmz_get_groups(kmz_ctx *ctx, kmz_group *out, uint64_t cap);
 int kmz_get_endpoints(kmz_ctx *ctx, kmz_endpoint *out, uint64_t cap);
 /* unique edge keys, unordered: key = anc_ep<<40 | desc_ep<<16 | distance<<1 | on */
 int kmz_get_triples(kmz_ctx *ctx, uint64_t *out, uint64_t cap, uint64_t *n_out);
+/* the loaded batch's columns back in host memory (any pointer may be NULL);
+ * e.g. after kmz_json_load, for the per-span host work of small batches */
+int kmz_get_spans(kmz_ctx *ctx, uint64_t *span_id, uint64_t *parent_id, uint8_t *kind, uint32_t *shape,
+                  uint16_t *status, uint32_t *duration, int64_t *timestamp, uint64_t cap);
 /* per span: first non-CLIENT ancestor (KMZ_NONE if none) and, for rows, the
  * row's global first-occurrence index (KMZ_NONE if the span is not a row) */
 int kmz_get_span_links(kmz_ctx *ctx, uint32_t *cparent, uint64_t *rowpos, uint64_t cap);
@@ -358,7 +384,8 @@ void kmz_host_free(void *p);
 #define KMZ_K_SETTLE 12  /* K4 k_chain_settle: staged keys + deferred chain checks */
 #define KMZ_K_TAIL 13    /* service tail: k_tail_links + k_tail_compact           */
 #define KMZ_K_ORDER 14   /* entry order of the reduced graph (KMZ_RUN_DEP_ORDER)  */
-#define KMZ_K_COUNT 15
+#define KMZ_K_JSON 15    /* K1 on the device: kmz_json_parse's kernels            */
+#define KMZ_K_COUNT 16
 int kmz_set_profiling(kmz_ctx *ctx, int on);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);

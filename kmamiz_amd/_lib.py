@@ -35,7 +35,7 @@ ERRORS = {
 }
 
 KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final", "join", "cert", "reduce", "pend", "check",
-           "settle", "tail", "order"]
+           "settle", "tail", "order", "json"]
 SYNTH_BOOKINFO, SYNTH_MESH, SYNTH_POWER = 2, 3, 5
 PART_GROUPS, PART_ENDPOINTS, PART_TRIPLES = 0, 1, 2
 
@@ -158,6 +158,11 @@ SIGNATURES = [
     ("kmz_get_triples", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("kmz_get_span_links", C.c_int, [_P, _P, _P, C.c_uint64]),
     ("kmz_get_dep_entries", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, _P, C.c_uint64]),
+    ("kmz_get_spans", C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, C.c_uint64]),
+    ("kmz_json_parse", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32),
+                                 C.POINTER(C.c_uint32)]),
+    ("kmz_json_fields", C.c_int, [_P, _P, _P]),
+    ("kmz_json_load", C.c_int, [_P, _P, _P, C.POINTER(Shapes), C.c_uint64]),
     ("kmz_fetch", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64]),
     ("kmz_group_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_endpoint_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),

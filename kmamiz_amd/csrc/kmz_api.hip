@@ -59,6 +59,13 @@ struct kmz_ctx {
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n, cetab;  // K4 chain interning
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
+  // device JSON ingest (kmz_json.hip)
+  DevBuf j_buf, j_elem, j_state, j_jsc, j_mask, j_cnt, j_off, j_csc, j_small, j_starts, j_slices, j_tslot, j_stab,
+      j_ttab, j_reps, j_smap, j_tmap;
+  uint64_t j_n = 0, j_scap = 0, j_tcap = 0;
+  bool j_ready = false;
+  std::vector<uint64_t> j_sfields, j_tfields;  // raw shapes / statuses, first-occurrence order
+  std::vector<uint32_t> j_sslots, j_tslots;    // their table slots
   DevBuf o_key, o_val, o_out, o_rts, o_rsh;  // reduced-graph entry order (kmz_order.hip; o_key = the slot table)
   uint64_t o_n = 0;
   DevBuf imap_l, imap_g;  // local -> global flatten-index runs of a non-contiguous shard (kmz_shard.hip)
@@ -292,7 +299,9 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
                     &c->tl_sstat, &c->tl_rel, &c->o_key, &c->o_val, &c->o_out,
-                    &c->o_rts, &c->o_rsh};
+                    &c->o_rts, &c->o_rsh, &c->j_buf, &c->j_elem, &c->j_state, &c->j_jsc, &c->j_mask,
+                    &c->j_cnt, &c->j_off, &c->j_csc, &c->j_small, &c->j_starts, &c->j_slices, &c->j_tslot,
+                    &c->j_stab, &c->j_ttab, &c->j_reps, &c->j_smap, &c->j_tmap};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   if (c->hpin) hipHostFree(c->hpin);
@@ -381,6 +390,190 @@ int kmz_load(kmz_ctx *c, const kmz_spans *s, const kmz_shapes *sh, int where) {
     c->ts = P<int64_t>(c->in_ts);
   }
   c->loaded = true;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+// ---- K1 on the device: Zipkin JSON -> columns (kmz_json.hip) -----------------
+namespace {
+// the distinct entries of one interning table, sorted by first occurrence:
+// fields (offset, length) pairs and table slots
+int json_collect(kmz_ctx *c, DevBuf &tab, uint64_t cap, uint32_t first, uint32_t nf, uint64_t nspan,
+                 std::vector<uint64_t> &fields, std::vector<uint32_t> &slots) {
+  unsigned long long *cnt = P<unsigned long long>(c->j_small) + 4;
+  uint64_t ocap = std::min<uint64_t>(cap, 1ull << 16);
+  for (;;) {
+    if (ensure(c, c->j_reps, ocap * (2 + nf) * 8)) return KMZ_E_HIP;
+    HIPCHK(c, hipMemsetAsync(cnt, 0, 8, c->stream));
+    launch_json_reps(c->stream, P<unsigned long long>(tab), cap, P<unsigned long long>(c->j_slices), first, nf,
+                     P<unsigned long long>(c->j_reps), ocap, nspan, cnt);
+    HIPCHK(c, hipGetLastError());
+    unsigned long long m = 0;
+    HIPCHK(c, hipMemcpyAsync(&m, cnt, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (m > ocap) {
+      ocap = m;
+      continue;
+    }
+    std::vector<uint64_t> h((size_t)m * (2 + nf));
+    if (m) HIPCHK(c, hipMemcpy(h.data(), c->j_reps.p, h.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> order((size_t)m);
+    for (uint32_t k = 0; k < m; ++k) order[k] = k;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return h[(size_t)a * (2 + nf)] < h[(size_t)b * (2 + nf)]; });
+    fields.assign((size_t)m * nf * 2, 0);
+    slots.assign((size_t)m, 0);
+    for (uint32_t r = 0; r < m; ++r) {
+      const uint64_t *e = &h[(size_t)order[r] * (2 + nf)];
+      slots[r] = (uint32_t)e[1];
+      for (uint32_t f = 0; f < nf; ++f) {
+        const uint64_t sl = e[2 + f], ln = sl & 0xFFFFFFull;
+        fields[((size_t)r * nf + f) * 2] = ln == 0xFFFFFFull ? 0 : (sl >> 24);
+        fields[((size_t)r * nf + f) * 2 + 1] = ln == 0xFFFFFFull ? KMZ_JSON_ABSENT : ln;
+      }
+    }
+    return KMZ_OK;
+  }
+}
+}  // namespace
+
+int kmz_json_parse(kmz_ctx *c, const char *json, uint64_t len, int mem, uint64_t *n_spans, uint32_t *n_shapes,
+                   uint32_t *n_statuses) {
+  if (!c || (!json && len) || !n_spans || !n_shapes || !n_statuses) return KMZ_E_ARG;
+  hipSetDevice(c->device);
+  c->j_ready = false;
+  c->loaded = false;  // the context's columns are rewritten
+  c->ran = 0;
+  c->hpin_valid = false;
+  if (len == 0) return KMZ_E_UNSUPPORTED;
+  const uint64_t nch = (len + JCHUNK - 1) / JCHUNK;
+  const uint8_t *b = reinterpret_cast<const uint8_t *>(json);
+  if (mem == KMZ_MEM_HOST) {
+    if (ensure(c, c->j_buf, len + JCHUNK)) return KMZ_E_HIP;
+    HIPCHK(c, hipMemcpyAsync(c->j_buf.p, json, len, hipMemcpyHostToDevice, c->stream));
+    b = P<uint8_t>(c->j_buf);
+  }
+  const uint64_t sc = json_scan_scratch(nch);
+  if (ensure(c, c->j_elem, nch * sizeof(JElem)) || ensure(c, c->j_state, nch * sizeof(JElem)) ||
+      ensure(c, c->j_jsc, sc * sizeof(JElem)) || ensure(c, c->j_mask, nch * 8) || ensure(c, c->j_cnt, nch * 4) ||
+      ensure(c, c->j_off, nch * 4) || ensure(c, c->j_csc, sc * 4) || ensure(c, c->j_small, 64))
+    return KMZ_E_HIP;
+  // j_small: [0..12) JElem total, [16) u32 count total, [20) u32 flags, [32) u64 rep count
+  uint8_t *sm = P<uint8_t>(c->j_small);
+  unsigned int *flags = reinterpret_cast<unsigned int *>(sm + 20);
+  HIPCHK(c, hipMemsetAsync(sm, 0, 64, c->stream));
+  {
+    Timed t(c, KMZ_K_JSON);
+    launch_json_structure(c->stream, b, len, nch, P<JElem>(c->j_elem), P<JElem>(c->j_state),
+                          reinterpret_cast<JElem *>(sm), P<JElem>(c->j_jsc), P<unsigned long long>(c->j_mask),
+                          P<uint32_t>(c->j_cnt), P<uint32_t>(c->j_off), reinterpret_cast<uint32_t *>(sm + 16),
+                          P<uint32_t>(c->j_csc), flags);
+  }
+  HIPCHK(c, hipGetLastError());
+  uint8_t hs[32];
+  HIPCHK(c, hipMemcpyAsync(hs, sm, 32, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  JElem tot;
+  uint32_t n32, fl;
+  memcpy(&tot, hs, sizeof(tot));
+  memcpy(&n32, hs + 16, 4);
+  memcpy(&fl, hs + 20, 4);
+  if ((fl & JF_BAD) || !(fl & JF_TOP) || tot.p != 0 || tot.d0 != 0) return KMZ_E_UNSUPPORTED;
+  const uint64_t n = n32;
+  // interning tables at load <= 1/2 for the shapes a realtime window has
+  // (tens of thousands); a fuller table flags JF_FULL and the spans are parsed
+  // again with a larger one
+  uint64_t scap = 1024, tcap = 4096;
+  while (scap < 2 * n + 1024 && scap < (1ull << 20)) scap *= 2;
+  if (ensure(c, c->j_starts, (n + 1) * 8) || ensure(c, c->in_sid, (n + 1) * 8) || ensure(c, c->in_pid, (n + 1) * 8) ||
+      ensure(c, c->in_kind, n + 1) || ensure(c, c->in_shape, (n + 1) * 4) || ensure(c, c->in_status, (n + 1) * 2) ||
+      ensure(c, c->in_dur, (n + 1) * 4) || ensure(c, c->in_ts, (n + 1) * 8) || ensure(c, c->j_slices, (n + 1) * 64) ||
+      ensure(c, c->j_tslot, (n + 1) * 4))
+    return KMZ_E_HIP;
+  {
+    Timed t(c, KMZ_K_JSON);
+    launch_json_starts(c->stream, P<unsigned long long>(c->j_mask), P<uint32_t>(c->j_off), nch,
+                       P<unsigned long long>(c->j_starts));
+  }
+  for (int attempt = 0;; ++attempt) {
+    if (ensure(c, c->j_stab, scap * 16) || ensure(c, c->j_ttab, tcap * 16)) return KMZ_E_HIP;
+    HIPCHK(c, hipMemsetAsync(c->j_stab.p, 0, scap * 16, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->j_ttab.p, 0, tcap * 16, c->stream));
+    HIPCHK(c, hipMemsetAsync(flags, 0, 4, c->stream));
+    {
+      Timed t(c, KMZ_K_JSON);
+      launch_json_spans(c->stream, b, len, P<unsigned long long>(c->j_starts), n, P<uint64_t>(c->in_sid),
+                        P<uint64_t>(c->in_pid), P<uint8_t>(c->in_kind), P<uint32_t>(c->in_dur), P<int64_t>(c->in_ts),
+                        P<unsigned long long>(c->j_slices), P<uint32_t>(c->in_shape), P<uint32_t>(c->j_tslot),
+                        P<unsigned long long>(c->j_stab), scap, P<unsigned long long>(c->j_ttab), tcap, flags);
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(&fl, flags, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (fl & JF_BAD) return KMZ_E_UNSUPPORTED;
+    if (!(fl & JF_FULL)) {
+      if (fl & JF_COLLIDE) return KMZ_E_UNSUPPORTED;
+      break;
+    }
+    if (attempt >= 6) return KMZ_E_UNSUPPORTED;
+    scap *= 4;
+    tcap *= 4;
+  }
+  int r = json_collect(c, c->j_stab, scap, 0, 7, n, c->j_sfields, c->j_sslots);
+  if (!r) r = json_collect(c, c->j_ttab, tcap, 7, 1, n, c->j_tfields, c->j_tslots);
+  if (r) return r;
+  c->j_n = n;
+  c->j_scap = scap;
+  c->j_tcap = tcap;
+  c->j_ready = true;
+  *n_spans = n;
+  *n_shapes = (uint32_t)c->j_sslots.size();
+  *n_statuses = (uint32_t)c->j_tslots.size();
+  return KMZ_OK;
+}
+
+int kmz_json_fields(kmz_ctx *c, uint64_t *shape_fields, uint64_t *status_fields) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->j_ready) return fail(c, KMZ_E_STATE, "kmz_json_fields before a successful kmz_json_parse");
+  if (shape_fields && !c->j_sfields.empty()) memcpy(shape_fields, c->j_sfields.data(), c->j_sfields.size() * 8);
+  if (status_fields && !c->j_tfields.empty()) memcpy(status_fields, c->j_tfields.data(), c->j_tfields.size() * 8);
+  return KMZ_OK;
+}
+
+int kmz_json_load(kmz_ctx *c, const uint32_t *shape_of_raw, const uint32_t *status_of_raw, const kmz_shapes *shapes,
+                  uint64_t index_base) {
+  if (!c || !shapes) return KMZ_E_ARG;
+  if (!c->j_ready) return fail(c, KMZ_E_STATE, "kmz_json_load before a successful kmz_json_parse");
+  const size_t ns = c->j_sslots.size(), nt = c->j_tslots.size();
+  if ((ns && !shape_of_raw) || (nt && !status_of_raw)) return KMZ_E_ARG;
+  std::vector<uint32_t> sm(c->j_scap, 0), tm(c->j_tcap, 0);
+  for (size_t k = 0; k < ns; ++k) sm[c->j_sslots[k]] = shape_of_raw[k];
+  for (size_t k = 0; k < nt; ++k) {
+    if (status_of_raw[k] > 0xFFFFu) return fail(c, KMZ_E_RANGE, "status id >= 65536");
+    tm[c->j_tslots[k]] = status_of_raw[k];
+  }
+  int r = load_shapes(c, shapes);
+  if (r) return r;
+  if (ensure(c, c->j_smap, sm.size() * 4) || ensure(c, c->j_tmap, tm.size() * 4)) return KMZ_E_HIP;
+  HIPCHK(c, hipMemcpyAsync(c->j_smap.p, sm.data(), sm.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->j_tmap.p, tm.data(), tm.size() * 4, hipMemcpyHostToDevice, c->stream));
+  launch_json_remap(c->stream, c->j_n, P<uint32_t>(c->in_shape), P<uint32_t>(c->j_tslot), P<uint16_t>(c->in_status),
+                    P<uint32_t>(c->j_smap), P<uint32_t>(c->j_tmap));
+  HIPCHK(c, hipGetLastError());
+  c->n = c->j_n;
+  c->index_base = index_base;
+  c->imap_n = 0;
+  c->ran = 0;
+  c->table_hint = false;
+  c->hpin_valid = false;
+  c->sid = P<uint64_t>(c->in_sid);
+  c->pid = P<uint64_t>(c->in_pid);
+  c->kind = P<uint8_t>(c->in_kind);
+  c->shape = P<uint32_t>(c->in_shape);
+  c->status = P<uint16_t>(c->in_status);
+  c->dur = P<uint32_t>(c->in_dur);
+  c->ts = P<int64_t>(c->in_ts);
+  c->loaded = true;
+  c->j_ready = false;  // the columns now hold the caller's ids
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KMZ_OK;
 }
@@ -993,6 +1186,25 @@ int kmz_fetch(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint
       eps[e].external = f == ~0ull ? 0u : (uint32_t)((f & 1) == 0);
     }
   }
+  return KMZ_OK;
+}
+
+int kmz_get_spans(kmz_ctx *c, uint64_t *span_id, uint64_t *parent_id, uint8_t *kind, uint32_t *shape,
+                  uint16_t *status, uint32_t *duration, int64_t *timestamp, uint64_t cap) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->loaded) return fail(c, KMZ_E_STATE, "no batch loaded");
+  if (cap < c->n) return fail(c, KMZ_E_ARG, "output too small");
+  const uint64_t n = c->n;
+  if (n) {
+    if (span_id) HIPCHK(c, hipMemcpyAsync(span_id, c->sid, n * 8, hipMemcpyDeviceToHost, c->stream));
+    if (parent_id) HIPCHK(c, hipMemcpyAsync(parent_id, c->pid, n * 8, hipMemcpyDeviceToHost, c->stream));
+    if (kind) HIPCHK(c, hipMemcpyAsync(kind, c->kind, n, hipMemcpyDeviceToHost, c->stream));
+    if (shape) HIPCHK(c, hipMemcpyAsync(shape, c->shape, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (status) HIPCHK(c, hipMemcpyAsync(status, c->status, n * 2, hipMemcpyDeviceToHost, c->stream));
+    if (duration) HIPCHK(c, hipMemcpyAsync(duration, c->dur, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (timestamp) HIPCHK(c, hipMemcpyAsync(timestamp, c->ts, n * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return KMZ_OK;
 }
 

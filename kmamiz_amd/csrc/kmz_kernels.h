@@ -168,4 +168,26 @@ void launch_dep_order(hipStream_t s, const uint8_t *kind, const uint32_t *shape,
                       int64_t *row_ts, uint32_t *row_shape, unsigned int *counters);
 uint64_t dep_order_slot_bytes();
 
+// Zipkin JSON -> columns on the device (kmz_json.hip)
+struct JElem {
+  int p, d0, d1;  // quote parity; depth change if the chunk starts outside / inside a string
+};
+constexpr uint32_t JCHUNK = 64;
+constexpr uint32_t JF_BAD = 1, JF_COLLIDE = 2, JF_TOP = 4, JF_FULL = 8;
+uint64_t json_scan_scratch(uint64_t n);
+void launch_json_structure(hipStream_t s, const uint8_t *b, uint64_t len, uint64_t nch, JElem *elem, JElem *state,
+                           JElem *jtotal, JElem *jscratch, unsigned long long *mask, uint32_t *cnt, uint32_t *off,
+                           uint32_t *ctotal, uint32_t *cscratch, unsigned int *flags);
+void launch_json_starts(hipStream_t s, const unsigned long long *mask, const uint32_t *off, uint64_t nch,
+                        unsigned long long *starts);
+void launch_json_spans(hipStream_t s, const uint8_t *b, uint64_t len, const unsigned long long *starts, uint64_t n,
+                       uint64_t *sid, uint64_t *pid, uint8_t *kind, uint32_t *dur, int64_t *ts,
+                       unsigned long long *slices, uint32_t *shape_slot, uint32_t *status_slot, unsigned long long *stab,
+                       uint64_t scap, unsigned long long *ttab, uint64_t tcap, unsigned int *flags);
+void launch_json_reps(hipStream_t s, const unsigned long long *tab, uint64_t cap, const unsigned long long *slices,
+                      uint32_t first, uint32_t nf, unsigned long long *out, uint64_t ocap, uint64_t nspan,
+                      unsigned long long *count);
+void launch_json_remap(hipStream_t s, uint64_t n, uint32_t *shape, const uint32_t *status_slot, uint16_t *status,
+                       const uint32_t *smap, const uint32_t *tmap);
+
 }  // namespace kmz

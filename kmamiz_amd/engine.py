@@ -146,6 +146,53 @@ class Engine:
         self.n_dep_ep = shapes.n_dep_ep
         self.n_status = max(1, shapes.n_status)
 
+    # ---- K1 on the device: Zipkin JSON -> columns (kmz_json_parse) -------------
+    def json_parse(self, data=None, ptr: Optional[int] = None, length: int = 0, device: bool = False):
+        """Parse Trace[][] JSON on the GPU: ``data`` (bytes-like, host) or a raw
+        ``ptr`` + ``length`` (host memory, e.g. pinned, or device memory with
+        device=True).  -> (n_spans, n_shapes, n_statuses), or None outside the
+        fast path (nothing loaded: parse on the host)."""
+        n, ns, nt = C.c_uint64(), C.c_uint32(), C.c_uint32()
+        if ptr is None:
+            buf = data if isinstance(data, bytes) else bytes(data)
+            src, length = C.c_char_p(buf), len(buf)
+        else:
+            src = C.c_void_p(ptr)
+        rc = self._lib.kmz_json_parse(self.ctx, src, length, L.MEM_DEVICE if device else L.MEM_HOST, C.byref(n),
+                                      C.byref(ns), C.byref(nt))
+        if rc == L.E_UNSUPPORTED:
+            return None
+        L.check(self.ctx, rc)
+        return int(n.value), int(ns.value), int(nt.value)
+
+    def json_fields(self, n_shapes: int, n_statuses: int):
+        """(shape_fields [n_shapes*7, 2], status_fields [n_statuses, 2]) of the last json_parse."""
+        sf = np.zeros((max(1, n_shapes) * 7, 2), np.uint64)
+        tf = np.zeros((max(1, n_statuses), 2), np.uint64)
+        L.check(self.ctx, self._lib.kmz_json_fields(self.ctx, L.ptr(sf), L.ptr(tf)))
+        return sf[: n_shapes * 7], tf[:n_statuses]
+
+    def json_load(self, shape_of_raw: np.ndarray, status_of_raw: np.ndarray, shapes: ShapeTable, index_base: int = 0,
+                  n: Optional[int] = None):
+        sm = np.ascontiguousarray(shape_of_raw, dtype=np.uint32)
+        tm = np.ascontiguousarray(status_of_raw, dtype=np.uint32)
+        sh = shapes.c_struct()
+        L.check(self.ctx, self._lib.kmz_json_load(self.ctx, L.ptr(sm), L.ptr(tm), C.byref(sh), index_base))
+        self.n = n if n is not None else self.n
+        self.index_base = index_base
+        self.n_dep_ep = shapes.n_dep_ep
+        self.n_status = max(1, shapes.n_status)
+
+    def spans(self) -> SpanBatch:
+        """The loaded batch's columns, copied to the host (kmz_get_spans)."""
+        n = self.n
+        cols = dict(span_id=np.zeros(n, np.uint64), parent_id=np.zeros(n, np.uint64), kind=np.zeros(n, np.uint8),
+                    shape=np.zeros(n, np.uint32), status=np.zeros(n, np.uint16), duration=np.zeros(n, np.uint32),
+                    timestamp=np.zeros(n, np.int64))
+        L.check(self.ctx, self._lib.kmz_get_spans(self.ctx, *(L.ptr(cols[k]) for k in (
+            "span_id", "parent_id", "kind", "shape", "status", "duration", "timestamp")), n))
+        return SpanBatch(index_base=self.index_base, **cols)
+
     def load_synthetic(self, config: int, seed: int, trace_begin: int, trace_end: int) -> int:
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_synth_load(self.ctx, config, seed, trace_begin, trace_end, C.byref(n)))

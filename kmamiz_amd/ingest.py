@@ -391,6 +391,48 @@ def ingest_rows(rows: Sequence[dict]):
     return batch, table, d, first_row
 
 
+def dictionary_from_fields(data: bytes, sf: np.ndarray, tf: np.ndarray):
+    """The Dictionary of a parsed batch from its raw shape / status slices
+    ([n*7, 2] and [n, 2] (offset, length) into ``data``): the identity rules run
+    once per distinct shape, on one json.loads of all slices.  -> (Dictionary,
+    raw shape -> shape id, raw status -> status id)."""
+    import json
+
+    from . import _lib as L
+
+    ns, nt = len(sf) // 7, len(tf)
+    fields = np.concatenate([sf.reshape(-1, 2), tf.reshape(-1, 2)]).tolist()
+    present = [ln != L.JSON_ABSENT for _, ln in fields]
+    dec = iter(json.loads(b"[" + b",".join(data[o:o + ln] for (o, ln), p in zip(fields, present) if p) + b"]"))
+    vals = [next(dec) if p else UNDEFINED for p in present]
+    d = Dictionary()
+    smap = np.zeros(max(1, ns), dtype=np.uint32)
+    for i in range(ns):
+        v = vals[7 * i:7 * i + 7]
+        tags = {t: x for t, x in zip(SHAPE_TAGS, v[1:]) if x is not UNDEFINED}
+        smap[i] = d.shape_id(v[0], tags)
+    tmap = np.zeros(max(1, nt), dtype=np.uint32)
+    for i in range(nt):
+        tmap[i] = d.status_id(vals[7 * ns + i])
+    if len(d.statuses) > 65535:
+        raise ValueError("more than 65535 distinct status strings")
+    return d, smap, tmap
+
+
+def ingest_json_device(eng, data: bytes, index_base: int = 0):
+    """Zipkin Trace[][] JSON bytes parsed on the GPU (kmz_json_parse, K1) and
+    loaded as the engine's batch: -> (Dictionary, n_spans), or None when the
+    batch is outside the fast path (nothing loaded; parse on the host)."""
+    r = eng.json_parse(data)
+    if r is None:
+        return None
+    n, ns, nt = r
+    sf, tf = eng.json_fields(ns, nt)
+    d, smap, tmap = dictionary_from_fields(data, sf, tf)
+    eng.json_load(smap[:ns], tmap[:nt], d.shape_table(), index_base, n=n)
+    return d, n
+
+
 def ingest_json(data: bytes, index_base: int = 0, threads: int = 0):
     """Zipkin Trace[][] JSON bytes -> (SpanBatch, Dictionary) through the native
     parser (kmz_parse_zipkin), or None when the batch is
@@ -417,29 +459,12 @@ def ingest_json(data: bytes, index_base: int = 0, threads: int = 0):
         sid, pid = col(b.span_id, np.uint64), col(b.parent_id, np.uint64)
         kind, dur, ts = col(b.kind, np.uint8), col(b.duration, np.uint32), col(b.timestamp, np.int64)
         shp, sts = col(b.shape, np.uint32), col(b.status, np.uint32)
-        absent = L.JSON_ABSENT
         ns, nt = int(b.n_shapes), int(b.n_statuses)
         sf = np.ctypeslib.as_array(b.shape_fields, shape=(max(1, ns) * 14,))[: ns * 14].reshape(ns * 7, 2)
         tf = np.ctypeslib.as_array(b.status_fields, shape=(max(1, nt) * 2,))[: nt * 2].reshape(nt, 2)
-        # every raw field slice decoded by one json.loads of "[s0,s1,...]"
-        fields = np.concatenate([sf, tf]).tolist()
-        present = [ln != absent for _, ln in fields]
-        dec = iter(json.loads(b"[" + b",".join(data[o:o + ln] for (o, ln), p in zip(fields, present) if p) + b"]"))
-        vals = [next(dec) if p else UNDEFINED for p in present]
-
-        d = Dictionary()
-        smap = np.zeros(max(1, ns), dtype=np.uint32)
-        for i in range(ns):
-            v = vals[7 * i:7 * i + 7]
-            tags = {t: x for t, x in zip(SHAPE_TAGS, v[1:]) if x is not UNDEFINED}
-            smap[i] = d.shape_id(v[0], tags)
-        tmap = np.zeros(max(1, nt), dtype=np.uint32)
-        for i in range(nt):
-            tmap[i] = d.status_id(vals[7 * ns + i])
+        d, smap, tmap = dictionary_from_fields(data, sf, tf)
     finally:
         L.lib().kmz_zipkin_free(out)
-    if len(d.statuses) > 65535:
-        raise ValueError("more than 65535 distinct status strings")
     batch = SpanBatch(sid, pid, kind, smap[shp] if n else shp, (tmap[sts] if n else sts).astype(np.uint16), dur,
                       ts, index_base)
     return batch, d

@@ -10,6 +10,11 @@ Stages, each timed on its own and as one chain (median of `reps`):
             and the reduced dependency graph (MockData: the exact per-row
             toEndpointDependencies() JSON and combineWith([]).trim())
 
+and the same chain with K1 on the GPU (kmz_json_parse, kmz_json.hip): the JSON
+bytes go to HBM (from pageable memory, and from a pinned buffer as an HTTP
+client would receive into), are parsed there, the distinct shapes come back
+for the identity rules, and the batch is loaded without a column H2D.
+
 usage: python tools/bench_e2e.py [config2_traces]  -> one JSON line
 """
 import json
@@ -102,10 +107,73 @@ def config2(eng, ntr, reps=5):
         "groups/edge_keys": res}}
 
 
+def device_json(eng, config, ntr, reps=5):
+    import ctypes as C
+
+    from kmamiz_amd.ingest import dictionary_from_fields
+
+    b, off = synth.host_batch(config, 0, ntr)
+    data = json.dumps(synth.to_traces(config, b, off)).encode()
+    n = len(b)
+    pin = L.lib().kmz_host_alloc(len(data))
+    C.memmove(pin, data, len(data))
+    eng.set_profiling(True)
+
+    def parse(pinned):
+        r = eng.json_parse(ptr=pin, length=len(data)) if pinned else eng.json_parse(data)
+        assert r is not None and r[0] == n
+        return r
+
+    tp, _ = med(lambda: parse(False), reps)
+    eng.kernel_times(reset=True)
+    tq, r = med(lambda: parse(True), reps)
+    kt = eng.kernel_times(reset=True)
+    json_ms = kt["json"][0] / reps
+    _, ns, nt = r
+
+    def ident():
+        sf, tf = eng.json_fields(ns, nt)
+        d, smap, tmap = dictionary_from_fields(data, sf, tf)
+        eng.json_load(smap[:ns], tmap[:nt], d.shape_table(), 0, n=n)
+        return d
+
+    tis = []
+    for _ in range(reps):  # (each load consumes its parse)
+        parse(True)
+        t0 = time.perf_counter()
+        ident()
+        tis.append(time.perf_counter() - t0)
+    ti = statistics.median(tis)
+
+    def run():
+        eng.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        eng.sync()
+
+    tr, _ = med(run, reps)
+
+    def chain():
+        parse(True)
+        ident()
+        run()
+        g, k, e = eng.fetch()
+        return len(k)
+
+    tc, _ = med(chain, reps)
+    eng.set_profiling(False)
+    L.lib().kmz_host_free(C.c_void_p(pin))
+    return {f"config{config} device JSON": {
+        "spans": n, "json_bytes": len(data), "parse_pageable_ms": round(tp * 1e3, 2),
+        "parse_pinned_ms": round(tq * 1e3, 2), "json_kernels_ms": round(json_ms, 3),
+        "kernel_GB_per_s": round(len(data) / (json_ms * 1e-3) / 1e9, 1) if json_ms else None,
+        "identities_and_load_ms": round(ti * 1e3, 2), "run_ms": round(tr * 1e3, 3), "chain_ms": round(tc * 1e3, 2),
+        "end_to_end_spans_per_s": round(n / tc), "parse_pinned_spans_per_s": round(n / tq)}}
+
+
 def main():
     ntr = int(sys.argv[1]) if len(sys.argv) > 1 else 136000
     eng = Engine(0)
-    out = {"tool": "tools/bench_e2e.py", **mockdata(eng), **config2(eng, ntr)}
+    out = {"tool": "tools/bench_e2e.py", **mockdata(eng), **config2(eng, ntr), **device_json(eng, 2, ntr),
+           **device_json(eng, 3, ntr // 4)}
     eng.close()
     print(json.dumps(out))
 
