@@ -183,9 +183,18 @@ int kmz_json_parse(kmz_ctx *ctx, const char *json, uint64_t len, int mem, uint64
 int kmz_json_fields(kmz_ctx *ctx, uint64_t *shape_fields, uint64_t *status_fields);
 /* make the parsed spans the loaded batch (as kmz_load): raw shape k becomes
  * shape_of_raw[k], raw status k status_of_raw[k] (< 65536); the identity
- * tables as kmz_load takes them */
+ * tables as kmz_load takes them.  The context remembers these ids by the raw
+ * JSON text of each shape / status (kmz_json_known). */
 int kmz_json_load(kmz_ctx *ctx, const uint32_t *shape_of_raw, const uint32_t *status_of_raw, const kmz_shapes *shapes,
                   uint64_t index_base);
+/* Identities across batches (a realtime worker sees the same endpoints every
+ * window): after kmz_json_parse, the id given in an earlier kmz_json_load to
+ * the same raw text, per raw shape / status of this batch, or KMZ_NONE (new:
+ * the caller runs the identity rules for those only).  Exact: keyed by the
+ * raw bytes, not a hash.  kmz_json_forget drops what was remembered (the
+ * caller's dictionary was reset). */
+int kmz_json_known(kmz_ctx *ctx, uint32_t *shape_of_raw, uint32_t *status_of_raw);
+int kmz_json_forget(kmz_ctx *ctx);
 
 /* ---- lifecycle ---------------------------------------------------------- */
 int kmz_abi_version(void);

@@ -163,6 +163,8 @@ SIGNATURES = [
                                  C.POINTER(C.c_uint32)]),
     ("kmz_json_fields", C.c_int, [_P, _P, _P]),
     ("kmz_json_load", C.c_int, [_P, _P, _P, C.POINTER(Shapes), C.c_uint64]),
+    ("kmz_json_known", C.c_int, [_P, _P, _P]),
+    ("kmz_json_forget", C.c_int, [_P]),
     ("kmz_fetch", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64]),
     ("kmz_group_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_endpoint_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),

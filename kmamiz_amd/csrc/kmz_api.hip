@@ -8,6 +8,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "kmz_kernels.h"
@@ -66,6 +68,10 @@ struct kmz_ctx {
   bool j_ready = false;
   std::vector<uint64_t> j_sfields, j_tfields;  // raw shapes / statuses, first-occurrence order
   std::vector<uint32_t> j_sslots, j_tslots;    // their table slots
+  // identities across batches: raw JSON text of a shape's seven fields (or of
+  // a status) -> the id the caller gave it in kmz_json_load
+  std::unordered_map<std::string, uint32_t> j_known_s, j_known_t;
+  std::vector<std::string> j_skeys, j_tkeys;  // the current batch's raw keys
   DevBuf o_key, o_val, o_out, o_rts, o_rsh;  // reduced-graph entry order (kmz_order.hip; o_key = the slot table)
   uint64_t o_n = 0;
   DevBuf imap_l, imap_g;  // local -> global flatten-index runs of a non-contiguous shard (kmz_shard.hip)
@@ -434,7 +440,60 @@ int json_collect(kmz_ctx *c, DevBuf &tab, uint64_t cap, uint32_t first, uint32_t
     return KMZ_OK;
   }
 }
+// the raw keys (per field: u32 length or ~0 + bytes) of the distinct entries,
+// from the caller's buffer (host) or gathered on the device
+int json_keys(kmz_ctx *c, const char *json, int mem, uint32_t nf, const std::vector<uint64_t> &fields,
+              std::vector<std::string> &keys) {
+  const size_t m = fields.size() / (2 * nf);
+  keys.assign(m, std::string());
+  std::vector<char> dev;
+  const char *src = json;
+  if (mem != KMZ_MEM_HOST) {  // copy the spans' byte range once (fields are offsets into it)
+    uint64_t lo = ~0ull, hi = 0;
+    for (size_t k = 0; k < fields.size(); k += 2)
+      if (fields[k + 1] != KMZ_JSON_ABSENT) {
+        lo = std::min(lo, fields[k]);
+        hi = std::max(hi, fields[k] + fields[k + 1]);
+      }
+    if (hi > lo) {
+      dev.resize(hi - lo);
+      HIPCHK(c, hipMemcpy(dev.data(), json + lo, hi - lo, hipMemcpyDeviceToHost));
+      src = dev.data() - lo;
+    }
+  }
+  for (size_t e = 0; e < m; ++e) {
+    std::string &k = keys[e];
+    for (uint32_t f = 0; f < nf; ++f) {
+      const uint64_t off = fields[(e * nf + f) * 2], len = fields[(e * nf + f) * 2 + 1];
+      const uint32_t l32 = len == KMZ_JSON_ABSENT ? 0xFFFFFFFFu : (uint32_t)len;
+      k.append(reinterpret_cast<const char *>(&l32), 4);
+      if (len != KMZ_JSON_ABSENT) k.append(src + off, (size_t)len);
+    }
+  }
+  return KMZ_OK;
+}
 }  // namespace
+
+int kmz_json_known(kmz_ctx *c, uint32_t *shape_of_raw, uint32_t *status_of_raw) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->j_ready) return fail(c, KMZ_E_STATE, "kmz_json_known before a successful kmz_json_parse");
+  for (size_t k = 0; shape_of_raw && k < c->j_skeys.size(); ++k) {
+    auto it = c->j_known_s.find(c->j_skeys[k]);
+    shape_of_raw[k] = it == c->j_known_s.end() ? KMZ_NONE : it->second;
+  }
+  for (size_t k = 0; status_of_raw && k < c->j_tkeys.size(); ++k) {
+    auto it = c->j_known_t.find(c->j_tkeys[k]);
+    status_of_raw[k] = it == c->j_known_t.end() ? KMZ_NONE : it->second;
+  }
+  return KMZ_OK;
+}
+
+int kmz_json_forget(kmz_ctx *c) {
+  if (!c) return KMZ_E_ARG;
+  c->j_known_s.clear();
+  c->j_known_t.clear();
+  return KMZ_OK;
+}
 
 int kmz_json_parse(kmz_ctx *c, const char *json, uint64_t len, int mem, uint64_t *n_spans, uint32_t *n_shapes,
                    uint32_t *n_statuses) {
@@ -521,6 +580,8 @@ int kmz_json_parse(kmz_ctx *c, const char *json, uint64_t len, int mem, uint64_t
   int r = json_collect(c, c->j_stab, scap, 0, 7, n, c->j_sfields, c->j_sslots);
   if (!r) r = json_collect(c, c->j_ttab, tcap, 7, 1, n, c->j_tfields, c->j_tslots);
   if (r) return r;
+  if ((r = json_keys(c, json, mem, 7, c->j_sfields, c->j_skeys)) || (r = json_keys(c, json, mem, 1, c->j_tfields, c->j_tkeys)))
+    return r;
   c->j_n = n;
   c->j_scap = scap;
   c->j_tcap = tcap;
@@ -551,6 +612,9 @@ int kmz_json_load(kmz_ctx *c, const uint32_t *shape_of_raw, const uint32_t *stat
     if (status_of_raw[k] > 0xFFFFu) return fail(c, KMZ_E_RANGE, "status id >= 65536");
     tm[c->j_tslots[k]] = status_of_raw[k];
   }
+  // remembered for kmz_json_known on later batches
+  for (size_t k = 0; k < ns; ++k) c->j_known_s[c->j_skeys[k]] = shape_of_raw[k];
+  for (size_t k = 0; k < nt; ++k) c->j_known_t[c->j_tkeys[k]] = status_of_raw[k];
   int r = load_shapes(c, shapes);
   if (r) return r;
   if (ensure(c, c->j_smap, sm.size() * 4) || ensure(c, c->j_tmap, tm.size() * 4)) return KMZ_E_HIP;

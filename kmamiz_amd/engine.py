@@ -172,6 +172,14 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_json_fields(self.ctx, L.ptr(sf), L.ptr(tf)))
         return sf[: n_shapes * 7], tf[:n_statuses]
 
+    def json_known(self, n_shapes: int, n_statuses: int):
+        """Ids remembered from earlier json_load calls for this batch's raw shapes /
+        statuses (kmz_json_known); NONE32 where new."""
+        ks = np.zeros(max(1, n_shapes), np.uint32)
+        kt = np.zeros(max(1, n_statuses), np.uint32)
+        L.check(self.ctx, self._lib.kmz_json_known(self.ctx, L.ptr(ks), L.ptr(kt)))
+        return ks[:n_shapes], kt[:n_statuses]
+
     def json_load(self, shape_of_raw: np.ndarray, status_of_raw: np.ndarray, shapes: ShapeTable, index_base: int = 0,
                   n: Optional[int] = None):
         sm = np.ascontiguousarray(shape_of_raw, dtype=np.uint32)

@@ -391,11 +391,12 @@ def ingest_rows(rows: Sequence[dict]):
     return batch, table, d, first_row
 
 
-def dictionary_from_fields(data: bytes, sf: np.ndarray, tf: np.ndarray):
+def dictionary_from_fields(data: bytes, sf: np.ndarray, tf: np.ndarray, d: Optional["Dictionary"] = None):
     """The Dictionary of a parsed batch from its raw shape / status slices
     ([n*7, 2] and [n, 2] (offset, length) into ``data``): the identity rules run
-    once per distinct shape, on one json.loads of all slices.  -> (Dictionary,
-    raw shape -> shape id, raw status -> status id)."""
+    once per distinct shape, on one json.loads of all slices.  ``d``: intern
+    into an existing Dictionary.  -> (Dictionary, raw shape -> shape id, raw
+    status -> status id)."""
     import json
 
     from . import _lib as L
@@ -405,7 +406,7 @@ def dictionary_from_fields(data: bytes, sf: np.ndarray, tf: np.ndarray):
     present = [ln != L.JSON_ABSENT for _, ln in fields]
     dec = iter(json.loads(b"[" + b",".join(data[o:o + ln] for (o, ln), p in zip(fields, present) if p) + b"]"))
     vals = [next(dec) if p else UNDEFINED for p in present]
-    d = Dictionary()
+    d = d if d is not None else Dictionary()
     smap = np.zeros(max(1, ns), dtype=np.uint32)
     for i in range(ns):
         v = vals[7 * i:7 * i + 7]
@@ -417,6 +418,36 @@ def dictionary_from_fields(data: bytes, sf: np.ndarray, tf: np.ndarray):
     if len(d.statuses) > 65535:
         raise ValueError("more than 65535 distinct status strings")
     return d, smap, tmap
+
+
+class DeviceIngest:
+    """Zipkin JSON -> the engine's batch with K1 on the GPU, for a realtime
+    worker that parses a window every 5 s: the Dictionary persists across
+    batches and the context remembers each raw shape's id (kmz_json_known), so
+    the identity rules run once per shape ever seen, not once per window."""
+
+    def __init__(self, eng):
+        self.eng = eng
+        self.d = Dictionary()
+
+    def ingest(self, data: bytes, index_base: int = 0, ptr: Optional[int] = None) -> Optional[int]:
+        """-> the batch's span count, or None outside the fast path (nothing
+        loaded).  ``ptr``: the same bytes in pinned host memory (faster H2D)."""
+        from . import _lib as L
+
+        r = self.eng.json_parse(data) if ptr is None else self.eng.json_parse(ptr=ptr, length=len(data))
+        if r is None:
+            return None
+        n, ns, nt = r
+        ks, kt = self.eng.json_known(ns, nt)
+        new_s, new_t = np.nonzero(ks == L.NONE32)[0], np.nonzero(kt == L.NONE32)[0]
+        if len(new_s) or len(new_t):
+            sf, tf = self.eng.json_fields(ns, nt)
+            _, sm, tm = dictionary_from_fields(data, sf.reshape(ns, 7, 2)[new_s].reshape(-1, 2), tf[new_t], self.d)
+            ks[new_s] = sm[: len(new_s)]
+            kt[new_t] = tm[: len(new_t)]
+        self.eng.json_load(ks, kt, self.d.shape_table(), index_base, n=n)
+        return n
 
 
 def ingest_json_device(eng, data: bytes, index_base: int = 0):

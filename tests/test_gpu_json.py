@@ -184,3 +184,36 @@ def test_device_ingest_runs_like_host_ingest(engine):
     assert g1.tobytes() == g2.tobytes()
     assert np.array_equal(np.sort(k1), np.sort(k2))
     assert e1.tobytes() == e2.tobytes()
+
+
+def test_device_ingest_remembers_identities(engine):
+    """DeviceIngest over overlapping windows: each window's batch equals the
+    host parse of the same bytes (shapes compared by content), the second
+    window finds its repeated shapes in kmz_json_known, and kmz_json_forget
+    clears them."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+    from kmamiz_amd.ingest import DeviceIngest, ingest_json
+
+    b, off = synth.host_batch(3, 0, 6000)
+    tr = synth.to_traces(3, b, off)
+    windows = [tr[:3000] + mixed_traces(40), tr[2000:5000], tr[4000:] + mixed_traces(80)]
+    di = DeviceIngest(engine)
+    for k, w in enumerate(windows):
+        data = json.dumps(w).encode()
+        if k == 1:
+            r = engine.json_parse(data)
+            ks, kt = engine.json_known(r[1], r[2])
+            assert (ks != L.NONE32).sum() > 0 and (ks == L.NONE32).sum() > 0
+        n = di.ingest(data)
+        hb, hd = ingest_json(data)
+        got = engine.spans()
+        assert n == len(hb)
+        for f in ("span_id", "parent_id", "kind", "duration", "timestamp"):
+            assert np.array_equal(getattr(got, f), getattr(hb, f)), f
+        assert [di.d.shapes[i] for i in got.shape] == [hd.shapes[i] for i in hb.shape]
+        assert [di.d.statuses[i] for i in got.status] == [hd.statuses[i] for i in hb.status]
+    r = engine.json_parse(json.dumps(windows[0]).encode())
+    assert (engine.json_known(r[1], r[2])[0] != L.NONE32).all()
+    L.check(engine.ctx, L.lib().kmz_json_forget(engine.ctx))
+    assert (engine.json_known(r[1], r[2])[0] == L.NONE32).all()

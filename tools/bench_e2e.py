@@ -108,15 +108,22 @@ def config2(eng, ntr, reps=5):
 
 
 def device_json(eng, config, ntr, reps=5):
+    """K1 on the GPU through DeviceIngest (a worker's persistent dictionary):
+    the first window runs the identity rules for every shape ("cold"), later
+    windows only look the raw shapes up (kmz_json_known, "warm")."""
     import ctypes as C
 
-    from kmamiz_amd.ingest import dictionary_from_fields
+    from kmamiz_amd.ingest import DeviceIngest
 
     b, off = synth.host_batch(config, 0, ntr)
     data = json.dumps(synth.to_traces(config, b, off)).encode()
     n = len(b)
     pin = L.lib().kmz_host_alloc(len(data))
     C.memmove(pin, data, len(data))
+    di = DeviceIngest(eng)
+    t0 = time.perf_counter()
+    assert di.ingest(data, ptr=pin) == n
+    cold = time.perf_counter() - t0
     eng.set_profiling(True)
 
     def parse(pinned):
@@ -129,21 +136,6 @@ def device_json(eng, config, ntr, reps=5):
     tq, r = med(lambda: parse(True), reps)
     kt = eng.kernel_times(reset=True)
     json_ms = kt["json"][0] / reps
-    _, ns, nt = r
-
-    def ident():
-        sf, tf = eng.json_fields(ns, nt)
-        d, smap, tmap = dictionary_from_fields(data, sf, tf)
-        eng.json_load(smap[:ns], tmap[:nt], d.shape_table(), 0, n=n)
-        return d
-
-    tis = []
-    for _ in range(reps):  # (each load consumes its parse)
-        parse(True)
-        t0 = time.perf_counter()
-        ident()
-        tis.append(time.perf_counter() - t0)
-    ti = statistics.median(tis)
 
     def run():
         eng.run(L.RUN_STATS_TAG | L.RUN_DEPS)
@@ -152,8 +144,7 @@ def device_json(eng, config, ntr, reps=5):
     tr, _ = med(run, reps)
 
     def chain():
-        parse(True)
-        ident()
+        di.ingest(data, ptr=pin)
         run()
         g, k, e = eng.fetch()
         return len(k)
@@ -162,11 +153,12 @@ def device_json(eng, config, ntr, reps=5):
     eng.set_profiling(False)
     L.lib().kmz_host_free(C.c_void_p(pin))
     return {f"config{config} device JSON": {
-        "spans": n, "json_bytes": len(data), "parse_pageable_ms": round(tp * 1e3, 2),
+        "spans": n, "json_bytes": len(data), "distinct_shapes": r[1], "parse_pageable_ms": round(tp * 1e3, 2),
         "parse_pinned_ms": round(tq * 1e3, 2), "json_kernels_ms": round(json_ms, 3),
         "kernel_GB_per_s": round(len(data) / (json_ms * 1e-3) / 1e9, 1) if json_ms else None,
-        "identities_and_load_ms": round(ti * 1e3, 2), "run_ms": round(tr * 1e3, 3), "chain_ms": round(tc * 1e3, 2),
-        "end_to_end_spans_per_s": round(n / tc), "parse_pinned_spans_per_s": round(n / tq)}}
+        "first_window_ingest_ms": round(cold * 1e3, 2), "run_ms": round(tr * 1e3, 3),
+        "chain_ms": round(tc * 1e3, 2), "end_to_end_spans_per_s": round(n / tc),
+        "parse_pinned_spans_per_s": round(n / tq)}}
 
 
 def main():
