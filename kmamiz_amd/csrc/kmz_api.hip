@@ -553,6 +553,11 @@ int kmz_json_parse(kmz_ctx *c, const char *json, uint64_t len, int mem, uint64_t
     launch_json_starts(c->stream, P<unsigned long long>(c->j_mask), P<uint32_t>(c->j_off), nch,
                        P<unsigned long long>(c->j_starts));
   }
+  {  // starts[n] = len: the end of the last span (the span kernels' staging bound)
+    const uint64_t end = len;
+    HIPCHK(c, hipMemcpyAsync(P<uint64_t>(c->j_starts) + n, &end, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   for (int attempt = 0;; ++attempt) {
     if (ensure(c, c->j_stab, scap * 16) || ensure(c, c->j_ttab, tcap * 16)) return KMZ_E_HIP;
     HIPCHK(c, hipMemsetAsync(c->j_stab.p, 0, scap * 16, c->stream));

@@ -51,33 +51,82 @@ __device__ __forceinline__ bool esc_carry(const uint8_t *__restrict__ b, uint64_
   return run & 1;
 }
 
+// ---- bit-parallel chunk classification (64 bytes -> 64-bit masks) -------------
+// bit j of eq4(w, c) <=> byte j of w equals c (exact zero-byte test)
+__device__ __forceinline__ uint32_t eq4(uint32_t w, uint32_t c) {
+  const uint32_t t = w ^ (c * 0x01010101u);
+  const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+  return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+struct CMasks {
+  uint64_t q, bs, open, close, comma, ws, valid;
+};
+__device__ __forceinline__ CMasks chunk_masks(const uint8_t *__restrict__ b, uint64_t s, uint64_t e) {
+  CMasks m{0, 0, 0, 0, 0, 0, 0};
+  if (e - s == JCHUNK && (reinterpret_cast<uintptr_t>(b + s) & 15) == 0) {
+    const uint4 *v = reinterpret_cast<const uint4 *>(b + s);
+    const uint4 w0 = v[0], w1 = v[1], w2 = v[2], w3 = v[3];
+    const uint32_t w[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
+                            w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t x = w[k];
+      const int sh = 4 * k;
+      m.q |= (uint64_t)eq4(x, '"') << sh;
+      m.bs |= (uint64_t)eq4(x, '\\') << sh;
+      m.open |= (uint64_t)(eq4(x, '{') | eq4(x, '[')) << sh;
+      m.close |= (uint64_t)(eq4(x, '}') | eq4(x, ']')) << sh;
+      m.comma |= (uint64_t)eq4(x, ',') << sh;
+      m.ws |= (uint64_t)(eq4(x, ' ') | eq4(x, '\n') | eq4(x, '\r') | eq4(x, '\t')) << sh;
+    }
+    m.valid = ~0ull;
+  } else {
+    for (uint64_t i = s; i < e; ++i) {
+      const uint8_t ch = b[i];
+      const uint64_t bit = 1ull << (i - s);
+      if (ch == '"') m.q |= bit;
+      if (ch == '\\') m.bs |= bit;
+      if (ch == '{' || ch == '[') m.open |= bit;
+      if (ch == '}' || ch == ']') m.close |= bit;
+      if (ch == ',') m.comma |= bit;
+      if (is_ws(ch)) m.ws |= bit;
+    }
+    m.valid = e - s == JCHUNK ? ~0ull : ((1ull << (e - s)) - 1);
+  }
+  return m;
+}
+// characters escaped by a preceding odd-length backslash run; `carry`: the
+// chunk's first character is escaped (a run ending at the previous chunk)
+__device__ __forceinline__ uint64_t escaped_mask(uint64_t bs, bool carry) {
+  const uint64_t even = 0x5555555555555555ull, odd = ~even;
+  if (carry) bs &= ~1ull;  // (an escaped backslash starts no escape)
+  const uint64_t starts = bs & ~(bs << 1);
+  const uint64_t even_ends = (bs + (starts & even)) & ~bs;
+  const uint64_t odd_ends = (bs + (starts & odd)) & ~bs;
+  return ((even_ends & odd) | (odd_ends & even)) | (carry ? 1ull : 0ull);
+}
+// bit i = XOR of bits 0..i
+__device__ __forceinline__ uint64_t prefix_xor(uint64_t x) {
+  x ^= x << 1;
+  x ^= x << 2;
+  x ^= x << 4;
+  x ^= x << 8;
+  x ^= x << 16;
+  x ^= x << 32;
+  return x;
+}
+
 __global__ void __launch_bounds__(256) k_json_sum(const uint8_t *__restrict__ b, uint64_t len, uint64_t nch,
                                                   JElem *__restrict__ elem) {
   for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nch; c += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = c * JCHUNK, e = min<uint64_t>(s + JCHUNK, len);
-    bool esc = esc_carry(b, s);
-    int in = 0, d0 = 0, tot = 0;
-    uint32_t p = 0;
-    for (uint64_t i = s; i < e; ++i) {
-      const uint8_t ch = b[i];
-      if (esc) {
-        esc = false;
-        continue;
-      }
-      if (ch == '\\') {
-        esc = true;
-        continue;
-      }
-      if (ch == '"') {
-        in ^= 1;
-        p ^= 1;
-        continue;
-      }
-      const int v = (ch == '{' || ch == '[') ? 1 : ((ch == '}' || ch == ']') ? -1 : 0);
-      tot += v;
-      if (!in) d0 += v;
-    }
-    elem[c] = JElem{(int)p, d0, tot - d0};
+    const CMasks m = chunk_masks(b, s, e);
+    const uint64_t esc = escaped_mask(m.bs, esc_carry(b, s)) & m.valid;
+    const uint64_t qu = m.q & ~esc, op = m.open & ~esc, cl = m.close & ~esc;
+    const uint64_t out0 = ~prefix_xor(qu);  // outside strings if the chunk starts outside one
+    const int d0 = __popcll(op & out0) - __popcll(cl & out0);
+    const int tot = __popcll(op) - __popcll(cl);
+    elem[c] = JElem{(int)(__popcll(qu) & 1), d0, tot - d0};
   }
 }
 
@@ -162,78 +211,86 @@ __device__ __forceinline__ int next_nw(const uint8_t *__restrict__ b, uint64_t i
   return -1;
 }
 
+// bits a+1 .. b-1 (a may be -1, b may be 64)
+__device__ __forceinline__ uint64_t between(int a, int b) {
+  const uint64_t hi = b >= 64 ? ~0ull : ((1ull << b) - 1);
+  const uint64_t lo = a + 1 >= 64 ? ~0ull : ((1ull << (a + 1)) - 1);
+  return hi & ~lo;
+}
+
 __global__ void __launch_bounds__(256) k_json_struct(const uint8_t *__restrict__ b, uint64_t len, uint64_t nch,
                                                      const JElem *__restrict__ state,
                                                      unsigned long long *__restrict__ mask,
                                                      uint32_t *__restrict__ cnt, unsigned int *__restrict__ flags) {
   for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nch; c += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t s = c * JCHUNK, e = min<uint64_t>(s + JCHUNK, len);
-    bool esc = esc_carry(b, s);
-    int in = state[c].p, depth = state[c].d0;
-    uint64_t m = 0;
-    bool bad = false, top = false;
-    for (uint64_t i = s; i < e; ++i) {
+    const CMasks m = chunk_masks(b, s, e);
+    const uint64_t esc = escaped_mask(m.bs, esc_carry(b, s)) & m.valid;
+    const uint64_t qu = m.q & ~esc;
+    const uint64_t instr = (prefix_xor(qu) ^ (state[c].p ? ~0ull : 0ull)) & m.valid;  // (opening quotes included)
+    const uint64_t outside = ~instr & m.valid;
+    bool bad = (m.bs & ~esc & outside) != 0;  // a backslash outside a string
+    bool top = false;
+    uint64_t starts_m = 0;
+    const uint64_t tokens = (m.open | m.close) & ~esc & outside;
+    // bytes at depth <= 2 that must be whitespace (depth 0) or whitespace and
+    // commas (1, 2); an opening quote there starts a string outside a span
+    const uint64_t stray0 = outside & ~m.ws, stray12 = stray0 & ~m.comma, openq = qu & instr;
+    int depth = state[c].d0;
+    int prev = -1;
+    uint64_t t = tokens;
+    for (;;) {
+      const int pos = t ? __builtin_ctzll(t) : 64;
+      if (depth <= 2) {  // the region (prev, pos) at this depth
+        const uint64_t r = between(prev, pos) & m.valid;
+        if ((r & openq) || (r & (depth == 0 ? stray0 : stray12))) bad = true;
+        uint64_t cm = depth == 0 ? 0 : (r & m.comma & outside);
+        while (cm) {
+          const uint64_t i = s + (uint64_t)__builtin_ctzll(cm);
+          cm &= cm - 1;
+          const int pv = prev_nw(b, i), nx = next_nw(b, i, len);
+          if (depth == 1 ? (pv != ']' || nx != '[') : (pv != '}' || nx != '{')) bad = true;
+        }
+      }
+      if (pos == 64) break;
+      t &= t - 1;
+      const uint64_t i = s + (uint64_t)pos;
       const uint8_t ch = b[i];
-      if (esc) {
-        esc = false;
-        continue;
-      }
-      if (in) {
-        if (ch == '\\')
-          esc = true;
-        else if (ch == '"')
-          in = 0;
-        continue;
-      }
-      if (ch == '"') {
-        if (depth <= 2) bad = true;  // a string outside a span
-        in = 1;
-        continue;
-      }
-      if (ch == '\\') {
-        bad = true;
-        continue;
-      }
-      if (is_ws(ch)) continue;
       if (depth >= 3) {
-        if (ch == '{' || ch == '[') ++depth;
-        if (ch == '}' || ch == ']') --depth;
-        continue;
-      }
-      const int pv = prev_nw(b, i);
-      if (depth == 0) {  // the top-level array, first in the input
-        if (ch != '[' || pv != -1) bad = true;
-        top = true;
-        depth = 1;
-      } else if (depth == 1) {  // between traces
-        if (ch == '[') {
-          if (pv != '[' && pv != ',') bad = true;
-          depth = 2;
-        } else if (ch == ',') {
-          if (pv != ']' || next_nw(b, i, len) != '[') bad = true;
-        } else if (ch == ']') {
-          if (pv != '[' && pv != ']') bad = true;
-          depth = 0;
-        } else {
-          bad = true;
-        }
-      } else {  // depth 2: between the spans of a trace
-        if (ch == '{') {
-          if (pv != '[' && pv != ',') bad = true;
-          m |= 1ull << (i - s);
-          depth = 3;
-        } else if (ch == ',') {
-          if (pv != '}' || next_nw(b, i, len) != '{') bad = true;
-        } else if (ch == ']') {
-          if (pv != '[' && pv != '}') bad = true;
+        depth += (ch == '{' || ch == '[') ? 1 : -1;
+      } else {
+        const int pv = prev_nw(b, i);
+        if (depth == 0) {  // the top-level array, first in the input
+          if (ch != '[' || pv != -1) bad = true;
+          top = true;
           depth = 1;
-        } else {
-          bad = true;
+        } else if (depth == 1) {  // between traces
+          if (ch == '[') {
+            if (pv != '[' && pv != ',') bad = true;
+            depth = 2;
+          } else if (ch == ']') {
+            if (pv != '[' && pv != ']') bad = true;
+            depth = 0;
+          } else {
+            bad = true;
+          }
+        } else {  // depth 2: between the spans of a trace
+          if (ch == '{') {
+            if (pv != '[' && pv != ',') bad = true;
+            starts_m |= 1ull << pos;
+            depth = 3;
+          } else if (ch == ']') {
+            if (pv != '[' && pv != '}') bad = true;
+            depth = 1;
+          } else {
+            bad = true;
+          }
         }
       }
+      prev = pos;
     }
-    mask[c] = m;
-    cnt[c] = (uint32_t)__popcll(m);
+    mask[c] = starts_m;
+    cnt[c] = (uint32_t)__popcll(starts_m);
     if (bad) atomicOr(&flags[0], JF_BAD);
     if (top) atomicOr(&flags[0], JF_TOP);
   }
@@ -254,15 +311,34 @@ __global__ void __launch_bounds__(256) k_json_starts(const unsigned long long *_
 }
 
 // ---- J5: one span --------------------------------------------------------------
+// The span parser reads bytes through an accessor: a wave first stages the
+// bytes of up to 64 consecutive spans into LDS with 16-byte coalesced loads
+// (LBytes); a span too large for the stage is parsed from global memory
+// (GBytes).  Either way the parse is the host parser's, byte for byte.
+constexpr uint32_t JSPAN_T = 64;           // one wave per workgroup
+constexpr uint32_t JSPAN_LDS = 32 * 1024;  // bytes staged per round (5 workgroups per CU)
+
+struct GBytes {
+  const uint8_t *__restrict__ g;
+  __device__ __forceinline__ uint8_t operator[](uint64_t i) const { return g[i]; }
+};
+struct LBytes {
+  const uint8_t *l;
+  uint64_t base;
+  __device__ __forceinline__ uint8_t operator[](uint64_t i) const { return l[i - base]; }
+};
+template <class B>
 struct Cur {
-  const uint8_t *b;
+  B b;
   uint64_t p, e;
   bool bad;
 };
-__device__ __forceinline__ void ws(Cur &c) {
+template <class B>
+__device__ __forceinline__ void ws(Cur<B> &c) {
   while (c.p < c.e && is_ws(c.b[c.p])) ++c.p;
 }
-__device__ __forceinline__ bool eat(Cur &c, uint8_t ch) {
+template <class B>
+__device__ __forceinline__ bool eat(Cur<B> &c, uint8_t ch) {
   ws(c);
   if (c.p < c.e && c.b[c.p] == ch) {
     ++c.p;
@@ -271,7 +347,8 @@ __device__ __forceinline__ bool eat(Cur &c, uint8_t ch) {
   return false;
 }
 // at '"': past the closing quote; *esc: an escape occurred
-__device__ __forceinline__ bool skip_string(Cur &c, bool *esc) {
+template <class B>
+__device__ __forceinline__ bool skip_string(Cur<B> &c, bool *esc) {
   uint64_t p = c.p + 1;
   while (p < c.e) {
     const uint8_t ch = c.b[p];
@@ -288,7 +365,8 @@ __device__ __forceinline__ bool skip_string(Cur &c, bool *esc) {
   }
   return false;
 }
-__device__ bool skip_value(Cur &c) {
+template <class B>
+__device__ bool skip_value(Cur<B> &c) {
   ws(c);
   if (c.p >= c.e) return false;
   const uint8_t ch = c.b[c.p];
@@ -319,7 +397,8 @@ __device__ bool skip_value(Cur &c) {
   return true;
 }
 // a key without escapes: [ks, ks + kl)
-__device__ __forceinline__ bool key(Cur &c, uint64_t *ks, uint32_t *kl) {
+template <class B>
+__device__ __forceinline__ bool key(Cur<B> &c, uint64_t *ks, uint32_t *kl) {
   ws(c);
   if (c.p >= c.e || c.b[c.p] != '"') return false;
   const uint64_t s = c.p + 1;
@@ -330,15 +409,16 @@ __device__ __forceinline__ bool key(Cur &c, uint64_t *ks, uint32_t *kl) {
   *kl = (uint32_t)(c.p - 1 - s);
   return eat(c, ':');
 }
-template <int N>
-__device__ __forceinline__ bool key_is(const Cur &c, uint64_t ks, uint32_t kl, const char (&lit)[N]) {
+template <class B, int N>
+__device__ __forceinline__ bool key_is(const Cur<B> &c, uint64_t ks, uint32_t kl, const char (&lit)[N]) {
   if (kl != N - 1) return false;
   for (int i = 0; i < N - 1; ++i)
     if (c.b[ks + i] != (uint8_t)lit[i]) return false;
   return true;
 }
 // packed slice: offset << 24 | length (SL_ABSENT: property missing)
-__device__ __forceinline__ uint64_t value_slice(Cur &c) {
+template <class B>
+__device__ __forceinline__ uint64_t value_slice(Cur<B> &c) {
   ws(c);
   const uint64_t s = c.p;
   if (!skip_value(c)) {
@@ -357,7 +437,8 @@ __device__ __forceinline__ int hexv(uint8_t ch) {
   if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
   return -1;
 }
-__device__ uint64_t hex_id(Cur &c, bool allow_empty) {
+template <class B>
+__device__ uint64_t hex_id(Cur<B> &c, bool allow_empty) {
   ws(c);
   if (c.p >= c.e) return c.bad = true, 0;
   if (allow_empty && c.b[c.p] == 'n' && c.e - c.p >= 4 && c.b[c.p + 1] == 'u' && c.b[c.p + 2] == 'l' &&
@@ -382,7 +463,8 @@ __device__ uint64_t hex_id(Cur &c, bool allow_empty) {
   c.p = s + 17;
   return v;
 }
-__device__ int64_t int_value(Cur &c, int64_t lo, int64_t hi) {
+template <class B>
+__device__ int64_t int_value(Cur<B> &c, int64_t lo, int64_t hi) {
   ws(c);
   uint64_t s = c.p;
   bool neg = false;
@@ -412,7 +494,8 @@ __device__ __forceinline__ uint64_t hmix(uint64_t x) {
   x *= 0xc4ceb9fe1a85ec53ull;
   return x ^ (x >> 33);
 }
-__device__ uint64_t slices_hash(const uint8_t *__restrict__ b, const uint64_t *sl, int nf) {
+template <class B>
+__device__ uint64_t slices_hash(const B &b, const uint64_t *sl, int nf) {
   uint64_t h = 0x9E3779B97F4A7C15ull * (uint64_t)(nf + 1);
   for (int f = 0; f < nf; ++f) {
     const uint64_t n = sl[f] & SL_ABSENT;
@@ -455,138 +538,197 @@ __device__ uint32_t intern(unsigned long long *__restrict__ tab, uint64_t cap, u
   return 0;
 }
 
-__global__ void __launch_bounds__(256) k_json_span(const uint8_t *__restrict__ b, uint64_t len,
-                                                   const unsigned long long *__restrict__ starts, uint64_t n,
-                                                   uint64_t *__restrict__ sid, uint64_t *__restrict__ pid,
-                                                   uint8_t *__restrict__ kind, uint32_t *__restrict__ dur,
-                                                   int64_t *__restrict__ ts, unsigned long long *__restrict__ slices,
-                                                   uint32_t *__restrict__ shape_slot, uint32_t *__restrict__ status_slot,
-                                                   unsigned long long *__restrict__ stab, uint64_t scap,
-                                                   unsigned long long *__restrict__ ttab, uint64_t tcap,
-                                                   unsigned int *__restrict__ flags) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    Cur c{b, starts[i], len, false};
-    uint64_t s_id = 0, p_id = 0;
-    bool have_id = false, have_dur = false, have_ts = false, ok = true;
-    uint8_t kd = KMZ_KIND_OTHER;
-    int64_t du = 0, t = 0;
-    uint64_t f[NF + 1];
-    for (uint32_t k = 0; k <= NF; ++k) f[k] = SL_ABSENT;
-    if (!eat(c, '{')) ok = false;
-    ws(c);
-    if (ok && c.p < c.e && c.b[c.p] == '}') {
-      ++c.p;
-      c.bad = true;  // a span without id / duration / timestamp
-    } else {
-      while (ok && !c.bad) {
-        uint64_t ks;
-        uint32_t kl;
-        if (!key(c, &ks, &kl)) {
-          ok = false;
-          break;
-        }
-        if (key_is(c, ks, kl, "id")) {
-          s_id = hex_id(c, false);
-          have_id = true;
-        } else if (key_is(c, ks, kl, "parentId")) {
-          p_id = hex_id(c, true);
-        } else if (key_is(c, ks, kl, "kind")) {
-          ws(c);
-          if (c.p < c.e && c.b[c.p] == '"') {
-            const uint64_t s0 = c.p + 1;
-            bool esc = false;
-            if (!skip_string(c, &esc)) {
-              ok = false;
-              break;
-            }
-            if (esc) c.bad = true;
-            const uint32_t vl = (uint32_t)(c.p - 1 - s0);
-            kd = key_is(c, s0, vl, "SERVER") ? KMZ_KIND_SERVER
-                                              : (key_is(c, s0, vl, "CLIENT") ? KMZ_KIND_CLIENT : KMZ_KIND_OTHER);
-          } else {
-            if (!skip_value(c)) {
-              ok = false;
-              break;
-            }
-            kd = KMZ_KIND_OTHER;
+struct SpanOut {
+  uint64_t *__restrict__ sid, *__restrict__ pid;
+  uint8_t *__restrict__ kind;
+  uint32_t *__restrict__ dur;
+  int64_t *__restrict__ ts;
+  unsigned long long *__restrict__ slices;
+  uint32_t *__restrict__ shape_slot, *__restrict__ status_slot;
+  unsigned long long *__restrict__ stab, *__restrict__ ttab;
+  uint64_t scap, tcap;
+  unsigned int *__restrict__ flags;
+};
+
+template <class B>
+__device__ void parse_one(const B &bytes, uint64_t start, uint64_t end, uint64_t i, const SpanOut &o) {
+  Cur<B> c{bytes, start, end, false};
+  uint64_t s_id = 0, p_id = 0;
+  bool have_id = false, have_dur = false, have_ts = false, ok = true;
+  uint8_t kd = KMZ_KIND_OTHER;
+  int64_t du = 0, t = 0;
+  uint64_t f[NF + 1];
+  for (uint32_t k = 0; k <= NF; ++k) f[k] = SL_ABSENT;
+  if (!eat(c, '{')) ok = false;
+  ws(c);
+  if (ok && c.p < c.e && c.b[c.p] == '}') {
+    ++c.p;
+    c.bad = true;  // a span without id / duration / timestamp
+  } else {
+    while (ok && !c.bad) {
+      uint64_t ks;
+      uint32_t kl;
+      if (!key(c, &ks, &kl)) {
+        ok = false;
+        break;
+      }
+      if (key_is(c, ks, kl, "id")) {
+        s_id = hex_id(c, false);
+        have_id = true;
+      } else if (key_is(c, ks, kl, "parentId")) {
+        p_id = hex_id(c, true);
+      } else if (key_is(c, ks, kl, "kind")) {
+        ws(c);
+        if (c.p < c.e && c.b[c.p] == '"') {
+          const uint64_t s0 = c.p + 1;
+          bool esc = false;
+          if (!skip_string(c, &esc)) {
+            ok = false;
+            break;
           }
-        } else if (key_is(c, ks, kl, "name")) {
-          f[0] = value_slice(c);
-        } else if (key_is(c, ks, kl, "duration")) {
-          du = int_value(c, 0, 0xFFFFFFFFll);
-          have_dur = true;
-        } else if (key_is(c, ks, kl, "timestamp")) {
-          t = int_value(c, -(int64_t)0x7FFFFFFFFFFFFFFFll, 0x7FFFFFFFFFFFFFFFll);
-          have_ts = true;
-        } else if (key_is(c, ks, kl, "tags")) {
-          for (uint32_t k = 1; k <= NF; ++k) f[k] = SL_ABSENT;
+          if (esc) c.bad = true;
+          const uint32_t vl = (uint32_t)(c.p - 1 - s0);
+          kd = key_is(c, s0, vl, "SERVER") ? KMZ_KIND_SERVER
+                                            : (key_is(c, s0, vl, "CLIENT") ? KMZ_KIND_CLIENT : KMZ_KIND_OTHER);
+        } else {
+          if (!skip_value(c)) {
+            ok = false;
+            break;
+          }
+          kd = KMZ_KIND_OTHER;
+        }
+      } else if (key_is(c, ks, kl, "name")) {
+        f[0] = value_slice(c);
+      } else if (key_is(c, ks, kl, "duration")) {
+        du = int_value(c, 0, 0xFFFFFFFFll);
+        have_dur = true;
+      } else if (key_is(c, ks, kl, "timestamp")) {
+        t = int_value(c, -(int64_t)0x7FFFFFFFFFFFFFFFll, 0x7FFFFFFFFFFFFFFFll);
+        have_ts = true;
+      } else if (key_is(c, ks, kl, "tags")) {
+        for (uint32_t k = 1; k <= NF; ++k) f[k] = SL_ABSENT;
+        ws(c);
+        if (c.p + 4 <= c.e && c.b[c.p] == 'n' && c.b[c.p + 1] == 'u' && c.b[c.p + 2] == 'l' && c.b[c.p + 3] == 'l') {
+          c.p += 4;
+        } else if (!eat(c, '{')) {
+          c.bad = true;
+        } else {
           ws(c);
-          if (c.p + 4 <= c.e && c.b[c.p] == 'n' && c.b[c.p + 1] == 'u' && c.b[c.p + 2] == 'l' && c.b[c.p + 3] == 'l') {
-            c.p += 4;
-          } else if (!eat(c, '{')) {
-            c.bad = true;
+          if (c.p < c.e && c.b[c.p] == '}') {
+            ++c.p;
           } else {
-            ws(c);
-            if (c.p < c.e && c.b[c.p] == '}') {
-              ++c.p;
-            } else {
-              for (;;) {
-                uint64_t ts0;
-                uint32_t tl;
-                if (!key(c, &ts0, &tl)) {
-                  ok = false;
-                  break;
-                }
-                int hit = -1;
-                if (key_is(c, ts0, tl, "http.method")) hit = 1;
-                else if (key_is(c, ts0, tl, "http.url")) hit = 2;
-                else if (key_is(c, ts0, tl, "istio.canonical_revision")) hit = 3;
-                else if (key_is(c, ts0, tl, "istio.canonical_service")) hit = 4;
-                else if (key_is(c, ts0, tl, "istio.namespace")) hit = 5;
-                else if (key_is(c, ts0, tl, "istio.mesh_id")) hit = 6;
-                else if (key_is(c, ts0, tl, "http.status_code")) hit = NF;
-                if (hit >= 0)
-                  f[hit] = value_slice(c);
-                else if (!skip_value(c)) {
-                  ok = false;
-                  break;
-                }
-                if (eat(c, ',')) continue;
-                if (eat(c, '}')) break;
+            for (;;) {
+              uint64_t ts0;
+              uint32_t tl;
+              if (!key(c, &ts0, &tl)) {
                 ok = false;
                 break;
               }
+              int hit = -1;
+              if (key_is(c, ts0, tl, "http.method")) hit = 1;
+              else if (key_is(c, ts0, tl, "http.url")) hit = 2;
+              else if (key_is(c, ts0, tl, "istio.canonical_revision")) hit = 3;
+              else if (key_is(c, ts0, tl, "istio.canonical_service")) hit = 4;
+              else if (key_is(c, ts0, tl, "istio.namespace")) hit = 5;
+              else if (key_is(c, ts0, tl, "istio.mesh_id")) hit = 6;
+              else if (key_is(c, ts0, tl, "http.status_code")) hit = NF;
+              if (hit >= 0)
+                f[hit] = value_slice(c);
+              else if (!skip_value(c)) {
+                ok = false;
+                break;
+              }
+              if (eat(c, ',')) continue;
+              if (eat(c, '}')) break;
+              ok = false;
+              break;
             }
           }
-        } else if (!skip_value(c)) {
-          ok = false;
-          break;
         }
-        if (!ok || c.bad) break;
-        if (eat(c, ',')) continue;
-        if (eat(c, '}')) break;
+      } else if (!skip_value(c)) {
         ok = false;
+        break;
       }
+      if (!ok || c.bad) break;
+      if (eat(c, ',')) continue;
+      if (eat(c, '}')) break;
+      ok = false;
     }
-    if (!have_id || !have_dur || !have_ts) c.bad = true;
-    if (!ok || c.bad) {
-      atomicOr(flags, JF_BAD);
-      shape_slot[i] = status_slot[i] = NONE;  // (J6 skips it)
-      continue;
+  }
+  if (!have_id || !have_dur || !have_ts) c.bad = true;
+  if (!ok || c.bad) {
+    atomicOr(o.flags, JF_BAD);
+    o.shape_slot[i] = o.status_slot[i] = NONE;  // (J6 skips it)
+    return;
+  }
+  o.sid[i] = s_id;
+  o.pid[i] = p_id;
+  o.kind[i] = kd;
+  o.dur[i] = (uint32_t)du;
+  o.ts[i] = t;
+  for (uint32_t k = 0; k <= NF; ++k) o.slices[i * (NF + 1) + k] = f[k];
+  o.shape_slot[i] = intern(o.stab, o.scap, slices_hash(bytes, f, NF), i, o.flags);
+  o.status_slot[i] = intern(o.ttab, o.tcap, slices_hash(bytes, f + NF, 1), i, o.flags);
+}
+
+// Copy bytes [a0, hi) (a0 16-aligned) into lds with 16-byte loads (bytewise
+// past the end of the buffer).
+__device__ __forceinline__ void stage(const uint8_t *__restrict__ b, uint64_t len, uint64_t a0, uint64_t hi,
+                                      uint8_t *lds) {
+  const uint64_t nq = (hi - a0 + 15) / 16;
+  for (uint64_t q = threadIdx.x; q < nq; q += blockDim.x) {
+    const uint64_t g = a0 + 16 * q;
+    if (g + 16 <= len) {
+      *reinterpret_cast<uint4 *>(lds + 16 * q) = *reinterpret_cast<const uint4 *>(b + g);
+    } else {
+      for (uint64_t k = 0; k < 16 && g + k < len; ++k) lds[16 * q + k] = b[g + k];
     }
-    sid[i] = s_id;
-    pid[i] = p_id;
-    kind[i] = kd;
-    dur[i] = (uint32_t)du;
-    ts[i] = t;
-    for (uint32_t k = 0; k <= NF; ++k) slices[i * (NF + 1) + k] = f[k];
-    shape_slot[i] = intern(stab, scap, slices_hash(b, f, NF), i, flags);
-    status_slot[i] = intern(ttab, tcap, slices_hash(b, f + NF, 1), i, flags);
   }
 }
 
+// Span groups of 64: each round stages the longest prefix of the remaining
+// spans whose bytes fit the stage (starts[n] = len), parses them from LDS,
+// and a span alone too large for it is parsed from global memory.
+template <class Body>
+__device__ __forceinline__ void for_staged_spans(const uint8_t *__restrict__ b, uint64_t len,
+                                                 const unsigned long long *__restrict__ starts, uint64_t n,
+                                                 uint8_t *lds, Body body) {
+  const uint32_t lane = threadIdx.x;
+  const bool aligned = (reinterpret_cast<uintptr_t>(b) & 15) == 0;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * JSPAN_T; i0 < n; i0 += (uint64_t)gridDim.x * JSPAN_T) {
+    const uint64_t iend = min<uint64_t>(n, i0 + JSPAN_T);
+    uint64_t cur = i0;
+    while (cur < iend) {
+      const uint64_t lo = starts[cur], a0 = lo & ~15ull;
+      const bool fits = aligned && cur + lane < iend && starts[cur + lane + 1] - a0 <= JSPAN_LDS;
+      const uint64_t m = (uint64_t)__popcll(__ballot(fits));  // (a prefix: starts increase)
+      if (m == 0) {  // one span larger than the stage: from global memory
+        if (lane == 0) body(GBytes{b}, cur, len);
+        cur += 1;
+        continue;
+      }
+      const uint64_t hi = starts[cur + m];
+      __syncthreads();  // the previous round's readers are done
+      stage(b, len, a0, hi, lds);
+      __syncthreads();
+      if (lane < m) body(LBytes{lds, a0}, cur + lane, hi);
+      cur += m;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(JSPAN_T) k_json_span(const uint8_t *__restrict__ b, uint64_t len,
+                                                       const unsigned long long *__restrict__ starts, uint64_t n,
+                                                       SpanOut o) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[JSPAN_LDS];
+  for_staged_spans(b, len, starts, n, lds, [&](const auto &bytes, uint64_t i, uint64_t end) {
+    parse_one(bytes, starts[i], end, i, o);
+  });
+}
+
 // ---- J6 --------------------------------------------------------------------------
-__device__ __forceinline__ bool slices_equal(const uint8_t *__restrict__ b, const unsigned long long *x,
+template <class B>
+__device__ __forceinline__ bool slices_equal(const B &bx, const unsigned long long *x, const uint8_t *__restrict__ g,
                                              const unsigned long long *y, int nf) {
   for (int f = 0; f < nf; ++f) {
     const uint64_t nx = x[f] & SL_ABSENT, ny = y[f] & SL_ABSENT;
@@ -594,27 +736,29 @@ __device__ __forceinline__ bool slices_equal(const uint8_t *__restrict__ b, cons
     if (nx == SL_ABSENT) continue;
     const uint64_t ox = x[f] >> 24, oy = y[f] >> 24;
     for (uint64_t i = 0; i < nx; ++i)
-      if (b[ox + i] != b[oy + i]) return false;
+      if (bx[ox + i] != g[oy + i]) return false;
   }
   return true;
 }
-__global__ void __launch_bounds__(256) k_json_verify(const uint8_t *__restrict__ b, uint64_t n,
-                                                     const unsigned long long *__restrict__ slices,
-                                                     const uint32_t *__restrict__ shape_slot,
-                                                     const uint32_t *__restrict__ status_slot,
-                                                     const unsigned long long *__restrict__ stab, uint64_t scap,
-                                                     const unsigned long long *__restrict__ ttab, uint64_t tcap,
-                                                     unsigned int *__restrict__ flags) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+__global__ void __launch_bounds__(JSPAN_T) k_json_verify(const uint8_t *__restrict__ b, uint64_t len,
+                                                         const unsigned long long *__restrict__ starts, uint64_t n,
+                                                         const unsigned long long *__restrict__ slices,
+                                                         const uint32_t *__restrict__ shape_slot,
+                                                         const uint32_t *__restrict__ status_slot,
+                                                         const unsigned long long *__restrict__ stab, uint64_t scap,
+                                                         const unsigned long long *__restrict__ ttab, uint64_t tcap,
+                                                         unsigned int *__restrict__ flags) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[JSPAN_LDS];
+  for_staged_spans(b, len, starts, n, lds, [&](const auto &bytes, uint64_t i, uint64_t) {
     const unsigned long long *mine = slices + i * (NF + 1);
-    const uint32_t ss = shape_slot[i], ts = status_slot[i];
-    if (ss >= scap || ts >= tcap) continue;  // a span outside the fast path (JF_BAD is set)
-    const uint64_t rs = ~stab[2 * (uint64_t)ss + 1], rt = ~ttab[2 * (uint64_t)ts + 1];
-    if (rs >= n || rt >= n) continue;  // an insert that failed (JF_FULL is set)
-    if ((rs != i && !slices_equal(b, mine, slices + rs * (NF + 1), NF)) ||
-        (rt != i && !slices_equal(b, mine + NF, slices + rt * (NF + 1) + NF, 1)))
+    const uint32_t ss = shape_slot[i], tsl = status_slot[i];
+    if (ss >= scap || tsl >= tcap) return;  // a span outside the fast path (JF_BAD is set)
+    const uint64_t rs = ~stab[2 * (uint64_t)ss + 1], rt = ~ttab[2 * (uint64_t)tsl + 1];
+    if (rs >= n || rt >= n) return;  // an insert that failed (JF_FULL is set)
+    if ((rs != i && !slices_equal(bytes, mine, b, slices + rs * (NF + 1), NF)) ||
+        (rt != i && !slices_equal(bytes, mine + NF, b, slices + rt * (NF + 1) + NF, 1)))
       atomicOr(flags, JF_COLLIDE);
-  }
+  });
 }
 
 // ---- J7 --------------------------------------------------------------------------
@@ -677,10 +821,11 @@ void launch_json_spans(hipStream_t s, const uint8_t *b, uint64_t len, const unsi
                        unsigned long long *slices, uint32_t *shape_slot, uint32_t *status_slot, unsigned long long *stab,
                        uint64_t scap, unsigned long long *ttab, uint64_t tcap, unsigned int *flags) {
   if (!n) return;
-  hipLaunchKernelGGL(k_json_span, dim3(grid_of(n)), dim3(256), 0, s, b, len, starts, n, sid, pid, kind, dur, ts,
-                     slices, shape_slot, status_slot, stab, scap, ttab, tcap, flags);
-  hipLaunchKernelGGL(k_json_verify, dim3(grid_of(n)), dim3(256), 0, s, b, n, slices, shape_slot, status_slot, stab,
-                     scap, ttab, tcap, flags);
+  const uint32_t groups = (uint32_t)std::min<uint64_t>((n + JSPAN_T - 1) / JSPAN_T, 1u << 16);
+  SpanOut o{sid, pid, kind, dur, ts, slices, shape_slot, status_slot, stab, ttab, scap, tcap, flags};
+  hipLaunchKernelGGL(k_json_span, dim3(groups), dim3(JSPAN_T), 0, s, b, len, starts, n, o);
+  hipLaunchKernelGGL(k_json_verify, dim3(groups), dim3(JSPAN_T), 0, s, b, len, starts, n, slices, shape_slot,
+                     status_slot, stab, scap, ttab, tcap, flags);
 }
 
 void launch_json_reps(hipStream_t s, const unsigned long long *tab, uint64_t cap, const unsigned long long *slices,

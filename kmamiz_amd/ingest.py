@@ -427,8 +427,13 @@ class DeviceIngest:
     the identity rules run once per shape ever seen, not once per window."""
 
     def __init__(self, eng):
+        from . import _lib as L
+
         self.eng = eng
         self.d = Dictionary()
+        # one identity space per context: ids remembered for another
+        # dictionary would index this one wrongly
+        L.check(eng.ctx, L.lib().kmz_json_forget(eng.ctx))
 
     def ingest(self, data: bytes, index_base: int = 0, ptr: Optional[int] = None) -> Optional[int]:
         """-> the batch's span count, or None outside the fast path (nothing
@@ -454,12 +459,15 @@ def ingest_json_device(eng, data: bytes, index_base: int = 0):
     """Zipkin Trace[][] JSON bytes parsed on the GPU (kmz_json_parse, K1) and
     loaded as the engine's batch: -> (Dictionary, n_spans), or None when the
     batch is outside the fast path (nothing loaded; parse on the host)."""
+    from . import _lib as L
+
     r = eng.json_parse(data)
     if r is None:
         return None
     n, ns, nt = r
     sf, tf = eng.json_fields(ns, nt)
     d, smap, tmap = dictionary_from_fields(data, sf, tf)
+    L.check(eng.ctx, L.lib().kmz_json_forget(eng.ctx))  # (a fresh dictionary: a fresh identity space)
     eng.json_load(smap[:ns], tmap[:nt], d.shape_table(), index_base, n=n)
     return d, n
 

@@ -141,6 +141,7 @@ def device_json(eng, config, ntr, reps=5):
         eng.run(L.RUN_STATS_TAG | L.RUN_DEPS)
         eng.sync()
 
+    di.ingest(data, ptr=pin)  # (a bare json_parse leaves nothing loaded)
     tr, _ = med(run, reps)
 
     def chain():
