@@ -327,6 +327,25 @@ struct LBytes {
   uint64_t base;
   __device__ __forceinline__ uint8_t operator[](uint64_t i) const { return l[i - base]; }
 };
+// the first '"' or '\\' at or after p (< e), or e: eight bytes per LDS read
+__device__ __forceinline__ uint64_t find_qb(const GBytes &b, uint64_t p, uint64_t e) {
+  while (p < e && b[p] != '"' && b[p] != '\\') ++p;
+  return p;
+}
+__device__ __forceinline__ uint64_t find_qb(const LBytes &b, uint64_t p, uint64_t e) {
+  const uint64_t lo = 0x0101010101010101ull, hi = 0x8080808080808080ull;
+  while (p < e) {
+    const uint64_t rel = p - b.base, al = rel & ~7ull;
+    uint64_t w = *reinterpret_cast<const uint64_t *>(b.l + al);
+    const uint64_t q = w ^ (lo * '"'), s = w ^ (lo * '\\');
+    // exact zero-byte masks (no borrow false positives)
+    const uint64_t zq = ~(((q & ~hi) + ~hi) | q | ~hi), zs = ~(((s & ~hi) + ~hi) | s | ~hi);
+    const uint64_t m = (zq | zs) & (~0ull << (8 * (rel - al)));
+    if (m) return min<uint64_t>(b.base + al + (__builtin_ctzll(m) >> 3), e);
+    p = b.base + al + 8;
+  }
+  return e;
+}
 template <class B>
 struct Cur {
   B b;
@@ -350,20 +369,16 @@ __device__ __forceinline__ bool eat(Cur<B> &c, uint8_t ch) {
 template <class B>
 __device__ __forceinline__ bool skip_string(Cur<B> &c, bool *esc) {
   uint64_t p = c.p + 1;
-  while (p < c.e) {
-    const uint8_t ch = c.b[p];
-    if (ch == '"') {
+  for (;;) {
+    p = find_qb(c.b, p, c.e);
+    if (p >= c.e) return false;
+    if (c.b[p] == '"') {
       c.p = p + 1;
       return true;
     }
-    if (ch == '\\') {
-      *esc = true;
-      p += 2;
-      continue;
-    }
-    ++p;
+    *esc = true;  // a backslash: skip the escaped character
+    p += 2;
   }
-  return false;
 }
 template <class B>
 __device__ bool skip_value(Cur<B> &c) {
