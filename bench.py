@@ -275,6 +275,19 @@ def main():
              "reduce": "k3_reduce", "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check",
              "tail": "k_tail_links"}[dom]
     tr = traffic_of(kname, config, n_local)
+    # SURVEY.md 8d's kernels as whole units (every launch that does that
+    # unit's work), next to the pieces: K2 = join + certificate + its fix-ups,
+    # K3 = produce + reduce (or the one-pass k_stats / k3_small), K4 = the walk
+    # + settle + pending ancestries
+    units = {}
+    for u, parts, alg in (("K2", ("join", "cert", "check", "resolve"), 57 * n_local),
+                          ("K3", ("stats", "reduce"), 19 * n_local),
+                          ("K4", ("walk", "settle", "pend"), 12 * A)):
+        ms = sum(per_kernel[k]["ms_per_step"] for k in parts if k in per_kernel)
+        if ms:
+            gbs = alg / (ms * 1e-3) / 1e9
+            units[u] = {"ms_per_step": round(ms, 4), "alg_bytes": alg, "gbs": round(gbs, 1),
+                        "frac": round(gbs / HBM_PEAK_GBS, 4), "pieces": [k for k in parts if k in per_kernel]}
     h2d = None
     if rank == 0 and not args.no_h2d:
         # the kmz_spans columns (35 B/span) from pinned host memory, as kmz_load
@@ -341,6 +354,7 @@ def main():
                 "pipeline_gbs": round(pipe_bytes / (kern_ms * 1e-3) / 1e9, 1),
                 "kernel_ms_per_step": round(kern_ms, 4),
                 "kernels": per_kernel,
+                "units": units,
             },
             "cpu_baseline": cpu,
             "h2d": h2d,
