@@ -98,11 +98,13 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(config, target_seconds):
+def cpu_baseline(config, target_seconds, tail=None):
     """The all-core OpenMP restatement (oracle/kmz_cpu_omp.c: per-thread group
     moments, a concurrent span-id table, one walk per row into per-thread edge
     sets) on a bounded prefix of the same synthetic workload, timed on this
-    host's cores (OMP_NUM_THREADS; 16 on the GPU box)."""
+    host's cores (OMP_NUM_THREADS; 16 on the GPU box).  ``tail(stats, keys,
+    endpoints)``, when given, is the step's service tail on the CPU, timed
+    with it (oracle/tail_np.py + the same host finish)."""
     from kmamiz_amd import synth
     from oracle import c_oracle
 
@@ -111,8 +113,10 @@ def cpu_baseline(config, target_seconds):
     def run(ntr):
         batch, _ = synth.host_batch(config, 0, ntr)
         t = time.perf_counter()
-        c_oracle.omp_stats(batch, table.tag_ep, table.n_tag_ep, table.n_status)
-        c_oracle.omp_deps(batch, table.dep_ep, table.n_dep_ep)
+        st = c_oracle.omp_stats(batch, table.tag_ep, table.n_tag_ep, table.n_status)
+        keys, ep, _ = c_oracle.omp_deps(batch, table.dep_ep, table.n_dep_ep)
+        if tail is not None:
+            tail(st, keys, ep)
         return len(batch), time.perf_counter() - t
 
     run(2000)  # warm (thread pool, page faults)
@@ -127,7 +131,9 @@ def cpu_baseline(config, target_seconds):
         "cores": threads,
         "kind": "port",
         "sample": f"first {ntr} traces ({n} spans) of the same synthetic workload, seed 0x4B4D414D495A, "
-        f"oracle/kmz_cpu_omp.c stats+deps on {threads} OpenMP threads, {t:.1f} s",
+        f"oracle/kmz_cpu_omp.c stats+deps on {threads} OpenMP threads"
+        + (" + service tail (oracle/tail_np.py, metrics, realtime risk; numpy)" if tail is not None else "")
+        + f", {t:.1f} s",
     }
 
 
@@ -172,7 +178,7 @@ def main():
         import numpy as np
 
         from kmamiz_amd.ingest import SHAPE_TAGS, UNDEFINED, tag_identity
-        from kmamiz_amd.tail import maps_for_synth, realtime_risk_arrays, run_tail
+        from kmamiz_amd.tail import maps_for_synth, realtime_risk_columns, run_tail
 
         args.no_fetch = False
         tmaps = maps_for_synth(config)
@@ -189,12 +195,12 @@ def main():
         is_5xx = np.array([str(x).startswith("5") for x in synth.STATUSES[:n_status]], dtype=bool)
 
     def service_tail():
-        g, _, e = state["groups"], state["keys"], state["endpoints"]
-        t = run_tail(eng, tmaps, e)
+        g, e = state["groups"], state["endpoints"]
+        t = run_tail(eng, tmaps, e)  # reads the edge keys where the run left them, in HBM
         state["metrics"] = t.metrics()
         used = np.nonzero(g["combined"] > 0)[0]
-        state["risk"] = realtime_risk_arrays(t, tag_sid[used // n_status], sid_names, g["combined"][used],
-                                             g["cv"][used], is_5xx[used % n_status], first=g["first"][used])
+        state["risk"] = realtime_risk_columns(t, tag_sid[used // n_status], sid_names, g["combined"][used],
+                                              g["cv"][used], is_5xx[used % n_status], first=g["first"][used])
 
     def step():
         eng.run(flags)
@@ -215,9 +221,10 @@ def main():
             eng.import_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
             eng.finalize()
             if not args.no_fetch:
-                state["groups"], state["keys"], state["endpoints"] = eng.fetch()
-        elif not args.no_fetch:  # the three result sets, one synchronisation
-            state["groups"], state["keys"], state["endpoints"] = eng.fetch()
+                state["groups"], state["keys"], state["endpoints"] = eng.fetch(keys=not tail_on)
+        elif not args.no_fetch:  # the three result sets, one synchronisation (with the tail
+            # on, the edge keys stay in HBM for kmz_tail_run: the service tail is the output)
+            state["groups"], state["keys"], state["endpoints"] = eng.fetch(keys=not tail_on)
         if tail_on:
             service_tail()
 
@@ -311,7 +318,18 @@ def main():
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0:
-            cpu = cpu_baseline(config, args.cpu_seconds)
+            cpu_tail = None
+            if tail_on:
+                def cpu_tail(st, keys, ep):
+                    from oracle.tail_np import tail_np
+
+                    first = np.where(ep["has_row"], ep["first"], np.iinfo(np.uint64).max).astype(np.uint64)
+                    t = tail_np(keys, tmaps, ep["has_row"], first)
+                    t.metrics()
+                    used = np.nonzero(st["combined"] > 0)[0]
+                    realtime_risk_columns(t, tag_sid[used // n_status], sid_names, st["combined"][used],
+                                          st["cv"][used], is_5xx[used % n_status], first=st["first"][used])
+            cpu = cpu_baseline(config, args.cpu_seconds, cpu_tail)
         line = {
             "metric": "spans/sec -> endpoint dependency graph + combined stats (node); % HBM roofline",
             "value": round(spans_per_s, 1),
@@ -340,6 +358,9 @@ def main():
                 "edge_keys": info["n_triples"],
                 "parallelism": f"traceId-shard x{world}" if world > 1 else "single GPU",
                 "service_tail": tail_on,
+                "fetched": ("groups + endpoints to the host; the edge keys stay in HBM, where "
+                            "kmz_tail_run reads them" if tail_on else
+                            "nothing (--no-fetch)" if args.no_fetch else "groups + edge keys + endpoints"),
             },
             "roofline": {
                 "bound": "hbm",

@@ -272,18 +272,21 @@ class Engine:
             out.sort()
         return out
 
-    def fetch(self, groups: bool = True, deps: bool = True):
+    def fetch(self, groups: bool = True, deps: bool = True, keys: bool = True):
         """All result sets of the last run with one stream synchronisation
         (kmz_fetch).  Returns (groups, triples, endpoints); groups and triples
         are views of reused pinned buffers (valid until the next fetch),
-        triples unordered."""
+        triples unordered.  ``keys=False`` leaves the edge keys in HBM (a
+        consumer on the device, e.g. kmz_tail_run, reads them there) and
+        returns None for them."""
         info = self.info()  # the run's cached read-back: no device round trip
+        keys = keys and deps
         g = self._pinned_array("groups", info["n_groups"], L.GROUP_DTYPE) if groups else None
-        t = self._pinned_array("triples", info["n_triples"], np.uint64) if deps else None
+        t = self._pinned_array("triples", info["n_triples"], np.uint64) if keys else None
         e = np.zeros(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE) if deps else None
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_fetch(self.ctx, L.ptr(g) if groups else None, len(g) if groups else 0,
-                                              L.ptr(t) if deps else None, len(t) if deps else 0,
+                                              L.ptr(t) if keys else None, len(t) if keys else 0,
                                               C.byref(n) if deps else None, L.ptr(e) if deps else None,
                                               len(e) if deps else 0))
         return g, t, e

@@ -14,6 +14,8 @@ MINIMUM_PROB = 0.01
 
 def _to_precise(x: float) -> float:
     t = (x + 2.220446049250313e-16) * 1e14
+    if not math.isfinite(t):  # Math.round(NaN / +-Infinity) is itself
+        return t / 1e14
     r = math.floor(t)
     if t - r >= 0.5:
         r += 1

@@ -306,16 +306,47 @@ class ServiceTail:
 
 
 # -- risk over column arrays (RiskAnalyzer.ts:10-122, 171-248) -------------------
-def realtime_risk_arrays(tail: ServiceTail, data_sid: np.ndarray, sid_names: Sequence[str], combined: np.ndarray,
-                         cv: np.ndarray, is_5xx: np.ndarray, replicas: Optional[List[dict]] = None,
-                         first: Optional[np.ndarray] = None) -> List[dict]:
+def _js_max(a: np.ndarray) -> float:
+    """Math.max / Python max over a list: numpy's when no NaN is present (the
+    same value), the builtin's left-to-right rule otherwise."""
+    if not len(a):
+        return -math.inf
+    return float(a.max()) if not np.isnan(a).any() else max(a.tolist())
+
+
+def _js_min(a: np.ndarray) -> float:
+    if not len(a):
+        return math.inf
+    return float(a.min()) if not np.isnan(a).any() else min(a.tolist())
+
+
+def _fixed_ratio(a: np.ndarray) -> np.ndarray:
+    """Normalizer.Strategy.FixedRatio (Normalizer.ts:45-52) on an array."""
+    hi = _js_max(a)
+    return a if hi == 0 else a / hi
+
+
+def _linear(a: np.ndarray, minimum: float = 0.1) -> np.ndarray:
+    """Normalizer.Strategy.Linear (Normalizer.ts:54-64) on an array."""
+    if minimum >= 1:
+        return a
+    return _fixed_ratio(a) * (1 - minimum) + minimum
+
+
+def realtime_risk_columns(tail: ServiceTail, data_sid: np.ndarray, sid_names: Sequence[str], combined: np.ndarray,
+                          cv: np.ndarray, is_5xx: np.ndarray, replicas: Optional[List[dict]] = None,
+                          first: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
     """RiskAnalyzer.RealtimeRisk over the combined rows as columns:
     ``data_sid[i]`` indexes ``sid_names`` (row i's uniqueServiceName).  Rows
     are in toCombinedRealtimeData order, or in any order with ``first`` (each
     row's first span index), which orders services by first occurrence
-    (RiskAnalyzer.ts:18).  Same arithmetic as ``risk.realtime_risk``, which
-    takes row dicts and the full service dependencies."""
-    from .risk import MINIMUM_PROB, Normalizer
+    (RiskAnalyzer.ts:18).  Same fp64 operations, in the same order, as
+    ``risk.realtime_risk`` (which takes row dicts and the full service
+    dependencies), as numpy columns: ``sid`` (service ids in output order),
+    ``risk``, ``impact``, ``probability``, ``norm`` (one element when every
+    risk is equal, Normalizer.ts:22)."""
+    from .cache import to_precise
+    from .risk import MINIMUM_PROB as MP
 
     sid = np.asarray(data_sid, dtype=np.int64)
     if first is None:
@@ -335,41 +366,62 @@ def realtime_risk_arrays(tail: ServiceTail, data_sid: np.ndarray, sid_names: Seq
     wsum = np.bincount(r, weights=np.asarray(cv, dtype=np.float64) * comb, minlength=k)
     cnt = np.bincount(r, weights=comb, minlength=k)
     err = np.bincount(r, weights=comb * np.asarray(is_5xx, dtype=bool), minlength=k)
-    rel_norm = Normalizer.Strategy.SigmoidAdj([wsum[i] / cnt[i] if cnt[i] else math.nan for i in range(k)])
-    total = float(cnt.sum())
-    npro = [(cnt[i] / total) * (1 - MINIMUM_PROB) + MINIMUM_PROB for i in range(k)]
-    nerr = [(err[i] / cnt[i]) * (1 - MINIMUM_PROB) + MINIMUM_PROB for i in range(k)]
-    base = Normalizer.Strategy.Linear([p * nerr[i] for i, p in enumerate(npro)], MINIMUM_PROB)
-    prob = [(rel_norm[i] * (MINIMUM_PROB if base[i] < MINIMUM_PROB else base[i])) * (1 - MINIMUM_PROB) + MINIMUM_PROB
-            for i in range(k)]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rel = np.where(cnt != 0, wsum / np.where(cnt != 0, cnt, 1.0), math.nan)
+        # SigmoidAdj (Normalizer.ts:32-41): the libm exp of risk.py, element by element
+        z = 2 * math.log(3)
+        rel_norm = to_precise(1 / (1 + np.array([math.exp(x) for x in (-z * (rel - 1.5)).tolist()], dtype=np.float64)))
+        total = float(cnt.sum())
+        npro = (cnt / total) * (1 - MP) + MP
+        nerr = (err / cnt) * (1 - MP) + MP
+    base = _linear(npro * nerr, MP)
+    prob = (rel_norm * np.where(base < MP, MP, base)) * (1 - MP) + MP
     # impact (RiskAnalyzer.ts:51-85): factors sorted by localeCompare, zipped
     # with the names in code-unit order
     sv = tail.services
-    rf = tail.relying_factor()[sv]
+    rf = tail.relying_factor()[sv].astype(np.float64)
     ais, ads = tail._acs()
-    acs = (ais * ads)[sv]
+    acs = (ais * ads)[sv].astype(np.float64)
     by_locale = np.argsort(tail.maps.rank("locale")[sv], kind="stable")
-    nrf = Normalizer.Strategy.FixedRatio([float(x) for x in rf[by_locale]])
-    nacs = Normalizer.Strategy.FixedRatio([float(x) for x in acs[by_locale]])
-    names_sorted = [tail.maps.svc_names[v] for v in sv[np.argsort(tail.maps.rank("code")[sv], kind="stable")]]
-    rep = {}
-    for x in replicas or []:
-        rep.setdefault(x["uniqueServiceName"], x.get("replicas"))
-    raw = []
-    for i, usn in enumerate(names_sorted):
-        div = rep.get(usn) or 1
-        raw.append((usn, (nrf[i] + nacs[i]) / div))
-    ni = Normalizer.Strategy.Linear([x[1] for x in raw])
-    imp: Dict[str, float] = {}
-    for i, (usn, _) in enumerate(raw):
-        imp.setdefault(usn, ni[i])
-    risks = []
-    for i, v in enumerate(order_ids.tolist()):
+    by_code = sv[np.argsort(tail.maps.rank("code")[sv], kind="stable")]
+    raw = _fixed_ratio(rf[by_locale]) + _fixed_ratio(acs[by_locale])
+    if replicas:
+        rep = {}
+        for x in replicas:
+            rep.setdefault(x["uniqueServiceName"], x.get("replicas"))
+        names = tail.maps.svc_names
+        raw = raw / np.array([rep.get(names[v]) or 1 for v in by_code.tolist()], dtype=np.float64)
+    ni = _linear(raw)
+    # service id (sid_names) -> position in code-unit order, through the names
+    pos_of = tail.__dict__.setdefault("_code_pos", {})
+    key = (id(sid_names), len(sid_names))
+    if key not in pos_of:
+        at = {tail.maps.svc_names[v]: i for i, v in enumerate(by_code.tolist())}
+        pos_of.clear()
+        pos_of[key] = (sid_names, np.array([at.get(u, -1) for u in sid_names], dtype=np.int64))
+    at_sid = pos_of[key][1][order_ids]  # `imp.get(usn) || 0` below
+    im = np.where(at_sid >= 0, ni[np.maximum(at_sid, 0)] if len(ni) else 0.0, 0.0)
+    p = np.where(prob == 0, MP, prob)  # `probability || MINIMUM_PROB`
+    risk = im * p
+    hi, lo = _js_max(risk), _js_min(risk)
+    norm = np.array([0.1]) if hi - lo == 0 else ((risk - lo) / (hi - lo)) * 0.9 + 0.1
+    return {"sid": order_ids, "risk": risk, "impact": im, "probability": p, "norm": norm}
+
+
+def realtime_risk_arrays(tail: ServiceTail, data_sid: np.ndarray, sid_names: Sequence[str], combined: np.ndarray,
+                         cv: np.ndarray, is_5xx: np.ndarray, replicas: Optional[List[dict]] = None,
+                         first: Optional[np.ndarray] = None) -> List[dict]:
+    """``realtime_risk_columns`` as RiskAnalyzer.RealtimeRisk's row objects."""
+    c = realtime_risk_columns(tail, data_sid, sid_names, combined, cv, is_5xx, replicas, first)
+    norm = c["norm"].tolist()
+    out = []
+    for i, (v, rk, im, p) in enumerate(zip(c["sid"].tolist(), c["risk"].tolist(), c["impact"].tolist(),
+                                           c["probability"].tolist())):
         usn = sid_names[v]
         s, n, ver = (usn.split("\t") + [None] * 3)[:3]
-        im = imp.get(usn) or 0
-        p = prob[i] or MINIMUM_PROB
-        risks.append({"uniqueServiceName": usn, "service": s, "namespace": n, "version": ver, "risk": im * p,
-                      "impact": im, "probability": p})
-    norm = Normalizer.Strategy.BetweenFixedNumber([x["risk"] for x in risks])
-    return [{**x, **({"norm": norm[i]} if i < len(norm) else {})} for i, x in enumerate(risks)]
+        x = {"uniqueServiceName": usn, "service": s, "namespace": n, "version": ver, "risk": rk, "impact": im,
+             "probability": p}
+        if i < len(norm):
+            x["norm"] = norm[i]
+        out.append(x)
+    return out
