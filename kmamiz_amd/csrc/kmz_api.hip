@@ -59,6 +59,7 @@ struct kmz_ctx {
   DevBuf k3pool, k3dir, k3part, tile_tmp, sgrp;
   DevBuf dp, cpool1, cpool2, ccur, cdir, mkey, mval;  // window join + certificate
   DevBuf ctab, plist, kstage, kstage_n, kdefer, kdefer_n, cetab;  // K4 chain interning
+  DevBuf kbucket, kbucket_n;  // staged keys partitioned by edge-set slice (k_key_part)
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
   // device JSON ingest (kmz_json.hip)
@@ -88,7 +89,13 @@ struct kmz_ctx {
   bool ctab_dirty = true;  // the chain table holds entries no list records (new, or a list overflowed)
   int path = 0;             // kmz_info.path of the last dependency run
   bool sstats = false;      // shape-level K3 partials computed in this run
-  bool chain_ran = false;   // this run's dependency graph came from k4_chain
+  bool chain_ran = false;   // this run's dependency graph came from k4_chain's chain interning
+  // K4 mode: chain interning, or direct enumeration (every row stages all its
+  // keys) when most rows start a new chain -- chosen from the last interning
+  // run's chains/rows for this shape table, measured again every 64 runs
+  uint64_t k4_key = ~0ull;
+  bool k4_auto_direct = false, k4_direct_ran = false;
+  uint32_t k4_since = 0;
   uint64_t cap = 0, tcap = 1ull << 16, ccap = 1ull << 20;
   uint64_t sig_seed = SIG_SEED0;  // K4 ancestry-hash seed (changed after a collision)
   uint32_t dcap = 1024;
@@ -301,7 +308,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
                     &c->tl_sstat, &c->tl_rel, &c->o_key, &c->o_val, &c->o_out,
@@ -783,6 +790,19 @@ static int run_shape_stats(kmz_ctx *c) {
   return KMZ_OK;
 }
 
+static bool k4_direct(kmz_ctx *c) {
+  if (c->ablate & (1u << 28)) return true;  // test knobs: force direct enumeration / chain interning
+  if (c->ablate & (1u << 29)) return false;
+  const uint64_t key = ((uint64_t)c->n_shapes << 32) | c->n_dep;
+  if (key != c->k4_key) {
+    c->k4_key = key;
+    c->k4_auto_direct = false;
+    c->k4_since = 0;
+  }
+  // (small batches: either mode is quick, keep interning)
+  return c->k4_auto_direct && c->n >= (1u << 20) && (++c->k4_since % 64) != 0;
+}
+
 static int run_deps(kmz_ctx *c, bool links) {
   const uint32_t n = (uint32_t)c->n;
   // unique edge keys are far fewer than spans; start at ~n/32 (grown on overflow)
@@ -815,17 +835,24 @@ static int run_deps(kmz_ctx *c, bool links) {
     // unique span ids: rows are the SERVER spans; chain interning (kmz_chain.hip)
     if (!c->sstats && (r = run_shape_stats(c))) return r;
     const uint32_t nt = chain_tiles(n);
-    // per persistent workgroup: staged keys of candidate new chains and
-    // deferred chain checks (overflow is handled in place, just slower)
-    // and the slots each workgroup claims in the chain table (wcap each; the
-    // run's global list of wcap more follows them)
+    const bool direct = k4_direct(c);
+    // per persistent workgroup: staged keys (of candidate new chains, or of
+    // every row when direct) in one run per coarse bin of the edge set's
+    // slices, and deferred chain checks (overflow is handled in place, just
+    // slower) and the slots each workgroup claims in the chain table (wcap
+    // each; the run's global list of wcap more follows them); the staged keys
+    // partitioned per slice (as many again)
     const uint32_t scap = c->scap, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
+    uint32_t lb1, lb2;
+    if (!key_bins(c->tcap, &lb1, &lb2)) return fail(c, KMZ_E_ARG, "edge-set capacity is not ESLICE * 2^k");
+    const uint64_t nsl = c->tcap / ESLICE, bcap = ((uint64_t)ng * scap + nsl - 1) / nsl;
     void *old_ctab = c->ctab.p;
     if (ensure(c, c->ctab, c->ccap * CHAIN_ENTRY_BYTES) || ensure(c, c->ctile, (size_t)nt * 16) ||
         ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, (size_t)ng * scap * 8) ||
-        ensure(c, c->kstage_n, (size_t)ng * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 16) ||
+        ensure(c, c->kstage_n, ((size_t)ng << lb1) * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 16) ||
         ensure(c, c->kdefer_n, (size_t)ng * 4) || ensure(c, c->kwpos, ((size_t)ng + 1) * wcap * 4) ||
-        ensure(c, c->kwpos_n, (size_t)ng * 4) || ensure(c, c->cetab, ((size_t)c->n_shapes + 1) * 16))
+        ensure(c, c->kwpos_n, (size_t)ng * 4) || ensure(c, c->cetab, ((size_t)c->n_shapes + 1) * 16) ||
+        ensure(c, c->kbucket, nsl * bcap * 8) || ensure(c, c->kbucket_n, nsl * 4))
       return KMZ_E_HIP;
     if (c->ctab.p != old_ctab) c->ctab_dirty = true;
     uint32_t *wpos = P<uint32_t>(c->kwpos), *gpos = wpos + (size_t)ng * wcap;
@@ -833,10 +860,12 @@ static int run_deps(kmz_ctx *c, bool links) {
       Timed t(c, KMZ_K_MEMSET);
       // the chain table is cleared entry by entry after each run; a full
       // memset only when it is new or a list overflowed
-      if (c->ctab_dirty) HIPCHK(c, hipMemsetAsync(c->ctab.p, 0, c->ccap * CHAIN_ENTRY_BYTES, c->stream));
+      if (c->ctab_dirty && !direct) HIPCHK(c, hipMemsetAsync(c->ctab.p, 0, c->ccap * CHAIN_ENTRY_BYTES, c->stream));
       HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
+      HIPCHK(c, hipMemsetAsync(c->kbucket_n.p, 0, nsl * 4, c->stream));
     }
-    c->ctab_dirty = true;  // until this run's slots are cleared below
+    const bool was_dirty = c->ctab_dirty;
+    if (!direct) c->ctab_dirty = true;  // until this run's slots are cleared below
     {
       Timed t(c, KMZ_K_WALK);
       launch_chain(c->stream, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
@@ -844,22 +873,23 @@ static int run_deps(kmz_ctx *c, bool links) {
                    P<unsigned long long>(c->trip), c->tcap, epp, links ? P<unsigned long long>(c->rowpos) : nullptr,
                    P<uint32_t>(c->plist), n + 1, cnt, P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage),
                    scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
-                   wpos, wcap, P<uint32_t>(c->kwpos_n), P<uint4>(c->cetab),
+                   wpos, wcap, P<uint32_t>(c->kwpos_n), P<uint4>(c->cetab), direct,
                    // (test knob 24 forces sig collisions on the first seed only)
                    c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)));
     }
     {
       Timed t(c, KMZ_K_SETTLE);
-      launch_chain_settle(c->stream, n, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
+      launch_chain_settle(c->stream, n, direct, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
                           P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), scap,
-                          P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
+                          P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kbucket), bcap,
+                          P<uint32_t>(c->kbucket_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
                           gpos, wcap);
     }
     {  // ancestries that left their window: one pass, sized on the device (no host round trip)
       Timed t(c, KMZ_K_PEND);
       launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent),
                         n, P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
-                        P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, wcap);
+                        P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, wcap, direct);
     }
     if (c->overlap) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_k3, 0));  // the shape-level K3 partials
     {
@@ -869,11 +899,13 @@ static int run_deps(kmz_ctx *c, bool links) {
       launch_collapse_endpoints(c->stream, P<unsigned long long>(c->sgrp), c->n_shapes, c->n_status,
                                 P<uint32_t>(c->d_dep), c->n_dep, P<uint32_t>(c->cparent), c->index_base, epp,
                                 epp + c->n_dep, cnt);
-      launch_chain_clear(c->stream, n, c->ctab.p, wpos, wcap, P<uint32_t>(c->kwpos_n), gpos, wcap, cnt);
+      if (!direct) launch_chain_clear(c->stream, n, c->ctab.p, wpos, wcap, P<uint32_t>(c->kwpos_n), gpos, wcap, cnt);
     }
-    c->ctab_dirty = false;  // (set again after the run if a list overflowed: F_CTAB_DIRTY)
-    c->path = (joined ? 1 : 0) | 2;
-    c->chain_ran = true;
+    // (set again after the run if a list overflowed: F_CTAB_DIRTY)
+    c->ctab_dirty = direct ? was_dirty : false;
+    c->path = (joined ? 1 : 0) | 2 | (direct ? 4 : 0);
+    c->chain_ran = !direct;
+    c->k4_direct_ran = direct;
     return KMZ_OK;
   }
   // repeated span ids: the row of an id is its last occurrence at its first
@@ -1112,6 +1144,8 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     // chain table at load factor <= 1/8 while it fits the 256 MB MALL, else
     // <= 1/4: a found chain is then almost always at its home slot (each
     // extra slot is another dependent probe round trip)
+    // most rows start a new chain (config 5): enumerate directly next time
+    if (c->chain_ran) c->k4_auto_direct = s64[S_CHAINS] * 2 > s64[S_ROWS];
     while (c->chain_ran && c->ccap < (1ull << 31) &&
            (s64[S_CHAINS] * 4 > c->ccap || (s64[S_CHAINS] * 8 > c->ccap && c->ccap * CHAIN_ENTRY_BYTES < (256ull << 20))))
       c->ccap *= 2;

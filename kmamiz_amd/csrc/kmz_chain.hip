@@ -64,6 +64,9 @@ constexpr uint16_t W_NONE = 0xFFFF, W_CYC = 0xFFFE, W_OUT = 0xFFFD;
 constexpr uint32_t WIN_DEPTH = 255;  // deeper in-window ancestries take the pending path
 constexpr uint32_t PROBE_MAX = 512;
 constexpr uint32_t IMAP = 256;  // LDS map: one inserting leader per distinct new chain
+// staged keys are binned by the edge set's slices: 2^lb1 coarse bins per tile
+// workgroup (k4_chain), each split into 2^lb2 slices by k_key_part
+constexpr uint32_t KB1_MAX = 6, KB2_MAX = 10;
 #ifndef KMZ_CHAIN_WAVES
 #define KMZ_CHAIN_WAVES 4
 #endif
@@ -115,7 +118,7 @@ __device__ __forceinline__ void edge_insert(uint64_t key, unsigned long long *__
       cur = atomicCAS(&trip[pos], 0ull, (unsigned long long)key);
       if (cur == 0 || cur == key) return;
     }
-    pos = pos + 1 == tcap ? 0 : pos + 1;
+    pos = eset_next(pos, tcap);
   }
   *flags |= F_TRIPLE_OVERFLOW;
 }
@@ -157,6 +160,7 @@ __device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, 
 
 __device__ unsigned long long g_chain_dbg[8];  // diagnostic phase clocks (KMZ_ABLATE bit 22 only)
 
+template <bool DIRECT>
 __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape, const int64_t *__restrict__ ts,
     const uint32_t *__restrict__ cparent, uint32_t n, const uint4 *__restrict__ etab, uint32_t n_shapes,
@@ -166,12 +170,13 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     unsigned int *__restrict__ counters, uint32_t *__restrict__ wg_stats, unsigned long long *__restrict__ stage,
     uint32_t scap, uint32_t *__restrict__ stage_n, unsigned long long *__restrict__ defer, uint32_t dcap,
     uint32_t *__restrict__ defer_n, uint32_t *__restrict__ wpos, uint32_t wcap, uint32_t *__restrict__ wpos_n,
-    uint32_t nt, uint32_t ablate) {
+    uint32_t nt, uint32_t lb1, uint32_t lb2, uint32_t ablate) {
   // one 16-byte record per window slot: element hash (x, y), endpoint (z),
   // contracted parent | kind << 16 (w) -- a walk step is one LDS read
   __shared__ uint4 lrec[CW];
   __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP];
-  __shared__ uint32_t scnt, dcnt;  // keys staged for k_chain_settle, records deferred to k_chain_settle
+  __shared__ uint32_t lbin[1u << KB1_MAX];  // keys staged per coarse bin (k_key_part), deferred records
+  __shared__ uint32_t dcnt;
   __shared__ uint32_t wcnt;        // chain-table slots this workgroup claimed (cleared after the run)
   __shared__ uint32_t red[CTT / 64][4];
   // diagnostic phase clock (KMZ_ABLATE bit 22 only): s_memtime deltas by thread 0
@@ -202,12 +207,35 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
 #pragma unroll
     for (int q = 0; q < CPW; ++q) e[q] = etab[sh[q] < n_shapes ? sh[q] : 0];
   };
-  if (threadIdx.x == 0) scnt = dcnt = wcnt = 0;
+  if (threadIdx.x == 0) dcnt = wcnt = 0;
+  if (threadIdx.x < (1u << KB1_MAX)) lbin[threadIdx.x] = 0;
   if (blockIdx.x < nt) {
     fetch(blockIdx.x);
     gather_ep();
   }
   uint32_t rows = 0, rel = 0, maxd = 0, fresh_n = 0, flags = 0;
+  // staged keys: this workgroup's region holds 2^lb1 runs of `sub` keys, one
+  // per coarse bin of the edge set's slices (k_key_part takes them from there)
+  const uint32_t sub = scap >> lb1;
+  auto stage_key = [&](uint64_t key) {
+    const uint32_t b = (uint32_t)((slot_of(key, tcap) / ESLICE) >> lb2);
+    const uint32_t x = atomicAdd(&lbin[b], 1u);
+    if (x < sub) {
+      stage[(((uint64_t)blockIdx.x << lb1) + b) * sub + x] = key;
+    } else {  // this run is full: insert here (slow: one lane per key); more staging next run
+      edge_insert(key, trip, tcap, &flags);
+      flags |= F_STAGE_FULL;
+    }
+  };
+  // the keys of the row in window slot jl: (ancestor k, row endpoint es, k, ancestor is SERVER)
+  auto stage_row = [&](uint32_t jl, uint32_t es, uint32_t d) {
+    uint32_t a = lrec[jl].w & 0xFFFF;
+    for (uint32_t kk = 1; kk <= d; ++kk) {
+      const uint4 r = lrec[a];
+      stage_key(edge_key(r.z, es, kk, ((r.w >> 16) & 3) == KIND_SERVER));
+      a = r.w & 0xFFFF;
+    }
+  };
   for (uint32_t tile = blockIdx.x; tile < nt; tile += gridDim.x) {
     KMZ_STAMP(0);
     const uint32_t t0 = tile * CT, t1 = min(n, t0 + CT);
@@ -259,6 +287,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       st[q] = S_DONE;
       if (!hash_on) continue;
       if (kq[q] == KIND_SERVER && r.z >= n_ep) flags |= F_RANGE;
+      if (DIRECT && kq[q] != KIND_SERVER) continue;  // direct: only rows walk (no chains to intern)
       wa[q] = r.w & 0xFFFF;
     }
     // the TPW walks of a thread step together: TPW independent LDS reads in
@@ -284,6 +313,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           else
             flags |= F_RANGE;
         }
+        // direct: a row stages each key as its walk reaches the ancestor (a
+        // row that turns out pending stages them all again in k4_chain_pend:
+        // duplicates are harmless in the edge set)
+        if (DIRECT && act) stage_key(edge_key(r[q].z, myep[q], dd[q] + 1, ((r[q].w >> 16) & 3) == KIND_SERVER));
         acc[q] = act ? nacc : acc[q];
         dd[q] += act ? 1u : 0u;
         wa[q] = act ? (r[q].w & 0xFFFF) : wa[q];
@@ -301,6 +334,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         sg[q] = 0;
         continue;
       }
+      if (DIRECT) continue;  // every row stages its keys: no chain sig
       const uint32_t d = dd[q];
       ps[q] = d ? sig_final(acc[q], d - 1, seed, &flags) : ROOT_SIG;
       sg[q] = sig_final(rotl64(sg[q], SIG_R * d) ^ acc[q], d, seed, &flags);
@@ -310,110 +344,99 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       }
       if (!(ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
-    ulonglong2 w01[TPW];  // (sig, parent sig) of the probed slot
-    uint64_t pos[TPW];
+    if (DIRECT) {  // (the rows staged their keys during the walk)
+      if (more) gather_ep();
+    } else {
+      ulonglong2 w01[TPW];  // (sig, parent sig) of the probed slot
+      uint64_t pos[TPW];
 #pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-      const bool pr = st[q] == S_PUT;
-      pos[q] = pr ? cslot(sg[q], ccap) : 0;
-      const unsigned long long *en = ctab + 2 * pos[q];
-      w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(en) : make_ulonglong2(0, 0);
-    }
-    KMZ_STAMP(2);
-    // check what the probes found against (parent sig, endpoint, kind); a
-    // chain not found (or not yet published) elects one leader per distinct
-    // sig in this workgroup
-    uint32_t hslot[TPW];
+      for (int q = 0; q < TPW; ++q) {
+        const bool pr = st[q] == S_PUT;
+        pos[q] = pr ? cslot(sg[q], ccap) : 0;
+        const unsigned long long *en = ctab + 2 * pos[q];
+        w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(en) : make_ulonglong2(0, 0);
+      }
+      KMZ_STAMP(2);
+      // check what the probes found against (parent sig, endpoint, kind); a
+      // chain not found (or not yet published) elects one leader per distinct
+      // sig in this workgroup
+      uint32_t hslot[TPW];
 #pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-      hslot[q] = IMAP + 1;  // not an insert
-      if (st[q] != S_PUT) continue;
-      for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
-        pos[q] = pos[q] + 1 == ccap ? 0 : pos[q] + 1;
-        w01[q] = *reinterpret_cast<const ulonglong2 *>(ctab + 2 * pos[q]);
-      }
-      st[q] = S_DONE;
-      if (w01[q].x == sg[q] && w01[q].y != 0) {
-        if (w01[q].y != ps[q]) flags |= F_SIG;
-        continue;
-      }
-      uint32_t h = (uint32_t)(sg[q] >> 32) & (IMAP - 1);
-      hslot[q] = IMAP;  // a leader without a map slot (map full)
-      for (uint32_t t = 0; t < 8; ++t) {
-        const unsigned long long kk = atomicCAS(&imap_sig[h], 0ull, (unsigned long long)sg[q]);
-        if (kk == 0) {  // leader: publish what the followers compare against
-          imap_psig[h] = ps[q];
-          hslot[q] = h;
-          break;
+      for (int q = 0; q < TPW; ++q) {
+        hslot[q] = IMAP + 1;  // not an insert
+        if (st[q] != S_PUT) continue;
+        for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
+          pos[q] = pos[q] + 1 == ccap ? 0 : pos[q] + 1;
+          w01[q] = *reinterpret_cast<const ulonglong2 *>(ctab + 2 * pos[q]);
         }
-        if (kk == sg[q]) {  // follower
-          hslot[q] = h | 0x80000000u;
-          break;
+        st[q] = S_DONE;
+        if (w01[q].x == sg[q] && w01[q].y != 0) {
+          if (w01[q].y != ps[q]) flags |= F_SIG;
+          continue;
         }
-        h = (h + 1) & (IMAP - 1);
-      }
-    }
-    if (more) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
-    if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
-#pragma unroll
-      for (int q = 0; q < TPW; ++q) hslot[q] = IMAP + 1;
-    __syncthreads();
-    KMZ_STAMP(3);
-    // followers compare with their leader; leaders claim the slot the probe
-    // ended on (one CAS), publish if they won, and defer a final check to
-    // k_chain_settle otherwise.  Keys of a leader's chain are staged whether
-    // or not it is new (duplicates are harmless in the edge set), so nothing
-    // here waits on another workgroup.
-#pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-      if (hslot[q] > IMAP) {
-        if (hslot[q] != IMAP + 1) {  // follower
-          const uint32_t h = hslot[q] & (IMAP - 1);
-          if (imap_psig[h] != ps[q]) flags |= F_SIG;
-        }
-        continue;
-      }
-      const uint32_t jl = toff + q * CTT + threadIdx.x;
-      unsigned long long *en = ctab + 2 * pos[q];
-      const unsigned long long cv = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
-      const uint32_t d = dd[q];
-      // a row whose chain this leader inserted (or lost to another chain: the
-      // deferred check may insert it) stages its keys; one that joined the
-      // same chain leaves them to the winner (knob 19: diagnostic, none)
-      if (kq[q] == KIND_SERVER && d && cv != sg[q] && !(ablate & (1u << 19))) {
-        const uint32_t es = myep[q];
-        const uint32_t base = atomicAdd(&scnt, d);
-        uint32_t a = lrec[jl].w & 0xFFFF;
-        for (uint32_t kk = 1; kk <= d; ++kk) {
-          const uint4 r = lrec[a];
-          const uint64_t key = edge_key(r.z, es, kk, ((r.w >> 16) & 3) == KIND_SERVER);
-          if (base + d <= scap)
-            stage[(uint64_t)blockIdx.x * scap + base + kk - 1] = key;  // inserted by k_chain_settle
-          else {
-            edge_insert(key, trip, tcap, &flags);  // staging region full: insert here (slow: one lane per chain)
-            flags |= F_STAGE_FULL;
+        uint32_t h = (uint32_t)(sg[q] >> 32) & (IMAP - 1);
+        hslot[q] = IMAP;  // a leader without a map slot (map full)
+        for (uint32_t t = 0; t < 8; ++t) {
+          const unsigned long long kk = atomicCAS(&imap_sig[h], 0ull, (unsigned long long)sg[q]);
+          if (kk == 0) {  // leader: publish what the followers compare against
+            imap_psig[h] = ps[q];
+            hslot[q] = h;
+            break;
           }
-          a = r.w & 0xFFFF;
+          if (kk == sg[q]) {  // follower
+            hslot[q] = h | 0x80000000u;
+            break;
+          }
+          h = (h + 1) & (IMAP - 1);
         }
       }
-      if (cv == 0) {  // won the slot: publish
-        atomicExch(&en[1], (unsigned long long)ps[q]);
-        ++fresh_n;
-        const uint32_t x = atomicAdd(&wcnt, 1u);
-        if (x < wcap)
-          wpos[(uint64_t)blockIdx.x * wcap + x] = (uint32_t)pos[q];
-        else
-          flags |= F_CTAB_DIRTY;
-      } else {  // joined an unpublished entry, or lost the slot to another chain
-        const uint32_t x = atomicAdd(&dcnt, 1u);
-        if (x < dcap) {
-          *reinterpret_cast<ulonglong2 *>(defer + 2 * ((uint64_t)blockIdx.x * dcap + x)) = make_ulonglong2(sg[q], ps[q]);
-        } else {
-          int rr = 0;
-          for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t)
-            rr = chain_put(ctab, ccap, sg[q], ps[q], &flags, wpos + (uint64_t)gridDim.x * wcap, wcap,
-                           counters);  // (the run's global written list follows the per-workgroup ones)
-          fresh_n += rr == 1;
+      if (more) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
+      if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) hslot[q] = IMAP + 1;
+      __syncthreads();
+      KMZ_STAMP(3);
+      // followers compare with their leader; leaders claim the slot the probe
+      // ended on (one CAS), publish if they won, and defer a final check to
+      // k_chain_settle otherwise.  Keys of a leader's chain are staged whether
+      // or not it is new (duplicates are harmless in the edge set), so nothing
+      // here waits on another workgroup.
+#pragma unroll
+      for (int q = 0; q < TPW; ++q) {
+        if (hslot[q] > IMAP) {
+          if (hslot[q] != IMAP + 1) {  // follower
+            const uint32_t h = hslot[q] & (IMAP - 1);
+            if (imap_psig[h] != ps[q]) flags |= F_SIG;
+          }
+          continue;
+        }
+        const uint32_t jl = toff + q * CTT + threadIdx.x;
+        unsigned long long *en = ctab + 2 * pos[q];
+        const unsigned long long cv = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
+        const uint32_t d = dd[q];
+        // a row whose chain this leader inserted (or lost to another chain: the
+        // deferred check may insert it) stages its keys; one that joined the
+        // same chain leaves them to the winner (knob 19: diagnostic, none)
+        if (kq[q] == KIND_SERVER && d && cv != sg[q] && !(ablate & (1u << 19))) stage_row(jl, myep[q], d);
+        if (cv == 0) {  // won the slot: publish
+          atomicExch(&en[1], (unsigned long long)ps[q]);
+          ++fresh_n;
+          const uint32_t x = atomicAdd(&wcnt, 1u);
+          if (x < wcap)
+            wpos[(uint64_t)blockIdx.x * wcap + x] = (uint32_t)pos[q];
+          else
+            flags |= F_CTAB_DIRTY;
+        } else {  // joined an unpublished entry, or lost the slot to another chain
+          const uint32_t x = atomicAdd(&dcnt, 1u);
+          if (x < dcap) {
+            *reinterpret_cast<ulonglong2 *>(defer + 2 * ((uint64_t)blockIdx.x * dcap + x)) = make_ulonglong2(sg[q], ps[q]);
+          } else {
+            int rr = 0;
+            for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t)
+              rr = chain_put(ctab, ccap, sg[q], ps[q], &flags, wpos + (uint64_t)gridDim.x * wcap, wcap,
+                             counters);  // (the run's global written list follows the per-workgroup ones)
+            fresh_n += rr == 1;
+          }
         }
       }
     }
@@ -465,8 +488,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     for (int w = 0; w < CTT / 64; ++w) a = threadIdx.x == 2 ? max(a, red[w][2]) : a + red[w][threadIdx.x];
     wg_stats[(uint64_t)blockIdx.x * 4 + threadIdx.x] = a;
   }
+  for (uint32_t b = threadIdx.x; b < (1u << lb1); b += CTT) stage_n[((uint64_t)blockIdx.x << lb1) + b] = min(lbin[b], sub);
   if (threadIdx.x == 0) {
-    stage_n[blockIdx.x] = min(scnt, scap);
     defer_n[blockIdx.x] = min(dcnt, dcap);
     wpos_n[blockIdx.x] = min(wcnt, wcap);
   }
@@ -475,23 +498,182 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
 #undef KMZ_STAMP
 }
 
-// keys of the chains the tile kernel staged, per workgroup -> the edge set;
-// and the deferred chain checks: every entry the tile kernel claimed is
-// published by now, so each deferred (sig, parent sig, endpoint/kind) is
+// Direct enumeration stages every relation's key (~450M at config 5's 1e8
+// spans, ~30 per distinct key): they reach the edge set in two passes that
+// keep every HBM access streaming and every probe in LDS:
+//   k_key_part   one (workgroup, coarse bin) run at a time, 4096 keys per
+//                step: ranks within the run's 2^lb2 slices from an LDS
+//                histogram, one global reservation per (step, slice), the
+//                keys counting-sorted by slice in LDS and written out as one
+//                contiguous piece per slice (~64 keys at config 5)
+//   k_key_slice  one slice per workgroup: its ESLICE slots of the edge set
+//                into LDS, its bucket's keys inserted there (the slice is a
+//                self-contained table, eset_next), the slice written back
+// A full bucket inserts in place (edge_insert) and asks for more staging.
+// Chain interning stages few keys (new chains only): k_chain_settle inserts
+// them in place, which is cheaper at that volume.
+constexpr uint32_t KP_T = 256, KP_PER = 16, KP_STEP = KP_T * KP_PER;  // 4096 keys per step
+
+// exclusive prefix sum of v[0..m) in LDS (m <= 4 * KP_T), by the whole workgroup
+__device__ __forceinline__ void kp_scan(uint32_t *__restrict__ v, uint32_t m, uint32_t *__restrict__ wsum) {
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t loc[4], run = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t i = 4 * t + j;
+    loc[j] = run;
+    run += i < m ? v[i] : 0;
+  }
+  uint32_t x = run;  // inclusive scan of the per-thread totals over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = x - run;
+  for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t i = 4 * t + j;
+    if (i < m) v[i] = before + loc[j];
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__restrict__ stage, uint32_t sub,
+                                                   const uint32_t *__restrict__ stage_n, uint32_t nruns, uint32_t lb1,
+                                                   uint32_t lb2, unsigned long long *__restrict__ bucket,
+                                                   uint64_t bcap, uint32_t *__restrict__ bucket_n,
+                                                   unsigned long long *__restrict__ trip, uint64_t tcap,
+                                                   unsigned int *__restrict__ counters) {
+  __shared__ unsigned long long sorted[KP_STEP];  // 32 KB
+  __shared__ uint16_t sbin[KP_STEP];
+  __shared__ uint32_t hist[1u << KB2_MAX], off[1u << KB2_MAX], base[1u << KB2_MAX], wsum[KP_T / 64];
+  static_assert((1u << KB2_MAX) <= 4 * KP_T, "kp_scan covers the slices of a coarse bin");
+  const uint32_t nf = 1u << lb2;
+  uint32_t flags = 0;
+  for (uint32_t r = blockIdx.x; r < nruns; r += gridDim.x) {
+    const uint32_t m = stage_n[r];
+    const uint32_t c = r & ((1u << lb1) - 1);  // the run's coarse bin
+    const unsigned long long *src = stage + (uint64_t)r * sub;
+    for (uint32_t c0 = 0; c0 < m; c0 += KP_STEP) {
+      const uint32_t cnt = min(m - c0, KP_STEP);
+      for (uint32_t x = threadIdx.x; x < nf; x += KP_T) hist[x] = 0;
+      __syncthreads();
+      uint64_t k[KP_PER];
+      uint32_t f[KP_PER], rk[KP_PER];
+#pragma unroll
+      for (int j = 0; j < (int)KP_PER; ++j) {  // all loads in flight together
+        const uint32_t i = j * KP_T + threadIdx.x;
+        k[j] = i < cnt ? src[c0 + i] : 0;  // (edge keys are nonzero)
+      }
+#pragma unroll
+      for (int j = 0; j < (int)KP_PER; ++j) {
+        f[j] = (uint32_t)(slot_of(k[j], tcap) / ESLICE) & (nf - 1);
+        rk[j] = k[j] ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
+      }
+      __syncthreads();
+      for (uint32_t x = threadIdx.x; x < nf; x += KP_T) {
+        const uint32_t h = hist[x];
+        base[x] = h ? atomicAdd(&bucket_n[(c << lb2) + x], h) : 0;
+        off[x] = h;
+      }
+      __syncthreads();
+      kp_scan(off, nf, wsum);
+#pragma unroll
+      for (int j = 0; j < (int)KP_PER; ++j) {
+        if (!k[j]) continue;
+        const uint32_t q = off[f[j]] + rk[j];
+        sorted[q] = k[j];
+        sbin[q] = (uint16_t)f[j];
+      }
+      __syncthreads();
+      // consecutive threads -> consecutive slots of one slice's bucket
+      for (uint32_t i = threadIdx.x; i < cnt; i += KP_T) {
+        const uint32_t fb = sbin[i];
+        const uint64_t p = (uint64_t)base[fb] + (i - off[fb]);
+        if (p < bcap) {
+          bucket[(uint64_t)((c << lb2) + fb) * bcap + p] = sorted[i];
+        } else {
+          edge_insert(sorted[i], trip, tcap, &flags);
+          flags |= F_STAGE_FULL;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (flags) atomicOr(&counters[C_FLAGS], flags);
+}
+
+constexpr uint32_t KS_T = 1024, KS_PER = 8;  // 16 waves per slice, 8 keys per thread in flight
+__global__ void __launch_bounds__(KS_T) k_key_slice(const unsigned long long *__restrict__ bucket, uint64_t bcap,
+                                                    const uint32_t *__restrict__ bucket_n, uint32_t nsl,
+                                                    unsigned long long *__restrict__ trip, uint64_t tcap,
+                                                    unsigned int *__restrict__ counters) {
+  __shared__ unsigned long long tab[ESLICE];  // 64 KB
+  uint32_t flags = 0;
+  for (uint32_t b = blockIdx.x; b < nsl; b += gridDim.x) {
+    const uint32_t m = (uint32_t)min((uint64_t)bucket_n[b], bcap);
+    if (!m) continue;  // (uniform over the workgroup) the slice keeps what it holds
+    ulonglong2 *g = reinterpret_cast<ulonglong2 *>(trip + (uint64_t)b * ESLICE);
+    ulonglong2 *l = reinterpret_cast<ulonglong2 *>(tab);
+    for (uint32_t x = threadIdx.x; x < ESLICE / 2; x += KS_T) l[x] = g[x];
+    __syncthreads();
+    const unsigned long long *src = bucket + (uint64_t)b * bcap;
+    for (uint32_t x0 = 0; x0 < m; x0 += KS_T * KS_PER) {
+      unsigned long long k[KS_PER];
+#pragma unroll
+      for (int j = 0; j < (int)KS_PER; ++j) {
+        const uint32_t i = x0 + j * KS_T + threadIdx.x;
+        k[j] = i < m ? src[i] : 0;
+      }
+#pragma unroll
+      for (int j = 0; j < (int)KS_PER; ++j) {
+        if (!k[j]) continue;
+        uint32_t p = (uint32_t)(slot_of(k[j], tcap) & (ESLICE - 1));
+        uint32_t z = 0;
+        for (; z < PROBE_MAX; ++z) {
+          unsigned long long cur = tab[p];
+          if (cur == k[j]) break;
+          if (cur == 0) {
+            cur = atomicCAS(&tab[p], 0ull, k[j]);
+            if (cur == 0 || cur == k[j]) break;
+          }
+          p = (p + 1) & (uint32_t)(ESLICE - 1);
+        }
+        if (z == PROBE_MAX) flags |= F_TRIPLE_OVERFLOW;
+      }
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < ESLICE / 2; x += KS_T) g[x] = l[x];
+    __syncthreads();
+  }
+  if (flags) atomicOr(&counters[C_FLAGS], flags);
+}
+
+// chain interning: the keys the tile kernel staged (workgroup w's runs) ->
+// the edge set in place; and the deferred chain checks: every entry the tile
+// kernel claimed is published by now, so each deferred (sig, parent sig) is
 // joined and checked, or inserted if its slot was lost to another chain
-__global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *__restrict__ stage, uint32_t scap,
-                                                      const uint32_t *__restrict__ stage_n,
+__global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *__restrict__ stage, uint32_t sub,
+                                                      const uint32_t *__restrict__ stage_n, uint32_t lb1,
+                                                      unsigned long long *__restrict__ trip, uint64_t tcap,
                                                       const unsigned long long *__restrict__ defer, uint32_t dcap,
                                                       const uint32_t *__restrict__ defer_n, uint32_t nwg,
-                                                      unsigned long long *__restrict__ trip, uint64_t tcap,
                                                       unsigned long long *__restrict__ ctab, uint64_t ccap,
                                                       unsigned int *__restrict__ counters,
                                                       unsigned long long *__restrict__ stats64,
                                                       uint32_t *__restrict__ gpos, uint32_t gcap) {
   uint32_t flags = 0, fresh = 0;
   for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
-    const uint32_t m = stage_n[w];
-    for (uint32_t x = threadIdx.x; x < m; x += blockDim.x) edge_insert(stage[(uint64_t)w * scap + x], trip, tcap, &flags);
+    for (uint32_t b = 0; b < (1u << lb1); ++b) {
+      const uint64_t r = ((uint64_t)w << lb1) + b;
+      const uint32_t m = stage_n[r];
+      for (uint32_t x = threadIdx.x; x < m; x += blockDim.x) edge_insert(stage[r * sub + x], trip, tcap, &flags);
+    }
     const uint32_t md = defer_n[w];
     for (uint32_t x = threadIdx.x; x < md; x += blockDim.x) {
       const unsigned long long *r = defer + 2 * ((uint64_t)w * dcap + x);
@@ -521,7 +703,7 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
                                                      unsigned long long *__restrict__ ep_ts,
                                                      unsigned int *__restrict__ counters,
                                                      unsigned long long *__restrict__ stats64,
-                                                     uint32_t *__restrict__ gpos, uint32_t gcap) {
+                                                     uint32_t *__restrict__ gpos, uint32_t gcap, bool direct) {
   const uint32_t m = min(counters[C_PLIST], pcap);
   uint32_t flags = 0;
   for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
@@ -556,7 +738,7 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     }
     if (bad) continue;
     const uint64_t sg = sig_final(acc, d, seed, &flags), psig = a == NONE ? ROOT_SIG : sig_final(pacc, d - 1, seed, &flags);
-    int r = 0;
+    int r = direct ? 3 : 0;  // direct: no chain table, every row inserts its keys
     for (uint32_t t = 0; t < 1u << 20 && r == 0; ++t)
       r = chain_put(ctab, ccap, sg, psig, &flags, gpos, gcap, counters);
     if (r <= 0) continue;
@@ -571,7 +753,7 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
           flags |= F_RANGE;
           break;
         }
-        if (r == 1) edge_insert(edge_key(ea, es, kk, ka == KIND_SERVER), trip, tcap, &flags);
+        if (r != 2) edge_insert(edge_key(ea, es, kk, ka == KIND_SERVER), trip, tcap, &flags);
         if (ka != KIND_SERVER) atomicMax(&ep_ts[ea], (unsigned long long)((uint64_t)ts[cur] ^ TS_BIAS));
       }
       atomicAdd(&stats64[S_ROWS], 1ull);
@@ -634,27 +816,55 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint32_t pcap, unsigned int *counters, uint32_t *wg_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
                   uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
-                  uint4 *etab, uint32_t ablate) {
+                  uint4 *etab, bool direct, uint32_t ablate) {
   const uint32_t nt = chain_tiles(n);
   if (!nt) return;
+  uint32_t lb1, lb2;
+  key_bins(tcap, &lb1, &lb2);
   const uint32_t g = chain_grid(n);
   unsigned long long *tab = reinterpret_cast<unsigned long long *>(ctab);
   hipLaunchKernelGGL(k_chain_etab, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_shapes + 255) / 256, 1024))),
                      dim3(256), 0, s, dep_ep, n_shapes, seed, etab);
-  hipLaunchKernelGGL(k4_chain, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, etab, n_shapes, n_ep,
-                     index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
-                     scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, ablate);
+  if (direct)
+    hipLaunchKernelGGL(k4_chain<true>, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, etab, n_shapes, n_ep,
+                       index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
+                       scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, lb1, lb2, ablate);
+  else
+    hipLaunchKernelGGL(k4_chain<false>, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, etab, n_shapes, n_ep,
+                       index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
+                       scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, lb1, lb2, ablate);
 }
 
-void launch_chain_settle(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip, uint64_t tcap,
-                         unsigned int *counters, const uint32_t *wg_stats, unsigned long long *stats64,
+bool key_bins(uint64_t tcap, uint32_t *lb1, uint32_t *lb2) {
+  // slices of the edge set: tcap / ESLICE (tcap a power of two >= ESLICE)
+  uint32_t ls = 0;
+  while ((ESLICE << ls) < tcap) ++ls;
+  *lb1 = std::min<uint32_t>(ls, KB1_MAX);
+  *lb2 = ls - *lb1;
+  return (ESLICE << ls) == tcap && *lb2 <= KB2_MAX;
+}
+
+void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uint64_t ccap, unsigned long long *trip,
+                         uint64_t tcap, unsigned int *counters, const uint32_t *wg_stats, unsigned long long *stats64,
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
+                         unsigned long long *bucket, uint64_t bcap, uint32_t *bucket_n,
                          const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
                          uint32_t gcap) {
   if (!chain_tiles(n)) return;
   const uint32_t g = chain_grid(n);
-  hipLaunchKernelGGL(k_chain_settle, dim3(g), dim3(256), 0, s, stage, scap, stage_n, defer, dcap, defer_n, g, trip,
-                     tcap, reinterpret_cast<unsigned long long *>(ctab), ccap, counters, stats64, gpos, gcap);
+  uint32_t lb1, lb2;
+  key_bins(tcap, &lb1, &lb2);
+  const uint32_t nsl = (uint32_t)(tcap / ESLICE), nruns = g << lb1;
+  if (direct) {
+    hipLaunchKernelGGL(k_key_part, dim3(std::min<uint32_t>(nruns, 8192)), dim3(KP_T), 0, s, stage, scap >> lb1,
+                       stage_n, nruns, lb1, lb2, bucket, bcap, bucket_n, trip, tcap, counters);
+    hipLaunchKernelGGL(k_key_slice, dim3(std::min<uint32_t>(nsl, 8192)), dim3(KS_T), 0, s, bucket, bcap, bucket_n, nsl,
+                       trip, tcap, counters);
+  } else {
+    hipLaunchKernelGGL(k_chain_settle, dim3(g), dim3(256), 0, s, stage, scap >> lb1, stage_n, lb1, trip, tcap, defer,
+                       dcap, defer_n, g, reinterpret_cast<unsigned long long *>(ctab), ccap, counters, stats64, gpos,
+                       gcap);
+  }
   launch_tile_sum(s, wg_stats, g, 4u, 4u, stats64 + S_ROWS, 2u);  // rows, rel, maxd, chains
 }
 
@@ -687,10 +897,10 @@ void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, cons
                        const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
-                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap) {
+                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct) {
   hipLaunchKernelGGL(k4_chain_pend, dim3(1024), dim3(256), 0, s, plist, pcap, kind, shape, ts, cparent, n, dep_ep,
                      n_shapes, n_ep, seed, reinterpret_cast<unsigned long long *>(ctab), ccap, trip, tcap, ep_ts,
-                     counters, stats64, gpos, gcap);
+                     counters, stats64, gpos, gcap, direct);
 }
 
 }  // namespace kmz

@@ -57,6 +57,17 @@ KMZ_HD uint32_t shard_of(uint64_t hi, uint64_t lo, uint32_t world) {
 KMZ_HD uint64_t slot_of(uint64_t k, uint64_t cap) { return mulhi64(mix64(k ^ 0x5bd1e9955bd1e995ull), cap); }
 KMZ_HD uint32_t tag_of(uint64_t k) { return (uint32_t)(mix64(k + 0x9e3779b97f4a7c15ull) >> 32); }
 
+// Edge-key sets (the run's `trip` table) probe linearly inside slices of
+// ESLICE slots: a key's probe sequence wraps within the slice of its home
+// slot, so every slice is a self-contained table (kmz_chain.hip builds each
+// one in LDS from the keys partitioned to it).  A cap that is not a multiple
+// of ESLICE probes the whole table.
+constexpr uint64_t ESLICE = 8192;
+KMZ_HD uint64_t eset_next(uint64_t pos, uint64_t cap) {
+  if (cap % ESLICE) return pos + 1 == cap ? 0 : pos + 1;
+  return (pos & ~(ESLICE - 1)) | ((pos + 1) & (ESLICE - 1));
+}
+
 // ---- JS number semantics ----------------------------------------------------
 // Math.round: nearest, ties toward +inf (ECMA-262 Math.round)
 KMZ_HD double js_round(double x) {

@@ -396,7 +396,7 @@ __device__ __forceinline__ void triple_global(uint64_t key, unsigned long long *
       }
       if (cur == key) return;
     }
-    pos = (pos + 1 == tcap) ? 0 : pos + 1;
+    pos = eset_next(pos, tcap);  // (sliced probing, kmz_common.h)
   }
   atomicOr(&counters[C_FLAGS], F_TRIPLE_OVERFLOW);
 }

@@ -282,7 +282,13 @@ def test_device_generation_equals_host(engine):
         assert a[0].tobytes() == b[0].tobytes()
         assert np.array_equal(a[1], b[1])
         assert a[2].tobytes() == b[2].tobytes()
-        assert a[3] == b[3]
+        assert _info_results(a[3]) == _info_results(b[3])
+
+
+def _info_results(info):
+    """kmz_info without the fields that say which K4 mode ran (chain interning
+    or direct enumeration: the same results, different diagnostics)."""
+    return {k: v for k, v in info.items() if k not in ("n_chains", "path")}
 
 
 @pytest.mark.parametrize("config,ntr", [(2, 136000)])
@@ -405,10 +411,10 @@ def test_window_join_matches_span_table(engine):
         b = run(e2)
     finally:
         e2.close()
-    assert a[4]["path"] == 3 and b[4]["path"] == 2
+    assert a[4]["path"] & 3 == 3 and b[4]["path"] & 3 == 2  # (bit 4: which K4 mode ran)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
     assert a[3].tobytes() == b[3].tobytes()
-    assert {k: v for k, v in a[4].items() if k != "path"} == {k: v for k, v in b[4].items() if k != "path"}
+    assert _info_results(a[4]) == _info_results(b[4])
 
 
 # ---------------------------------------------------------------------------
@@ -441,7 +447,7 @@ def test_sig_collision_is_detected_and_retried(engine):
         e2.close()
     assert np.array_equal(a[0], b[0])
     assert a[1].tobytes() == b[1].tobytes()
-    assert a[2] == b[2]
+    assert _info_results(a[2]) == _info_results(b[2])
 
 
 def test_deep_chain_takes_the_pending_path(engine):
@@ -563,11 +569,12 @@ def test_from_json_equals_object_ingest(engine, src):
     assert a.toEndpointDependencies().toJSON() == b.toEndpointDependencies().toJSON()
 
 
-@pytest.mark.parametrize("knob", [1 << 30])
+@pytest.mark.parametrize("knob", [1 << 30, (1 << 30) | (1 << 28)])
 def test_key_staging_paths_equal(engine, knob):
-    """K4's staged edge keys reach the edge set through k_chain_settle, or in
-    place when a workgroup's staging overflows (KMZ_ABLATE bit 30: 256 slots;
-    the staging then grows run by run).  Same graph either way."""
+    """K4's staged edge keys reach the edge set through k_key_part +
+    k_key_slice, or in place when a workgroup's staging overflows (KMZ_ABLATE
+    bit 30: 256 slots; the staging then grows run by run), with chain
+    interning or direct enumeration (bit 28).  Same graph either way."""
     import os
 
     from kmamiz_amd import Engine
@@ -590,9 +597,75 @@ def test_key_staging_paths_equal(engine, knob):
             b = run(e2)
             assert np.array_equal(a[0], b[0])
             assert a[1].tobytes() == b[1].tobytes()
-            assert {k: v for k, v in a[2].items() if k != "flags"} == {k: v for k, v in b[2].items() if k != "flags"}
+            skip = ("flags", "n_chains", "path")  # (which K4 mode ran: diagnostics, not results)
+            assert {k: v for k, v in a[2].items() if k not in skip} == {k: v for k, v in b[2].items() if k not in skip}
     finally:
         e2.close()
+
+
+def _engine_with(knob):
+    import os
+
+    from kmamiz_amd import Engine
+
+    os.environ["KMZ_ABLATE"] = str(knob)
+    try:
+        return Engine(0)
+    finally:
+        del os.environ["KMZ_ABLATE"]
+
+
+@pytest.fixture(scope="module")
+def direct_engine():
+    """An engine whose K4 always enumerates directly (KMZ_ABLATE bit 28: every
+    row stages all its keys, no chain table)."""
+    e = _engine_with(1 << 28)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("config,ntr", [(2, 30000), (3, 4000), (3, 40000), (5, 2000), (5, 20000)])
+def test_direct_enumeration_vs_c_oracle(direct_engine, config, ntr):
+    from kmamiz_amd import synth
+
+    batch, off = synth.host_batch(config, 0, ntr)
+    for _ in range(2):  # the second run reuses the edge set, buckets and staging
+        info = _compare_synth(direct_engine, batch, synth.shape_table(config))
+        assert info["path"] & 4 and info["n_chains"] == 0
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 3))
+def test_direct_enumeration_messy_batches(direct_engine, seed):
+    test_messy_batches_vs_oracle(direct_engine, seed)
+
+
+def test_direct_enumeration_deep_chain(direct_engine):
+    test_deep_chain_takes_the_pending_path(direct_engine)
+
+
+def test_k4_mode_follows_chain_reuse(engine):
+    """Auto mode: config 5 (most rows start a new chain) switches to direct
+    enumeration after an interning run; config 3 (chains repeat; a small
+    batch) stays interning.  The graph is the same either way."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    e = _engine_with(0)
+    try:
+        for config, ntr, want in ((5, 20000, 4), (3, 20000, 0)):
+            e.load_synthetic(config, synth.SEED, 0, ntr)
+            runs = []
+            for _ in range(3):
+                e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+                runs.append((e.triples(), e.endpoints(), e.info()))
+            # (the first kmz_run interns; a retry inside it -- the edge set
+            # grown -- may already enumerate)
+            assert runs[1][2]["path"] & 4 == want and runs[2][2]["path"] & 4 == want
+            assert (runs[2][2]["n_chains"] > 0) == (want == 0)
+            for t, ep, _ in runs[1:]:
+                assert np.array_equal(t, runs[0][0]) and ep.tobytes() == runs[0][1].tobytes()
+    finally:
+        e.close()
 
 
 @pytest.mark.parametrize("seed", range(6))
