@@ -227,12 +227,21 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       flags |= F_STAGE_FULL;
     }
   };
-  // the keys of the row in window slot jl: (ancestor k, row endpoint es, k, ancestor is SERVER)
+  // chain interning (one run per workgroup, lb1 = 0): the keys of the row in
+  // window slot jl, (ancestor k, row endpoint es, k, ancestor is SERVER),
+  // under one reservation
   auto stage_row = [&](uint32_t jl, uint32_t es, uint32_t d) {
+    const uint32_t base = atomicAdd(&lbin[0], d);
     uint32_t a = lrec[jl].w & 0xFFFF;
     for (uint32_t kk = 1; kk <= d; ++kk) {
       const uint4 r = lrec[a];
-      stage_key(edge_key(r.z, es, kk, ((r.w >> 16) & 3) == KIND_SERVER));
+      const uint64_t key = edge_key(r.z, es, kk, ((r.w >> 16) & 3) == KIND_SERVER);
+      if (base + kk - 1 < sub) {
+        stage[(uint64_t)blockIdx.x * sub + base + kk - 1] = key;
+      } else {
+        edge_insert(key, trip, tcap, &flags);
+        flags |= F_STAGE_FULL;
+      }
       a = r.w & 0xFFFF;
     }
   };
@@ -821,6 +830,10 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
   if (!nt) return;
   uint32_t lb1, lb2;
   key_bins(tcap, &lb1, &lb2);
+  if (!direct) {  // chain interning stages few keys: one run per workgroup, inserted in place
+    lb2 += lb1;
+    lb1 = 0;
+  }
   const uint32_t g = chain_grid(n);
   unsigned long long *tab = reinterpret_cast<unsigned long long *>(ctab);
   hipLaunchKernelGGL(k_chain_etab, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_shapes + 255) / 256, 1024))),
@@ -854,6 +867,10 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
   const uint32_t g = chain_grid(n);
   uint32_t lb1, lb2;
   key_bins(tcap, &lb1, &lb2);
+  if (!direct) {  // (as launch_chain)
+    lb2 += lb1;
+    lb1 = 0;
+  }
   const uint32_t nsl = (uint32_t)(tcap / ESLICE), nruns = g << lb1;
   if (direct) {
     hipLaunchKernelGGL(k_key_part, dim3(std::min<uint32_t>(nruns, 8192)), dim3(KP_T), 0, s, stage, scap >> lb1,

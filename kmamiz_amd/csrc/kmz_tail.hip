@@ -197,7 +197,10 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
 }
 
 // aggregation tables -> dense kmz_tail_detail (MODE 0) / kmz_tail_pair (MODE 1)
-// records, wave-aggregated output positions
+// records.  Each workgroup owns a contiguous range of the table, counts its
+// entries, reserves their output range with ONE atomic (a per-wave atomic on
+// one counter serialises: ~10^5 of them cost 1.5 ms), then writes them.
+constexpr uint32_t TAIL_COMPACT_BLOCKS = 1024;
 template <int MODE>
 __global__ void __launch_bounds__(256) k_tail_compact(const unsigned long long *__restrict__ akey,
                                                       const uint32_t *__restrict__ aval, uint64_t cap,
@@ -206,18 +209,35 @@ __global__ void __launch_bounds__(256) k_tail_compact(const unsigned long long *
                                                       uint32_t *__restrict__ rel, uint32_t n_dist,
                                                       unsigned int *__restrict__ counters) {
   constexpr uint32_t W = MODE == 0 ? 6 : 3;  // record words
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x; p0 < cap; p0 += (uint64_t)gridDim.x * blockDim.x) {
+  __shared__ uint32_t wsum[4];
+  __shared__ unsigned long long base;
+  const uint64_t per = (cap + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(cap, b0 + per);
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t c = 0;
+  for (uint64_t p = b0 + threadIdx.x; p < b1; p += 256) c += akey[p] != 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) wsum[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    base = t ? atomicAdd(count, (unsigned long long)t) : 0;
+  }
+  __syncthreads();
+  unsigned long long run = base;
+  for (uint64_t p0 = b0; p0 < b1; p0 += 256) {
     const uint64_t p = p0 + threadIdx.x;
-    const unsigned long long k = p < cap ? akey[p] : 0;
+    const unsigned long long k = p < b1 ? akey[p] : 0;
     const uint64_t m = __ballot(k != 0);
-    if (!m) continue;
-    const int lead = __ffsll((long long)m) - 1;
-    unsigned long long base = 0;
-    if ((int)lane == lead) base = atomicAdd(count, (unsigned long long)__popcll(m));
-    base = __shfl(base, lead, 64);
+    if (lane == 0) wsum[w] = __popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t v = 0; v < 4; ++v) {
+      before += v < w ? wsum[v] : 0;
+      tot += wsum[v];
+    }
     if (k) {
-      uint32_t *r = out + (uint64_t)W * (base + __popcll(m & ((1ull << lane) - 1)));
+      uint32_t *r = out + (uint64_t)W * (run + before + __popcll(m & ((1ull << lane) - 1)));
       if (MODE == 0) {  // detail key svc << 40 | lsvc << 16 | d
         r[0] = (uint32_t)(k >> 40);
         r[1] = (uint32_t)(k >> 16) & 0xFFFFFFu;
@@ -240,6 +260,8 @@ __global__ void __launch_bounds__(256) k_tail_compact(const unsigned long long *
         r[2] = aval[p];
       }
     }
+    run += tot;
+    __syncthreads();
   }
 }
 
@@ -254,10 +276,10 @@ void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned l
   hipLaunchKernelGGL(k_tail_links, dim3(g), dim3(256), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls,
                      lset, lcap, akey, aval, acap, pset, pcap, pkey, pval, pacap, hasin, fkey, fval, fcap, sstat, rel,
                      n_dist, counters);
-  const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((acap + 255) / 256, 4096));
+  const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((acap + 255) / 256, TAIL_COMPACT_BLOCKS));
   hipLaunchKernelGGL(k_tail_compact<0>, dim3(ga), dim3(256), 0, s, akey, aval, acap, links_out, out_counts, rel, n_dist,
                      counters);
-  const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pacap + 255) / 256, 4096));
+  const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pacap + 255) / 256, TAIL_COMPACT_BLOCKS));
   hipLaunchKernelGGL(k_tail_compact<1>, dim3(gp), dim3(256), 0, s, pkey, pval, pacap, pairs_out, out_counts + 1, rel,
                      n_dist, counters);
 }

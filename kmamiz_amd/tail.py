@@ -144,8 +144,11 @@ def run_tail(eng, maps: TailMaps, endpoints: np.ndarray) -> "ServiceTail":
 
     if dist.value == 0:  # a distance beyond the dense relying table: sum the details instead
         det, pairs = fetch()
-        return ServiceTail.from_details(maps, det, pairs, hasin, endpoints)
-    return ServiceTail(maps, stats, by_dist, hasin, endpoints, fetch)
+        t = ServiceTail.from_details(maps, det, pairs, hasin, endpoints)
+    else:
+        t = ServiceTail(maps, stats, by_dist, hasin, endpoints, fetch)
+    t.n_details, t.n_pairs = nd_, npairs_
+    return t
 
 
 def _by(n, idx, w=None):
@@ -392,14 +395,17 @@ def realtime_risk_columns(tail: ServiceTail, data_sid: np.ndarray, sid_names: Se
         names = tail.maps.svc_names
         raw = raw / np.array([rep.get(names[v]) or 1 for v in by_code.tolist()], dtype=np.float64)
     ni = _linear(raw)
-    # service id (sid_names) -> position in code-unit order, through the names
-    pos_of = tail.__dict__.setdefault("_code_pos", {})
+    # service id (sid_names) -> tail service id, through the names (cached on
+    # the maps, which outlive the per-run tails), then -> position in code-unit order
+    cache = tail.maps.__dict__.setdefault("_sid_to_svc", {})
     key = (id(sid_names), len(sid_names))
-    if key not in pos_of:
-        at = {tail.maps.svc_names[v]: i for i, v in enumerate(by_code.tolist())}
-        pos_of.clear()
-        pos_of[key] = (sid_names, np.array([at.get(u, -1) for u in sid_names], dtype=np.int64))
-    at_sid = pos_of[key][1][order_ids]  # `imp.get(usn) || 0` below
+    if key not in cache:
+        at = {u: v for v, u in enumerate(tail.maps.svc_names)}
+        cache.clear()
+        cache[key] = (sid_names, np.array([at.get(u, -1) for u in sid_names], dtype=np.int64))
+    code_pos = np.full(len(tail.maps.svc_names) + 1, -1, dtype=np.int64)
+    code_pos[by_code] = np.arange(len(by_code))
+    at_sid = code_pos[cache[key][1][order_ids]]  # (index -1 -> the sentinel: `imp.get(usn) || 0` below)
     im = np.where(at_sid >= 0, ni[np.maximum(at_sid, 0)] if len(ni) else 0.0, 0.0)
     p = np.where(prob == 0, MP, prob)  # `probability || MINIMUM_PROB`
     risk = im * p

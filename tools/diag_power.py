@@ -77,6 +77,7 @@ def main():
     out = {k: round(statistics.median(v[1:]) * 1e3, 3) for k, v in marks.items()}
     out["spans"] = n
     out["edge_keys"] = int(nk)
+    out["tail_details"], out["tail_pairs"] = int(tl.n_details), int(tl.n_pairs)
     out["info"] = {k: v for k, v in eng.info().items() if isinstance(v, int)}
     print(json.dumps(out))
     eng.close()
