@@ -1149,7 +1149,9 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     while (c->chain_ran && c->ccap < (1ull << 31) &&
            (s64[S_CHAINS] * 4 > c->ccap || (s64[S_CHAINS] * 8 > c->ccap && c->ccap * CHAIN_ENTRY_BYTES < (256ull << 20))))
       c->ccap *= 2;
-    if ((flags & KMZ_RUN_DEPS) && s64[S_TRIP_OUT] * 2 > c->tcap) c->tcap *= 2;
+    if ((flags & KMZ_RUN_DEPS) && ((c->ablate & (1u << 31)) ? s64[S_TRIP_OUT] * 8 > c->tcap * 7
+                                                           : s64[S_TRIP_OUT] * 2 > c->tcap))
+      c->tcap *= 2;  // (knob 31: diagnostic, a MALL-sized edge set at load <= 7/8)
     bool retry = false;
     if (h[C_FLAGS] & F_MISS_OVERFLOW) {
       c->mcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(2ull * c->mcap, 2ull * h[C_MISS] + 64), 0xFFFFFFF0ull);
@@ -1916,3 +1918,35 @@ int kmz_synth_host(int config, uint64_t seed, uint64_t t0, uint64_t t1, uint64_t
 }
 
 }  // extern "C"
+
+// diagnostic (tools/diag_power.py): K4 staging occupancy of the last run --
+// scap, staged keys (sum, max per run), bucket fill (sum, max), bucket
+// capacity, slices, coarse bins
+extern "C" int kmz__debug_k4(kmz_ctx *c, unsigned long long *out) {
+  if (!c || !out) return KMZ_E_ARG;
+  const uint32_t ng = chain_grid((uint32_t)c->n);
+  uint32_t lb1 = 0, lb2 = 0;
+  key_bins(c->tcap, &lb1, &lb2);
+  if (!c->k4_direct_ran) {
+    lb2 += lb1;
+    lb1 = 0;
+  }
+  const uint64_t nsl = c->tcap / ESLICE;
+  std::vector<uint32_t> sn((size_t)ng << lb1), bn(nsl);
+  if (c->kstage_n.p && hipMemcpy(sn.data(), c->kstage_n.p, sn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return KMZ_E_HIP;
+  if (c->kbucket_n.p && hipMemcpy(bn.data(), c->kbucket_n.p, bn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return KMZ_E_HIP;
+  unsigned long long s1 = 0, m1 = 0, s2 = 0, m2 = 0;
+  for (uint32_t v : sn) s1 += v, m1 = std::max<unsigned long long>(m1, v);
+  for (uint32_t v : bn) s2 += v, m2 = std::max<unsigned long long>(m2, v);
+  out[0] = c->scap;
+  out[1] = s1;
+  out[2] = m1;
+  out[3] = s2;
+  out[4] = m2;
+  out[5] = ((uint64_t)ng * c->scap + nsl - 1) / nsl;
+  out[6] = nsl;
+  out[7] = 1ull << lb1;
+  return KMZ_OK;
+}

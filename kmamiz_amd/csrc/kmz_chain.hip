@@ -67,6 +67,10 @@ constexpr uint32_t IMAP = 256;  // LDS map: one inserting leader per distinct ne
 // staged keys are binned by the edge set's slices: 2^lb1 coarse bins per tile
 // workgroup (k4_chain), each split into 2^lb2 slices by k_key_part
 constexpr uint32_t KB1_MAX = 6, KB2_MAX = 10;
+// direct enumeration: a workgroup drops keys it staged recently (a direct-mapped
+// LDS cache of KCACHE keys).  Hot edge keys repeat ~10^5 times per run; without
+// the cache they overfill their slice's bucket.
+constexpr uint32_t KCACHE = 2048;
 #ifndef KMZ_CHAIN_WAVES
 #define KMZ_CHAIN_WAVES 4
 #endif
@@ -176,6 +180,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   __shared__ uint4 lrec[CW];
   __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP];
   __shared__ uint32_t lbin[1u << KB1_MAX];  // keys staged per coarse bin (k_key_part), deferred records
+  __shared__ unsigned long long kcache[DIRECT ? KCACHE : 1];
   __shared__ uint32_t dcnt;
   __shared__ uint32_t wcnt;        // chain-table slots this workgroup claimed (cleared after the run)
   __shared__ uint32_t red[CTT / 64][4];
@@ -209,6 +214,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   };
   if (threadIdx.x == 0) dcnt = wcnt = 0;
   if (threadIdx.x < (1u << KB1_MAX)) lbin[threadIdx.x] = 0;
+  if (DIRECT)
+    for (uint32_t x = threadIdx.x; x < KCACHE; x += CTT) kcache[x] = 0;
   if (blockIdx.x < nt) {
     fetch(blockIdx.x);
     gather_ep();
@@ -218,8 +225,18 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   // per coarse bin of the edge set's slices (k_key_part takes them from there)
   const uint32_t sub = scap >> lb1;
   auto stage_key = [&](uint64_t key) {
-    const uint32_t b = (uint32_t)((slot_of(key, tcap) / ESLICE) >> lb2);
+    if (ablate & (1u << 21)) return;  // diagnostic knob: walk only
+    const uint64_t pos = slot_of(key, tcap);
+    unsigned long long &ce = kcache[DIRECT ? (uint32_t)pos & (KCACHE - 1) : 0];
+    if (ce == key) return;  // staged recently by this workgroup (races only let a duplicate through)
+    ce = key;
+    if (ablate & (1u << 31)) {  // diagnostic knob: insert in place (no staging)
+      edge_insert(key, trip, tcap, &flags);
+      return;
+    }
+    const uint32_t b = (uint32_t)((pos / ESLICE) >> lb2);
     const uint32_t x = atomicAdd(&lbin[b], 1u);
+    if (ablate & (1u << 20)) return;  // diagnostic knob: no staging store
     if (x < sub) {
       stage[(((uint64_t)blockIdx.x << lb1) + b) * sub + x] = key;
     } else {  // this run is full: insert here (slow: one lane per key); more staging next run
@@ -264,7 +281,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       if (jl < wn) lrec[jl] = make_uint4((uint32_t)el, (uint32_t)(el >> 32), ep, cp | ((uint32_t)(k[q] & 3) << 16));
       other |= jl < wn && (k[q] & 3) != KIND_SERVER && !client;
     }
-    for (uint32_t x = threadIdx.x; x < IMAP; x += CTT) imap_sig[x] = 0;
+    if (!DIRECT)
+      for (uint32_t x = threadIdx.x; x < IMAP; x += CTT) imap_sig[x] = 0;
     const bool any_other = __syncthreads_or(other);
     KMZ_STAMP(1);
     const bool more = tile + gridDim.x < nt;

@@ -1,6 +1,7 @@
 """Where config 5's step time goes (bench.py --config power): device run,
 result fetch, device tail, host tail finish (metrics, realtime risk).
 usage: python tools/diag_power.py [traces] -> one JSON line of median ms"""
+import ctypes as C
 import json
 import os
 import statistics
@@ -31,6 +32,7 @@ def main():
                 hi = mid
         ntr = lo
     n = eng.load_synthetic(cfg, synth.SEED, 0, ntr)
+    print("loaded", n, file=sys.stderr, flush=True)
     from kmamiz_amd.ingest import SHAPE_TAGS, UNDEFINED, tag_identity
 
     tmaps = maps_for_synth(cfg)
@@ -47,11 +49,18 @@ def main():
     is_5xx_st = np.array([str(x).startswith("5") for x in synth.STATUSES[:n_status]], dtype=bool)
     flags = L.RUN_STATS_TAG | L.RUN_DEPS
     marks = {k: [] for k in ("run", "fetch_all", "fetch_no_keys", "tail_device", "metrics", "risk", "risk_dicts")}
+    dbg_fn = L.lib().kmz__debug_k4
+    dbg_fn.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    k4 = []  # scap, staged sum, max per run, bucket sum, max, bcap, slices, coarse bins, flags, path
     for rep in range(6):
         t = time.perf_counter()
         eng.run(flags)
         eng.sync()
         marks["run"].append(time.perf_counter() - t)
+        dbg = (C.c_ulonglong * 8)()
+        L.check(eng.ctx, dbg_fn(eng.ctx, dbg))
+        k4.append([int(x) for x in dbg] + [eng.info()["flags"], eng.info()["path"]])
+        print("rep", rep, k4[-1], round(marks["run"][-1] * 1e3, 3), file=sys.stderr, flush=True)
         t = time.perf_counter()
         g, k, e = eng.fetch()
         nk = len(k)
@@ -77,6 +86,7 @@ def main():
     out = {k: round(statistics.median(v[1:]) * 1e3, 3) for k, v in marks.items()}
     out["spans"] = n
     out["edge_keys"] = int(nk)
+    out["k4"] = k4
     out["tail_details"], out["tail_pairs"] = int(tl.n_details), int(tl.n_pairs)
     out["info"] = {k: v for k, v in eng.info().items() if isinstance(v, int)}
     print(json.dumps(out))
