@@ -612,6 +612,7 @@ class _DepResult:
         self.info = eng.info()
         self.index_base = eng.index_base
         self.order = eng.dep_entries()
+        self.eng, self.gen = eng, eng.gen  # (the engine still holds this run while its gen is unchanged)
         for e in d.poison["dep"]:
             if self.endpoints["has_row"][e] or np.any((self.triples >> np.uint64(40)) == np.uint64(e)):
                 raise self._poison_error(e)
@@ -714,10 +715,12 @@ class EndpointDependencies:
 
         if self._native is None:
             raise ValueError("service_tail() needs an engine-backed result")
-        traces = self._native.traces
-        eng = traces._load()
-        eng.run(L.RUN_DEPS)
-        return run_tail(eng, maps_from_dictionary(self._native.dict, labelMap), eng.endpoints())
+        nat = self._native
+        eng = nat.eng
+        if eng.gen != nat.gen:  # the engine ran something else since: this batch's dependency pass again
+            eng = nat.traces._load()
+            eng.run(L.RUN_DEPS)
+        return run_tail(eng, maps_from_dictionary(nat.dict, labelMap), eng.endpoints())
 
     def toReduced(self, reg=None):
         """Columns of ``EndpointDependencies([]).combineWith(self).trim()``

@@ -70,7 +70,7 @@ constexpr uint32_t KB1_MAX = 6, KB2_MAX = 10;
 // direct enumeration: a workgroup drops keys it staged recently (a direct-mapped
 // LDS cache of KCACHE keys).  Hot edge keys repeat ~10^5 times per run; without
 // the cache they overfill their slice's bucket.
-constexpr uint32_t KCACHE = 2048;
+constexpr uint32_t KCACHE = 1024;
 #ifndef KMZ_CHAIN_WAVES
 #define KMZ_CHAIN_WAVES 4
 #endif
@@ -114,7 +114,7 @@ __device__ __forceinline__ uint64_t edge_key(uint32_t ea, uint32_t es, uint32_t 
 // is counted by the compaction
 __device__ __forceinline__ void edge_insert(uint64_t key, unsigned long long *__restrict__ trip, uint64_t tcap,
                                            uint32_t *flags) {
-  uint64_t pos = slot_of(key, tcap);
+  uint64_t pos = eslot(key, tcap);
   for (uint32_t z = 0; z < PROBE_MAX; ++z) {
     uint64_t cur = trip[pos];
     if (cur == key) return;
@@ -178,9 +178,12 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   // one 16-byte record per window slot: element hash (x, y), endpoint (z),
   // contracted parent | kind << 16 (w) -- a walk step is one LDS read
   __shared__ uint4 lrec[CW];
-  __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP];
+  __shared__ unsigned long long imap_sig[DIRECT ? 1 : IMAP], imap_psig[DIRECT ? 1 : IMAP];
   __shared__ uint32_t lbin[1u << KB1_MAX];  // keys staged per coarse bin (k_key_part), deferred records
   __shared__ unsigned long long kcache[DIRECT ? KCACHE : 1];
+  // direct: per-wave ring of keys waiting to be staged (the walk's active
+  // lanes append; 64 at a time are staged by all lanes together)
+  __shared__ unsigned long long squeue[DIRECT ? CTT / 64 : 1][DIRECT ? 256 : 1];
   __shared__ uint32_t dcnt;
   __shared__ uint32_t wcnt;        // chain-table slots this workgroup claimed (cleared after the run)
   __shared__ uint32_t red[CTT / 64][4];
@@ -224,9 +227,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   // staged keys: this workgroup's region holds 2^lb1 runs of `sub` keys, one
   // per coarse bin of the edge set's slices (k_key_part takes them from there)
   const uint32_t sub = scap >> lb1;
+  const uint32_t tshift = 64u - (uint32_t)__builtin_ctzll(tcap);  // (tcap is ESLICE * 2^k: key_bins)
   auto stage_key = [&](uint64_t key) {
     if (ablate & (1u << 21)) return;  // diagnostic knob: walk only
-    const uint64_t pos = slot_of(key, tcap);
+    const uint64_t pos = (key * 0x9E3779B97F4A7C15ull) >> tshift;  // eslot(key, tcap): tcap = 2^(64 - tshift)
     unsigned long long &ce = kcache[DIRECT ? (uint32_t)pos & (KCACHE - 1) : 0];
     if (ce == key) return;  // staged recently by this workgroup (races only let a duplicate through)
     ce = key;
@@ -236,7 +240,6 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     }
     const uint32_t b = (uint32_t)((pos / ESLICE) >> lb2);
     const uint32_t x = atomicAdd(&lbin[b], 1u);
-    if (ablate & (1u << 20)) return;  // diagnostic knob: no staging store
     if (x < sub) {
       stage[(((uint64_t)blockIdx.x << lb1) + b) * sub + x] = key;
     } else {  // this run is full: insert here (slow: one lane per key); more staging next run
@@ -318,12 +321,25 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       wa[q] = r.w & 0xFFFF;
     }
     // the TPW walks of a thread step together: TPW independent LDS reads in
-    // flight per step
+    // flight per step.  Direct: the loop runs while any lane of the wave walks
+    // (wave-uniform), the keys go through the wave's ring.
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t qh = 0, qt = 0;  // ring head / tail (wave-uniform)
+    auto drain = [&](bool all) {
+      while (qt - qh >= 64 || (all && qt != qh)) {
+        const uint32_t m = min(qt - qh, 64u);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        if (lane < m) stage_key(squeue[DIRECT ? wv : 0][(qh + lane) & 255]);
+        qh += m;
+        __builtin_amdgcn_wave_barrier();  // the slots are rewritten by the next appends
+      }
+    };
     for (;;) {
       bool go = false;
 #pragma unroll
       for (int q = 0; q < TPW; ++q) go |= wa[q] < CW && dd[q] < WIN_DEPTH;
-      if (!go) break;
+      if (DIRECT ? __ballot(go) == 0 : !go) break;
       // all TPW reads first, then branch-free updates (selects), so the reads
       // stay in flight together
       uint4 r[TPW];
@@ -343,12 +359,20 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         // direct: a row stages each key as its walk reaches the ancestor (a
         // row that turns out pending stages them all again in k4_chain_pend:
         // duplicates are harmless in the edge set)
-        if (DIRECT && act) stage_key(edge_key(r[q].z, myep[q], dd[q] + 1, ((r[q].w >> 16) & 3) == KIND_SERVER));
+        if (DIRECT) {
+          const uint64_t mk = __ballot(act);
+          if (act)
+            squeue[DIRECT ? wv : 0][(qt + __popcll(mk & ((1ull << lane) - 1))) & 255] =
+                edge_key(r[q].z, myep[q], dd[q] + 1, ((r[q].w >> 16) & 3) == KIND_SERVER);
+          qt += __popcll(mk);
+        }
         acc[q] = act ? nacc : acc[q];
         dd[q] += act ? 1u : 0u;
         wa[q] = act ? (r[q].w & 0xFFFF) : wa[q];
       }
+      if (DIRECT) drain(false);
     }
+    if (DIRECT) drain(true);
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
       if (st[q] != S_DONE || !hash_on) {
@@ -599,7 +623,7 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__r
       }
 #pragma unroll
       for (int j = 0; j < (int)KP_PER; ++j) {
-        f[j] = (uint32_t)(slot_of(k[j], tcap) / ESLICE) & (nf - 1);
+        f[j] = (uint32_t)(eslot(k[j], tcap) / ESLICE) & (nf - 1);
         rk[j] = k[j] ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
       }
       __syncthreads();
@@ -618,8 +642,10 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__r
         sbin[q] = (uint16_t)f[j];
       }
       __syncthreads();
-      // consecutive threads -> consecutive slots of one slice's bucket
-      for (uint32_t i = threadIdx.x; i < cnt; i += KP_T) {
+      // consecutive threads -> consecutive slots of one slice's bucket (the
+      // nonzero keys only: a zero word is never a key)
+      const uint32_t nz = off[nf - 1] + hist[nf - 1];
+      for (uint32_t i = threadIdx.x; i < nz; i += KP_T) {
         const uint32_t fb = sbin[i];
         const uint64_t p = (uint64_t)base[fb] + (i - off[fb]);
         if (p < bcap) {
@@ -660,7 +686,7 @@ __global__ void __launch_bounds__(KS_T) k_key_slice(const unsigned long long *__
 #pragma unroll
       for (int j = 0; j < (int)KS_PER; ++j) {
         if (!k[j]) continue;
-        uint32_t p = (uint32_t)(slot_of(k[j], tcap) & (ESLICE - 1));
+        uint32_t p = (uint32_t)(eslot(k[j], tcap) & (ESLICE - 1));
         uint32_t z = 0;
         for (; z < PROBE_MAX; ++z) {
           unsigned long long cur = tab[p];

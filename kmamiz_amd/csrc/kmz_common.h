@@ -63,6 +63,10 @@ KMZ_HD uint32_t tag_of(uint64_t k) { return (uint32_t)(mix64(k + 0x9e3779b97f4a7
 // one in LDS from the keys partitioned to it).  A cap that is not a multiple
 // of ESLICE probes the whole table.
 constexpr uint64_t ESLICE = 8192;
+// home slot of an edge key: Fibonacci hashing (one 64-bit multiply; the top
+// bits of the product depend on every key bit), range-reduced like slot_of.
+// For a power-of-two cap it is the product's top log2(cap) bits.
+KMZ_HD uint64_t eslot(uint64_t k, uint64_t cap) { return mulhi64(k * 0x9E3779B97F4A7C15ull, cap); }
 KMZ_HD uint64_t eset_next(uint64_t pos, uint64_t cap) {
   if (cap % ESLICE) return pos + 1 == cap ? 0 : pos + 1;
   return (pos & ~(ESLICE - 1)) | ((pos + 1) & (ESLICE - 1));

@@ -381,7 +381,7 @@ constexpr uint32_t K4_EP_DIRECT = 2048; // endpoints privatised in LDS (32 KiB)
 
 __device__ __forceinline__ void triple_global(uint64_t key, unsigned long long *__restrict__ trip, uint64_t tcap,
                                               unsigned int *__restrict__ counters) {
-  uint64_t pos = slot_of(key, tcap);
+  uint64_t pos = eslot(key, tcap);
   // bounded probing: at load <= 0.7 a run of 256 occupied slots does not occur;
   // if it does, the table is (being) overfilled and the host retries bigger
   for (uint64_t p = 0; p < 256; ++p) {

@@ -138,6 +138,7 @@ class Engine:
 
     # ---- input ---------------------------------------------------------------
     def load(self, batch: SpanBatch, shapes: ShapeTable):
+        self.gen += 1
         s = batch.c_struct()
         sh = shapes.c_struct()
         L.check(self.ctx, self._lib.kmz_load(self.ctx, C.byref(s), C.byref(sh), L.MEM_HOST))
@@ -182,6 +183,7 @@ class Engine:
 
     def json_load(self, shape_of_raw: np.ndarray, status_of_raw: np.ndarray, shapes: ShapeTable, index_base: int = 0,
                   n: Optional[int] = None):
+        self.gen += 1
         sm = np.ascontiguousarray(shape_of_raw, dtype=np.uint32)
         tm = np.ascontiguousarray(status_of_raw, dtype=np.uint32)
         sh = shapes.c_struct()
@@ -202,6 +204,7 @@ class Engine:
         return SpanBatch(index_base=self.index_base, **cols)
 
     def load_synthetic(self, config: int, seed: int, trace_begin: int, trace_end: int) -> int:
+        self.gen += 1
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_synth_load(self.ctx, config, seed, trace_begin, trace_end, C.byref(n)))
         d = L.SynthDesc()
@@ -215,6 +218,7 @@ class Engine:
                              rank: int) -> int:
         """The traces of [trace_begin, trace_end) with shard(traceId) == rank
         (kmz_synth_load_shard), with their global flatten indices."""
+        self.gen += 1
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_synth_load_shard(self.ctx, config, seed, trace_begin, trace_end, world, rank,
                                                          C.byref(n)))
@@ -237,7 +241,12 @@ class Engine:
         self.index_base = 0
 
     # ---- compute -------------------------------------------------------------
+    # every call that changes the device results bumps `gen`, so a result
+    # object can tell whether the engine still holds its run
+    gen = 0
+
     def run(self, flags: int):
+        self.gen += 1
         L.check(self.ctx, self._lib.kmz_run(self.ctx, flags))
 
     def sync(self):
@@ -330,14 +339,17 @@ class Engine:
                                                       L.MEM_DEVICE if device else L.MEM_HOST, 0))
 
     def import_partials(self, which: int, src_ptr: int, words: int, device: bool):
+        self.gen += 1
         L.check(self.ctx, self._lib.kmz_partials_copy(self.ctx, which, C.c_void_p(src_ptr), words,
                                                       L.MEM_DEVICE if device else L.MEM_HOST, 1))
 
     def finalize(self):
+        self.gen += 1
         L.check(self.ctx, self._lib.kmz_finalize(self.ctx))
 
     def merge_triples(self, src_ptr: int, n: int, device: bool):
         """Union other shards' edge keys (u64, 0 = padding) into this run's set."""
+        self.gen += 1
         L.check(self.ctx, self._lib.kmz_merge_triples(self.ctx, C.c_void_p(src_ptr), n,
                                                       L.MEM_DEVICE if device else L.MEM_HOST))
 

@@ -192,3 +192,24 @@ def test_risk_arrays_row_order_free():
     assert [r["uniqueServiceName"] for r in got] == [r["uniqueServiceName"] for r in risk]
     for g, e in zip(got, risk):
         assert g["risk"] == pytest.approx(e["risk"], rel=REL, abs=1e-15)
+
+
+@pytest.mark.gpu
+def test_service_tail_reuses_the_dependency_run(engine):
+    """service_tail() reads the edge set the dependency run left in HBM (no
+    second kmz_run); after another run on the engine it runs the dependency
+    pass again, with the same result."""
+    from kmamiz_amd import Traces, synth
+
+    batch, off = synth.host_batch(3, 0, 300)
+    traces = synth.to_traces(3, batch, off)
+    t = Traces(traces, engine=engine)
+    deps = t.toEndpointDependencies()
+    g = engine.gen
+    a = deps.service_tail()
+    assert engine.gen == g  # no run in between: reused
+    t.toRealTimeData().toCombinedRealtimeData().toJSON()  # a stats run on the same engine
+    assert engine.gen != g
+    b = deps.service_tail()
+    assert a.instability() == b.instability() and a.coupling() == b.coupling()
+    assert a.cohesion() == b.cohesion()
