@@ -66,7 +66,7 @@ constexpr uint32_t PROBE_MAX = 512;
 constexpr uint32_t IMAP = 256;  // LDS map: one inserting leader per distinct new chain
 // staged keys are binned by the edge set's slices: 2^lb1 coarse bins per tile
 // workgroup (k4_chain), each split into 2^lb2 slices by k_key_part
-constexpr uint32_t KB1_MAX = 6, KB2_MAX = 10;
+constexpr uint32_t KB1_MAX = 8, KB2_MAX = 8;
 // direct enumeration: a workgroup drops keys it staged recently (a direct-mapped
 // LDS cache of KCACHE keys).  Hot edge keys repeat ~10^5 times per run; without
 // the cache they overfill their slice's bucket.
@@ -601,62 +601,73 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__r
                                                    unsigned long long *__restrict__ trip, uint64_t tcap,
                                                    unsigned int *__restrict__ counters) {
   __shared__ unsigned long long sorted[KP_STEP];  // 32 KB
-  __shared__ uint16_t sbin[KP_STEP];
   __shared__ uint32_t hist[1u << KB2_MAX], off[1u << KB2_MAX], base[1u << KB2_MAX], wsum[KP_T / 64];
   static_assert((1u << KB2_MAX) <= 4 * KP_T, "kp_scan covers the slices of a coarse bin");
   const uint32_t nf = 1u << lb2;
   uint32_t flags = 0;
-  for (uint32_t r = blockIdx.x; r < nruns; r += gridDim.x) {
-    const uint32_t m = stage_n[r];
-    const uint32_t c = r & ((1u << lb1) - 1);  // the run's coarse bin
-    const unsigned long long *src = stage + (uint64_t)r * sub;
-    for (uint32_t c0 = 0; c0 < m; c0 += KP_STEP) {
-      const uint32_t cnt = min(m - c0, KP_STEP);
-      for (uint32_t x = threadIdx.x; x < nf; x += KP_T) hist[x] = 0;
-      __syncthreads();
-      uint64_t k[KP_PER];
-      uint32_t f[KP_PER], rk[KP_PER];
-#pragma unroll
-      for (int j = 0; j < (int)KP_PER; ++j) {  // all loads in flight together
-        const uint32_t i = j * KP_T + threadIdx.x;
-        k[j] = i < cnt ? src[c0 + i] : 0;  // (edge keys are nonzero)
-      }
-#pragma unroll
-      for (int j = 0; j < (int)KP_PER; ++j) {
-        f[j] = (uint32_t)(eslot(k[j], tcap) / ESLICE) & (nf - 1);
-        rk[j] = k[j] ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
-      }
-      __syncthreads();
-      for (uint32_t x = threadIdx.x; x < nf; x += KP_T) {
-        const uint32_t h = hist[x];
-        base[x] = h ? atomicAdd(&bucket_n[(c << lb2) + x], h) : 0;
-        off[x] = h;
-      }
-      __syncthreads();
-      kp_scan(off, nf, wsum);
-#pragma unroll
-      for (int j = 0; j < (int)KP_PER; ++j) {
-        if (!k[j]) continue;
-        const uint32_t q = off[f[j]] + rk[j];
-        sorted[q] = k[j];
-        sbin[q] = (uint16_t)f[j];
-      }
-      __syncthreads();
-      // consecutive threads -> consecutive slots of one slice's bucket (the
-      // nonzero keys only: a zero word is never a key)
-      const uint32_t nz = off[nf - 1] + hist[nf - 1];
-      for (uint32_t i = threadIdx.x; i < nz; i += KP_T) {
-        const uint32_t fb = sbin[i];
-        const uint64_t p = (uint64_t)base[fb] + (i - off[fb]);
-        if (p < bcap) {
-          bucket[(uint64_t)((c << lb2) + fb) * bcap + p] = sorted[i];
-        } else {
-          edge_insert(sorted[i], trip, tcap, &flags);
-          flags |= F_STAGE_FULL;
-        }
-      }
-      __syncthreads();
+  // this workgroup's steps: runs blockIdx.x, +gridDim.x, ..., 4096 keys at a
+  // time; the next step's keys are loaded while this one is sorted
+  uint32_t r = blockIdx.x, c0 = 0, m = 0;
+  auto seek = [&]() {
+    while (r < nruns && c0 >= (m = stage_n[r])) {
+      r += gridDim.x;
+      c0 = 0;
     }
+  };
+  uint64_t kn[KP_PER];
+  auto load = [&]() {
+    const unsigned long long *src = stage + (uint64_t)min(r, nruns - 1) * sub;
+#pragma unroll
+    for (int j = 0; j < (int)KP_PER; ++j) {
+      const uint32_t i = c0 + j * KP_T + threadIdx.x;
+      kn[j] = (r < nruns && i < m) ? src[i] : 0;  // (edge keys are nonzero)
+    }
+  };
+  seek();
+  load();
+  while (r < nruns) {
+    const uint32_t c = r & ((1u << lb1) - 1);  // this step's coarse bin
+    uint64_t k[KP_PER];
+#pragma unroll
+    for (int j = 0; j < (int)KP_PER; ++j) k[j] = kn[j];
+    c0 += KP_STEP;
+    seek();
+    load();  // (in flight during the LDS work below)
+    for (uint32_t x = threadIdx.x; x < nf; x += KP_T) hist[x] = 0;
+    __syncthreads();
+    uint32_t f[KP_PER], rk[KP_PER];
+#pragma unroll
+    for (int j = 0; j < (int)KP_PER; ++j) {
+      f[j] = (uint32_t)(eslot(k[j], tcap) / ESLICE) & (nf - 1);
+      rk[j] = k[j] ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < nf; x += KP_T) {
+      const uint32_t h = hist[x];
+      base[x] = h ? atomicAdd(&bucket_n[(c << lb2) + x], h) : 0;
+      off[x] = h;
+    }
+    __syncthreads();
+    kp_scan(off, nf, wsum);
+#pragma unroll
+    for (int j = 0; j < (int)KP_PER; ++j)
+      if (k[j]) sorted[off[f[j]] + rk[j]] = k[j];
+    __syncthreads();
+    // consecutive threads -> consecutive slots of one slice's bucket (the
+    // nonzero keys only: a zero word is never a key)
+    const uint32_t nz = off[nf - 1] + hist[nf - 1];
+    for (uint32_t i = threadIdx.x; i < nz; i += KP_T) {
+      const unsigned long long key = sorted[i];
+      const uint32_t fb = (uint32_t)(eslot(key, tcap) / ESLICE) & (nf - 1);
+      const uint64_t p = (uint64_t)base[fb] + (i - off[fb]);
+      if (p < bcap) {
+        bucket[(uint64_t)((c << lb2) + fb) * bcap + p] = key;
+      } else {
+        edge_insert(key, trip, tcap, &flags);
+        flags |= F_STAGE_FULL;
+      }
+    }
+    __syncthreads();
   }
   if (flags) atomicOr(&counters[C_FLAGS], flags);
 }
@@ -896,7 +907,8 @@ bool key_bins(uint64_t tcap, uint32_t *lb1, uint32_t *lb2) {
   // slices of the edge set: tcap / ESLICE (tcap a power of two >= ESLICE)
   uint32_t ls = 0;
   while ((ESLICE << ls) < tcap) ++ls;
-  *lb1 = std::min<uint32_t>(ls, KB1_MAX);
+  *lb1 = std::min<uint32_t>(ls, 6);  // 64 coarse bins, more when the slices outnumber 64 x 2^KB2_MAX
+  if (ls - *lb1 > KB2_MAX) *lb1 = std::min<uint32_t>(ls - KB2_MAX, KB1_MAX);
   *lb2 = ls - *lb1;
   return (ESLICE << ls) == tcap && *lb2 <= KB2_MAX;
 }
