@@ -178,7 +178,7 @@ def main():
         import numpy as np
 
         from kmamiz_amd.ingest import SHAPE_TAGS, UNDEFINED, tag_identity
-        from kmamiz_amd.tail import maps_for_synth, realtime_risk_columns, run_tail
+        from kmamiz_amd.tail import maps_for_synth, realtime_risk_from_sums, run_tail, service_sums_grid
 
         args.no_fetch = False
         tmaps = maps_for_synth(config)
@@ -198,9 +198,11 @@ def main():
         g, e = state["groups"], state["endpoints"]
         t = run_tail(eng, tmaps, e)  # reads the edge keys where the run left them, in HBM
         state["metrics"] = t.metrics()
-        used = np.nonzero(g["combined"] > 0)[0]
-        state["risk"] = realtime_risk_columns(t, tag_sid[used // n_status], sid_names, g["combined"][used],
-                                              g["cv"][used], is_5xx[used % n_status], first=g["first"][used])
+        # RiskAnalyzer.RealtimeRisk over the combined groups (per-service sums
+        # straight from the endpoint x status grid)
+        sums = service_sums_grid(g["combined"], g["cv"], g["first"], is_5xx, tag_sid[: len(g) // n_status],
+                                 len(sid_names))
+        state["risk"] = realtime_risk_from_sums(t, sid_names, *sums)
 
     def step():
         eng.run(flags)
@@ -326,9 +328,9 @@ def main():
                     first = np.where(ep["has_row"], ep["first"], np.iinfo(np.uint64).max).astype(np.uint64)
                     t = tail_np(keys, tmaps, ep["has_row"], first)
                     t.metrics()
-                    used = np.nonzero(st["combined"] > 0)[0]
-                    realtime_risk_columns(t, tag_sid[used // n_status], sid_names, st["combined"][used],
-                                          st["cv"][used], is_5xx[used % n_status], first=st["first"][used])
+                    realtime_risk_from_sums(t, sid_names, *service_sums_grid(
+                        st["combined"], st["cv"], st["first"], is_5xx, tag_sid[: len(st["combined"]) // n_status],
+                        len(sid_names)))
             cpu = cpu_baseline(config, args.cpu_seconds, cpu_tail)
         line = {
             "metric": "spans/sec -> endpoint dependency graph + combined stats (node); % HBM roofline",

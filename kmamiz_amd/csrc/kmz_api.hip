@@ -96,6 +96,7 @@ struct kmz_ctx {
   uint64_t k4_key = ~0ull;
   bool k4_auto_direct = false, k4_direct_ran = false;
   uint32_t k4_since = 0;
+  uint32_t k4_lb1 = 0, k4_nsl = 0, k4_ng = 0;  // the last K4 run's staging layout (kmz__debug_k4)
   uint64_t cap = 0, tcap = 1ull << 16, ccap = 1ull << 20;
   uint64_t sig_seed = SIG_SEED0;  // K4 ancestry-hash seed (changed after a collision)
   uint32_t dcap = 1024;
@@ -790,6 +791,10 @@ static int run_shape_stats(kmz_ctx *c) {
   return KMZ_OK;
 }
 
+// bytes of K4 key staging (and as many again of slice buckets): 4 GB, or
+// 40 B per span for larger batches (HBM is 288 GB)
+static uint64_t stage_limit(uint64_t n) { return std::max<uint64_t>(4ull << 30, 40ull * n); }
+
 static bool k4_direct(kmz_ctx *c) {
   if (c->ablate & (1u << 28)) return true;  // test knobs: force direct enumeration / chain interning
   if (c->ablate & (1u << 29)) return false;
@@ -842,11 +847,19 @@ static int run_deps(kmz_ctx *c, bool links) {
     // slower) and the slots each workgroup claims in the chain table (wcap
     // each; the run's global list of wcap more follows them); the staged keys
     // partitioned per slice (as many again)
+    // (a batch starts with staging for ~8 keys per span -- direct enumeration
+    // of config 5 stages ~4.5 -- within the staging limit)
+    while (!(c->ablate & (1u << 30)) && (uint64_t)c->scap * chain_grid(n) < 8ull * n &&
+           (uint64_t)chain_grid(n) * c->scap * 2 * 8 <= stage_limit(n))
+      c->scap *= 2;
     const uint32_t scap = c->scap, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
     uint32_t lb1, lb2;
     if (!key_bins(c->tcap, &lb1, &lb2)) return fail(c, KMZ_E_ARG, "edge-set capacity is not ESLICE * 2^k");
     const uint64_t nsl = c->tcap / ESLICE, bcap = ((uint64_t)ng * scap + nsl - 1) / nsl;
     void *old_ctab = c->ctab.p;
+    c->k4_lb1 = direct ? lb1 : 0;
+    c->k4_nsl = (uint32_t)nsl;
+    c->k4_ng = ng;
     if (ensure(c, c->ctab, c->ccap * CHAIN_ENTRY_BYTES) || ensure(c, c->ctile, (size_t)nt * 16) ||
         ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, (size_t)ng * scap * 8) ||
         ensure(c, c->kstage_n, ((size_t)ng << lb1) * 4) || ensure(c, c->kdefer, (size_t)ng * dcap * 16) ||
@@ -1133,8 +1146,12 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     // staged keys overflowed (low chain reuse, config 5): the overflow was
     // inserted in place, correct but serial per leader; stage more next time
     // (<= 8 GB of staging)
-    if ((h[C_FLAGS] & F_STAGE_FULL) && (uint64_t)chain_grid((uint32_t)c->n) * c->scap * 4 * 8 <= (8ull << 30))
-      c->scap *= 4;
+    if (h[C_FLAGS] & F_STAGE_FULL) {  // x4, or as far as the staging limit allows
+      const uint64_t ng = chain_grid((uint32_t)c->n);
+      uint64_t want = (uint64_t)c->scap * 4;
+      while (want > c->scap && ng * want * 8 > stage_limit(c->n)) want /= 2;
+      c->scap = (uint32_t)want;
+    }
     if ((flags & KMZ_RUN_DEPS) && (c->path & 1) && h[C_CERT]) {  // a repeated span id: the table path, same run
       c->table_hint = true;
       continue;
@@ -1924,18 +1941,12 @@ int kmz_synth_host(int config, uint64_t seed, uint64_t t0, uint64_t t1, uint64_t
 // capacity, slices, coarse bins
 extern "C" int kmz__debug_k4(kmz_ctx *c, unsigned long long *out) {
   if (!c || !out) return KMZ_E_ARG;
-  const uint32_t ng = chain_grid((uint32_t)c->n);
-  uint32_t lb1 = 0, lb2 = 0;
-  key_bins(c->tcap, &lb1, &lb2);
-  if (!c->k4_direct_ran) {
-    lb2 += lb1;
-    lb1 = 0;
-  }
-  const uint64_t nsl = c->tcap / ESLICE;
+  const uint32_t ng = c->k4_ng, lb1 = c->k4_lb1;
+  const uint64_t nsl = c->k4_nsl;
+  if (!ng) return KMZ_E_STATE;
   std::vector<uint32_t> sn((size_t)ng << lb1), bn(nsl);
-  if (c->kstage_n.p && hipMemcpy(sn.data(), c->kstage_n.p, sn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
-    return KMZ_E_HIP;
-  if (c->kbucket_n.p && hipMemcpy(bn.data(), c->kbucket_n.p, bn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(sn.data(), c->kstage_n.p, sn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(bn.data(), c->kbucket_n.p, bn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
     return KMZ_E_HIP;
   unsigned long long s1 = 0, m1 = 0, s2 = 0, m2 = 0;
   for (uint32_t v : sn) s1 += v, m1 = std::max<unsigned long long>(m1, v);

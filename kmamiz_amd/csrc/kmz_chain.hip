@@ -114,6 +114,9 @@ __device__ __forceinline__ uint64_t edge_key(uint32_t ea, uint32_t es, uint32_t 
 // is counted by the compaction
 __device__ __forceinline__ void edge_insert(uint64_t key, unsigned long long *__restrict__ trip, uint64_t tcap,
                                            uint32_t *flags) {
+  // an overfull set makes every insert probe PROBE_MAX slots: once this
+  // thread has seen it, the run is repeated with a larger set anyway
+  if (*flags & F_TRIPLE_OVERFLOW) return;
   uint64_t pos = eslot(key, tcap);
   for (uint32_t z = 0; z < PROBE_MAX; ++z) {
     uint64_t cur = trip[pos];
@@ -137,6 +140,7 @@ __device__ __forceinline__ void edge_insert(uint64_t key, unsigned long long *__
 __device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, uint64_t ccap, uint64_t sig,
                                          uint64_t psig, uint32_t *flags, uint32_t *__restrict__ gpos,
                                          uint32_t gcap, unsigned int *__restrict__ counters) {
+  if (*flags & F_CHAIN_OVERFLOW) return -1;  // (this thread found the table full: the run is repeated larger)
   uint64_t pos = cslot(sig, ccap);
   for (uint32_t z = 0; z < PROBE_MAX; ++z) {
     unsigned long long *e = ctab + 2 * pos;
@@ -696,7 +700,7 @@ __global__ void __launch_bounds__(KS_T) k_key_slice(const unsigned long long *__
       }
 #pragma unroll
       for (int j = 0; j < (int)KS_PER; ++j) {
-        if (!k[j]) continue;
+        if (!k[j] || (flags & F_TRIPLE_OVERFLOW)) continue;  // (a full slice: the run is repeated larger)
         uint32_t p = (uint32_t)(eslot(k[j], tcap) & (ESLICE - 1));
         uint32_t z = 0;
         for (; z < PROBE_MAX; ++z) {

@@ -336,6 +336,59 @@ def _linear(a: np.ndarray, minimum: float = 0.1) -> np.ndarray:
     return _fixed_ratio(a) * (1 - minimum) + minimum
 
 
+def service_sums(data_sid: np.ndarray, n_sid: int, combined: np.ndarray, cv: np.ndarray, is_5xx: np.ndarray,
+                 first: Optional[np.ndarray] = None):
+    """Per service of the combined rows (RiskAnalyzer.ts:18, 228-248): the
+    services in first-occurrence order (``first``: each row's first span
+    index; else row order) and, in that order, sum(cv * combined),
+    sum(combined) and sum(combined of 5xx rows)."""
+    sid = np.asarray(data_sid, dtype=np.int64)
+    if first is None:
+        uniq, pos = np.unique(sid, return_index=True)
+        order_ids = uniq[np.argsort(pos, kind="stable")]
+    else:
+        mn = np.full(n_sid, np.iinfo(np.uint64).max, dtype=np.uint64)
+        np.minimum.at(mn, sid, np.asarray(first, dtype=np.uint64))
+        uniq = np.nonzero(mn != np.iinfo(np.uint64).max)[0]
+        order_ids = uniq[np.argsort(mn[uniq], kind="stable")]
+    remap = np.full(n_sid, -1, dtype=np.int64)
+    remap[order_ids] = np.arange(len(order_ids))
+    r = remap[sid]
+    k = len(order_ids)
+    comb = np.asarray(combined, dtype=np.float64)
+    wsum = np.bincount(r, weights=np.asarray(cv, dtype=np.float64) * comb, minlength=k)
+    cnt = np.bincount(r, weights=comb, minlength=k)
+    err = np.bincount(r, weights=comb * np.asarray(is_5xx, dtype=bool), minlength=k)
+    return order_ids, wsum, cnt, err
+
+
+def service_sums_grid(combined: np.ndarray, cv: np.ndarray, first: np.ndarray, status_5xx: np.ndarray,
+                      ep_sid: np.ndarray, n_sid: int):
+    """``service_sums`` over the engine's group grid (endpoint-major, one column
+    per status; unused groups have combined == 0): summed per endpoint first,
+    then per service (the fp64 sums reassociate, within the 1e-9 of the
+    parity tests), without gathering the used rows."""
+    n_st = len(status_5xx)
+    comb = np.asarray(combined, dtype=np.float64).reshape(-1, n_st)
+    w_ep = (np.asarray(cv, dtype=np.float64).reshape(-1, n_st) * comb).sum(axis=1)
+    c_ep = comb.sum(axis=1)
+    e_ep = comb[:, np.asarray(status_5xx, dtype=bool)].sum(axis=1)
+    big = np.iinfo(np.uint64).max
+    f_ep = np.where(comb > 0, np.asarray(first, dtype=np.uint64).reshape(-1, n_st), big).min(axis=1)
+    has = c_ep > 0
+    sid = np.asarray(ep_sid, dtype=np.int64)[has]
+    mn = np.full(n_sid, big, dtype=np.uint64)
+    np.minimum.at(mn, sid, f_ep[has])
+    uniq = np.nonzero(mn != big)[0]
+    order_ids = uniq[np.argsort(mn[uniq], kind="stable")]
+    remap = np.full(n_sid, -1, dtype=np.int64)
+    remap[order_ids] = np.arange(len(order_ids))
+    r = remap[sid]
+    k = len(order_ids)
+    return (order_ids, np.bincount(r, weights=w_ep[has], minlength=k), np.bincount(r, weights=c_ep[has], minlength=k),
+            np.bincount(r, weights=e_ep[has], minlength=k))
+
+
 def realtime_risk_columns(tail: ServiceTail, data_sid: np.ndarray, sid_names: Sequence[str], combined: np.ndarray,
                           cv: np.ndarray, is_5xx: np.ndarray, replicas: Optional[List[dict]] = None,
                           first: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
@@ -348,27 +401,17 @@ def realtime_risk_columns(tail: ServiceTail, data_sid: np.ndarray, sid_names: Se
     dependencies), as numpy columns: ``sid`` (service ids in output order),
     ``risk``, ``impact``, ``probability``, ``norm`` (one element when every
     risk is equal, Normalizer.ts:22)."""
+    return realtime_risk_from_sums(tail, sid_names, *service_sums(data_sid, len(sid_names), combined, cv, is_5xx, first),
+                                   replicas=replicas)
+
+
+def realtime_risk_from_sums(tail: ServiceTail, sid_names: Sequence[str], order_ids: np.ndarray, wsum: np.ndarray,
+                            cnt: np.ndarray, err: np.ndarray, replicas: Optional[List[dict]] = None):
+    """The rest of ``realtime_risk_columns`` from ``service_sums``."""
     from .cache import to_precise
     from .risk import MINIMUM_PROB as MP
 
-    sid = np.asarray(data_sid, dtype=np.int64)
-    if first is None:
-        uniq, pos = np.unique(sid, return_index=True)
-        order_ids = uniq[np.argsort(pos, kind="stable")]
-    else:
-        mn = np.full(len(sid_names), np.iinfo(np.uint64).max, dtype=np.uint64)
-        np.minimum.at(mn, sid, np.asarray(first, dtype=np.uint64))
-        uniq = np.nonzero(mn != np.iinfo(np.uint64).max)[0]
-        order_ids = uniq[np.argsort(mn[uniq], kind="stable")]
-    remap = np.full(len(sid_names), -1, dtype=np.int64)
-    remap[order_ids] = np.arange(len(order_ids))
-    r = remap[sid]
     k = len(order_ids)
-    comb = np.asarray(combined, dtype=np.float64)
-    # latency CV per service weighted by request count (RiskAnalyzer.ts:228-248)
-    wsum = np.bincount(r, weights=np.asarray(cv, dtype=np.float64) * comb, minlength=k)
-    cnt = np.bincount(r, weights=comb, minlength=k)
-    err = np.bincount(r, weights=comb * np.asarray(is_5xx, dtype=bool), minlength=k)
     with np.errstate(divide="ignore", invalid="ignore"):
         rel = np.where(cnt != 0, wsum / np.where(cnt != 0, cnt, 1.0), math.nan)
         # SigmoidAdj (Normalizer.ts:32-41): the libm exp of risk.py, element by element

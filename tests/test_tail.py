@@ -213,3 +213,26 @@ def test_service_tail_reuses_the_dependency_run(engine):
     b = deps.service_tail()
     assert a.instability() == b.instability() and a.coupling() == b.coupling()
     assert a.cohesion() == b.cohesion()
+
+
+def test_service_sums_grid_equals_row_sums():
+    """service_sums_grid (the bench's per-endpoint pre-reduction over the group
+    grid) = service_sums over the used rows: same service order, sums within
+    1e-12 (reassociated), counts exact."""
+    from kmamiz_amd.tail import service_sums, service_sums_grid
+
+    rng = np.random.default_rng(7)
+    n_ep, n_st, n_sid = 3000, 3, 97
+    comb = rng.integers(0, 40, (n_ep, n_st)).astype(np.uint64)
+    comb[rng.random((n_ep, n_st)) < 0.3] = 0
+    cv = np.where(comb > 0, rng.random((n_ep, n_st)) * 2, 0.0)
+    first = rng.permutation(n_ep * n_st).astype(np.uint64).reshape(n_ep, n_st)
+    ep_sid = rng.integers(0, n_sid, n_ep)
+    st5 = np.array([False, False, True])
+    used = np.nonzero(comb.reshape(-1) > 0)[0]
+    a = service_sums(ep_sid[used // n_st], n_sid, comb.reshape(-1)[used], cv.reshape(-1)[used], st5[used % n_st],
+                     first.reshape(-1)[used])
+    b = service_sums_grid(comb.reshape(-1), cv.reshape(-1), first.reshape(-1), st5, ep_sid, n_sid)
+    assert np.array_equal(a[0], b[0])
+    assert np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
+    np.testing.assert_allclose(a[1], b[1], rtol=1e-12)

@@ -15,7 +15,8 @@ import numpy as np  # noqa: E402
 
 from kmamiz_amd import Engine, synth  # noqa: E402
 from kmamiz_amd import _lib as L  # noqa: E402
-from kmamiz_amd.tail import maps_for_synth, realtime_risk_arrays, realtime_risk_columns, run_tail  # noqa: E402
+from kmamiz_amd.tail import (maps_for_synth, realtime_risk_arrays, realtime_risk_columns, realtime_risk_from_sums,
+                             run_tail, service_sums_grid)  # noqa: E402
 
 
 def main():
@@ -48,7 +49,7 @@ def main():
         tag_sid[sh] = sid_of[usn]
     is_5xx_st = np.array([str(x).startswith("5") for x in synth.STATUSES[:n_status]], dtype=bool)
     flags = L.RUN_STATS_TAG | L.RUN_DEPS
-    marks = {k: [] for k in ("run", "fetch_all", "fetch_no_keys", "tail_device", "metrics", "risk", "risk_dicts")}
+    marks = {k: [] for k in ("run", "fetch_all", "fetch_no_keys", "tail_device", "metrics", "risk", "risk_dicts", "risk_grid")}
     dbg_fn = L.lib().kmz__debug_k4
     dbg_fn.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
     k4 = []  # scap, staged sum, max per run, bucket sum, max, bcap, slices, coarse bins, flags, path
@@ -83,6 +84,10 @@ def main():
         realtime_risk_arrays(tl, tag_sid[used // n_status], sid_names, g["combined"][used], g["cv"][used],
                              is_5xx_st[used % n_status], first=g["first"][used])
         marks["risk_dicts"].append(time.perf_counter() - t)
+        t = time.perf_counter()
+        realtime_risk_from_sums(tl, sid_names, *service_sums_grid(g["combined"], g["cv"], g["first"], is_5xx_st,
+                                                                   tag_sid[: len(g) // n_status], len(sid_names)))
+        marks["risk_grid"].append(time.perf_counter() - t)
     out = {k: round(statistics.median(v[1:]) * 1e3, 3) for k, v in marks.items()}
     out["spans"] = n
     out["edge_keys"] = int(nk)
