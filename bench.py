@@ -79,6 +79,11 @@ def traffic_of(kernel, config, n_local):
     return None
 
 
+def progress(msg):
+    """Progress on stderr (stdout carries only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -139,6 +144,10 @@ def cpu_baseline(config, target_seconds, tail=None):
 
 def main():
     args = parse()
+    if os.environ.get("KMZ_BENCH_TRACE"):  # diagnostic: Python stacks every 30 s
+        import faulthandler
+
+        faulthandler.dump_traceback_later(30, repeat=True)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -169,6 +178,7 @@ def main():
         n_local = eng.load_synthetic_shard(config, synth.SEED, 0, n_traces, world, rank)
     else:
         n_local = eng.load_synthetic(config, synth.SEED, 0, n_traces)
+    progress(f"loaded {n_local} spans")
     digest = synth.table_digest(config)  # every rank indexes partials by the same synthetic id tables
     flags = L.RUN_STATS_TAG | L.RUN_DEPS
     dev = torch.device("cuda", local)
@@ -178,7 +188,7 @@ def main():
         import numpy as np
 
         from kmamiz_amd.ingest import SHAPE_TAGS, UNDEFINED, tag_identity
-        from kmamiz_amd.tail import maps_for_synth, realtime_risk_from_sums, run_tail, service_sums_grid
+        from kmamiz_amd.tail import maps_for_synth, realtime_risk_columns, run_tail
 
         args.no_fetch = False
         tmaps = maps_for_synth(config)
@@ -198,11 +208,11 @@ def main():
         g, e = state["groups"], state["endpoints"]
         t = run_tail(eng, tmaps, e)  # reads the edge keys where the run left them, in HBM
         state["metrics"] = t.metrics()
-        # RiskAnalyzer.RealtimeRisk over the combined groups (per-service sums
-        # straight from the endpoint x status grid)
-        sums = service_sums_grid(g["combined"], g["cv"], g["first"], is_5xx, tag_sid[: len(g) // n_status],
-                                 len(sid_names))
-        state["risk"] = realtime_risk_from_sums(t, sid_names, *sums)
+        # RiskAnalyzer.RealtimeRisk over the used combined groups as columns
+        # (tools/diag_power.py: 1.8 ms against 3.2 ms from the whole grid)
+        used = np.nonzero(g["combined"] > 0)[0]
+        state["risk"] = realtime_risk_columns(t, tag_sid[used // n_status], sid_names, g["combined"][used],
+                                              g["cv"][used], is_5xx[used % n_status], first=g["first"][used])
 
     def step():
         eng.run(flags)
@@ -230,8 +240,9 @@ def main():
         if tail_on:
             service_tail()
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         step()
+        progress(f"warmup step {w + 1}/{args.warmup}")
     info = eng.info()
     eng.kernel_times(reset=True)
     eng.set_profiling(True)
@@ -328,9 +339,9 @@ def main():
                     first = np.where(ep["has_row"], ep["first"], np.iinfo(np.uint64).max).astype(np.uint64)
                     t = tail_np(keys, tmaps, ep["has_row"], first)
                     t.metrics()
-                    realtime_risk_from_sums(t, sid_names, *service_sums_grid(
-                        st["combined"], st["cv"], st["first"], is_5xx, tag_sid[: len(st["combined"]) // n_status],
-                        len(sid_names)))
+                    used = np.nonzero(st["combined"] > 0)[0]
+                    realtime_risk_columns(t, tag_sid[used // n_status], sid_names, st["combined"][used],
+                                          st["cv"][used], is_5xx[used % n_status], first=st["first"][used])
             cpu = cpu_baseline(config, args.cpu_seconds, cpu_tail)
         line = {
             "metric": "spans/sec -> endpoint dependency graph + combined stats (node); % HBM roofline",

@@ -472,9 +472,13 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         // a row whose chain this leader inserted (or lost to another chain: the
         // deferred check may insert it) stages its keys; one that joined the
         // same chain leaves them to the winner (knob 19: diagnostic, none)
+        // publish before anything below can wait: a lane that spins on another
+        // workgroup's unpublished entry (chain_put) must never hold back, in
+        // its own wave, the publish of an entry that workgroup may spin on
+        if (cv == 0) atomicExch(&en[1], (unsigned long long)ps[q]);
+        __builtin_amdgcn_wave_barrier();
         if (kq[q] == KIND_SERVER && d && cv != sg[q] && !(ablate & (1u << 19))) stage_row(jl, myep[q], d);
-        if (cv == 0) {  // won the slot: publish
-          atomicExch(&en[1], (unsigned long long)ps[q]);
+        if (cv == 0) {  // won the slot (published above)
           ++fresh_n;
           const uint32_t x = atomicAdd(&wcnt, 1u);
           if (x < wcap)
