@@ -49,12 +49,19 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "kmz_kernels.h"
 
 namespace kmz {
 
-constexpr uint32_t CT = 768, CH = 128, CW = CT + 2 * CH;
+#ifndef KMZ_CHAIN_CT
+#define KMZ_CHAIN_CT 768
+#endif
+#ifndef KMZ_CHAIN_CH
+#define KMZ_CHAIN_CH 128
+#endif
+constexpr uint32_t CT = KMZ_CHAIN_CT, CH = KMZ_CHAIN_CH, CW = CT + 2 * CH;
 constexpr int CTT = 256;
 constexpr int CPW = CW / CTT;  // window slots per thread (slot jl = q * CTT + thread)
 constexpr int TPW = CT / CTT;  // tile slots per thread
@@ -71,6 +78,9 @@ constexpr uint32_t KB1_MAX = 8, KB2_MAX = 8;
 // LDS cache of KCACHE keys).  Hot edge keys repeat ~10^5 times per run; without
 // the cache they overfill their slice's bucket.
 constexpr uint32_t KCACHE = 1024;
+#ifndef KMZ_GATHER_EARLY
+#define KMZ_GATHER_EARLY 1
+#endif
 #ifndef KMZ_CHAIN_WAVES
 #define KMZ_CHAIN_WAVES 4
 #endif
@@ -339,6 +349,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         __builtin_amdgcn_wave_barrier();  // the slots are rewritten by the next appends
       }
     };
+    // (two copies of the loop: the non-SERVER-ancestor branch is compiled out
+    // of the usual all-SERVER/CLIENT window)
+    auto walk = [&](auto other_tag) {
+    constexpr bool OTHER = decltype(other_tag)::value;
     for (;;) {
       bool go = false;
 #pragma unroll
@@ -353,7 +367,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       for (int q = 0; q < TPW; ++q) {
         const bool act = wa[q] < CW && dd[q] < WIN_DEPTH;
         const uint64_t nacc = sig_step(acc[q], (uint64_t)r[q].y << 32 | r[q].x);
-        if (any_other && act && kq[q] == KIND_SERVER && ((r[q].w >> 16) & 3) != KIND_SERVER) {
+        if (OTHER && act && kq[q] == KIND_SERVER && ((r[q].w >> 16) & 3) != KIND_SERVER) {
           // (rare) a non-SERVER ancestor of a row
           if (r[q].z < n_ep)
             atomicMax(&ep_ts[r[q].z], (unsigned long long)((uint64_t)ts[w0 + wa[q]] ^ TS_BIAS));
@@ -376,6 +390,11 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       }
       if (DIRECT) drain(false);
     }
+    };
+    if (any_other)
+      walk(std::true_type{});
+    else
+      walk(std::false_type{});
     if (DIRECT) drain(true);
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
@@ -402,6 +421,11 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     if (DIRECT) {  // (the rows staged their keys during the walk)
       if (more) gather_ep();
     } else {
+#if KMZ_GATHER_EARLY
+      // the next tile's endpoints: its shapes landed during the walk; the
+      // gather's round trip overlaps the probes' below (vmcnt is in order)
+      if (more) gather_ep();
+#endif
       ulonglong2 w01[TPW];  // (sig, parent sig) of the probed slot
       uint64_t pos[TPW];
 #pragma unroll
@@ -445,7 +469,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           h = (h + 1) & (IMAP - 1);
         }
       }
+#if !KMZ_GATHER_EARLY
       if (more) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
+#endif
       if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
 #pragma unroll
         for (int q = 0; q < TPW; ++q) hslot[q] = IMAP + 1;

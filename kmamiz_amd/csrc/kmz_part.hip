@@ -182,18 +182,41 @@ static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32
 // concatenation of the runs over its lanes (coalesced 16-byte reads, four per
 // lane in flight); a record finds its run by a binary search over the wave's
 // 64 run starts in LDS.
+//
+// PACK (a slice holds < 2^22 records: ceil(ntiles / S) * K3T < 2^22): four LDS
+// atomics per record instead of six --
+//   a_cs  += 2^42 + d       count in bits 42..63, sum of durations < 2^20 in
+//                           bits 0..41 (< 2^22 of them: no carry)
+//   a_s2  += d^2            (d < 2^20: d^2 < 2^40, the sum < 2^62)
+//   a_tsx  max, a_fst min   the first index as a u32 within the slice
+//                           (monotone in the global index)
+// a duration >= 2^20 us (rare) counts in a_cs, adds d to a_s1b and d^2 as
+// lo32 into a_s2 and hi32 into a_s2h.  Written out in the unpacked partial
+// format (s2 split into lo32 / hi32 limbs).
 constexpr int K3RT = 256;
 constexpr uint32_t K3RB = 64;  // runs per wave batch (one per lane)
+constexpr uint32_t K3_SMALL_D = 1u << 20;
+template <bool PACK>
 __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
                                                   uint32_t ntiles, uint32_t S, uint32_t G, uint64_t index_base,
                                                   unsigned long long *__restrict__ part) {
-  __shared__ unsigned long long a_cnt[K3R], a_s1[K3R], a_s2a[K3R], a_s2b[K3R], a_tsx[K3R], a_fst[K3R];
+  constexpr uint32_t A = PACK ? 1 : K3R;  // (the unpacked arrays)
+  constexpr uint32_t B = PACK ? K3R : 1;  // (the packed arrays)
+  __shared__ unsigned long long a_cnt[A], a_s1[A], a_s2a[A], a_s2b[A], a_tsx[K3R], a_fst[A];
+  __shared__ unsigned long long a_cs[B], a_s2[B], a_s1b[B], a_s2h[B];
+  __shared__ uint32_t a_fst32[B];
   constexpr uint32_t NW = K3RT / 64;
   __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB];  // per wave: run starts in the batch, pool offsets
   const uint32_t s = blockIdx.x, p = blockIdx.y;
   for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
-    a_cnt[k] = a_s1[k] = a_s2a[k] = a_s2b[k] = a_tsx[k] = 0;
-    a_fst[k] = ~0ull;
+    a_tsx[k] = 0;
+    if (PACK) {
+      a_cs[k] = a_s2[k] = a_s1b[k] = a_s2h[k] = 0;
+      a_fst32[k] = ~0u;
+    } else {
+      a_cnt[k] = a_s1[k] = a_s2a[k] = a_s2b[k] = 0;
+      a_fst[k] = ~0ull;
+    }
   }
   __syncthreads();
   const uint32_t *row = dir + (uint64_t)p * ntiles;
@@ -237,12 +260,28 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
         if (!v[u]) continue;
         const uint32_t kl = xr[u].w & (K3R - 1);
         const uint64_t d = xr[u].d, dd = d * d;
-        atomicAdd(&a_cnt[kl], 1ull);
-        atomicAdd(&a_s1[kl], (unsigned long long)d);
-        atomicAdd(&a_s2a[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
-        atomicAdd(&a_s2b[kl], (unsigned long long)(dd >> 32));
-        atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
-        atomicMin(&a_fst[kl], (unsigned long long)(index_base + (k0 + run[u] * step) * K3T + (xr[u].w >> 10)));
+        if (PACK) {
+          if (d < K3_SMALL_D) {
+            atomicAdd(&a_cs[kl], (1ull << 42) + d);
+            atomicAdd(&a_s2[kl], (unsigned long long)dd);
+          } else {  // (rare)
+            atomicAdd(&a_cs[kl], 1ull << 42);
+            atomicAdd(&a_s1b[kl], (unsigned long long)d);
+            atomicAdd(&a_s2[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
+            atomicAdd(&a_s2h[kl], (unsigned long long)(dd >> 32));
+          }
+          atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
+          // this slice's tiles are s, s + S, ...: (k - s) / S numbers them
+          const uint32_t m = (uint32_t)((k0 - s) / S) + run[u] * (uint32_t)(step / S);
+          atomicMin(&a_fst32[kl], m * K3T + (xr[u].w >> 10));
+        } else {
+          atomicAdd(&a_cnt[kl], 1ull);
+          atomicAdd(&a_s1[kl], (unsigned long long)d);
+          atomicAdd(&a_s2a[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
+          atomicAdd(&a_s2b[kl], (unsigned long long)(dd >> 32));
+          atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
+          atomicMin(&a_fst[kl], (unsigned long long)(index_base + (k0 + run[u] * step) * K3T + (xr[u].w >> 10)));
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();  // r_pre / r_off are rewritten by the next batch
@@ -252,12 +291,23 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
     uint64_t g = (uint64_t)p * K3R + k;
     if (g >= G) break;
     unsigned long long *b = part + (uint64_t)s * 6 * G + g;
-    b[0] = a_cnt[k];
-    b[G] = a_s1[k];
-    b[2ull * G] = a_s2a[k];
-    b[3ull * G] = a_s2b[k];
-    b[4ull * G] = a_tsx[k];
-    b[5ull * G] = a_fst[k];
+    if (PACK) {
+      const unsigned long long cs = a_cs[k], s2 = a_s2[k];
+      const uint32_t f = a_fst32[k];
+      b[0] = cs >> 42;
+      b[G] = (cs & ((1ull << 42) - 1)) + a_s1b[k];
+      b[2ull * G] = s2 & 0xFFFFFFFFull;
+      b[3ull * G] = (s2 >> 32) + a_s2h[k];
+      b[4ull * G] = a_tsx[k];
+      b[5ull * G] = f == ~0u ? ~0ull : index_base + ((uint64_t)s + (uint64_t)(f / K3T) * S) * K3T + f % K3T;
+    } else {
+      b[0] = a_cnt[k];
+      b[G] = a_s1[k];
+      b[2ull * G] = a_s2a[k];
+      b[3ull * G] = a_s2b[k];
+      b[4ull * G] = a_tsx[k];
+      b[5ull * G] = a_fst[k];
+    }
   }
 }
 
@@ -410,7 +460,17 @@ void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base
                       const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp) {
   if (!n || !G) return;
   const uint32_t P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
-  hipLaunchKernelGGL(k3_reduce, dim3(S, P), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, S, G, index_base, part);
+#ifndef KMZ_K3_PACK
+#define KMZ_K3_PACK 1
+#endif
+  // packed accumulators while a slice's records stay below 2^22 (counts and
+  // in-slice first indices fit their fields)
+  if (KMZ_K3_PACK && (uint64_t)((ntiles + S - 1) / S) * K3T < (1ull << 22))
+    hipLaunchKernelGGL(k3_reduce<true>, dim3(S, P), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, S, G, index_base,
+                       part);
+  else
+    hipLaunchKernelGGL(k3_reduce<false>, dim3(S, P), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, S, G,
+                       index_base, part);
   hipLaunchKernelGGL(k3_combine, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part, S, G,
                      grp);
 }

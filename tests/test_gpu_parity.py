@@ -256,6 +256,25 @@ def test_synthetic_vs_c_oracle(engine, config, ntr):
     assert info["n_dups"] == 0
 
 
+@pytest.mark.parametrize("ntr", [4000, 366000])
+def test_wide_durations_vs_c_oracle(engine, ntr):
+    """K3's packed accumulators (k3_reduce<PACK>) take durations < 2^20 us;
+    wider ones (up to 2^32 - 1) take the rare split path: both against the C
+    oracle on the mesh (partitioned K3), at 1e5 and 1e7 spans."""
+    from kmamiz_amd import synth
+    from kmamiz_amd.engine import SpanBatch
+
+    batch, _ = synth.host_batch(3, 0, ntr)
+    rng = np.random.default_rng(11)
+    d = batch.duration.astype(np.uint64)
+    wide = rng.random(len(d)) < 0.05
+    d[wide] = rng.integers(1 << 20, 1 << 32, int(wide.sum()), dtype=np.uint64)
+    d[rng.random(len(d)) < 0.001] = (1 << 32) - 1
+    b2 = SpanBatch(batch.span_id, batch.parent_id, batch.kind, batch.shape, batch.status,
+                   d.astype(batch.duration.dtype), batch.timestamp, batch.index_base)
+    _compare_synth(engine, b2, synth.shape_table(3))
+
+
 def test_synthetic_shard_base_vs_c_oracle(engine):
     from kmamiz_amd import synth
 
