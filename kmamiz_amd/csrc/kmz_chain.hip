@@ -353,11 +353,14 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     // of the usual all-SERVER/CLIENT window)
     auto walk = [&](auto other_tag) {
     constexpr bool OTHER = decltype(other_tag)::value;
-    for (;;) {
+    // every walk starts at step 0 and advances once per step while it is in
+    // the window, so a walk's depth is the step count: the depth bound is the
+    // (wave-uniform) loop bound, and the loop runs while any lane walks
+    for (uint32_t it = 0; it < WIN_DEPTH; ++it) {
       bool go = false;
 #pragma unroll
-      for (int q = 0; q < TPW; ++q) go |= wa[q] < CW && dd[q] < WIN_DEPTH;
-      if (DIRECT ? __ballot(go) == 0 : !go) break;
+      for (int q = 0; q < TPW; ++q) go |= wa[q] < CW;
+      if (__ballot(go) == 0) break;
       // all TPW reads first, then branch-free updates (selects), so the reads
       // stay in flight together
       uint4 r[TPW];
@@ -365,7 +368,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       for (int q = 0; q < TPW; ++q) r[q] = lrec[wa[q] < CW ? wa[q] : 0];
 #pragma unroll
       for (int q = 0; q < TPW; ++q) {
-        const bool act = wa[q] < CW && dd[q] < WIN_DEPTH;
+        const bool act = wa[q] < CW;
         const uint64_t nacc = sig_step(acc[q], (uint64_t)r[q].y << 32 | r[q].x);
         if (OTHER && act && kq[q] == KIND_SERVER && ((r[q].w >> 16) & 3) != KIND_SERVER) {
           // (rare) a non-SERVER ancestor of a row
@@ -385,7 +388,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           qt += __popcll(mk);
         }
         acc[q] = act ? nacc : acc[q];
-        dd[q] += act ? 1u : 0u;
+        dd[q] = act ? it + 1 : dd[q];
         wa[q] = act ? (r[q].w & 0xFFFF) : wa[q];
       }
       if (DIRECT) drain(false);

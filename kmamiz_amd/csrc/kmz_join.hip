@@ -93,7 +93,9 @@ static_assert(JB == 1024, "bucket indices are the top 10 bits of the 32-bit hash
 __device__ __forceinline__ uint32_t jfold(uint64_t id) { return (uint32_t)id ^ (uint32_t)(id >> 32); }
 __device__ __forceinline__ uint32_t jb1(uint32_t x) { return (x * 0x9E3779B1u) >> 22; }
 __device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >> 22; }
-__device__ __forceinline__ uint32_t jfp(uint32_t x) { return ((x * 0x9E3779B1u) >> 18) & 0xF; }
+// fingerprints are 1..15: an empty entry (0) never matches one, so a lookup
+// compares fingerprints only
+__device__ __forceinline__ uint32_t jfp(uint32_t x) { return max(((x * 0x9E3779B1u) >> 18) & 0xF, 1u); }
 
 // lanes of this wave whose `v` (6 bits) equals mine, among `valid` lanes
 __device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
@@ -210,14 +212,15 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
       const uint32_t f = jfp(h), pb1 = jb1(h), pb2 = jb2(h);
       const uint4 x = lbkt[pb1], y = lbkt[pb2];
       const uint32_t c[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-      // candidates: occupied entries with the fingerprint (two per word, SWAR)
+      // candidates: entries with the fingerprint (two per word, SWAR; empty
+      // entries have fingerprint 0, which no id has)
       const uint32_t pat = (f << 12) | (f << 28);
       uint32_t cand = 0;
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const uint32_t v = c[t], z = v ^ pat;
-        cand |= (((z & 0xF000u) == 0 && (v & 0xFFFFu) != 0) ? 1u : 0u) << (2 * t);
-        cand |= (((z & 0xF0000000u) == 0 && (v >> 16) != 0) ? 1u : 0u) << (2 * t + 1);
+        cand |= ((z & 0xF000u) == 0 ? 1u : 0u) << (2 * t);
+        cand |= ((z & 0xF0000000u) == 0 ? 1u : 0u) << (2 * t + 1);
       }
       while (cand) {  // usually one candidate: the parent
         const uint32_t t = __builtin_ctz(cand);
@@ -342,7 +345,9 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
 }
 
 // pass 2: for one bin, the runs of TPC tiles -> 2^B2 sub-bins (dynamic LDS:
-// PQ * 1024 u64 staging + 2 * 2^B2 u32).  (PQ = 16, i.e. runs twice as long
+// PQ * 1024 u64 staging + 2 * 2^B2 u32).  (Reserving four sub-bins per
+// 64-bit atomic, as 16-bit fields, measured 0.59 against 0.57 ms on config 3:
+// the per-sub-bin reservations are not what bounds this pass.)  (PQ = 16, i.e. runs twice as long
 // per sub-bin, measured slower: 0.59 against 0.55 ms on config 3.)
 template <int PQ>
 __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *__restrict__ pool1,

@@ -748,6 +748,25 @@ def test_certificate_at_scale_finds_one_repeated_id(engine):
         assert info["n_dups"] == 1
 
 
+def test_certificate_massively_repeated_id(engine):
+    """One span id repeated 70 000 times puts more than 2^16 ids into one
+    certificate sub-bin (far past its capacity): the certificate must fail
+    (never a silent window answer) and the run must equal the C oracle on the
+    table path."""
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(3, 0, 40000)
+    rng = np.random.default_rng(5)
+    # leaves (span ids no one points at), so that every parent stays resolvable
+    parents = set(int(p) for p in batch.parent_id if p)
+    cand = np.array([i for i in range(len(batch)) if int(batch.span_id[i]) not in parents])
+    sel = rng.choice(cand, 70000, replace=False)
+    batch.span_id[sel] = batch.span_id[sel[0]]
+    info = _compare_synth(engine, batch, synth.shape_table(3))
+    assert not (info["path"] & 1)
+    assert info["n_dups"] > 0
+
+
 # ---------------------------------------------------------------------------
 # traceId sharding: device shard generation + index map (SURVEY.md 8e)
 # ---------------------------------------------------------------------------

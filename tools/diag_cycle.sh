@@ -5,8 +5,10 @@ set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-x}
 mkdir -p gpurun_out/diag_$TAG
-KMZ_BENCH_TRACE=1 timeout -k 10 240 python -u bench.py --config power --steps 5 --warmup 3 --cpu-seconds 0 \
-  > gpurun_out/diag_$TAG/power.json 2> gpurun_out/diag_$TAG/power.err || exit 1
+if [ -n "$POWER" ]; then
+  KMZ_BENCH_TRACE=1 timeout -k 10 240 python -u bench.py --config power --steps 5 --warmup 3 --cpu-seconds 0 \
+    > gpurun_out/diag_$TAG/power.json 2> gpurun_out/diag_$TAG/power.err || exit 1
+fi
 KR="k4_chain|k_join_window|k3_produce|k3_reduce|k_cert_split|k_cert_check"
 run() {  # name, counters...
   local name=$1; shift
