@@ -154,9 +154,17 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # (KMZ_DIST_BACKEND=gloo and more ranks than GPUs: a rehearsal of the
+    # multi-rank path on a one-GPU box; the driver's runs use RCCL, one GPU per rank)
+    backend = os.environ.get("KMZ_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from kmamiz_amd import Engine
     from kmamiz_amd import _lib as L
