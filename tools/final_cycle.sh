@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-end measurement (run on the box via gpurun): every GPU test, the
+# rocprofv3 kernel trace of the default bench, the stamped PMC traffic of
+# this build, then the bench lines of configs 2/3/5 (+ 1e9 spans on one GPU)
+# with their CPU baselines.  Every GPU step has its own limit; stop at the
+# first failure.  usage: tools/final_cycle.sh TAG
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${1:-final}
+O=gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $O/tests.log 2>&1
+rc=$?; echo "tests exit $rc" >> $O/tests.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o mesh -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 > $O/prof.log 2>&1 || exit 1
+bash tools/traffic.sh $TAG > $O/traffic.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py > $O/bench_mesh.json 2> $O/bench_mesh.err || exit 1
+timeout -k 10 300 python -u bench.py --config bookinfo --steps 20 --warmup 5 > $O/bench_book.json 2> $O/bench_book.err || exit 1
+timeout -k 10 300 python -u bench.py --config power --steps 10 --warmup 3 > $O/bench_power.json 2> $O/bench_power.err || exit 1
+timeout -k 10 300 python -u bench.py --spans 1e9 --steps 5 --warmup 2 --cpu-seconds 0 > $O/bench_mesh1B.json 2> $O/bench_mesh1B.err || exit 1
+echo FINAL_DONE
