@@ -15,8 +15,8 @@
 // chain emits its keys; nothing per relation is written to HBM.
 //
 // `sig` is a 64-bit hash of the whole ancestry (a rotate-xor fold of the
-// ancestors' element hashes, finished by the mix64 bijection), computed by
-// walking the ancestors in LDS, so every span probes the table once, in one
+// ancestors' mix64 element hashes, finished by an xor with a depth constant),
+// computed by walking the ancestors in LDS, so every span probes the table once, in one
 // round, with no dependency on its parent's probe or insert.  Exactness does
 // not rest on the hash: every span checks the entry it found or joined against
 // its own parent sig.  The table holds one entry per sig, so by induction from
@@ -78,6 +78,9 @@ constexpr uint32_t KB1_MAX = 8, KB2_MAX = 8;
 // LDS cache of KCACHE keys).  Hot edge keys repeat ~10^5 times per run; without
 // the cache they overfill their slice's bucket.
 constexpr uint32_t KCACHE = 1024;
+#ifndef KMZ_SIG_MIX
+#define KMZ_SIG_MIX 0
+#endif
 #ifndef KMZ_GATHER_EARLY
 #define KMZ_GATHER_EARLY 1
 #endif
@@ -106,15 +109,26 @@ __device__ __forceinline__ uint64_t rotl64(uint64_t x, uint32_t r) {
 __device__ __forceinline__ uint64_t sig_step(uint64_t acc, uint64_t el) {
   return ((acc << SIG_R) | (acc >> (64 - SIG_R))) ^ el;
 }
+// The finish is an xor with a depth and seed constant: a bijection for each
+// depth, which is all the exactness argument needs.  The fold is already an
+// xor of rotated mix64 outputs (uniform bits), so no further mixing is needed
+// for the table's placement; a final mix64 (two 64-bit multiplies per sig,
+// two sigs per span) cost 4 % of k4_chain (mesh 1.33 against 1.28 ms).
 // 0 marks an unwritten word and ROOT_SIG a root's parent: a sig equal to
 // either is treated as a collision (another seed)
 __device__ __forceinline__ uint64_t sig_final(uint64_t acc, uint32_t d, uint64_t seed, uint32_t *flags) {
+#if KMZ_SIG_MIX
   const uint64_t z = mix64(acc ^ ((uint64_t)d * 0x632BE59BD9B4E019ull) ^ (seed << 1));
+#else
+  const uint64_t z = acc ^ ((uint64_t)d * 0x632BE59BD9B4E019ull) ^ (seed << 1);
+#endif
   if (z == 0 || z == ROOT_SIG) *flags |= F_SIG;
   return z;
 }
-// the sig is already a mix64 output: its high bits place it
-__device__ __forceinline__ uint64_t cslot(uint64_t sig, uint64_t ccap) { return mulhi64(sig, ccap); }
+// home slot: the sig's high bits (ccap is a power of two: mulhi64(sig, ccap))
+__device__ __forceinline__ uint64_t cslot(uint64_t sig, uint64_t ccap) {
+  return sig >> (64 - __builtin_ctzll(ccap));
+}
 
 __device__ __forceinline__ uint64_t edge_key(uint32_t ea, uint32_t es, uint32_t d, bool on) {
   return ((uint64_t)ea << 40) | ((uint64_t)es << 16) | ((uint64_t)d << 1) | (on ? 1ull : 0ull);
