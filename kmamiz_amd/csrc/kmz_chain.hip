@@ -65,6 +65,15 @@ constexpr uint32_t CT = KMZ_CHAIN_CT, CH = KMZ_CHAIN_CH, CW = CT + 2 * CH;
 constexpr int CTT = 256;
 constexpr int CPW = CW / CTT;  // window slots per thread (slot jl = q * CTT + thread)
 constexpr int TPW = CT / CTT;  // tile slots per thread
+// walker slots per thread and round: the tile's non-CLIENT spans (the only
+// ones that walk, probe and count) are compacted into a list first, so a
+// thread works on TW of them per round instead of TPW slots of which about
+// half are CLIENT spans
+#ifndef KMZ_CHAIN_TW
+#define KMZ_CHAIN_TW 2
+#endif
+constexpr int TW = KMZ_CHAIN_TW;
+static_assert(TW <= TPW, "walker slots per thread");
 static_assert(CT % CTT == 0, "tile slots must split evenly over the threads");
 static_assert(CW % CTT == 0, "window slots must split evenly over the threads");
 constexpr uint16_t W_NONE = 0xFFFF, W_CYC = 0xFFFE, W_OUT = 0xFFFD;
@@ -213,6 +222,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   // lanes append; 64 at a time are staged by all lanes together)
   __shared__ unsigned long long squeue[DIRECT ? CTT / 64 : 1][DIRECT ? 256 : 1];
   __shared__ uint32_t dcnt;
+  __shared__ uint16_t wlist[CT];  // this tile's non-CLIENT spans (tile-local), compacted
+  __shared__ uint32_t wcount;
   __shared__ uint32_t wcnt;        // chain-table slots this workgroup claimed (cleared after the run)
   __shared__ uint32_t red[CTT / 64][4];
   // diagnostic phase clock (KMZ_ABLATE bit 22 only): s_memtime deltas by thread 0
@@ -243,7 +254,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
 #pragma unroll
     for (int q = 0; q < CPW; ++q) e[q] = etab[sh[q] < n_shapes ? sh[q] : 0];
   };
-  if (threadIdx.x == 0) dcnt = wcnt = 0;
+  if (threadIdx.x == 0) dcnt = wcnt = wcount = 0;
   if (threadIdx.x < (1u << KB1_MAX)) lbin[threadIdx.x] = 0;
   if (DIRECT)
     for (uint32_t x = threadIdx.x; x < KCACHE; x += CTT) kcache[x] = 0;
@@ -297,6 +308,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     KMZ_STAMP(0);
     const uint32_t t0 = tile * CT, t1 = min(n, t0 + CT);
     const uint32_t w0 = t0 > CH ? t0 - CH : 0, w1 = min(n, t1 + CH), wn = w1 - w0;
+    if (threadIdx.x == 0) wcount = 0;  // (read by every thread before the last barrier of the previous tile)
     // window -> LDS, with every non-CLIENT slot's element hash
     bool other = false;  // a span neither SERVER nor CLIENT in the window (rows' lastUsage path)
 #pragma unroll
@@ -318,6 +330,29 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     KMZ_STAMP(1);
     const bool more = tile + gridDim.x < nt;
     if (more) fetch(tile + gridDim.x);  // lands while this tile computes
+    const uint32_t toff = t0 - w0;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // compact the tile's non-CLIENT spans into wlist (one LDS add per wave and
+    // slot); CLIENT spans are not rows
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+      const uint32_t jl = toff + q * CTT + threadIdx.x;
+      const bool in = w0 + jl < t1;
+      const bool isw = in && ((lrec[min(jl, CW - 1)].w >> 16) & 3) != KIND_CLIENT;
+      if (rowpos_out && in && !isw) rowpos_out[w0 + jl] = NONE64;
+      const uint64_t mk = __ballot(isw);
+      uint32_t b = 0;
+      if (lane == 0 && mk) b = atomicAdd(&wcount, (uint32_t)__popcll(mk));
+      b = __shfl(b, 0, 64);
+      if (isw) wlist[b + __popcll(mk & ((1ull << lane) - 1))] = (uint16_t)(jl - toff);
+    }
+    __syncthreads();
+    const uint32_t m = wcount;
+    // rounds of TW walkers per thread (uniform); the first always runs and
+    // issues the next tile's endpoint gather at one fixed point (so the
+    // gathered registers are dead before it)
+    auto round = [&](const uint32_t r0, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
     // hash the ancestry of every non-CLIENT span of the tile by a fold walk
     // over the LDS element hashes of its ancestors a1..aD:
     //   pacc = rotl^(D-1)(elem(a1)) ^ ... ^ elem(aD)
@@ -325,15 +360,17 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     // (the parent's own sig, so halo spans need no walk), and issue the probes
     // at once.  A row's walk also gives its non-SERVER ancestors (not rows)
     // their lastUsage.
-    const uint32_t toff = t0 - w0;
-    uint64_t sg[TPW], ps[TPW], acc[TPW];
-    uint32_t dd[TPW], wa[TPW], myep[TPW];
-    uint8_t st[TPW], kq[TPW];
+    uint64_t sg[TW], ps[TW], acc[TW];
+    uint32_t dd[TW], wa[TW], myep[TW], jq[TW];
+    uint8_t st[TW], kq[TW];
     const bool hash_on = !(ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
 #pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-      const uint32_t jl = toff + q * CTT + threadIdx.x;
-      const uint4 r = lrec[min(jl, CW - 1)];
+    for (int q = 0; q < TW; ++q) {
+      const uint32_t idx = r0 + q * CTT + threadIdx.x;
+      const bool on = idx < m;
+      const uint32_t jl = on ? toff + wlist[idx] : CW - 1;
+      jq[q] = jl;
+      const uint4 r = lrec[jl];
       kq[q] = (r.w >> 16) & 3;
       myep[q] = r.z;
       sg[q] = (uint64_t)r.y << 32 | r.x;  // the element hash until the walk is done
@@ -341,17 +378,19 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       dd[q] = 0;
       wa[q] = W_NONE;
       st[q] = S_NONE;
-      if (w0 + jl >= t1 || kq[q] == KIND_CLIENT) continue;
+      if (!on) {  // (no walker in this slot)
+        kq[q] = KIND_CLIENT;
+        continue;
+      }
       st[q] = S_DONE;
       if (!hash_on) continue;
       if (kq[q] == KIND_SERVER && r.z >= n_ep) flags |= F_RANGE;
       if (DIRECT && kq[q] != KIND_SERVER) continue;  // direct: only rows walk (no chains to intern)
       wa[q] = r.w & 0xFFFF;
     }
-    // the TPW walks of a thread step together: TPW independent LDS reads in
+    // the TW walks of a thread step together: TW independent LDS reads in
     // flight per step.  Direct: the loop runs while any lane of the wave walks
     // (wave-uniform), the keys go through the wave's ring.
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t qh = 0, qt = 0;  // ring head / tail (wave-uniform)
     auto drain = [&](bool all) {
       while (qt - qh >= 64 || (all && qt != qh)) {
@@ -373,15 +412,15 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     for (uint32_t it = 0; it < WIN_DEPTH; ++it) {
       bool go = false;
 #pragma unroll
-      for (int q = 0; q < TPW; ++q) go |= wa[q] < CW;
+      for (int q = 0; q < TW; ++q) go |= wa[q] < CW;
       if (__ballot(go) == 0) break;
-      // all TPW reads first, then branch-free updates (selects), so the reads
+      // all TW reads first, then branch-free updates (selects), so the reads
       // stay in flight together
-      uint4 r[TPW];
+      uint4 r[TW];
 #pragma unroll
-      for (int q = 0; q < TPW; ++q) r[q] = lrec[wa[q] < CW ? wa[q] : 0];
+      for (int q = 0; q < TW; ++q) r[q] = lrec[wa[q] < CW ? wa[q] : 0];
 #pragma unroll
-      for (int q = 0; q < TPW; ++q) {
+      for (int q = 0; q < TW; ++q) {
         const bool act = wa[q] < CW;
         const uint64_t nacc = sig_step(acc[q], (uint64_t)r[q].y << 32 | r[q].x);
         if (OTHER && act && kq[q] == KIND_SERVER && ((r[q].w >> 16) & 3) != KIND_SERVER) {
@@ -414,7 +453,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       walk(std::false_type{});
     if (DIRECT) drain(true);
 #pragma unroll
-    for (int q = 0; q < TPW; ++q) {
+    for (int q = 0; q < TW; ++q) {
       if (st[q] != S_DONE || !hash_on) {
         sg[q] = 0;
         continue;
@@ -436,17 +475,17 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       if (!(ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
     if (DIRECT) {  // (the rows staged their keys during the walk)
-      if (more) gather_ep();
+      if (more && FIRST) gather_ep();
     } else {
 #if KMZ_GATHER_EARLY
       // the next tile's endpoints: its shapes landed during the walk; the
       // gather's round trip overlaps the probes' below (vmcnt is in order)
-      if (more) gather_ep();
+      if (more && FIRST) gather_ep();
 #endif
-      ulonglong2 w01[TPW];  // (sig, parent sig) of the probed slot
-      uint64_t pos[TPW];
+      ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
+      uint64_t pos[TW];
 #pragma unroll
-      for (int q = 0; q < TPW; ++q) {
+      for (int q = 0; q < TW; ++q) {
         const bool pr = st[q] == S_PUT;
         pos[q] = pr ? cslot(sg[q], ccap) : 0;
         const unsigned long long *en = ctab + 2 * pos[q];
@@ -456,9 +495,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       // check what the probes found against (parent sig, endpoint, kind); a
       // chain not found (or not yet published) elects one leader per distinct
       // sig in this workgroup
-      uint32_t hslot[TPW];
+      uint32_t hslot[TW];
 #pragma unroll
-      for (int q = 0; q < TPW; ++q) {
+      for (int q = 0; q < TW; ++q) {
         hslot[q] = IMAP + 1;  // not an insert
         if (st[q] != S_PUT) continue;
         for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
@@ -487,11 +526,11 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         }
       }
 #if !KMZ_GATHER_EARLY
-      if (more) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
+      if (more && FIRST) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
 #endif
       if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
 #pragma unroll
-        for (int q = 0; q < TPW; ++q) hslot[q] = IMAP + 1;
+        for (int q = 0; q < TW; ++q) hslot[q] = IMAP + 1;
       __syncthreads();
       KMZ_STAMP(3);
       // followers compare with their leader; leaders claim the slot the probe
@@ -500,7 +539,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       // or not it is new (duplicates are harmless in the edge set), so nothing
       // here waits on another workgroup.
 #pragma unroll
-      for (int q = 0; q < TPW; ++q) {
+      for (int q = 0; q < TW; ++q) {
         if (hslot[q] > IMAP) {
           if (hslot[q] != IMAP + 1) {  // follower
             const uint32_t h = hslot[q] & (IMAP - 1);
@@ -508,7 +547,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           }
           continue;
         }
-        const uint32_t jl = toff + q * CTT + threadIdx.x;
+        const uint32_t jl = jq[q];
         unsigned long long *en = ctab + 2 * pos[q];
         const unsigned long long cv = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
         const uint32_t d = dd[q];
@@ -545,9 +584,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     KMZ_STAMP(4);
     // per span of the tile: row counts, pending list, rowpos
 #pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-      const uint32_t jl = toff + q * CTT + threadIdx.x, i = w0 + jl;
-      if (i >= t1) continue;
+    for (int q = 0; q < TW; ++q) {
+      const uint32_t jl = jq[q], i = w0 + jl;
+      if (kq[q] == KIND_CLIENT) continue;  // (an empty walker slot)
       const uint8_t kj = kq[q];
       uint64_t rp = NONE64;
       if (kj != KIND_CLIENT) {
@@ -567,8 +606,11 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       }
       if (rowpos_out) rowpos_out[i] = rp;
     }
-    __syncthreads();  // LDS is rewritten by the next tile
+    __syncthreads();  // LDS is rewritten by the next round / tile
     KMZ_STAMP(5);
+    };
+    round(0u, std::true_type{});
+    for (uint32_t r0 = TW * CTT; r0 < m; r0 += TW * CTT) round(r0, std::false_type{});
   }
   // per workgroup: rows, relations, max depth, new chains
   if (flags) atomicOr(&counters[C_FLAGS], flags);
