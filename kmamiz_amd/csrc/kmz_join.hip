@@ -358,6 +358,8 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   constexpr uint32_t CERT_CHUNK = PQ * 1024, CERT_TPC = PQ * 24;  // ~32 ids per tile run at 64 bins
   extern __shared__ uint64_t dyn[];
   __shared__ uint32_t wsum[16], tcnt[CERT_TPC], toff[CERT_TPC];
+  __shared__ uint8_t tof[CERT_CHUNK];  // record -> its tile in the chunk (CERT_TPC <= 256)
+  static_assert(CERT_TPC <= 256, "tile numbers are bytes");
   uint64_t *stg = dyn;
   const uint32_t M = 1u << B2;
   uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn + CERT_CHUNK), *base = cnt + M;
@@ -366,8 +368,9 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   if (T0 >= ntiles) return;
   const uint32_t nt = min(CERT_TPC, ntiles - T0);
   for (uint32_t k = threadIdx.x; k < M; k += blockDim.x) cnt[k] = 0;
+  uint32_t c = 0;
   if (threadIdx.x < CERT_TPC) {
-    uint32_t c = 0, o = 0;
+    uint32_t o = 0;
     if (threadIdx.x < nt) {
       const uint32_t t = T0 + threadIdx.x;
       const uint32_t tsize = min(JT, n - t * JT);
@@ -386,9 +389,13 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
     if (threadIdx.x == 0) atomicOr(&counters[C_CERT], CERT_OVF);
     return;
   }
-  // gather the chunk's records straight into registers: record e belongs to
-  // the last tile whose run starts at or before e (binary search in LDS);
-  // every load is in flight before any is used
+  // record -> tile map: each tile's thread writes its run (one LDS lookup per
+  // record below instead of a binary search of dependent LDS reads)
+  if (threadIdx.x < nt)
+    for (uint32_t j = 0, p = tcnt[threadIdx.x]; j < c; ++j) tof[p + j] = (uint8_t)threadIdx.x;
+  __syncthreads();
+  // gather the chunk's records straight into registers: every load is in
+  // flight before any is used
   uint64_t h[PQ];
   uint32_t rk[PQ];
 #pragma unroll
@@ -396,12 +403,7 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
     const uint32_t e = q * 1024 + threadIdx.x;
     h[q] = 0;
     if (e < cn) {
-      uint32_t lo = 0, hi = nt;  // tcnt[lo] <= e < tcnt[hi] (tcnt[nt] = cn)
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (tcnt[mid] <= e) lo = mid;
-        else hi = mid;
-      }
+      const uint32_t lo = tof[e];
       h[q] = pool1[(uint64_t)(T0 + lo) * JT + toff[lo] + (e - tcnt[lo])];
     }
   }
