@@ -74,8 +74,9 @@ def traffic_of(kernel, config, n_local):
             continue
         if t.get("build") != bid or t.get("config") != config or abs(t.get("n_spans", 0) - n_local) > 0.02 * n_local:
             continue
-        k = t.get("kernels", {}).get(kernel)
-        return (k["traffic_bytes"], os.path.basename(f)) if k else None
+        # (template instances, e.g. k4_chain<false>, count as their kernel)
+        ks = [v for name, v in t.get("kernels", {}).items() if name.split("<")[0] == kernel]
+        return (sum(v["traffic_bytes"] for v in ks), os.path.basename(f)) if ks else None
     return None
 
 
