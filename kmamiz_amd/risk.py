@@ -93,12 +93,61 @@ def relying_factor(service_deps: List[dict]) -> List[dict]:
     return [{"uniqueServiceName": k, "factor": v} for k, v in fm.items()]
 
 
+# String.prototype.localeCompare as the reference's Node runs it (ICU root
+# order, en-US; pinned by tests/golden/locale_order.json, generated with that
+# Node by tests/golden/gen_locale_order.js): three levels --
+#   primary   whitespace < punctuation (in the order below) < digits < letters
+#             (case-folded; accented letters by their base letter); C0 controls
+#             other than whitespace are ignorable
+#   secondary the combining marks of each letter (NFD), in ICU's mark order
+#   tertiary  lowercase < uppercase
+# Letters without a canonical decomposition outside ASCII (ae ligature,
+# o-stroke, sharp s, ...) sort after all ASCII letters here: parity unpinned.
+_PUNCT = "\t\n\x0b\x0c\r _-,;:!?.'\"()[]{}@*/\\&#%`^+<=>|~$"
+_PUNCT_RANK = {c: i for i, c in enumerate(_PUNCT)}
+_IGNORABLE = {chr(i) for i in list(range(0, 9)) + list(range(14, 32))}
+# combining marks U+0300..U+036F in ICU's secondary order (equal ranks tie)
+_MARK_ORDER = [
+    (0x34f,), (0x332,), (0x313, 0x343), (0x314,), (0x301, 0x341), (0x300, 0x340), (0x306,), (0x302,), (0x30c,),
+    (0x30a,), (0x342,), (0x308,), (0x344,), (0x30b,), (0x303,), (0x307,), (0x338,), (0x327,), (0x328,),
+    (0x304,), (0x30d, 0x30e, 0x312, 0x315, 0x31a, 0x33d, 0x33e, 0x33f, 0x346, 0x34a, 0x34b, 0x34c, 0x350, 0x351,
+     0x352, 0x357, 0x35b, 0x35d, 0x35e),
+    (0x316, 0x317, 0x318, 0x319, 0x31c, 0x31d, 0x31e, 0x31f, 0x320, 0x329, 0x32a, 0x32b, 0x32c, 0x32f, 0x333,
+     0x33a, 0x33b, 0x33c, 0x347, 0x348, 0x349, 0x34d, 0x34e, 0x353, 0x354, 0x355, 0x356, 0x359, 0x35a, 0x35c,
+     0x35f, 0x362),
+    (0x336, 0x337), (0x335,), (0x305,), (0x309,), (0x30f,), (0x310,), (0x311,), (0x31b,), (0x321,), (0x322,),
+    (0x323,), (0x324,), (0x325,), (0x326,), (0x32d,), (0x32e,), (0x330,), (0x331,), (0x334,), (0x339,), (0x345,),
+    (0x358,), (0x360,), (0x361,), (0x363,), (0x368,), (0x369,), (0x364,), (0x36a,), (0x365,), (0x36b,), (0x366,),
+    (0x36c,), (0x36d,), (0x367,), (0x36e,), (0x36f,)]
+_MARK_RANK = {m: r for r, ms in enumerate(_MARK_ORDER) for m in ms}
+
+
 def _collation_key(s: str):
-    # localeCompare on the ASCII service names KMamiz produces: punctuation <
-    # digits < letters, case-insensitive first (ICU root order); the synthetic
-    # names are zero padded so this equals code-unit order there.
-    prim = [(0, ord(c)) if not c.isalnum() else ((1, c) if c.isdigit() else (2, c.lower())) for c in s]
-    return prim, [c.isupper() for c in s]
+    import unicodedata
+
+    prim, sec, ter = [], [], []
+    for ch in unicodedata.normalize("NFD", s):
+        o = ord(ch)
+        if o in _MARK_RANK:
+            if sec:
+                sec[-1] = sec[-1] + (_MARK_RANK[o],)
+            continue
+        if ch in _IGNORABLE:
+            continue
+        if ch in _PUNCT_RANK:
+            prim.append((1, _PUNCT_RANK[ch]))
+            ter.append(0)
+        elif "0" <= ch <= "9":
+            prim.append((2, o))
+            ter.append(0)
+        elif ch.isascii() and ch.isalpha():
+            prim.append((3, ord(ch.lower())))
+            ter.append(1 if ch.isupper() else 0)
+        else:
+            prim.append((4, o))
+            ter.append(0)
+        sec.append(())
+    return prim, sec, ter
 
 
 def impact(service_deps: List[dict], replicas: List[dict]) -> List[dict]:

@@ -34,10 +34,12 @@ JS semantics reproduced:
 Parity pinning: every known answer in the reference's jest suite for this
 path is checked in ``tests/test_oracle_goldens.py``.
 
-Known approximation: ``String.prototype.localeCompare`` (used by
-``RiskAnalyzer.Impact``, ``RiskAnalyzer.ts:57-60``) is restated as an ICU-root
-style key that is exact for the lowercase/digit/punctuation names used by the
-fixtures and the synthetic generator (zero padded, so both orders agree).
+``String.prototype.localeCompare`` (used by ``RiskAnalyzer.Impact``,
+``RiskAnalyzer.ts:57-60``) is restated as a three-level ICU-root key whose
+tables come from the reference's own Node (tests/golden/locale_order.json);
+it is pinned on that file's corpus (ASCII names, tabs, punctuation, case,
+decomposable Latin accents).  Letters without a canonical decomposition
+outside ASCII remain unpinned.
 """
 from __future__ import annotations
 
@@ -968,19 +970,58 @@ class Normalizer:
         return [n * (1 - minimum) + minimum for n in Normalizer.FixedRatio(inp)]
 
 
+def _locale_tables():
+    """ICU root tables as the reference's Node reports them
+    (tests/golden/locale_order.json, made by tests/golden/gen_locale_order.js):
+    whitespace/punctuation primary order, ignorable controls, and the
+    secondary order of the combining marks U+0300..U+036F."""
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                        "locale_order.json")
+    d = json.load(open(path))
+    ign = set(d["punct_ignorable"])
+    punct = {c: i for i, c in enumerate(c for c in d["punct_sorted"] if c not in ign)}
+    marks, r = {}, 0
+    for i, m in enumerate(d["marks_sorted"]):
+        if i and d["marks_signs"][i - 1] != 0:
+            r += 1
+        marks[m] = r
+    return punct, ign, marks
+
+
+_LOCALE = None
+
+
 def _locale_key(s: str):
-    """ICU-root-like collation key for ASCII (see module docstring)."""
-    prim = []
-    for ch in s:
-        o = ord(ch)
-        if ch.isalpha():
-            prim.append((3, ch.lower()))
-        elif ch.isdigit():
+    """localeCompare (ICU root, en-US) as three levels: primary (whitespace <
+    punctuation < digits < case-folded base letters; ignorable controls
+    skipped), secondary (NFD combining marks per letter), tertiary (case)."""
+    import unicodedata
+
+    global _LOCALE
+    if _LOCALE is None:
+        _LOCALE = _locale_tables()
+    punct, ign, marks = _LOCALE
+    prim, sec, tert = [], [], []
+    for ch in unicodedata.normalize("NFD", s):
+        if ord(ch) in marks:
+            if sec:
+                sec[-1] = sec[-1] + (marks[ord(ch)],)
+            continue
+        if ch in ign:
+            continue
+        if ch in punct:
+            prim.append((1, punct[ch]))
+        elif ch.isdigit() and ch.isascii():
             prim.append((2, ch))
+        elif ch.isalpha() and ch.isascii():
+            prim.append((3, ch.lower()))
         else:
-            prim.append((1, o))
-    tert = [0 if c.islower() else 1 for c in s]
-    return (prim, tert)
+            prim.append((4, ord(ch)))
+        sec.append(())
+        tert.append(1 if ch.isupper() else 0)
+    return (prim, sec, tert)
 
 
 def _sort_locale(items, key):
