@@ -855,7 +855,15 @@ static int run_deps(kmz_ctx *c, bool links) {
     const uint32_t scap = c->scap, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
     uint32_t lb1, lb2;
     if (!key_bins(c->tcap, &lb1, &lb2)) return fail(c, KMZ_E_ARG, "edge-set capacity is not ESLICE * 2^k");
-    const uint64_t nsl = c->tcap / ESLICE, bcap = ((uint64_t)ng * scap + nsl - 1) / nsl;
+    // slice buckets (direct enumeration): KMZ_BUCKET_X times the mean fill --
+    // hot endpoints concentrate keys in a few slices (config 5: the fullest
+    // slice holds ~3x the mean), and what overflows is inserted in place
+#ifndef KMZ_BUCKET_X
+#define KMZ_BUCKET_X 3  // (x1 -> x3: config 5's k_key_part + k_key_slice 2.97 -> 2.69 ms)
+#endif
+    const uint64_t nsl = c->tcap / ESLICE, bmean = ((uint64_t)ng * scap + nsl - 1) / nsl;
+    const uint64_t bcap = direct ? std::min<uint64_t>(bmean * KMZ_BUCKET_X, std::max<uint64_t>(bmean, (12ull << 30) / 8 / nsl))
+                                 : bmean;
     void *old_ctab = c->ctab.p;
     c->k4_lb1 = direct ? lb1 : 0;
     c->k4_nsl = (uint32_t)nsl;
