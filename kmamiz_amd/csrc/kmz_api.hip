@@ -763,13 +763,13 @@ static int run_shape_stats(kmz_ctx *c) {
   if (part) {
     const uint32_t Pp = k3_partitions((uint32_t)Gs), nt = k3_tiles(n);
     const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(64, 2048 / Pp));
-    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, (size_t)Pp * nt * 4 + 4) ||
+    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, k3_dir_words(n, Pp, S) * 4 + 4) ||
         ensure(c, c->k3part, (size_t)S * 6 * Gs * 8) || ensure(c, c->tile_tmp, (size_t)nt * 16))
       return KMZ_E_HIP;
     {
       Timed t(c, KMZ_K_STATS);
       launch_k3_produce(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_shapes,
-                        c->n_status, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp));
+                        c->n_status, S, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp));
     }
     {
       Timed t(c, KMZ_K_REDUCE);

@@ -61,7 +61,7 @@ void launch_synth_fill(hipStream_t s, int config, uint64_t seed, uint64_t t0, ui
 // partitioned K3 / K4 (kmz_part.hip)
 void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
                        const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
-                       uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, unsigned int *counters,
+                       uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint32_t S, unsigned int *counters,
                        unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp);
 void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
                       const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp);
@@ -76,6 +76,7 @@ uint32_t k3_partitions(uint32_t G);
 uint32_t k3_pmax();
 uint64_t k3_pool_bytes(uint32_t n);
 uint32_t k3_tiles(uint32_t n);
+uint64_t k3_dir_words(uint32_t n, uint32_t P, uint32_t S);
 void launch_tile_sum(hipStream_t s, const uint32_t *v, uint32_t ntiles, uint32_t stride, uint32_t fields,
                      unsigned long long *out, uint32_t max_field);
 

@@ -64,18 +64,22 @@ struct __align__(16) Rec {
   uint32_t w;    // group within the partition (10 bits) | span index within the tile << 10 (11 bits)
 };
 
-constexpr uint32_t K3T = 2048;     // spans per tile
+#ifndef KMZ_K3T
+#define KMZ_K3T 2048
+#endif
+constexpr uint32_t K3T = KMZ_K3T;  // spans per tile
 constexpr uint32_t K3R = 1024;     // groups per partition
 constexpr uint32_t K3PMAX = 1024;  // partitions (G <= 1M)
-constexpr int K3PT = 512;          // producer threads
-static_assert(K3R <= 1024 && K3T <= 2048, "record word: 10 group bits, 11 index bits");
+constexpr int K3PT = K3T / 4;      // producer threads (four spans each)
+static_assert(K3R <= 1024 && K3T <= 4096 && K3PT <= 1024, "record word: 10 group bits, 12 index bits");
 
 __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
                                                    const uint16_t *__restrict__ status, const uint32_t *__restrict__ dur,
                                                    const int64_t *__restrict__ ts, uint32_t n,
                                                    const uint32_t *__restrict__ ep_of_shape, uint32_t n_shapes,
                                                    uint32_t n_ep, uint32_t n_status, uint32_t P, uint32_t ntiles,
-                                                   Rec *__restrict__ pool, uint32_t *__restrict__ dir,
+                                                   uint32_t S, uint32_t tps, Rec *__restrict__ pool,
+                                                   uint32_t *__restrict__ dir,
                                                    unsigned int *__restrict__ counters,
                                                    uint32_t *__restrict__ tile_servers) {
   __shared__ uint32_t cnt[K3PMAX], off[K3PMAX];
@@ -124,7 +128,10 @@ __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ k
   if (flags) atomicOr(&counters[C_FLAGS], flags);
   __syncthreads();
   uint32_t total = block_excl_scan_pairs<K3PT>(cnt, off, P, wave_tot);
-  for (uint32_t p = threadIdx.x; p < P; p += K3PT) dir[(uint64_t)p * ntiles + tile] = (off[p] << 16) | cnt[p];
+  // directory: [partition][slice][tile within the slice], so a reduce
+  // workgroup's words are contiguous (slice s holds tiles s, s + S, ...)
+  for (uint32_t p = threadIdx.x; p < P; p += K3PT)
+    dir[((uint64_t)p * S + tile % S) * tps + tile / S] = (off[p] << 16) | cnt[p];
 #pragma unroll
   for (int k = 0; k < PER; ++k)
     if (pp[k] != NONE) stage[off[pp[k]] + rr[k]] = rec[k];
@@ -219,14 +226,15 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
     }
   }
   __syncthreads();
-  const uint32_t *row = dir + (uint64_t)p * ntiles;
+  const uint32_t tps = (ntiles + S - 1) / S;
+  const uint32_t *row = dir + ((uint64_t)p * S + s) * tps;  // this slice's tiles, in order
   constexpr uint32_t U = 4;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t step = (uint64_t)S * NW;  // consecutive tiles of this wave
   for (uint64_t k0 = (uint64_t)s + (uint64_t)w * S; k0 < ntiles; k0 += step * K3RB) {
     // this lane's run: tile k0 + lane * step
     const uint64_t k = k0 + lane * step;
-    const uint32_t x = k < ntiles ? row[k] : 0;
+    const uint32_t x = k < ntiles ? row[(k - s) / S] : 0;
     const uint32_t o = x >> 16;
     const uint32_t c = (o + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;  // a well-formed directory never exceeds the tile
     uint32_t incl = c;
@@ -446,12 +454,13 @@ void launch_k3_small(hipStream_t s, const uint8_t *kind, const uint32_t *shape, 
 
 void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
                        const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
-                       uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, unsigned int *counters,
+                       uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint32_t S, unsigned int *counters,
                        unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp) {
   if (!n || !n_ep) return;
   const uint32_t G = n_ep * n_status, P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
   hipLaunchKernelGGL(k3_produce, dim3(ntiles), dim3(K3PT), 0, s, kind, shape, status, dur, ts, n, ep_of_shape,
-                     n_shapes, n_ep, n_status, P, ntiles, (Rec *)pool, dir, counters, tile_tmp);
+                     n_shapes, n_ep, n_status, P, ntiles, S, (ntiles + S - 1) / S, (Rec *)pool, dir, counters,
+                     tile_tmp);
   hipLaunchKernelGGL(k_tile_sum, dim3(std::max<uint32_t>(1, tile_sum_blocks(ntiles))), dim3(1024), 0, s, tile_tmp, ntiles, 1u, 1u,
                      n_server, 99u);
 }
@@ -479,6 +488,10 @@ uint32_t k3_partitions(uint32_t G) { return (G + K3R - 1) / K3R; }
 uint32_t k3_pmax() { return K3PMAX; }
 uint64_t k3_pool_bytes(uint32_t n) { return (uint64_t)((n + K3T - 1) / K3T) * K3T * sizeof(Rec); }
 uint32_t k3_tiles(uint32_t n) { return (n + K3T - 1) / K3T; }
+uint64_t k3_dir_words(uint32_t n, uint32_t P, uint32_t S) {
+  const uint64_t nt = k3_tiles(n);
+  return (uint64_t)P * S * ((nt + S - 1) / S);
+}
 
 void launch_tile_sum(hipStream_t s, const uint32_t *v, uint32_t ntiles, uint32_t stride, uint32_t fields,
                      unsigned long long *out, uint32_t max_field) {
