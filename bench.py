@@ -339,7 +339,7 @@ def main():
         del host, devb
     if rank == 0:
         cpu = None
-        if args.cpu_seconds > 0:
+        if args.cpu_seconds > 0 and world == 1:  # (the CPU baseline is an N = 1 figure)
             cpu_tail = None
             if tail_on:
                 def cpu_tail(st, keys, ep):
