@@ -26,7 +26,7 @@
 // finish may not produce, 0 and ROOT_SIG, raise F_SIG like a failed check: the
 // run is repeated with another hash seed.)  An entry is 16 bytes.
 //
-//   k4_chain       persistent workgroups over 768-span tiles + a 128-span halo
+//   k4_chain       persistent workgroups over 1024-span tiles + a 128-span halo
 //                  per side in LDS (contracted parent, kind, endpoint, element
 //                  hash).  Per tile: hash every non-CLIENT ancestry in the
 //                  window (a Horner walk over the LDS element hashes), probe
@@ -56,7 +56,7 @@
 namespace kmz {
 
 #ifndef KMZ_CHAIN_CT
-#define KMZ_CHAIN_CT 768
+#define KMZ_CHAIN_CT 1024  // (768 -> 1024: less halo per span, mesh walk 1.20 -> 1.10 ms)
 #endif
 #ifndef KMZ_CHAIN_CH
 #define KMZ_CHAIN_CH 128
