@@ -174,18 +174,28 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   KMZ_JSTAMP(0);
   bool ovf = false;
   if (!(ablate & 256)) {  // insert: the emptier of the two buckets, else the other, else the stash
+    // (in lockstep over the thread's PW ids: the bucket counts, then the
+    // slot claims, each step's LDS operations in flight together)
+    uint32_t bq[PW], sq[PW];
+    bool iq[PW];
+#pragma unroll
+    for (int q = 0; q < PW; ++q) {
+      iq[q] = w0 + q * JTT + threadIdx.x < w1 && s[q] != 0;
+      const uint32_t b1 = jb1(hs[q]), b2 = jb2(hs[q]);
+      bq[q] = lcnt[b1] <= lcnt[b2] ? b1 : b2;
+    }
+#pragma unroll
+    for (int q = 0; q < PW; ++q) sq[q] = iq[q] ? atomicAdd(&lcnt[bq[q]], 1u) : 0u;
 #pragma unroll
     for (int q = 0; q < PW; ++q) {
       const uint32_t jl = q * JTT + threadIdx.x;
-      if (w0 + jl >= w1 || s[q] == 0) continue;
-      const uint32_t b1 = jb1(hs[q]), b2 = jb2(hs[q]);
-      const uint16_t e = (uint16_t)((jfp(hs[q]) << 12) | (jl + 1));
-      uint32_t b = lcnt[b1] <= lcnt[b2] ? b1 : b2;
-      uint32_t slot = atomicAdd(&lcnt[b], 1u);
-      if (slot >= 8) {
-        b = b ^ b1 ^ b2;
+      if (!iq[q]) continue;
+      uint32_t b = bq[q], slot = sq[q];
+      if (slot >= 8) {  // (rare) the other bucket
+        b = b ^ jb1(hs[q]) ^ jb2(hs[q]);
         slot = atomicAdd(&lcnt[b], 1u);
       }
+      const uint16_t e = (uint16_t)((jfp(hs[q]) << 12) | (jl + 1));
       if (slot < 8) {
         reinterpret_cast<uint16_t *>(&lbkt[b])[slot] = e;
       } else {
@@ -200,38 +210,66 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   __syncthreads();
   KMZ_JSTAMP(1);
   const uint32_t ns = min(nstash, JSTASH);
-  // window parents: tile spans, and CLIENT spans of the halo (chains pass through them)
+  // window parents: tile spans, and CLIENT spans of the halo (chains pass
+  // through them).  The PW lookups of a thread go in lockstep, each step's
+  // LDS reads in flight together: both buckets; the first fingerprint
+  // candidate's entry; its id.  Further candidates (a fingerprint collision)
+  // and the stash are the rare tail.
+  uint32_t cq[PW], hq[PW], eq[PW];
+  bool nq[PW];
+  uint16_t rq[PW];
 #pragma unroll
   for (int q = 0; q < PW; ++q) {
     const uint32_t jl = q * JTT + threadIdx.x, j = w0 + jl;
-    if (j >= w1) continue;
-    uint32_t r = L_NONE;
-    if (p[q] != 0 && ((j >= t0 && j < t1) || k[q] == KIND_CLIENT) && !(ablate & 512)) {
-      r = L_MISS;
-      const uint32_t h = jfold(p[q]);
-      const uint32_t f = jfp(h), pb1 = jb1(h), pb2 = jb2(h);
-      const uint4 x = lbkt[pb1], y = lbkt[pb2];
-      const uint32_t c[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-      // candidates: entries with the fingerprint (two per word, SWAR; empty
-      // entries have fingerprint 0, which no id has)
-      const uint32_t pat = (f << 12) | (f << 28);
-      uint32_t cand = 0;
+    nq[q] = j < w1 && p[q] != 0 && ((j >= t0 && j < t1) || k[q] == KIND_CLIENT) && !(ablate & 512);
+    rq[q] = nq[q] ? L_MISS : L_NONE;
+    hq[q] = jfold(p[q]);
+    const uint32_t f = jfp(hq[q]);
+    const uint4 x = lbkt[nq[q] ? jb1(hq[q]) : 0], y = lbkt[nq[q] ? jb2(hq[q]) : 0];
+    const uint32_t c[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    // candidates: entries with the fingerprint (two per word, SWAR; empty
+    // entries have fingerprint 0, which no id has)
+    const uint32_t pat = (f << 12) | (f << 28);
+    uint32_t cand = 0;
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const uint32_t v = c[t], z = v ^ pat;
-        cand |= ((z & 0xF000u) == 0 ? 1u : 0u) << (2 * t);
-        cand |= ((z & 0xF0000000u) == 0 ? 1u : 0u) << (2 * t + 1);
+    for (int t = 0; t < 8; ++t) {
+      const uint32_t v = c[t], z = v ^ pat;
+      cand |= ((z & 0xF000u) == 0 ? 1u : 0u) << (2 * t);
+      cand |= ((z & 0xF0000000u) == 0 ? 1u : 0u) << (2 * t + 1);
+    }
+    cq[q] = nq[q] ? cand : 0;
+  }
+  const uint16_t *lbkt16 = reinterpret_cast<const uint16_t *>(lbkt);
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {  // the first candidate's entry (local index + 1)
+    const uint32_t t = __builtin_ctz(cq[q] | 0x10000u);
+    const uint32_t b = t < 8 ? jb1(hq[q]) : jb2(hq[q]);
+    eq[q] = cq[q] ? lbkt16[b * 8 + (t & 7)] & 0xFFF : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {  // its id
+    const bool hit = eq[q] && lsid[eq[q] ? eq[q] - 1 : 0] == p[q];
+    if (hit) rq[q] = (uint16_t)(eq[q] - 1);
+    if (!hit) cq[q] &= cq[q] - 1;  // (the rest, if the first was a fingerprint collision)
+    else cq[q] = 0;
+  }
+#pragma unroll
+  for (int q = 0; q < PW; ++q) {
+    const uint32_t jl = q * JTT + threadIdx.x;
+    if (w0 + jl >= w1) continue;
+    uint32_t r = rq[q];
+    uint32_t cand = cq[q];
+    while (cand) {  // (rare) further candidates
+      const uint32_t t = __builtin_ctz(cand);
+      cand &= cand - 1;
+      const uint32_t en = lbkt16[(t < 8 ? jb1(hq[q]) : jb2(hq[q])) * 8 + (t & 7)] & 0xFFF;
+      if (lsid[en - 1] == p[q]) {
+        r = en - 1;
+        break;
       }
-      while (cand) {  // usually one candidate: the parent
-        const uint32_t t = __builtin_ctz(cand);
-        cand &= cand - 1;
-        // (re-read the entry from LDS: no dynamic indexing of registers)
-        const uint32_t en = reinterpret_cast<const uint16_t *>(&lbkt[t < 8 ? pb1 : pb2])[t & 7] & 0xFFF;
-        if (lsid[en - 1] == p[q]) {
-          r = en - 1;
-          break;
-        }
-      }
+    }
+    if (nq[q] && r == L_MISS) {
+      const uint32_t f = jfp(hq[q]);
       for (uint32_t t = 0; t < ns; ++t) {
         const uint32_t en = stash[t];
         if ((en >> 12) == f && lsid[(en & 4095) - 1] == p[q]) r = (en & 4095) - 1;
