@@ -17,7 +17,7 @@
 //   k_cert_check    pass 3: exact duplicate check of each sub-bin in LDS.
 //
 // A window hit is the Map's answer only if the id occurs once in the whole
-// batch; the certificate proves that (mix64 is a bijection, so equal hashes
+// batch; the certificate proves that (cert_hash is a bijection, so equal hashes
 // are equal ids).  If any id repeats, the host runs the global table path
 // (kmz_kernels.hip: K1 build/fixup, K2 resolve), which implements the Map's
 // last-value/first-position rule.  MISS parents are looked up with a
@@ -77,7 +77,7 @@ __device__ void block_scan_lds(uint32_t *a, uint32_t m, uint32_t *wsum) {
 }
 
 // LDS hash of a window: two-choice buckets of 8 u16 entries (one 16-byte LDS
-// read each), entry = fingerprint (4 bits of mix64(id)) << 12 | local index + 1.
+// read each), entry = fingerprint (4 bits of a multiplicative hash of the id) << 12 | local index + 1.
 // A lookup reads its two buckets and compares 16 fingerprints; only a
 // fingerprint hit reads the 64-bit id.  Entries that find both buckets full go
 // to a small stash that lookups scan (broadcast reads) when it is not empty.
@@ -88,8 +88,17 @@ constexpr uint32_t JSTASH = 64;
 // Window-hash placement: two 32-bit multiplicative hashes of the folded id.
 // Placement quality only affects speed (an overfull bucket pair goes to the
 // stash, a full stash to the table path); exactness comes from comparing the
-// full 64-bit ids, and the certificate keeps its own bijective mix64.
+// full 64-bit ids, and the certificate keeps its own bijective cert_hash.
 static_assert(JB == 1024, "bucket indices are the top 10 bits of the 32-bit hashes");
+// the certificate's hash of a span id: a bijection of the 64-bit ids (an odd
+// multiplier, then an xorshift), so equal hashes are equal ids; its top bits
+// pick the bin and sub-bin, its low bits the check's bucket.  (mix64's second
+// multiply and shifts bought nothing here: one multiply spreads sequential
+// ids over the top bits, the xorshift brings them to the low bits.)  0 -> 0.
+__device__ __forceinline__ uint64_t cert_hash(uint64_t x) {
+  x *= 0x9E3779B97F4A7C15ull;
+  return x ^ (x >> 29);
+}
 __device__ __forceinline__ uint32_t jfold(uint64_t id) { return (uint32_t)id ^ (uint32_t)(id >> 32); }
 __device__ __forceinline__ uint32_t jb1(uint32_t x) { return (x * 0x9E3779B1u) >> 22; }
 __device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >> 22; }
@@ -331,7 +340,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
       pend += cp[q] == PEND;
       const uint64_t key = lsid[i - w0];
       zero += key == 0;
-      hv[q] = mix64(key);
+      hv[q] = cert_hash(key);
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
@@ -513,7 +522,7 @@ __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__
   bool lost = false;
 #pragma unroll
   for (int q = 0; q < CK_PER; ++q) {
-    if (h[q] == 0) continue;  // padding (and mix64(0) == 0: span id 0, reported as F_ZERO_ID)
+    if (h[q] == 0) continue;  // padding (and cert_hash(0) == 0: span id 0, reported as F_ZERO_ID)
     const uint32_t b = (uint32_t)h[q] & (CK_NB - 1);
     const uint32_t slot = atomicAdd(&bcnt[b], 1u);
     if (slot < CK_S) {
