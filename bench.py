@@ -379,6 +379,9 @@ def main():
                 "relations_per_gpu": A,
                 "edge_keys": info["n_triples"],
                 "parallelism": f"traceId-shard x{world}" if world > 1 else "single GPU",
+                "sharding_guards": ("in every timed step: id-table/size agreement, unresolved parents, "
+                                    "cross-shard repeated span ids (all-to-all of hashed ids + certificate)"
+                                    if world > 1 else None),
                 "service_tail": tail_on,
                 "fetched": ("groups + endpoints to the host; the edge keys stay in HBM, where "
                             "kmz_tail_run reads them" if tail_on else

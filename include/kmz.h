@@ -133,7 +133,9 @@ typedef struct kmz_info {
   uint64_t n_groups;    /* group slots = n_ep * n_status                    */
   uint32_t flags;       /* internal error bits                             */
   uint32_t path;        /* last dependency run: bit 0 window join (else global span table),
-                           bit 1 chain-interning walk (else per-relation global walk) */
+                           bit 1 chain walk k4_chain (else per-relation global walk k_walk),
+                           bit 2 direct enumeration (else chain interning),
+                           bit 3 k_walk redo after a chain-table wait ran out (F_SPIN) */
   uint64_t n_chains;    /* distinct interned ancestor chains (chain-interning path) */
 } kmz_info;
 
@@ -305,6 +307,20 @@ void kmz_finalize_host(const uint64_t *partials, uint64_t n_groups, kmz_group *o
 int kmz_unresolved_parents(kmz_ctx *ctx, uint64_t *ids, uint64_t cap, uint64_t *n_out, int mem);
 /* how many of the given ids (0 = padding) are span ids of the loaded batch */
 int kmz_count_ids(kmz_ctx *ctx, const uint64_t *ids, uint64_t n, int mem, uint64_t *found);
+/* The other half of the global span map (Traces.ts:117-123: a span id seen
+ * twice collapses to one row, last value at the first position): ids that
+ * repeat ACROSS shards.  kmz_route_ids writes the loaded batch's span ids,
+ * each hashed by the certificate's bijection, grouped by owner rank
+ * r = (hash >> 32) * world >> 32: rank r's values are out[o_r, o_r + counts[r]),
+ * o_r = counts[0] + .. + counts[r-1] (out: n_spans values, host or device
+ * memory per `mem`; counts: host, `world` entries, 1 <= world <= 1024).
+ * After an all-to-all of those segments, kmz_id_repeats on what a rank
+ * received sets *repeated = 1 if any value occurs twice, i.e. some span id
+ * is in two shards (the uniqueness certificate over the values; exact).
+ * KMZ_E_UNSUPPORTED when it cannot decide (more values than the certificate
+ * plans for, or a bucket overflow): the caller checks another way. */
+int kmz_route_ids(kmz_ctx *ctx, uint32_t world, uint64_t *out, uint64_t cap, int mem, uint64_t *counts);
+int kmz_id_repeats(kmz_ctx *ctx, const uint64_t *vals, uint64_t n, int mem, uint32_t *repeated);
 
 /* ---- traceId sharding (shard = h(traceId) mod G) ------------ */
 /* The shard of a trace, from its traceId string (the reference dedups and

@@ -62,6 +62,7 @@ struct kmz_ctx {
   DevBuf kbucket, kbucket_n;  // staged keys partitioned by edge-set slice (k_key_part)
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
+  DevBuf rt_hist, rt_tot, rt_out, rt_ctr;  // cross-shard repeated-id guard: routing scratch, certificate counters
   // device JSON ingest (kmz_json.hip)
   DevBuf j_buf, j_elem, j_state, j_jsc, j_mask, j_cnt, j_off, j_csc, j_small, j_starts, j_slices, j_tslot, j_stab,
       j_ttab, j_reps, j_smap, j_tmap;
@@ -90,6 +91,7 @@ struct kmz_ctx {
   int path = 0;             // kmz_info.path of the last dependency run
   bool sstats = false;      // shape-level K3 partials computed in this run
   bool chain_ran = false;   // this run's dependency graph came from k4_chain's chain interning
+  bool walk_once = false;   // a K4 wait ran out (F_SPIN): this run is redone on the exact per-row walk
   // K4 mode: chain interning, or direct enumeration (every row stages all its
   // keys) when most rows start a new chain -- chosen from the last interning
   // run's chains/rows for this shape table, measured again every 64 runs
@@ -309,7 +311,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
                     &c->tl_sstat, &c->tl_rel, &c->o_key, &c->o_val, &c->o_out,
@@ -836,7 +838,7 @@ static int run_deps(kmz_ctx *c, bool links) {
     dups = hc[C_DUPS];
   }
   if (ensure(c, c->trip, c->tcap * 8) || ensure(c, c->trip_out, c->tcap * 8)) return KMZ_E_HIP;
-  if (dups == 0 && !(c->ablate & 16)) {
+  if (dups == 0 && !(c->ablate & 16) && !c->walk_once) {
     // unique span ids: rows are the SERVER spans; chain interning (kmz_chain.hip)
     if (!c->sstats && (r = run_shape_stats(c))) return r;
     const uint32_t nt = chain_tiles(n);
@@ -852,7 +854,10 @@ static int run_deps(kmz_ctx *c, bool links) {
     while (!(c->ablate & (1u << 30)) && (uint64_t)c->scap * chain_grid(n) < 8ull * n &&
            (uint64_t)chain_grid(n) * c->scap * 2 * 8 <= stage_limit(n))
       c->scap *= 2;
-    const uint32_t scap = c->scap, dcap = 1u << 12, wcap = 1u << 16, ng = chain_grid(n);
+    // deferred chain checks per workgroup (KMZ_ABLATE bit 10, test knob: 4, so
+    // that leaders fall through to the in-place chain_put waits)
+    const uint32_t scap = c->scap, dcap = (c->ablate & (1u << 10)) ? 4u : 1u << 12, wcap = 1u << 16,
+                   ng = chain_grid(n);
     uint32_t lb1, lb2;
     if (!key_bins(c->tcap, &lb1, &lb2)) return fail(c, KMZ_E_ARG, "edge-set capacity is not ESLICE * 2^k");
     // slice buckets (direct enumeration): KMZ_BUCKET_X times the mean fill --
@@ -904,13 +909,13 @@ static int run_deps(kmz_ctx *c, bool links) {
                           P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), scap,
                           P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kbucket), bcap,
                           P<uint32_t>(c->kbucket_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
-                          gpos, wcap);
+                          gpos, wcap, c->ablate);
     }
     {  // ancestries that left their window: one pass, sized on the device (no host round trip)
       Timed t(c, KMZ_K_PEND);
       launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent),
                         n, P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
-                        P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, wcap, direct);
+                        P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, wcap, direct, c->ablate);
     }
     if (c->overlap) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_k3, 0));  // the shape-level K3 partials
     {
@@ -930,8 +935,10 @@ static int run_deps(kmz_ctx *c, bool links) {
     return KMZ_OK;
   }
   // repeated span ids: the row of an id is its last occurrence at its first
-  // position; one global walk per row over the table path's links
-  c->path = joined ? 1 : 0;
+  // position; one global walk per row over the table path's links.  Also the
+  // exact redo of a run whose chain-table wait ran out (F_SPIN): with unique
+  // ids the walk reads no table.
+  c->path = (joined ? 1 : 0) | (c->walk_once ? 8 : 0);
   HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
   {
     // the table is read only for repeated ids (dups > 0), which implies run_table
@@ -1103,6 +1110,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
   const bool links = (flags & (KMZ_RUN_SPAN_LINKS | KMZ_RUN_DEP_ORDER)) != 0;
   hipSetDevice(c->device);
   c->hpin_valid = false;
+  c->walk_once = false;
   for (int attempt = 0; attempt < 8; ++attempt) {
     c->sstats = false;
     c->chain_ran = false;
@@ -1184,6 +1192,13 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     }
     if (h[C_FLAGS] & F_TRIPLE_OVERFLOW) {
       c->tcap *= 4;
+      retry = true;
+    }
+    if ((flags & KMZ_RUN_DEPS) && (h[C_FLAGS] & F_SPIN) && !c->walk_once) {
+      // a chain-table wait ran out: some check, row or key may be missing.
+      // Redo this run on the exact per-row walk (kmz_info.path bit 3 says so)
+      c->walk_once = true;
+      c->ctab_dirty = true;  // (entries may be half written: a full clear next time)
       retry = true;
     }
     if (h[C_FLAGS] & F_SIG) {  // an ancestry-hash collision: same run, another seed
@@ -1669,6 +1684,65 @@ int kmz_count_ids(kmz_ctx *c, const uint64_t *ids, uint64_t n, int mem, uint64_t
   HIPCHK(c, hipMemcpyAsync(&f, cnt + 1, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   *found = f;
+  return KMZ_OK;
+}
+
+int kmz_route_ids(kmz_ctx *c, uint32_t world, uint64_t *out, uint64_t cap, int mem, uint64_t *counts) {
+  if (!c || !counts || world == 0 || (c->n && !out)) return KMZ_E_ARG;
+  if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_route_ids before kmz_load");
+  if (cap < c->n) return fail(c, KMZ_E_ARG, "output too small");
+  const uint32_t n = (uint32_t)c->n;
+  if (ensure(c, c->rt_hist, (size_t)route_chunks(n) * world * 4) || ensure(c, c->rt_tot, (size_t)world * 8))
+    return KMZ_E_HIP;
+  unsigned long long *dst = reinterpret_cast<unsigned long long *>(out);
+  if (mem != KMZ_MEM_DEVICE) {
+    if (ensure(c, c->rt_out, (size_t)n * 8)) return KMZ_E_HIP;
+    dst = P<unsigned long long>(c->rt_out);
+  }
+  if (!launch_route(c->stream, c->sid, n, world, P<uint32_t>(c->rt_hist), P<unsigned long long>(c->rt_tot), dst))
+    return fail(c, KMZ_E_ARG, "world must be 1..1024");
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(counts, c->rt_tot.p, (size_t)world * 8, hipMemcpyDeviceToHost, c->stream));
+  if (mem != KMZ_MEM_DEVICE && n) HIPCHK(c, hipMemcpyAsync(out, dst, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32_t *repeated) {
+  if (!c || !repeated || (n && !vals)) return KMZ_E_ARG;
+  *repeated = 0;
+  if (n < 2) return KMZ_OK;
+  CertPlan pl;
+  if (n >= 0xFFFFFFFFull || !cert_plan((uint32_t)n, &pl))
+    return fail(c, KMZ_E_UNSUPPORTED, "too many values for the certificate: check on the host");
+  const uint32_t m = (uint32_t)n;
+  const size_t nsub = (size_t)cert_bins() << pl.B2;
+  if (ensure(c, c->cpool1, cert_pool1_words(m) * 8) || ensure(c, c->cdir, cert_dir_entries(m) * 2) ||
+      ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) || ensure(c, c->rt_ctr, C_COUNT * 4))
+    return KMZ_E_HIP;
+  const unsigned long long *src = reinterpret_cast<const unsigned long long *>(vals);
+  if (mem != KMZ_MEM_DEVICE) {
+    if (ensure(c, c->rt_out, (size_t)m * 8)) return KMZ_E_HIP;
+    HIPCHK(c, hipMemcpyAsync(c->rt_out.p, vals, (size_t)m * 8, hipMemcpyHostToDevice, c->stream));
+    src = P<unsigned long long>(c->rt_out);
+  }
+  unsigned int *cnt = P<unsigned int>(c->rt_ctr);
+  unsigned int *cur2 = P<unsigned int>(c->ccur);
+  HIPCHK(c, hipMemsetAsync(cnt, 0, C_COUNT * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(cur2, 0, nsub * 4, c->stream));
+  launch_cert_bin(c->stream, src, m, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir));
+  launch_cert_split(c->stream, m, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
+                    P<unsigned long long>(c->cpool2), cur2, cnt);
+  launch_cert_check(c->stream, m, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
+  HIPCHK(c, hipGetLastError());
+  unsigned int h[C_COUNT];
+  HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (h[C_CERT] & CERT_DUP) {
+    *repeated = 1;
+    return KMZ_OK;
+  }
+  if (h[C_CERT] & CERT_OVF) return fail(c, KMZ_E_UNSUPPORTED, "certificate overflow: check on the host");
   return KMZ_OK;
 }
 

@@ -49,6 +49,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 
 #include "kmz_kernels.h"
@@ -79,6 +80,13 @@ static_assert(CW % CTT == 0, "window slots must split evenly over the threads");
 constexpr uint16_t W_NONE = 0xFFFF, W_CYC = 0xFFFE, W_OUT = 0xFFFD;
 constexpr uint32_t WIN_DEPTH = 255;  // deeper in-window ancestries take the pending path
 constexpr uint32_t PROBE_MAX = 512;
+// bound of a wait on another lane's publish (chain_put returning 0).  The
+// publish is the instruction after that lane's claim, so a wait this long
+// means something is wrong; it raises F_SPIN (the run is redone exactly) and
+// never drops a check, a row or a key.  KMZ_ABLATE bit 11 (test knob) makes
+// the bound 0, i.e. every wait "runs out".
+constexpr uint32_t SPIN_MAX = 1u << 20;
+__host__ __device__ __forceinline__ uint32_t spin_bound(uint32_t ablate) { return (ablate & (1u << 11)) ? 0u : SPIN_MAX; }
 constexpr uint32_t IMAP = 256;  // LDS map: one inserting leader per distinct new chain
 // staged keys are binned by the edge set's slices: 2^lb1 coarse bins per tile
 // workgroup (k4_chain), each split into 2^lb2 slices by k_key_part
@@ -228,8 +236,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   __shared__ uint32_t red[CTT / 64][4];
   // diagnostic phase clock (KMZ_ABLATE bit 22 only): s_memtime deltas by thread 0
   const bool dbg_t = (ablate & (1u << 22)) != 0;
+  const uint32_t spin = spin_bound(ablate);
   unsigned long long tprev = 0, tacc[6] = {0, 0, 0, 0, 0, 0};
-#define KMZ_STAMP(k)                                            \
+#define KMZ_STAMP(k)                                         \
   if (dbg_t) {                                                  \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     if (threadIdx.x == 0 && tprev) tacc[k] += t_ - tprev;       \
@@ -573,9 +582,10 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
             *reinterpret_cast<ulonglong2 *>(defer + 2 * ((uint64_t)blockIdx.x * dcap + x)) = make_ulonglong2(sg[q], ps[q]);
           } else {
             int rr = 0;
-            for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t)
+            for (uint32_t t = 0; t < spin && rr == 0; ++t)
               rr = chain_put(ctab, ccap, sg[q], ps[q], &flags, wpos + (uint64_t)gridDim.x * wcap, wcap,
                              counters);  // (the run's global written list follows the per-workgroup ones)
+            if (rr == 0) flags |= F_SPIN;  // unchecked: the run is redone on the exact walk
             fresh_n += rr == 1;
           }
         }
@@ -823,7 +833,7 @@ __global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *
                                                       unsigned long long *__restrict__ ctab, uint64_t ccap,
                                                       unsigned int *__restrict__ counters,
                                                       unsigned long long *__restrict__ stats64,
-                                                      uint32_t *__restrict__ gpos, uint32_t gcap) {
+                                                      uint32_t *__restrict__ gpos, uint32_t gcap, uint32_t spin) {
   uint32_t flags = 0, fresh = 0;
   for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
     for (uint32_t b = 0; b < (1u << lb1); ++b) {
@@ -835,8 +845,9 @@ __global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *
     for (uint32_t x = threadIdx.x; x < md; x += blockDim.x) {
       const unsigned long long *r = defer + 2 * ((uint64_t)w * dcap + x);
       int rr = 0;
-      for (uint32_t t = 0; t < (1u << 20) && rr == 0; ++t)
+      for (uint32_t t = 0; t < spin && rr == 0; ++t)
         rr = chain_put(ctab, ccap, r[0], r[1], &flags, gpos, gcap, counters);
+      if (rr == 0) flags |= F_SPIN;
       fresh += rr == 1;
     }
   }
@@ -860,7 +871,8 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
                                                      unsigned long long *__restrict__ ep_ts,
                                                      unsigned int *__restrict__ counters,
                                                      unsigned long long *__restrict__ stats64,
-                                                     uint32_t *__restrict__ gpos, uint32_t gcap, bool direct) {
+                                                     uint32_t *__restrict__ gpos, uint32_t gcap, bool direct,
+                                                     uint32_t spin) {
   const uint32_t m = min(counters[C_PLIST], pcap);
   uint32_t flags = 0;
   for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
@@ -896,9 +908,10 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     if (bad) continue;
     const uint64_t sg = sig_final(acc, d, seed, &flags), psig = a == NONE ? ROOT_SIG : sig_final(pacc, d - 1, seed, &flags);
     int r = direct ? 3 : 0;  // direct: no chain table, every row inserts its keys
-    for (uint32_t t = 0; t < 1u << 20 && r == 0; ++t)
+    for (uint32_t t = 0; t < spin && r == 0; ++t)
       r = chain_put(ctab, ccap, sg, psig, &flags, gpos, gcap, counters);
-    if (r <= 0) continue;
+    if (r == 0) flags |= F_SPIN;  // (the row is not counted: the run is redone on the exact walk)
+    if (r <= 0) continue;         // (-1: F_CHAIN_OVERFLOW, redone with a larger table)
     if (on) {  // a row: its relations, keys (new chain) and non-SERVER ancestors
       uint32_t kk = 0;
       for (uint32_t cur = a; cur != NONE; cur = cparent[cur]) {
@@ -953,7 +966,28 @@ extern "C" int kmz__debug_chain(unsigned long long *out, int reset) {
 }
 namespace kmz {
 
-uint32_t chain_grid(uint32_t n) { return std::min<uint32_t>(chain_tiles(n), CHAIN_WG); }
+// persistent workgroups of k4_chain: what the device keeps resident at once
+// (CUs x the occupancy of the larger of the two instances), so a workgroup
+// only ever waits on workgroups that are running.  Queried once per device;
+// CHAIN_WG (the 256-CU figure at CHAIN_WAVES) if the query fails.
+static uint32_t chain_resident() {
+  static std::mutex mu;
+  static uint32_t cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return CHAIN_WG;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!cached[dev]) {
+    int cus = 0, o0 = 0, o1 = 0;
+    uint32_t g = CHAIN_WG;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&o0, k4_chain<false>, CTT, 0) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, k4_chain<true>, CTT, 0) == hipSuccess && std::min(o0, o1) > 0)
+      g = (uint32_t)cus * (uint32_t)std::min(o0, o1);
+    cached[dev] = g;
+  }
+  return cached[dev];
+}
+uint32_t chain_grid(uint32_t n) { return std::min<uint32_t>(chain_tiles(n), chain_resident()); }
 
 // per shape: its dependency endpoint and the element hash of a SERVER span of
 // it under this run's seed (the walk's per-slot hash is then one gather)
@@ -1011,7 +1045,7 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
                          unsigned long long *bucket, uint64_t bcap, uint32_t *bucket_n,
                          const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
-                         uint32_t gcap) {
+                         uint32_t gcap, uint32_t ablate) {
   if (!chain_tiles(n)) return;
   const uint32_t g = chain_grid(n);
   uint32_t lb1, lb2;
@@ -1029,7 +1063,7 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
   } else {
     hipLaunchKernelGGL(k_chain_settle, dim3(g), dim3(256), 0, s, stage, scap >> lb1, stage_n, lb1, trip, tcap, defer,
                        dcap, defer_n, g, reinterpret_cast<unsigned long long *>(ctab), ccap, counters, stats64, gpos,
-                       gcap);
+                       gcap, spin_bound(ablate));
   }
   launch_tile_sum(s, wg_stats, g, 4u, 4u, stats64 + S_ROWS, 2u);  // rows, rel, maxd, chains
 }
@@ -1063,10 +1097,10 @@ void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, cons
                        const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
-                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct) {
+                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct, uint32_t ablate) {
   hipLaunchKernelGGL(k4_chain_pend, dim3(1024), dim3(256), 0, s, plist, pcap, kind, shape, ts, cparent, n, dep_ep,
                      n_shapes, n_ep, seed, reinterpret_cast<unsigned long long *>(ctab), ccap, trip, tcap, ep_ts,
-                     counters, stats64, gpos, gcap, direct);
+                     counters, stats64, gpos, gcap, direct, spin_bound(ablate));
 }
 
 }  // namespace kmz

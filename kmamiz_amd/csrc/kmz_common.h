@@ -28,6 +28,10 @@ constexpr uint32_t F_CTAB_DIRTY = 512u;     // (informational) the chain table c
 constexpr uint32_t F_STAGE_FULL = 1024u;    // (informational) K4 key staging overflowed: keys went straight to the edge set
 constexpr uint32_t F_MISS_OVERFLOW = 256u;  // the window join's miss table is too small (grown, run again)
 constexpr uint32_t F_SIG = 128u;  // a 64-bit ancestry hash collision (K4 retries with another seed)
+// a K4 wait on another lane's chain-table publish ran out of its bound: the
+// entry's check (and for a pending row its counts and keys) did not happen, so
+// the run is repeated on the exact per-row walk (kmz_run)
+constexpr uint32_t F_SPIN = 2048u;
 
 // splitmix64 finaliser: a bijection on u64 with mix64(0) == 0.
 KMZ_HD uint64_t mix64(uint64_t z) {
@@ -52,6 +56,17 @@ KMZ_HD uint64_t shard_hash(uint64_t hi, uint64_t lo) { return mix64(hi ^ mix64(l
 KMZ_HD uint32_t shard_of(uint64_t hi, uint64_t lo, uint32_t world) {
   return (uint32_t)mulhi64(shard_hash(hi, lo), world);
 }
+
+// The uniqueness certificate's hash of a span id (kmz_join.hip) and the
+// cross-shard id routing (kmz_guard.hip): a bijection of the 64-bit ids (an
+// odd multiplier, then an xorshift), so equal hashes are equal ids; 0 -> 0.
+KMZ_HD uint64_t id_hash(uint64_t x) {
+  x *= 0x9E3779B97F4A7C15ull;
+  return x ^ (x >> 29);
+}
+// owner rank of a hashed id among `world` ranks (a range of the hash space;
+// the host mirror in dist.py computes the same in numpy uint64)
+KMZ_HD uint32_t id_owner(uint64_t h, uint32_t world) { return (uint32_t)(((h >> 32) * world) >> 32); }
 
 // position of key k in a table of `cap` slots (any cap, no pow2 rounding)
 KMZ_HD uint64_t slot_of(uint64_t k, uint64_t cap) { return mulhi64(mix64(k ^ 0x5bd1e9955bd1e995ull), cap); }

@@ -9,7 +9,8 @@
 // counts how many of the other ranks' ids occur among its own span ids.  A
 // nonzero total means the shards are not independent; the caller re-runs
 // unsharded.  For Zipkin's Trace[][] (and the synthetic configs) the lists
-// are empty and nothing is exchanged.
+// are empty and nothing is exchanged.  The other half of the global map's
+// semantics, ids repeated across shards, is checked by routing (below).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -62,6 +63,83 @@ __global__ void __launch_bounds__(256) k_ids_count(const uint64_t *__restrict__ 
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(found, (unsigned long long)c);
+}
+
+// ---- cross-shard repeated span ids ------------------------------------------
+// The reference's span map is global (Traces.ts:117-123): an id that occurs in
+// two shards collapses to one row there.  Each rank routes the id_hash of its
+// span ids to an owner rank (id_owner: a range of the hash
+// space), the ranks exchange them (all-to-all), and each owner runs the
+// uniqueness certificate over what it received (kmz_id_repeats).  Every
+// shard's own ids are unique already (its certificate), so a repeat among the
+// received values is an id shared by two shards.
+//   k_route_hist     per chunk: owner histogram in LDS
+//   k_route_scan     one workgroup: each (chunk, owner)'s output offset
+//   k_route_scatter  per chunk: the hashes to their owner's segment
+constexpr uint32_t RT_T = 256, RT_MAXW = 1024;
+
+__global__ void __launch_bounds__(RT_T) k_route_hist(const uint64_t *__restrict__ sid, uint32_t n, uint32_t chunk,
+                                                     uint32_t world, uint32_t *__restrict__ hist) {
+  __shared__ uint32_t h[RT_MAXW];
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T) h[r] = 0;
+  __syncthreads();
+  const uint32_t b = blockIdx.x * chunk, e = min(n, b + chunk);
+  for (uint32_t i = b + threadIdx.x; i < e; i += RT_T) atomicAdd(&h[id_owner(id_hash(sid[i]), world)], 1u);
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T) hist[(uint64_t)blockIdx.x * world + r] = h[r];
+}
+
+// hist[chunk][owner] -> exclusive output offsets (owner-major); tot[owner] = its count
+__global__ void __launch_bounds__(RT_T) k_route_scan(uint32_t *__restrict__ hist, uint32_t nchunks, uint32_t world,
+                                                     unsigned long long *__restrict__ tot) {
+  __shared__ unsigned long long seg[RT_MAXW];
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T) {
+    unsigned long long a = 0;
+    for (uint32_t c = 0; c < nchunks; ++c) {
+      const uint32_t x = hist[(uint64_t)c * world + r];
+      hist[(uint64_t)c * world + r] = (uint32_t)a;  // (a shard holds < 2^32 spans)
+      a += x;
+    }
+    seg[r] = a;
+    tot[r] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long a = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+      const unsigned long long x = seg[r];
+      seg[r] = a;
+      a += x;
+    }
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T)
+    for (uint32_t c = 0; c < nchunks; ++c) hist[(uint64_t)c * world + r] += (uint32_t)seg[r];
+}
+
+__global__ void __launch_bounds__(RT_T) k_route_scatter(const uint64_t *__restrict__ sid, uint32_t n, uint32_t chunk,
+                                                        uint32_t world, const uint32_t *__restrict__ off,
+                                                        unsigned long long *__restrict__ out) {
+  __shared__ uint32_t cur[RT_MAXW];
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T) cur[r] = off[(uint64_t)blockIdx.x * world + r];
+  __syncthreads();
+  const uint32_t b = blockIdx.x * chunk, e = min(n, b + chunk);
+  for (uint32_t i = b + threadIdx.x; i < e; i += RT_T) {  // (order inside a segment is free: the check is a set test)
+    const uint64_t h = id_hash(sid[i]);
+    out[atomicAdd(&cur[id_owner(h, world)], 1u)] = h;
+  }
+}
+
+uint32_t route_chunks(uint32_t n) { return std::max<uint32_t>(1, std::min<uint32_t>(1024, (n + 4095) / 4096)); }
+
+bool launch_route(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint32_t *hist,
+                  unsigned long long *tot, unsigned long long *out) {
+  if (world == 0 || world > RT_MAXW) return false;
+  const uint32_t g = route_chunks(n), chunk = (n + g - 1) / g;
+  hipLaunchKernelGGL(k_route_hist, dim3(g), dim3(RT_T), 0, s, sid, n, chunk, world, hist);
+  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(RT_T), 0, s, hist, g, world, tot);
+  if (n) hipLaunchKernelGGL(k_route_scatter, dim3(g), dim3(RT_T), 0, s, sid, n, chunk, world, hist, out);
+  return true;
 }
 
 void launch_unresolved(hipStream_t s, const uint64_t *pid, const uint32_t *dp, uint32_t n, unsigned long long *out,

@@ -95,10 +95,7 @@ static_assert(JB == 1024, "bucket indices are the top 10 bits of the 32-bit hash
 // pick the bin and sub-bin, its low bits the check's bucket.  (mix64's second
 // multiply and shifts bought nothing here: one multiply spreads sequential
 // ids over the top bits, the xorshift brings them to the low bits.)  0 -> 0.
-__device__ __forceinline__ uint64_t cert_hash(uint64_t x) {
-  x *= 0x9E3779B97F4A7C15ull;
-  return x ^ (x >> 29);
-}
+__device__ __forceinline__ uint64_t cert_hash(uint64_t x) { return id_hash(x); }  // (kmz_common.h)
 __device__ __forceinline__ uint32_t jfold(uint64_t id) { return (uint32_t)id ^ (uint32_t)(id >> 32); }
 __device__ __forceinline__ uint32_t jb1(uint32_t x) { return (x * 0x9E3779B1u) >> 22; }
 __device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >> 22; }
@@ -389,6 +386,55 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   KMZ_JSTAMP(4);
   if (dbg_t && threadIdx.x == 0)
     for (int kk = 0; kk < 5; ++kk) atomicAdd(&g_join_dbg[kk], tacc[kk]);
+}
+
+// Certificate pass 1 over a plain array of values (no join): the cross-shard
+// repeated-id guard (kmz_guard.hip) checks the routed id hashes it received
+// with the same split + check.  Each value is hashed once more (cert_hash,
+// still a bijection): the routing fixed the top bits of the values a rank
+// receives, and the bins need them uniform.  Same tile-major layout as
+// k_join_window's pass 1 (pool1, jdir).
+__global__ void __launch_bounds__(JTT) k_cert_bin(const unsigned long long *__restrict__ v, uint32_t n,
+                                                  unsigned long long *__restrict__ pool1, uint16_t *__restrict__ jdir) {
+  constexpr uint32_t NW = JTT / 64, PT = JT / JTT;
+  __shared__ uint64_t stg[JT];
+  __shared__ uint32_t wcnt[CERT_BINS * NW], wsum[NW];
+  const uint32_t t0 = blockIdx.x * JT, t1 = min(n, t0 + JT);
+  for (uint32_t e = threadIdx.x; e < CERT_BINS * NW; e += JTT) wcnt[e] = 0;
+  uint64_t hv[PT];
+#pragma unroll
+  for (int q = 0; q < (int)PT; ++q) {
+    const uint32_t i = t0 + q * JTT + threadIdx.x;
+    hv[q] = i < t1 ? cert_hash(v[i]) : 0;
+  }
+  __syncthreads();
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t rk[PT];
+#pragma unroll
+  for (int q = 0; q < (int)PT; ++q) {
+    const bool ok = t0 + q * JTT + threadIdx.x < t1;
+    const uint32_t bin = (uint32_t)(hv[q] >> (64 - CERT_B1));
+    const uint64_t peers = match6(bin, __ballot(ok));
+    uint32_t prior = 0;
+    if (ok) prior = wcnt[bin * NW + w];
+    rk[q] = prior + __popcll(peers & lt);
+    if (ok && (peers & lt) == 0) wcnt[bin * NW + w] = prior + __popcll(peers);
+  }
+  __syncthreads();
+  block_scan_lds(wcnt, CERT_BINS * NW, wsum);
+  if (threadIdx.x < CERT_BINS) jdir[(uint64_t)blockIdx.x * CERT_BINS + threadIdx.x] = (uint16_t)wcnt[threadIdx.x * NW];
+#pragma unroll
+  for (int q = 0; q < (int)PT; ++q)
+    if (t0 + q * JTT + threadIdx.x < t1) stg[wcnt[(uint32_t)(hv[q] >> (64 - CERT_B1)) * NW + w] + rk[q]] = hv[q];
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) pool1[(uint64_t)t0 + e] = stg[e];
+}
+
+void launch_cert_bin(hipStream_t s, const unsigned long long *v, uint32_t n, unsigned long long *pool1,
+                     uint16_t *jdir) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_cert_bin, dim3(join_tiles(n)), dim3(JTT), 0, s, v, n, pool1, jdir);
 }
 
 // pass 2: for one bin, the runs of TPC tiles -> 2^B2 sub-bins (dynamic LDS:

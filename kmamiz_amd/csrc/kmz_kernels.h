@@ -104,7 +104,7 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
                          unsigned long long *bucket, uint64_t bcap, uint32_t *bucket_n,
                          const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
-                         uint32_t gcap);
+                         uint32_t gcap, uint32_t ablate = 0);
 // zero the chain-table entries this run wrote (instead of a memset of the table)
 void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
                         const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);
@@ -113,7 +113,7 @@ void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, cons
                        const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
-                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct);
+                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct, uint32_t ablate = 0);
 // shape-level K3 partials -> endpoint groups / dependency-endpoint records
 void launch_collapse_groups(hipStream_t s, const unsigned long long *sg, uint32_t n_shapes, uint32_t S,
                             const uint32_t *map, uint32_t n_ep, unsigned long long *grp, unsigned int *counters);
@@ -133,6 +133,11 @@ void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned l
 // multi-GPU sharding guard (kmz_guard.hip)
 void launch_unresolved(hipStream_t s, const uint64_t *pid, const uint32_t *dp, uint32_t n, unsigned long long *out,
                        uint64_t cap, unsigned long long *count);
+// cross-shard repeated ids: hashes of the span ids grouped by owner rank;
+// hist [route_chunks(n) * world] u32 scratch, tot [world] counts
+uint32_t route_chunks(uint32_t n);
+bool launch_route(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint32_t *hist,
+                  unsigned long long *tot, unsigned long long *out);
 void launch_ids_count(hipStream_t s, const unsigned long long *ids, uint64_t m, unsigned long long *set, uint64_t cap,
                       const uint64_t *sid, uint32_t n, unsigned long long *found);
 
@@ -162,6 +167,9 @@ void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool
                        const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters);
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
                        const unsigned int *cur2, unsigned int *counters);
+// pass 1 of the certificate over a plain value array (cross-shard id guard)
+void launch_cert_bin(hipStream_t s, const unsigned long long *v, uint32_t n, unsigned long long *pool1,
+                     uint16_t *jdir);
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,
                  unsigned long long *mkey, uint32_t *mval, uint32_t mcap, const unsigned int *counters);
 void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent,

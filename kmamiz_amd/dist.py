@@ -8,6 +8,9 @@ partials then merge with collectives over the default process group:
                     [max timestamp]                                all_reduce MAX
                     [min first index]                              all_reduce MIN
 * endpoint partials [max timestamp] MAX, [min first_row<<1|!external] MIN
+* guards            a fixed-size agreement all-reduce (id tables, sizes), the
+                    unresolved-parent exchange and the cross-shard repeated
+                    span-id check (an all-to-all of hashed ids by owner rank)
 * edge keys         size all_reduce MAX, padded all_gather, then a union:
                     into the engine's own device edge set (kmz_merge_triples,
                     ``merge_edge_keys_into``) or ``torch.unique`` (CPU tensors)
@@ -21,6 +24,9 @@ production, ``gloo`` on CPU tensors in the tests.
 """
 from __future__ import annotations
 
+from typing import Optional
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -63,57 +69,143 @@ def merge_endpoint_partials(e: torch.Tensor, n_ep: int) -> torch.Tensor:
 
 
 def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: torch.Tensor, engine=None,
-              digest: int = 0, group=None):
-    """The whole per-step merge in three collectives (the bench's N > 1 path):
-    one SUM all-reduce of the group moments, one MAX all-reduce that carries
-    every max field and every min field negated (min x = -max -x in signed
-    order) plus the edge-key count and the id-table digest, and one
-    all-gather of the padded keys.  Same results as merge_group_partials +
-    merge_endpoint_partials + merge_edge_keys(_into); returns the merged keys
-    when ``engine`` is None.
+              digest: int = 0, group=None, check_ids: bool = True):
+    """The whole per-step merge: one fixed-size MAX all-reduce that makes the
+    ranks agree (group/endpoint counts, the id-table digest, the unresolved
+    parent count) before any size-dependent collective, the sharding guards,
+    then one SUM all-reduce of the group moments, one MAX all-reduce that
+    carries every max field and every min field negated (min x = -max -x in
+    signed order) plus the edge-key count, and one all-gather of the padded
+    keys.  Same results as merge_group_partials + merge_endpoint_partials +
+    merge_edge_keys(_into); returns the merged keys when ``engine`` is None.
 
     The same collective calls run on device tensors (RCCL) and on CPU tensors
     (gloo), so the CPU tests exercise the production sequence.  ``digest``:
     a digest of the endpoint/status id tables this rank's partials are indexed
-    by (shard.exchange_tables); ranks that disagree raise ShardingError."""
+    by (shard.exchange_tables); ranks that disagree raise ShardingError.
+    ``check_ids`` (with an engine): the cross-shard repeated-span-id guard
+    (check_repeated_ids) before the merge."""
     world = dist.get_world_size(group)
     if world == 1:
         return None if engine is not None else torch.unique(keys)
     G, E = n_groups, n_ep
+    dev = p.device
+    # agreement first: every later collective's size depends on G and E
+    # (ranks that disagree would hang RCCL or fail inside gloo before a clear
+    # error); the sharding guard's count rides along
+    nu = _unresolved(engine) if engine is not None else 0
+    dg = int(digest) & ((1 << 62) - 1)
+    agree = torch.tensor([G, -G, E, -E, dg, -dg, nu, 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(agree, op=dist.ReduceOp.MAX, group=group)
+    a = agree.tolist()
+    if a[0] != -a[1] or a[2] != -a[3] or a[4] != -a[5]:
+        raise ShardingError("ranks merged partials over different endpoint/status id tables "
+                            "(assign global ids with shard.exchange_tables)")
+    if a[6] > 0:
+        _check_shards(engine, nu, int(a[6]), dev, group)
+    if engine is not None and check_ids:
+        check_repeated_ids(engine, dev, group)
     if G:
         dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM, group=group)  # modular: exact for u64
-    dev = p.device
-    # sharding guard: this rank's parent ids that are not in its shard
-    nu = _unresolved(engine) if engine is not None else 0
     ming = p[5 * G : 6 * G]
     mine = e[E : 2 * E]
-    dg = int(digest) & ((1 << 62) - 1)
     mx = torch.cat([
         _as_signed_order(p[4 * G : 5 * G]),
         _as_signed_order(e[:E]),
         -torch.where(ming == -1, torch.full_like(ming, _I64_MAX), ming),
         -torch.where(mine == -1, torch.full_like(mine, _I64_MAX), mine),
-        torch.tensor([nu, keys.numel(), dg, -dg, G, -G, E, -E], dtype=torch.int64, device=dev),
+        torch.tensor([keys.numel()], dtype=torch.int64, device=dev),
     ])
     dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-    tail = mx[-8:].tolist()
-    if tail[2] != -tail[3] or tail[4] != -tail[5] or tail[6] != -tail[7]:
-        raise ShardingError("ranks merged partials over different endpoint/status id tables "
-                            "(assign global ids with shard.exchange_tables)")
-    if tail[0] > 0:
-        _check_shards(engine, nu, int(tail[0]), dev, group)
+    nk = int(mx[-1].item())
     p[4 * G : 5 * G] = _as_signed_order(mx[:G])
     e[:E] = _as_signed_order(mx[G : G + E])
     fg = -mx[G + E : 2 * G + E]
     fe = -mx[2 * G + E : 2 * G + 2 * E]
     p[5 * G : 6 * G] = torch.where(fg == _I64_MAX, torch.full_like(fg, -1), fg)
     e[E : 2 * E] = torch.where(fe == _I64_MAX, torch.full_like(fe, -1), fe)
-    allk = _gather_padded(keys, int(tail[1]), world, group)
+    allk = _gather_padded(keys, nk, world, group)
     if engine is not None:
         engine.merge_triples(allk.data_ptr(), allk.numel(), keys.is_cuda)
         return None
     u = torch.unique(allk)
     return u[u != 0]
+
+
+# ---- cross-shard repeated span ids -------------------------------------------
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def id_hash_np(ids: np.ndarray) -> np.ndarray:
+    """kmz_common.h id_hash (the certificate's bijection) over uint64 ids."""
+    with np.errstate(over="ignore"):
+        x = ids.astype(np.uint64) * _GOLD
+    return x ^ (x >> np.uint64(29))
+
+
+def id_owner_np(h: np.ndarray, world: int) -> np.ndarray:
+    """kmz_common.h id_owner: the owner rank of each hashed id."""
+    return ((h >> np.uint64(32)) * np.uint64(world)) >> np.uint64(32)
+
+
+def route_ids_np(span_ids: np.ndarray, world: int):
+    """Host mirror of kmz_route_ids: (hashes grouped by owner, counts)."""
+    h = id_hash_np(np.asarray(span_ids, dtype=np.uint64))
+    own = id_owner_np(h, world).astype(np.int64)
+    order = np.argsort(own, kind="stable")
+    return h[order], np.bincount(own, minlength=world).astype(np.int64)
+
+
+def check_repeated_ids(engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None) -> None:
+    """Raise ShardingError if a span id occurs in two shards.
+
+    The reference keys one Map by span id over the whole batch
+    (Traces.ts:117-123): an id seen twice is one row (its last value at its
+    first position), which per-shard runs cannot reproduce when the two
+    occurrences sit in different shards.  Each rank routes the hashes of its
+    span ids (a bijection: equal hashes are equal ids) to the rank that owns
+    that hash range (kmz_route_ids), one all-to-all delivers them, and each
+    owner runs the uniqueness certificate over what it received
+    (kmz_id_repeats); a shard's own ids are unique already (its own
+    certificate, or the span-table path that _unresolved refuses).  Cost per
+    span: 8 bytes over the all-to-all and ~40 bytes of HBM traffic on its
+    owner.  ``span_ids`` (no engine): the same protocol on the host (numpy
+    hashes, a sort for the check), for CPU tensors under gloo."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    if engine is not None:
+        # device tensors under RCCL; host tensors under gloo (its all-to-all is CPU-only)
+        on_dev = dev is not None and torch.device(dev).type == "cuda" and dist.get_backend(group) == "nccl"
+        n = int(engine.n)
+        send = torch.empty(max(1, n), dtype=torch.int64, device=dev if on_dev else "cpu")
+        counts = engine.route_ids(world, send.data_ptr(), n, on_dev)
+        send = send[:n]
+    else:
+        h, c = route_ids_np(span_ids, world)
+        send = torch.from_numpy(h.view(np.int64).copy())
+        counts = c.tolist()
+        on_dev = False
+    cdev = send.device
+    cnt = torch.tensor(counts, dtype=torch.int64, device=cdev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rc = rcnt.tolist()
+    recv = torch.empty(max(1, sum(rc)), dtype=torch.int64, device=cdev)
+    dist.all_to_all_single(recv[: sum(rc)], send, output_split_sizes=rc, input_split_sizes=counts, group=group)
+    recv = recv[: sum(rc)]
+    if on_dev:
+        torch.cuda.current_stream(cdev).synchronize()  # (the engine's stream may not be torch's)
+    rep = None
+    if engine is not None and recv.numel():
+        rep = engine.id_repeats(recv.data_ptr(), recv.numel(), on_dev)
+    if rep is None:  # host check (no engine, or the certificate could not decide)
+        rep = bool(recv.numel()) and torch.unique(recv).numel() != recv.numel()
+    flag = torch.tensor([1 if rep else 0], dtype=torch.int64, device=cdev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        raise ShardingError("a span id occurs in two shards: the reference's global span map would merge them "
+                            "(Traces.ts:117-123); run unsharded")
 
 
 def _gather_padded(x: torch.Tensor, m: int, world: int, group=None) -> torch.Tensor:

@@ -153,6 +153,7 @@ class Engine:
         ``ptr`` + ``length`` (host memory, e.g. pinned, or device memory with
         device=True).  -> (n_spans, n_shapes, n_statuses), or None outside the
         fast path (nothing loaded: parse on the host)."""
+        self.gen += 1  # kmz_json_parse overwrites the columns and drops the last run, even on E_UNSUPPORTED
         n, ns, nt = C.c_uint64(), C.c_uint32(), C.c_uint32()
         if ptr is None:
             buf = data if isinstance(data, bytes) else bytes(data)
@@ -233,6 +234,7 @@ class Engine:
     def set_index_map(self, local_start: np.ndarray, global_start: np.ndarray):
         """Local -> global flatten-index runs of a non-contiguous shard
         (kmz_set_index_map): results then report global indices."""
+        self.gen += 1  # (clears the last run)
         ls = np.ascontiguousarray(local_start, dtype=np.uint64)
         gs = np.ascontiguousarray(global_start, dtype=np.uint64)
         if len(ls) != len(gs):
@@ -368,6 +370,25 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_count_ids(self.ctx, C.c_void_p(src_ptr) if n else None, n,
                                                   L.MEM_DEVICE if device else L.MEM_HOST, C.byref(f)))
         return f.value
+
+    def route_ids(self, world: int, dst_ptr: int, cap: int, device: bool) -> list:
+        """This batch's span ids, hashed (the certificate's bijection) and
+        grouped by owner rank (kmz_route_ids) into dst; -> counts per rank."""
+        counts = np.zeros(max(1, world), np.uint64)
+        L.check(self.ctx, self._lib.kmz_route_ids(self.ctx, world, C.c_void_p(dst_ptr) if dst_ptr else None, cap,
+                                                  L.MEM_DEVICE if device else L.MEM_HOST, L.ptr(counts)))
+        return [int(x) for x in counts[:world]]
+
+    def id_repeats(self, src_ptr: int, n: int, device: bool) -> Optional[bool]:
+        """Whether any of the n routed values occurs twice (kmz_id_repeats);
+        None when the certificate cannot decide (the caller checks another way)."""
+        r = C.c_uint32()
+        rc = self._lib.kmz_id_repeats(self.ctx, C.c_void_p(src_ptr) if n else None, n,
+                                      L.MEM_DEVICE if device else L.MEM_HOST, C.byref(r))
+        if rc == L.E_UNSUPPORTED:
+            return None
+        L.check(self.ctx, rc)
+        return bool(r.value)
 
     # ---- profiling -------------------------------------------------------------
     def set_profiling(self, on: bool):

@@ -22,6 +22,33 @@ def _to_precise(x: float) -> float:
     return float(r) / 1e14
 
 
+# JS number semantics the reference's arithmetic relies on: Math.max/min
+# propagate NaN (and give -/+Infinity on no arguments), `x || d` replaces 0 and
+# NaN, and a division by zero gives NaN or +-Infinity instead of raising.
+def _js_max(inp) -> float:
+    if any(math.isnan(v) for v in inp):
+        return math.nan
+    return max(inp) if inp else -math.inf
+
+
+def _js_min(inp) -> float:
+    if any(math.isnan(v) for v in inp):
+        return math.nan
+    return min(inp) if inp else math.inf
+
+
+def _js_or(v, default):
+    return default if v is None or v == 0 or (isinstance(v, float) and math.isnan(v)) else v
+
+
+def _js_div(a: float, b: float) -> float:
+    if b != 0:
+        return a / b
+    if a == 0 or math.isnan(a):
+        return math.nan
+    return math.copysign(math.inf, a) * math.copysign(1.0, b)
+
+
 class Normalizer:
     """Normalizer.ts:17-70."""
 
@@ -32,8 +59,7 @@ class Normalizer:
     class Strategy:
         @staticmethod
         def BetweenFixedNumber(inp):
-            hi = max(inp) if inp else -math.inf
-            lo = min(inp) if inp else math.inf
+            hi, lo = _js_max(inp), _js_min(inp)
             if hi - lo == 0:
                 return [0.1]  # Normalizer.ts:22, a single element, as in the TS
             return [((v - lo) / (hi - lo)) * 0.9 + 0.1 for v in inp]
@@ -49,8 +75,8 @@ class Normalizer:
 
         @staticmethod
         def FixedRatio(inp):
-            hi = max(inp) if inp else -math.inf
-            return inp if hi == 0 else [v / hi for v in inp]
+            hi = _js_max(inp)
+            return inp if hi == 0 else [_js_div(v, hi) for v in inp]
 
         @staticmethod
         def Linear(inp, minimum=0.1):
@@ -180,7 +206,7 @@ def probability(data: List[dict]) -> List[dict]:
         a[0] += d["latency"]["cv"] * d["combined"]
         a[1] += d["combined"]
     rel_names = list(cv)
-    rel_norm = Normalizer.Strategy.SigmoidAdj([cv[k][0] / cv[k][1] if cv[k][1] else math.nan for k in rel_names])
+    rel_norm = Normalizer.Strategy.SigmoidAdj([_js_div(cv[k][0], cv[k][1]) for k in rel_names])
     # invoke probability and 5xx error rate (171-213)
     cnt: Dict[str, List[int]] = {}
     for d in data:
@@ -191,8 +217,8 @@ def probability(data: List[dict]) -> List[dict]:
     for v in cnt.values():
         total += v[0]
     names = list(cnt)
-    npro = [(cnt[k][0] / total) * (1 - MINIMUM_PROB) + MINIMUM_PROB for k in names]
-    nerr = [(cnt[k][1] / cnt[k][0]) * (1 - MINIMUM_PROB) + MINIMUM_PROB for k in names]
+    npro = [_js_div(cnt[k][0], total) * (1 - MINIMUM_PROB) + MINIMUM_PROB for k in names]
+    nerr = [_js_div(cnt[k][1], cnt[k][0]) * (1 - MINIMUM_PROB) + MINIMUM_PROB for k in names]
     base = Normalizer.Strategy.Linear([p * nerr[i] for i, p in enumerate(npro)], MINIMUM_PROB)
     base_of = dict(zip(names, base))
     out = []
@@ -214,8 +240,8 @@ def realtime_risk(data: List[dict], service_deps: List[dict], replicas: List[dic
     risks = []
     for usn in dict.fromkeys(d["uniqueServiceName"] for d in data):
         s, n, v = (usn.split("\t") + [None] * 3)[:3]
-        i = imp.get(usn) or 0
-        p = prob.get(usn) or MINIMUM_PROB
+        i = _js_or(imp.get(usn), 0)
+        p = _js_or(prob.get(usn), MINIMUM_PROB)
         risks.append(
             {"uniqueServiceName": usn, "service": s, "namespace": n, "version": v, "risk": i * p, "impact": i,
              "probability": p}

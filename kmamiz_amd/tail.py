@@ -310,17 +310,16 @@ class ServiceTail:
 
 # -- risk over column arrays (RiskAnalyzer.ts:10-122, 171-248) -------------------
 def _js_max(a: np.ndarray) -> float:
-    """Math.max / Python max over a list: numpy's when no NaN is present (the
-    same value), the builtin's left-to-right rule otherwise."""
+    """Math.max(...a): NaN if any element is NaN, -Infinity for no elements."""
     if not len(a):
         return -math.inf
-    return float(a.max()) if not np.isnan(a).any() else max(a.tolist())
+    return float(a.max())  # (numpy's max propagates NaN, as Math.max does)
 
 
 def _js_min(a: np.ndarray) -> float:
     if not len(a):
         return math.inf
-    return float(a.min()) if not np.isnan(a).any() else min(a.tolist())
+    return float(a.min())
 
 
 def _fixed_ratio(a: np.ndarray) -> np.ndarray:
@@ -450,7 +449,8 @@ def realtime_risk_from_sums(tail: ServiceTail, sid_names: Sequence[str], order_i
     code_pos[by_code] = np.arange(len(by_code))
     at_sid = code_pos[cache[key][1][order_ids]]  # (index -1 -> the sentinel: `imp.get(usn) || 0` below)
     im = np.where(at_sid >= 0, ni[np.maximum(at_sid, 0)] if len(ni) else 0.0, 0.0)
-    p = np.where(prob == 0, MP, prob)  # `probability || MINIMUM_PROB`
+    im = np.where(np.isnan(im), 0.0, im)  # `impact || 0` (NaN is falsy)
+    p = np.where((prob == 0) | np.isnan(prob), MP, prob)  # `probability || MINIMUM_PROB`
     risk = im * p
     hi, lo = _js_max(risk), _js_min(risk)
     norm = np.array([0.1]) if hi - lo == 0 else ((risk - lo) / (hi - lo)) * 0.9 + 0.1

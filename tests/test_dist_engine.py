@@ -157,6 +157,70 @@ def test_cross_shard_parent_is_refused():
     assert res[1] == (1, 1, "refused"), res
 
 
+def _repeat_worker(rank, world, port, q, repeat):
+    """The last rank's batch reuses one span id of rank 0's shard (a leaf
+    SERVER span, so no parent link crosses shards)."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kmamiz_amd import Engine
+        from kmamiz_amd import _lib as L
+        from kmamiz_amd import dist as kdist
+        from kmamiz_amd import synth
+
+        ntr = 900
+        cut = [ntr * r // world for r in range(world + 1)]
+        table = synth.shape_table(synth.MESH)
+        b0, _ = synth.host_batch(synth.MESH, 0, 1)
+        batch, _ = synth.host_batch(synth.MESH, cut[rank], cut[rank + 1])
+        if repeat and rank == world - 1:
+            kids = set(batch.parent_id.tolist())
+            leaf = next(i for i in range(len(batch)) if batch.kind[i] == 1 and int(batch.span_id[i]) not in kids)
+            batch.span_id[leaf] = b0.span_id[len(b0) - 1]
+        e = Engine(0)
+        e.load(batch, table)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        gw, ew, tw = (e.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
+        g = torch.zeros(gw, dtype=torch.int64)
+        ep = torch.zeros(ew, dtype=torch.int64)
+        t = torch.zeros(max(1, tw), dtype=torch.int64)
+        e.export_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
+        e.export_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
+        e.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, False)
+        try:
+            kdist.merge_all(g, gw // 6, ep, ew // 2, t[:tw], engine=e)
+            q.put((rank, "merged"))
+        except kdist.ShardingError:
+            q.put((rank, "refused"))
+        e.close()
+    except Exception as ex:  # surfaced by the parent
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_cross_shard_repeated_span_id_is_refused(world):
+    """SURVEY.md 8e's global duplicate check: a span id present in two shards
+    (Traces.ts:117-123 keeps one row for it) makes merge_all refuse on every
+    rank; the same shards without the repeat merge."""
+    for repeat, want in ((False, "merged"), (True, "refused")):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _port()
+        ps = [ctx.Process(target=_repeat_worker, args=(r, world, port, q, repeat)) for r in range(world)]
+        for p in ps:
+            p.start()
+        res = sorted(q.get(timeout=180) for _ in range(world))
+        for p in ps:
+            p.join(timeout=60)
+        assert [r[1] for r in res] == [want] * world, res
+
+
 # ---------------------------------------------------------------------------
 # traceId sharding with different JSON shards (SURVEY.md 8e, config 4's merge)
 # ---------------------------------------------------------------------------

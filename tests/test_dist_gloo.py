@@ -132,3 +132,84 @@ def test_two_rank_merge_equals_single_batch():
         p.join(300)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=10) is True
+
+
+# ---------------------------------------------------------------------------
+# sharding guards: ids repeated across shards, and
+# ranks that disagree on the partials' sizes
+# ---------------------------------------------------------------------------
+def _guard_worker(rank, world, port, q, case):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kmamiz_amd import dist as kdist
+        from kmamiz_amd import synth
+
+        ntr = 300
+        cut = [ntr * r // world for r in range(world + 1)]
+        batch, _ = synth.host_batch(synth.MESH, cut[rank], cut[rank + 1])
+        ids = batch.span_id.copy()
+        if case == "repeat" and rank == world - 1:
+            first, _ = synth.host_batch(synth.MESH, 0, 1)
+            ids[len(ids) // 2] = first.span_id[1]  # one id of rank 0's shard, far from it here
+        if case in ("clean", "repeat"):
+            try:
+                kdist.check_repeated_ids(span_ids=ids)
+                q.put((rank, "passed"))
+            except kdist.ShardingError:
+                q.put((rank, "refused"))
+        else:  # "sizes": rank 1 holds one group more -- refused before any size-dependent collective
+            G = 3 + (rank == 1)
+            p = torch.zeros(6 * G, dtype=torch.int64)
+            e = torch.zeros(4, dtype=torch.int64)
+            k = torch.ones(2, dtype=torch.int64)
+            try:
+                kdist.merge_all(p, G, e, 2, k)
+                q.put((rank, "merged"))
+            except kdist.ShardingError:
+                q.put((rank, "refused"))
+    except Exception as ex:  # surfaced by the parent
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_guard(world, case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_guard_worker, args=(r, world, port, q, case)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    return [r[1] for r in res]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_span_id_repeated_across_shards_is_refused(world):
+    """The reference's span map is global (Traces.ts:117-123): one id in two
+    shards is one row there.  Routing the hashed ids to their owner rank and
+    checking each owner's values finds it on every rank; a clean batch passes."""
+    assert _run_guard(world, "clean") == ["passed"] * world
+    assert _run_guard(world, "repeat") == ["refused"] * world
+
+
+def test_ranks_with_different_sizes_are_refused():
+    assert _run_guard(2, "sizes") == ["refused"] * 2
+
+
+def test_route_ids_np_partitions_by_owner():
+    from kmamiz_amd import dist as kdist
+
+    rng = np.random.default_rng(7)
+    ids = rng.integers(1, 2**63, size=5000, dtype=np.uint64)
+    for world in (1, 2, 3, 8):
+        h, c = kdist.route_ids_np(ids, world)
+        assert c.sum() == len(ids) and len(c) == world
+        own = kdist.id_owner_np(h, world)
+        assert np.all(np.diff(own.astype(np.int64)) >= 0)  # grouped by owner, in rank order
+        assert np.array_equal(np.sort(h), np.sort(kdist.id_hash_np(ids)))
+    # id_hash is a bijection: distinct ids give distinct hashes
+    assert len(np.unique(kdist.id_hash_np(np.arange(1, 100001, dtype=np.uint64)))) == 100000

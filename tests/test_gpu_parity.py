@@ -469,6 +469,50 @@ def test_sig_collision_is_detected_and_retried(engine):
     assert _info_results(a[2]) == _info_results(b[2])
 
 
+SPIN_TINY_DEFER = 1 << 10  # KMZ_ABLATE: 4 deferred chain checks per workgroup (in-place chain_put waits)
+SPIN_NO_WAIT = 1 << 11     # KMZ_ABLATE: every chain-table wait "runs out" at once (F_SPIN)
+FORCE_INTERNING = 1 << 29  # KMZ_ABLATE: K4 chain interning even where auto mode would enumerate
+
+
+@pytest.mark.parametrize("knob", [SPIN_TINY_DEFER, SPIN_NO_WAIT, SPIN_TINY_DEFER | SPIN_NO_WAIT])
+def test_chain_waits_never_drop_results(knob):
+    """The chain-table waits of kmz_chain.hip (a leader whose workgroup's
+    deferred list is full, k_chain_settle's deferred checks, k4_chain_pend)
+    on config 5 with chain interning, where a fresh table makes workgroups
+    race on the same new chains.  A tiny deferred list forces the in-place
+    waits that once hung config 5; a zero wait bound makes every wait run out,
+    which must raise F_SPIN and redo the run on the exact walk (path bit 3),
+    never drop a row, an ancestor's timestamp or a check.  Both equal the C
+    oracle (Traces.ts:128-143, 192-208)."""
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(5, 0, 20000)
+    table = synth.shape_table(5)
+    odeps = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    e = _engine_with(knob | FORCE_INTERNING)
+    try:
+        for run in range(2):  # a fresh chain table, then a cleared one
+            info = _compare_synth(e, batch, table, odeps)
+            if knob & SPIN_NO_WAIT and run == 0:
+                assert info["path"] & 8, "no chain-table wait ran out: the knob did not reach the waits"
+            if not knob & SPIN_NO_WAIT:
+                assert not info["path"] & 8  # (the waits finish normally)
+    finally:
+        e.close()
+
+
+def test_spin_exhaustion_on_the_pending_path():
+    """A 300-deep chain always takes k4_chain_pend, whose chain_put wait runs
+    out at once under the zero bound: F_SPIN, and the exact walk gives the
+    oracle's order-exact rows."""
+    e = _engine_with(SPIN_NO_WAIT | FORCE_INTERNING)
+    try:
+        test_deep_chain_takes_the_pending_path(e)
+        assert e.info()["path"] & 8
+    finally:
+        e.close()
+
+
 def test_deep_chain_takes_the_pending_path(engine):
     """A 300-deep SERVER/CLIENT chain is deeper than the LDS window and
     WIN_DEPTH: its spans hash over the global contracted parents."""

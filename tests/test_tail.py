@@ -8,6 +8,8 @@ form ``EndpointDependencies([]).combineWith(deps).trim()``
 * GPU: the kernel through the C ABI, on the reference fixtures, synthetic
   configs 2/3/5, with and without a label map.
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -236,3 +238,50 @@ def test_service_sums_grid_equals_row_sums():
     assert np.array_equal(a[0], b[0])
     assert np.array_equal(a[2], b[2]) and np.array_equal(a[3], b[3])
     np.testing.assert_allclose(a[1], b[1], rtol=1e-12)
+
+
+def _same(a, b):
+    if isinstance(a, float) and isinstance(b, float) and math.isnan(a) and math.isnan(b):
+        return True
+    return a == pytest.approx(b, rel=REL, abs=1e-15)
+
+
+def test_risk_with_a_zero_count_service_follows_js():
+    """A service whose combined rows all count 0: its latency CV metric and
+    error rate are 0/0 = NaN in JS, Math.max/Math.min then give NaN, and
+    `probability || MINIMUM_PROB` / `impact || 0` replace NaN
+    (RiskAnalyzer.ts:10-49, 87-122; Normalizer.ts:17-64).  Both host paths
+    (row dicts in risk.py, columns in tail.py) equal the oracle."""
+    import math as _m  # noqa: F401
+
+    from kmamiz_amd import risk as R
+    from kmamiz_amd import synth
+    from kmamiz_amd.tail import maps_for_synth, realtime_risk_arrays
+    from oracle import c_oracle
+
+    batch, off = synth.host_batch(5, 0, 150)
+    table = synth.shape_table(5)
+    keys, oep, _ = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    first = np.where(oep["has_row"], oep["first"], np.iinfo(np.uint64).max).astype(np.uint64)
+    tail = _tail_np(keys, maps_for_synth(5), oep["has_row"], first)
+    od, data, _ = _oracle(synth.to_traces(5, batch, off))
+    zero = data[len(data) // 2]["uniqueServiceName"]
+    data = [dict(d, combined=0) if d["uniqueServiceName"] == zero else d for d in data]
+    sdeps = od.toServiceDependencies()
+    exp = O.strip_undef(O.RiskAnalyzer.RealtimeRisk(data, sdeps, []))
+    assert any(isinstance(e["risk"], float) and math.isnan(e["risk"]) for e in exp) or any(
+        e["uniqueServiceName"] == zero for e in exp)
+    got_rows = R.realtime_risk(data, sdeps, [])
+    names = list(dict.fromkeys(d["uniqueServiceName"] for d in data))
+    ids = {u: i for i, u in enumerate(names)}
+    got_cols = realtime_risk_arrays(tail, np.array([ids[d["uniqueServiceName"]] for d in data]), names,
+                                    np.array([d["combined"] for d in data]),
+                                    np.array([d["latency"]["cv"] for d in data]),
+                                    np.array([str(d["status"]).startswith("5") for d in data]))
+    for got in (got_rows, got_cols):
+        assert [r["uniqueServiceName"] for r in got] == [r["uniqueServiceName"] for r in exp]
+        for g, e in zip(got, exp):
+            for k in ("risk", "impact", "probability", "norm"):
+                assert (k in g) == (k in e), k
+                if k in g:
+                    assert _same(g[k], e[k]), (k, g[k], e[k])
