@@ -47,3 +47,21 @@ def test_id_repeats_finds_one_repeat(engine, m):
     d = torch.from_numpy(w.view(np.int64)).cuda()
     torch.cuda.synchronize()
     assert engine.id_repeats(d.data_ptr(), m, True) is True
+
+
+def test_id_repeats_past_1e8_values(engine):
+    """1.5e8 values: the certificate's split runs in rounds (2^10 sub-bins,
+    k_cert_split_r); distinct values pass, one repeat is found."""
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(synth.MESH, 0, 20)
+    engine.load(batch, synth.shape_table(synth.MESH))
+    m = 150_000_000
+    v = torch.arange(1, m + 1, dtype=torch.int64, device="cuda") * 0x2545F4914F6CDD1D  # odd: distinct mod 2^64
+    torch.cuda.synchronize()
+    assert engine.id_repeats(v.data_ptr(), m, True) is False
+    v[m - 7] = v[12345]
+    torch.cuda.synchronize()
+    assert engine.id_repeats(v.data_ptr(), m, True) is True
+    del v
+    torch.cuda.empty_cache()

@@ -502,15 +502,45 @@ def test_chain_waits_never_drop_results(knob):
 
 
 def test_spin_exhaustion_on_the_pending_path():
-    """A 300-deep chain always takes k4_chain_pend, whose chain_put wait runs
-    out at once under the zero bound: F_SPIN, and the exact walk gives the
-    oracle's order-exact rows."""
+    """A 300-deep chain (unique ids: the window join and k4_chain) always
+    takes k4_chain_pend, whose chain_put wait runs out at once under the zero
+    bound: F_SPIN, and the exact walk gives the oracle's order-exact rows."""
+    from kmamiz_amd import Traces
+
+    front = [_deep_span(100000, "SERVER", None, "front")]
+    deep = _deep_trace(300)
     e = _engine_with(SPIN_NO_WAIT | FORCE_INTERNING)
     try:
-        test_deep_chain_takes_the_pending_path(e)
-        assert e.info()["path"] & 8
+        got = Traces([front, deep], engine=e).toEndpointDependencies().toJSON()
+        info = e.info()
+        assert info["path"] & 1 and info["path"] & 8, info["path"]
     finally:
         e.close()
+    assert got == O.strip_undef(O.Traces([front, deep]).toEndpointDependencies(max_depth=10000).toJSON())
+
+
+def _deep_span(i, kind, parent, svc):
+    tags = {"http.url": f"http://{svc}/x", "http.method": "GET", "istio.canonical_revision": "v1",
+            "http.status_code": "200"}
+    d = {"id": f"{i + 1:016x}", "kind": kind, "name": f"{svc}.ns.svc.cluster.local:80/x", "timestamp": 1000 + i,
+         "duration": 10 + i % 7, "tags": tags}
+    if parent is not None:
+        d["parentId"] = f"{parent + 1:016x}"
+    return d
+
+
+def _deep_trace(levels):
+    trace, prev, i = [], None, 0
+    for level in range(levels):
+        svc = f"s{level % 5}"
+        if prev is not None:
+            trace.append(_deep_span(i, "CLIENT", prev, svc))
+            i += 1
+            prev = i - 1
+        trace.append(_deep_span(i, "SERVER", prev, svc))
+        prev = i
+        i += 1
+    return trace
 
 
 def test_deep_chain_takes_the_pending_path(engine):
@@ -966,6 +996,65 @@ def test_headline_size_config3_properties(engine):
     assert finalize_host(g, G).tobytes() == g1.tobytes()
     assert np.array_equal(e[E:] >> np.uint64(1), np.where(e1["has_row"] == 1, e1["first_row"], e[E:] >> np.uint64(1)))
     assert np.array_equal(np.union1d(ka, kb), k1)
+
+
+def test_config4_size_on_one_gpu():
+    """Config 4's whole batch (1e9 mesh spans, 35 GB of columns) on one GPU:
+    one pass, then the same traces as 8 traceId shards (kmz_synth_load_shard,
+    SURVEY.md 8e: shard = h(traceId) mod 8) merged with merge_all's
+    arithmetic (sums of the integer moments, max timestamps, min first
+    indices, the union of the edge keys).  Groups, endpoints and edge keys
+    must be bit-identical; every SERVER span is one row and one group member
+    (the bulk batch of Initializer.ts:40-101, at 10^4 x its 10^5 traces)."""
+    from kmamiz_amd import Engine, finalize_host
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    ntr = 36578450  # bench.py --spans 1e9
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS
+    eng = Engine(0)
+    try:
+        n = eng.load_synthetic(3, synth.SEED, 0, ntr)
+        assert n > 9.9e8
+        eng.run(flags)
+        i1 = eng.info()
+        g1, k1, e1 = (x.copy() for x in eng.fetch())
+        k1.sort()
+        assert int(g1["combined"].sum()) == i1["n_server"] == i1["n_rows"]
+        assert i1["n_dups"] == 0 and i1["max_depth"] == 7 and i1["path"] & 3 == 3
+        assert np.all(e1["first_row"][e1["has_row"] == 1] < n)
+        G = len(g1)
+        world = 8
+        acc = None
+        keys = []
+        n_sum = 0
+        for rank in range(world):
+            n_sum += eng.load_synthetic_shard(3, synth.SEED, 0, ntr, world, rank)
+            eng.run(flags)
+            gw, ew, tw = (eng.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
+            g, e, k = np.zeros(gw, np.uint64), np.zeros(ew, np.uint64), np.zeros(max(1, tw), np.uint64)
+            eng.export_partials(L.PART_GROUPS, g.ctypes.data, gw, False)
+            eng.export_partials(L.PART_ENDPOINTS, e.ctypes.data, ew, False)
+            eng.export_partials(L.PART_TRIPLES, k.ctypes.data, tw, False)
+            keys.append(k[:tw])
+            if acc is None:
+                acc = [g, e]
+                continue
+            ga, ea = acc
+            E = len(ea) // 2
+            acc = [np.concatenate([ga[:4 * G] + g[:4 * G], np.maximum(ga[4 * G:5 * G], g[4 * G:5 * G]),
+                                   np.minimum(ga[5 * G:], g[5 * G:])]),
+                   np.concatenate([np.maximum(ea[:E], e[:E]), np.minimum(ea[E:], e[E:])])]
+    finally:
+        eng.close()
+    assert n_sum == n
+    g, e = acc
+    E = len(e) // 2
+    assert finalize_host(g, G).tobytes() == g1.tobytes()
+    assert np.array_equal(e[E:] >> np.uint64(1), np.where(e1["has_row"] == 1, e1["first_row"], e[E:] >> np.uint64(1)))
+    assert np.array_equal((e[:E] ^ np.uint64(1 << 63)).view(np.int64)[e1["has_row"] == 1],
+                          e1["last_ts"][e1["has_row"] == 1])
+    assert np.array_equal(np.unique(np.concatenate(keys)), k1)
 
 
 def test_headline_config5_vs_c_oracle_and_tail():

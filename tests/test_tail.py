@@ -285,3 +285,25 @@ def test_risk_with_a_zero_count_service_follows_js():
                 assert (k in g) == (k in e), k
                 if k in g:
                     assert _same(g[k], e[k]), (k, g[k], e[k])
+
+
+@pytest.mark.gpu
+def test_service_tail_after_a_json_parse_on_the_engine(engine):
+    """kmz_json_parse overwrites the engine's columns and drops its run (also
+    when it refuses the input); service_tail() must notice (Engine.gen) and
+    run the dependency pass again instead of failing with KMZ_E_STATE."""
+    import json
+
+    from kmamiz_amd import Traces, synth
+
+    batch, off = synth.host_batch(3, 0, 300)
+    traces = synth.to_traces(3, batch, off)
+    deps = Traces(traces, engine=engine).toEndpointDependencies()
+    a = deps.service_tail()
+    other, ooff = synth.host_batch(2, 0, 50)
+    engine.json_parse(json.dumps(synth.to_traces(2, other, ooff)).encode())
+    b = deps.service_tail()
+    assert a.instability() == b.instability() and a.coupling() == b.coupling()
+    engine.json_parse(b"not json")  # refused (E_UNSUPPORTED): still a new generation
+    c = deps.service_tail()
+    assert a.instability() == c.instability()
