@@ -22,6 +22,7 @@
  */
 const path = require("path");
 const addon = require(path.join(__dirname, "kmz.node"));
+const cache = require(path.join(__dirname, "kmz_cache"));
 
 const KIND_SERVER = 1;
 const KIND_CLIENT = 2;
@@ -225,6 +226,7 @@ function identities(shapes, statuses) {
     statuses,
     ident,
     poison,
+    epNames,
   };
 }
 
@@ -476,6 +478,24 @@ class NativeTraces {
       };
     });
   }
+  // EndpointDependencies([]).combineWith(this.toEndpointDependencies()).trim()
+  // as cache columns (kmz_cache.ReducedDependencies), from the engine's entry
+  // order (kmz_get_dep_entries): no object per row or entry.  `reg`: the
+  // registry of the cache it will merge into (RealtimeWorkerImpl.ts:67-70).
+  toReducedDependencies(reg) {
+    const b = this._batch();
+    const ctx = this._engine();
+    addon.run(ctx, addon.RUN_DEPS | addon.RUN_DEP_ORDER);
+    const E = b.shapesTable.n_dep_ep;
+    const dep = addon.depEntries(ctx, E);
+    const ep = addon.endpoints(ctx, E);
+    const shapeFields = (sh) => {
+      const f = b.ident.dep[sh];
+      if (!f) throw b.poison.dep.get(b.shapesTable.dep_ep[sh]);
+      return f;
+    };
+    return cache.ReducedDependencies.fromWindow(dep, ep, b.epNames.dep, shapeFields, reg);
+  }
   static ToEndpointInfo(trace) {
     const tags = trace.tags || {};
     const key = [trace.name].concat(SHAPE_TAGS.map((k) => tags[k]));
@@ -643,6 +663,25 @@ class NativeRealtimeDataList {
     }
     return out;
   }
+  // toCombinedRealtimeData() as cache columns (kmz_cache.CombinedColumns)
+  // straight from the engine's groups; the no-log case (no content types or
+  // bodies) without replicas (avgReplica is not kept by combineWith).  `like`:
+  // the cache state whose tables it shares.
+  toCombinedColumns(like) {
+    if (this._logs) throw new Error("toCombinedColumns: Envoy logs need toCombinedRealtimeData()");
+    const b = this._t._batch();
+    const ctx = this._t._engine();
+    addon.run(ctx, this._rule === "rt" ? addon.RUN_STATS_RT : addon.RUN_STATS_TAG);
+    const epOf = b.shapesTable[this._rule + "_ep"];
+    const shapeOf = new Map();
+    for (let sh = 0; sh < epOf.length; sh++) if (!shapeOf.has(epOf[sh])) shapeOf.set(epOf[sh], sh);
+    const fields = (e) => {
+      const f = b.ident[this._rule][shapeOf.get(e)];
+      if (!f) throw b.poison[this._rule].get(e);
+      return f;
+    };
+    return cache.CombinedColumns.fromGroups(addon.groups(ctx), b.shapesTable.n_status, fields, b.statuses, like);
+  }
   toCombinedRealtimeData() {
     const b = this._t._batch();
     const ctx = this._t._engine();
@@ -719,5 +758,8 @@ class NativeRealtimeDataList {
   }
 }
 
+// the cache layer's merges, with the reference's Utils.Merge / ObjectToInterfaceString for bodies
+const newCombinedCache = (init) => new cache.CCombinedRealtimeData(init, mergeValues, objectToInterfaceString);
+
 module.exports = { NativeTraces, NativeRealtimeDataList, explodeUrl, ingest, ingestJSON, addon, mergeStringBody,
-                   objectToInterfaceString };
+                   objectToInterfaceString, mergeValues, cache, newCombinedCache };

@@ -247,6 +247,39 @@ static napi_value js_triples(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* depEntries(ctx, n_dep) -> {entries: ArrayBuffer of kmz_dep_entry[m] (48-byte
+ * records), rowTs: BigInt64Array(n_dep), rowShape: Uint32Array(n_dep)}: the
+ * reduced graph of the last KMZ_RUN_DEPS | KMZ_RUN_DEP_ORDER run in its exact
+ * entry order (kmz_get_dep_entries), i.e. EndpointDependencies([]).combineWith(
+ * traces.toEndpointDependencies()).trim() without a per-row object */
+static napi_value js_dep_entries(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2], out, v;
+  uint32_t n_dep = 0;
+  CHECK(napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  kmz_ctx *c = get_ctx(env, argv[0]);
+  if (!c) return NULL;
+  napi_get_value_uint32(env, argv[1], &n_dep);
+  uint64_t m = 0;
+  int rc = kmz_get_dep_entries(c, NULL, 0, &m, NULL, NULL, 0);
+  if (rc) return throw_rc(env, c, rc);
+  void *de, *dt, *ds;
+  napi_value abe = new_buffer(env, m * sizeof(kmz_dep_entry), &de), abt = new_buffer(env, (size_t)n_dep * 8, &dt),
+             abs = new_buffer(env, (size_t)n_dep * 4, &ds);
+  if (!abe || !abt || !abs) return NULL;
+  rc = kmz_get_dep_entries(c, (kmz_dep_entry *)de, m, &m, (int64_t *)dt, (uint32_t *)ds, n_dep);
+  if (rc) return throw_rc(env, c, rc);
+  CHECK(napi_create_object(env, &out));
+  CHECK(napi_set_named_property(env, out, "entries", abe));
+  CHECK(napi_create_typedarray(env, napi_bigint64_array, n_dep, abt, 0, &v));
+  CHECK(napi_set_named_property(env, out, "rowTs", v));
+  CHECK(napi_create_typedarray(env, napi_uint32_array, n_dep, abs, 0, &v));
+  CHECK(napi_set_named_property(env, out, "rowShape", v));
+  CHECK(napi_create_double(env, (double)m, &v));
+  CHECK(napi_set_named_property(env, out, "n", v));
+  return out;
+}
+
 /* serviceTail(ctx, {svc: Uint32Array, cls: Uint32Array, lsvc: Uint32Array,
  * n_svc, n_lsvc}) -> {stats: Uint32Array(n_svc * 8), byDist: Uint32Array,
  * nDist, hasIn: Uint8Array(n_ep)}: kmz_tail_map_set + kmz_tail_run +
@@ -417,6 +450,8 @@ NAPI_MODULE_INIT() {
   export_fn(env, exports, "spanLinks", js_span_links);
   export_fn(env, exports, "parseZipkin", js_parse_zipkin);
   export_fn(env, exports, "serviceTail", js_service_tail);
+  export_fn(env, exports, "depEntries", js_dep_entries);
+  export_u32(env, exports, "RUN_DEP_ORDER", KMZ_RUN_DEP_ORDER);
   export_u32(env, exports, "RUN_STATS_RT", KMZ_RUN_STATS_RT);
   export_u32(env, exports, "RUN_STATS_TAG", KMZ_RUN_STATS_TAG);
   export_u32(env, exports, "RUN_DEPS", KMZ_RUN_DEPS);

@@ -139,6 +139,7 @@ class Engine:
     # ---- input ---------------------------------------------------------------
     def load(self, batch: SpanBatch, shapes: ShapeTable):
         self.gen += 1
+        self._loaded_token = None
         s = batch.c_struct()
         sh = shapes.c_struct()
         L.check(self.ctx, self._lib.kmz_load(self.ctx, C.byref(s), C.byref(sh), L.MEM_HOST))
@@ -154,6 +155,7 @@ class Engine:
         device=True).  -> (n_spans, n_shapes, n_statuses), or None outside the
         fast path (nothing loaded: parse on the host)."""
         self.gen += 1  # kmz_json_parse overwrites the columns and drops the last run, even on E_UNSUPPORTED
+        self._loaded_token = None  # (no drop-in Traces owns the loaded batch any more)
         n, ns, nt = C.c_uint64(), C.c_uint32(), C.c_uint32()
         if ptr is None:
             buf = data if isinstance(data, bytes) else bytes(data)
@@ -185,6 +187,7 @@ class Engine:
     def json_load(self, shape_of_raw: np.ndarray, status_of_raw: np.ndarray, shapes: ShapeTable, index_base: int = 0,
                   n: Optional[int] = None):
         self.gen += 1
+        self._loaded_token = None
         sm = np.ascontiguousarray(shape_of_raw, dtype=np.uint32)
         tm = np.ascontiguousarray(status_of_raw, dtype=np.uint32)
         sh = shapes.c_struct()
@@ -206,6 +209,7 @@ class Engine:
 
     def load_synthetic(self, config: int, seed: int, trace_begin: int, trace_end: int) -> int:
         self.gen += 1
+        self._loaded_token = None
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_synth_load(self.ctx, config, seed, trace_begin, trace_end, C.byref(n)))
         d = L.SynthDesc()
@@ -220,6 +224,7 @@ class Engine:
         """The traces of [trace_begin, trace_end) with shard(traceId) == rank
         (kmz_synth_load_shard), with their global flatten indices."""
         self.gen += 1
+        self._loaded_token = None
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_synth_load_shard(self.ctx, config, seed, trace_begin, trace_end, world, rank,
                                                          C.byref(n)))
