@@ -139,6 +139,11 @@ typedef struct kmz_info {
   uint64_t n_chains;    /* distinct interned ancestor chains (chain-interning path) */
 } kmz_info;
 
+/* Runs of batches below 2^23 spans are replayed from hipGraphs (a run whose
+ * launch sequence repeats is captured once): how many runs were replayed so
+ * far on this context, and how many graphs it holds (diagnostic). */
+int kmz_get_graph_stats(kmz_ctx *ctx, uint64_t *launches, uint32_t *cached);
+
 /* ---- host ingest: Zipkin JSON -> kmz_spans columns ---- */
 /* Parses the Trace[][] JSON that ZipkinService.getTraceListFromZipkinByServiceName
  * returns (ZipkinService.ts:44-57; span shape Trace.ts:1-38) in flatten order

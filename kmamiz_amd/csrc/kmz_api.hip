@@ -92,6 +92,20 @@ struct kmz_ctx {
   bool sstats = false;      // shape-level K3 partials computed in this run
   bool chain_ran = false;   // this run's dependency graph came from k4_chain's chain interning
   bool walk_once = false;   // a K4 wait ran out (F_SPIN): this run is redone on the exact per-row walk
+  bool k4_now = false;      // this kmz_run's K4 mode (direct enumeration), decided once per call
+  // hipGraphs of a whole run for small batches (launch-bound): a run whose
+  // launch sequence (kmz_run key) repeats is captured once and replayed
+  struct RunGraph {
+    uint64_t key = 0;
+    hipGraphExec_t exec = nullptr;
+    uint64_t used = 0;
+    // host-side state the captured enqueue left (restored on a replay)
+    int path = 0;
+    bool sstats = false, chain_ran = false, k4_direct_ran = false, ctab_dirty = false;
+    uint32_t G = 0, ep_mode = 0, k4_lb1 = 0, k4_nsl = 0, k4_ng = 0;
+  };
+  RunGraph graphs[4];
+  uint64_t graph_seen = 0, graph_clock = 0, graph_launches = 0;
   // K4 mode: chain interning, or direct enumeration (every row stages all its
   // keys) when most rows start a new chain -- chosen from the last interning
   // run's chains/rows for this shape table, measured again every 64 runs
@@ -320,6 +334,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->j_stab, &c->j_ttab, &c->j_reps, &c->j_smap, &c->j_tmap};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
+  for (auto &g : c->graphs)
+    if (g.exec) hipGraphExecDestroy(g.exec);
   if (c->hpin) hipHostFree(c->hpin);
   if (c->hep) hipHostFree(c->hep);
   if (c->side) {
@@ -842,7 +858,7 @@ static int run_deps(kmz_ctx *c, bool links) {
     // unique span ids: rows are the SERVER spans; chain interning (kmz_chain.hip)
     if (!c->sstats && (r = run_shape_stats(c))) return r;
     const uint32_t nt = chain_tiles(n);
-    const bool direct = k4_direct(c);
+    const bool direct = c->k4_now;
     // per persistent workgroup: staged keys (of candidate new chains, or of
     // every row when direct) in one run per coarse bin of the edge set's
     // slices, and deferred chain checks (overflow is handled in place, just
@@ -1101,6 +1117,146 @@ uint32_t kmz_trace_shard(const char *trace_id, uint64_t len, uint32_t world) {
   return shard_of(hi, lo, world);
 }
 
+// Everything one kmz_run attempt puts on the stream, up to the read-back of
+// the counters into pinned memory: no host synchronisation inside on the
+// window-join path (run_table, the repeated-id path, synchronises).
+static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, unsigned long long *s64) {
+  const uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
+  c->sstats = false;
+  c->chain_ran = false;
+  HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->stats64.p, 0, S_COUNT * 8, c->stream));
+  int r;
+  c->main = c->stream;
+  if (c->overlap) {
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    c->stream = c->side;
+  }
+  r = smode ? run_stats(c, smode) : 0;
+  if (c->overlap) {
+    c->stream = c->main;
+    HIPCHK(c, hipEventRecord(c->ev_k3, c->side));
+  }
+  if (r) return r;
+  if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, links))) {
+    c->stream = c->main;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipStreamIsCapturing(c->main, &cs);
+    if (c->overlap && cs == hipStreamCaptureStatusNone) hipStreamSynchronize(c->side);
+    return r;
+  }
+  if (c->overlap) {  // everything queued on the side stream, before the read-back
+    HIPCHK(c, hipEventRecord(c->ev_done, c->side));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
+  }
+  HIPCHK(c, hipMemcpyAsync(h, c->counters.p, C_COUNT * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(s64, c->stats64.p, S_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
+  return KMZ_OK;
+}
+
+// The launch sequence of a run is a function of this state (buffer addresses
+// and sizes, table capacities, seeds, modes, the batch's shape counts): runs
+// with equal keys enqueue identical work.
+static uint64_t run_key(kmz_ctx *c, uint32_t flags) {
+  uint64_t k = 0xcbf29ce484222325ull;
+  auto mix = [&](uint64_t v) { k = mix64(k ^ v) + 0x9E3779B97F4A7C15ull; };
+  for (uint64_t v : {(uint64_t)flags, c->n, c->index_base, (uint64_t)c->n_shapes, (uint64_t)c->n_status,
+                     (uint64_t)c->n_rt, (uint64_t)c->n_tag, (uint64_t)c->n_dep, c->tcap, c->ccap, (uint64_t)c->scap,
+                     (uint64_t)c->mcap, (uint64_t)c->dcap, c->sig_seed, (uint64_t)c->ablate, (uint64_t)c->overlap,
+                     (uint64_t)c->k4_now, (uint64_t)c->ctab_dirty, (uint64_t)c->walk_once,
+                     (uint64_t)(uintptr_t)c->stream, (uint64_t)(uintptr_t)c->side, (uint64_t)(uintptr_t)c->hpin,
+                     (uint64_t)(uintptr_t)c->sid, (uint64_t)(uintptr_t)c->pid, (uint64_t)(uintptr_t)c->kind,
+                     (uint64_t)(uintptr_t)c->shape, (uint64_t)(uintptr_t)c->status, (uint64_t)(uintptr_t)c->dur,
+                     (uint64_t)(uintptr_t)c->ts, (uint64_t)(uintptr_t)c->d_rt.p, (uint64_t)(uintptr_t)c->d_tag.p,
+                     (uint64_t)(uintptr_t)c->d_dep.p, (uint64_t)chain_grid((uint32_t)c->n)})
+    mix(v);
+  for (DevBuf *b : {&c->table, &c->dups, &c->dkey, &c->dval, &c->cparent, &c->rowpos, &c->grp, &c->grp_final, &c->epp,
+                    &c->trip, &c->trip_out, &c->counters, &c->stats64, &c->k3pool, &c->k3dir, &c->k3part,
+                    &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey, &c->mval,
+                    &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n, &c->cetab, &c->kbucket,
+                    &c->kbucket_n, &c->ctile, &c->kwpos, &c->kwpos_n}) {
+    mix((uint64_t)(uintptr_t)b->p);
+    mix(b->bytes);
+  }
+  return k;
+}
+
+// Small batches (< 2^23 spans) are launch-bound: ~25 kernels and memsets per
+// run.  A run whose key was seen on the previous run is captured into a
+// hipGraph (stream capture, both streams) and replayed while the key holds;
+// the first run of a key (and any run that grows a buffer) is enqueued
+// directly, so a capture never allocates.  KMZ_ABLATE bit 13 turns it off.
+static int run_enqueue_graphed(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, unsigned long long *s64) {
+  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && !(c->ablate & (1u << 13)) &&
+                        !c->table_hint && !c->walk_once && !(c->ablate & (32u | 16u));
+  if (!eligible) return run_enqueue(c, flags, links, h, s64);
+  const uint64_t key = run_key(c, flags);
+  ++c->graph_clock;
+  for (auto &g : c->graphs) {
+    if (!g.exec || g.key != key) continue;
+    HIPCHK(c, hipGraphLaunch(g.exec, c->stream));
+    g.used = c->graph_clock;
+    ++c->graph_launches;
+    c->path = g.path;
+    c->sstats = g.sstats;
+    c->chain_ran = g.chain_ran;
+    c->k4_direct_ran = g.k4_direct_ran;
+    c->ctab_dirty = g.ctab_dirty;
+    c->G = g.G;
+    c->ep_mode = g.ep_mode;
+    c->k4_lb1 = g.k4_lb1;
+    c->k4_nsl = g.k4_nsl;
+    c->k4_ng = g.k4_ng;
+    c->main = c->stream;
+    return KMZ_OK;
+  }
+  if (c->graph_seen != key) {  // first run of this key: direct (buffers settle)
+    c->graph_seen = key;
+    return run_enqueue(c, flags, links, h, s64);
+  }
+  // second run of this key: capture it (the host state the enqueue changes is
+  // restored if the capture fails, then the run is enqueued directly)
+  const bool dirty0 = c->ctab_dirty;
+  hipStream_t s0 = c->stream;
+  hipGraph_t graph = nullptr;
+  bool ok = hipStreamBeginCapture(s0, hipStreamCaptureModeThreadLocal) == hipSuccess;
+  int r = ok ? run_enqueue(c, flags, links, h, s64) : KMZ_OK;
+  c->stream = s0;
+  if (ok) ok = hipStreamEndCapture(s0, &graph) == hipSuccess && graph && r == KMZ_OK && run_key(c, flags) == key;
+  hipGraphExec_t exec = nullptr;
+  if (ok) ok = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
+  if (graph) hipGraphDestroy(graph);
+  if (!ok) {
+    if (exec) hipGraphExecDestroy(exec);
+    (void)hipGetLastError();
+    c->ctab_dirty = dirty0;
+    c->graph_seen = 0;
+    c->err.clear();
+    return run_enqueue(c, flags, links, h, s64);
+  }
+  auto *slot = &c->graphs[0];
+  for (auto &g : c->graphs)
+    if (!g.exec || g.used < slot->used) slot = &g;
+  if (slot->exec) hipGraphExecDestroy(slot->exec);
+  slot->key = key;
+  slot->exec = exec;
+  slot->used = c->graph_clock;
+  slot->path = c->path;
+  slot->sstats = c->sstats;
+  slot->chain_ran = c->chain_ran;
+  slot->k4_direct_ran = c->k4_direct_ran;
+  slot->ctab_dirty = c->ctab_dirty;
+  slot->G = c->G;
+  slot->ep_mode = c->ep_mode;
+  slot->k4_lb1 = c->k4_lb1;
+  slot->k4_nsl = c->k4_nsl;
+  slot->k4_ng = c->k4_ng;
+  HIPCHK(c, hipGraphLaunch(exec, s0));
+  ++c->graph_launches;
+  return KMZ_OK;
+}
+
 int kmz_run(kmz_ctx *c, uint32_t flags) {
   if (!c) return KMZ_E_ARG;
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_run before kmz_load");
@@ -1111,13 +1267,15 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
   hipSetDevice(c->device);
   c->hpin_valid = false;
   c->walk_once = false;
+  // one read-back per run: counters + statistics into pinned host memory
+  if (!c->hpin && hipHostMalloc(&c->hpin, C_COUNT * 4 + S_COUNT * 8, hipHostMallocDefault) != hipSuccess) {
+    c->hpin = nullptr;
+    return fail(c, KMZ_E_HIP, "hipHostMalloc (run read-back)");
+  }
+  unsigned int *h = reinterpret_cast<unsigned int *>(c->hpin);
+  unsigned long long *s64 = reinterpret_cast<unsigned long long *>(h + C_COUNT);
+  c->k4_now = (flags & KMZ_RUN_DEPS) ? k4_direct(c) : false;
   for (int attempt = 0; attempt < 8; ++attempt) {
-    c->sstats = false;
-    c->chain_ran = false;
-    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->stats64.p, 0, S_COUNT * 8, c->stream));
-    int r;
-    c->main = c->stream;
     // K3 (+ the certificate, see run_join) on the side stream while the main
     // stream joins and walks (KMZ_ABLATE bit 25: serial, for comparison)
     // Only small batches (< 2^23 spans) overlap: they are launch- and
@@ -1127,35 +1285,8 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     // roofline accounting (profiles/r01_overlap_ab/).  KMZ_ABLATE bit 27 forces it.
     c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25)) &&
                  (c->n < (1ull << 23) || (c->ablate & (1u << 27)));
-    if (c->overlap) {
-      HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
-      HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      c->stream = c->side;
-    }
-    r = smode ? run_stats(c, smode) : 0;
-    if (c->overlap) {
-      c->stream = c->main;
-      HIPCHK(c, hipEventRecord(c->ev_k3, c->side));
-    }
+    int r = run_enqueue_graphed(c, flags, links, h, s64);
     if (r) return r;
-    if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, links))) {
-      c->stream = c->main;
-      if (c->overlap) hipStreamSynchronize(c->side);
-      return r;
-    }
-    if (c->overlap) {  // everything queued on the side stream, before the read-back
-      HIPCHK(c, hipEventRecord(c->ev_done, c->side));
-      HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
-    }
-    // one read-back per run: counters + statistics into pinned host memory
-    if (!c->hpin && hipHostMalloc(&c->hpin, C_COUNT * 4 + S_COUNT * 8, hipHostMallocDefault) != hipSuccess) {
-      c->hpin = nullptr;
-      return fail(c, KMZ_E_HIP, "hipHostMalloc (run read-back)");
-    }
-    unsigned int *h = reinterpret_cast<unsigned int *>(c->hpin);
-    unsigned long long *s64 = reinterpret_cast<unsigned long long *>(h + C_COUNT);
-    HIPCHK(c, hipMemcpyAsync(h, c->counters.p, C_COUNT * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(s64, c->stats64.p, S_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
     if (h[C_FLAGS] & F_CTAB_DIRTY) c->ctab_dirty = true;
@@ -1226,6 +1357,17 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     }
   }
   return fail(c, KMZ_E_OVERFLOW, "table growth did not converge");
+}
+
+int kmz_get_graph_stats(kmz_ctx *c, uint64_t *launches, uint32_t *cached) {
+  if (!c) return KMZ_E_ARG;
+  if (launches) *launches = c->graph_launches;
+  if (cached) {
+    uint32_t k = 0;
+    for (auto &g : c->graphs) k += g.exec != nullptr;
+    *cached = k;
+  }
+  return KMZ_OK;
 }
 
 int kmz_get_info(kmz_ctx *c, kmz_info *out) {

@@ -532,121 +532,6 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
 }
 
-// pass 2 for many sub-bins (B2 >= 10: batches past ~10^8 spans): the same
-// split over R rounds of PQ * 1024 records per workgroup, with ONE global
-// reservation per (workgroup, sub-bin) for all R rounds.  At 2^12 sub-bins a
-// one-round chunk of 8192 records reserved a sub-bin per 2 records (6.7e8
-// device-scope atomics at 10^9 spans: the split took 8.7 ms against 0.51 ms
-// at 10^8).  The records of all rounds stay in registers; each round is
-// ranked, staged in LDS by sub-bin and written contiguously per sub-bin.
-// Dynamic LDS: PQ * 1024 u64 staging (the record -> tile map while loading)
-// + 4 * 2^B2 u32 (totals, reservations, written so far, round offsets).
-template <int PQ, int R>
-__global__ void __launch_bounds__(1024) k_cert_split_r(const unsigned long long *__restrict__ pool1,
-                                                       const uint16_t *__restrict__ jdir, uint32_t n,
-                                                       uint32_t chunks, uint32_t B2,
-                                                       unsigned long long *__restrict__ pool2, uint32_t cap2,
-                                                       unsigned int *__restrict__ cur2,
-                                                       unsigned int *__restrict__ counters) {
-  constexpr uint32_t RC = PQ * 1024, TPC = PQ * 24 * R;  // records per round, tiles per chunk
-  static_assert(TPC <= 1024, "one thread per tile run");
-  extern __shared__ uint64_t dyn[];
-  __shared__ uint32_t wsum[16], tcnt[TPC], toff[TPC];
-  uint64_t *stg = dyn;
-  uint16_t *tof = reinterpret_cast<uint16_t *>(dyn);  // record -> tile of one round (only while loading)
-  const uint32_t M = 1u << B2;
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn + RC), *base = cnt + M, *run = base + M, *loc = run + M;
-  const uint32_t b = blockIdx.x / chunks, ch = blockIdx.x % chunks;
-  const uint32_t ntiles = join_tiles(n), T0 = ch * TPC;
-  if (T0 >= ntiles) return;
-  const uint32_t nt = min(TPC, ntiles - T0);
-  for (uint32_t k = threadIdx.x; k < M; k += blockDim.x) cnt[k] = run[k] = 0;
-  uint32_t c = 0;
-  if (threadIdx.x < TPC) {
-    uint32_t o = 0;
-    if (threadIdx.x < nt) {
-      const uint32_t t = T0 + threadIdx.x;
-      const uint32_t tsize = min(JT, n - t * JT);
-      o = jdir[(uint64_t)t * CERT_BINS + b];
-      const uint32_t e = b + 1 < CERT_BINS ? jdir[(uint64_t)t * CERT_BINS + b + 1] : tsize;
-      c = e - o;
-    }
-    tcnt[threadIdx.x] = c;
-    toff[threadIdx.x] = o;
-  }
-  __syncthreads();
-  const uint32_t last = tcnt[TPC - 1];
-  block_scan_lds(tcnt, TPC, wsum);  // tcnt := position of the tile's run in the chunk
-  const uint32_t cn = tcnt[TPC - 1] + last;
-  if (cn > R * RC) {  // (hashed ids: ~20 sigma)
-    if (threadIdx.x == 0) atomicOr(&counters[C_CERT], CERT_OVF);
-    return;
-  }
-  uint64_t h[R][PQ];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t w0 = r * RC, w1 = w0 + RC;
-    if (threadIdx.x < nt) {  // this round's part of the tile's run
-      const uint32_t p0 = tcnt[threadIdx.x], p1 = p0 + c;
-      for (uint32_t j = max(p0, w0); j < min(p1, w1); ++j) tof[j - w0] = (uint16_t)threadIdx.x;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PQ; ++q) {
-      const uint32_t e = w0 + q * 1024 + threadIdx.x;
-      h[r][q] = 0;
-      if (e < cn) {
-        const uint32_t lo = tof[e - w0];
-        h[r][q] = pool1[(uint64_t)(T0 + lo) * JT + toff[lo] + (e - tcnt[lo])];
-      }
-    }
-    __syncthreads();  // (tof is rewritten by the next round)
-  }
-  const uint32_t sh = 64 - CERT_B1 - B2;
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int q = 0; q < PQ; ++q)
-      if (r * RC + q * 1024 + threadIdx.x < cn) atomicAdd(&cnt[(uint32_t)(h[r][q] >> sh) & (M - 1)], 1u);
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < M; k += blockDim.x) {
-    const uint32_t x = cnt[k];
-    base[k] = x ? atomicAdd(&cur2[(b << B2) | k], x) : 0;
-  }
-  bool ovf = false;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const uint32_t w0 = r * RC;
-    if (w0 >= cn) break;  // (uniform)
-    const uint32_t mr = min(cn - w0, RC);
-    for (uint32_t k = threadIdx.x; k < M; k += blockDim.x) loc[k] = 0;
-    __syncthreads();
-    uint32_t rk[PQ];
-#pragma unroll
-    for (int q = 0; q < PQ; ++q)
-      rk[q] = w0 + q * 1024 + threadIdx.x < cn ? atomicAdd(&loc[(uint32_t)(h[r][q] >> sh) & (M - 1)], 1u) : 0;
-    __syncthreads();
-    block_scan_lds(loc, M, wsum);  // loc := this round's offsets by sub-bin
-#pragma unroll
-    for (int q = 0; q < PQ; ++q)
-      if (w0 + q * 1024 + threadIdx.x < cn) stg[loc[(uint32_t)(h[r][q] >> sh) & (M - 1)] + rk[q]] = h[r][q];
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < mr; e += blockDim.x) {
-      const uint64_t x = stg[e];
-      const uint32_t sb = (uint32_t)(x >> sh) & (M - 1);
-      const uint32_t pos = base[sb] + run[sb] + (e - loc[sb]);
-      if (pos < cap2)
-        pool2[(uint64_t)((b << B2) | sb) * cap2 + pos] = x;
-      else
-        ovf = true;
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < M; k += blockDim.x) run[k] += (k + 1 < M ? loc[k + 1] : mr) - loc[k];
-    __syncthreads();
-  }
-  if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
-}
-
 // pass 3: exact duplicate check of one sub-bin, without probe loops.  Every
 // hashed id goes to bucket (low bits of the hash) of an LDS table of 8-slot
 // buckets: one returning LDS add gives its slot, one store places it; ids
@@ -830,18 +715,20 @@ __global__ void __launch_bounds__(256) k_pend(const uint8_t *__restrict__ kind, 
 
 // ---------------------------------------------------------------------------
 
-// split rounds per workgroup by sub-bin count: ~12 records per (workgroup,
-// sub-bin) reservation at 2^9 .. 2^12 sub-bins
-static uint32_t cert_rounds(uint32_t B2) { return B2 <= 9 ? 1u : (B2 <= 11 ? 2u : 4u); }
-
+// (Measured and dropped at 10^9 ids, where this pass 2 takes 8.7 ms against
+// 0.51 ms at 10^8: R rounds of 8192 records per workgroup with one
+// reservation per (workgroup, sub-bin) -- 8.85 ms, so the 6.7e8 device-scope
+// reservations are not what bounds it; a pass 3 that holds a 4x larger
+// sub-bin in registers and checks it in 4 phases, so that pass 2 writes runs
+// 4x longer -- split 8.9 -> 7.4 ms but check 2.9 -> 5.6 ms, and at 10^8
+// split 0.56 -> 0.49, check 0.27 -> 0.50 ms; 8 phases worse still.)
 bool cert_plan(uint32_t n, CertPlan *pl) {
   uint32_t B2 = 0;
   while (B2 < 12 && (uint64_t)n > (3072ull << (CERT_B1 + B2))) ++B2;
   const double mean2 = (double)n / ((uint64_t)CERT_BINS << B2);
   pl->B2 = B2;
   pl->cap2 = (uint32_t)(mean2 * 1.15) + 256;
-  const uint32_t tpc = CERT_PQ * 24 * cert_rounds(B2);
-  pl->chunks = (join_tiles(n) + tpc - 1) / tpc;
+  pl->chunks = (join_tiles(n) + CERT_PQ * 24 - 1) / (CERT_PQ * 24);
   return pl->cap2 <= CERT_SET * 3 / 4;
 }
 
@@ -860,20 +747,9 @@ void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const 
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
                        const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters) {
   if (!n) return;
-  const uint32_t R = cert_rounds(pl.B2);
-  if (R == 1) {
-    const size_t lds = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B2) * 4;
-    hipLaunchKernelGGL(k_cert_split<CERT_PQ>, dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n,
-                       pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
-    return;
-  }
-  const size_t lds = CERT_PQ * 1024 * 8 + (size_t)4 * (1u << pl.B2) * 4;
-  if (R == 2)
-    hipLaunchKernelGGL((k_cert_split_r<CERT_PQ, 2>), dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n,
-                       pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
-  else
-    hipLaunchKernelGGL((k_cert_split_r<CERT_PQ, 4>), dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n,
-                       pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
+  const size_t lds = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B2) * 4;
+  hipLaunchKernelGGL(k_cert_split<CERT_PQ>, dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n, pl.chunks,
+                     pl.B2, pool2, pl.cap2, cur2, counters);
 }
 
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,

@@ -395,6 +395,12 @@ class Engine:
         L.check(self.ctx, rc)
         return bool(r.value)
 
+    def graph_stats(self):
+        """(runs replayed from hipGraphs so far, graphs held) (kmz_get_graph_stats)."""
+        n, k = C.c_uint64(), C.c_uint32()
+        L.check(self.ctx, self._lib.kmz_get_graph_stats(self.ctx, C.byref(n), C.byref(k)))
+        return int(n.value), int(k.value)
+
     # ---- profiling -------------------------------------------------------------
     def set_profiling(self, on: bool):
         L.check(self.ctx, self._lib.kmz_set_profiling(self.ctx, 1 if on else 0))

@@ -1091,3 +1091,45 @@ def test_headline_config5_vs_c_oracle_and_tail():
             np.testing.assert_allclose(np.asarray(mt[k], dtype=float), np.asarray(mr[k], dtype=float), rtol=REL)
     finally:
         e.close()
+
+
+# ---------------------------------------------------------------------------
+# hipGraph replay of small-batch runs (kmz_api.hip run_enqueue_graphed)
+# ---------------------------------------------------------------------------
+GRAPH_OFF = 1 << 13  # KMZ_ABLATE: no hipGraph capture
+
+
+def _run_results(e, flags):
+    e.run(flags)
+    g, k, ep = e.fetch()
+    return g.tobytes(), np.sort(k).tobytes(), ep.tobytes(), _info_results(e.info())
+
+
+@pytest.mark.parametrize("config,ntr", [(2, 2500), (3, 2500), (5, 2500), (5, 40000)])
+def test_graph_replay_equals_direct_runs(config, ntr):
+    """Production-tick batches (2 500 traces, RealtimeWorkerImpl.ts:31-35):
+    runs replayed from a captured hipGraph give the results of runs enqueued
+    one launch at a time, run after run, also when the loaded data change
+    under the same launch sequence (same size, other durations / timestamps)."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(config, 0, ntr)
+    table = synth.shape_table(config)
+    other = batch.__class__(**{f: (lambda v: v.copy() if isinstance(v, np.ndarray) else v)(getattr(batch, f))
+                               for f in batch.__dataclass_fields__})
+    other.duration = other.duration[::-1].copy()
+    other.timestamp = other.timestamp + 7
+    on, off = _engine_with(0), _engine_with(GRAPH_OFF)
+    try:
+        for flags in (L.RUN_STATS_TAG | L.RUN_DEPS, L.RUN_STATS_RT | L.RUN_DEPS | L.RUN_SPAN_LINKS):
+            for b in (batch, other, batch):
+                on.load(b, table)
+                off.load(b, table)
+                exp = _run_results(off, flags)
+                for _ in range(4):
+                    assert _run_results(on, flags) == exp
+        assert on.graph_stats()[0] > 0 and off.graph_stats() == (0, 0)
+    finally:
+        on.close()
+        off.close()

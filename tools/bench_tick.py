@@ -1,0 +1,66 @@
+"""Production-tick latency: the reference's realtime worker
+takes up to 2 500 traces per 5-s tick (RealtimeWorkerImpl.ts:31-35).  Per tick
+on one GPU: kmz_load of the host columns (H2D) + kmz_run (stats + dependency
+graph) + kmz_fetch of the results, timed over many ticks, with the run's
+hipGraph replay on (default) and off (KMZ_ABLATE bit 13).  Prints one JSON
+object; kernel launches per tick come from rocprofv3 (tools/tick_profile.sh).
+
+    python tools/bench_tick.py [--traces 2500] [--ticks 200]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--traces", type=int, default=2500)
+    ap.add_argument("--ticks", type=int, default=200)
+    args = ap.parse_args()
+    import numpy as np
+
+    from kmamiz_amd import Engine
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    out = {"metric": "per-tick latency, 2 500 traces per call (RealtimeWorkerImpl.ts:31-35)", "unit": "us",
+           "ticks": args.ticks, "configs": {}}
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS
+    for name, cfg in (("bookinfo", synth.BOOKINFO), ("mesh", synth.MESH), ("power", synth.POWER)):
+        batch, _ = synth.host_batch(cfg, 0, args.traces)
+        table = synth.shape_table(cfg)
+        res = {"spans": len(batch)}
+        for mode, knob in (("graph", 0), ("no_graph", 1 << 13)):
+            os.environ["KMZ_ABLATE"] = str(knob)
+            e = Engine(0)
+            del os.environ["KMZ_ABLATE"]
+            for _ in range(10):  # warm: buffers, the graph capture
+                e.load(batch, table)
+                e.run(flags)
+                e.fetch()
+            t_run, t_tick = [], []
+            for _ in range(args.ticks):
+                t0 = time.perf_counter()
+                e.load(batch, table)
+                t1 = time.perf_counter()
+                e.run(flags)
+                e.fetch()
+                t2 = time.perf_counter()
+                t_run.append(t2 - t1)
+                t_tick.append(t2 - t0)
+            res[mode] = {"run_fetch_us_median": round(float(np.median(t_run)) * 1e6, 1),
+                         "tick_us_median": round(float(np.median(t_tick)) * 1e6, 1),
+                         "tick_us_p99": round(float(np.percentile(t_tick, 99)) * 1e6, 1),
+                         "graph_replays": e.graph_stats()[0]}
+            e.close()
+        out["configs"][name] = res
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
