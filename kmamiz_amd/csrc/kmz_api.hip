@@ -305,10 +305,14 @@ kmz_ctx *kmz_create(int device, void *stream) {
   }
   if (const char *a = getenv("KMZ_ABLATE")) c->ablate = (uint32_t)strtoul(a, nullptr, 0);
   if (c->ablate & (1u << 30)) c->scap = 256;  // test knob: tiny key staging (overflow + growth paths)
-  if (ensure(c, c->counters, C_COUNT * 4) || ensure(c, c->stats64, S_COUNT * 8)) {
+  // counters (u32) and statistics (u64) in one allocation: one fill and one
+  // read-back per run (stats64 is a view, not freed on its own)
+  if (ensure(c, c->counters, C_COUNT * 4 + S_COUNT * 8)) {
     delete c;
     return nullptr;
   }
+  c->stats64.p = static_cast<char *>(c->counters.p) + C_COUNT * 4;
+  c->stats64.bytes = S_COUNT * 8;
   return c;
 }
 
@@ -321,7 +325,7 @@ void kmz_destroy(kmz_ctx *c) {
   DevBuf *bufs[] = {&c->in_sid, &c->in_pid,    &c->in_kind,  &c->in_shape,  &c->in_status, &c->in_dur,
                     &c->in_ts,  &c->d_rt,      &c->d_tag,    &c->d_dep,     &c->table,     &c->dups,
                     &c->dkey,   &c->dval,      &c->cparent,  &c->rowpos,    &c->grp,       &c->grp_final,
-                    &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->stats64,   &c->scratch,
+                    &c->epp,    &c->trip,      &c->trip_out, &c->counters,  &c->scratch,
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
@@ -688,8 +692,15 @@ static int run_join(kmz_ctx *c, bool *ok) {
     return KMZ_E_HIP;
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
-  HIPCHK(c, hipMemsetAsync(cur2, 0, nsub * 4, c->stream));
   if (ensure(c, c->mkey, (size_t)c->mcap * 8) || ensure(c, c->mval, (size_t)c->mcap * 4)) return KMZ_E_HIP;
+  {
+    Timed t(c, KMZ_K_MEMSET);
+    FillArgs f;
+    f.add(cur2, nsub * 4, 0);
+    f.add(c->mkey.p, (size_t)c->mcap * 8, 0);
+    f.add(c->mval.p, (size_t)c->mcap * 4, 0xFF);  // ids not in the batch: NONE
+    launch_fill(c->stream, f);
+  }
   {
     Timed t(c, KMZ_K_JOIN);
     launch_join(c->stream, c->sid, c->pid, c->kind, n, P<uint32_t>(c->cparent), P<uint32_t>(c->dp),
@@ -721,8 +732,6 @@ static int run_join(kmz_ctx *c, bool *ok) {
     // host never waits here.  The certificate is read after the run: if an id
     // repeats, kmz_run discards the run and takes the table path.
     Timed t(c, KMZ_K_RESOLVE);
-    HIPCHK(c, hipMemsetAsync(c->mkey.p, 0, (size_t)c->mcap * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->mval.p, 0xFF, (size_t)c->mcap * 4, c->stream));  // ids not in the batch: NONE
     launch_miss(c->stream, c->sid, c->pid, P<uint32_t>(c->dp), n, P<unsigned long long>(c->mkey),
                 P<uint32_t>(c->mval), c->mcap, cnt);
     launch_pend(c->stream, c->kind, P<uint32_t>(c->dp), n, P<uint32_t>(c->cparent), cnt);
@@ -775,12 +784,18 @@ static int run_shape_stats(kmz_ctx *c) {
   const bool part = Gs > 1024 && k3_partitions((uint32_t)Gs) <= k3_pmax() && !(c->ablate & 8);
   {
     Timed t(c, KMZ_K_MEMSET);
-    HIPCHK(c, hipMemsetAsync(sg, 0, Gs * 40, c->stream));
-    HIPCHK(c, hipMemsetAsync(sg + 5 * Gs, 0xFF, Gs * 8, c->stream));
+    FillArgs f;
+    f.add(sg, Gs * 40, 0);
+    f.add(sg + 5 * Gs, Gs * 8, 0xFF);
+    launch_fill(c->stream, f);
   }
   if (part) {
     const uint32_t Pp = k3_partitions((uint32_t)Gs), nt = k3_tiles(n);
-    const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(64, 2048 / Pp));
+    // slices per partition: enough workgroups to fill the GPU at scale; one
+    // for small batches, whose reduce then writes the group partials directly
+    // (no k3_combine over S x G: at a 2 500-trace tick of the mesh, 34 slices
+    // x 6 x 60k groups made the combine cost more than the records)
+    const uint32_t S = nt <= 64 ? 1u : std::max<uint32_t>(1, std::min<uint32_t>({64u, 2048 / Pp, nt / 32}));
     if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, k3_dir_words(n, Pp, S) * 4 + 4) ||
         ensure(c, c->k3part, (size_t)S * 6 * Gs * 8) || ensure(c, c->tile_tmp, (size_t)nt * 16))
       return KMZ_E_HIP;
@@ -838,8 +853,10 @@ static int run_deps(kmz_ctx *c, bool links) {
   unsigned long long *epp = P<unsigned long long>(c->epp);
   {
     Timed t(c, KMZ_K_MEMSET);
-    HIPCHK(c, hipMemsetAsync(epp, 0, (size_t)c->n_dep * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(epp + c->n_dep, 0xFF, (size_t)c->n_dep * 8, c->stream));
+    FillArgs f;
+    f.add(epp, (size_t)c->n_dep * 8, 0);
+    f.add(epp + c->n_dep, (size_t)c->n_dep * 8, 0xFF);
+    launch_fill(c->stream, f);
   }
   bool joined = false;
   int r = run_join(c, &joined);
@@ -902,9 +919,11 @@ static int run_deps(kmz_ctx *c, bool links) {
       Timed t(c, KMZ_K_MEMSET);
       // the chain table is cleared entry by entry after each run; a full
       // memset only when it is new or a list overflowed
-      if (c->ctab_dirty && !direct) HIPCHK(c, hipMemsetAsync(c->ctab.p, 0, c->ccap * CHAIN_ENTRY_BYTES, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->kbucket_n.p, 0, nsl * 4, c->stream));
+      FillArgs f;
+      if (c->ctab_dirty && !direct) f.add(c->ctab.p, c->ccap * CHAIN_ENTRY_BYTES, 0);
+      f.add(c->trip.p, c->tcap * 8, 0);
+      f.add(c->kbucket_n.p, nsl * 4, 0);
+      launch_fill(c->stream, f);
     }
     const bool was_dirty = c->ctab_dirty;
     if (!direct) c->ctab_dirty = true;  // until this run's slots are cleared below
@@ -985,8 +1004,10 @@ static int run_stats(kmz_ctx *c, uint32_t mode) {
   unsigned long long *grp = P<unsigned long long>(c->grp);
   {
     Timed t(c, KMZ_K_MEMSET);
-    HIPCHK(c, hipMemsetAsync(grp, 0, G * 40, c->stream));
-    HIPCHK(c, hipMemsetAsync(grp + 5 * G, 0xFF, G * 8, c->stream));
+    FillArgs f;
+    f.add(grp, G * 40, 0);
+    f.add(grp + 5 * G, G * 8, 0xFF);
+    launch_fill(c->stream, f);
   }
   {
     Timed t(c, KMZ_K_FINAL);
@@ -1124,8 +1145,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   const uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
   c->sstats = false;
   c->chain_ran = false;
-  HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->stats64.p, 0, S_COUNT * 8, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4 + S_COUNT * 8, c->stream));
   int r;
   c->main = c->stream;
   if (c->overlap) {
@@ -1150,8 +1170,9 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     HIPCHK(c, hipEventRecord(c->ev_done, c->side));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
   }
-  HIPCHK(c, hipMemcpyAsync(h, c->counters.p, C_COUNT * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(s64, c->stats64.p, S_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
+  static_assert(C_COUNT * 4 % 8 == 0, "the statistics follow the counters in one buffer and in hpin");
+  (void)s64;
+  HIPCHK(c, hipMemcpyAsync(h, c->counters.p, C_COUNT * 4 + S_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
   return KMZ_OK;
 }
 

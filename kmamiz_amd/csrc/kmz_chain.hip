@@ -835,14 +835,18 @@ __global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *
                                                       unsigned long long *__restrict__ stats64,
                                                       uint32_t *__restrict__ gpos, uint32_t gcap, uint32_t spin) {
   uint32_t flags = 0, fresh = 0;
+  // parts workgroups per tile workgroup's runs (gridDim.y): the inserts are
+  // latency-bound device-scope CASes, so small batches (few tile workgroups,
+  // every chain new) want more threads than one workgroup per run
+  const uint32_t parts = gridDim.y, t0 = blockIdx.y * blockDim.x + threadIdx.x, ts = parts * blockDim.x;
   for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
     for (uint32_t b = 0; b < (1u << lb1); ++b) {
       const uint64_t r = ((uint64_t)w << lb1) + b;
       const uint32_t m = stage_n[r];
-      for (uint32_t x = threadIdx.x; x < m; x += blockDim.x) edge_insert(stage[r * sub + x], trip, tcap, &flags);
+      for (uint32_t x = t0; x < m; x += ts) edge_insert(stage[r * sub + x], trip, tcap, &flags);
     }
     const uint32_t md = defer_n[w];
-    for (uint32_t x = threadIdx.x; x < md; x += blockDim.x) {
+    for (uint32_t x = t0; x < md; x += ts) {
       const unsigned long long *r = defer + 2 * ((uint64_t)w * dcap + x);
       int rr = 0;
       for (uint32_t t = 0; t < spin && rr == 0; ++t)
@@ -1061,7 +1065,8 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
     hipLaunchKernelGGL(k_key_slice, dim3(std::min<uint32_t>(nsl, 8192)), dim3(KS_T), 0, s, bucket, bcap, bucket_n, nsl,
                        trip, tcap, counters);
   } else {
-    hipLaunchKernelGGL(k_chain_settle, dim3(g), dim3(256), 0, s, stage, scap >> lb1, stage_n, lb1, trip, tcap, defer,
+    const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(16, 2048 / g));
+    hipLaunchKernelGGL(k_chain_settle, dim3(g, parts), dim3(256), 0, s, stage, scap >> lb1, stage_n, lb1, trip, tcap, defer,
                        dcap, defer_n, g, reinterpret_cast<unsigned long long *>(ctab), ccap, counters, stats64, gpos,
                        gcap, spin_bound(ablate));
   }

@@ -35,6 +35,23 @@ struct DupEntry {
   uint32_t pos, idx, winner, pad;
 };
 
+// up to FILL_MAX buffer fills (byte value each) in one launch (k_fill)
+constexpr uint32_t FILL_MAX = 8;
+struct FillArgs {
+  void *p[FILL_MAX];
+  uint64_t bytes[FILL_MAX];
+  uint32_t val[FILL_MAX];
+  uint32_t n = 0;
+  void add(void *ptr, uint64_t nbytes, uint32_t byte) {
+    if (!nbytes) return;
+    p[n] = ptr;
+    bytes[n] = nbytes;
+    val[n] = byte;
+    ++n;
+  }
+};
+void launch_fill(hipStream_t s, const FillArgs &a);
+
 void launch_build(hipStream_t s, const uint64_t *sid, uint32_t n, unsigned long long *table, uint64_t cap,
                   DupEntry *dups, uint32_t dup_cap, unsigned int *counters);
 void launch_fixup(hipStream_t s, const DupEntry *dups, const unsigned int *counters, uint32_t dup_cap,

@@ -474,14 +474,17 @@ void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base
 #endif
   // packed accumulators while a slice's records stay below 2^22 (counts and
   // in-slice first indices fit their fields)
+  // one slice: its partials are the group partials ([6][G], the same layout)
+  unsigned long long *dst = S == 1 ? grp : part;
   if (KMZ_K3_PACK && (uint64_t)((ntiles + S - 1) / S) * K3T < (1ull << 22))
     hipLaunchKernelGGL(k3_reduce<true>, dim3(S, P), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, S, G, index_base,
-                       part);
+                       dst);
   else
     hipLaunchKernelGGL(k3_reduce<false>, dim3(S, P), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, S, G,
-                       index_base, part);
-  hipLaunchKernelGGL(k3_combine, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part, S, G,
-                     grp);
+                       index_base, dst);
+  if (S > 1)
+    hipLaunchKernelGGL(k3_combine, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part, S,
+                       G, grp);
 }
 
 uint32_t k3_partitions(uint32_t G) { return (G + K3R - 1) / K3R; }
