@@ -224,6 +224,9 @@ def main():
                                               g["cv"][used], is_5xx[used % n_status], first=g["first"][used])
 
     def step():
+        # N > 1: the repeated-span-id guard routes this batch's ids and posts
+        # its all-to-all before the run, so the exchange overlaps the kernels
+        guard = kdist.IdGuard(eng, dev).start() if world > 1 else None
         eng.run(flags)
         if world > 1:
             gw = eng.partials_words(L.PART_GROUPS)
@@ -237,7 +240,7 @@ def main():
             eng.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, True)
             # three collectives: SUM moments, MAX of max / negated min fields
             # + key count, all-gather of the keys (union in the engine's set)
-            kdist.merge_all(g, gw // 6, e, ew // 2, t[:tw], engine=eng, digest=digest)
+            kdist.merge_all(g, gw // 6, e, ew // 2, t[:tw], engine=eng, digest=digest, check_ids=guard)
             eng.import_partials(L.PART_GROUPS, g.data_ptr(), gw, True)
             eng.import_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
             eng.finalize()
@@ -380,8 +383,8 @@ def main():
                 "edge_keys": info["n_triples"],
                 "parallelism": f"traceId-shard x{world}" if world > 1 else "single GPU",
                 "sharding_guards": ("in every timed step: id-table/size agreement, unresolved parents, "
-                                    "cross-shard repeated span ids (all-to-all of hashed ids + certificate)"
-                                    if world > 1 else None),
+                                    "cross-shard repeated span ids (all-to-all of hashed ids, overlapping the run, "
+                                    "+ certificate)" if world > 1 else None),
                 "service_tail": tail_on,
                 "fetched": ("groups + endpoints to the host; the edge keys stay in HBM, where "
                             "kmz_tail_run reads them" if tail_on else

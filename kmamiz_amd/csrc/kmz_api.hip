@@ -795,7 +795,12 @@ static int run_shape_stats(kmz_ctx *c) {
     // for small batches, whose reduce then writes the group partials directly
     // (no k3_combine over S x G: at a 2 500-trace tick of the mesh, 34 slices
     // x 6 x 60k groups made the combine cost more than the records)
-    const uint32_t S = nt <= 64 ? 1u : std::max<uint32_t>(1, std::min<uint32_t>({64u, 2048 / Pp, nt / 32}));
+#ifndef KMZ_K3_SMALL_S
+#define KMZ_K3_SMALL_S 1
+#endif
+    const uint32_t S = (KMZ_K3_SMALL_S && nt <= 64) ? 1u
+                                                     : std::max<uint32_t>(1, std::min<uint32_t>({64u, 2048 / Pp,
+                                                                                                  std::max(nt / 32, 1u)}));
     if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, k3_dir_words(n, Pp, S) * 4 + 4) ||
         ensure(c, c->k3part, (size_t)S * 6 * Gs * 8) || ensure(c, c->tile_tmp, (size_t)nt * 16))
       return KMZ_E_HIP;

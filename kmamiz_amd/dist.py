@@ -84,7 +84,8 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
     a digest of the endpoint/status id tables this rank's partials are indexed
     by (shard.exchange_tables); ranks that disagree raise ShardingError.
     ``check_ids`` (with an engine): the cross-shard repeated-span-id guard
-    (check_repeated_ids) before the merge."""
+    (check_repeated_ids) before the merge; an IdGuard started before the run
+    is finished here instead."""
     world = dist.get_world_size(group)
     if world == 1:
         return None if engine is not None else torch.unique(keys)
@@ -103,7 +104,9 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
                             "(assign global ids with shard.exchange_tables)")
     if a[6] > 0:
         _check_shards(engine, nu, int(a[6]), dev, group)
-    if engine is not None and check_ids:
+    if isinstance(check_ids, IdGuard):  # started before the run: its exchange overlapped it
+        check_ids.finish()
+    elif engine is not None and check_ids:
         check_repeated_ids(engine, dev, group)
     if G:
         dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM, group=group)  # modular: exact for u64
@@ -156,6 +159,68 @@ def route_ids_np(span_ids: np.ndarray, world: int):
     return h[order], np.bincount(own, minlength=world).astype(np.int64)
 
 
+class IdGuard:
+    """The cross-shard repeated-span-id check (check_repeated_ids) split in
+    two, so that its all-to-all overlaps the run: ``start()`` routes this
+    rank's id hashes (kmz_route_ids, on the engine's stream) and posts the
+    exchange asynchronously; ``finish()`` waits for it, runs the uniqueness
+    certificate over what this rank received (kmz_id_repeats) and agrees on
+    the verdict (a MAX all-reduce), raising ShardingError on a repeat."""
+
+    def __init__(self, engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None):
+        self.engine, self.group, self.span_ids = engine, group, span_ids
+        self.world = dist.get_world_size(group)
+        # device tensors under RCCL; host tensors under gloo (its all-to-all is CPU-only)
+        self.on_dev = (engine is not None and dev is not None and torch.device(dev).type == "cuda"
+                       and dist.get_backend(group) == "nccl")
+        self.dev = torch.device(dev) if self.on_dev else torch.device("cpu")
+        self.work = None
+
+    def start(self) -> "IdGuard":
+        if self.world == 1:
+            return self
+        if self.engine is not None:
+            n = int(self.engine.n)
+            send = torch.empty(max(1, n), dtype=torch.int64, device=self.dev)
+            counts = self.engine.route_ids(self.world, send.data_ptr(), n, self.on_dev)
+            send = send[:n]
+        else:
+            h, c = route_ids_np(self.span_ids, self.world)
+            send = torch.from_numpy(h.view(np.int64).copy())
+            counts = c.tolist()
+        cnt = torch.tensor(counts, dtype=torch.int64, device=self.dev)
+        rcnt = torch.empty_like(cnt)
+        dist.all_to_all_single(rcnt, cnt, group=self.group)
+        rc = rcnt.tolist()
+        self.recv = torch.empty(max(1, sum(rc)), dtype=torch.int64, device=self.dev)
+        self.m = sum(rc)
+        self.send = send  # (kept alive until the exchange is done)
+        self.work = dist.all_to_all_single(self.recv[: self.m], send, output_split_sizes=rc, input_split_sizes=counts,
+                                           group=self.group, async_op=True)
+        return self
+
+    def finish(self) -> None:
+        if self.world == 1:
+            return
+        if self.work is None:
+            self.start()
+        self.work.wait()
+        recv = self.recv[: self.m]
+        if self.on_dev:
+            torch.cuda.current_stream(self.dev).synchronize()  # (the engine's stream may not be torch's)
+        rep = None
+        if self.engine is not None and recv.numel():
+            rep = self.engine.id_repeats(recv.data_ptr(), recv.numel(), self.on_dev)
+        if rep is None:  # host check (no engine, or the certificate could not decide)
+            rep = bool(recv.numel()) and torch.unique(recv).numel() != recv.numel()
+        flag = torch.tensor([1 if rep else 0], dtype=torch.int64, device=self.dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        self.work = self.send = self.recv = None
+        if int(flag.item()):
+            raise ShardingError("a span id occurs in two shards: the reference's global span map would merge them "
+                                "(Traces.ts:117-123); run unsharded")
+
+
 def check_repeated_ids(engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None) -> None:
     """Raise ShardingError if a span id occurs in two shards.
 
@@ -170,42 +235,9 @@ def check_repeated_ids(engine=None, dev=None, group=None, span_ids: Optional[np.
     certificate, or the span-table path that _unresolved refuses).  Cost per
     span: 8 bytes over the all-to-all and ~40 bytes of HBM traffic on its
     owner.  ``span_ids`` (no engine): the same protocol on the host (numpy
-    hashes, a sort for the check), for CPU tensors under gloo."""
-    world = dist.get_world_size(group)
-    if world == 1:
-        return
-    if engine is not None:
-        # device tensors under RCCL; host tensors under gloo (its all-to-all is CPU-only)
-        on_dev = dev is not None and torch.device(dev).type == "cuda" and dist.get_backend(group) == "nccl"
-        n = int(engine.n)
-        send = torch.empty(max(1, n), dtype=torch.int64, device=dev if on_dev else "cpu")
-        counts = engine.route_ids(world, send.data_ptr(), n, on_dev)
-        send = send[:n]
-    else:
-        h, c = route_ids_np(span_ids, world)
-        send = torch.from_numpy(h.view(np.int64).copy())
-        counts = c.tolist()
-        on_dev = False
-    cdev = send.device
-    cnt = torch.tensor(counts, dtype=torch.int64, device=cdev)
-    rcnt = torch.empty_like(cnt)
-    dist.all_to_all_single(rcnt, cnt, group=group)
-    rc = rcnt.tolist()
-    recv = torch.empty(max(1, sum(rc)), dtype=torch.int64, device=cdev)
-    dist.all_to_all_single(recv[: sum(rc)], send, output_split_sizes=rc, input_split_sizes=counts, group=group)
-    recv = recv[: sum(rc)]
-    if on_dev:
-        torch.cuda.current_stream(cdev).synchronize()  # (the engine's stream may not be torch's)
-    rep = None
-    if engine is not None and recv.numel():
-        rep = engine.id_repeats(recv.data_ptr(), recv.numel(), on_dev)
-    if rep is None:  # host check (no engine, or the certificate could not decide)
-        rep = bool(recv.numel()) and torch.unique(recv).numel() != recv.numel()
-    flag = torch.tensor([1 if rep else 0], dtype=torch.int64, device=cdev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-    if int(flag.item()):
-        raise ShardingError("a span id occurs in two shards: the reference's global span map would merge them "
-                            "(Traces.ts:117-123); run unsharded")
+    hashes, a sort for the check), for CPU tensors under gloo.  IdGuard splits
+    it around the run."""
+    IdGuard(engine, dev, group, span_ids).start().finish()
 
 
 def _gather_padded(x: torch.Tensor, m: int, world: int, group=None) -> torch.Tensor:
