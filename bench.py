@@ -197,7 +197,7 @@ def main():
         import numpy as np
 
         from kmamiz_amd.ingest import SHAPE_TAGS, UNDEFINED, tag_identity
-        from kmamiz_amd.tail import maps_for_synth, realtime_risk_columns, run_tail
+        from kmamiz_amd.tail import maps_for_synth, realtime_risk_columns, realtime_risk_from_sums, run_tail
 
         args.no_fetch = False
         tmaps = maps_for_synth(config)
@@ -212,16 +212,15 @@ def main():
                 sid_names.append(usn)
             tag_sid[sh] = sid_of[usn]
         is_5xx = np.array([str(x).startswith("5") for x in synth.STATUSES[:n_status]], dtype=bool)
+        eng.set_service_map(tag_sid, len(sid_names), is_5xx)  # the groups' services, for kmz_service_sums
 
     def service_tail():
-        g, e = state["groups"], state["endpoints"]
-        t = run_tail(eng, tmaps, e)  # reads the edge keys where the run left them, in HBM
+        t = run_tail(eng, tmaps)  # reads the edge keys where the run left them, in HBM
         state["metrics"] = t.metrics()
-        # RiskAnalyzer.RealtimeRisk over the used combined groups as columns
-        # (tools/diag_power.py: 1.8 ms against 3.2 ms from the whole grid)
-        used = np.nonzero(g["combined"] > 0)[0]
-        state["risk"] = realtime_risk_columns(t, tag_sid[used // n_status], sid_names, g["combined"][used],
-                                              g["cv"][used], is_5xx[used % n_status], first=g["first"][used])
+        # RiskAnalyzer.RealtimeRisk: the per-service sums over the combined
+        # groups on the device (kmz_service_sums, bit-equal to the host's row
+        # sums), the rest over the ~10^3 services on the host
+        state["risk"] = realtime_risk_from_sums(t, sid_names, *eng.service_sums())
 
     def step():
         # N > 1: the repeated-span-id guard routes this batch's ids and posts

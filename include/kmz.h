@@ -382,11 +382,33 @@ int kmz_tail_run(kmz_ctx *ctx, uint64_t *n_details, uint64_t *n_pairs);
  *   [3] distance-1 details with dependingOn > 0 (ADS)   (RiskAnalyzer.ts:150-166)
  *   [4] distance-1 consumer services, [5] sum of their consumes
  *       (toServiceEndpointCohesion, EndpointDependencies.ts:569-596)
+ *   [6] endpoints with a row (totalEndpoints, EndpointDependencies.ts:566-573, 606)
+ *   [7] 1 if some row has an empty dependingBy (a gateway, RiskAnalyzer.ts:155-158)
  * and by_dist[svc * n_dist + d] = sum of dependingBy at distance d
  * (RelyingFactor, RiskAnalyzer.ts:124-137).  *n_dist = 0 when some distance
- * exceeded the dense table (the caller then sums the details). */
+ * exceeded the dense table (the caller then sums the details).  Copied back
+ * by kmz_tail_run itself: no device synchronisation here. */
 int kmz_tail_service_stats(kmz_ctx *ctx, uint32_t *stats, uint64_t scap, uint32_t *by_dist, uint64_t dcap,
                            uint32_t *n_dist);
+/* per service id: the global index of its first row (UINT64_MAX: no row) --
+ * toServiceDependencies' service order (EndpointDependencies.ts:372-384) */
+int kmz_tail_service_first(kmz_ctx *ctx, uint64_t *first, uint64_t cap);
+
+/* ---- RiskAnalyzer.RealtimeRisk's per-service sums (RiskAnalyzer.ts:18, 228-248) */
+/* Over the finalised groups of the last stats run (after any multi-GPU merge):
+ * the groups of stats endpoint e belong to service sid_of_ep[e]; is_5xx[s]
+ * marks status id s as a 5xx.  Per service, over its groups with combined > 0:
+ *   wsum  = sum(cv * combined), in ascending group index (bit-equal to the
+ *           host's per-row sum in that order)
+ *   count = sum(combined), err = sum(combined of 5xx groups)
+ *   first = smallest first index (UINT64_MAX: no group) -- the service order */
+typedef struct kmz_service_sum {
+  double wsum, count, err;
+  uint64_t first;
+} kmz_service_sum;
+int kmz_service_map_set(kmz_ctx *ctx, const uint32_t *sid_of_ep, uint32_t n_ep, uint32_t n_sid, const uint8_t *is_5xx,
+                        uint32_t n_status);
+int kmz_service_sums(kmz_ctx *ctx, kmz_service_sum *out, uint64_t cap);
 /* copy the results: details and pairs in no particular order; has_in[e] = 1
  * when endpoint e's merged row has a non-empty dependingBy */
 int kmz_tail_get(kmz_ctx *ctx, kmz_tail_detail *details, uint64_t dcap, kmz_tail_pair *pairs, uint64_t pcap,

@@ -107,6 +107,7 @@ DEP_ENTRY_DTYPE = np.dtype([("key", "<u8"), ("row", "<u8"), ("span", "<u8"), ("p
 TAIL_DETAIL_DTYPE = np.dtype([("svc", "<u4"), ("lsvc", "<u4"), ("distance", "<u4"), ("count", "<u4"),
                               ("depending_by", "<u4"), ("depending_on", "<u4")])
 TAIL_PAIR_DTYPE = np.dtype([("svc", "<u4"), ("consumer", "<u4"), ("consumes", "<u4")])
+SERVICE_SUM_DTYPE = np.dtype([("wsum", "<f8"), ("count", "<f8"), ("err", "<f8"), ("first", "<u8")])  # kmz_service_sum
 
 
 class TailMap(C.Structure):
@@ -184,6 +185,9 @@ SIGNATURES = [
     ("kmz_tail_run", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("kmz_tail_get", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, _P, C.c_uint64]),
     ("kmz_tail_service_stats", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint32)]),
+    ("kmz_tail_service_first", C.c_int, [_P, _P, C.c_uint64]),
+    ("kmz_service_map_set", C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, C.c_uint32]),
+    ("kmz_service_sums", C.c_int, [_P, _P, C.c_uint64]),
     ("kmz_finalize", C.c_int, [_P]),
     ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
     ("kmz_host_alloc", _P, [C.c_uint64]),

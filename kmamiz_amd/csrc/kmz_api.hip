@@ -87,6 +87,14 @@ struct kmz_ctx {
   uint32_t tl_rel_dist = 0;  // distances in the last run's relying table (0: not complete, use the details)
   bool tl_map = false, tl_ran = false;
   uint64_t tl_acap = 0, tl_pacap = 0, tl_lcap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0;
+  DevBuf tl_sfirst;              // per service: first row (k_tail_service_rows)
+  void *tl_host = nullptr;       // pinned: the tail's counters, per-service stats, relying table, first rows
+  size_t tl_host_bytes = 0;
+  // RiskAnalyzer.RealtimeRisk's per-service sums (k_service_sums): CSR of the
+  // services' stats endpoints, 5xx status mask, output
+  DevBuf sv_off, sv_eps, sv_5xx, sv_out;
+  uint32_t sv_n_ep = 0, sv_n_sid = 0, sv_n_status = 0;
+  bool sv_map = false;
   bool ctab_dirty = true;  // the chain table holds entries no list records (new, or a list overflowed)
   int path = 0;             // kmz_info.path of the last dependency run
   bool sstats = false;      // shape-level K3 partials computed in this run
@@ -332,7 +340,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
-                    &c->tl_sstat, &c->tl_rel, &c->o_key, &c->o_val, &c->o_out,
+                    &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
+                    &c->o_key, &c->o_val, &c->o_out,
                     &c->o_rts, &c->o_rsh, &c->j_buf, &c->j_elem, &c->j_state, &c->j_jsc, &c->j_mask,
                     &c->j_cnt, &c->j_off, &c->j_csc, &c->j_small, &c->j_starts, &c->j_slices, &c->j_tslot,
                     &c->j_stab, &c->j_ttab, &c->j_reps, &c->j_smap, &c->j_tmap};
@@ -342,6 +351,7 @@ void kmz_destroy(kmz_ctx *c) {
     if (g.exec) hipGraphExecDestroy(g.exec);
   if (c->hpin) hipHostFree(c->hpin);
   if (c->hep) hipHostFree(c->hep);
+  if (c->tl_host) hipHostFree(c->tl_host);
   if (c->side) {
     hipStreamSynchronize(c->side);
     hipStreamDestroy(c->side);
@@ -801,18 +811,29 @@ static int run_shape_stats(kmz_ctx *c) {
     const uint32_t S = (KMZ_K3_SMALL_S && nt <= 64) ? 1u
                                                      : std::max<uint32_t>(1, std::min<uint32_t>({64u, 2048 / Pp,
                                                                                                   std::max(nt / 32, 1u)}));
-    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, k3_dir_words(n, Pp, S) * 4 + 4) ||
-        ensure(c, c->k3part, (size_t)S * 6 * Gs * 8) || ensure(c, c->tile_tmp, (size_t)nt * 16))
+    // larger batches: work items sized by each partition's records (the
+    // partitions are far from equal: hot endpoints); KMZ_ABLATE bit 14: S
+    // fixed slices per partition, for comparison
+    const bool bal = S > 1 && !(c->ablate & (1u << 14));
+    const uint32_t Sd = bal ? 1u : S;  // the directory's slices ([partition][tile] for the balanced reduce)
+    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, (k3_dir_words(n, Pp, Sd) + 2 * Pp + 2) * 4) ||
+        ensure(c, c->k3part, bal ? k3_bal_part_bytes((uint32_t)Gs) : (size_t)S * 6 * Gs * 8) ||
+        ensure(c, c->tile_tmp, (size_t)nt * 16))
       return KMZ_E_HIP;
     {
       Timed t(c, KMZ_K_STATS);
       launch_k3_produce(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_shapes,
-                        c->n_status, S, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp));
+                        c->n_status, Sd, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp));
     }
     {
       Timed t(c, KMZ_K_REDUCE);
-      launch_k3_reduce(c->stream, n, (uint32_t)Gs, c->index_base, c->k3pool.p, P<uint32_t>(c->k3dir),
-                       P<unsigned long long>(c->k3part), S, sg);
+      if (bal)
+        launch_k3_reduce_bal(c->stream, n, (uint32_t)Gs, c->index_base, c->k3pool.p, P<uint32_t>(c->k3dir),
+                             P<uint32_t>(c->k3dir) + k3_dir_words(n, Pp, 1), P<unsigned long long>(c->k3part), sg,
+                             (c->ablate & (1u << 15)) != 0);  // (bit 15, test knob: unpacked accumulators)
+      else
+        launch_k3_reduce(c->stream, n, (uint32_t)Gs, c->index_base, c->k3pool.p, P<uint32_t>(c->k3dir),
+                         P<unsigned long long>(c->k3part), S, sg);
     }
   } else if (Gs <= 1024 && !(c->ablate & 8)) {
     const uint32_t nb = k3_small_blocks(n);
@@ -1706,24 +1727,41 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
         ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
         ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
         ensure(c, c->tl_fkey, acap * 8) || ensure(c, c->tl_fval, acap * 4) ||
-        ensure(c, c->tl_sstat, (size_t)c->tl_n_svc * 32) || ensure(c, c->tl_rel, (size_t)c->tl_n_svc * c->tl_n_dist * 4))
+        ensure(c, c->tl_sstat, (size_t)c->tl_n_svc * 32) || ensure(c, c->tl_rel, (size_t)c->tl_n_svc * c->tl_n_dist * 4) ||
+        ensure(c, c->tl_sfirst, (size_t)c->tl_n_svc * 8 + 8))
       return KMZ_E_HIP;
+    // the read-back (pinned): counters [64 B], stats [n_svc x 8 u32], first rows [n_svc u64], relying table
+    const uint32_t nd_run = c->tl_n_dist;
+    const size_t hb = 64 + (size_t)c->tl_n_svc * 40 + (size_t)c->tl_n_svc * nd_run * 4;
+    if (c->tl_host_bytes < hb) {
+      if (c->tl_host) hipHostFree(c->tl_host);
+      c->tl_host_bytes = 0;
+      if (hipHostMalloc(&c->tl_host, hb, hipHostMallocDefault) != hipSuccess) {
+        c->tl_host = nullptr;
+        return fail(c, KMZ_E_HIP, "hipHostMalloc (tail read-back)");
+      }
+      c->tl_host_bytes = hb;
+    }
     {
       Timed t(c, KMZ_K_MEMSET);
-      HIPCHK(c, hipMemsetAsync(c->tl_lset.p, 0, lcap * 8, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_akey.p, 0, acap * 8, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_aval.p, 0, acap * 16, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_pset.p, 0, pcap * 8, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_pkey.p, 0, pacap * 8, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_pval.p, 0, pacap * 4, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_hasin.p, 0, c->tl_n_ep ? c->tl_n_ep : 1, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_cnt.p, 0, 64, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_fkey.p, 0, acap * 8, c->stream));
-      HIPCHK(c, hipMemsetAsync(c->tl_fval.p, 0, acap * 4, c->stream));
+      FillArgs f, g;
+      f.add(c->tl_lset.p, lcap * 8, 0);
+      f.add(c->tl_akey.p, acap * 8, 0);
+      f.add(c->tl_aval.p, acap * 16, 0);
+      f.add(c->tl_pset.p, pcap * 8, 0);
+      f.add(c->tl_pkey.p, pacap * 8, 0);
+      f.add(c->tl_pval.p, pacap * 4, 0);
+      f.add(c->tl_hasin.p, c->tl_n_ep ? c->tl_n_ep : 1, 0);
+      f.add(c->tl_cnt.p, 64, 0);
+      g.add(c->tl_fkey.p, acap * 8, 0);
+      g.add(c->tl_fval.p, acap * 4, 0);
       if (c->tl_n_svc) {
-        HIPCHK(c, hipMemsetAsync(c->tl_sstat.p, 0, (size_t)c->tl_n_svc * 32, c->stream));
-        HIPCHK(c, hipMemsetAsync(c->tl_rel.p, 0, (size_t)c->tl_n_svc * c->tl_n_dist * 4, c->stream));
+        g.add(c->tl_sstat.p, (size_t)c->tl_n_svc * 32, 0);
+        g.add(c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4, 0);
+        g.add(c->tl_sfirst.p, (size_t)c->tl_n_svc * 8, 0xFF);
       }
+      launch_fill(c->stream, f);
+      launch_fill(c->stream, g);
     }
     unsigned long long *cnt64 = P<unsigned long long>(c->tl_cnt);  // [0] flags (u32), [1] details, [2] pairs
     {
@@ -1733,13 +1771,29 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
                   P<unsigned long long>(c->tl_lset), lcap, P<unsigned long long>(c->tl_akey), P<uint32_t>(c->tl_aval),
                   acap, P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey),
                   P<uint32_t>(c->tl_pval), pacap, P<uint8_t>(c->tl_hasin), P<unsigned long long>(c->tl_fkey),
-                  P<uint32_t>(c->tl_fval), acap, P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), c->tl_n_dist,
-                  P<unsigned int>(c->tl_cnt), P<uint32_t>(c->tl_det), P<uint32_t>(c->tl_pairs), cnt64 + 1);
+                  P<uint32_t>(c->tl_fval), acap, P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), nd_run,
+                  P<unsigned int>(c->tl_cnt), P<uint32_t>(c->tl_det), P<uint32_t>(c->tl_pairs), cnt64 + 1,
+                  // diagnostic knobs (timing only, wrong results): KMZ_ABLATE bit 7 skips the
+                  // link keys, bit 12 the cohesion pairs
+                  ((c->ablate >> 7) & 1u) | (((c->ablate >> 12) & 1u) << 1));
+      launch_tail_service_rows(c->stream, P<unsigned long long>(c->epp) + c->n_dep, P<uint32_t>(c->tl_svc),
+                               P<uint8_t>(c->tl_hasin), c->tl_n_ep, P<uint32_t>(c->tl_sstat),
+                               P<unsigned long long>(c->tl_sfirst));
     }
-    unsigned long long h[5];
-    HIPCHK(c, hipMemcpyAsync(h, c->tl_cnt.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    // one read-back and one synchronisation for the counters and every per-service output
+    char *hh = static_cast<char *>(c->tl_host);
+    HIPCHK(c, hipMemcpyAsync(hh, c->tl_cnt.p, 64, hipMemcpyDeviceToHost, c->stream));
+    if (c->tl_n_svc) {
+      HIPCHK(c, hipMemcpyAsync(hh + 64, c->tl_sstat.p, (size_t)c->tl_n_svc * 32, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemcpyAsync(hh + 64 + (size_t)c->tl_n_svc * 32, c->tl_sfirst.p, (size_t)c->tl_n_svc * 8,
+                               hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemcpyAsync(hh + 64 + (size_t)c->tl_n_svc * 40, c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4,
+                               hipMemcpyDeviceToHost, c->stream));
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
+    unsigned long long h[5];
+    memcpy(h, hh, sizeof(h));
     const uint32_t fl = (uint32_t)h[0];
     if (fl & F_RANGE) return fail(c, KMZ_E_RANGE, "edge key endpoint outside the tail map");
     if (fl & F_TRIPLE_OVERFLOW) {
@@ -1763,7 +1817,7 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
     c->tl_deep = (uint32_t)h[3];
     if (c->tl_deep >= c->tl_n_dist && (uint64_t)c->tl_n_svc * (c->tl_deep + 1) <= (1ull << 26))
       c->tl_n_dist = c->tl_deep + 1;
-    c->tl_rel_dist = c->tl_deep ? 0 : c->tl_n_dist;
+    c->tl_rel_dist = c->tl_deep ? 0 : nd_run;
     c->tl_ran = true;
     if (n_details) *n_details = h[1];
     if (n_pairs) *n_pairs = h[2];
@@ -1778,8 +1832,56 @@ int kmz_tail_service_stats(kmz_ctx *c, uint32_t *stats, uint64_t scap, uint32_t 
   *n_dist = c->tl_rel_dist;
   const uint64_t ns = (uint64_t)c->tl_n_svc * 8, nd = (uint64_t)c->tl_n_svc * c->tl_rel_dist;
   if ((stats && scap < ns) || (by_dist && dcap < nd)) return fail(c, KMZ_E_ARG, "output too small");
-  if (stats && ns) HIPCHK(c, hipMemcpyAsync(stats, c->tl_sstat.p, ns * 4, hipMemcpyDeviceToHost, c->stream));
-  if (by_dist && nd) HIPCHK(c, hipMemcpyAsync(by_dist, c->tl_rel.p, nd * 4, hipMemcpyDeviceToHost, c->stream));
+  const char *hh = static_cast<const char *>(c->tl_host);  // (copied back by kmz_tail_run)
+  if (stats && ns) memcpy(stats, hh + 64, ns * 4);
+  if (by_dist && nd) memcpy(by_dist, hh + 64 + (size_t)c->tl_n_svc * 40, nd * 4);
+  return KMZ_OK;
+}
+
+int kmz_tail_service_first(kmz_ctx *c, uint64_t *first, uint64_t cap) {
+  if (!c || (!first && cap)) return KMZ_E_ARG;
+  if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
+  if (cap < c->tl_n_svc) return fail(c, KMZ_E_ARG, "output too small");
+  if (c->tl_n_svc) memcpy(first, static_cast<const char *>(c->tl_host) + 64 + (size_t)c->tl_n_svc * 32, (size_t)c->tl_n_svc * 8);
+  return KMZ_OK;
+}
+
+int kmz_service_map_set(kmz_ctx *c, const uint32_t *sid_of_ep, uint32_t n_ep, uint32_t n_sid, const uint8_t *is_5xx,
+                        uint32_t n_status) {
+  if (!c || (n_ep && !sid_of_ep) || (n_status && !is_5xx) || !n_status) return KMZ_E_ARG;
+  std::vector<uint32_t> off((size_t)n_sid + 1, 0), eps(n_ep);
+  for (uint32_t e = 0; e < n_ep; ++e) {
+    if (sid_of_ep[e] >= n_sid) return fail(c, KMZ_E_RANGE, "service id out of range");
+    ++off[sid_of_ep[e] + 1];
+  }
+  for (uint32_t v = 0; v < n_sid; ++v) off[v + 1] += off[v];
+  std::vector<uint32_t> at(off.begin(), off.end() - 1);
+  for (uint32_t e = 0; e < n_ep; ++e) eps[at[sid_of_ep[e]]++] = e;  // ascending within each service
+  if (ensure(c, c->sv_off, off.size() * 4) || ensure(c, c->sv_eps, (size_t)n_ep * 4 + 4) ||
+      ensure(c, c->sv_5xx, n_status) || ensure(c, c->sv_out, (size_t)n_sid * sizeof(kmz_service_sum) + 8))
+    return KMZ_E_HIP;
+  HIPCHK(c, hipMemcpyAsync(c->sv_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice, c->stream));
+  if (n_ep) HIPCHK(c, hipMemcpyAsync(c->sv_eps.p, eps.data(), (size_t)n_ep * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->sv_5xx.p, is_5xx, n_status, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->sv_n_ep = n_ep;
+  c->sv_n_sid = n_sid;
+  c->sv_n_status = n_status;
+  c->sv_map = true;
+  return KMZ_OK;
+}
+
+int kmz_service_sums(kmz_ctx *c, kmz_service_sum *out, uint64_t cap) {
+  if (!c || (!out && cap)) return KMZ_E_ARG;
+  if (!c->sv_map) return fail(c, KMZ_E_STATE, "kmz_service_map_set first");
+  if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
+  if ((uint64_t)c->sv_n_ep * c->sv_n_status != c->G) return fail(c, KMZ_E_ARG, "service map size differs from the groups");
+  if (cap < c->sv_n_sid) return fail(c, KMZ_E_ARG, "output too small");
+  if (!c->sv_n_sid) return KMZ_OK;
+  launch_service_sums(c->stream, P<kmz_group>(c->grp_final), c->sv_n_status, P<uint32_t>(c->sv_off),
+                      P<uint32_t>(c->sv_eps), P<uint8_t>(c->sv_5xx), c->sv_n_sid, P<kmz_service_sum>(c->sv_out));
+  HIPCHK(c, hipMemcpyAsync(out, c->sv_out.p, (size_t)c->sv_n_sid * sizeof(kmz_service_sum), hipMemcpyDeviceToHost,
+                           c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return KMZ_OK;
 }

@@ -80,6 +80,13 @@ void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape
                        const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
                        uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint32_t S, unsigned int *counters,
                        unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp);
+// balanced K3 reduce (directory [partition][tile], i.e. produced with S = 1):
+// plan = 2 P + 1 u32 scratch, part = k3_bal_part_bytes(G)
+void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
+                          const uint32_t *dir, uint32_t *plan, unsigned long long *part, unsigned long long *grp,
+                          bool unpacked = false);
+uint32_t k3_bal_items(uint32_t G);
+uint64_t k3_bal_part_bytes(uint32_t G);
 void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
                       const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp);
 // small key spaces (G <= 1024): per-chunk LDS partials, part = [k3_small_blocks(n)][6][G] u64
@@ -145,7 +152,13 @@ void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned l
                  uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
                  uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned long long *fkey, uint32_t *fval,
                  uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
-                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts);
+                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts, uint32_t knobs = 0);
+// per service: rows / gateway into sstat slots 6 / 7, first row into sfirst (after launch_tail)
+void launch_tail_service_rows(hipStream_t s, const unsigned long long *epf, const uint32_t *svc, const uint8_t *hasin,
+                              uint32_t n_ep, uint32_t *sstat, unsigned long long *sfirst);
+// RiskAnalyzer.RealtimeRisk's per-service sums over the finalised groups
+void launch_service_sums(hipStream_t s, const kmz_group *grp, uint32_t n_status, const uint32_t *off, const uint32_t *eps,
+                         const uint8_t *is5, uint32_t n_sid, kmz_service_sum *out);
 
 // multi-GPU sharding guard (kmz_guard.hip)
 void launch_unresolved(hipStream_t s, const uint64_t *pid, const uint32_t *dp, uint32_t n, unsigned long long *out,

@@ -319,6 +319,213 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Balanced K3 reduce.  Partitions are far from equal: config 5's hot
+// endpoints put 6.2x the mean record count into one partition (the mesh: 1.8x),
+// so with a fixed number of slices per partition the hot partitions' slices
+// set the kernel's length.  Here the directory is [partition][tile]; k3_psum
+// counts each partition's records, k3_plan gives partition p
+// S_p = ceil(T_p / target) work items (about K3_ITEMS in all, each a
+// contiguous tile range of its partition: records are spread evenly over the
+// tiles), and k3_reduce_bal runs one workgroup per item.  k3_combine_bal folds
+// the items of each partition.
+// ---------------------------------------------------------------------------
+constexpr uint32_t K3_ITEMS = 1536;       // ~2 rounds of 3 workgroups per CU
+constexpr uint32_t K3_ITEM_MIN = 4096;    // records: below that an item is not worth its partial write-out
+
+__global__ void __launch_bounds__(256) k3_psum(const uint32_t *__restrict__ dir, uint32_t ntiles,
+                                               uint32_t *__restrict__ tot) {
+  __shared__ uint32_t red[4];
+  const uint32_t *row = dir + (uint64_t)blockIdx.x * ntiles;
+  uint32_t s = 0;
+  for (uint32_t k = threadIdx.x; k < ntiles; k += 256) {
+    const uint32_t x = row[k], o = x >> 16, c = x & 0xFFFF;
+    s += (o + c <= K3T) ? c : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) tot[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// one workgroup: S_p and the exclusive scan item_off[0..P] (P <= K3PMAX)
+__global__ void __launch_bounds__(1024) k3_plan(const uint32_t *__restrict__ tot, uint32_t P, uint32_t ntiles,
+                                                uint32_t *__restrict__ item_off) {
+  __shared__ unsigned long long rsum[16];
+  __shared__ uint32_t wsum[16];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t c = t < P ? tot[t] : 0;
+  unsigned long long r = c;
+  for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+  if (lane == 0) rsum[w] = r;
+  __syncthreads();
+  unsigned long long R = 0;
+  for (int k = 0; k < 16; ++k) R += rsum[k];
+  const unsigned long long target = max((R + K3_ITEMS - 1) / K3_ITEMS, (unsigned long long)K3_ITEM_MIN);
+  const uint32_t sp = t < P ? (uint32_t)min((c + target - 1) / target, (unsigned long long)ntiles) : 0;
+  const uint32_t s1 = t < P ? max(sp, 1u) : 0;
+  uint32_t x = s1;  // inclusive scan over the workgroup
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+  if (t < P) item_off[t] = before + x - s1;
+  if (t == P - 1) item_off[P] = before + x;
+}
+
+// item -> (partition, tile range); partials [item][6][K3R] in the final form
+// of the group partials (first index global).  The packed accumulators of
+// k3_reduce are used when the item holds < 2^22 records (counted first from
+// its directory words: records need not be spread evenly, e.g. input sorted by
+// endpoint), else the unpacked ones -- one 48 KB LDS block either way.
+__global__ void __launch_bounds__(K3RT) k3_reduce_bal(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
+                                                      uint32_t ntiles, uint32_t P, const uint32_t *__restrict__ item_off,
+                                                      uint32_t G, uint64_t index_base, uint32_t upk,
+                                                      unsigned long long *__restrict__ part) {
+  __shared__ unsigned long long acc[6 * K3R];
+  constexpr uint32_t NW = K3RT / 64;
+  __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB], wred[NW];
+  const uint32_t item = blockIdx.x;
+  if (item >= item_off[P]) return;  // (the grid is an upper bound; uniform over the workgroup)
+  uint32_t lo = 0, hi = P;  // the partition: item_off[p] <= item < item_off[p + 1]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (item_off[mid] <= item) lo = mid; else hi = mid;
+  }
+  const uint32_t p = lo, j = item - item_off[p], sp = item_off[p + 1] - item_off[p];
+  const uint64_t tb = (uint64_t)j * ntiles / sp, te = (uint64_t)(j + 1) * ntiles / sp;
+  const uint32_t *row = dir + (uint64_t)p * ntiles;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t nrec = 0;
+  for (uint64_t k = tb + threadIdx.x; k < te; k += K3RT) {
+    const uint32_t x = row[k];
+    nrec += ((x >> 16) + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) nrec += __shfl_xor(nrec, o, 64);
+  if (lane == 0) wred[w] = nrec;
+  for (uint32_t k = threadIdx.x; k < 6 * K3R; k += K3RT) acc[k] = k < 5 * K3R ? 0ull : ~0ull;
+  __syncthreads();
+  uint32_t tot = 0;
+  for (uint32_t k = 0; k < NW; ++k) tot += wred[k];
+  const bool pack = tot < (1u << 22) && !upk;  // (upk: test knob)
+  // packed: cs, s2, s1b, s2h, tsx, fst32 (u32) -- unpacked: cnt, s1, s2a, s2b, tsx, fst
+  unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
+                     *a_fst = acc + 5 * K3R;
+  uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
+  constexpr uint32_t U = 4;
+  for (uint64_t k0 = tb + (uint64_t)w * K3RB; k0 < te; k0 += (uint64_t)NW * K3RB) {
+    const uint64_t k = k0 + lane;  // this lane's run: tile k
+    const uint32_t x = k < te ? row[k] : 0;
+    const uint32_t o = x >> 16;
+    const uint32_t c = (o + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;
+    uint32_t incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    r_pre[w][lane] = incl - c;
+    r_off[w][lane] = (uint32_t)(k < te ? k : 0) * K3T + o;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    for (uint32_t q0 = 0; q0 < total; q0 += 64 * U) {
+      Rec xr[U];
+      uint32_t run[U];
+      bool v[U];
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        const uint32_t q = q0 + u * 64 + lane;
+        v[u] = q < total;
+        uint32_t jj = 0;
+#pragma unroll
+        for (uint32_t b = 32; b; b >>= 1)
+          if (r_pre[w][jj + b] <= q) jj += b;
+        run[u] = jj;
+        xr[u] = pool[v[u] ? r_off[w][jj] + (q - r_pre[w][jj]) : 0];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < U; ++u) {
+        if (!v[u]) continue;
+        const uint32_t kl = xr[u].w & (K3R - 1);
+        const uint64_t d = xr[u].d, dd = d * d;
+        const uint64_t tile = k0 + run[u];
+        if (pack) {
+          if (d < K3_SMALL_D) {
+            atomicAdd(&a0[kl], (1ull << 42) + d);
+            atomicAdd(&a1[kl], (unsigned long long)dd);
+          } else {  // (rare)
+            atomicAdd(&a0[kl], 1ull << 42);
+            atomicAdd(&a2[kl], (unsigned long long)d);
+            atomicAdd(&a1[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
+            atomicAdd(&a3[kl], (unsigned long long)(dd >> 32));
+          }
+          atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
+          atomicMin(&a_fst32[kl], (uint32_t)(tile - tb) * K3T + (xr[u].w >> 10));
+        } else {
+          atomicAdd(&a0[kl], 1ull);
+          atomicAdd(&a1[kl], (unsigned long long)d);
+          atomicAdd(&a2[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
+          atomicAdd(&a3[kl], (unsigned long long)(dd >> 32));
+          atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
+          atomicMin(&a_fst[kl], (unsigned long long)(index_base + tile * K3T + (xr[u].w >> 10)));
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // r_pre / r_off are rewritten by the next batch
+  }
+  __syncthreads();
+  unsigned long long *b = part + (uint64_t)item * 6 * K3R;
+  for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
+    if ((uint64_t)p * K3R + k >= G) break;
+    if (pack) {
+      const unsigned long long cs = a0[k], s2 = a1[k];
+      const uint32_t f = a_fst32[k];
+      b[k] = cs >> 42;
+      b[K3R + k] = (cs & ((1ull << 42) - 1)) + a2[k];
+      b[2 * K3R + k] = s2 & 0xFFFFFFFFull;
+      b[3 * K3R + k] = (s2 >> 32) + a3[k];
+      b[4 * K3R + k] = a_tsx[k];
+      b[5 * K3R + k] = f == ~0u ? ~0ull : index_base + tb * K3T + f;
+    } else {
+      b[k] = a0[k];
+      b[K3R + k] = a1[k];
+      b[2 * K3R + k] = a2[k];
+      b[3 * K3R + k] = a3[k];
+      b[4 * K3R + k] = a_tsx[k];
+      b[5 * K3R + k] = a_fst[k];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k3_combine_bal(const unsigned long long *__restrict__ part,
+                                                      const uint32_t *__restrict__ item_off, uint32_t G,
+                                                      unsigned long long *__restrict__ grp) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+    const uint32_t p = g / K3R, k = g % K3R;
+    unsigned long long c = 0, s1 = 0, s2a = 0, s2b = 0, tsx = 0, fst = ~0ull;
+    for (uint32_t it = item_off[p]; it < item_off[p + 1]; ++it) {
+      const unsigned long long *b = part + (uint64_t)it * 6 * K3R + k;
+      c += b[0];
+      s1 += b[K3R];
+      s2a += b[2 * K3R];
+      s2b += b[3 * K3R];
+      tsx = max(tsx, b[4 * K3R]);
+      fst = min(fst, b[5 * K3R]);
+    }
+    grp[g] = c;
+    grp[G + g] = s1;
+    grp[2ull * G + g] = s2a;
+    grp[3ull * G + g] = s2b;
+    grp[4ull * G + g] = tsx;
+    grp[5ull * G + g] = fst;
+  }
+}
+
 __global__ void __launch_bounds__(256) k3_combine(const unsigned long long *__restrict__ part, uint32_t S, uint32_t G,
                                                   unsigned long long *__restrict__ grp) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
@@ -487,6 +694,23 @@ void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base
                        G, grp);
 }
 
+// balanced: per-partition record counts, the item plan, one workgroup per item
+void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
+                          const uint32_t *dir, uint32_t *plan, unsigned long long *part, unsigned long long *grp,
+                          bool unpacked) {
+  if (!n || !G) return;
+  const uint32_t P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
+  uint32_t *tot = plan, *item_off = plan + P;
+  hipLaunchKernelGGL(k3_psum, dim3(P), dim3(256), 0, s, dir, ntiles, tot);
+  hipLaunchKernelGGL(k3_plan, dim3(1), dim3(1024), 0, s, tot, P, ntiles, item_off);
+  hipLaunchKernelGGL(k3_reduce_bal, dim3(k3_bal_items(G)), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, P, item_off,
+                     G, index_base, unpacked ? 1u : 0u, part);
+  hipLaunchKernelGGL(k3_combine_bal, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part,
+                     item_off, G, grp);
+}
+
+uint32_t k3_bal_items(uint32_t G) { return K3_ITEMS + (G + K3R - 1) / K3R; }  // an upper bound of the plan's items
+uint64_t k3_bal_part_bytes(uint32_t G) { return (uint64_t)k3_bal_items(G) * 6 * K3R * 8; }
 uint32_t k3_partitions(uint32_t G) { return (G + K3R - 1) / K3R; }
 uint32_t k3_pmax() { return K3PMAX; }
 uint64_t k3_pool_bytes(uint32_t n) { return (uint64_t)((n + K3T - 1) / K3T) * K3T * sizeof(Rec); }

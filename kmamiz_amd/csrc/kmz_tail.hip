@@ -45,7 +45,8 @@ namespace kmz {
 
 constexpr uint32_t TAIL_PROBE_MAX = 1024;
 // per-service counters (8 u32 per service, kmz_tail_service_stats)
-constexpr uint32_t TS_NBY = 0, TS_NON = 1, TS_AIS = 2, TS_ADS = 3, TS_CONSUMERS = 4, TS_CONSUMES = 5;
+constexpr uint32_t TS_NBY = 0, TS_NON = 1, TS_AIS = 2, TS_ADS = 3, TS_CONSUMERS = 4, TS_CONSUMES = 5, TS_ROWS = 6,
+                   TS_GATEWAY = 7;
 static_assert(TS_NON == TS_NBY + 1 && TS_ADS == TS_AIS + 1, "the link type (0 CLIENT, 1 SERVER) selects the counter");
 
 // insert `key` (nonzero) into an open-addressing set; true if this call put it there
@@ -125,7 +126,8 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
                                                     uint8_t *__restrict__ hasin, unsigned long long *__restrict__ fkey,
                                                     uint32_t *__restrict__ fval, uint64_t fcap,
                                                     uint32_t *__restrict__ sstat, uint32_t *__restrict__ rel,
-                                                    uint32_t n_dist, unsigned int *__restrict__ counters) {
+                                                    uint32_t n_dist, unsigned int *__restrict__ counters,
+                                                    uint32_t knobs) {
   const uint64_t n = *n_keys;
   uint32_t flags = 0, won_l = 0, won_p = 0;  // first occurrences in the link / pair sets (sizes the next run's sets)
   // winners' details are summed in LDS first (hot (service, linked service,
@@ -151,6 +153,7 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
     uint64_t lk[2];
     lk[side++] = ((uint64_t)svc[s] << 40) | ((uint64_t)cls[a] << 16) | d;
     if (on) lk[side++] = ((uint64_t)svc[a] << 40) | ((uint64_t)cls[s] << 16) | (1u << 15) | d;
+    if (knobs & 1) side = 0;  // (diagnostic knob: no link keys -- timing only, wrong results)
     for (uint32_t t = 0; t < side; ++t) {
       if (!tail_set_put(lset, lcap, lk[t], &flags)) continue;
       ++won_l;
@@ -172,7 +175,7 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
       if (!done) detail_add(dk, 1u, ty == 0, ty == 1, akey, aval, acap, fkey, fval, fcap, sstat, &flags);
     }
     // cohesion: (consumer service, consumed endpoint) at distance 1
-    if (d == 1 && tail_set_put(pset, pcap, ((uint64_t)(s + 1) << 32) | usn[a], &flags)) {
+    if (d == 1 && !(knobs & 2) && tail_set_put(pset, pcap, ((uint64_t)(s + 1) << 32) | usn[a], &flags)) {
       ++won_p;
       const uint64_t p = tail_agg_slot(pkey, pacap, ((uint64_t)(svc[s] + 1) << 32) | usn[a], &flags);
       if (p != pacap) {
@@ -265,17 +268,112 @@ __global__ void __launch_bounds__(256) k_tail_compact(const unsigned long long *
   }
 }
 
+// per service, from the dependency endpoints' merged rows (what
+// toServiceDependencies groups by uniqueServiceName, EndpointDependencies.ts:
+// 372-384): rows (endpoints with a row), gateway (some row without a
+// dependingBy, RiskAnalyzer.ts:155-158) and the first row's global index
+// (the services' output order).  `epf` is the endpoint partial of the first
+// row: (first row << 1 | not external), UINT64_MAX for none.  Integer
+// atomics: the result does not depend on their order.
+__global__ void __launch_bounds__(256) k_tail_service_rows(const unsigned long long *__restrict__ epf,
+                                                           const uint32_t *__restrict__ svc,
+                                                           const uint8_t *__restrict__ hasin, uint32_t n_ep,
+                                                           uint32_t *__restrict__ sstat,
+                                                           unsigned long long *__restrict__ sfirst) {
+  for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < n_ep; e += gridDim.x * 256) {
+    const unsigned long long f = epf[e];
+    if (f == ~0ull) continue;
+    const uint32_t v = svc[e];
+    atomicAdd(&sstat[8 * v + TS_ROWS], 1u);
+    if (!hasin[e]) atomicOr(&sstat[8 * v + TS_GATEWAY], 1u);
+    atomicMin(&sfirst[v], f >> 1);
+  }
+}
+
+void launch_tail_service_rows(hipStream_t s, const unsigned long long *epf, const uint32_t *svc, const uint8_t *hasin,
+                              uint32_t n_ep, uint32_t *sstat, unsigned long long *sfirst) {
+  if (!n_ep) return;
+  hipLaunchKernelGGL(k_tail_service_rows, dim3(std::min<uint32_t>((n_ep + 255) / 256, 1024)), dim3(256), 0, s, epf, svc,
+                     hasin, n_ep, sstat, sfirst);
+}
+
+// RiskAnalyzer.RealtimeRisk's per-service sums over the combined groups
+// (RiskAnalyzer.ts:18, 228-248): for the groups with combined > 0 of the
+// service's endpoints, sum(cv * combined), sum(combined), sum(combined of 5xx
+// statuses) and the smallest first index (the services' output order).  One
+// wave per service walks its groups in ascending group index -- the order in
+// which the host's per-row sums (np.bincount over the rows) add them -- and
+// lane 0 adds the products in that order, so the fp64 sum is the host's bit
+// for bit (no contraction: -ffp-contract=off).  `off` / `eps`: the services'
+// endpoints in ascending order (CSR).
+__global__ void __launch_bounds__(256) k_service_sums(const kmz_group *__restrict__ grp, uint32_t n_status,
+                                                      const uint32_t *__restrict__ off, const uint32_t *__restrict__ eps,
+                                                      const uint8_t *__restrict__ is5, uint32_t n_sid,
+                                                      kmz_service_sum *__restrict__ out) {
+  __shared__ double prod[4][64];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t sid = blockIdx.x * 4 + w;
+  if (sid >= n_sid) return;  // (whole waves; no workgroup barrier below)
+  const uint32_t a = off[sid], m = (off[sid + 1] - a) * n_status;
+  double ws = 0.0;
+  unsigned long long cnt = 0, err = 0, first = ~0ull;
+  for (uint32_t j0 = 0; j0 < m; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    double p = 0.0;
+    bool used = false;
+    if (j < m) {
+      const uint32_t st = j % n_status;
+      const kmz_group &x = grp[(uint64_t)eps[a + j / n_status] * n_status + st];
+      const unsigned long long c = x.combined;
+      if (c) {
+        used = true;
+        p = x.cv * (double)c;
+        cnt += c;
+        if (is5[st]) err += c;
+        first = min(first, (unsigned long long)x.first);
+      }
+    }
+    prod[w][lane] = p;
+    const uint64_t um = __ballot(used);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lane == 0)
+      for (uint64_t b = um; b; b &= b - 1) ws += prod[w][__builtin_ctzll(b)];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o, 64);
+    err += __shfl_xor(err, o, 64);
+    first = min(first, (unsigned long long)__shfl_xor(first, o, 64));
+  }
+  if (lane == 0) {
+    kmz_service_sum r;
+    r.wsum = ws;
+    r.count = (double)cnt;
+    r.err = (double)err;
+    r.first = first;
+    out[sid] = r;
+  }
+}
+
+void launch_service_sums(hipStream_t s, const kmz_group *grp, uint32_t n_status, const uint32_t *off, const uint32_t *eps,
+                         const uint8_t *is5, uint32_t n_sid, kmz_service_sum *out) {
+  if (!n_sid) return;
+  hipLaunchKernelGGL(k_service_sums, dim3((n_sid + 3) / 4), dim3(256), 0, s, grp, n_status, off, eps, is5, n_sid, out);
+}
+
 void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned long long *n_keys, uint64_t n_max,
                  const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
                  uint32_t n_ep, uint32_t n_cls, unsigned long long *lset, uint64_t lcap, unsigned long long *akey,
                  uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
                  uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned long long *fkey, uint32_t *fval,
                  uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
-                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts) {
+                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts, uint32_t knobs) {
   const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + 255) / 256, 1024));
   hipLaunchKernelGGL(k_tail_links, dim3(g), dim3(256), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls,
                      lset, lcap, akey, aval, acap, pset, pcap, pkey, pval, pacap, hasin, fkey, fval, fcap, sstat, rel,
-                     n_dist, counters);
+                     n_dist, counters, knobs);
   const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((acap + 255) / 256, TAIL_COMPACT_BLOCKS));
   hipLaunchKernelGGL(k_tail_compact<0>, dim3(ga), dim3(256), 0, s, akey, aval, acap, links_out, out_counts, rel, n_dist,
                      counters);

@@ -401,6 +401,29 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_get_graph_stats(self.ctx, C.byref(n), C.byref(k)))
         return int(n.value), int(k.value)
 
+    # ---- RiskAnalyzer.RealtimeRisk's per-service sums (RiskAnalyzer.ts:18, 228-248)
+    def set_service_map(self, sid_of_ep: np.ndarray, n_sid: int, is_5xx: np.ndarray):
+        """Services of the stats endpoints (the groups' endpoint ids) and the
+        5xx statuses, for ``service_sums`` (kmz_service_map_set; kept until
+        replaced)."""
+        sid = np.ascontiguousarray(sid_of_ep, dtype=np.uint32)
+        m = np.ascontiguousarray(is_5xx, dtype=np.uint8)
+        L.check(self.ctx, self._lib.kmz_service_map_set(self.ctx, L.ptr(sid), len(sid), int(n_sid), L.ptr(m), len(m)))
+        self._n_sid = int(n_sid)
+
+    def service_sums(self):
+        """Per service over the finalised groups with combined > 0, on the
+        device (kmz_service_sums): -> (order_ids, wsum, cnt, err) exactly as
+        ``tail.service_sums`` returns them for the same rows: services in
+        first-occurrence order, sum(cv * combined) added in ascending group
+        order, sum(combined), sum(combined of 5xx)."""
+        out = np.empty(self._n_sid, dtype=L.SERVICE_SUM_DTYPE)
+        L.check(self.ctx, self._lib.kmz_service_sums(self.ctx, L.ptr(out), len(out)))
+        big = np.iinfo(np.uint64).max
+        present = np.nonzero(out["first"] != big)[0]
+        order = present[np.argsort(out["first"][present], kind="stable")]
+        return order, out["wsum"][order], out["count"][order], out["err"][order]
+
     # ---- profiling -------------------------------------------------------------
     def set_profiling(self, on: bool):
         L.check(self.ctx, self._lib.kmz_set_profiling(self.ctx, 1 if on else 0))

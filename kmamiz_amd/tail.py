@@ -113,11 +113,13 @@ def maps_for_synth(config: int, label_map: Optional[Dict[str, str]] = None) -> T
     return TailMaps(fields, label_map)
 
 
-def run_tail(eng, maps: TailMaps, endpoints: np.ndarray) -> "ServiceTail":
+def run_tail(eng, maps: TailMaps, endpoints: Optional[np.ndarray] = None) -> "ServiceTail":
     """kmz_tail_run over the engine's current edge set (after a dependency run
     and any multi-GPU merge).  Only the per-service counters come back to the
-    host; the link details and cohesion pairs are copied when a list output
-    needs them."""
+    host (one read-back: the link counters, each service's rows, gateway flag
+    and first row); the link details and cohesion pairs are copied when a list
+    output needs them.  ``endpoints`` is no longer needed (kept for callers
+    that pass it)."""
     lib = L.lib()
     if getattr(eng, "_tail_maps", None) is not maps:
         m = maps.c_struct()
@@ -133,8 +135,9 @@ def run_tail(eng, maps: TailMaps, endpoints: np.ndarray) -> "ServiceTail":
     by_dist = np.empty((n_svc, dist.value), dtype=np.uint32)
     L.check(eng.ctx, lib.kmz_tail_service_stats(eng.ctx, L.ptr(stats), stats.size, L.ptr(by_dist), by_dist.size,
                                                   C.byref(dist)))
-    hasin = np.empty(maps.n_ep, dtype=np.uint8)
-    L.check(eng.ctx, lib.kmz_tail_get(eng.ctx, None, 0, None, 0, L.ptr(hasin), len(hasin)))
+    first = np.empty(n_svc, dtype=np.uint64)
+    L.check(eng.ctx, lib.kmz_tail_service_first(eng.ctx, L.ptr(first), n_svc))
+    rows = (stats[:, 6], stats[:, 7] != 0, first)
 
     def fetch():
         det = np.empty(nd_, dtype=L.TAIL_DETAIL_DTYPE)
@@ -144,9 +147,9 @@ def run_tail(eng, maps: TailMaps, endpoints: np.ndarray) -> "ServiceTail":
 
     if dist.value == 0:  # a distance beyond the dense relying table: sum the details instead
         det, pairs = fetch()
-        t = ServiceTail.from_details(maps, det, pairs, hasin, endpoints)
+        t = ServiceTail.from_details(maps, det, pairs, None, None, rows=rows)
     else:
-        t = ServiceTail(maps, stats, by_dist, hasin, endpoints, fetch)
+        t = ServiceTail(maps, stats, by_dist, None, None, fetch, rows=rows)
     t.n_details, t.n_pairs = nd_, npairs_
     return t
 
@@ -162,29 +165,38 @@ class ServiceTail:
     dependingBy / dependingOn, distance-1 AIS/ADS details, cohesion consumers
     and consumes), ``by_dist[svc, d]`` the dependingBy sums per distance."""
 
-    def __init__(self, maps: TailMaps, stats: np.ndarray, by_dist: np.ndarray, hasin: np.ndarray,
-                 endpoints: np.ndarray, fetch=None, details: Optional[np.ndarray] = None,
-                 pairs: Optional[np.ndarray] = None):
+    def __init__(self, maps: TailMaps, stats: np.ndarray, by_dist: np.ndarray, hasin: Optional[np.ndarray],
+                 endpoints: Optional[np.ndarray], fetch=None, details: Optional[np.ndarray] = None,
+                 pairs: Optional[np.ndarray] = None, rows=None):
+        """``rows`` = (endpoints with a row, gateway, first row) per service as
+        kmz_tail_run computes them on the device; else they are derived here
+        from ``endpoints`` (kmz_endpoint records) and ``hasin``."""
         self.maps = maps
         self.stats = stats.astype(np.int64)
         self.by_dist = by_dist
         self._fetch = fetch
         self._details, self._pairs = details, pairs
         n_svc = len(maps.svc_names)
-        rows = np.nonzero(endpoints["has_row"] != 0)[0]
-        rsvc = maps.svc[rows].astype(np.int64)
-        first = np.full(n_svc, np.iinfo(np.uint64).max, dtype=np.uint64)
-        np.minimum.at(first, rsvc, endpoints["first_row"][rows])
-        self.total = np.bincount(rsvc, minlength=n_svc)
-        gw = np.zeros(n_svc, dtype=bool)
-        gw[rsvc[hasin[rows] == 0]] = True
-        self.gateway = gw
+        if rows is not None:
+            total, gw, first = rows
+            self.total = np.asarray(total, dtype=np.int64)
+            self.gateway = np.asarray(gw, dtype=bool)
+            first = np.asarray(first, dtype=np.uint64)
+        else:
+            r = np.nonzero(endpoints["has_row"] != 0)[0]
+            rsvc = maps.svc[r].astype(np.int64)
+            first = np.full(n_svc, np.iinfo(np.uint64).max, dtype=np.uint64)
+            np.minimum.at(first, rsvc, endpoints["first_row"][r])
+            self.total = np.bincount(rsvc, minlength=n_svc)
+            gw = np.zeros(n_svc, dtype=bool)
+            gw[rsvc[hasin[r] == 0]] = True
+            self.gateway = gw
         present = np.nonzero(self.total > 0)[0]
         self.services = present[np.argsort(first[present], kind="stable")]  # first-row order (EndpointDependencies.ts:372-384)
 
     @classmethod
-    def from_details(cls, maps: TailMaps, details: np.ndarray, pairs: np.ndarray, hasin: np.ndarray,
-                     endpoints: np.ndarray) -> "ServiceTail":
+    def from_details(cls, maps: TailMaps, details: np.ndarray, pairs: np.ndarray, hasin: Optional[np.ndarray],
+                     endpoints: Optional[np.ndarray], rows=None) -> "ServiceTail":
         """The same counters summed from the link details and pairs (the path
         for distances beyond the dense table, and the CPU restatement's)."""
         n = len(maps.svc_names)
@@ -205,7 +217,7 @@ class ServiceTail:
         nd = int(d["distance"].max()) + 1 if len(d) else 1
         by_dist = np.zeros((n, nd), dtype=np.int64)
         np.add.at(by_dist, (d["svc"].astype(np.int64), d["distance"].astype(np.int64)), d["depending_by"])
-        return cls(maps, stats, by_dist, hasin, endpoints, None, details, pairs)
+        return cls(maps, stats, by_dist, hasin, endpoints, None, details, pairs, rows=rows)
 
     # -- lists (copied from the device on demand) ----------------------------------
     def _lists(self):

@@ -708,6 +708,48 @@ def _engine_with(knob):
         del os.environ["KMZ_ABLATE"]
 
 
+K3_FIXED_SLICES = 1 << 14  # KMZ_ABLATE: K3 reduce with S fixed slices per partition (no record-balanced items)
+K3_UNPACKED = 1 << 15      # KMZ_ABLATE: the balanced K3 reduce with unpacked accumulators in every item
+
+
+@pytest.mark.parametrize("config,ntr", [(5, 20000), (3, 40000)])
+def test_k3_reduce_variants_equal(engine, config, ntr):
+    """The record-balanced K3 reduce (items sized by each partition's records:
+    config 5's hot partitions hold ~6x the mean), the fixed-slice reduce and
+    the balanced one with unpacked accumulators give byte-identical group
+    partials and groups, equal to the C oracle's combined groups."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+    from oracle import c_oracle
+
+    def run(e):
+        n = e.load_synthetic(config, synth.SEED, 0, ntr)
+        e.run(L.RUN_STATS_TAG)
+        gw = e.partials_words(L.PART_GROUPS)
+        g = np.zeros(gw, np.uint64)
+        e.export_partials(L.PART_GROUPS, g.ctypes.data, gw, False)
+        return n, g, e.groups()
+
+    n, pa, ga = run(engine)
+    assert n > 64 * 2048  # past the one-slice small-batch path
+    for knob in (K3_FIXED_SLICES, K3_UNPACKED):
+        e2 = _engine_with(knob)
+        try:
+            _, pb, gb = run(e2)
+        finally:
+            e2.close()
+        assert pa.tobytes() == pb.tobytes(), knob
+        assert ga.tobytes() == gb.tobytes(), knob
+    batch, _ = synth.host_batch(config, 0, ntr)
+    table = synth.shape_table(config)
+    ref = c_oracle.stats(batch, table.tag_ep, table.n_tag_ep, table.n_status)
+    assert np.array_equal(ga["combined"], ref["combined"])
+    used = ref["combined"] > 0
+    assert np.array_equal(ga["first"][used], ref["first"][used])
+    assert np.array_equal(ga["latest_timestamp"][used], ref["latest_timestamp"][used])
+    np.testing.assert_allclose(ga["mean"][used], ref["mean"][used], rtol=REL, atol=0)
+
+
 @pytest.fixture(scope="module")
 def direct_engine():
     """An engine whose K4 always enumerates directly (KMZ_ABLATE bit 28: every

@@ -163,7 +163,11 @@ def test_tail_full_size_matches_restatement(engine):
     for f in tail.pairs.dtype.names:
         assert np.array_equal(tail.pairs[f], ref.pairs[f]), f
     assert np.array_equal(tail.gateway, ref.gateway)
-    assert np.array_equal(tail.stats, ref.stats)
+    # rows / gateway / first row per service: computed on the device (slots 6, 7
+    # and kmz_tail_service_first) = derived on the host from the endpoints
+    assert np.array_equal(tail.total, ref.total)
+    assert np.array_equal(tail.services, ref.services)
+    assert np.array_equal(tail.stats[:, :6], ref.stats[:, :6])
     nd = min(tail.by_dist.shape[1], ref.by_dist.shape[1])
     assert np.array_equal(tail.by_dist[:, :nd], ref.by_dist[:, :nd])
     assert not tail.by_dist[:, nd:].any() and not ref.by_dist[:, nd:].any()
@@ -307,3 +311,53 @@ def test_service_tail_after_a_json_parse_on_the_engine(engine):
     engine.json_parse(b"not json")  # refused (E_UNSUPPORTED): still a new generation
     c = deps.service_tail()
     assert a.instability() == c.instability()
+
+
+def _synth_service_map(config):
+    """Per stats (tag) endpoint of a synthetic config: its service id (by
+    uniqueServiceName) and the service names, as bench.py builds them."""
+    from kmamiz_amd import synth
+    from kmamiz_amd.ingest import SHAPE_TAGS, UNDEFINED, tag_identity
+
+    n_shapes, n_status, _ = synth.describe(config)
+    sid_of, names = {}, []
+    sid = np.zeros(n_shapes, dtype=np.int64)
+    for sh in range(n_shapes):
+        name, tags = synth.shape_tags(config, sh)
+        usn = tag_identity((name,) + tuple(tags.get(t, UNDEFINED) for t in SHAPE_TAGS))["uniqueServiceName"]
+        sid[sh] = sid_of.setdefault(usn, len(names))
+        if sid[sh] == len(names):
+            names.append(usn)
+    is5 = np.array([str(x).startswith("5") for x in synth.STATUSES[:n_status]], dtype=bool)
+    return sid, names, is5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,ntr", [(5, 60000), (3, 3000), (2, 2000)])
+def test_service_sums_on_device_equal_row_sums(engine, config, ntr):
+    """kmz_service_sums (RiskAnalyzer.RealtimeRisk's per-service sums on the
+    device) = tail.service_sums over the fetched used groups: same service
+    order, counts exact, and sum(cv * combined) bit-equal (both add in
+    ascending group order); the realtime risk from either is identical."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+    from kmamiz_amd.tail import maps_for_synth, realtime_risk_from_sums, run_tail, service_sums
+
+    sid, names, is5 = _synth_service_map(config)
+    n_status = len(is5)
+    engine.load_synthetic(config, synth.SEED, 0, ntr)
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    g = engine.groups()
+    engine.set_service_map(sid, len(names), is5)
+    dev = engine.service_sums()
+    used = np.nonzero(g["combined"] > 0)[0]
+    host = service_sums(sid[used // n_status], len(names), g["combined"][used], g["cv"][used], is5[used % n_status],
+                        g["first"][used])
+    assert np.array_equal(dev[0], host[0])
+    for a, b in zip(dev[1:], host[1:]):
+        assert a.tobytes() == b.tobytes()
+    tail = run_tail(engine, maps_for_synth(config))
+    ra = realtime_risk_from_sums(tail, names, *dev)
+    rb = realtime_risk_from_sums(tail, names, *host)
+    for k in ra:
+        assert ra[k].tobytes() == rb[k].tobytes(), k
