@@ -138,6 +138,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -312,6 +313,8 @@ kmz_ctx *kmz_create(int device, void *stream) {
     return nullptr;
   }
   if (const char *a = getenv("KMZ_ABLATE")) c->ablate = (uint32_t)strtoul(a, nullptr, 0);
+  if (const char *a = getenv("KMZ_ABLATE2")) c->ablate2 = (uint32_t)strtoul(a, nullptr, 0);
+  if (c->ablate2 & 2u) c->tcap = 1ull << 20;  // test knob: an edge set large enough for compact staging from the start
   if (c->ablate & (1u << 30)) c->scap = 256;  // test knob: tiny key staging (overflow + growth paths)
   // counters (u32) and statistics (u64) in one allocation: one fill and one
   // read-back per run (stats64 is a view, not freed on its own)
@@ -928,6 +931,11 @@ static int run_deps(kmz_ctx *c, bool links) {
     const uint64_t nsl = c->tcap / ESLICE, bmean = ((uint64_t)ng * scap + nsl - 1) / nsl;
     const uint64_t bcap = direct ? std::min<uint64_t>(bmean * KMZ_BUCKET_X, std::max<uint64_t>(bmean, (12ull << 30) / 8 / nsl))
                                  : bmean;
+    // direct enumeration stages 4-byte keys where every edge key of the batch
+    // can be compact (dependency endpoints < 2^16; a key with a distance >= 32
+    // is inserted in place) -- half the bytes of the walk's staging writes,
+    // k_key_part and k_key_slice (KMZ_ABLATE2 bit 0: 8-byte keys, for comparison)
+    const bool cmode = direct && compact_staging(c->tcap, c->n_dep) && !(c->ablate2 & 1u);
     void *old_ctab = c->ctab.p;
     c->k4_lb1 = direct ? lb1 : 0;
     c->k4_nsl = (uint32_t)nsl;
@@ -962,7 +970,7 @@ static int run_deps(kmz_ctx *c, bool links) {
                    scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
                    wpos, wcap, P<uint32_t>(c->kwpos_n), P<uint4>(c->cetab), direct,
                    // (test knob 24 forces sig collisions on the first seed only)
-                   c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)));
+                   c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)), cmode);
     }
     {
       Timed t(c, KMZ_K_SETTLE);
@@ -970,7 +978,7 @@ static int run_deps(kmz_ctx *c, bool links) {
                           P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), scap,
                           P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kbucket), bcap,
                           P<uint32_t>(c->kbucket_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
-                          gpos, wcap, c->ablate);
+                          gpos, wcap, c->ablate, cmode);
     }
     {  // ancestries that left their window: one pass, sized on the device (no host round trip)
       Timed t(c, KMZ_K_PEND);
@@ -1210,7 +1218,7 @@ static uint64_t run_key(kmz_ctx *c, uint32_t flags) {
   auto mix = [&](uint64_t v) { k = mix64(k ^ v) + 0x9E3779B97F4A7C15ull; };
   for (uint64_t v : {(uint64_t)flags, c->n, c->index_base, (uint64_t)c->n_shapes, (uint64_t)c->n_status,
                      (uint64_t)c->n_rt, (uint64_t)c->n_tag, (uint64_t)c->n_dep, c->tcap, c->ccap, (uint64_t)c->scap,
-                     (uint64_t)c->mcap, (uint64_t)c->dcap, c->sig_seed, (uint64_t)c->ablate, (uint64_t)c->overlap,
+                     (uint64_t)c->mcap, (uint64_t)c->dcap, c->sig_seed, (uint64_t)c->ablate, (uint64_t)c->ablate2, (uint64_t)c->overlap,
                      (uint64_t)c->k4_now, (uint64_t)c->ctab_dirty, (uint64_t)c->walk_once,
                      (uint64_t)(uintptr_t)c->stream, (uint64_t)(uintptr_t)c->side, (uint64_t)(uintptr_t)c->hpin,
                      (uint64_t)(uintptr_t)c->sid, (uint64_t)(uintptr_t)c->pid, (uint64_t)(uintptr_t)c->kind,

@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     unsigned int *__restrict__ counters, uint32_t *__restrict__ wg_stats, unsigned long long *__restrict__ stage,
     uint32_t scap, uint32_t *__restrict__ stage_n, unsigned long long *__restrict__ defer, uint32_t dcap,
     uint32_t *__restrict__ defer_n, uint32_t *__restrict__ wpos, uint32_t wcap, uint32_t *__restrict__ wpos_n,
-    uint32_t nt, uint32_t lb1, uint32_t lb2, uint32_t ablate) {
+    uint32_t nt, uint32_t lb1, uint32_t lb2, uint32_t ablate, uint32_t cmode) {
   // one 16-byte record per window slot: element hash (x, y), endpoint (z),
   // contracted parent | kind << 16 (w) -- a walk step is one LDS read
   __shared__ uint4 lrec[CW];
@@ -276,20 +276,30 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   // per coarse bin of the edge set's slices (k_key_part takes them from there)
   const uint32_t sub = scap >> lb1;
   const uint32_t tshift = 64u - (uint32_t)__builtin_ctzll(tcap);  // (tcap is ESLICE * 2^k: key_bins)
+  // compact staging (cmode: endpoints < 2^16, >= 64 coarse bins): a compact
+  // key is staged as the low 38 - lb1 <= 32 bits of its x38 (kmz_common.h),
+  // its coarse bin being the top lb1; other keys are inserted in place (rare:
+  // distances >= 32)
+  uint32_t *const stage32 = reinterpret_cast<uint32_t *>(stage);
   auto stage_key = [&](uint64_t key) {
     if (ablate & (1u << 21)) return;  // diagnostic knob: walk only
-    const uint64_t pos = (key * 0x9E3779B97F4A7C15ull) >> tshift;  // eslot(key, tcap): tcap = 2^(64 - tshift)
+    const uint64_t h = ekey_hash(key);
+    const uint64_t pos = h >> tshift;  // eslot(key, tcap): tcap = 2^(64 - tshift)
     unsigned long long &ce = kcache[DIRECT ? (uint32_t)pos & (KCACHE - 1) : 0];
     if (ce == key) return;  // staged recently by this workgroup (races only let a duplicate through)
     ce = key;
-    if (ablate & (1u << 31)) {  // diagnostic knob: insert in place (no staging)
+    if ((ablate & (1u << 31)) || (cmode && !ekey_compact(key))) {  // (knob 31, diagnostic: insert in place)
       edge_insert(key, trip, tcap, &flags);
       return;
     }
     const uint32_t b = (uint32_t)((pos / ESLICE) >> lb2);
     const uint32_t x = atomicAdd(&lbin[b], 1u);
+    const uint64_t at = (((uint64_t)blockIdx.x << lb1) + b) * sub + x;
     if (x < sub) {
-      stage[(((uint64_t)blockIdx.x << lb1) + b) * sub + x] = key;
+      if (cmode)
+        stage32[at] = (uint32_t)((h >> 26) & ((1ull << (38 - lb1)) - 1));
+      else
+        stage[at] = key;
     } else {  // this run is full: insert here (slow: one lane per key); more staging next run
       edge_insert(key, trip, tcap, &flags);
       flags |= F_STAGE_FULL;
@@ -697,17 +707,38 @@ __device__ __forceinline__ void kp_scan(uint32_t *__restrict__ v, uint32_t m, ui
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__restrict__ stage, uint32_t sub,
+// C (compact staging): the runs hold 32-bit x38 residuals below their coarse
+// bin's lb1 bits, and the buckets 32-bit residuals below the slice's
+// lb1 + lb2 bits (kmz_common.h); else whole 64-bit keys
+template <bool C>
+__global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stage_v, uint32_t sub,
                                                    const uint32_t *__restrict__ stage_n, uint32_t nruns, uint32_t lb1,
-                                                   uint32_t lb2, unsigned long long *__restrict__ bucket,
+                                                   uint32_t lb2, void *__restrict__ bucket_v,
                                                    uint64_t bcap, uint32_t *__restrict__ bucket_n,
                                                    unsigned long long *__restrict__ trip, uint64_t tcap,
                                                    unsigned int *__restrict__ counters) {
-  __shared__ unsigned long long sorted[KP_STEP];  // 32 KB
+  using KT = typename std::conditional<C, uint32_t, unsigned long long>::type;
+  const KT *__restrict__ stage = static_cast<const KT *>(stage_v);
+  KT *__restrict__ bucket = static_cast<KT *>(bucket_v);
+  __shared__ KT sorted[KP_STEP];  // 32 KB (16 KB compact)
   __shared__ uint32_t hist[1u << KB2_MAX], off[1u << KB2_MAX], base[1u << KB2_MAX], wsum[KP_T / 64];
   static_assert((1u << KB2_MAX) <= 4 * KP_T, "kp_scan covers the slices of a coarse bin");
   const uint32_t nf = 1u << lb2;
+  const uint32_t ls = lb1 + lb2;  // slices = 2^ls
   uint32_t flags = 0;
+  // fine slice of a staged entry of coarse bin c, and the entry as a bucket entry
+  auto fine = [&](KT v) -> uint32_t {
+    if (C) return (uint32_t)((uint64_t)v >> (38 - ls)) & (nf - 1);  // (v: below the coarse bits)
+    return (uint32_t)(eslot((uint64_t)v, tcap) / ESLICE) & (nf - 1);
+  };
+  auto to_bucket = [&](KT v) -> KT {
+    if (C) return (KT)((uint64_t)v & ((1ull << (38 - ls)) - 1));
+    return v;
+  };
+  auto whole = [&](KT v, uint32_t c) -> uint64_t {
+    if (C) return ekey_from_x38(((uint64_t)c << (38 - lb1)) | (uint64_t)v);
+    return (uint64_t)v;
+  };
   // this workgroup's steps: runs blockIdx.x, +gridDim.x, ..., 4096 keys at a
   // time; the next step's keys are loaded while this one is sorted
   uint32_t r = blockIdx.x, c0 = 0, m = 0;
@@ -717,20 +748,23 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__r
       c0 = 0;
     }
   };
-  uint64_t kn[KP_PER];
+  KT kn[KP_PER];
+  uint32_t nn = 0;  // valid entries of the loaded step
   auto load = [&]() {
-    const unsigned long long *src = stage + (uint64_t)min(r, nruns - 1) * sub;
+    const KT *src = stage + (uint64_t)min(r, nruns - 1) * sub;
+    nn = r < nruns ? min(m - c0, KP_STEP) : 0;
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j) {
       const uint32_t i = c0 + j * KP_T + threadIdx.x;
-      kn[j] = (r < nruns && i < m) ? src[i] : 0;  // (edge keys are nonzero)
+      kn[j] = (r < nruns && i < m) ? src[i] : (KT)0;
     }
   };
   seek();
   load();
   while (r < nruns) {
     const uint32_t c = r & ((1u << lb1) - 1);  // this step's coarse bin
-    uint64_t k[KP_PER];
+    KT k[KP_PER];
+    const uint32_t nv = nn;
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j) k[j] = kn[j];
     c0 += KP_STEP;
@@ -741,8 +775,9 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__r
     uint32_t f[KP_PER], rk[KP_PER];
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j) {
-      f[j] = (uint32_t)(eslot(k[j], tcap) / ESLICE) & (nf - 1);
-      rk[j] = k[j] ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
+      const bool v = j * KP_T + threadIdx.x < nv;
+      f[j] = fine(k[j]);
+      rk[j] = v ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
     }
     __syncthreads();
     for (uint32_t x = threadIdx.x; x < nf; x += KP_T) {
@@ -754,19 +789,18 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__r
     kp_scan(off, nf, wsum);
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j)
-      if (k[j]) sorted[off[f[j]] + rk[j]] = k[j];
+      if (j * KP_T + threadIdx.x < nv) sorted[off[f[j]] + rk[j]] = k[j];
     __syncthreads();
-    // consecutive threads -> consecutive slots of one slice's bucket (the
-    // nonzero keys only: a zero word is never a key)
+    // consecutive threads -> consecutive slots of one slice's bucket
     const uint32_t nz = off[nf - 1] + hist[nf - 1];
     for (uint32_t i = threadIdx.x; i < nz; i += KP_T) {
-      const unsigned long long key = sorted[i];
-      const uint32_t fb = (uint32_t)(eslot(key, tcap) / ESLICE) & (nf - 1);
+      const KT key = sorted[i];
+      const uint32_t fb = fine(key);
       const uint64_t p = (uint64_t)base[fb] + (i - off[fb]);
       if (p < bcap) {
-        bucket[(uint64_t)((c << lb2) + fb) * bcap + p] = key;
+        bucket[(uint64_t)((c << lb2) + fb) * bcap + p] = to_bucket(key);
       } else {
-        edge_insert(key, trip, tcap, &flags);
+        edge_insert(whole(key, c), trip, tcap, &flags);
         flags |= F_STAGE_FULL;
       }
     }
@@ -776,10 +810,13 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const unsigned long long *__r
 }
 
 constexpr uint32_t KS_T = 1024, KS_PER = 8;  // 16 waves per slice, 8 keys per thread in flight
-__global__ void __launch_bounds__(KS_T) k_key_slice(const unsigned long long *__restrict__ bucket, uint64_t bcap,
-                                                    const uint32_t *__restrict__ bucket_n, uint32_t nsl,
+template <bool C>
+__global__ void __launch_bounds__(KS_T) k_key_slice(const void *__restrict__ bucket_v, uint64_t bcap,
+                                                    const uint32_t *__restrict__ bucket_n, uint32_t nsl, uint32_t ls,
                                                     unsigned long long *__restrict__ trip, uint64_t tcap,
                                                     unsigned int *__restrict__ counters) {
+  using KT = typename std::conditional<C, uint32_t, unsigned long long>::type;
+  const KT *__restrict__ bucket = static_cast<const KT *>(bucket_v);
   __shared__ unsigned long long tab[ESLICE];  // 64 KB
   uint32_t flags = 0;
   for (uint32_t b = blockIdx.x; b < nsl; b += gridDim.x) {
@@ -789,25 +826,26 @@ __global__ void __launch_bounds__(KS_T) k_key_slice(const unsigned long long *__
     ulonglong2 *l = reinterpret_cast<ulonglong2 *>(tab);
     for (uint32_t x = threadIdx.x; x < ESLICE / 2; x += KS_T) l[x] = g[x];
     __syncthreads();
-    const unsigned long long *src = bucket + (uint64_t)b * bcap;
+    const KT *src = bucket + (uint64_t)b * bcap;
     for (uint32_t x0 = 0; x0 < m; x0 += KS_T * KS_PER) {
-      unsigned long long k[KS_PER];
+      KT k[KS_PER];
 #pragma unroll
       for (int j = 0; j < (int)KS_PER; ++j) {
         const uint32_t i = x0 + j * KS_T + threadIdx.x;
-        k[j] = i < m ? src[i] : 0;
+        k[j] = i < m ? src[i] : (KT)0;
       }
 #pragma unroll
       for (int j = 0; j < (int)KS_PER; ++j) {
-        if (!k[j] || (flags & F_TRIPLE_OVERFLOW)) continue;  // (a full slice: the run is repeated larger)
-        uint32_t p = (uint32_t)(eslot(k[j], tcap) & (ESLICE - 1));
+        if (x0 + j * KS_T + threadIdx.x >= m || (flags & F_TRIPLE_OVERFLOW)) continue;  // (a full slice: the run is repeated larger)
+        const uint64_t key = C ? ekey_from_x38(((uint64_t)b << (38 - ls)) | (uint64_t)k[j]) : (uint64_t)k[j];
+        uint32_t p = (uint32_t)(eslot(key, tcap) & (ESLICE - 1));
         uint32_t z = 0;
         for (; z < PROBE_MAX; ++z) {
           unsigned long long cur = tab[p];
-          if (cur == k[j]) break;
+          if (cur == key) break;
           if (cur == 0) {
-            cur = atomicCAS(&tab[p], 0ull, k[j]);
-            if (cur == 0 || cur == k[j]) break;
+            cur = atomicCAS(&tab[p], 0ull, (unsigned long long)key);
+            if (cur == 0 || cur == key) break;
           }
           p = (p + 1) & (uint32_t)(ESLICE - 1);
         }
@@ -1011,7 +1049,7 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint32_t pcap, unsigned int *counters, uint32_t *wg_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
                   uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
-                  uint4 *etab, bool direct, uint32_t ablate) {
+                  uint4 *etab, bool direct, uint32_t ablate, bool cmode) {
   const uint32_t nt = chain_tiles(n);
   if (!nt) return;
   uint32_t lb1, lb2;
@@ -1027,11 +1065,16 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
   if (direct)
     hipLaunchKernelGGL(k4_chain<true>, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, etab, n_shapes, n_ep,
                        index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
-                       scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, lb1, lb2, ablate);
+                       scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, lb1, lb2, ablate, cmode ? 1u : 0u);
   else
     hipLaunchKernelGGL(k4_chain<false>, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, etab, n_shapes, n_ep,
                        index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
-                       scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, lb1, lb2, ablate);
+                       scap, stage_n, defer, dcap, defer_n, wpos, wcap, wpos_n, nt, lb1, lb2, ablate, 0u);
+}
+
+bool compact_staging(uint64_t tcap, uint32_t n_ep) {
+  uint32_t lb1, lb2;
+  return key_bins(tcap, &lb1, &lb2) && lb1 >= 6 && n_ep <= 65536;  // (x38 residuals below >= 6 coarse bits: <= 32 bits)
 }
 
 bool key_bins(uint64_t tcap, uint32_t *lb1, uint32_t *lb2) {
@@ -1049,7 +1092,7 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
                          unsigned long long *bucket, uint64_t bcap, uint32_t *bucket_n,
                          const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
-                         uint32_t gcap, uint32_t ablate) {
+                         uint32_t gcap, uint32_t ablate, bool cmode) {
   if (!chain_tiles(n)) return;
   const uint32_t g = chain_grid(n);
   uint32_t lb1, lb2;
@@ -1060,10 +1103,18 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
   }
   const uint32_t nsl = (uint32_t)(tcap / ESLICE), nruns = g << lb1;
   if (direct) {
-    hipLaunchKernelGGL(k_key_part, dim3(std::min<uint32_t>(nruns, 8192)), dim3(KP_T), 0, s, stage, scap >> lb1,
-                       stage_n, nruns, lb1, lb2, bucket, bcap, bucket_n, trip, tcap, counters);
-    hipLaunchKernelGGL(k_key_slice, dim3(std::min<uint32_t>(nsl, 8192)), dim3(KS_T), 0, s, bucket, bcap, bucket_n, nsl,
-                       trip, tcap, counters);
+    const uint32_t gp = std::min<uint32_t>(nruns, 8192), gs = std::min<uint32_t>(nsl, 8192);
+    if (cmode) {
+      hipLaunchKernelGGL(k_key_part<true>, dim3(gp), dim3(KP_T), 0, s, (const void *)stage, scap >> lb1, stage_n,
+                         nruns, lb1, lb2, (void *)bucket, bcap, bucket_n, trip, tcap, counters);
+      hipLaunchKernelGGL(k_key_slice<true>, dim3(gs), dim3(KS_T), 0, s, (const void *)bucket, bcap, bucket_n, nsl,
+                         lb1 + lb2, trip, tcap, counters);
+    } else {
+      hipLaunchKernelGGL(k_key_part<false>, dim3(gp), dim3(KP_T), 0, s, (const void *)stage, scap >> lb1, stage_n,
+                         nruns, lb1, lb2, (void *)bucket, bcap, bucket_n, trip, tcap, counters);
+      hipLaunchKernelGGL(k_key_slice<false>, dim3(gs), dim3(KS_T), 0, s, (const void *)bucket, bcap, bucket_n, nsl,
+                         lb1 + lb2, trip, tcap, counters);
+    }
   } else {
     const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(16, 2048 / g));
     hipLaunchKernelGGL(k_chain_settle, dim3(g, parts), dim3(256), 0, s, stage, scap >> lb1, stage_n, lb1, trip, tcap, defer,

@@ -78,10 +78,39 @@ KMZ_HD uint32_t tag_of(uint64_t k) { return (uint32_t)(mix64(k + 0x9e3779b97f4a7
 // one in LDS from the keys partitioned to it).  A cap that is not a multiple
 // of ESLICE probes the whole table.
 constexpr uint64_t ESLICE = 8192;
-// home slot of an edge key: Fibonacci hashing (one 64-bit multiply; the top
-// bits of the product depend on every key bit), range-reduced like slot_of.
-// For a power-of-two cap it is the product's top log2(cap) bits.
-KMZ_HD uint64_t eslot(uint64_t k, uint64_t cap) { return mulhi64(k * 0x9E3779B97F4A7C15ull, cap); }
+// Edge keys are ancestor << 40 | descendant << 16 | distance << 1 | on.  A key
+// with both endpoints < 2^16 and distance < 32 is *compact*: its 38-bit code
+// (anc 16 | desc 16 | d 5 | on 1) times an odd constant mod 2^38 is a
+// bijection of the codes, so the 38 bits x38 name the key, and a key staged
+// in a slice known from x38's top bits needs only x38's low 32 bits
+// (kmz_chain.hip: direct enumeration stages 4-byte keys).
+constexpr uint64_t EK_PHI = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t EK_M38 = (1ull << 38) - 1;
+constexpr uint64_t ek_inv64(uint64_t a) {  // a^-1 mod 2^64 (a odd): Newton, 6 steps
+  uint64_t x = a;
+  for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+  return x;
+}
+constexpr uint64_t EK_PHI_INV = ek_inv64(EK_PHI);
+static_assert(EK_PHI * EK_PHI_INV == 1, "inverse of the edge-key multiplier");
+KMZ_HD bool ekey_compact(uint64_t k) {
+  return (k >> 56) == 0 && ((k >> 32) & 0xFF) == 0 && ((k >> 6) & 0x3FF) == 0;  // anc, desc < 2^16, d < 32
+}
+KMZ_HD uint64_t ekey_code(uint64_t k) {  // (compact keys)
+  return ((k >> 40) << 22) | (((k >> 16) & 0xFFFF) << 6) | (k & 63);
+}
+KMZ_HD uint64_t ekey_x38(uint64_t k) { return (ekey_code(k) * EK_PHI) & EK_M38; }
+KMZ_HD uint64_t ekey_from_x38(uint64_t x) {
+  const uint64_t c = (x * EK_PHI_INV) & EK_M38;
+  return ((c >> 22) << 40) | (((c >> 6) & 0xFFFF) << 16) | (c & 63);
+}
+// the edge set's hash of a key: x38 in the top bits for compact keys, the
+// 64-bit Fibonacci product for the others (any fixed function of the key will
+// do: the set compares whole keys)
+KMZ_HD uint64_t ekey_hash(uint64_t k) { return ekey_compact(k) ? ekey_x38(k) << 26 : k * EK_PHI; }
+// home slot of an edge key, range-reduced like slot_of.  For a power-of-two
+// cap it is the hash's top log2(cap) bits.
+KMZ_HD uint64_t eslot(uint64_t k, uint64_t cap) { return mulhi64(ekey_hash(k), cap); }
 KMZ_HD uint64_t eset_next(uint64_t pos, uint64_t cap) {
   if (cap % ESLICE) return pos + 1 == cap ? 0 : pos + 1;
   return (pos & ~(ESLICE - 1)) | ((pos + 1) & (ESLICE - 1));

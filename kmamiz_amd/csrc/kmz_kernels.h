@@ -113,11 +113,13 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint32_t pcap, unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
                   uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
-                  uint4 *etab, bool direct, uint32_t ablate = 0);
+                  uint4 *etab, bool direct, uint32_t ablate = 0, bool cmode = false);
 uint32_t chain_grid(uint32_t n);
 // coarse bins per tile workgroup (2^lb1) and slices per coarse bin (2^lb2) of
 // an edge set of tcap slots; false if tcap is not ESLICE * a power of two
 bool key_bins(uint64_t tcap, uint32_t *lb1, uint32_t *lb2);
+// direct enumeration may stage 4-byte keys (kmz_common.h, compact edge keys)
+bool compact_staging(uint64_t tcap, uint32_t n_ep);
 constexpr uint64_t CHAIN_ENTRY_BYTES = 16;  // {sig, parent sig}
 void launch_key_insert(hipStream_t s, const unsigned long long *keys, uint64_t n, unsigned long long *trip,
                        uint64_t tcap, unsigned int *counters);
@@ -128,7 +130,7 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
                          unsigned long long *bucket, uint64_t bcap, uint32_t *bucket_n,
                          const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
-                         uint32_t gcap, uint32_t ablate = 0);
+                         uint32_t gcap, uint32_t ablate = 0, bool cmode = false);
 // zero the chain-table entries this run wrote (instead of a memset of the table)
 void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
                         const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);

@@ -708,6 +708,69 @@ def _engine_with(knob):
         del os.environ["KMZ_ABLATE"]
 
 
+WIDE_KEYS = 1        # KMZ_ABLATE2: direct enumeration stages 8-byte keys (no compact 4-byte keys)
+BIG_EDGE_SET = 2     # KMZ_ABLATE2: the edge set starts at 2^20 slots (compact staging from the first run)
+
+
+def _engine_with2(knob, knob2):
+    import os
+
+    from kmamiz_amd import Engine
+
+    os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"] = str(knob), str(knob2)
+    try:
+        return Engine(0)
+    finally:
+        del os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"]
+
+
+def test_compact_key_staging_equals_wide_keys():
+    """Direct enumeration's 4-byte staged keys (x38 residuals below the slice
+    bits, kmz_common.h) and its 8-byte keys give the same edge set and
+    endpoints on config 5, equal to the C oracle's keys."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    def run(e):
+        e.load_synthetic(5, synth.SEED, 0, 20000)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        return e.triples(), e.endpoints(), e.info()
+
+    out = []
+    for knob2 in (BIG_EDGE_SET, BIG_EDGE_SET | WIDE_KEYS):
+        e = _engine_with2(1 << 28, knob2)
+        try:
+            for _ in range(2):
+                r = run(e)
+            assert r[2]["path"] & 4  # direct enumeration
+            out.append(r)
+        finally:
+            e.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1].tobytes() == out[1][1].tobytes()
+    batch, _ = synth.host_batch(5, 0, 20000)
+    table = synth.shape_table(5)
+    keys, _, _ = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    assert np.array_equal(np.sort(out[0][0]), np.sort(keys))
+
+
+def test_compact_staging_with_distances_past_32():
+    """A 40-deep SERVER/CLIENT chain inside one LDS window: direct enumeration
+    with compact staging inserts its keys of distance >= 32 in place (they have
+    no 38-bit code); the rows equal the oracle's, order-exact."""
+    from kmamiz_amd import Traces
+
+    front = [_deep_span(100000, "SERVER", None, "front")]
+    deep = _deep_trace(40)
+    e = _engine_with2(1 << 28, BIG_EDGE_SET)
+    try:
+        got = Traces([front, deep], engine=e).toEndpointDependencies().toJSON()
+        assert e.info()["path"] & 4
+    finally:
+        e.close()
+    assert got == O.strip_undef(O.Traces([front, deep]).toEndpointDependencies(max_depth=10000).toJSON())
+
+
 K3_FIXED_SLICES = 1 << 14  # KMZ_ABLATE: K3 reduce with S fixed slices per partition (no record-balanced items)
 K3_UNPACKED = 1 << 15      # KMZ_ABLATE: the balanced K3 reduce with unpacked accumulators in every item
 
