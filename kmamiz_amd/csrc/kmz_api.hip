@@ -138,7 +138,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -1365,8 +1365,12 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     // extra slot is another dependent probe round trip)
     // most rows start a new chain (config 5): enumerate directly next time
     if (c->chain_ran) c->k4_auto_direct = s64[S_CHAINS] * 2 > s64[S_ROWS];
+    // (KMZ_ABLATE2 bits 2 / 3, for comparison: load <= 1/2 / <= 1/4 whatever the size)
+    const uint64_t lf_small = (c->ablate2 & 4u) ? 2 : (c->ablate2 & 8u) ? 4 : 8;
+    const uint64_t lf_big = (c->ablate2 & 4u) ? 2 : 4;
     while (c->chain_ran && c->ccap < (1ull << 31) &&
-           (s64[S_CHAINS] * 4 > c->ccap || (s64[S_CHAINS] * 8 > c->ccap && c->ccap * CHAIN_ENTRY_BYTES < (256ull << 20))))
+           (s64[S_CHAINS] * lf_big > c->ccap ||
+            (s64[S_CHAINS] * lf_small > c->ccap && c->ccap * CHAIN_ENTRY_BYTES < (256ull << 20))))
       c->ccap *= 2;
     if ((flags & KMZ_RUN_DEPS) && ((c->ablate & (1u << 31)) ? s64[S_TRIP_OUT] * 8 > c->tcap * 7
                                                            : s64[S_TRIP_OUT] * 2 > c->tcap))

@@ -24,6 +24,8 @@ b power_fixed 16384 --config power
 KMZ_ABLATE2=1 b power_wide 0 --config power
 b mesh 0
 b mesh_fixed 16384
+KMZ_ABLATE2=4 b mesh_lf2 0
+KMZ_ABLATE2=8 b mesh_lf4 0
 b power_nolinks 128 --config power
 b power_nopairs 4096 --config power
 echo K3_DONE
