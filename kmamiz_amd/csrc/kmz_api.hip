@@ -1810,8 +1810,8 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
     if (fl & F_RANGE) return fail(c, KMZ_E_RANGE, "edge key endpoint outside the tail map");
     if (fl & F_TRIPLE_OVERFLOW) {
       if (attempt >= 3) return fail(c, KMZ_E_OVERFLOW, "service tail table overflow");
-      c->tl_acap *= 4;
-      c->tl_pacap *= 4;
+      c->tl_acap = std::max(c->tl_acap * 4, pow2_at_least(nt / 2 + 4096));
+      c->tl_pacap = std::max(c->tl_pacap * 4, pow2_at_least(nt / 4 + 4096));
       c->tl_lcap = std::max(c->tl_lcap * 4, pow2_at_least(4 * nt + 64));
       c->tl_pcap = std::max(c->tl_pcap * 4, pow2_at_least(2 * nt + 64));
       continue;
@@ -1819,9 +1819,12 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
     const uint64_t won_l = (uint32_t)h[4], won_p = (uint32_t)(h[4] >> 32);
     c->tl_lcap = pow2_at_least(2 * won_l + 4096);  // the next run's sets (this run's keys at load <= 1/2)
     c->tl_pcap = pow2_at_least(2 * won_p + 4096);
-    // keep the detail / pair tables at load <= 1/2 for the next run
-    while (h[1] * 2 > c->tl_acap) c->tl_acap *= 2;
-    while (h[2] * 2 > c->tl_pacap) c->tl_pacap *= 2;
+    // the detail / pair tables at load <= 1/2 of this run's counts for the
+    // next run (they start at nt / 2 and nt / 4 slots: config 5 has ~10^5
+    // details for 1.4e7 edge keys, and every slot is filled and scanned per
+    // run); a larger next batch overflows and repeats the tail 4x larger
+    c->tl_acap = pow2_at_least(2 * h[1] + 4096);
+    c->tl_pacap = pow2_at_least(2 * h[2] + 4096);
     c->tl_nd = h[1];
     c->tl_np = h[2];
     // relying-factor distances beyond the dense table: reported, and the

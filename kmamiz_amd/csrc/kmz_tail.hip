@@ -108,7 +108,13 @@ __device__ __forceinline__ void detail_add(uint64_t dk, uint32_t cnt, uint32_t b
   }
 }
 
-constexpr uint32_t TAIL_LAGG = 2048;  // per-workgroup LDS detail slots (40 KB)
+constexpr uint32_t TAIL_LAGG = 1024;  // per-workgroup LDS detail slots (20 KB)
+// Link keys repeat: config 5's 2.7e7 link keys per step hold ~5e4 distinct
+// ones.  A workgroup remembers the link / pair keys it has already put in the
+// global sets (direct-mapped LDS caches); a key found there is in its set, so
+// it is not a first occurrence and needs no global probe.  (A slot overwritten
+// by another key only costs a probe.)
+constexpr uint32_t TAIL_LSEEN = 2048, TAIL_PSEEN = 512;
 
 // link key: svc << 40 | cls << 16 | type << 15 | d   (type 1 = SERVER / dependingOn)
 // detail key: svc << 40 | lsvc << 16 | d
@@ -134,6 +140,9 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
   // distance) entries see one global update per workgroup, not one per link)
   __shared__ unsigned long long lkey[TAIL_LAGG];
   __shared__ uint32_t lval[TAIL_LAGG][3];
+  __shared__ unsigned long long lseen[TAIL_LSEEN], pseen[TAIL_PSEEN];
+  for (uint32_t x = threadIdx.x; x < TAIL_LSEEN; x += blockDim.x) lseen[x] = 0;
+  for (uint32_t x = threadIdx.x; x < TAIL_PSEEN; x += blockDim.x) pseen[x] = 0;
   for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += blockDim.x) {
     lkey[x] = 0;
     lval[x][0] = lval[x][1] = lval[x][2] = 0;
@@ -155,7 +164,11 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
     if (on) lk[side++] = ((uint64_t)svc[a] << 40) | ((uint64_t)cls[s] << 16) | (1u << 15) | d;
     if (knobs & 1) side = 0;  // (diagnostic knob: no link keys -- timing only, wrong results)
     for (uint32_t t = 0; t < side; ++t) {
-      if (!tail_set_put(lset, lcap, lk[t], &flags)) continue;
+      unsigned long long &seen = lseen[(uint32_t)(lk[t] * 0x9E3779B97F4A7C15ull >> 53) & (TAIL_LSEEN - 1)];
+      if (seen == lk[t]) continue;  // put in the set by this workgroup already
+      const bool won = tail_set_put(lset, lcap, lk[t], &flags);
+      seen = lk[t];  // (in the set now, whoever won)
+      if (!won) continue;
       ++won_l;
       const uint32_t c = (uint32_t)(lk[t] >> 16) & 0xFFFFFFu;
       const uint64_t dk = (lk[t] & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
@@ -175,7 +188,16 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
       if (!done) detail_add(dk, 1u, ty == 0, ty == 1, akey, aval, acap, fkey, fval, fcap, sstat, &flags);
     }
     // cohesion: (consumer service, consumed endpoint) at distance 1
-    if (d == 1 && !(knobs & 2) && tail_set_put(pset, pcap, ((uint64_t)(s + 1) << 32) | usn[a], &flags)) {
+    bool pwon = false;
+    if (d == 1 && !(knobs & 2)) {
+      const uint64_t pk = ((uint64_t)(s + 1) << 32) | usn[a];
+      unsigned long long &pseen_e = pseen[(uint32_t)(pk * 0x9E3779B97F4A7C15ull >> 55) & (TAIL_PSEEN - 1)];
+      if (pseen_e != pk) {
+        pwon = tail_set_put(pset, pcap, pk, &flags);
+        pseen_e = pk;
+      }
+    }
+    if (pwon) {
       ++won_p;
       const uint64_t p = tail_agg_slot(pkey, pacap, ((uint64_t)(svc[s] + 1) << 32) | usn[a], &flags);
       if (p != pacap) {
