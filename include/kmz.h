@@ -139,9 +139,11 @@ typedef struct kmz_info {
   uint64_t n_chains;    /* distinct interned ancestor chains (chain-interning path) */
 } kmz_info;
 
-/* Runs of batches below 2^23 spans are replayed from hipGraphs (a run whose
- * launch sequence repeats is captured once): how many runs were replayed so
- * far on this context, and how many graphs it holds (diagnostic). */
+/* With KMZ_HIPGRAPH=1 in the environment at kmz_create, runs of batches
+ * below 2^23 spans are replayed from hipGraphs (a run whose launch sequence
+ * repeats is captured once; off by default: slower than direct launches at a
+ * 2 500-trace tick on MI355X).  How many runs were replayed so far on this
+ * context, and how many graphs it holds (diagnostic). */
 int kmz_get_graph_stats(kmz_ctx *ctx, uint64_t *launches, uint32_t *cached);
 
 /* ---- host ingest: Zipkin JSON -> kmz_spans columns ---- */

@@ -314,6 +314,7 @@ kmz_ctx *kmz_create(int device, void *stream) {
   }
   if (const char *a = getenv("KMZ_ABLATE")) c->ablate = (uint32_t)strtoul(a, nullptr, 0);
   if (const char *a = getenv("KMZ_ABLATE2")) c->ablate2 = (uint32_t)strtoul(a, nullptr, 0);
+  if (const char *a = getenv("KMZ_HIPGRAPH")) if (atoi(a) == 1) c->ablate |= 1u << 13;  // opt-in run graphs
   if (c->ablate2 & 2u) c->tcap = 1ull << 20;  // test knob: an edge set large enough for compact staging from the start
   if (c->ablate & (1u << 30)) c->scap = 256;  // test knob: tiny key staging (overflow + growth paths)
   // counters (u32) and statistics (u64) in one allocation: one fill and one
@@ -1238,12 +1239,14 @@ static uint64_t run_key(kmz_ctx *c, uint32_t flags) {
 }
 
 // Small batches (< 2^23 spans) are launch-bound: ~25 kernels and memsets per
-// run.  A run whose key was seen on the previous run is captured into a
-// hipGraph (stream capture, both streams) and replayed while the key holds;
-// the first run of a key (and any run that grows a buffer) is enqueued
-// directly, so a capture never allocates.  KMZ_ABLATE bit 13 turns it off.
+// run.  With KMZ_HIPGRAPH=1 (or KMZ_ABLATE bit 13) a run whose key was seen
+// on the previous run is captured into a hipGraph (stream capture, both
+// streams) and replayed while the key holds; the first run of a key (and any
+// run that grows a buffer) is enqueued directly, so a capture never
+// allocates.  Off by default: at a 2 500-trace tick the replays measured
+// 10-20 % slower than direct launches (tools/bench_tick.py).
 static int run_enqueue_graphed(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, unsigned long long *s64) {
-  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && !(c->ablate & (1u << 13)) &&
+  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && (c->ablate & (1u << 13)) &&
                         !c->table_hint && !c->walk_once && !(c->ablate & (32u | 16u));
   if (!eligible) return run_enqueue(c, flags, links, h, s64);
   const uint64_t key = run_key(c, flags);

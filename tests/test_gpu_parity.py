@@ -1201,7 +1201,7 @@ def test_headline_config5_vs_c_oracle_and_tail():
 # ---------------------------------------------------------------------------
 # hipGraph replay of small-batch runs (kmz_api.hip run_enqueue_graphed)
 # ---------------------------------------------------------------------------
-GRAPH_OFF = 1 << 13  # KMZ_ABLATE: no hipGraph capture
+GRAPH_ON = 1 << 13  # KMZ_ABLATE: hipGraph capture / replay of small runs (KMZ_HIPGRAPH=1; off by default)
 
 
 def _run_results(e, flags):
@@ -1225,7 +1225,7 @@ def test_graph_replay_equals_direct_runs(config, ntr):
                                for f in batch.__dataclass_fields__})
     other.duration = other.duration[::-1].copy()
     other.timestamp = other.timestamp + 7
-    on, off = _engine_with(0), _engine_with(GRAPH_OFF)
+    on, off = _engine_with(GRAPH_ON), _engine_with(0)
     try:
         for flags in (L.RUN_STATS_TAG | L.RUN_DEPS, L.RUN_STATS_RT | L.RUN_DEPS | L.RUN_SPAN_LINKS):
             for b in (batch, other, batch):

@@ -35,8 +35,8 @@ def main():
         batch, _ = synth.host_batch(cfg, 0, args.traces)
         table = synth.shape_table(cfg)
         res = {"spans": len(batch)}
-        for mode, knob in (("graph", 0), ("no_graph", 1 << 13), ("no_graph_serial", (1 << 13) | (1 << 25)),
-                           ("graph_serial", 1 << 25)):
+        for mode, knob in (("graph", 1 << 13), ("no_graph", 0), ("no_graph_serial", 1 << 25),
+                           ("graph_serial", (1 << 13) | (1 << 25))):
             os.environ["KMZ_ABLATE"] = str(knob)
             e = Engine(0)
             del os.environ["KMZ_ABLATE"]
