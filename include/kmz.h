@@ -135,7 +135,8 @@ typedef struct kmz_info {
   uint32_t path;        /* last dependency run: bit 0 window join (else global span table),
                            bit 1 chain walk k4_chain (else per-relation global walk k_walk),
                            bit 2 direct enumeration (else chain interning),
-                           bit 3 k_walk redo after a chain-table wait ran out (F_SPIN) */
+                           bit 3 k_walk redo after a chain-table wait ran out (F_SPIN),
+                           bit 4 join and chain walk fused in one kernel (k_join_chain) */
   uint64_t n_chains;    /* distinct interned ancestor chains (chain-interning path) */
 } kmz_info;
 
@@ -439,7 +440,8 @@ void kmz_host_free(void *p);
 #define KMZ_K_TAIL 13    /* service tail: k_tail_links + k_tail_compact           */
 #define KMZ_K_ORDER 14   /* entry order of the reduced graph (KMZ_RUN_DEP_ORDER)  */
 #define KMZ_K_JSON 15    /* K1 on the device: kmz_json_parse's kernels            */
-#define KMZ_K_COUNT 16
+#define KMZ_K_JOINWALK 16 /* K2 + K4 fused: k_join_chain (join, contraction, chain walk) */
+#define KMZ_K_COUNT 17
 int kmz_set_profiling(kmz_ctx *ctx, int on);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);

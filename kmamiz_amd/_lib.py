@@ -35,7 +35,7 @@ ERRORS = {
 }
 
 KERNELS = ["memset", "build", "fixup", "resolve", "stats", "walk", "final", "join", "cert", "reduce", "pend", "check",
-           "settle", "tail", "order", "json"]
+           "settle", "tail", "order", "json", "joinwalk"]
 SYNTH_BOOKINFO, SYNTH_MESH, SYNTH_POWER = 2, 3, 5
 PART_GROUPS, PART_ENDPOINTS, PART_TRIPLES = 0, 1, 2
 

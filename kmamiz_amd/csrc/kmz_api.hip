@@ -138,7 +138,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -871,6 +871,146 @@ static bool k4_direct(kmz_ctx *c) {
   return c->k4_auto_direct && c->n >= (1u << 20) && (++c->k4_since % 64) != 0;
 }
 
+// The join and the chain walk of chain interning as one kernel per LDS window
+// (kmz_fuse.hip), then the certificate, the MISS / PEND fix-ups, the settle of
+// the staged keys and deferred checks, and the pending ancestries -- the same
+// outputs as run_join + the chain path of run_deps.  Taken by window-join runs
+// that intern chains on batches of [KMZ_FUSE_MIN, KMZ_FUSE_MAX) spans: there
+// one kernel instead of two pays (mesh 10^6: 0.57 -> 0.49 ms/step, 4*10^6:
+// 0.70 -> 0.67; Bookinfo 10^6: 0.37 -> 0.24).  At 10^8 spans the fused kernel
+// (64 KB of LDS and ~112 VGPRs per 512-thread workgroup: 2 workgroups per CU,
+// each a chain of dependent round trips: loads, probes, claims) took 2.72 ms
+// against 1.09 + 1.11 ms for k_join_window + the persistent, prefetching
+// k4_chain; at a 2 500-trace tick (68k mesh / 142k config-5 spans: 33 / 70
+// workgroups) 320 / 569 us against 304 / 487 us per run.  KMZ_ABLATE2 bit 4:
+// never fused; bit 5: fused at any size (tests/bench_tick.py).
+#ifndef KMZ_FUSE_MIN
+#define KMZ_FUSE_MIN (1u << 19)
+#endif
+#ifndef KMZ_FUSE_MAX
+#define KMZ_FUSE_MAX (1u << 23)
+#endif
+static bool fused_eligible(kmz_ctx *c) {
+  CertPlan pl;
+  const bool size_ok = (c->n >= KMZ_FUSE_MIN && c->n < KMZ_FUSE_MAX) || (c->ablate2 & 32u);
+  return c->n > 0 && size_ok && !c->k4_now && !(c->ablate2 & 16u) && !c->table_hint && !(c->ablate & (32u | 16u)) &&
+         !c->walk_once && cert_plan((uint32_t)c->n, &pl);
+}
+
+static int run_fused(kmz_ctx *c, bool links) {
+  const uint32_t n = (uint32_t)c->n;
+  CertPlan pl;
+  cert_plan(n, &pl);
+  const size_t nsub = (size_t)cert_bins() << pl.B2;
+  unsigned int *cnt = P<unsigned int>(c->counters);
+  unsigned int *cur2 = P<unsigned int>(c->ccur);
+  unsigned long long *st = P<unsigned long long>(c->stats64);
+  unsigned long long *epp = P<unsigned long long>(c->epp);
+  if (!c->sstats) {
+    int r = run_shape_stats(c);
+    if (r) return r;
+  }
+  // the global lists: staged keys (as many as the per-workgroup runs of the
+  // two-kernel path hold), deferred checks (KMZ_ABLATE bit 10, test knob: 4,
+  // so that leaders fall through to the in-place chain_put waits), claimed slots
+  while (!(c->ablate & (1u << 30)) && (uint64_t)c->scap * chain_grid(n) < 8ull * n &&
+         (uint64_t)chain_grid(n) * c->scap * 2 * 8 <= stage_limit(n))
+    c->scap *= 2;
+  const uint32_t ng = chain_grid(n), wcap = 1u << 16;
+  // (staged keys: only new chains stage; <= 2^28 keys, 2 GB, whatever the batch)
+  const uint64_t stot = std::min<uint64_t>((uint64_t)ng * c->scap, 1ull << 28), dtot = (c->ablate & (1u << 10)) ? 4u : (uint64_t)ng << 12,
+                 gtot = ((uint64_t)ng + 1) * wcap;
+  if (stot >= (1ull << 32) || dtot >= (1ull << 32) || gtot >= (1ull << 32))
+    return fail(c, KMZ_E_ARG, "fused join + walk: list sizes past 2^32");
+  void *old_ctab = c->ctab.p;
+  if (ensure(c, c->dp, (size_t)(n + 1) * 4) || ensure(c, c->cpool1, cert_pool1_words(n) * 8) ||
+      ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) ||
+      ensure(c, c->cdir, cert_dir_entries(n) * 2) || ensure(c, c->mkey, (size_t)c->mcap * 8) ||
+      ensure(c, c->mval, (size_t)c->mcap * 4) || ensure(c, c->ctab, c->ccap * CHAIN_ENTRY_BYTES) ||
+      ensure(c, c->ctile, (size_t)chain_tiles(n) * 16) || ensure(c, c->plist, (size_t)(n + 1) * 4) ||
+      ensure(c, c->kstage, stot * 8) || ensure(c, c->kdefer, dtot * 16) || ensure(c, c->kwpos, gtot * 4) ||
+      ensure(c, c->cetab, ((size_t)c->n_shapes + 1) * 16))
+    return KMZ_E_HIP;
+  cur2 = P<unsigned int>(c->ccur);
+  if (c->ctab.p != old_ctab) c->ctab_dirty = true;
+  uint32_t *gpos = P<uint32_t>(c->kwpos);
+  {
+    Timed t(c, KMZ_K_MEMSET);
+    FillArgs f;
+    f.add(cur2, nsub * 4, 0);
+    f.add(c->mkey.p, (size_t)c->mcap * 8, 0);
+    f.add(c->mval.p, (size_t)c->mcap * 4, 0xFF);  // ids not in the batch: NONE
+    if (c->ctab_dirty) f.add(c->ctab.p, c->ccap * CHAIN_ENTRY_BYTES, 0);
+    f.add(c->trip.p, c->tcap * 8, 0);
+    launch_fill(c->stream, f);
+  }
+  c->ctab_dirty = true;  // until this run's slots are cleared below
+  {
+    Timed t(c, KMZ_K_JOINWALK);
+    launch_join_chain(c->stream, c->sid, c->pid, c->kind, c->shape, c->ts, n, P<uint32_t>(c->d_dep), c->n_shapes,
+                      c->n_dep, c->index_base, c->sig_seed, P<uint32_t>(c->cparent), P<uint32_t>(c->dp),
+                      P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, c->ctab.p, c->ccap,
+                      P<unsigned long long>(c->trip), c->tcap, epp, links ? P<unsigned long long>(c->rowpos) : nullptr,
+                      P<uint32_t>(c->plist), n + 1, P<uint32_t>(c->ctile), P<unsigned long long>(c->kstage),
+                      (uint32_t)stot, P<unsigned long long>(c->kdefer), (uint32_t)dtot, gpos, (uint32_t)gtot,
+                      P<uint4>(c->cetab),
+                      // (test knob 24 forces sig collisions on the first seed only)
+                      c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)));
+  }
+  // the certificate beside the settle (small batches), as run_join
+  const bool cert_side = c->overlap && !(c->ablate & (1u << 26)) && c->ccap * CHAIN_ENTRY_BYTES <= (256ull << 20);
+  if (cert_side) {
+    HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
+    c->stream = c->side;
+  }
+  {
+    Timed t(c, KMZ_K_CERT);
+    launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
+                      P<unsigned long long>(c->cpool2), cur2, cnt);
+  }
+  {
+    Timed t(c, KMZ_K_CHECK);
+    launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
+  }
+  c->stream = c->main;
+  {
+    Timed t(c, KMZ_K_RESOLVE);
+    launch_miss(c->stream, c->sid, c->pid, P<uint32_t>(c->dp), n, P<unsigned long long>(c->mkey),
+                P<uint32_t>(c->mval), c->mcap, cnt);
+    launch_pend(c->stream, c->kind, P<uint32_t>(c->dp), n, P<uint32_t>(c->cparent), cnt);
+  }
+  {
+    Timed t(c, KMZ_K_SETTLE);
+    launch_chain_settle_list(c->stream, n, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
+                             P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), (uint32_t)stot,
+                             P<unsigned long long>(c->kdefer), (uint32_t)dtot, gpos, (uint32_t)gtot, c->ablate);
+  }
+  {
+    Timed t(c, KMZ_K_PEND);
+    launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n,
+                      P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
+                      P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, (uint32_t)gtot, false, c->ablate);
+  }
+  if (c->overlap) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_k3, 0));  // the shape-level K3 partials
+  {
+    Timed t(c, KMZ_K_FINAL);
+    launch_compact(c->stream, P<unsigned long long>(c->trip), c->tcap, P<unsigned long long>(c->trip_out),
+                   st + S_TRIP_OUT);
+    launch_collapse_endpoints(c->stream, P<unsigned long long>(c->sgrp), c->n_shapes, c->n_status,
+                              P<uint32_t>(c->d_dep), c->n_dep, P<uint32_t>(c->cparent), c->index_base, epp,
+                              epp + c->n_dep, cnt);
+    launch_chain_clear_list(c->stream, c->ctab.p, gpos, (uint32_t)gtot, cnt);
+  }
+  c->ctab_dirty = false;  // (set again after the run if the list overflowed: F_CTAB_DIRTY)
+  c->path = 1 | 2 | 16;
+  c->chain_ran = true;
+  c->k4_direct_ran = false;
+  c->k4_lb1 = 0;
+  c->k4_ng = ng;
+  return KMZ_OK;
+}
+
 static int run_deps(kmz_ctx *c, bool links) {
   const uint32_t n = (uint32_t)c->n;
   // unique edge keys are far fewer than spans; start at ~n/32 (grown on overflow)
@@ -887,6 +1027,10 @@ static int run_deps(kmz_ctx *c, bool links) {
     f.add(epp, (size_t)c->n_dep * 8, 0);
     f.add(epp + c->n_dep, (size_t)c->n_dep * 8, 0xFF);
     launch_fill(c->stream, f);
+  }
+  if (fused_eligible(c)) {
+    if (ensure(c, c->trip, c->tcap * 8) || ensure(c, c->trip_out, c->tcap * 8)) return KMZ_E_HIP;
+    return run_fused(c, links);
   }
   bool joined = false;
   int r = run_join(c, &joined);
@@ -1341,8 +1485,11 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
     // kernel fills the GPU by itself, overlap buys <= 3 % (mesh 5.29 -> 5.12 ms)
     // or loses (config 5: 19.6 -> 25.7 ms), and it blurs the per-kernel
     // roofline accounting (profiles/r01_overlap_ab/).  KMZ_ABLATE bit 27 forces it.
+    // Below 2^17 spans (a 2 500-trace tick) the second stream's fork / join
+    // costs more than the overlap gives: Bookinfo 164 -> 149 us, mesh
+    // 320 -> 300 us per run serial (tools/bench_tick.py).
     c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25)) &&
-                 (c->n < (1ull << 23) || (c->ablate & (1u << 27)));
+                 ((c->n >= (1ull << 17) && c->n < (1ull << 23)) || (c->ablate & (1u << 27)));
     int r = run_enqueue_graphed(c, flags, links, h, s64);
     if (r) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));

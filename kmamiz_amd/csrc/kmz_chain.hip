@@ -52,7 +52,7 @@
 #include <mutex>
 #include <type_traits>
 
-#include "kmz_kernels.h"
+#include "kmz_chainw.h"
 
 namespace kmz {
 
@@ -77,17 +77,6 @@ constexpr int TW = KMZ_CHAIN_TW;
 static_assert(TW <= TPW, "walker slots per thread");
 static_assert(CT % CTT == 0, "tile slots must split evenly over the threads");
 static_assert(CW % CTT == 0, "window slots must split evenly over the threads");
-constexpr uint16_t W_NONE = 0xFFFF, W_CYC = 0xFFFE, W_OUT = 0xFFFD;
-constexpr uint32_t WIN_DEPTH = 255;  // deeper in-window ancestries take the pending path
-constexpr uint32_t PROBE_MAX = 512;
-// bound of a wait on another lane's publish (chain_put returning 0).  The
-// publish is the instruction after that lane's claim, so a wait this long
-// means something is wrong; it raises F_SPIN (the run is redone exactly) and
-// never drops a check, a row or a key.  KMZ_ABLATE bit 11 (test knob) makes
-// the bound 0, i.e. every wait "runs out".
-constexpr uint32_t SPIN_MAX = 1u << 20;
-__host__ __device__ __forceinline__ uint32_t spin_bound(uint32_t ablate) { return (ablate & (1u << 11)) ? 0u : SPIN_MAX; }
-constexpr uint32_t IMAP = 256;  // LDS map: one inserting leader per distinct new chain
 // staged keys are binned by the edge set's slices: 2^lb1 coarse bins per tile
 // workgroup (k4_chain), each split into 2^lb2 slices by k_key_part
 constexpr uint32_t KB1_MAX = 8, KB2_MAX = 8;
@@ -95,9 +84,6 @@ constexpr uint32_t KB1_MAX = 8, KB2_MAX = 8;
 // LDS cache of KCACHE keys).  Hot edge keys repeat ~10^5 times per run; without
 // the cache they overfill their slice's bucket.
 constexpr uint32_t KCACHE = 1024;
-#ifndef KMZ_SIG_MIX
-#define KMZ_SIG_MIX 0
-#endif
 #ifndef KMZ_GATHER_EARLY
 #define KMZ_GATHER_EARLY 1
 #endif
@@ -106,107 +92,6 @@ constexpr uint32_t KCACHE = 1024;
 #endif
 constexpr int CHAIN_WAVES = KMZ_CHAIN_WAVES;  // waves per SIMD: 4 -> 2 workgroups per CU (<= 128 VGPRs), 6 -> 3
 constexpr uint32_t CHAIN_WG = 256 * CHAIN_WAVES * 4 / (CTT / 64);  // persistent workgroups (fill the CUs)
-constexpr uint32_t SIG_R = 21;  // fold rotation (odd: x ^ rotl(x, R) is 2-to-1 only on {x, ~x})
-// per-slot byte: kind in bits 0-1, state in bits 2-3 (state written only by the slot's owner)
-constexpr uint8_t S_NONE = 0, S_DONE = 1, S_PUT = 2, S_PEND = 3;
-__device__ __forceinline__ uint8_t kf_kind(uint8_t b) { return b & 3; }
-__device__ __forceinline__ uint8_t kf_st(uint8_t b) { return b >> 2; }
-__device__ __forceinline__ uint8_t kf_make(uint8_t kind, uint8_t st) { return (uint8_t)(kind | (st << 2)); }
-
-__host__ __device__ __forceinline__ uint64_t sig_elem(uint32_t ep, bool on, uint64_t seed) {
-  return mix64((((uint64_t)ep << 1) | (on ? 1ull : 0ull)) ^ seed);
-}
-constexpr uint64_t ROOT_SIG = ~0ull;  // the "parent sig" of a root
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, uint32_t r) {
-  r &= 63;
-  return r ? (x << r) | (x >> (64 - r)) : x;
-}
-// one fold step: the ancestors a1 (nearest) .. aD give
-//   acc = rotl^(D-1)(e(a1)) ^ ... ^ rotl(e(aD-1)) ^ e(aD)
-__device__ __forceinline__ uint64_t sig_step(uint64_t acc, uint64_t el) {
-  return ((acc << SIG_R) | (acc >> (64 - SIG_R))) ^ el;
-}
-// The finish is an xor with a depth and seed constant: a bijection for each
-// depth, which is all the exactness argument needs.  The fold is already an
-// xor of rotated mix64 outputs (uniform bits), so no further mixing is needed
-// for the table's placement; a final mix64 (two 64-bit multiplies per sig,
-// two sigs per span) cost 4 % of k4_chain (mesh 1.33 against 1.28 ms).
-// 0 marks an unwritten word and ROOT_SIG a root's parent: a sig equal to
-// either is treated as a collision (another seed)
-__device__ __forceinline__ uint64_t sig_final(uint64_t acc, uint32_t d, uint64_t seed, uint32_t *flags) {
-#if KMZ_SIG_MIX
-  const uint64_t z = mix64(acc ^ ((uint64_t)d * 0x632BE59BD9B4E019ull) ^ (seed << 1));
-#else
-  const uint64_t z = acc ^ ((uint64_t)d * 0x632BE59BD9B4E019ull) ^ (seed << 1);
-#endif
-  if (z == 0 || z == ROOT_SIG) *flags |= F_SIG;
-  return z;
-}
-// home slot: the sig's high bits (ccap is a power of two: mulhi64(sig, ccap))
-__device__ __forceinline__ uint64_t cslot(uint64_t sig, uint64_t ccap) {
-  return sig >> (64 - __builtin_ctzll(ccap));
-}
-
-__device__ __forceinline__ uint64_t edge_key(uint32_t ea, uint32_t es, uint32_t d, bool on) {
-  return ((uint64_t)ea << 40) | ((uint64_t)es << 16) | ((uint64_t)d << 1) | (on ? 1ull : 0ull);
-}
-
-// the global edge-key set (one insert per key of a NEW chain only); its size
-// is counted by the compaction
-__device__ __forceinline__ void edge_insert(uint64_t key, unsigned long long *__restrict__ trip, uint64_t tcap,
-                                           uint32_t *flags) {
-  // an overfull set makes every insert probe PROBE_MAX slots: once this
-  // thread has seen it, the run is repeated with a larger set anyway
-  if (*flags & F_TRIPLE_OVERFLOW) return;
-  uint64_t pos = eslot(key, tcap);
-  for (uint32_t z = 0; z < PROBE_MAX; ++z) {
-    uint64_t cur = trip[pos];
-    if (cur == key) return;
-    if (cur == 0) {
-      cur = atomicCAS(&trip[pos], 0ull, (unsigned long long)key);
-      if (cur == 0 || cur == key) return;
-    }
-    pos = eset_next(pos, tcap);
-  }
-  *flags |= F_TRIPLE_OVERFLOW;
-}
-
-// Chain table entry words: [0] sig, [1] parent sig (ROOT_SIG at a root).
-// Both are written once with a nonzero value, so a reader needs no ordering
-// between them: an entry is published once both are nonzero.
-// Insert (or join) the chain `sig`.  Returns 1 inserted, 2 found (and
-// checked), 0 not yet decidable (the winner has not published), -1 probe bound.
-// A slot this call claims is appended to the run's written list (gpos, counted
-// in counters[C_WPOS]) so that it can be cleared after the run.
-__device__ __forceinline__ int chain_put(unsigned long long *__restrict__ ctab, uint64_t ccap, uint64_t sig,
-                                         uint64_t psig, uint32_t *flags, uint32_t *__restrict__ gpos,
-                                         uint32_t gcap, unsigned int *__restrict__ counters) {
-  if (*flags & F_CHAIN_OVERFLOW) return -1;  // (this thread found the table full: the run is repeated larger)
-  uint64_t pos = cslot(sig, ccap);
-  for (uint32_t z = 0; z < PROBE_MAX; ++z) {
-    unsigned long long *e = ctab + 2 * pos;
-    const unsigned long long c = atomicCAS(&e[0], 0ull, (unsigned long long)sig);
-    if (c == 0) {
-      atomicExch(&e[1], (unsigned long long)psig);
-      const uint32_t x = atomicAdd(&counters[C_WPOS], 1u);  // (rare paths only)
-      if (x < gcap)
-        gpos[x] = (uint32_t)pos;
-      else
-        *flags |= F_CTAB_DIRTY;
-      return 1;
-    }
-    if (c == sig) {
-      const unsigned long long ps = atomicAdd(&e[1], 0ull);  // memory-side read
-      if (ps == 0) return 0;
-      if (ps != psig) *flags |= F_SIG;
-      return 2;
-    }
-    pos = pos + 1 == ccap ? 0 : pos + 1;
-  }
-  *flags |= F_CHAIN_OVERFLOW;
-  return -1;
-}
-
 __device__ unsigned long long g_chain_dbg[8];  // diagnostic phase clocks (KMZ_ABLATE bit 22 only)
 
 template <bool DIRECT>
@@ -1042,6 +927,11 @@ __global__ void __launch_bounds__(256) k_chain_etab(const uint32_t *__restrict__
   }
 }
 
+void launch_chain_etab(hipStream_t s, const uint32_t *dep_ep, uint32_t n_shapes, uint64_t seed, uint4 *etab) {
+  hipLaunchKernelGGL(k_chain_etab, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_shapes + 255) / 256, 1024))),
+                     dim3(256), 0, s, dep_ep, n_shapes, seed, etab);
+}
+
 void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const int64_t *ts,
                   const uint32_t *cparent, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes, uint32_t n_ep,
                   uint64_t index_base, uint64_t seed, void *ctab, uint64_t ccap, unsigned long long *trip,
@@ -1060,8 +950,7 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
   }
   const uint32_t g = chain_grid(n);
   unsigned long long *tab = reinterpret_cast<unsigned long long *>(ctab);
-  hipLaunchKernelGGL(k_chain_etab, dim3(std::max<uint32_t>(1, std::min<uint32_t>((n_shapes + 255) / 256, 1024))),
-                     dim3(256), 0, s, dep_ep, n_shapes, seed, etab);
+  launch_chain_etab(s, dep_ep, n_shapes, seed, etab);
   if (direct)
     hipLaunchKernelGGL(k4_chain<true>, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, etab, n_shapes, n_ep,
                        index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,
@@ -1146,6 +1035,11 @@ void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *w
   const uint32_t g = chain_grid(n);
   hipLaunchKernelGGL(k_chain_clear, dim3(g), dim3(256), 0, s, reinterpret_cast<unsigned long long *>(ctab), wpos,
                      wcap, wpos_n, g, gpos, gcap, counters);
+}
+
+void launch_chain_clear_list(hipStream_t s, void *ctab, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters) {
+  hipLaunchKernelGGL(k_chain_clear, dim3(1024), dim3(256), 0, s, reinterpret_cast<unsigned long long *>(ctab), gpos, 0u,
+                     gpos, 0u, gpos, gcap, counters);
 }
 
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,

@@ -27,92 +27,17 @@
 
 #include <algorithm>
 
-#include "kmz_kernels.h"
+#include "kmz_joinw.h"
 
 namespace kmz {
 
-constexpr uint32_t JT = 2048, JH = 256, JW = JT + 2 * JH, JTT = 512;
-static_assert(JW < 4096, "local index + 1 must fit an entry's 12 bits");
-constexpr uint16_t L_NONE = 0xFFFF, L_MISS = 0xFFFE;
-constexpr uint32_t CERT_B1 = 6, CERT_BINS = 1u << CERT_B1;
 #ifndef KMZ_CERT_PQ
 #define KMZ_CERT_PQ 8
 #endif
 constexpr uint32_t CERT_PQ = KMZ_CERT_PQ;  // pass 2: records per thread (chunks of PQ * 1024 records of one bin)
 constexpr uint32_t CERT_SET = 8192;    // pass-3 LDS set (u64), sub-bins <= 6144 records
 
-
-// exclusive scan of LDS u32 array a[0..m) in place, any m <= 64 * blockDim.x
 __host__ __device__ uint32_t join_tiles(uint32_t n) { return (n + JT - 1) / JT; }
-
-__device__ void block_scan_lds(uint32_t *a, uint32_t m, uint32_t *wsum) {
-  const uint32_t per = (m + blockDim.x - 1) / blockDim.x;
-  const uint32_t b = threadIdx.x * per, e = min(m, b + per);
-  uint32_t s = 0;
-  for (uint32_t k = b; k < e; ++k) s += a[k];
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t x = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
-  if (lane == 63) wsum[w] = x;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0;
-    for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
-      uint32_t t = wsum[k];
-      wsum[k] = acc;
-      acc += t;
-    }
-  }
-  __syncthreads();
-  uint32_t run = wsum[w] + x - s;
-  for (uint32_t k = b; k < e; ++k) {
-    uint32_t t = a[k];
-    a[k] = run;
-    run += t;
-  }
-  __syncthreads();
-}
-
-// LDS hash of a window: two-choice buckets of 8 u16 entries (one 16-byte LDS
-// read each), entry = fingerprint (4 bits of a multiplicative hash of the id) << 12 | local index + 1.
-// A lookup reads its two buckets and compares 16 fingerprints; only a
-// fingerprint hit reads the 64-bit id.  Entries that find both buckets full go
-// to a small stash that lookups scan (broadcast reads) when it is not empty.
-// No probe loops: constant work per span, no wave waiting on its unluckiest lane.
-constexpr uint32_t JB = 1024;     // buckets (8192 entries, load <= 0.31)
-static_assert(JB * 16 >= JT * 8, "the buckets double as the tile's certificate staging");
-constexpr uint32_t JSTASH = 64;
-// Window-hash placement: two 32-bit multiplicative hashes of the folded id.
-// Placement quality only affects speed (an overfull bucket pair goes to the
-// stash, a full stash to the table path); exactness comes from comparing the
-// full 64-bit ids, and the certificate keeps its own bijective cert_hash.
-static_assert(JB == 1024, "bucket indices are the top 10 bits of the 32-bit hashes");
-// the certificate's hash of a span id: a bijection of the 64-bit ids (an odd
-// multiplier, then an xorshift), so equal hashes are equal ids; its top bits
-// pick the bin and sub-bin, its low bits the check's bucket.  (mix64's second
-// multiply and shifts bought nothing here: one multiply spreads sequential
-// ids over the top bits, the xorshift brings them to the low bits.)  0 -> 0.
-__device__ __forceinline__ uint64_t cert_hash(uint64_t x) { return id_hash(x); }  // (kmz_common.h)
-__device__ __forceinline__ uint32_t jfold(uint64_t id) { return (uint32_t)id ^ (uint32_t)(id >> 32); }
-__device__ __forceinline__ uint32_t jb1(uint32_t x) { return (x * 0x9E3779B1u) >> 22; }
-__device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >> 22; }
-// fingerprints are 1..15: an empty entry (0) never matches one, so a lookup
-// compares fingerprints only
-__device__ __forceinline__ uint32_t jfp(uint32_t x) { return max(((x * 0x9E3779B1u) >> 18) & 0xF, 1u); }
-
-// lanes of this wave whose `v` (6 bits) equals mine, among `valid` lanes
-__device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
-  uint64_t m = valid;
-#pragma unroll
-  for (int bit = 0; bit < 6; ++bit) {
-    const uint64_t b = __ballot((v >> bit) & 1);
-    m &= ((v >> bit) & 1) ? b : ~b;
-  }
-  return m;
-}
 
 __device__ unsigned long long g_join_dbg[16];  // diagnostic phase clocks (KMZ_ABLATE bit 23 only)
 #define KMZ_JSTAMP(k)                                           \

@@ -22,7 +22,9 @@ enum {
   C_CERT = 5,
   C_PLIST = 6,  // K4 spans whose ancestry leaves their LDS window (pending list length)
   C_WPOS = 7,   // K4 chain-table slots written outside the tile kernel (cleared after the run)
-  C_COUNT = 8
+  C_FSTAGE = 8,  // fused join + walk: keys staged in the global list
+  C_FDEFER = 9,  // fused join + walk: deferred chain checks in the global list
+  C_COUNT = 10
 };
 // C_CERT bits: the window join's answers cannot be used (global table path)
 constexpr uint32_t CERT_DUP = 1u, CERT_OVF = 2u;
@@ -131,9 +133,29 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
                          unsigned long long *bucket, uint64_t bcap, uint32_t *bucket_n,
                          const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
                          uint32_t gcap, uint32_t ablate = 0, bool cmode = false);
+// per shape: dependency endpoint + SERVER element hash under `seed` (the walk's gather table)
+void launch_chain_etab(hipStream_t s, const uint32_t *dep_ep, uint32_t n_shapes, uint64_t seed, uint4 *etab);
+// K2 + K4 fused over one LDS window, chain interning (kmz_fuse.hip); its
+// staged keys, deferred checks and claimed slots are global lists
+// (counters C_FSTAGE, C_FDEFER, C_WPOS), settled by launch_chain_settle_list
+void launch_join_chain(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind,
+                       const uint32_t *shape, const int64_t *ts, uint32_t n, const uint32_t *dep_ep, uint32_t n_shapes,
+                       uint32_t n_ep, uint64_t index_base, uint64_t seed, uint32_t *cparent, uint32_t *dp,
+                       unsigned long long *pool1, uint16_t *jdir, unsigned int *counters, void *ctab, uint64_t ccap,
+                       unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned long long *rowpos,
+                       uint32_t *plist, uint32_t pcap, uint32_t *tile_stats, unsigned long long *stage, uint32_t scap,
+                       unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap, uint4 *etab,
+                       uint32_t ablate = 0);
+void launch_chain_settle_list(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip,
+                              uint64_t tcap, unsigned int *counters, const uint32_t *tile_stats,
+                              unsigned long long *stats64, const unsigned long long *stage, uint32_t scap,
+                              const unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap,
+                              uint32_t ablate = 0);
 // zero the chain-table entries this run wrote (instead of a memset of the table)
 void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
                         const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);
+// (the global list only: the fused kernel's claimed slots)
+void launch_chain_clear_list(hipStream_t s, void *ctab, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,
                        const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, uint32_t n,
                        const uint32_t *dep_ep,

@@ -311,8 +311,8 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
     } else {
       b[0] = a_cnt[k];
       b[G] = a_s1[k];
-      b[2ull * G] = a_s2a[k];
-      b[3ull * G] = a_s2b[k];
+      b[2ull * G] = a_s2a[k] & 0xFFFFFFFFull;  // (canonical limbs when this is the last word: S = 1)
+      b[3ull * G] = a_s2b[k] + (a_s2a[k] >> 32);
       b[4ull * G] = a_tsx[k];
       b[5ull * G] = a_fst[k];
     }
@@ -519,8 +519,8 @@ __global__ void __launch_bounds__(256) k3_combine_bal(const unsigned long long *
     }
     grp[g] = c;
     grp[G + g] = s1;
-    grp[2ull * G + g] = s2a;
-    grp[3ull * G + g] = s2b;
+    grp[2ull * G + g] = s2a & 0xFFFFFFFFull;  // canonical limbs: S2 = s2a + 2^32 s2b with s2a < 2^32,
+    grp[3ull * G + g] = s2b + (s2a >> 32);     // whatever split the items' sums had
     grp[4ull * G + g] = tsx;
     grp[5ull * G + g] = fst;
   }
@@ -541,8 +541,8 @@ __global__ void __launch_bounds__(256) k3_combine(const unsigned long long *__re
     }
     grp[g] = c;
     grp[G + g] = s1;
-    grp[2ull * G + g] = s2a;
-    grp[3ull * G + g] = s2b;
+    grp[2ull * G + g] = s2a & 0xFFFFFFFFull;  // (canonical limbs, as k3_combine_bal)
+    grp[3ull * G + g] = s2b + (s2a >> 32);
     grp[4ull * G + g] = tsx;
     grp[5ull * G + g] = fst;
   }

@@ -436,6 +436,73 @@ def test_window_join_matches_span_table(engine):
     assert _info_results(a[4]) == _info_results(b[4])
 
 
+SEPARATE_JOIN_WALK = 16  # KMZ_ABLATE2: k_join_window + k4_chain instead of the fused k_join_chain
+FUSED_ANY_SIZE = 32      # KMZ_ABLATE2: the fused k_join_chain at any batch size
+
+
+@pytest.mark.parametrize("case", ["mesh", "power", "far", "messy"])
+def test_fused_join_walk_equals_two_kernels(engine, case):
+    """The fused join + chain walk (kmz_fuse.hip: one LDS window for the parent
+    join, the contraction and the walk; halo spans resolved in-window, the rest
+    pending) gives the same span links, edge keys, endpoints and counts as
+    k_join_window followed by k4_chain, on the mesh, config 5 (interning
+    forced), a batch with 5 % of its spans moved far from their traces (MISS
+    parents, PEND chains, pending ancestries) and messy batches."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+    from kmamiz_amd.engine import SpanBatch
+
+    if case in ("mesh", "power"):
+        cfg = 3 if case == "mesh" else 5
+        batch, _ = synth.host_batch(cfg, 0, 8000)
+        table = synth.shape_table(cfg)
+    elif case == "far":
+        batch, _ = synth.host_batch(3, 0, 6000)
+        n = len(batch)
+        rng = np.random.default_rng(11)
+        perm = np.arange(n)
+        sel = np.flatnonzero(rng.random(n) < 0.05)
+        perm[sel] = perm[rng.permutation(sel)]
+        batch = _permuted(batch, perm)
+        table = synth.shape_table(3)
+
+    def run(e):
+        if case == "messy":
+            out = []
+            from kmamiz_amd import CycleError, Traces
+
+            for seed in range(12):
+                rng = random.Random(1000 + seed)
+                traces = messy_batch(rng, rng.randint(4, 40), rng.choice([8, 64, 4096, 4096]))
+                try:
+                    out.append((Traces(traces, engine=e).toEndpointDependencies().toJSON(), e.info()["path"]))
+                except CycleError:  # (random parent ids can close a loop: both paths must refuse it)
+                    out.append(("cycle", 0))
+            return out
+        e.load(batch, table)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS | L.RUN_SPAN_LINKS)
+        cp, rp = e.span_links()
+        return cp, rp, e.triples(), e.endpoints(), e.info(), e.groups()
+
+    sep = _engine_with2(1 << 29, SEPARATE_JOIN_WALK)  # (bit 29: chain interning on config 5 too)
+    fused = _engine_with2(1 << 29, FUSED_ANY_SIZE)
+    try:
+        a, b = run(fused), run(sep)
+    finally:
+        sep.close()
+        fused.close()
+    if case == "messy":
+        assert [x[0] for x in a] == [x[0] for x in b]
+        assert any(x[1] & 16 for x in a) and not any(x[1] & 16 for x in b)
+        return
+    assert a[4]["path"] & 16 and not b[4]["path"] & 16 and a[4]["path"] & 3 == 3
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert a[3].tobytes() == b[3].tobytes() and a[5].tobytes() == b[5].tobytes()
+    assert _info_results(a[4]) == _info_results(b[4])
+    keys, _, _ = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    assert np.array_equal(a[2], keys)
+
+
 # ---------------------------------------------------------------------------
 # K4 chain interning: hash collisions, deep chains (kmz_chain.hip)
 # ---------------------------------------------------------------------------
@@ -1051,8 +1118,20 @@ def test_shard_generation_and_index_map(engine, config, t0, t1, world):
     wg, we = np.zeros(gw, np.uint64), np.zeros(ew, np.uint64)
     engine.export_partials(L.PART_GROUPS, wg.ctypes.data, gw, False)
     engine.export_partials(L.PART_ENDPOINTS, we.ctypes.data, ew, False)
-    assert np.array_equal(wg, g)
+    assert np.array_equal(canon_limbs(wg), canon_limbs(g))
     assert np.array_equal(we, e)
+
+
+def canon_limbs(g):
+    """Group partials with their sum of squared durations in canonical limbs
+    (S2 = s2a + 2^32 s2b, s2a < 2^32): summed partials (a merge) may carry
+    low-limb sums past 2^32, which finalise to the same S2."""
+    G = len(g) // 6
+    g = g.copy()
+    a = g[2 * G: 3 * G].copy()
+    g[2 * G: 3 * G] = a & np.uint64(0xFFFFFFFF)
+    g[3 * G: 4 * G] += a >> np.uint64(32)
+    return g
 
 
 def test_headline_size_config3_properties(engine):
@@ -1188,7 +1267,11 @@ def test_headline_config5_vs_c_oracle_and_tail():
         for f in tail.pairs.dtype.names:
             assert np.array_equal(tail.pairs[f], ref.pairs[f]), f
         assert np.array_equal(tail.gateway, ref.gateway)
-        assert np.array_equal(tail.stats, ref.stats)
+        assert np.array_equal(tail.total, ref.total)
+        # (columns 6 / 7 are the device's per-service rows and gateway flag,
+        # compared above as total / gateway; the restatement derives those
+        # from the endpoint records instead)
+        assert np.array_equal(tail.stats[:, :6], ref.stats[:, :6])
         assert tail.instability() == ref.instability()
         assert tail.coupling() == ref.coupling()
         mt, mr = tail.metrics(), ref.metrics()

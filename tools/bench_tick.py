@@ -2,7 +2,8 @@
 takes up to 2 500 traces per 5-s tick (RealtimeWorkerImpl.ts:31-35).  Per tick
 on one GPU: kmz_load of the host columns (H2D) + kmz_run (stats + dependency
 graph) + kmz_fetch of the results, timed over many ticks, with the run's
-hipGraph replay on (default) and off (KMZ_ABLATE bit 13).  Prints one JSON
+join + chain walk fused (default) or as two kernels, hipGraph replay on or
+off (KMZ_ABLATE bit 13).  Prints one JSON
 object; kernel launches per tick come from rocprofv3 (tools/tick_profile.sh).
 
     python tools/bench_tick.py [--traces 2500] [--ticks 200]
@@ -35,11 +36,14 @@ def main():
         batch, _ = synth.host_batch(cfg, 0, args.traces)
         table = synth.shape_table(cfg)
         res = {"spans": len(batch)}
-        for mode, knob in (("graph", 1 << 13), ("no_graph", 0), ("no_graph_serial", 1 << 25),
-                           ("graph_serial", (1 << 13) | (1 << 25))):
-            os.environ["KMZ_ABLATE"] = str(knob)
+        # default: direct launches, the join + chain walk fused (kmz_fuse.hip);
+        # separate: k_join_window + k4_chain (KMZ_ABLATE2 bit 4); graph: hipGraph
+        # replay (KMZ_ABLATE bit 13); serial: no side stream (bit 25)
+        for mode, knob, knob2 in (("default", 0, 0), ("separate", 0, 16), ("graph", 1 << 13, 0),
+                                  ("serial", 1 << 25, 0)):
+            os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"] = str(knob), str(knob2)
             e = Engine(0)
-            del os.environ["KMZ_ABLATE"]
+            del os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"]
             for _ in range(10):  # warm: buffers, the graph capture
                 e.load(batch, table)
                 e.run(flags)
