@@ -138,7 +138,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -698,11 +698,14 @@ static int run_join(kmz_ctx *c, bool *ok) {
   const uint32_t n = (uint32_t)c->n;
   *ok = false;
   CertPlan pl;
-  if (n == 0 || !cert_plan(n, &pl) || c->table_hint || (c->ablate & 32)) return KMZ_OK;
-  const size_t nsub = (size_t)cert_bins() << pl.B2;
+  // (KMZ_ABLATE2 bit 6, test knob: the certificate's 2^8 pass-1 bins at any
+  // size; bit 7: never, for comparison)
+  if (n == 0 || !cert_plan(n, &pl, !(c->ablate2 & 128u), (c->ablate2 & 64u) != 0) || c->table_hint || (c->ablate & 32))
+    return KMZ_OK;
+  const size_t nsub = (size_t)1 << (pl.B1 + pl.B2);
   if (ensure(c, c->dp, (size_t)(n + 1) * 4) || ensure(c, c->cpool1, cert_pool1_words(n) * 8) ||
       ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) ||
-      ensure(c, c->cdir, cert_dir_entries(n) * 2))
+      ensure(c, c->cdir, cert_dir_entries(n, pl) * 2))
     return KMZ_E_HIP;
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
@@ -718,7 +721,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
   {
     Timed t(c, KMZ_K_JOIN);
     launch_join(c->stream, c->sid, c->pid, c->kind, n, P<uint32_t>(c->cparent), P<uint32_t>(c->dp),
-                P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, c->ablate);
+                P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, pl, c->ablate);
   }
   // ... only while the chain table fits the 256 MB MALL: then the walk's
   // probes leave HBM to the certificate (measured: mesh 5.21 -> 5.12 ms,
@@ -820,7 +823,7 @@ static int run_shape_stats(kmz_ctx *c) {
     // fixed slices per partition, for comparison
     const bool bal = S > 1 && !(c->ablate & (1u << 14));
     const uint32_t Sd = bal ? 1u : S;  // the directory's slices ([partition][tile] for the balanced reduce)
-    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, (k3_dir_words(n, Pp, Sd) + 2 * Pp + 2) * 4) ||
+    if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, (k3_dir_words(n, Pp, Sd) + k3_plan_words(Pp) + 1) * 4) ||
         ensure(c, c->k3part, bal ? k3_bal_part_bytes((uint32_t)Gs) : (size_t)S * 6 * Gs * 8) ||
         ensure(c, c->tile_tmp, (size_t)nt * 16))
       return KMZ_E_HIP;
@@ -894,14 +897,15 @@ static bool fused_eligible(kmz_ctx *c) {
   CertPlan pl;
   const bool size_ok = (c->n >= KMZ_FUSE_MIN && c->n < KMZ_FUSE_MAX) || (c->ablate2 & 32u);
   return c->n > 0 && size_ok && !c->k4_now && !(c->ablate2 & 16u) && !c->table_hint && !(c->ablate & (32u | 16u)) &&
-         !c->walk_once && cert_plan((uint32_t)c->n, &pl);
+         !c->walk_once && cert_plan((uint32_t)c->n, &pl, true, (c->ablate2 & 64u) != 0) &&
+         pl.B1 == 6;  // (the fused kernel bins by 2^6)
 }
 
 static int run_fused(kmz_ctx *c, bool links) {
   const uint32_t n = (uint32_t)c->n;
   CertPlan pl;
   cert_plan(n, &pl);
-  const size_t nsub = (size_t)cert_bins() << pl.B2;
+  const size_t nsub = (size_t)1 << (pl.B1 + pl.B2);
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
   unsigned long long *st = P<unsigned long long>(c->stats64);
@@ -925,7 +929,7 @@ static int run_fused(kmz_ctx *c, bool links) {
   void *old_ctab = c->ctab.p;
   if (ensure(c, c->dp, (size_t)(n + 1) * 4) || ensure(c, c->cpool1, cert_pool1_words(n) * 8) ||
       ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) ||
-      ensure(c, c->cdir, cert_dir_entries(n) * 2) || ensure(c, c->mkey, (size_t)c->mcap * 8) ||
+      ensure(c, c->cdir, cert_dir_entries(n, pl) * 2) || ensure(c, c->mkey, (size_t)c->mcap * 8) ||
       ensure(c, c->mval, (size_t)c->mcap * 4) || ensure(c, c->ctab, c->ccap * CHAIN_ENTRY_BYTES) ||
       ensure(c, c->ctile, (size_t)chain_tiles(n) * 16) || ensure(c, c->plist, (size_t)(n + 1) * 4) ||
       ensure(c, c->kstage, stot * 8) || ensure(c, c->kdefer, dtot * 16) || ensure(c, c->kwpos, gtot * 4) ||
@@ -2148,11 +2152,11 @@ int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32
   *repeated = 0;
   if (n < 2) return KMZ_OK;
   CertPlan pl;
-  if (n >= 0xFFFFFFFFull || !cert_plan((uint32_t)n, &pl))
+  if (n >= 0xFFFFFFFFull || !cert_plan((uint32_t)n, &pl, false))  // (k_cert_bin bins by 2^6)
     return fail(c, KMZ_E_UNSUPPORTED, "too many values for the certificate: check on the host");
   const uint32_t m = (uint32_t)n;
-  const size_t nsub = (size_t)cert_bins() << pl.B2;
-  if (ensure(c, c->cpool1, cert_pool1_words(m) * 8) || ensure(c, c->cdir, cert_dir_entries(m) * 2) ||
+  const size_t nsub = (size_t)1 << (pl.B1 + pl.B2);
+  if (ensure(c, c->cpool1, cert_pool1_words(m) * 8) || ensure(c, c->cdir, cert_dir_entries(m, pl) * 2) ||
       ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) || ensure(c, c->rt_ctr, C_COUNT * 4))
     return KMZ_E_HIP;
   const unsigned long long *src = reinterpret_cast<const unsigned long long *>(vals);

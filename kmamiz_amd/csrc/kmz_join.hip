@@ -49,19 +49,23 @@ __device__ unsigned long long g_join_dbg[16];  // diagnostic phase clocks (KMZ_A
 
 // (A persistent form of this kernel, the next tile's window loaded while the
 // current tile contracts and bins, measured 1.62 against 1.18 ms on config 3.)
+template <uint32_t B1>
 __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
                                                      const uint8_t *__restrict__ kind, uint32_t n,
                                                      uint32_t *__restrict__ cparent, uint32_t *__restrict__ dp,
                                                      unsigned long long *__restrict__ pool1,
                                                      uint16_t *__restrict__ jdir,
                                                      unsigned int *__restrict__ counters, uint32_t ablate) {
-  constexpr uint32_t NW = JTT / 64;
+  constexpr uint32_t NW = JTT / 64, BINS = 1u << B1;
   __shared__ uint64_t lsid[JW];
   __shared__ uint4 lbkt[JB];  // later: staging of the tile's hashed ids
-  __shared__ uint32_t lcnt[JB];
+  // the buckets' fill counts (insert phase), then the certificate's per-wave
+  // bin counts (pass 1)
+  __shared__ uint32_t lcw[JB > BINS * NW ? JB : BINS * NW];
+  uint32_t *const lcnt = lcw, *const wcnt = lcw;
   __shared__ uint16_t ldp[JW];
   __shared__ uint8_t lkind[JW];
-  __shared__ uint32_t wcnt[CERT_BINS * NW], wsum[NW];
+  __shared__ uint32_t wsum[NW];
   __shared__ uint16_t stash[JSTASH];
   __shared__ uint32_t nstash;
   constexpr int PW = JW / JTT, PT = JT / JTT;
@@ -277,9 +281,9 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   }
   KMZ_JSTAMP(3);
   if (ablate & 64) return;  // diagnostic: no certificate pass 1
-  // certificate pass 1: the tile's hashed ids into 64 bins.  Ranks come from
-  // wave ballots and per-wave counters (no LDS atomics on 64 hot words).
-  for (uint32_t e = threadIdx.x; e < CERT_BINS * NW; e += JTT) wcnt[e] = 0;
+  // certificate pass 1: the tile's hashed ids into 2^B1 bins.  Ranks come
+  // from wave ballots and per-wave counters (no LDS atomics on hot words).
+  for (uint32_t e = threadIdx.x; e < BINS * NW; e += JTT) wcnt[e] = 0;
   __syncthreads();  // lbkt free from here on
   uint64_t *stg = reinterpret_cast<uint64_t *>(lbkt);
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -289,22 +293,22 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   for (int q = 0; q < PT; ++q) {
     const uint32_t i = t0 + q * JTT + threadIdx.x;
     const bool ok = i < t1;
-    const uint32_t bin = (uint32_t)(hv[q] >> (64 - CERT_B1));
-    const uint64_t peers = match6(bin, __ballot(ok));
+    const uint32_t bin = (uint32_t)(hv[q] >> (64 - B1));
+    const uint64_t peers = match_bits<B1>(bin, __ballot(ok));
     uint32_t prior = 0;
     if (ok) prior = wcnt[bin * NW + w];
     rk[q] = prior + __popcll(peers & lt);
     if (ok && (peers & lt) == 0) wcnt[bin * NW + w] = prior + __popcll(peers);
   }
   __syncthreads();
-  block_scan_lds(wcnt, CERT_BINS * NW, wsum);  // bin-major, wave-minor offsets
+  block_scan_lds(wcnt, BINS * NW, wsum);  // bin-major, wave-minor offsets
   // tile-major output, bins in order: no global atomics; the bin offsets go
   // to the tile's directory row for pass 2
-  if (threadIdx.x < CERT_BINS) jdir[(uint64_t)blockIdx.x * CERT_BINS + threadIdx.x] = (uint16_t)wcnt[threadIdx.x * NW];
+  for (uint32_t b = threadIdx.x; b < BINS; b += JTT) jdir[(uint64_t)blockIdx.x * BINS + b] = (uint16_t)wcnt[b * NW];
 #pragma unroll
   for (int q = 0; q < PT; ++q) {
     const uint32_t i = t0 + q * JTT + threadIdx.x;
-    if (i < t1) stg[wcnt[(uint32_t)(hv[q] >> (64 - CERT_B1)) * NW + w] + rk[q]] = hv[q];
+    if (i < t1) stg[wcnt[(uint32_t)(hv[q] >> (64 - B1)) * NW + w] + rk[q]] = hv[q];
   }
   __syncthreads();
   for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) pool1[(uint64_t)t0 + e] = stg[e];
@@ -367,17 +371,23 @@ void launch_cert_bin(hipStream_t s, const unsigned long long *v, uint32_t n, uns
 // 64-bit atomic, as 16-bit fields, measured 0.59 against 0.57 ms on config 3:
 // the per-sub-bin reservations are not what bounds this pass.)  (PQ = 16, i.e. runs twice as long
 // per sub-bin, measured slower: 0.59 against 0.55 ms on config 3.)
-template <int PQ>
+// With 2^8 pass-1 bins (B1 = 8, batches past ~10^8 ids) a chunk takes 4x the
+// tiles (tile runs of ~8 records); a record then finds its tile run by a
+// binary search over the run starts instead of the byte map.
+template <int PQ, uint32_t B1>
 __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *__restrict__ pool1,
                                                      const uint16_t *__restrict__ jdir, uint32_t n, uint32_t chunks,
                                                      uint32_t B2, unsigned long long *__restrict__ pool2,
                                                      uint32_t cap2, unsigned int *__restrict__ cur2,
                                                      unsigned int *__restrict__ counters) {
-  constexpr uint32_t CERT_CHUNK = PQ * 1024, CERT_TPC = PQ * 24;  // ~32 ids per tile run at 64 bins
+  constexpr uint32_t BINS = 1u << B1;
+  // ~32 ids per tile run at 64 bins, ~8 at 256
+  constexpr uint32_t CERT_CHUNK = PQ * 1024, CERT_TPC = (PQ * 24) << (B1 - CERT_B1);
+  constexpr bool MAP = CERT_TPC <= 256;  // record -> tile by a byte map (else a binary search)
+  static_assert(CERT_TPC <= 1024, "one thread per tile run");
   extern __shared__ uint64_t dyn[];
   __shared__ uint32_t wsum[16], tcnt[CERT_TPC], toff[CERT_TPC];
-  __shared__ uint8_t tof[CERT_CHUNK];  // record -> its tile in the chunk (CERT_TPC <= 256)
-  static_assert(CERT_TPC <= 256, "tile numbers are bytes");
+  __shared__ uint8_t tof[MAP ? CERT_CHUNK : 1];  // record -> its tile in the chunk
   uint64_t *stg = dyn;
   const uint32_t M = 1u << B2;
   uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn + CERT_CHUNK), *base = cnt + M;
@@ -392,8 +402,8 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
     if (threadIdx.x < nt) {
       const uint32_t t = T0 + threadIdx.x;
       const uint32_t tsize = min(JT, n - t * JT);
-      o = jdir[(uint64_t)t * CERT_BINS + b];
-      const uint32_t e = b + 1 < CERT_BINS ? jdir[(uint64_t)t * CERT_BINS + b + 1] : tsize;
+      o = jdir[(uint64_t)t * BINS + b];
+      const uint32_t e = b + 1 < BINS ? jdir[(uint64_t)t * BINS + b + 1] : tsize;
       c = e - o;
     }
     tcnt[threadIdx.x] = c;
@@ -409,9 +419,17 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   }
   // record -> tile map: each tile's thread writes its run (one LDS lookup per
   // record below instead of a binary search of dependent LDS reads)
-  if (threadIdx.x < nt)
+  if (MAP && threadIdx.x < nt)
     for (uint32_t j = 0, p = tcnt[threadIdx.x]; j < c; ++j) tof[p + j] = (uint8_t)threadIdx.x;
   __syncthreads();
+  auto tile_of = [&](uint32_t e) -> uint32_t {
+    if (MAP) return tof[e];
+    uint32_t lo = 0;  // the last run starting at or before e (empty runs share the next one's start)
+#pragma unroll
+    for (uint32_t step = 512; step; step >>= 1)
+      if (lo + step < nt && tcnt[lo + step] <= e) lo += step;
+    return lo;
+  };
   // gather the chunk's records straight into registers: every load is in
   // flight before any is used
   uint64_t h[PQ];
@@ -421,11 +439,11 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
     const uint32_t e = q * 1024 + threadIdx.x;
     h[q] = 0;
     if (e < cn) {
-      const uint32_t lo = tof[e];
+      const uint32_t lo = tile_of(e);
       h[q] = pool1[(uint64_t)(T0 + lo) * JT + toff[lo] + (e - tcnt[lo])];
     }
   }
-  const uint32_t sh = 64 - CERT_B1 - B2;
+  const uint32_t sh = 64 - B1 - B2;
 #pragma unroll
   for (int q = 0; q < PQ; ++q) {
     const uint32_t e = q * 1024 + threadIdx.x;
@@ -647,40 +665,59 @@ __global__ void __launch_bounds__(256) k_pend(const uint8_t *__restrict__ kind, 
 // sub-bin in registers and checks it in 4 phases, so that pass 2 writes runs
 // 4x longer -- split 8.9 -> 7.4 ms but check 2.9 -> 5.6 ms, and at 10^8
 // split 0.56 -> 0.49, check 0.27 -> 0.50 ms; 8 phases worse still.)
-bool cert_plan(uint32_t n, CertPlan *pl) {
+bool cert_plan(uint32_t n, CertPlan *pl, bool wide, bool force_wide) {
+  // sub-bins of <= ~3072 ids (4096 with 2^8 bins): a check workgroup holds 6144
+  uint32_t B1 = CERT_B1, lim = 3072;
+  // (2^8 bins past ~1.0e8 ids and up to 2^29: measured at 5e8 ids, join +
+  // split + check 11.55 -> 11.01 ms; at 1e9, 22.0 -> 22.6 ms -- the wider
+  // join's 8 ballots and 2048-entry scan cost more than the split's 4x longer
+  // runs gain, whose time there is bound by its one-workgroup-per-CU latency)
+  if (force_wide || (wide && (uint64_t)n > (3072ull << (CERT_B1 + 9)) && n <= (1u << 29))) {
+    B1 = CERT_B1W;
+    lim = 4096;
+  }
   uint32_t B2 = 0;
-  while (B2 < 12 && (uint64_t)n > (3072ull << (CERT_B1 + B2))) ++B2;
-  const double mean2 = (double)n / ((uint64_t)CERT_BINS << B2);
+  while (B2 < 12 && (uint64_t)n > ((uint64_t)lim << (B1 + B2))) ++B2;
+  const double mean2 = (double)n / ((uint64_t)1 << (B1 + B2));
+  pl->B1 = B1;
   pl->B2 = B2;
   pl->cap2 = (uint32_t)(mean2 * 1.15) + 256;
-  pl->chunks = (join_tiles(n) + CERT_PQ * 24 - 1) / (CERT_PQ * 24);
+  const uint32_t tpc = (CERT_PQ * 24) << (B1 - CERT_B1);
+  pl->chunks = (join_tiles(n) + tpc - 1) / tpc;
   return pl->cap2 <= CERT_SET * 3 / 4;
 }
 
-uint32_t cert_bins() { return CERT_BINS; }
 uint64_t cert_pool1_words(uint32_t n) { return (uint64_t)join_tiles(n) * JT; }
-uint64_t cert_dir_entries(uint32_t n) { return (uint64_t)join_tiles(n) * CERT_BINS; }
+uint64_t cert_dir_entries(uint32_t n, const CertPlan &pl) { return (uint64_t)join_tiles(n) << pl.B1; }
 
 void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
                  uint32_t *cparent, uint32_t *dp, unsigned long long *pool1, uint16_t *jdir, unsigned int *counters,
-                 uint32_t ablate) {
+                 const CertPlan &pl, uint32_t ablate) {
   if (!n) return;
-  hipLaunchKernelGGL(k_join_window, dim3(join_tiles(n)), dim3(JTT), 0, s, sid, pid, kind, n, cparent, dp, pool1, jdir,
-                     counters, ablate);
+  if (pl.B1 == CERT_B1W)
+    hipLaunchKernelGGL(k_join_window<CERT_B1W>, dim3(join_tiles(n)), dim3(JTT), 0, s, sid, pid, kind, n, cparent, dp,
+                       pool1, jdir, counters, ablate);
+  else
+    hipLaunchKernelGGL(k_join_window<CERT_B1>, dim3(join_tiles(n)), dim3(JTT), 0, s, sid, pid, kind, n, cparent, dp,
+                       pool1, jdir, counters, ablate);
 }
 
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
                        const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters) {
   if (!n) return;
   const size_t lds = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B2) * 4;
-  hipLaunchKernelGGL(k_cert_split<CERT_PQ>, dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n, pl.chunks,
-                     pl.B2, pool2, pl.cap2, cur2, counters);
+  if (pl.B1 == CERT_B1W)
+    hipLaunchKernelGGL((k_cert_split<CERT_PQ, CERT_B1W>), dim3((1u << CERT_B1W) * pl.chunks), dim3(1024), lds, s, pool1,
+                       jdir, n, pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
+  else
+    hipLaunchKernelGGL((k_cert_split<CERT_PQ, CERT_B1>), dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n,
+                       pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
 }
 
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
                        const unsigned int *cur2, unsigned int *counters) {
   if (!n) return;
-  hipLaunchKernelGGL(k_cert_check, dim3(CERT_BINS << pl.B2), dim3(CCT), 0, s, pool2, pl.cap2, cur2, 1u, counters);
+  hipLaunchKernelGGL(k_cert_check, dim3(1u << (pl.B1 + pl.B2)), dim3(CCT), 0, s, pool2, pl.cap2, cur2, 1u, counters);
 }
 
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,

@@ -10,7 +10,9 @@ namespace kmz {
 constexpr uint32_t JT = 2048, JH = 256, JW = JT + 2 * JH, JTT = 512;
 static_assert(JW < 4096, "local index + 1 must fit an entry's 12 bits");
 constexpr uint16_t L_NONE = 0xFFFF, L_MISS = 0xFFFE;
-constexpr uint32_t CERT_B1 = 6, CERT_BINS = 1u << CERT_B1;
+// certificate pass 1: 2^6 bins per join tile; 2^8 (CERT_B1W) past ~10^8 ids,
+// so that pass 2 still writes runs of ~8 records per sub-bin (cert_plan)
+constexpr uint32_t CERT_B1 = 6, CERT_BINS = 1u << CERT_B1, CERT_B1W = 8;
 
 // exclusive scan of LDS u32 array a[0..m) in place, any m <= 64 * blockDim.x
 __device__ __forceinline__ void block_scan_lds(uint32_t *a, uint32_t m, uint32_t *wsum) {
@@ -71,15 +73,17 @@ __device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >
 // compares fingerprints only
 __device__ __forceinline__ uint32_t jfp(uint32_t x) { return max(((x * 0x9E3779B1u) >> 18) & 0xF, 1u); }
 
-// lanes of this wave whose `v` (6 bits) equals mine, among `valid` lanes
-__device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) {
+// lanes of this wave whose `v` (B bits) equals mine, among `valid` lanes
+template <int B>
+__device__ __forceinline__ uint64_t match_bits(uint32_t v, uint64_t valid) {
   uint64_t m = valid;
 #pragma unroll
-  for (int bit = 0; bit < 6; ++bit) {
+  for (int bit = 0; bit < B; ++bit) {
     const uint64_t b = __ballot((v >> bit) & 1);
     m &= ((v >> bit) & 1) ? b : ~b;
   }
   return m;
 }
+__device__ __forceinline__ uint64_t match6(uint32_t v, uint64_t valid) { return match_bits<6>(v, valid); }
 
 }  // namespace kmz

@@ -83,11 +83,12 @@ void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape
                        uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint32_t S, unsigned int *counters,
                        unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp);
 // balanced K3 reduce (directory [partition][tile], i.e. produced with S = 1):
-// plan = 2 P + 1 u32 scratch, part = k3_bal_part_bytes(G)
+// plan = k3_plan_words(P) u32 scratch, part = k3_bal_part_bytes(G)
 void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
                           const uint32_t *dir, uint32_t *plan, unsigned long long *part, unsigned long long *grp,
                           bool unpacked = false);
 uint32_t k3_bal_items(uint32_t G);
+uint32_t k3_plan_words(uint32_t P);
 uint64_t k3_bal_part_bytes(uint32_t G);
 void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
                       const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp);
@@ -207,16 +208,17 @@ void launch_remap_index(hipStream_t s, unsigned long long *v, uint64_t n, uint32
 
 // window parent join + uniqueness certificate (kmz_join.hip)
 struct CertPlan {
-  uint32_t B2, cap2, chunks;
+  uint32_t B1, B2, cap2, chunks;  // 2^B1 pass-1 bins, 2^B2 sub-bins per bin
 };
-bool cert_plan(uint32_t n, CertPlan *pl);
-uint32_t cert_bins();
+// wide: pass 1 may use 2^8 bins (the window join; the guard's k_cert_bin
+// always bins by 2^6); force_wide: 2^8 bins at any size (test knob)
+bool cert_plan(uint32_t n, CertPlan *pl, bool wide = true, bool force_wide = false);
 uint64_t cert_pool1_words(uint32_t n);
-uint64_t cert_dir_entries(uint32_t n);
+uint64_t cert_dir_entries(uint32_t n, const CertPlan &pl);
 __host__ __device__ uint32_t join_tiles(uint32_t n);
 void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
                  uint32_t *cparent, uint32_t *dp, unsigned long long *pool1, uint16_t *jdir, unsigned int *counters,
-                 uint32_t ablate = 0);
+                 const CertPlan &pl, uint32_t ablate = 0);
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
                        const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters);
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,

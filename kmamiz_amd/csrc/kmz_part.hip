@@ -333,19 +333,34 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
 constexpr uint32_t K3_ITEMS = 1536;       // ~2 rounds of 3 workgroups per CU
 constexpr uint32_t K3_ITEM_MIN = 4096;    // records: below that an item is not worth its partial write-out
 
+// per-partition record counts from the [partition][tile] directory, each row
+// summed by K3_PSUM_SPLIT workgroups into partial sums (one workgroup per
+// partition reading its whole ~10^5-word row took ~0.08 ms at 10^8 spans)
+constexpr uint32_t K3_PSUM_SPLIT = 16;
 __global__ void __launch_bounds__(256) k3_psum(const uint32_t *__restrict__ dir, uint32_t ntiles,
                                                uint32_t *__restrict__ tot) {
   __shared__ uint32_t red[4];
   const uint32_t *row = dir + (uint64_t)blockIdx.x * ntiles;
+  const uint32_t per = (ntiles + K3_PSUM_SPLIT - 1) / K3_PSUM_SPLIT;
+  const uint32_t k0 = blockIdx.y * per, k1 = min(ntiles, k0 + per);
   uint32_t s = 0;
-  for (uint32_t k = threadIdx.x; k < ntiles; k += 256) {
-    const uint32_t x = row[k], o = x >> 16, c = x & 0xFFFF;
-    s += (o + c <= K3T) ? c : 0;
+  for (uint32_t kb = k0; kb < k1; kb += 8 * 256) {  // eight loads in flight per thread
+    uint32_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t k = kb + u * 256 + threadIdx.x;
+      x[u] = k < k1 ? row[k] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t o = x[u] >> 16, c = x[u] & 0xFFFF;
+      s += (o + c <= K3T) ? c : 0;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) tot[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) tot[(uint64_t)blockIdx.x * K3_PSUM_SPLIT + blockIdx.y] = red[0] + red[1] + red[2] + red[3];
 }
 
 // one workgroup: S_p and the exclusive scan item_off[0..P] (P <= K3PMAX)
@@ -354,7 +369,9 @@ __global__ void __launch_bounds__(1024) k3_plan(const uint32_t *__restrict__ tot
   __shared__ unsigned long long rsum[16];
   __shared__ uint32_t wsum[16];
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const uint32_t c = t < P ? tot[t] : 0;
+  uint32_t c = 0;
+  if (t < P)
+    for (uint32_t j = 0; j < K3_PSUM_SPLIT; ++j) c += tot[(uint64_t)t * K3_PSUM_SPLIT + j];
   unsigned long long r = c;
   for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
   if (lane == 0) rsum[w] = r;
@@ -381,38 +398,15 @@ __global__ void __launch_bounds__(1024) k3_plan(const uint32_t *__restrict__ tot
 // of the group partials (first index global).  The packed accumulators of
 // k3_reduce are used when the item holds < 2^22 records (counted first from
 // its directory words: records need not be spread evenly, e.g. input sorted by
-// endpoint), else the unpacked ones -- one 48 KB LDS block either way.
-__global__ void __launch_bounds__(K3RT) k3_reduce_bal(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
-                                                      uint32_t ntiles, uint32_t P, const uint32_t *__restrict__ item_off,
-                                                      uint32_t G, uint64_t index_base, uint32_t upk,
-                                                      unsigned long long *__restrict__ part) {
-  __shared__ unsigned long long acc[6 * K3R];
+// endpoint), else the unpacked ones -- one 48 KB LDS block either way.  The
+// record loop is instantiated for each accumulator form and chosen once per
+// workgroup (as the fixed-slice k3_reduce<PACK> is compiled), not per record.
+template <bool PACK>
+__device__ __forceinline__ void k3_reduce_items(const Rec *__restrict__ pool, const uint32_t *__restrict__ row,
+                                                uint64_t tb, uint64_t te, uint64_t index_base, unsigned long long *acc,
+                                                uint32_t (*r_pre)[K3RB], uint32_t (*r_off)[K3RB]) {
   constexpr uint32_t NW = K3RT / 64;
-  __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB], wred[NW];
-  const uint32_t item = blockIdx.x;
-  if (item >= item_off[P]) return;  // (the grid is an upper bound; uniform over the workgroup)
-  uint32_t lo = 0, hi = P;  // the partition: item_off[p] <= item < item_off[p + 1]
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) / 2;
-    if (item_off[mid] <= item) lo = mid; else hi = mid;
-  }
-  const uint32_t p = lo, j = item - item_off[p], sp = item_off[p + 1] - item_off[p];
-  const uint64_t tb = (uint64_t)j * ntiles / sp, te = (uint64_t)(j + 1) * ntiles / sp;
-  const uint32_t *row = dir + (uint64_t)p * ntiles;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t nrec = 0;
-  for (uint64_t k = tb + threadIdx.x; k < te; k += K3RT) {
-    const uint32_t x = row[k];
-    nrec += ((x >> 16) + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;
-  }
-  for (int o = 32; o > 0; o >>= 1) nrec += __shfl_xor(nrec, o, 64);
-  if (lane == 0) wred[w] = nrec;
-  for (uint32_t k = threadIdx.x; k < 6 * K3R; k += K3RT) acc[k] = k < 5 * K3R ? 0ull : ~0ull;
-  __syncthreads();
-  uint32_t tot = 0;
-  for (uint32_t k = 0; k < NW; ++k) tot += wred[k];
-  const bool pack = tot < (1u << 22) && !upk;  // (upk: test knob)
-  // packed: cs, s2, s1b, s2h, tsx, fst32 (u32) -- unpacked: cnt, s1, s2a, s2b, tsx, fst
   unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
                      *a_fst = acc + 5 * K3R;
   uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
@@ -454,7 +448,7 @@ __global__ void __launch_bounds__(K3RT) k3_reduce_bal(const Rec *__restrict__ po
         const uint32_t kl = xr[u].w & (K3R - 1);
         const uint64_t d = xr[u].d, dd = d * d;
         const uint64_t tile = k0 + run[u];
-        if (pack) {
+        if (PACK) {
           if (d < K3_SMALL_D) {
             atomicAdd(&a0[kl], (1ull << 42) + d);
             atomicAdd(&a1[kl], (unsigned long long)dd);
@@ -478,6 +472,52 @@ __global__ void __launch_bounds__(K3RT) k3_reduce_bal(const Rec *__restrict__ po
     }
     __builtin_amdgcn_wave_barrier();  // r_pre / r_off are rewritten by the next batch
   }
+}
+
+__global__ void __launch_bounds__(K3RT) k3_reduce_bal(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
+                                                      uint32_t ntiles, uint32_t P, const uint32_t *__restrict__ item_off,
+                                                      uint32_t G, uint64_t index_base, uint32_t upk,
+                                                      unsigned long long *__restrict__ part) {
+  __shared__ unsigned long long acc[6 * K3R];
+  constexpr uint32_t NW = K3RT / 64;
+  __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB], wred[NW];
+  const uint32_t item = blockIdx.x;
+  if (item >= item_off[P]) return;  // (the grid is an upper bound; uniform over the workgroup)
+  uint32_t lo = 0, hi = P;  // the partition: item_off[p] <= item < item_off[p + 1]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (item_off[mid] <= item) lo = mid; else hi = mid;
+  }
+  const uint32_t p = lo, j = item - item_off[p], sp = item_off[p + 1] - item_off[p];
+  const uint64_t tb = (uint64_t)j * ntiles / sp, te = (uint64_t)(j + 1) * ntiles / sp;
+  const uint32_t *row = dir + (uint64_t)p * ntiles;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t nrec = 0;
+  for (uint64_t kb = tb; kb < te; kb += 8 * K3RT) {  // eight loads in flight per thread
+    uint32_t x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t k = kb + u * K3RT + threadIdx.x;
+      x[u] = k < te ? row[k] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) nrec += ((x[u] >> 16) + (x[u] & 0xFFFF) <= K3T) ? (x[u] & 0xFFFF) : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) nrec += __shfl_xor(nrec, o, 64);
+  if (lane == 0) wred[w] = nrec;
+  for (uint32_t k = threadIdx.x; k < 6 * K3R; k += K3RT) acc[k] = k < 5 * K3R ? 0ull : ~0ull;
+  __syncthreads();
+  uint32_t tot = 0;
+  for (uint32_t k = 0; k < NW; ++k) tot += wred[k];
+  const bool pack = tot < (1u << 22) && !upk;  // (upk: test knob)
+  // packed: cs, s2, s1b, s2h, tsx, fst32 (u32) -- unpacked: cnt, s1, s2a, s2b, tsx, fst
+  unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
+                     *a_fst = acc + 5 * K3R;
+  uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
+  if (pack)
+    k3_reduce_items<true>(pool, row, tb, te, index_base, acc, r_pre, r_off);
+  else
+    k3_reduce_items<false>(pool, row, tb, te, index_base, acc, r_pre, r_off);
   __syncthreads();
   unsigned long long *b = part + (uint64_t)item * 6 * K3R;
   for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
@@ -700,8 +740,8 @@ void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_
                           bool unpacked) {
   if (!n || !G) return;
   const uint32_t P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
-  uint32_t *tot = plan, *item_off = plan + P;
-  hipLaunchKernelGGL(k3_psum, dim3(P), dim3(256), 0, s, dir, ntiles, tot);
+  uint32_t *tot = plan, *item_off = plan + (uint64_t)P * K3_PSUM_SPLIT;
+  hipLaunchKernelGGL(k3_psum, dim3(P, K3_PSUM_SPLIT), dim3(256), 0, s, dir, ntiles, tot);
   hipLaunchKernelGGL(k3_plan, dim3(1), dim3(1024), 0, s, tot, P, ntiles, item_off);
   hipLaunchKernelGGL(k3_reduce_bal, dim3(k3_bal_items(G)), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, P, item_off,
                      G, index_base, unpacked ? 1u : 0u, part);
@@ -709,6 +749,7 @@ void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_
                      item_off, G, grp);
 }
 
+uint32_t k3_plan_words(uint32_t P) { return P * K3_PSUM_SPLIT + P + 1; }
 uint32_t k3_bal_items(uint32_t G) { return K3_ITEMS + (G + K3R - 1) / K3R; }  // an upper bound of the plan's items
 uint64_t k3_bal_part_bytes(uint32_t G) { return (uint64_t)k3_bal_items(G) * 6 * K3R * 8; }
 uint32_t k3_partitions(uint32_t G) { return (G + K3R - 1) / K3R; }

@@ -436,6 +436,41 @@ def test_window_join_matches_span_table(engine):
     assert _info_results(a[4]) == _info_results(b[4])
 
 
+WIDE_CERT_BINS = 64  # KMZ_ABLATE2: the certificate's pass 1 in 2^8 bins (default past ~10^8 ids) at any size
+
+
+@pytest.mark.parametrize("repeat", [False, True])
+def test_wide_certificate_bins(engine, repeat):
+    """The certificate with 2^8 pass-1 bins (k_join_window<8>, k_cert_split's
+    binary-searched tile runs: the layout batches past ~10^8 ids take) proves
+    a clean mesh batch unique -- the window answers stand, results equal the
+    default plan's -- and catches one span id repeated far apart."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(3, 0, 20000)
+    table = synth.shape_table(3)
+    if repeat:
+        batch.span_id[len(batch) - 7] = batch.span_id[5]
+
+    def run(e):
+        e.load(batch, table)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        return e.triples(), e.endpoints(), e.groups(), e.info()
+
+    wide = _engine_with2(0, WIDE_CERT_BINS)
+    try:
+        a = run(wide)
+    finally:
+        wide.close()
+    b = run(engine)
+    assert bool(a[3]["path"] & 1) == (not repeat) and bool(b[3]["path"] & 1) == (not repeat)
+    assert np.array_equal(a[0], b[0]) and a[1].tobytes() == b[1].tobytes() and a[2].tobytes() == b[2].tobytes()
+    assert _info_results(a[3]) == _info_results(b[3])
+    if repeat:
+        assert a[3]["n_dups"] == 1
+
+
 SEPARATE_JOIN_WALK = 16  # KMZ_ABLATE2: k_join_window + k4_chain instead of the fused k_join_chain
 FUSED_ANY_SIZE = 32      # KMZ_ABLATE2: the fused k_join_chain at any batch size
 
