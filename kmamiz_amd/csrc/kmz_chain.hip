@@ -84,7 +84,7 @@ constexpr uint32_t KB1_MAX = 8, KB2_MAX = 8;
 // LDS cache of KCACHE keys).  Hot edge keys repeat ~10^5 times per run; without
 // the cache they overfill their slice's bucket.
 constexpr uint32_t KCACHE = 1024;
-#ifndef KMZ_GATHER_EARLY
+#ifndef KMZ_GATHER_EARLY  // where the next tile's endpoint gather is issued: 1 before the probes, 0 after the check, 2 at the tile's end
 #define KMZ_GATHER_EARLY 1
 #endif
 #ifndef KMZ_CHAIN_WAVES
@@ -381,7 +381,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     if (DIRECT) {  // (the rows staged their keys during the walk)
       if (more && FIRST) gather_ep();
     } else {
-#if KMZ_GATHER_EARLY
+#if KMZ_GATHER_EARLY == 1
       // the next tile's endpoints: its shapes landed during the walk; the
       // gather's round trip overlaps the probes' below (vmcnt is in order)
       if (more && FIRST) gather_ep();
@@ -429,7 +429,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           h = (h + 1) & (IMAP - 1);
         }
       }
-#if !KMZ_GATHER_EARLY
+#if KMZ_GATHER_EARLY == 0
       if (more && FIRST) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
 #endif
       if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
@@ -516,6 +516,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     };
     round(0u, std::true_type{});
     for (uint32_t r0 = TW * CTT; r0 < m; r0 += TW * CTT) round(r0, std::false_type{});
+#if KMZ_GATHER_EARLY == 2
+    if (!DIRECT && more) gather_ep();  // (diagnostic variant: at the tile's end, a full tile after the shapes' loads)
+#endif
   }
   // per workgroup: rows, relations, max depth, new chains
   if (flags) atomicOr(&counters[C_FLAGS], flags);
