@@ -87,6 +87,9 @@ constexpr uint32_t KCACHE = 1024;
 #ifndef KMZ_GATHER_EARLY  // where the next tile's endpoint gather is issued: 1 before the probes, 0 after the check, 2 at the tile's end
 #define KMZ_GATHER_EARLY 1
 #endif
+#ifndef KMZ_CAS_EARLY  // 1: the leaders' claim CAS issued before the tile's row counts (variant)
+#define KMZ_CAS_EARLY 0
+#endif
 #ifndef KMZ_CHAIN_WAVES
 #define KMZ_CHAIN_WAVES 4
 #endif
@@ -355,6 +358,31 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       walk(std::true_type{});
     else
       walk(std::false_type{});
+    // per span of the tile: row counts, pending list, rowpos (reads the walk's
+    // state only: with KMZ_CAS_EARLY it runs while the leaders' claims are in flight)
+    auto tile_stats = [&]() {
+#pragma unroll
+      for (int q = 0; q < TW; ++q) {
+        const uint32_t jl = jq[q], i = w0 + jl;
+        if (kq[q] == KIND_CLIENT) continue;  // (an empty walker slot)
+        const uint8_t kj = kq[q];
+        uint64_t rp = NONE64;
+        const bool pending = st[q] == S_PEND;
+        if (kj == KIND_SERVER) {
+          rp = index_base + i;
+          if (!pending) {
+            ++rows;
+            rel += dd[q];
+            maxd = max(maxd, dd[q]);
+          }
+        }
+        if (pending) {
+          const uint32_t x = atomicAdd(&counters[C_PLIST], 1u);
+          if (x < pcap) plist[x] = i;
+        }
+        if (rowpos_out) rowpos_out[i] = rp;
+      }
+    };
     if (DIRECT) drain(true);
 #pragma unroll
     for (int q = 0; q < TW; ++q) {
@@ -442,6 +470,14 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       // k_chain_settle otherwise.  Keys of a leader's chain are staged whether
       // or not it is new (duplicates are harmless in the edge set), so nothing
       // here waits on another workgroup.
+#if KMZ_CAS_EARLY
+      // the leaders' claims in flight while the tile's row counts are taken
+      unsigned long long cvq[TW];
+#pragma unroll
+      for (int q = 0; q < TW; ++q)
+        cvq[q] = hslot[q] <= IMAP ? atomicCAS(ctab + 2 * pos[q], 0ull, (unsigned long long)sg[q]) : 0ull;
+      tile_stats();
+#endif
 #pragma unroll
       for (int q = 0; q < TW; ++q) {
         if (hslot[q] > IMAP) {
@@ -453,7 +489,11 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         }
         const uint32_t jl = jq[q];
         unsigned long long *en = ctab + 2 * pos[q];
+#if KMZ_CAS_EARLY
+        const unsigned long long cv = cvq[q];
+#else
         const unsigned long long cv = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
+#endif
         const uint32_t d = dd[q];
         // a row whose chain this leader inserted (or lost to another chain: the
         // deferred check may insert it) stages its keys; one that joined the
@@ -487,30 +527,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       }
     }
     KMZ_STAMP(4);
-    // per span of the tile: row counts, pending list, rowpos
-#pragma unroll
-    for (int q = 0; q < TW; ++q) {
-      const uint32_t jl = jq[q], i = w0 + jl;
-      if (kq[q] == KIND_CLIENT) continue;  // (an empty walker slot)
-      const uint8_t kj = kq[q];
-      uint64_t rp = NONE64;
-      if (kj != KIND_CLIENT) {
-        const bool pending = st[q] == S_PEND;
-        if (kj == KIND_SERVER) {
-          rp = index_base + i;
-          if (!pending) {
-            ++rows;
-            rel += dd[q];
-            maxd = max(maxd, dd[q]);
-          }
-        }
-        if (pending) {
-          const uint32_t x = atomicAdd(&counters[C_PLIST], 1u);
-          if (x < pcap) plist[x] = i;
-        }
-      }
-      if (rowpos_out) rowpos_out[i] = rp;
-    }
+    if (DIRECT || !KMZ_CAS_EARLY) tile_stats();
     __syncthreads();  // LDS is rewritten by the next round / tile
     KMZ_STAMP(5);
     };
