@@ -36,9 +36,11 @@ sys.path.insert(0, ROOT)
 #   check  k_cert_check   certificate check: one read of it       8 B/span
 #   tail   k_tail_links   service tail: one read of each edge key  8 B/key
 #          (+ k_tail_compact; config 5 only)
+#   joinwalk k_join_chain the join and the chain walk fused (batches of
+#                         2^19..2^23 spans): K2's + K4's bytes  57 B/span + 12 B/relation
 def alg_bytes(kernel, n, n_server, relations, n_keys=0):
     return {"join": 57 * n, "stats": 19 * n, "reduce": 16 * n_server, "walk": 12 * relations,
-            "cert": 16 * n, "check": 8 * n, "tail": 8 * n_keys}.get(kernel, 0)
+            "cert": 16 * n, "check": 8 * n, "tail": 8 * n_keys, "joinwalk": 57 * n + 12 * relations}.get(kernel, 0)
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -304,16 +306,19 @@ def main():
     pipe_bytes = sum(v["alg_bytes"] for v in per_kernel.values() if v["alg_bytes"])
     kname = {"join": "k_join_window", "stats": "k3_produce" if "reduce" in per_kernel else "k_stats",
              "reduce": "k3_reduce", "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check",
-             "tail": "k_tail_links"}[dom]
+             "tail": "k_tail_links", "joinwalk": "k_join_chain"}[dom]
     tr = traffic_of(kname, config, n_local)
     # SURVEY.md 8d's kernels as whole units (every launch that does that
     # unit's work), next to the pieces: K2 = join + certificate + its fix-ups,
     # K3 = produce + reduce (or the one-pass k_stats / k3_small), K4 = the walk
     # + settle + pending ancestries
     units = {}
-    for u, parts, alg in (("K2", ("join", "cert", "check", "resolve"), 57 * n_local),
-                          ("K3", ("stats", "reduce"), 19 * n_local),
-                          ("K4", ("walk", "settle", "pend"), 12 * A)):
+    unit_defs = [("K2", ("join", "cert", "check", "resolve"), 57 * n_local), ("K3", ("stats", "reduce"), 19 * n_local),
+                 ("K4", ("walk", "settle", "pend"), 12 * A)]
+    if "joinwalk" in per_kernel:  # (the fused kernel does K2's join and K4's walk: one unit)
+        unit_defs = [("K2+K4", ("joinwalk", "cert", "check", "resolve", "settle", "pend"), 57 * n_local + 12 * A),
+                     unit_defs[1]]
+    for u, parts, alg in unit_defs:
         ms = sum(per_kernel[k]["ms_per_step"] for k in parts if k in per_kernel)
         if ms:
             gbs = alg / (ms * 1e-3) / 1e9

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "kmz_kernels.h"
 
@@ -330,7 +331,7 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
 // tiles), and k3_reduce_bal runs one workgroup per item.  k3_combine_bal folds
 // the items of each partition.
 // ---------------------------------------------------------------------------
-constexpr uint32_t K3_ITEMS = 1536;       // ~2 rounds of 3 workgroups per CU
+constexpr uint32_t K3_ITEMS = 1536;       // an upper bound: 2 rounds of 3 workgroups per CU on 256 CUs
 constexpr uint32_t K3_ITEM_MIN = 4096;    // records: below that an item is not worth its partial write-out
 
 // per-partition record counts from the [partition][tile] directory, each row
@@ -365,7 +366,7 @@ __global__ void __launch_bounds__(256) k3_psum(const uint32_t *__restrict__ dir,
 
 // one workgroup: S_p and the exclusive scan item_off[0..P] (P <= K3PMAX)
 __global__ void __launch_bounds__(1024) k3_plan(const uint32_t *__restrict__ tot, uint32_t P, uint32_t ntiles,
-                                                uint32_t *__restrict__ item_off) {
+                                                uint32_t nitems, uint32_t *__restrict__ item_off) {
   __shared__ unsigned long long rsum[16];
   __shared__ uint32_t wsum[16];
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -378,7 +379,7 @@ __global__ void __launch_bounds__(1024) k3_plan(const uint32_t *__restrict__ tot
   __syncthreads();
   unsigned long long R = 0;
   for (int k = 0; k < 16; ++k) R += rsum[k];
-  const unsigned long long target = max((R + K3_ITEMS - 1) / K3_ITEMS, (unsigned long long)K3_ITEM_MIN);
+  const unsigned long long target = max((R + nitems - 1) / nitems, (unsigned long long)K3_ITEM_MIN);
   const uint32_t sp = t < P ? (uint32_t)min((c + target - 1) / target, (unsigned long long)ntiles) : 0;
   const uint32_t s1 = t < P ? max(sp, 1u) : 0;
   uint32_t x = s1;  // inclusive scan over the workgroup
@@ -734,6 +735,25 @@ void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base
                        G, grp);
 }
 
+// workgroups of k3_reduce_bal the device keeps resident (CUs x occupancy),
+// queried once per device; 768 (256 CUs x 3) if the query fails
+static uint32_t k3_resident() {
+  static std::mutex mu;
+  static uint32_t cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 768;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!cached[dev]) {
+    int cus = 0, occ = 0;
+    uint32_t g = 768;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k3_reduce_bal, K3RT, 0) == hipSuccess && occ > 0)
+      g = (uint32_t)cus * (uint32_t)occ;
+    cached[dev] = g;
+  }
+  return cached[dev];
+}
+
 // balanced: per-partition record counts, the item plan, one workgroup per item
 void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
                           const uint32_t *dir, uint32_t *plan, unsigned long long *part, unsigned long long *grp,
@@ -742,7 +762,12 @@ void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_
   const uint32_t P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
   uint32_t *tot = plan, *item_off = plan + (uint64_t)P * K3_PSUM_SPLIT;
   hipLaunchKernelGGL(k3_psum, dim3(P, K3_PSUM_SPLIT), dim3(256), 0, s, dir, ntiles, tot);
-  hipLaunchKernelGGL(k3_plan, dim3(1), dim3(1024), 0, s, tot, P, ntiles, item_off);
+  // items: Σ_p ceil(T_p / target) <= nitems + P, so nitems = 2 rounds of the
+  // resident workgroups less P keeps the rounding's extra items out of a third,
+  // nearly empty round (the mesh: 1595 items for 1536 slots took 0.35 ms)
+  const uint32_t slots = std::min<uint32_t>(K3_ITEMS, 2 * k3_resident());
+  const uint32_t nitems = slots > P + 256 ? slots - P : 256;
+  hipLaunchKernelGGL(k3_plan, dim3(1), dim3(1024), 0, s, tot, P, ntiles, nitems, item_off);
   hipLaunchKernelGGL(k3_reduce_bal, dim3(k3_bal_items(G)), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, P, item_off,
                      G, index_base, unpacked ? 1u : 0u, part);
   hipLaunchKernelGGL(k3_combine_bal, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part,
