@@ -84,8 +84,11 @@ constexpr uint32_t KB1_MAX = 8, KB2_MAX = 8;
 // LDS cache of KCACHE keys).  Hot edge keys repeat ~10^5 times per run; without
 // the cache they overfill their slice's bucket.
 constexpr uint32_t KCACHE = 1024;
-#ifndef KMZ_GATHER_EARLY  // where the next tile's endpoint gather is issued: 1 before the probes, 0 after the check, 2 at the tile's end
-#define KMZ_GATHER_EARLY 1
+// where the next tile's endpoint gather is issued: 0 after the probes' check
+// (round 3: mesh walk 1.11 -> 1.08 ms, two A/B runs, tools/r03_var.sh), 1
+// before the probes (round 2's choice), 2 at the tile's end (1.09-1.11)
+#ifndef KMZ_GATHER_EARLY
+#define KMZ_GATHER_EARLY 0
 #endif
 #ifndef KMZ_CAS_EARLY  // 1: the leaders' claim CAS issued before the tile's row counts (variant)
 #define KMZ_CAS_EARLY 0
@@ -410,8 +413,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
       if (more && FIRST) gather_ep();
     } else {
 #if KMZ_GATHER_EARLY == 1
-      // the next tile's endpoints: its shapes landed during the walk; the
-      // gather's round trip overlaps the probes' below (vmcnt is in order)
+      // the next tile's endpoints (variant): the gather's round trip overlaps
+      // the probes' below, but the shapes may not have landed yet
       if (more && FIRST) gather_ep();
 #endif
       ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
@@ -458,7 +461,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
         }
       }
 #if KMZ_GATHER_EARLY == 0
-      if (more && FIRST) gather_ep();  // the next tile's endpoints (its shapes have landed by now)
+      // the next tile's endpoints: its shapes have landed by now, and the
+      // gather's round trip overlaps the leaders and the row counts
+      if (more && FIRST) gather_ep();
 #endif
       if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
 #pragma unroll
