@@ -115,6 +115,10 @@ constexpr uint32_t TAIL_LAGG = 1024;  // per-workgroup LDS detail slots (20 KB)
 // it is not a first occurrence and needs no global probe.  (A slot overwritten
 // by another key only costs a probe.)
 constexpr uint32_t TAIL_LSEEN = 2048, TAIL_PSEEN = 512;
+#ifndef KMZ_TAIL_U
+#define KMZ_TAIL_U 4
+#endif
+constexpr int TAIL_U = KMZ_TAIL_U;  // edge keys per thread and step
 
 // link key: svc << 40 | cls << 16 | type << 15 | d   (type 1 = SERVER / dependingOn)
 // detail key: svc << 40 | lsvc << 16 | d
@@ -148,61 +152,87 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
     lval[x][0] = lval[x][1] = lval[x][2] = 0;
   }
   __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = keys[i];
-    const uint32_t a = (uint32_t)(k >> 40), s = (uint32_t)(k >> 16) & 0xFFFFFFu, d = (uint32_t)(k >> 1) & 0x7FFFu;
-    const bool on = (k & 1) != 0;
-    if (a >= n_ep || s >= n_ep || cls[a] >= n_cls || cls[s] >= n_cls) {
-      flags |= F_RANGE;
-      continue;
+  // TAIL_U keys per thread and step: their loads and table gathers are issued
+  // together (the per-key chain of dependent loads is what bounds this kernel)
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += TAIL_U * stride) {
+    uint64_t kq[TAIL_U];
+#pragma unroll
+    for (int u = 0; u < TAIL_U; ++u) {
+      const uint64_t i = i0 + u * stride;
+      kq[u] = i < n ? keys[i] : 0;
     }
-    if (!hasin[s]) hasin[s] = 1;  // (read first: ~10^7 keys share ~10^4 bytes)
-    // desc's row: (anc, d) in dependingBy
-    uint32_t side = 0;
-    uint64_t lk[2];
-    lk[side++] = ((uint64_t)svc[s] << 40) | ((uint64_t)cls[a] << 16) | d;
-    if (on) lk[side++] = ((uint64_t)svc[a] << 40) | ((uint64_t)cls[s] << 16) | (1u << 15) | d;
-    if (knobs & 1) side = 0;  // (diagnostic knob: no link keys -- timing only, wrong results)
-    for (uint32_t t = 0; t < side; ++t) {
-      unsigned long long &seen = lseen[(uint32_t)(lk[t] * 0x9E3779B97F4A7C15ull >> 53) & (TAIL_LSEEN - 1)];
-      if (seen == lk[t]) continue;  // put in the set by this workgroup already
-      const bool won = tail_set_put(lset, lcap, lk[t], &flags);
-      seen = lk[t];  // (in the set now, whoever won)
-      if (!won) continue;
-      ++won_l;
-      const uint32_t c = (uint32_t)(lk[t] >> 16) & 0xFFFFFFu;
-      const uint64_t dk = (lk[t] & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
-      const uint32_t ty = (uint32_t)(lk[t] >> 15) & 1u;  // dependingBy (CLIENT) / dependingOn (SERVER)
-      uint32_t h = (uint32_t)(mix64(dk) & (TAIL_LAGG - 1));
-      bool done = false;
-      for (uint32_t z = 0; z < 16; ++z) {
-        const unsigned long long cur = atomicCAS(&lkey[h], 0ull, (unsigned long long)dk);
-        if (cur == 0 || cur == dk) {
-          atomicAdd(&lval[h][0], 1u);
-          atomicAdd(&lval[h][1 + ty], 1u);
-          done = true;
-          break;
+    uint32_t cq_a[TAIL_U], cq_s[TAIL_U], sv_a[TAIL_U], sv_s[TAIL_U], us_a[TAIL_U];
+    bool okq[TAIL_U];
+#pragma unroll
+    for (int u = 0; u < TAIL_U; ++u) {
+      const uint32_t a = (uint32_t)(kq[u] >> 40), s = (uint32_t)(kq[u] >> 16) & 0xFFFFFFu;
+      okq[u] = i0 + u * stride < n;
+      const bool in = a < n_ep && s < n_ep;
+      cq_a[u] = in ? cls[a] : NONE;
+      cq_s[u] = in ? cls[s] : NONE;
+      sv_a[u] = in ? svc[a] : 0;
+      sv_s[u] = in ? svc[s] : 0;
+      us_a[u] = in ? usn[a] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < TAIL_U; ++u) {
+      if (!okq[u]) continue;
+      const uint64_t k = kq[u];
+      const uint32_t a = (uint32_t)(k >> 40), s = (uint32_t)(k >> 16) & 0xFFFFFFu, d = (uint32_t)(k >> 1) & 0x7FFFu;
+      const bool on = (k & 1) != 0;
+      if (a >= n_ep || s >= n_ep || cq_a[u] >= n_cls || cq_s[u] >= n_cls) {
+        flags |= F_RANGE;
+        continue;
+      }
+      if (!hasin[s]) hasin[s] = 1;  // (read first: ~10^7 keys share ~10^4 bytes)
+      // desc's row: (anc, d) in dependingBy
+      uint32_t side = 0;
+      uint64_t lk[2];
+      lk[side++] = ((uint64_t)sv_s[u] << 40) | ((uint64_t)cq_a[u] << 16) | d;
+      if (on) lk[side++] = ((uint64_t)sv_a[u] << 40) | ((uint64_t)cq_s[u] << 16) | (1u << 15) | d;
+      if (knobs & 1) side = 0;  // (diagnostic knob: no link keys -- timing only, wrong results)
+      for (uint32_t t = 0; t < side; ++t) {
+        unsigned long long &seen = lseen[(uint32_t)(lk[t] * 0x9E3779B97F4A7C15ull >> 53) & (TAIL_LSEEN - 1)];
+        if (seen == lk[t]) continue;  // put in the set by this workgroup already
+        const bool won = tail_set_put(lset, lcap, lk[t], &flags);
+        seen = lk[t];  // (in the set now, whoever won)
+        if (!won) continue;
+        ++won_l;
+        const uint32_t c = (uint32_t)(lk[t] >> 16) & 0xFFFFFFu;
+        const uint64_t dk = (lk[t] & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
+        const uint32_t ty = (uint32_t)(lk[t] >> 15) & 1u;  // dependingBy (CLIENT) / dependingOn (SERVER)
+        uint32_t h = (uint32_t)(mix64(dk) & (TAIL_LAGG - 1));
+        bool done = false;
+        for (uint32_t z = 0; z < 16; ++z) {
+          const unsigned long long cur = atomicCAS(&lkey[h], 0ull, (unsigned long long)dk);
+          if (cur == 0 || cur == dk) {
+            atomicAdd(&lval[h][0], 1u);
+            atomicAdd(&lval[h][1 + ty], 1u);
+            done = true;
+            break;
+          }
+          h = (h + 1) & (TAIL_LAGG - 1);
         }
-        h = (h + 1) & (TAIL_LAGG - 1);
+        if (!done) detail_add(dk, 1u, ty == 0, ty == 1, akey, aval, acap, fkey, fval, fcap, sstat, &flags);
       }
-      if (!done) detail_add(dk, 1u, ty == 0, ty == 1, akey, aval, acap, fkey, fval, fcap, sstat, &flags);
-    }
-    // cohesion: (consumer service, consumed endpoint) at distance 1
-    bool pwon = false;
-    if (d == 1 && !(knobs & 2)) {
-      const uint64_t pk = ((uint64_t)(s + 1) << 32) | usn[a];
-      unsigned long long &pseen_e = pseen[(uint32_t)(pk * 0x9E3779B97F4A7C15ull >> 55) & (TAIL_PSEEN - 1)];
-      if (pseen_e != pk) {
-        pwon = tail_set_put(pset, pcap, pk, &flags);
-        pseen_e = pk;
+      // cohesion: (consumer service, consumed endpoint) at distance 1
+      bool pwon = false;
+      if (d == 1 && !(knobs & 2)) {
+        const uint64_t pk = ((uint64_t)(s + 1) << 32) | us_a[u];
+        unsigned long long &pseen_e = pseen[(uint32_t)(pk * 0x9E3779B97F4A7C15ull >> 55) & (TAIL_PSEEN - 1)];
+        if (pseen_e != pk) {
+          pwon = tail_set_put(pset, pcap, pk, &flags);
+          pseen_e = pk;
+        }
       }
-    }
-    if (pwon) {
-      ++won_p;
-      const uint64_t p = tail_agg_slot(pkey, pacap, ((uint64_t)(svc[s] + 1) << 32) | usn[a], &flags);
-      if (p != pacap) {
-        atomicAdd(&sstat[8 * svc[s] + TS_CONSUMES], 1u);
-        if (atomicAdd(&pval[p], 1u) == 0) atomicAdd(&sstat[8 * svc[s] + TS_CONSUMERS], 1u);
+      if (pwon) {
+        ++won_p;
+        const uint64_t p = tail_agg_slot(pkey, pacap, ((uint64_t)(sv_s[u] + 1) << 32) | us_a[u], &flags);
+        if (p != pacap) {
+          atomicAdd(&sstat[8 * sv_s[u] + TS_CONSUMES], 1u);
+          if (atomicAdd(&pval[p], 1u) == 0) atomicAdd(&sstat[8 * sv_s[u] + TS_CONSUMERS], 1u);
+        }
       }
     }
   }
