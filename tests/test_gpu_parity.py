@@ -541,13 +541,12 @@ def test_fused_join_walk_equals_two_kernels(engine, case):
 # ---------------------------------------------------------------------------
 # K4 chain interning: hash collisions, deep chains (kmz_chain.hip)
 # ---------------------------------------------------------------------------
-def test_sig_collision_is_detected_and_retried(engine):
+@pytest.mark.parametrize("separate", [False, True])
+def test_sig_collision_is_detected_and_retried(engine, separate):
     """KMZ_ABLATE bit 24 truncates the ancestry sigs to 4 bits on the first
     seed: different chains share sigs, the exact entry checks raise F_SIG, and
-    the run repeats with another seed.  The result must equal a normal run."""
-    import os
-
-    from kmamiz_amd import Engine
+    the run repeats with another seed.  The result must equal a normal run --
+    in the fused join + walk (this batch's default) and in k4_chain."""
     from kmamiz_amd import _lib as L
     from kmamiz_amd import synth
 
@@ -557,11 +556,7 @@ def test_sig_collision_is_detected_and_retried(engine):
         return e.triples(), e.endpoints(), e.info()
 
     a = run(engine)
-    os.environ["KMZ_ABLATE"] = str(1 << 24)
-    try:
-        e2 = Engine(0)
-    finally:
-        del os.environ["KMZ_ABLATE"]
+    e2 = _engine_with2(1 << 24, 16 if separate else 0)  # (KMZ_ABLATE2 bit 4: the two kernels)
     try:
         b = run(e2)
     finally:
@@ -576,8 +571,9 @@ SPIN_NO_WAIT = 1 << 11     # KMZ_ABLATE: every chain-table wait "runs out" at on
 FORCE_INTERNING = 1 << 29  # KMZ_ABLATE: K4 chain interning even where auto mode would enumerate
 
 
+@pytest.mark.parametrize("separate", [False, True])
 @pytest.mark.parametrize("knob", [SPIN_TINY_DEFER, SPIN_NO_WAIT, SPIN_TINY_DEFER | SPIN_NO_WAIT])
-def test_chain_waits_never_drop_results(knob):
+def test_chain_waits_never_drop_results(knob, separate):
     """The chain-table waits of kmz_chain.hip (a leader whose workgroup's
     deferred list is full, k_chain_settle's deferred checks, k4_chain_pend)
     on config 5 with chain interning, where a fresh table makes workgroups
@@ -585,13 +581,14 @@ def test_chain_waits_never_drop_results(knob):
     waits that once hung config 5; a zero wait bound makes every wait run out,
     which must raise F_SPIN and redo the run on the exact walk (path bit 3),
     never drop a row, an ancestor's timestamp or a check.  Both equal the C
-    oracle (Traces.ts:128-143, 192-208)."""
+    oracle (Traces.ts:128-143, 192-208).  The batch (1.4e6 spans) takes the
+    fused join + walk; ``separate``: k_join_window + k4_chain."""
     from kmamiz_amd import synth
 
     batch, _ = synth.host_batch(5, 0, 20000)
     table = synth.shape_table(5)
     odeps = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
-    e = _engine_with(knob | FORCE_INTERNING)
+    e = _engine_with2(knob | FORCE_INTERNING, 16 if separate else 0)
     try:
         for run in range(2):  # a fresh chain table, then a cleared one
             info = _compare_synth(e, batch, table, odeps)
