@@ -22,7 +22,7 @@ fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o mesh -- python3 bench.py --steps 5 --warmup 2 --cpu-seconds 0 > $O/prof.log 2>&1 || exit 1
 bash tools/traffic.sh $TAG > $O/traffic.log 2>&1 || exit 1
 timeout -k 10 300 python -u bench.py > $O/bench_mesh.json 2> $O/bench_mesh.err || exit 1
-timeout -k 10 300 python -u bench.py --config bookinfo --steps 20 --warmup 5 > $O/bench_book.json 2> $O/bench_book.err || exit 1
+timeout -k 10 300 python -u bench.py --config bookinfo --steps 200 --warmup 50 > $O/bench_book.json 2> $O/bench_book.err || exit 1
 timeout -k 10 300 python -u bench.py --config power --steps 10 --warmup 3 > $O/bench_power.json 2> $O/bench_power.err || exit 1
 timeout -k 10 300 python -u tools/bench_tick.py > $O/tick.json 2> $O/tick.err || exit 1
 bash tools/rehearse_multi.sh 2 --spans 2e7 > $O/rehearse2.json 2> $O/rehearse2.err || exit 1
