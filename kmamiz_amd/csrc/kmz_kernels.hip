@@ -795,7 +795,10 @@ void launch_collapse_endpoints(hipStream_t s, const unsigned long long *sg, uint
 
 void launch_compact(hipStream_t s, const unsigned long long *trip, uint64_t tcap, unsigned long long *out,
                     unsigned long long *count) {
-  hipLaunchKernelGGL(k_compact, dim3(COMPACT_BLOCKS), dim3(256), 0, s, trip, tcap, out, count);
+  // (<= 8192 slots per workgroup: config 5's 2^25-slot set in 512 workgroups
+  // was a 256-step dependent loop per workgroup, 0.28 ms)
+  const uint32_t g = (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(COMPACT_BLOCKS, tcap / 8192));
+  hipLaunchKernelGGL(k_compact, dim3(g), dim3(256), 0, s, trip, tcap, out, count);
 }
 
 void launch_synth_count(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, uint64_t *cnt) {
