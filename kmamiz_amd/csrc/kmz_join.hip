@@ -36,6 +36,11 @@ namespace kmz {
 #endif
 constexpr uint32_t CERT_PQ = KMZ_CERT_PQ;  // pass 2: records per thread (chunks of PQ * 1024 records of one bin)
 constexpr uint32_t CERT_SET = 8192;    // pass-3 LDS set (u64), sub-bins <= 6144 records
+// certificate pass 1's ranks from LDS atomics (1) or from 6 wave ballots
+// per span (0: 1.09 against 1.00 ms for k_join_window on config 3)
+#ifndef KMZ_RANK_ATOMIC
+#define KMZ_RANK_ATOMIC 1
+#endif
 
 __host__ __device__ uint32_t join_tiles(uint32_t n) { return (n + JT - 1) / JT; }
 
@@ -282,13 +287,33 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   KMZ_JSTAMP(3);
   if (ablate & 64) return;  // diagnostic: no certificate pass 1
   // certificate pass 1: the tile's hashed ids into 2^B1 bins.  Ranks come
-  // from wave ballots and per-wave counters (no LDS atomics on hot words).
+  // from per-wave bin counters (LDS atomics with return), or where the LDS
+  // has no room for them (2^8 bins) from wave ballots.
   for (uint32_t e = threadIdx.x; e < BINS * NW; e += JTT) wcnt[e] = 0;
   __syncthreads();  // lbkt free from here on
   uint64_t *stg = reinterpret_cast<uint64_t *>(lbkt);
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1;
   uint32_t rk[PT];
+#if KMZ_RANK_ATOMIC
+  if constexpr (2 * BINS * NW <= (sizeof(lcw) / sizeof(uint32_t))) {
+    // wave-major counters (a wave's 64 lanes spread over the banks; the
+    // order within a bin is immaterial to the certificate), transposed to
+    // bin-major for the scan.  The 6 ballots per span this replaces were an
+    // eighth of the kernel's VALU instructions.
+    uint32_t *const wmaj = lcw + BINS * NW;
+    for (uint32_t e = threadIdx.x; e < BINS * NW; e += JTT) wmaj[e] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const uint32_t i = t0 + q * JTT + threadIdx.x;
+      rk[q] = i < t1 ? atomicAdd(&wmaj[w * BINS + (uint32_t)(hv[q] >> (64 - B1))], 1u) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < BINS * NW; e += JTT) wcnt[e] = wmaj[(e % NW) * BINS + e / NW];
+  } else
+#endif
+  {
 #pragma unroll
   for (int q = 0; q < PT; ++q) {
     const uint32_t i = t0 + q * JTT + threadIdx.x;
@@ -299,6 +324,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
     if (ok) prior = wcnt[bin * NW + w];
     rk[q] = prior + __popcll(peers & lt);
     if (ok && (peers & lt) == 0) wcnt[bin * NW + w] = prior + __popcll(peers);
+  }
   }
   __syncthreads();
   block_scan_lds(wcnt, BINS * NW, wsum);  // bin-major, wave-minor offsets
