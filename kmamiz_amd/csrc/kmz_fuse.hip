@@ -310,6 +310,22 @@ __global__ void __launch_bounds__(JTT, 4) k_join_chain(
     uint64_t *stg = reinterpret_cast<uint64_t *>(lbkt);
     const uint64_t lt = (1ull << lane) - 1;
     uint32_t rk[FPT];
+#if KMZ_RANK_ATOMIC
+    // ranks from wave-major LDS bin counters in the dead bucket counts
+    // (k_join_window), transposed to bin-major for the scan
+    uint32_t *const wmaj = lcnt;
+    static_assert(CERT_BINS * NW <= JB, "the wave-major counters live in the bucket counts");
+    for (uint32_t x = threadIdx.x; x < CERT_BINS * NW; x += JTT) wmaj[x] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < FPT; ++q)
+      rk[q] = t0 + q * JTT + threadIdx.x < t1
+                  ? atomicAdd(&wmaj[wv * CERT_BINS + (uint32_t)(hv[q] >> (64 - CERT_B1))], 1u)
+                  : 0u;
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < CERT_BINS * NW; x += JTT) wcnt[x] = wmaj[(x % NW) * CERT_BINS + x / NW];
+    (void)lt;
+#else
 #pragma unroll
     for (int q = 0; q < FPT; ++q) {
       const bool ok = t0 + q * JTT + threadIdx.x < t1;
@@ -320,6 +336,7 @@ __global__ void __launch_bounds__(JTT, 4) k_join_chain(
       rk[q] = prior + __popcll(peers & lt);
       if (ok && (peers & lt) == 0) wcnt[bin * NW + wv] = prior + __popcll(peers);
     }
+#endif
     __syncthreads();
     block_scan_lds(wcnt, CERT_BINS * NW, wsum);
     if (threadIdx.x < CERT_BINS) jdir[(uint64_t)blockIdx.x * CERT_BINS + threadIdx.x] = (uint16_t)wcnt[threadIdx.x * NW];

@@ -36,11 +36,6 @@ namespace kmz {
 #endif
 constexpr uint32_t CERT_PQ = KMZ_CERT_PQ;  // pass 2: records per thread (chunks of PQ * 1024 records of one bin)
 constexpr uint32_t CERT_SET = 8192;    // pass-3 LDS set (u64), sub-bins <= 6144 records
-// certificate pass 1's ranks from LDS atomics (1) or from 6 wave ballots
-// per span (0: 1.09 against 1.00 ms for k_join_window on config 3)
-#ifndef KMZ_RANK_ATOMIC
-#define KMZ_RANK_ATOMIC 1
-#endif
 
 __host__ __device__ uint32_t join_tiles(uint32_t n) { return (n + JT - 1) / JT; }
 

@@ -13,6 +13,11 @@ constexpr uint16_t L_NONE = 0xFFFF, L_MISS = 0xFFFE;
 // certificate pass 1: 2^6 bins per join tile; 2^8 (CERT_B1W) past ~10^8 ids,
 // so that pass 2 still writes runs of ~8 records per sub-bin (cert_plan)
 constexpr uint32_t CERT_B1 = 6, CERT_BINS = 1u << CERT_B1, CERT_B1W = 8;
+// certificate pass 1's ranks from LDS atomics (1) or from 6 wave ballots
+// per span (0: 1.09 against 1.00 ms for k_join_window on config 3)
+#ifndef KMZ_RANK_ATOMIC
+#define KMZ_RANK_ATOMIC 1
+#endif
 
 // exclusive scan of LDS u32 array a[0..m) in place, any m <= 64 * blockDim.x
 __device__ __forceinline__ void block_scan_lds(uint32_t *a, uint32_t m, uint32_t *wsum) {
