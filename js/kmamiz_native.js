@@ -393,7 +393,9 @@ class NativeTraces {
       }
       return chain;
     });
-    return rows.map((s, r) => {
+    // new EndpointDependencies(dependencies) (Traces.ts:210): the constructor's
+    // deprecation filter (EndpointDependencies.ts:44-74)
+    return cache.filterOutDeprecatedRows(rows.map((s, r) => {
       const by = uppers[r].map(([q, d]) => ({ endpoint: info(q), distance: d, type: "CLIENT" }));
       const seen = new Map();
       for (const [t, d] of lower.get(s) || []) seen.set(`${dep[b.spans.shape[t]]}\t${d}`, [t, d]);
@@ -408,7 +410,7 @@ class NativeTraces {
         dependingBy: by,
         dependingOn: on,
       };
-    });
+    }));
   }
   // Service-level tail of the reduced graph (EndpointDependencies([]).combineWith(deps).trim()),
   // from the GPU's per-service counters (kmz_tail_run): toServiceInstability

@@ -75,6 +75,45 @@ class Registry {
   }
 }
 
+// ---- the constructor's deprecation filter (EndpointDependencies.ts:20-74) ----------
+// EndpointDependencies.parseThresholdToMilliseconds (20-31)
+function parseThresholdToMilliseconds(s) {
+  if (!s) return 0;
+  const m = s.match(/(?:(\d+)d)?(?:(\d+)h)?(?:(\d+)m)?/);
+  if (!m) return 0;
+  const d = m[1] ? parseInt(m[1], 10) : 0, h = m[2] ? parseInt(m[2], 10) : 0, mi = m[3] ? parseInt(m[3], 10) : 0;
+  return ((d * 86400) + (h * 3600) + (mi * 60)) * 1000;
+}
+// the class's static threshold, parsed once at load from GlobalSettings'
+// DEPRECATED_ENDPOINT_THRESHOLD (GlobalSettings.ts:79, EndpointDependencies.ts:33-36)
+const deprecation = { ms: parseThresholdToMilliseconds(process.env.DEPRECATED_ENDPOINT_THRESHOLD || "") };
+function setDeprecatedThreshold(s) {
+  deprecation.ms = parseThresholdToMilliseconds(s || "");
+}
+// now - threshold, or 0 (no filter) -- taken when an EndpointDependencies is built (49-54)
+function deprecatedCutoff() {
+  return deprecation.ms === 0 ? 0 : Date.now() - deprecation.ms;
+}
+// filterOutDeprecatedEndpoint (44-74) over TEndpointDependency objects; like
+// the TS it assigns the filtered lists into the rows it keeps
+function filterOutDeprecatedRows(rows, cutoff) {
+  if (cutoff === undefined) cutoff = deprecatedCutoff();
+  if (cutoff === 0) return rows;
+  const gone = new Set();
+  const kept = rows.filter((d) => {
+    if (d.lastUsageTimestamp < cutoff) {
+      gone.add(d.endpoint.uniqueEndpointName);
+      return false;
+    }
+    return true;
+  });
+  for (const d of kept) {
+    d.dependingBy = d.dependingBy.filter((x) => !gone.has(x.endpoint.uniqueEndpointName));
+    d.dependingOn = d.dependingOn.filter((x) => !gone.has(x.endpoint.uniqueEndpointName));
+  }
+  return kept;
+}
+
 // Reduced EndpointDependencies: one merged row per endpoint.  Rows (in row
 // order): rowEp (registry id), rowInfo / rowTs (the row's `endpoint`), rowLast
 // (lastUsageTimestamp), rowExt (isDependedByExternal).  Entries: eRow (the
@@ -154,7 +193,7 @@ class ReducedDependencies {
       if (row > maxHi) maxHi = row;
     }
     out.nextHi = maxHi + 1;
-    return out;
+    return out.filtered();  // (every EndpointDependencies built on the way filters)
   }
 
   // Columns of TEndpointDependency objects (the cache's JSON).  mergeRows
@@ -167,6 +206,7 @@ class ReducedDependencies {
     const R = out.reg;
     const order = [];
     const byEp = new Map();
+    rows = filterOutDeprecatedRows(rows.slice());  // new EndpointDependencies(rows)
     const lists = (r) =>
       ["dependingBy", "dependingOn"].map((lk) => {
         const seen = new Map(), lst = [];
@@ -224,6 +264,29 @@ class ReducedDependencies {
         }
     }
     out.nextHi = 1;
+    return mergeRows ? out.filtered() : out;
+  }
+
+  // the constructor's deprecation filter (EndpointDependencies.ts:44-74) on the
+  // columns: rows used before the cutoff go, with every entry naming them
+  filtered(cutoff) {
+    if (cutoff === undefined) cutoff = deprecatedCutoff();
+    if (cutoff === 0) return this;
+    const gone = new Set();
+    this.rowEp.forEach((e, k) => {
+      if (this.rowLast[k] < cutoff) gone.add(e);
+    });
+    if (gone.size === 0) return this;
+    const out = new ReducedDependencies(this.reg);
+    const rk = [];
+    this.rowEp.forEach((e, k) => {
+      if (!gone.has(e)) rk.push(k);
+    });
+    for (const c of ["rowEp", "rowInfo", "rowTs", "rowLast", "rowExt"]) out[c] = rk.map((k) => this[c][k]);
+    const ek = [];
+    for (let j = 0; j < this.eRow.length; j++) if (!gone.has(this.eRow[j]) && !gone.has(this.eEp[j])) ek.push(j);
+    for (const c of ["eRow", "eSide", "eEp", "eDist", "eInfo", "eTs", "eHi", "eLo"]) out[c] = ek.map((j) => this[c][j]);
+    out.nextHi = this.nextHi;
     return out;
   }
 
@@ -279,13 +342,14 @@ class ReducedDependencies {
       out.eLo.push(rank++);
     }
     out.nextHi = this.nextHi + 1;
-    return out;
+    return out.filtered();  // new EndpointDependencies(...) (EndpointDependencies.ts:539-541)
   }
 
-  // EndpointDependencies.ts:91-112: the identity here (entries are unique per
-  // (row, side, name, distance) by construction)
+  // EndpointDependencies.ts:91-112: no list dedup needed here (entries are
+  // unique per (row, side, name, distance) by construction); the new object's
+  // constructor filters deprecated endpoints
   trim() {
-    return this;
+    return this.filtered();
   }
 
   get length() {
@@ -327,7 +391,8 @@ function trimRows(rows) {
     for (const x of lst) m.set(`${x.distance}\t${x.endpoint.uniqueEndpointName}`, x);
     return [...m.values()];
   };
-  return rows.map((d) => Object.assign({}, d, { dependingBy: dedup(d.dependingBy), dependingOn: dedup(d.dependingOn) }));
+  return filterOutDeprecatedRows(
+    rows.map((d) => Object.assign({}, d, { dependingBy: dedup(d.dependingBy), dependingOn: dedup(d.dependingOn) })));
 }
 
 // RealtimeWorkerImpl.ts:67-70: existingDep ? new EndpointDependencies(existingDep).combineWith(newDep) : newDep
@@ -555,4 +620,5 @@ class CCombinedRealtimeData {
 }
 
 module.exports = { Registry, ReducedDependencies, CombinedColumns, CEndpointDependencies, CCombinedRealtimeData,
-                   workerDependencies, combineLatencyCVAndMean, toPrecise, trimRows };
+                   workerDependencies, combineLatencyCVAndMean, toPrecise, trimRows, parseThresholdToMilliseconds,
+                   setDeprecatedThreshold, deprecatedCutoff, filterOutDeprecatedRows };

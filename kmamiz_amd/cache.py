@@ -26,6 +26,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
+from . import settings
 from .ingest import UNDEFINED, js_truthy, tpl
 
 I64_MIN = np.iinfo(np.int64).min
@@ -158,7 +159,7 @@ class ReducedDependencies:
         else:
             out.e_ord = ((entries["row"] << _U(32)) | within).astype(np.int64)
         out.next_ord = int(out.e_ord.max()) + 1 if len(k) else 0
-        return out
+        return out.filtered()  # (every EndpointDependencies built on the way filters, EndpointDependencies.ts:41)
 
     @classmethod
     def from_json(cls, rows: Sequence[dict], merge_rows: bool = False,
@@ -173,6 +174,7 @@ class ReducedDependencies:
         R = out.reg
         order: List[int] = []
         by_ep: Dict[int, list] = {}
+        rows = settings.filter_out_deprecated(list(rows), settings.deprecated_cutoff())  # new EndpointDependencies(rows)
         for r in rows:
             e = R.name_id(r["endpoint"]["uniqueEndpointName"])
             lists = []
@@ -232,9 +234,34 @@ class ReducedDependencies:
         out.e_ts = np.array(ents["ts"], np.float64)
         out.e_ord = np.arange(len(out.e_row), dtype=np.int64)
         out.next_ord = len(out.e_row)
-        return out
+        return out.filtered() if merge_rows else out
 
     # -- the reference's methods --------------------------------------------------
+    def filtered(self, cutoff: Optional[float] = None) -> "ReducedDependencies":
+        """The constructor's deprecation filter (EndpointDependencies.ts:44-74)
+        on the columns: rows with lastUsageTimestamp < cutoff go, and every
+        entry naming one of their endpoints (or belonging to one) with them.
+        ``cutoff`` defaults to settings.deprecated_cutoff() (now - threshold;
+        0: no filter)."""
+        if cutoff is None:
+            cutoff = settings.deprecated_cutoff()
+        if cutoff == 0 or not len(self.row_ep):
+            return self
+        last = np.where(self.row_last_int, 0.0, self.row_last)
+        stale = last < cutoff
+        if not stale.any():
+            return self
+        gone = self.row_ep[stale]
+        out = ReducedDependencies(self.reg)
+        keep = ~stale
+        for f in ("row_ep", "row_info", "row_ts", "row_last", "row_last_int", "row_ext"):
+            setattr(out, f, getattr(self, f)[keep])
+        ek = ~(np.isin(self.e_row, gone) | np.isin(self.e_ep, gone))
+        for f in ("e_row", "e_side", "e_ep", "e_dist", "e_info", "e_ts", "e_ord"):
+            setattr(out, f, getattr(self, f)[ek])
+        out.next_ord = self.next_ord
+        return out
+
     def _ck(self, row, side, ep, dist):
         return (row.astype(_U) << _U(40)) | (ep.astype(_U) << _U(16)) | (dist.astype(_U) << _U(1)) | side.astype(_U)
 
@@ -281,12 +308,13 @@ class ReducedDependencies:
         out.e_ts = np.concatenate([self.e_ts, other.e_ts[fresh]])
         out.e_ord = np.concatenate([self.e_ord, self.next_ord + rank])
         out.next_ord = self.next_ord + len(rank)
-        return out
+        return out.filtered()  # new EndpointDependencies(...) (EndpointDependencies.ts:539-541)
 
     def trim(self) -> "ReducedDependencies":
-        """EndpointDependencies.ts:91-112: the identity here (entries are unique
-        per (row, side, name, distance) by construction)."""
-        return self
+        """EndpointDependencies.ts:91-112: the lists need no dedup here (entries
+        are unique per (row, side, name, distance) by construction); the new
+        object's constructor filters deprecated endpoints."""
+        return self.filtered()
 
     def getData(self, namespace: Optional[str] = None) -> "ReducedDependencies":
         """Cacheable/CEndpointDependencies.ts:51-59: the rows whose endpoint

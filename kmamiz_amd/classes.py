@@ -21,6 +21,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import _lib as L
+from . import settings
 from .engine import Engine
 from .envoy import merge, merge_string_body, object_to_interface_string, parse_request_response_body
 from .ingest import (UNDEFINED, Dictionary, dep_identity, explode_url, ingest_json, ingest_rows, ingest_traces,
@@ -687,14 +688,17 @@ class _DepResult:
 
 class EndpointDependencies:
     def __init__(self, dependencies: Optional[List[dict]] = None, *, _native: Optional[_DepResult] = None):
-        # DEPRECATED_ENDPOINT_THRESHOLD unset: the constructor filter is the
-        # identity (EndpointDependencies.ts:44-54)
-        self._deps = dependencies
+        # the constructor's deprecation filter (EndpointDependencies.ts:40-74):
+        # the identity unless DEPRECATED_ENDPOINT_THRESHOLD is set; the cutoff
+        # is taken now (Date.now() in the constructor) and applied to an
+        # engine result when its rows or reduced form are first built
+        self._cutoff = settings.deprecated_cutoff()
+        self._deps = settings.filter_out_deprecated(dependencies, self._cutoff) if dependencies is not None else None
         self._native = _native
 
     def _list(self) -> List[dict]:
         if self._deps is None:
-            self._deps = self._native.materialize()
+            self._deps = settings.filter_out_deprecated(self._native.materialize(), self._cutoff)
         return self._deps
 
     def toJSON(self):
@@ -705,7 +709,18 @@ class EndpointDependencies:
         (anc_ep<<40|desc_ep<<16|distance<<1|on) + per-endpoint records."""
         if self._native is None:
             raise ValueError("reduced() needs an engine-backed result")
-        return self._native.triples, self._native.endpoints
+        keys, eps = self._native.triples, self._native.endpoints
+        if self._cutoff != 0:  # the constructor's filter on the reduced form (EndpointDependencies.ts:44-74)
+            lt = eps["last_ts"]
+            last = np.where(lt == np.iinfo(np.int64).min, 0.0, np.maximum(0.0, lt / 1000))
+            stale = (eps["has_row"] != 0) & (last < self._cutoff)
+            if stale.any():
+                a = (keys >> np.uint64(40)).astype(np.int64)
+                d = ((keys >> np.uint64(16)) & np.uint64(0xFFFFFF)).astype(np.int64)
+                keys = keys[~(stale[a] | stale[d])]
+                eps = eps.copy()
+                eps["has_row"][stale] = 0
+        return keys, eps
 
     def service_tail(self, labelMap: Optional[Dict[str, str]] = None):
         """Scale form of the service-level tail (tail.ServiceTail) of the
@@ -715,6 +730,9 @@ class EndpointDependencies:
 
         if self._native is None:
             raise ValueError("service_tail() needs an engine-backed result")
+        if self._cutoff != 0:
+            raise NotImplementedError("service_tail() runs on the unfiltered edge set; with "
+                                      "DEPRECATED_ENDPOINT_THRESHOLD set use toReduced() (filtered) and the host tail")
         nat = self._native
         eng = nat.eng
         if eng.gen != nat.gen:  # the engine ran something else since: this batch's dependency pass again
@@ -728,7 +746,7 @@ class EndpointDependencies:
         from .cache import ReducedDependencies
 
         if self._native is not None and self._deps is None:
-            return self._native.reduced_graph(reg)
+            return self._native.reduced_graph(reg).filtered(self._cutoff)
         return ReducedDependencies.from_json(self._list(), merge_rows=True, reg=reg)
 
     def trim(self):

@@ -46,6 +46,7 @@ from __future__ import annotations
 import json
 import math
 import re
+import time
 from typing import Any, Dict, List, Optional
 
 
@@ -667,11 +668,54 @@ class CombinedRealtimeDataList:
 # --------------------------------------------------------------------------
 # EndpointDependencies  (src/classes/EndpointDependencies.ts)
 # --------------------------------------------------------------------------
+def parse_threshold_to_ms(s):
+    r"""EndpointDependencies.parseThresholdToMilliseconds (EndpointDependencies.ts:20-31):
+    /(?:(\d+)d)?(?:(\d+)h)?(?:(\d+)m)?/ with String.match (first match, which
+    may be the empty one at index 0), parseInt base 10, JS number arithmetic."""
+    if not s:
+        return 0
+    m = re.match(r"(?:([0-9]+)d)?(?:([0-9]+)h)?(?:([0-9]+)m)?", s)
+    if m is None:
+        return 0
+    days = float(int(m.group(1))) if m.group(1) else 0.0
+    hours = float(int(m.group(2))) if m.group(2) else 0.0
+    minutes = float(int(m.group(3))) if m.group(3) else 0.0
+    return ((days * 86400) + (hours * 3600) + (minutes * 60)) * 1000
+
+
+# GlobalSettings.DeprecatedEndpointThreshold (GlobalSettings.ts:79), parsed
+# into the class's static (EndpointDependencies.ts:33-36), and Date.now():
+# unset / the wall clock unless a test pins them
+DEPRECATED_THRESHOLD_MS = 0
+DATE_NOW = None
+
+
+def _date_now():
+    return DATE_NOW() if DATE_NOW is not None else int(time.time() * 1000)
+
+
 class EndpointDependencies:
     def __init__(self, deps: List[dict]):
-        # deprecation filter is a no-op with DEPRECATED_ENDPOINT_THRESHOLD unset
-        # (EndpointDependencies.ts:44-54, GlobalSettings.ts:78-79)
-        self._deps = deps
+        self._deps = self._filter_out_deprecated(deps)
+
+    @staticmethod
+    def _filter_out_deprecated(deps):
+        """EndpointDependencies.ts:44-74 (mutates the kept rows' lists)."""
+        now = _date_now()
+        cut = 0 if DEPRECATED_THRESHOLD_MS == 0 else now - DEPRECATED_THRESHOLD_MS
+        if cut == 0:
+            return deps
+        names = set()
+        kept = []
+        for dep in deps:
+            if dep["lastUsageTimestamp"] < cut:
+                names.add(dep["endpoint"]["uniqueEndpointName"])
+            else:
+                kept.append(dep)
+        for dep in kept:
+            dep["dependingBy"] = [x for x in dep["dependingBy"] if x["endpoint"]["uniqueEndpointName"] not in names]
+            dep["dependingOn"] = [x for x in dep["dependingOn"] if x["endpoint"]["uniqueEndpointName"] not in names]
+        return kept
 
     def toJSON(self):
         return self._deps
