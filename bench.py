@@ -227,7 +227,9 @@ def main():
     def step():
         # N > 1: the repeated-span-id guard routes this batch's ids and posts
         # its all-to-all before the run, so the exchange overlaps the kernels
+        tg = time.perf_counter()
         guard = kdist.IdGuard(eng, dev).start() if world > 1 else None
+        state["guard_start_s"] = state.get("guard_start_s", 0.0) + (time.perf_counter() - tg)
         eng.run(flags)
         if world > 1:
             gw = eng.partials_words(L.PART_GROUPS)
@@ -266,6 +268,7 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
+    state["guard_start_s"] = 0.0
     t0 = time.perf_counter()
     marks = []
     for _ in range(args.steps):
@@ -303,7 +306,11 @@ def main():
     dom = max((k for k in per_kernel if per_kernel[k]["alg_bytes"]), key=lambda k: per_kernel[k]["avg_ms"])
     d = per_kernel[dom]
     kern_ms = sum(v["ms_per_step"] for v in per_kernel.values())
-    pipe_bytes = sum(v["alg_bytes"] for v in per_kernel.values() if v["alg_bytes"])
+    # the step's SURVEY.md 8d bytes: K2 57 + K3 19 per span, K4 12 per relation
+    # (K1 is not in the step: the batch is generated on the device); the
+    # certificate's and the reduce's extra passes are overhead, not 8d work
+    pipe_bytes = (57 + 19) * n_local + 12 * A
+    overhead = {k: per_kernel[k]["alg_bytes"] for k in ("cert", "check", "reduce", "tail") if k in per_kernel}
     kname = {"join": "k_join_window", "stats": "k3_produce" if "reduce" in per_kernel else "k_stats",
              "reduce": "k3_reduce", "walk": "k4_chain", "cert": "k_cert_split", "check": "k_cert_check",
              "tail": "k_tail_links", "joinwalk": "k_join_chain"}[dom]
@@ -389,6 +396,10 @@ def main():
                 "sharding_guards": ("in every timed step: id-table/size agreement, unresolved parents, "
                                     "cross-shard repeated span ids (all-to-all of hashed ids, overlapping the run, "
                                     "+ certificate)" if world > 1 else None),
+                # (IdGuard.start: kmz_route_ids + the blocking counts all-to-all,
+                # host time per step before the run is queued)
+                "guard_start_ms_per_step": (round(state["guard_start_s"] / args.steps * 1e3, 4)
+                                            if world > 1 else None),
                 "service_tail": tail_on,
                 "fetched": ("groups + endpoints to the host; the edge keys stay in HBM, where "
                             "kmz_tail_run reads them" if tail_on else
@@ -404,8 +415,13 @@ def main():
                 "traffic": (tr[0] if tr else None),
                 "traffic_source": (f"profiles/{tr[1]} (build {build_id()})" if tr else
                                    f"no PMC pass of build {build_id()} on this workload committed"),
+                "pipeline_bytes": pipe_bytes,
                 "pipeline_gbs": round(pipe_bytes / (kern_ms * 1e-3) / 1e9, 1),
                 "kernel_ms_per_step": round(kern_ms, 4),
+                # the whole step (bench clock) against 8d's bytes: (57 + 19) N + 12 A
+                "step_gbs": round(pipe_bytes / (secs / args.steps) / 1e9, 1),
+                "step_frac": round(pipe_bytes / (secs / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                "overhead_bytes": overhead,
                 "kernels": per_kernel,
                 "units": units,
             },

@@ -63,6 +63,7 @@ struct kmz_ctx {
   DevBuf mkeys_in, mtab;                                 // kmz_merge_triples staging / fallback set
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
   DevBuf rt_hist, rt_tot, rt_out, rt_ctr;  // cross-shard repeated-id guard: routing scratch, certificate counters
+  DevBuf rt_pool1, rt_dir, rt_pool2, rt_cur;  // ... and its own certificate buffers (the run's stay as the run left them)
   // device JSON ingest (kmz_json.hip)
   DevBuf j_buf, j_elem, j_state, j_jsc, j_mask, j_cnt, j_off, j_csc, j_small, j_starts, j_slices, j_tslot, j_stab,
       j_ttab, j_reps, j_smap, j_tmap;
@@ -341,7 +342,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
                     &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
@@ -903,8 +904,9 @@ static bool fused_eligible(kmz_ctx *c) {
 
 static int run_fused(kmz_ctx *c, bool links) {
   const uint32_t n = (uint32_t)c->n;
-  CertPlan pl;
-  cert_plan(n, &pl);
+  CertPlan pl;  // (the plan fused_eligible accepted: same arguments)
+  if (!cert_plan(n, &pl, true, (c->ablate2 & 64u) != 0) || pl.B1 != 6)
+    return fail(c, KMZ_E_STATE, "fused join + walk: certificate plan is not the kernel's 2^6 pass-1 binning");
   const size_t nsub = (size_t)1 << (pl.B1 + pl.B2);
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
@@ -2156,8 +2158,11 @@ int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32
     return fail(c, KMZ_E_UNSUPPORTED, "too many values for the certificate: check on the host");
   const uint32_t m = (uint32_t)n;
   const size_t nsub = (size_t)1 << (pl.B1 + pl.B2);
-  if (ensure(c, c->cpool1, cert_pool1_words(m) * 8) || ensure(c, c->cdir, cert_dir_entries(m, pl) * 2) ||
-      ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) || ensure(c, c->rt_ctr, C_COUNT * 4))
+  // (the guard's own certificate buffers: reusing the run's would resize them
+  // between runs, changing the run's addresses -- and its hipGraph key -- every
+  // multi-GPU step)
+  if (ensure(c, c->rt_pool1, cert_pool1_words(m) * 8) || ensure(c, c->rt_dir, cert_dir_entries(m, pl) * 2) ||
+      ensure(c, c->rt_pool2, nsub * pl.cap2 * 8) || ensure(c, c->rt_cur, nsub * 4) || ensure(c, c->rt_ctr, C_COUNT * 4))
     return KMZ_E_HIP;
   const unsigned long long *src = reinterpret_cast<const unsigned long long *>(vals);
   if (mem != KMZ_MEM_DEVICE) {
@@ -2166,13 +2171,13 @@ int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32
     src = P<unsigned long long>(c->rt_out);
   }
   unsigned int *cnt = P<unsigned int>(c->rt_ctr);
-  unsigned int *cur2 = P<unsigned int>(c->ccur);
+  unsigned int *cur2 = P<unsigned int>(c->rt_cur);
   HIPCHK(c, hipMemsetAsync(cnt, 0, C_COUNT * 4, c->stream));
   HIPCHK(c, hipMemsetAsync(cur2, 0, nsub * 4, c->stream));
-  launch_cert_bin(c->stream, src, m, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir));
-  launch_cert_split(c->stream, m, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
-                    P<unsigned long long>(c->cpool2), cur2, cnt);
-  launch_cert_check(c->stream, m, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
+  launch_cert_bin(c->stream, src, m, P<unsigned long long>(c->rt_pool1), P<uint16_t>(c->rt_dir));
+  launch_cert_split(c->stream, m, P<unsigned long long>(c->rt_pool1), P<uint16_t>(c->rt_dir), pl,
+                    P<unsigned long long>(c->rt_pool2), cur2, cnt);
+  launch_cert_check(c->stream, m, pl, P<unsigned long long>(c->rt_pool2), cur2, cnt);
   HIPCHK(c, hipGetLastError());
   unsigned int h[C_COUNT];
   HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));

@@ -94,11 +94,22 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
     # agreement first: every later collective's size depends on G and E
     # (ranks that disagree would hang RCCL or fail inside gloo before a clear
     # error); the sharding guard's count rides along
-    nu = _unresolved(engine) if engine is not None else 0
+    # (a shard on the span-table path is refused on every rank, not just on
+    # its own: a local raise would leave the others blocked in this all-reduce)
+    refused = None
+    try:
+        nu = _unresolved(engine) if engine is not None else 0
+    except ShardingError as err:
+        nu, refused = 0, err
     dg = int(digest) & ((1 << 62) - 1)
-    agree = torch.tensor([G, -G, E, -E, dg, -dg, nu, 0], dtype=torch.int64, device=dev)
+    agree = torch.tensor([G, -G, E, -E, dg, -dg, nu, 1 if refused else 0], dtype=torch.int64, device=dev)
     dist.all_reduce(agree, op=dist.ReduceOp.MAX, group=group)
     a = agree.tolist()
+    if a[7]:
+        if isinstance(check_ids, IdGuard):
+            check_ids.abandon()  # its exchange was posted before the run: drain it on every rank
+        raise refused or ShardingError("another rank's shard has repeated span ids: sharding is not exact, "
+                                       "run unsharded")
     if a[0] != -a[1] or a[2] != -a[3] or a[4] != -a[5]:
         raise ShardingError("ranks merged partials over different endpoint/status id tables "
                             "(assign global ids with shard.exchange_tables)")
@@ -198,6 +209,13 @@ class IdGuard:
         self.work = dist.all_to_all_single(self.recv[: self.m], send, output_split_sizes=rc, input_split_sizes=counts,
                                            group=self.group, async_op=True)
         return self
+
+    def abandon(self) -> None:
+        """Wait for a posted exchange without checking it (every rank calls
+        this when the merge is refused before the guard's verdict)."""
+        if self.work is not None:
+            self.work.wait()
+        self.work = self.send = self.recv = None
 
     def finish(self) -> None:
         if self.world == 1:

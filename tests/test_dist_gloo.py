@@ -158,6 +158,22 @@ def _guard_worker(rank, world, port, q, case):
                 q.put((rank, "passed"))
             except kdist.ShardingError:
                 q.put((rank, "refused"))
+        elif case == "internal":  # rank 0's shard repeats an id inside itself (the span-table path)
+            class _Eng:
+                def unresolved_parents(self):
+                    from kmamiz_amd._lib import KmzError
+
+                    if rank == 0:
+                        raise KmzError(-9, "span-table path")
+                    return 0
+
+            p = torch.zeros(6 * 3, dtype=torch.int64)
+            try:
+                kdist.merge_all(p, 3, torch.zeros(4, dtype=torch.int64), 2, torch.ones(2, dtype=torch.int64),
+                                engine=_Eng(), check_ids=False)
+                q.put((rank, "merged"))
+            except kdist.ShardingError:
+                q.put((rank, "refused"))
         else:  # "sizes": rank 1 holds one group more -- refused before any size-dependent collective
             G = 3 + (rank == 1)
             p = torch.zeros(6 * G, dtype=torch.int64)
@@ -198,6 +214,14 @@ def test_span_id_repeated_across_shards_is_refused(world):
 
 def test_ranks_with_different_sizes_are_refused():
     assert _run_guard(2, "sizes") == ["refused"] * 2
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_one_rank_on_the_span_table_path_refuses_every_rank(world):
+    """a shard with an id repeated inside it is refused on every
+    rank through the agreement all-reduce, so no rank waits in a collective
+    the refusing rank never joins."""
+    assert _run_guard(world, "internal") == ["refused"] * world
 
 
 def test_route_ids_np_partitions_by_owner():
