@@ -2,9 +2,9 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result
-SRC = kmamiz_amd/csrc/kmz_kernels.hip kmamiz_amd/csrc/kmz_part.hip kmamiz_amd/csrc/kmz_join.hip kmamiz_amd/csrc/kmz_chain.hip kmamiz_amd/csrc/kmz_api.hip kmamiz_amd/csrc/kmz_tail.hip kmamiz_amd/csrc/kmz_guard.hip kmamiz_amd/csrc/kmz_shard.hip kmamiz_amd/csrc/kmz_order.hip kmamiz_amd/csrc/kmz_json.hip kmamiz_amd/csrc/kmz_fuse.hip
-HDR = include/kmz.h kmamiz_amd/csrc/kmz_common.h kmamiz_amd/csrc/kmz_joinw.h kmamiz_amd/csrc/kmz_chainw.h kmamiz_amd/csrc/kmz_synth.h kmamiz_amd/csrc/kmz_kernels.h
-OBJ = build/kmz_kernels.o build/kmz_part.o build/kmz_join.o build/kmz_chain.o build/kmz_api.o build/kmz_ingest.o build/kmz_tail.o build/kmz_guard.o build/kmz_shard.o build/kmz_order.o build/kmz_json.o build/kmz_fuse.o
+SRC = kmamiz_amd/csrc/kmz_kernels.hip kmamiz_amd/csrc/kmz_part.hip kmamiz_amd/csrc/kmz_join.hip kmamiz_amd/csrc/kmz_chain.hip kmamiz_amd/csrc/kmz_api.hip kmamiz_amd/csrc/kmz_tail.hip kmamiz_amd/csrc/kmz_guard.hip kmamiz_amd/csrc/kmz_shard.hip kmamiz_amd/csrc/kmz_order.hip kmamiz_amd/csrc/kmz_json.hip kmamiz_amd/csrc/kmz_fuse.hip kmamiz_amd/csrc/kmz_walk.hip
+HDR = include/kmz.h kmamiz_amd/csrc/kmz_common.h kmamiz_amd/csrc/kmz_joinw.h kmamiz_amd/csrc/kmz_chainw.h kmamiz_amd/csrc/kmz_walkw.h kmamiz_amd/csrc/kmz_synth.h kmamiz_amd/csrc/kmz_kernels.h
+OBJ = build/kmz_kernels.o build/kmz_part.o build/kmz_join.o build/kmz_chain.o build/kmz_api.o build/kmz_ingest.o build/kmz_tail.o build/kmz_guard.o build/kmz_shard.o build/kmz_order.o build/kmz_json.o build/kmz_fuse.o build/kmz_walk.o
 
 all: kmamiz_amd/libkmz.so oracle addon
 

@@ -136,7 +136,9 @@ typedef struct kmz_info {
                            bit 1 chain walk k4_chain (else per-relation global walk k_walk),
                            bit 2 direct enumeration (else chain interning),
                            bit 3 k_walk redo after a chain-table wait ran out (F_SPIN),
-                           bit 4 join and chain walk fused in one kernel (k_join_chain) */
+                           bit 4 join and chain walk fused in one kernel (k_join_chain),
+                           bit 5 chain interning by one workgroup per tile (k4_tile; else
+                           the persistent k4_chain) */
   uint64_t n_chains;    /* distinct interned ancestor chains (chain-interning path) */
 } kmz_info;
 
@@ -300,6 +302,10 @@ int kmz_partials_copy(kmz_ctx *ctx, int which, void *buf, uint64_t words, int me
  * per `mem`) into this context's edge set after a KMZ_RUN_DEPS run;
  * kmz_get_triples / kmz_fetch / KMZ_PART_TRIPLES then return the union. */
 int kmz_merge_triples(kmz_ctx *ctx, const uint64_t *keys, uint64_t n, int mem);
+/* The same with the given keys REPLACING this context's edge set: the merge of
+ * traceId shards whose span-id map crosses shards, where one rank re-ran the
+ * dependency pass over the whole batch (dist.merge_all's exact fallback). */
+int kmz_set_triples(kmz_ctx *ctx, const uint64_t *keys, uint64_t n, int mem);
 /* re-finalise the groups after the partials were reduced in place */
 int kmz_finalize(kmz_ctx *ctx);
 /* host-side finalisation of one partial (same arithmetic as the device) */
@@ -344,6 +350,9 @@ uint32_t kmz_trace_shard(const char *trace_id, uint64_t len, uint32_t world);
  * span links) is then global; index_base is ignored.  n_runs = 0: contiguous
  * again.  kmz_load resets it. */
 int kmz_set_index_map(kmz_ctx *ctx, const uint64_t *local_start, const uint64_t *global_start, uint64_t n_runs);
+/* the global flatten index of every loaded span (index_base + i, or through
+ * the index map; n_spans values, host or device memory per `mem`) */
+int kmz_get_global_index(kmz_ctx *ctx, uint64_t *out, uint64_t cap, int mem);
 
 /* ---- service-level tail over the reduced edge set ---- */
 /* Replaces the per-row scans of EndpointDependencies.toServiceDependencies

@@ -172,6 +172,7 @@ SIGNATURES = [
     ("kmz_partials_size", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
     ("kmz_partials_copy", C.c_int, [_P, C.c_int, _P, C.c_uint64, C.c_int, C.c_int]),
     ("kmz_merge_triples", C.c_int, [_P, _P, C.c_uint64, C.c_int]),
+    ("kmz_set_triples", C.c_int, [_P, _P, C.c_uint64, C.c_int]),
     ("kmz_parse_zipkin", C.c_int, [C.c_char_p, C.c_uint64, C.c_int, C.POINTER(C.POINTER(ZipkinBatch))]),
     ("kmz_zipkin_free", None, [C.POINTER(ZipkinBatch)]),
     ("kmz_unresolved_parents", C.c_int, [_P, _P, C.c_uint64, C.POINTER(C.c_uint64), C.c_int]),
@@ -181,6 +182,7 @@ SIGNATURES = [
     ("kmz_id_repeats", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.POINTER(C.c_uint32)]),
     ("kmz_trace_shard", C.c_uint32, [C.c_char_p, C.c_uint64, C.c_uint32]),
     ("kmz_set_index_map", C.c_int, [_P, _P, _P, C.c_uint64]),
+    ("kmz_get_global_index", C.c_int, [_P, _P, C.c_uint64, C.c_int]),
     ("kmz_tail_map_set", C.c_int, [_P, C.POINTER(TailMap)]),
     ("kmz_tail_run", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("kmz_tail_get", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, _P, C.c_uint64]),

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "kmz_kernels.h"
+#include "kmz_walkw.h"
 
 using namespace kmz;
 
@@ -139,7 +140,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -795,8 +796,10 @@ static int run_shape_stats(kmz_ctx *c) {
   const uint32_t n = (uint32_t)c->n;
   const uint64_t Gs = (uint64_t)c->n_shapes * c->n_status;
   if (Gs >= 0xFFFFFFFFull) return fail(c, KMZ_E_ARG, "too many (shape x status) groups");
-  if (ensure(c, c->sgrp, (Gs + 1) * 48)) return KMZ_E_HIP;
+  // (the shape-level group partials, then the partitioned K3's escape block E)
+  if (ensure(c, c->sgrp, (Gs + 1) * 48 * 2)) return KMZ_E_HIP;
   unsigned long long *sg = P<unsigned long long>(c->sgrp);
+  unsigned long long *E = sg + 6 * Gs;
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned long long *nsrv = P<unsigned long long>(c->stats64) + S_SERVER;
   const bool part = Gs > 1024 && k3_partitions((uint32_t)Gs) <= k3_pmax() && !(c->ablate & 8);
@@ -805,6 +808,10 @@ static int run_shape_stats(kmz_ctx *c) {
     FillArgs f;
     f.add(sg, Gs * 40, 0);
     f.add(sg + 5 * Gs, Gs * 8, 0xFF);
+    if (part) {
+      f.add(E, Gs * 40, 0);
+      f.add(E + 5 * Gs, Gs * 8, 0xFF);
+    }
     launch_fill(c->stream, f);
   }
   if (part) {
@@ -842,6 +849,8 @@ static int run_shape_stats(kmz_ctx *c) {
       else
         launch_k3_reduce(c->stream, n, (uint32_t)Gs, c->index_base, c->k3pool.p, P<uint32_t>(c->k3dir),
                          P<unsigned long long>(c->k3part), S, sg);
+      launch_k3_escapes(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_status,
+                        c->index_base, c->k3pool.p, cnt, E, (uint32_t)Gs, sg);
     }
   } else if (Gs <= 1024 && !(c->ablate & 8)) {
     const uint32_t nb = k3_small_blocks(n);
@@ -988,7 +997,7 @@ static int run_fused(kmz_ctx *c, bool links) {
   }
   {
     Timed t(c, KMZ_K_SETTLE);
-    launch_chain_settle_list(c->stream, n, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
+    launch_chain_settle_list(c->stream, join_tiles(n), c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
                              P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), (uint32_t)stot,
                              P<unsigned long long>(c->kdefer), (uint32_t)dtot, gpos, (uint32_t)gtot, c->ablate);
   }
@@ -1010,6 +1019,97 @@ static int run_fused(kmz_ctx *c, bool links) {
   }
   c->ctab_dirty = false;  // (set again after the run if the list overflowed: F_CTAB_DIRTY)
   c->path = 1 | 2 | 16;
+  c->chain_ran = true;
+  c->k4_direct_ran = false;
+  c->k4_lb1 = 0;
+  c->k4_ng = ng;
+  return KMZ_OK;
+}
+
+// K4 by chain interning with one workgroup per tile (k4_tile, kmz_walk.hip):
+// the same global lists, settle, pending pass and slot clearing as the fused
+// kernel's tail (run_fused), after the window join (run_join / run_table).
+static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
+  const uint32_t n = (uint32_t)c->n;
+  unsigned int *cnt = P<unsigned int>(c->counters);
+  unsigned long long *st = P<unsigned long long>(c->stats64);
+  unsigned long long *epp = P<unsigned long long>(c->epp);
+  // the global lists (as run_fused): staged keys of new chains, deferred checks
+  // (KMZ_ABLATE bit 10, test knob: 4), claimed slots
+  while (!(c->ablate & (1u << 30)) && (uint64_t)c->scap * chain_grid(n) < 8ull * n &&
+         (uint64_t)chain_grid(n) * c->scap * 2 * 8 <= stage_limit(n))
+    c->scap *= 2;
+  const uint32_t nt = walk_tiles(n), ng = chain_grid(n), wcap = 1u << 16;
+  const uint64_t stot = std::min<uint64_t>((uint64_t)ng * c->scap, 1ull << 28),
+                 dtot = (c->ablate & (1u << 10)) ? 4u : (uint64_t)ng << 12, gtot = ((uint64_t)ng + 1) * wcap;
+  if (stot >= (1ull << 32) || dtot >= (1ull << 32) || gtot >= (1ull << 32))
+    return fail(c, KMZ_E_ARG, "chain walk: list sizes past 2^32");
+  void *old_ctab = c->ctab.p;
+  if (ensure(c, c->ctab, c->ccap * CHAIN_ENTRY_BYTES) || ensure(c, c->ctile, (size_t)nt * 16) ||
+      ensure(c, c->plist, (size_t)(n + 1) * 4) || ensure(c, c->kstage, stot * 8) || ensure(c, c->kdefer, dtot * 16) ||
+      ensure(c, c->kwpos, gtot * 4) || ensure(c, c->cetab, ((size_t)c->n_shapes + 1) * 16))
+    return KMZ_E_HIP;
+  if (c->ctab.p != old_ctab) c->ctab_dirty = true;
+  uint32_t *gpos = P<uint32_t>(c->kwpos);
+  {
+    Timed t(c, KMZ_K_MEMSET);
+    FillArgs f;
+    if (c->ctab_dirty) f.add(c->ctab.p, c->ccap * CHAIN_ENTRY_BYTES, 0);
+    f.add(c->trip.p, c->tcap * 8, 0);
+    launch_fill(c->stream, f);
+  }
+  c->ctab_dirty = true;  // until this run's slots are cleared below
+  {
+    ChainRun a;
+    a.ts = c->ts;
+    a.ctab = P<unsigned long long>(c->ctab);
+    a.ccap = c->ccap;
+    a.trip = P<unsigned long long>(c->trip);
+    a.tcap = c->tcap;
+    a.ep_ts = epp;
+    a.rowpos_out = links ? P<unsigned long long>(c->rowpos) : nullptr;
+    a.plist = P<uint32_t>(c->plist);
+    a.pcap = n + 1;
+    a.counters = cnt;
+    a.stage = P<unsigned long long>(c->kstage);
+    a.scap = (uint32_t)stot;
+    a.defer = P<unsigned long long>(c->kdefer);
+    a.dcap = (uint32_t)dtot;
+    a.gpos = gpos;
+    a.gcap = (uint32_t)gtot;
+    a.n_ep = c->n_dep;
+    a.index_base = c->index_base;
+    a.seed = c->sig_seed;
+    // (test knob 24 forces sig collisions on the first seed only)
+    a.ablate = c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24));
+    Timed t(c, KMZ_K_WALK);
+    launch_chain_tile(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep), c->n_shapes,
+                      P<uint4>(c->cetab), P<uint32_t>(c->ctile), a);
+  }
+  {
+    Timed t(c, KMZ_K_SETTLE);
+    launch_chain_settle_list(c->stream, nt, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
+                             P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), (uint32_t)stot,
+                             P<unsigned long long>(c->kdefer), (uint32_t)dtot, gpos, (uint32_t)gtot, c->ablate);
+  }
+  {
+    Timed t(c, KMZ_K_PEND);
+    launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n,
+                      P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
+                      P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, (uint32_t)gtot, false, c->ablate);
+  }
+  if (c->overlap) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_k3, 0));  // the shape-level K3 partials
+  {
+    Timed t(c, KMZ_K_FINAL);
+    launch_compact(c->stream, P<unsigned long long>(c->trip), c->tcap, P<unsigned long long>(c->trip_out),
+                   st + S_TRIP_OUT);
+    launch_collapse_endpoints(c->stream, P<unsigned long long>(c->sgrp), c->n_shapes, c->n_status,
+                              P<uint32_t>(c->d_dep), c->n_dep, P<uint32_t>(c->cparent), c->index_base, epp,
+                              epp + c->n_dep, cnt);
+    launch_chain_clear_list(c->stream, c->ctab.p, gpos, (uint32_t)gtot, cnt);
+  }
+  c->ctab_dirty = false;  // (set again after the run if the list overflowed: F_CTAB_DIRTY)
+  c->path = (joined ? 1 : 0) | 2 | 32;
   c->chain_ran = true;
   c->k4_direct_ran = false;
   c->k4_lb1 = 0;
@@ -1051,6 +1151,11 @@ static int run_deps(kmz_ctx *c, bool links) {
     dups = hc[C_DUPS];
   }
   if (ensure(c, c->trip, c->tcap * 8) || ensure(c, c->trip_out, c->tcap * 8)) return KMZ_E_HIP;
+  if (dups == 0 && !(c->ablate & 16) && !c->walk_once && !c->k4_now && !(c->ablate2 & 256u)) {
+    // unique span ids, chain interning: one workgroup per tile (kmz_walk.hip)
+    if (!c->sstats && (r = run_shape_stats(c))) return r;
+    return run_chain_tiles(c, links, joined);
+  }
   if (dups == 0 && !(c->ablate & 16) && !c->walk_once) {
     // unique span ids: rows are the SERVER spans; chain interning (kmz_chain.hip)
     if (!c->sstats && (r = run_shape_stats(c))) return r;
@@ -1781,12 +1886,17 @@ int kmz_partials_copy(kmz_ctx *c, int which, void *buf, uint64_t words, int mem,
   return KMZ_OK;
 }
 
-int kmz_merge_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, int mem) {
+// replace: the keys become the edge set (kmz_set_triples), else they join it
+static int merge_or_set_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, int mem, bool replace) {
   if (!c || (n && !keys)) return KMZ_E_ARG;
   if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
   uint64_t nl = 0;
   int r = kmz_partials_size(c, KMZ_PART_TRIPLES, &nl);
   if (r) return r;
+  if (replace) {
+    HIPCHK(c, hipMemsetAsync(c->trip.p, 0, c->tcap * 8, c->stream));
+    nl = 0;
+  }
   const unsigned long long *src = reinterpret_cast<const unsigned long long *>(keys);
   if (n && mem == KMZ_MEM_HOST) {
     if (ensure(c, c->mkeys_in, n * 8)) return KMZ_E_HIP;
@@ -1832,6 +1942,32 @@ int kmz_merge_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, int mem) {
   if (c->hpin_valid)
     reinterpret_cast<unsigned long long *>(reinterpret_cast<unsigned int *>(c->hpin) + C_COUNT)[S_TRIP_OUT] = nt;
   return KMZ_OK;
+}
+
+int kmz_get_global_index(kmz_ctx *c, uint64_t *out, uint64_t cap, int mem) {
+  if (!c || (c->n && !out)) return KMZ_E_ARG;
+  if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_get_global_index before kmz_load");
+  if (cap < c->n) return fail(c, KMZ_E_ARG, "output too small");
+  unsigned long long *dst = reinterpret_cast<unsigned long long *>(out);
+  if (mem != KMZ_MEM_DEVICE) {
+    if (ensure(c, c->rt_out, (size_t)c->n * 8 + 8)) return KMZ_E_HIP;
+    dst = P<unsigned long long>(c->rt_out);
+  }
+  launch_iota(c->stream, dst, c->n, c->imap_n ? 0 : c->index_base);
+  if (c->imap_n)
+    launch_remap_index(c->stream, dst, c->n, 1, 0, P<uint64_t>(c->imap_l), P<uint64_t>(c->imap_g), c->imap_n);
+  HIPCHK(c, hipGetLastError());
+  if (mem != KMZ_MEM_DEVICE && c->n) HIPCHK(c, hipMemcpyAsync(out, dst, (size_t)c->n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_merge_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, int mem) {
+  return merge_or_set_triples(c, keys, n, mem, false);
+}
+
+int kmz_set_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, int mem) {
+  return merge_or_set_triples(c, keys, n, mem, true);
 }
 
 static uint64_t pow2_at_least(uint64_t x) {

@@ -32,8 +32,8 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "kmz_chainw.h"
 #include "kmz_joinw.h"
+#include "kmz_walkw.h"
 
 namespace kmz {
 
@@ -73,25 +73,22 @@ __global__ void __launch_bounds__(JTT, 4) k_join_chain(
   __shared__ uint32_t wcnt[CERT_BINS * NW], wsum[NW];
   __shared__ uint16_t stash[JSTASH];
   __shared__ uint32_t nstash, wcount;
-  __shared__ unsigned long long imap_sig[IMAP], imap_psig[IMAP];
+  __shared__ ChainLds L;  // the walk's leader map and list reservations
   __shared__ uint16_t wlist[JT];
   __shared__ uint32_t red[NW][4];
-  __shared__ uint32_t l_need[3], l_base[3];  // a round's reservations in the global lists (stage, claimed, deferred)
   const bool dbg_t = (ablate & (1u << 22)) != 0;
-  unsigned long long tprev = 0, tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = 0, tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // (stamps 0-6)
   KMZ_FSTAMP(0);
   const uint32_t t0 = blockIdx.x * JT, t1 = min(n, t0 + JT);
   const uint32_t w0 = t0 > JH ? t0 - JH : 0, w1 = min(n, t1 + JH);
   const uint32_t toff = t0 - w0;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t spin = spin_bound(ablate);
   uint32_t flags = 0;
   for (uint32_t k = threadIdx.x; k < JB; k += JTT) {
     lbkt[k] = make_uint4(0, 0, 0, 0);
     lcnt[k] = 0;
   }
-  for (uint32_t x = threadIdx.x; x < IMAP; x += JTT) imap_sig[x] = 0;
-  if (threadIdx.x < 3) l_need[threadIdx.x] = 0;
+  chain_lds_init(L);
   if (threadIdx.x == 0) nstash = wcount = 0;
   // ---- 1. the join --------------------------------------------------------
   uint64_t s[FPW], p[FPW];
@@ -377,258 +374,34 @@ __global__ void __launch_bounds__(JTT, 4) k_join_chain(
   }
   const bool any_other = __syncthreads_or(other);
   KMZ_FSTAMP(5);
-  const uint32_t m = wcount;
   uint32_t rows = 0, rel = 0, maxd = 0, fresh_n = 0;
-  const bool hash_on = !(ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
-  for (uint32_t r0 = 0; r0 < m; r0 += FTW * JTT) {
-    uint64_t sg[FTW], ps[FTW], acc[FTW];
-    uint32_t dd[FTW], wa[FTW], myep[FTW], jq[FTW];
-    uint8_t st[FTW], kq[FTW];
-#pragma unroll
-    for (int q = 0; q < FTW; ++q) {
-      const uint32_t idx = r0 + q * JTT + threadIdx.x;
-      const bool on = idx < m;
-      const uint32_t jl = on ? toff + wlist[idx] : JW - 1;
-      jq[q] = jl;
-      const uint4 r = lrec[jl];
-      kq[q] = (r.w >> 16) & 3;
-      myep[q] = r.z;
-      sg[q] = (uint64_t)r.y << 32 | r.x;
-      acc[q] = 0;
-      dd[q] = 0;
-      wa[q] = W_NONE;
-      st[q] = S_NONE;
-      if (!on) {
-        kq[q] = KIND_CLIENT;
-        continue;
-      }
-      st[q] = S_DONE;
-      if (!hash_on) continue;
-      if (kq[q] == KIND_SERVER && r.z >= n_ep) flags |= F_RANGE;
-      wa[q] = r.w & 0xFFFF;
-    }
-    // the FTW walks of a thread step together (k4_chain: the depth is the
-    // step count, the loop runs while any lane of the wave walks)
-    auto walk = [&](auto other_tag) {
-      constexpr bool OTHER = decltype(other_tag)::value;
-      for (uint32_t it = 0; it < WIN_DEPTH; ++it) {
-        bool go = false;
-#pragma unroll
-        for (int q = 0; q < FTW; ++q) go |= wa[q] < JW;
-        if (__ballot(go) == 0) break;
-        uint4 r[FTW];
-#pragma unroll
-        for (int q = 0; q < FTW; ++q) r[q] = lrec[wa[q] < JW ? wa[q] : 0];
-#pragma unroll
-        for (int q = 0; q < FTW; ++q) {
-          const bool act = wa[q] < JW;
-          const uint64_t nacc = sig_step(acc[q], (uint64_t)r[q].y << 32 | r[q].x);
-          if (OTHER && act && kq[q] == KIND_SERVER && ((r[q].w >> 16) & 3) != KIND_SERVER) {
-            if (r[q].z < n_ep)
-              atomicMax(&ep_ts[r[q].z], (unsigned long long)((uint64_t)ts[w0 + wa[q]] ^ TS_BIAS));
-            else
-              flags |= F_RANGE;
-          }
-          acc[q] = act ? nacc : acc[q];
-          dd[q] = act ? it + 1 : dd[q];
-          wa[q] = act ? (r[q].w & 0xFFFF) : wa[q];
-        }
-      }
-    };
-    if (any_other)
-      walk(std::true_type{});
-    else
-      walk(std::false_type{});
-#pragma unroll
-    for (int q = 0; q < FTW; ++q) {
-      if (st[q] != S_DONE || !hash_on) {
-        sg[q] = 0;
-        continue;
-      }
-      if (wa[q] != W_NONE) {  // W_OUT: leaves the window (or deeper than WIN_DEPTH); W_CYC: CLIENT loop
-        if (wa[q] == W_CYC) flags |= F_CYCLE;
-        st[q] = S_PEND;
-        sg[q] = 0;
-        continue;
-      }
-      const uint32_t d = dd[q];
-      ps[q] = d ? sig_final(acc[q], d - 1, seed, &flags) : ROOT_SIG;
-      sg[q] = sig_final(rotl64(sg[q], SIG_R * d) ^ acc[q], d, seed, &flags);
-      if (ablate & (1u << 24)) {  // test knob: 4-bit sigs, i.e. collisions (F_SIG, then a retry with another seed)
-        sg[q] = (sg[q] & 0xF) + 2;
-        ps[q] = d ? (ps[q] & 0xF) + 2 : ROOT_SIG;
-      }
-      if (!(ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
-    }
-    ulonglong2 w01[FTW];  // (sig, parent sig) of the probed slot
-    uint64_t pos[FTW];
-#pragma unroll
-    for (int q = 0; q < FTW; ++q) {
-      const bool pr = st[q] == S_PUT;
-      pos[q] = pr ? cslot(sg[q], ccap) : 0;
-      w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(ctab + 2 * pos[q]) : make_ulonglong2(0, 0);
-    }
-    KMZ_FSTAMP(6);
-    // check what the probes found; one leader per distinct unknown sig
-    uint32_t hslot[FTW];
-#pragma unroll
-    for (int q = 0; q < FTW; ++q) {
-      hslot[q] = IMAP + 1;  // not an insert
-      if (st[q] != S_PUT) continue;
-      for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
-        pos[q] = pos[q] + 1 == ccap ? 0 : pos[q] + 1;
-        w01[q] = *reinterpret_cast<const ulonglong2 *>(ctab + 2 * pos[q]);
-      }
-      st[q] = S_DONE;
-      if (w01[q].x == sg[q] && w01[q].y != 0) {
-        if (w01[q].y != ps[q]) flags |= F_SIG;
-        continue;
-      }
-      uint32_t h = (uint32_t)(sg[q] >> 32) & (IMAP - 1);
-      hslot[q] = IMAP;  // a leader without a map slot (map full)
-      for (uint32_t t = 0; t < 8; ++t) {
-        const unsigned long long kk = atomicCAS(&imap_sig[h], 0ull, (unsigned long long)sg[q]);
-        if (kk == 0) {
-          imap_psig[h] = ps[q];
-          hslot[q] = h;
-          break;
-        }
-        if (kk == sg[q]) {
-          hslot[q] = h | 0x80000000u;
-          break;
-        }
-        h = (h + 1) & (IMAP - 1);
-      }
-    }
-    if (ablate & (1u << 18))  // diagnostic knob: probe but no inserts
-#pragma unroll
-      for (int q = 0; q < FTW; ++q) hslot[q] = IMAP + 1;
-    __syncthreads();
-    KMZ_FSTAMP(7);
-    // followers compare with their leader; leaders claim the probed slot (one
-    // CAS) and publish first (as k4_chain<false>).  Their list entries (the
-    // row's staged keys, the claimed slot or a deferred check) are reserved
-    // in LDS, then in the global lists with one atomic per list and workgroup
-    // (same-address device atomics per leader serialised the kernel)
-    unsigned long long cvq[FTW];
-    uint32_t os[FTW], ol[FTW];
-    bool lead[FTW];
-#pragma unroll
-    for (int q = 0; q < FTW; ++q) {
-      lead[q] = false;
-      os[q] = ol[q] = 0;
-      cvq[q] = 0;
-      if (hslot[q] > IMAP) {
-        if (hslot[q] != IMAP + 1) {
-          const uint32_t h = hslot[q] & (IMAP - 1);
-          if (imap_psig[h] != ps[q]) flags |= F_SIG;
-        }
-        continue;
-      }
-      lead[q] = true;
-      unsigned long long *en = ctab + 2 * pos[q];
-      cvq[q] = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
-      if (cvq[q] == 0) atomicExch(&en[1], (unsigned long long)ps[q]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    bool anyl = false;
-#pragma unroll
-    for (int q = 0; q < FTW; ++q) {
-      if (!lead[q]) continue;
-      anyl = true;
-      if (kq[q] == KIND_SERVER && dd[q] && cvq[q] != sg[q] && !(ablate & (1u << 19))) os[q] = atomicAdd(&l_need[0], dd[q]) + 1;
-      ol[q] = atomicAdd(&l_need[cvq[q] == 0 ? 1 : 2], 1u);
-    }
-    if (__syncthreads_or(anyl)) {
-      if (threadIdx.x < 3) {
-        const uint32_t need = l_need[threadIdx.x];
-        l_base[threadIdx.x] = need ? atomicAdd(&counters[threadIdx.x == 0 ? C_FSTAGE : (threadIdx.x == 1 ? C_WPOS : C_FDEFER)], need) : 0;
-        l_need[threadIdx.x] = 0;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < FTW; ++q) {
-        if (!lead[q]) continue;
-        const uint32_t d = dd[q];
-        if (os[q]) {  // the row's keys (ancestor k, row endpoint, k, ancestor is SERVER)
-          const uint64_t base = (uint64_t)l_base[0] + os[q] - 1;
-          uint32_t a = lrec[jq[q]].w & 0xFFFF;
-          for (uint32_t kk = 1; kk <= d; ++kk) {
-            const uint4 r = lrec[a];
-            const uint64_t key = edge_key(r.z, myep[q], kk, ((r.w >> 16) & 3) == KIND_SERVER);
-            if (base + kk - 1 < scap) {
-              stage[base + kk - 1] = key;
-            } else {
-              edge_insert(key, trip, tcap, &flags);
-              flags |= F_STAGE_FULL;
-            }
-            a = r.w & 0xFFFF;
-          }
-        }
-        if (cvq[q] == 0) {  // won the slot (published above)
-          ++fresh_n;
-          const uint64_t x = (uint64_t)l_base[1] + ol[q];
-          if (x < gcap)
-            gpos[x] = (uint32_t)pos[q];
-          else
-            flags |= F_CTAB_DIRTY;
-        } else {  // joined an unpublished entry, or lost the slot to another chain
-          const uint64_t x = (uint64_t)l_base[2] + ol[q];
-          if (x < dcap) {
-            *reinterpret_cast<ulonglong2 *>(defer + 2 * x) = make_ulonglong2(sg[q], ps[q]);
-          } else {
-            int rr = 0;
-            for (uint32_t t = 0; t < spin && rr == 0; ++t) rr = chain_put(ctab, ccap, sg[q], ps[q], &flags, gpos, gcap, counters);
-            if (rr == 0) flags |= F_SPIN;  // unchecked: the run is redone on the exact walk
-            fresh_n += rr == 1;
-          }
-        }
-      }
-    }
-    KMZ_FSTAMP(8);
-    // per walker: row counts, pending list, rowpos
-#pragma unroll
-    for (int q = 0; q < FTW; ++q) {
-      if (kq[q] == KIND_CLIENT) continue;  // (an empty walker slot)
-      const uint32_t i = w0 + jq[q];
-      const bool pending = st[q] == S_PEND;
-      uint64_t rp = NONE64;
-      if (kq[q] == KIND_SERVER) {
-        rp = index_base + i;
-        if (!pending) {
-          ++rows;
-          rel += dd[q];
-          maxd = max(maxd, dd[q]);
-        }
-      }
-      if (pending) {
-        const uint32_t x = atomicAdd(&counters[C_PLIST], 1u);
-        if (x < pcap) plist[x] = i;
-      }
-      if (rowpos_out) rowpos_out[i] = rp;
-    }
-    __syncthreads();  // (wlist / imap reads of this round before the next round's leaders)
-    KMZ_FSTAMP(9);
+  {
+    ChainRun a;
+    a.ts = ts;
+    a.ctab = ctab;
+    a.ccap = ccap;
+    a.trip = trip;
+    a.tcap = tcap;
+    a.ep_ts = ep_ts;
+    a.rowpos_out = rowpos_out;
+    a.plist = plist;
+    a.pcap = pcap;
+    a.counters = counters;
+    a.stage = stage;
+    a.scap = scap;
+    a.defer = defer;
+    a.dcap = dcap;
+    a.gpos = gpos;
+    a.gcap = gcap;
+    a.n_ep = n_ep;
+    a.index_base = index_base;
+    a.seed = seed;
+    a.ablate = ablate;
+    chain_walk_rounds<JW, JTT, FTW>(lrec, wlist, wcount, w0, toff, any_other, L, a, rows, rel, maxd, fresh_n, flags);
   }
+  KMZ_FSTAMP(6);
   if (flags) atomicOr(&counters[C_FLAGS], flags);
-  for (int o = 32; o > 0; o >>= 1) {
-    fresh_n += __shfl_xor(fresh_n, o, 64);
-    rows += __shfl_xor(rows, o, 64);
-    rel += __shfl_xor(rel, o, 64);
-    maxd = max(maxd, (uint32_t)__shfl_xor(maxd, o, 64));
-  }
-  if (lane == 0) {
-    red[wv][0] = rows;
-    red[wv][1] = rel;
-    red[wv][2] = maxd;
-    red[wv][3] = fresh_n;
-  }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    uint32_t a = 0;
-    for (uint32_t w = 0; w < NW; ++w) a = threadIdx.x == 2 ? max(a, red[w][2]) : a + red[w][threadIdx.x];
-    tile_stats[(uint64_t)blockIdx.x * 4 + threadIdx.x] = a;
-  }
+  chain_tile_stats<JTT>(rows, rel, maxd, fresh_n, red, tile_stats);
   if (dbg_t && threadIdx.x == 0)
     for (int kk = 0; kk < 10; ++kk) atomicAdd(&g_fuse_dbg[kk], tacc[kk]);
 }
@@ -675,13 +448,12 @@ void launch_join_chain(hipStream_t s, const uint64_t *sid, const uint64_t *pid, 
                      tile_stats, stage, scap, defer, dcap, gpos, gcap, ablate);
 }
 
-void launch_chain_settle_list(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip,
+void launch_chain_settle_list(hipStream_t s, uint32_t nt, void *ctab, uint64_t ccap, unsigned long long *trip,
                               uint64_t tcap, unsigned int *counters, const uint32_t *tile_stats,
                               unsigned long long *stats64, const unsigned long long *stage, uint32_t scap,
                               const unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap,
                               uint32_t ablate) {
-  if (!n) return;
-  const uint32_t nt = join_tiles(n);
+  if (!nt) return;
   hipLaunchKernelGGL(k_chain_settle_list, dim3(std::min<uint32_t>(2048, std::max<uint32_t>(64, nt))), dim3(256), 0, s,
                      stage, scap, defer, dcap, trip, tcap, reinterpret_cast<unsigned long long *>(ctab), ccap, counters,
                      stats64, gpos, gcap, spin_bound(ablate));

@@ -471,16 +471,27 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
     rk[q] = e < cn ? atomicAdd(&cnt[(uint32_t)(h[q] >> sh) & (M - 1)], 1u) : 0;
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < M; k += blockDim.x) {
-    const uint32_t c = cnt[k];
-    base[k] = c ? atomicAdd(&cur2[(b << B2) | k], c) : 0;
+  // each sub-bin's global run, reserved with one device atomic; the returned
+  // bases are stored to LDS only after the scan and the LDS scatter below, so
+  // the atomics' round trip overlaps them (barriers here wait for LDS only)
+  static_assert((1u << 12) <= 4 * 1024, "M <= 4 sub-bins per thread");
+  uint32_t rb[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u) {
+    const uint32_t k = u * 1024 + threadIdx.x;
+    const uint32_t c = k < M ? cnt[k] : 0;
+    if (c) rb[u] = atomicAdd(&cur2[(b << B2) | k], c);
   }
-  __syncthreads();
-  block_scan_lds(cnt, M, wsum);  // cnt := local offsets
+  block_scan_lds(cnt, M, wsum);  // cnt := local offsets (its first barrier orders the reads above)
 #pragma unroll
   for (int q = 0; q < PQ; ++q) {
     const uint32_t e = q * 1024 + threadIdx.x;
     if (e < cn) stg[cnt[(uint32_t)(h[q] >> sh) & (M - 1)] + rk[q]] = h[q];
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < 4; ++u) {
+    const uint32_t k = u * 1024 + threadIdx.x;
+    if (k < M) base[k] = rb[u];
   }
   __syncthreads();
   bool ovf = false;
@@ -549,16 +560,26 @@ __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__
   for (uint32_t b = threadIdx.x; b < CK_NB; b += CCT) {
     const uint32_t c = min(bcnt[b], CK_S);
     uint64_t x[CK_S];
+    // a bucket is 64 B (16 banks): read in lane order, lanes b, b+4, b+8,
+    // b+12 of a 16-lane group would hit the same four banks (4-way conflict on
+    // every ds_read_b128); rotating each lane's start by b/4 spreads a group
+    // over all 64 banks.  (Slot order does not matter to the pair test.)
+    const uint32_t rot = (b >> 2) & 3;
 #pragma unroll
     for (uint32_t j = 0; j < CK_S; j += 2) {
-      const ulonglong2 v = bkt2[(b * CK_S + j) / 2];
+      const uint32_t jj = (((j >> 1) + rot) & 3) << 1;
+      const ulonglong2 v = bkt2[(b * CK_S + jj) / 2];
       x[j] = v.x;
       x[j + 1] = v.y;
     }
+    // (x[] holds the slots in rotated order; slot s of the bucket is valid iff s < c)
+    bool ok[CK_S];
+#pragma unroll
+    for (uint32_t j = 0; j < CK_S; ++j) ok[j] = (((((j >> 1) + rot) & 3) << 1) | (j & 1)) < c;
 #pragma unroll
     for (uint32_t i = 0; i < CK_S; ++i)
 #pragma unroll
-      for (uint32_t j = i + 1; j < CK_S; ++j) dup |= j < c && x[i] == x[j];
+      for (uint32_t j = i + 1; j < CK_S; ++j) dup |= ok[i] && ok[j] && x[i] == x[j];
   }
   // overflow ids: against their bucket's slots and the later overflow ids
   const uint32_t no = min(novf, CK_OVF);

@@ -24,7 +24,8 @@ enum {
   C_WPOS = 7,   // K4 chain-table slots written outside the tile kernel (cleared after the run)
   C_FSTAGE = 8,  // fused join + walk: keys staged in the global list
   C_FDEFER = 9,  // fused join + walk: deferred chain checks in the global list
-  C_COUNT = 10
+  C_K3ESC = 10,  // partitioned K3: spans without a record (escapes)
+  C_COUNT = 12   // (even: the u64 statistics follow the counters)
 };
 // C_CERT bits: the window join's answers cannot be used (global table path)
 constexpr uint32_t CERT_DUP = 1u, CERT_OVF = 2u;
@@ -102,6 +103,15 @@ void launch_k3_small(hipStream_t s, const uint8_t *kind, const uint32_t *shape, 
 uint32_t k3_partitions(uint32_t G);
 uint32_t k3_pmax();
 uint64_t k3_pool_bytes(uint32_t n);
+uint64_t *k3_tbase(void *pool, uint32_t n);
+uint32_t *k3_esc(void *pool, uint32_t n);
+// the partitioned K3's escapes (spans whose duration or timestamp do not fit an
+// 8-byte record, counted in C_K3ESC): into E ([6][G] u64, zero / max 0 / min
+// ~0 filled before the run), then folded into the group partials grp
+void launch_k3_escapes(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
+                       const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
+                       uint32_t n_shapes, uint32_t n_status, uint64_t index_base, void *pool,
+                       const unsigned int *counters, unsigned long long *E, uint32_t G, unsigned long long *grp);
 uint32_t k3_tiles(uint32_t n);
 uint64_t k3_dir_words(uint32_t n, uint32_t P, uint32_t S);
 void launch_tile_sum(hipStream_t s, const uint32_t *v, uint32_t ntiles, uint32_t stride, uint32_t fields,
@@ -147,11 +157,18 @@ void launch_join_chain(hipStream_t s, const uint64_t *sid, const uint64_t *pid, 
                        uint32_t *plist, uint32_t pcap, uint32_t *tile_stats, unsigned long long *stage, uint32_t scap,
                        unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap, uint4 *etab,
                        uint32_t ablate = 0);
-void launch_chain_settle_list(hipStream_t s, uint32_t n, void *ctab, uint64_t ccap, unsigned long long *trip,
+// (nt: the tile kernel's tiles, whose tile_stats rows are summed)
+void launch_chain_settle_list(hipStream_t s, uint32_t nt, void *ctab, uint64_t ccap, unsigned long long *trip,
                               uint64_t tcap, unsigned int *counters, const uint32_t *tile_stats,
                               unsigned long long *stats64, const unsigned long long *stage, uint32_t scap,
                               const unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap,
                               uint32_t ablate = 0);
+// K4 chain interning, one workgroup per tile (kmz_walk.hip); same global
+// lists as the fused kernel (settled by launch_chain_settle_list over walk_tiles)
+struct ChainRun;
+uint32_t walk_tiles(uint32_t n);
+void launch_chain_tile(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint32_t *cparent, uint32_t n,
+                       const uint32_t *dep_ep, uint32_t n_shapes, uint4 *etab, uint32_t *tile_stats, const ChainRun &a);
 // zero the chain-table entries this run wrote (instead of a memset of the table)
 void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
                         const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);
@@ -203,6 +220,7 @@ void launch_synth_fill_shard(hipStream_t s, int config, uint64_t seed, uint64_t 
                              uint32_t rank, const uint64_t *goff, const uint64_t *loff, uint64_t gbase,
                              const uint32_t *dur_table, SynthOut out);
 void launch_add_base(hipStream_t s, uint64_t *v, uint64_t n, uint64_t base);
+void launch_iota(hipStream_t s, unsigned long long *v, uint64_t n, uint64_t base);
 void launch_remap_index(hipStream_t s, unsigned long long *v, uint64_t n, uint32_t stride, uint32_t shift,
                         const uint64_t *lstart, const uint64_t *gstart, uint64_t nruns);
 

@@ -58,35 +58,50 @@ __device__ __forceinline__ uint32_t block_excl_scan_pairs(const uint32_t *cnt, u
 // ===========================================================================
 // K3P
 // ===========================================================================
-// one SERVER span's record: 16 bytes
-struct __align__(16) Rec {
-  uint64_t tsx;  // timestamp ^ 2^63
-  uint32_t d;    // duration (us)
-  uint32_t w;    // group within the partition (10 bits) | span index within the tile << 10 (11 bits)
-};
-
+// one SERVER span's record: 8 bytes
+//   bits  0-7   group within its partition (K3R = 256 groups per partition)
+//   bits  8-18  span index within the tile (K3T = 2048)
+//   bits 19-38  duration (us, < 2^20)
+//   bits 39-63  timestamp - the tile's least SERVER timestamp (us, < 2^25: 33 s)
+// (16-byte records {timestamp, duration, group | index} until round 3: the
+// record round trip was half of K3's HBM traffic.)  A span whose duration or
+// timestamp does not fit is an escape: produce lists its index, k3_escape adds
+// it into a block of escape partials with device atomics, and k3_escape_fold
+// folds that block into the group partials.  Escapes are rare (requests of a
+// second or more; a tile of spans spread over more than 33 s).
 #ifndef KMZ_K3T
 #define KMZ_K3T 2048
 #endif
 constexpr uint32_t K3T = KMZ_K3T;  // spans per tile
-constexpr uint32_t K3R = 1024;     // groups per partition
-constexpr uint32_t K3PMAX = 1024;  // partitions (G <= 1M)
+constexpr uint32_t K3R = 256;      // groups per partition
+constexpr uint32_t K3PMAX = 1024;  // partitions (G <= 2^18)
 constexpr int K3PT = K3T / 4;      // producer threads (four spans each)
-static_assert(K3R <= 1024 && K3T <= 4096 && K3PT <= 1024, "record word: 10 group bits, 12 index bits");
+constexpr uint32_t K3_GB = 8, K3_IB = 11, K3_DB = 20, K3_TB = 25;
+static_assert(K3R == (1u << K3_GB) && K3T <= (1u << K3_IB) && K3_GB + K3_IB + K3_DB + K3_TB == 64, "record fields");
+static_assert(K3PT <= 1024, "producer threads");
+__device__ __forceinline__ uint64_t k3_rec(uint32_t gl, uint32_t li, uint32_t d, uint64_t toff) {
+  return (uint64_t)gl | ((uint64_t)li << K3_GB) | ((uint64_t)d << (K3_GB + K3_IB)) | (toff << (64 - K3_TB));
+}
+__device__ __forceinline__ uint32_t k3_rec_g(uint64_t x) { return (uint32_t)x & (K3R - 1); }
+__device__ __forceinline__ uint32_t k3_rec_li(uint64_t x) { return (uint32_t)(x >> K3_GB) & ((1u << K3_IB) - 1); }
+__device__ __forceinline__ uint32_t k3_rec_d(uint64_t x) { return (uint32_t)(x >> (K3_GB + K3_IB)) & ((1u << K3_DB) - 1); }
+__device__ __forceinline__ uint64_t k3_rec_toff(uint64_t x) { return x >> (64 - K3_TB); }
 
 __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
                                                    const uint16_t *__restrict__ status, const uint32_t *__restrict__ dur,
                                                    const int64_t *__restrict__ ts, uint32_t n,
                                                    const uint32_t *__restrict__ ep_of_shape, uint32_t n_shapes,
                                                    uint32_t n_ep, uint32_t n_status, uint32_t P, uint32_t ntiles,
-                                                   uint32_t S, uint32_t tps, Rec *__restrict__ pool,
-                                                   uint32_t *__restrict__ dir,
-                                                   unsigned int *__restrict__ counters,
+                                                   uint32_t S, uint32_t tps, uint64_t *__restrict__ pool,
+                                                   uint32_t *__restrict__ dir, uint64_t *__restrict__ tbase,
+                                                   uint32_t *__restrict__ esc, unsigned int *__restrict__ counters,
                                                    uint32_t *__restrict__ tile_servers) {
   __shared__ uint32_t cnt[K3PMAX], off[K3PMAX];
   __shared__ uint32_t wave_tot[K3PT / 64 + 1];
-  __shared__ Rec stage[K3T];
+  __shared__ unsigned long long wmin[K3PT / 64];
+  __shared__ uint64_t stage[K3T];
   const uint32_t tile = blockIdx.x, t0 = tile * K3T;
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   constexpr int PER = K3T / K3PT;
   // every column of the tile in flight at once (clamped, unconditional loads)
   uint8_t kd[PER];
@@ -103,27 +118,49 @@ __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ k
     tv[k] = ts[i];
   }
   for (uint32_t p = threadIdx.x; p < P; p += K3PT) cnt[p] = 0;
+  // the tile's least SERVER timestamp (order-preserving unsigned form): the
+  // records' time base
+  unsigned long long mn = ~0ull;
+#pragma unroll
+  for (int k = 0; k < PER; ++k)
+    if (t0 + k * K3PT + threadIdx.x < n && kd[k] == KIND_SERVER) mn = min(mn, (unsigned long long)((uint64_t)tv[k] ^ TS_BIAS));
+  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (unsigned long long)__shfl_xor(mn, o, 64));
+  if (lane == 0) wmin[w] = mn;
   __syncthreads();
+  uint64_t base = ~0ull;
+  for (int k = 0; k < K3PT / 64; ++k) base = min(base, (uint64_t)wmin[k]);
   uint32_t pp[PER], rr[PER];
-  Rec rec[PER];
+  uint64_t rec[PER];
   uint32_t servers = 0, flags = 0;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const uint32_t li = k * K3PT + threadIdx.x;
     pp[k] = NONE;
+    bool escape = false;
     if (t0 + li < n && kd[k] == KIND_SERVER) {
       ++servers;
       const uint32_t ep = sh[k] < n_shapes ? (ep_of_shape ? ep_of_shape[sh[k]] : sh[k]) : NONE;  // null map: by shape
       if (ep >= n_ep || st[k] >= n_status) {
         flags |= F_RANGE;
-        continue;
+      } else {
+        const uint32_t g = ep * n_status + st[k];
+        const uint64_t toff = ((uint64_t)tv[k] ^ TS_BIAS) - base;
+        if (du[k] < (1u << K3_DB) && toff < (1ull << K3_TB)) {
+          pp[k] = g / K3R;
+          rec[k] = k3_rec(g % K3R, li, du[k], toff);
+          rr[k] = atomicAdd(&cnt[pp[k]], 1u);
+        } else {
+          escape = true;
+        }
       }
-      const uint32_t g = ep * n_status + st[k];
-      pp[k] = g / K3R;
-      rec[k].tsx = (uint64_t)tv[k] ^ TS_BIAS;
-      rec[k].d = du[k];
-      rec[k].w = (g % K3R) | (li << 10);
-      rr[k] = atomicAdd(&cnt[pp[k]], 1u);
+    }
+    // escapes: one list reservation per wave
+    const uint64_t em = __ballot(escape);
+    if (em) {
+      uint32_t eb = 0;
+      if (lane == 0) eb = atomicAdd(&counters[C_K3ESC], (uint32_t)__popcll(em));
+      eb = __shfl(eb, 0, 64);
+      if (escape) esc[eb + __popcll(em & ((1ull << lane) - 1))] = t0 + li;
     }
   }
   if (flags) atomicOr(&counters[C_FLAGS], flags);
@@ -133,22 +170,66 @@ __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ k
   // workgroup's words are contiguous (slice s holds tiles s, s + S, ...)
   for (uint32_t p = threadIdx.x; p < P; p += K3PT)
     dir[((uint64_t)p * S + tile % S) * tps + tile / S] = (off[p] << 16) | cnt[p];
+  if (threadIdx.x == 0) tbase[tile] = base;
 #pragma unroll
   for (int k = 0; k < PER; ++k)
     if (pp[k] != NONE) stage[off[pp[k]] + rr[k]] = rec[k];
   __syncthreads();
-  // coalesced copy of the partition-sorted tile into its region
+  // coalesced copy of the partition-sorted tile into its region (16 bytes a lane)
   const uint4 *src = reinterpret_cast<const uint4 *>(stage);
   uint4 *dst = reinterpret_cast<uint4 *>(pool + (uint64_t)tile * K3T);
-  for (uint32_t w = threadIdx.x; w < total; w += K3PT) dst[w] = src[w];
+  for (uint32_t x = threadIdx.x; 2 * x < total; x += K3PT) dst[x] = src[x];
   // realtime-row count: per tile, summed later (no same-address atomics)
   for (int o = 32; o > 0; o >>= 1) servers += __shfl_xor(servers, o, 64);
-  if ((threadIdx.x & 63) == 0) wave_tot[threadIdx.x >> 6] = servers;
+  if (lane == 0) wave_tot[w] = servers;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
-    for (int w = 0; w < K3PT / 64; ++w) t += wave_tot[w];
+    for (int k = 0; k < K3PT / 64; ++k) t += wave_tot[k];
     tile_servers[tile] = t;
+  }
+}
+
+// the escapes (spans without a record) into the escape block E [6][G]:
+// device atomics, one span at a time (rare)
+__global__ void __launch_bounds__(256) k3_escape(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
+                                                 const uint16_t *__restrict__ status, const uint32_t *__restrict__ dur,
+                                                 const int64_t *__restrict__ ts, const uint32_t *__restrict__ ep_of_shape,
+                                                 uint32_t n_shapes, uint32_t n_status, uint64_t index_base,
+                                                 const uint32_t *__restrict__ esc, const unsigned int *__restrict__ counters,
+                                                 unsigned long long *__restrict__ E, uint32_t G) {
+  const uint32_t m = counters[C_K3ESC];
+  for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < m; x += gridDim.x * 256) {
+    const uint32_t i = esc[x];
+    const uint32_t sh = shape[i];
+    const uint32_t ep = ep_of_shape ? ep_of_shape[sh] : sh;  // (checked by produce: a listed span is in range)
+    const uint32_t g = ep * n_status + status[i];
+    const uint64_t d = dur[i], dd = d * d;
+    atomicAdd(&E[g], 1ull);
+    atomicAdd(&E[G + g], (unsigned long long)d);
+    atomicAdd(&E[2ull * G + g], (unsigned long long)(dd & 0xFFFFFFFFull));
+    atomicAdd(&E[3ull * G + g], (unsigned long long)(dd >> 32));
+    atomicMax(&E[4ull * G + g], (unsigned long long)((uint64_t)ts[i] ^ TS_BIAS));
+    atomicMin(&E[5ull * G + g], (unsigned long long)(index_base + i));
+    (void)kind;
+    (void)n_shapes;
+  }
+}
+
+// E into the group partials, one thread per group, canonical limbs kept
+__global__ void __launch_bounds__(256) k3_escape_fold(const unsigned int *__restrict__ counters,
+                                                      const unsigned long long *__restrict__ E, uint32_t G,
+                                                      unsigned long long *__restrict__ grp) {
+  if (counters[C_K3ESC] == 0) return;
+  for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < G; g += gridDim.x * 256) {
+    if (E[g] == 0) continue;
+    grp[g] += E[g];
+    grp[G + g] += E[G + g];
+    const unsigned long long s2a = grp[2ull * G + g] + E[2ull * G + g], s2b = grp[3ull * G + g] + E[3ull * G + g];
+    grp[2ull * G + g] = s2a & 0xFFFFFFFFull;
+    grp[3ull * G + g] = s2b + (s2a >> 32);
+    grp[4ull * G + g] = max(grp[4ull * G + g], E[4ull * G + g]);
+    grp[5ull * G + g] = min(grp[5ull * G + g], E[5ull * G + g]);
   }
 }
 
@@ -185,11 +266,11 @@ __global__ void __launch_bounds__(1024) k_tile_sum(const uint32_t *__restrict__ 
 static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32_t>(64, (ntiles + 1023) / 1024 + 0); }
 
 // slice s of partition p: tiles s, s+S, ...  -> part[(s*6 + f) * G + g].
-// Each wave takes 64 of the slice's tiles at a time (one directory word per
-// lane), scans their run lengths across the lanes, and spreads the
-// concatenation of the runs over its lanes (coalesced 16-byte reads, four per
-// lane in flight); a record finds its run by a binary search over the wave's
-// 64 run starts in LDS.
+// Each wave takes 64 of the slice's tiles at a time (one directory word and
+// time base per lane), scans their run lengths across the lanes, and spreads
+// the concatenation of the runs over its lanes (coalesced 8-byte reads, four
+// per lane in flight); a record finds its run by a binary search over the
+// wave's 64 run starts in LDS.
 //
 // PACK (a slice holds < 2^22 records: ceil(ntiles / S) * K3T < 2^22): four LDS
 // atomics per record instead of six --
@@ -198,34 +279,63 @@ static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32
 //   a_s2  += d^2            (d < 2^20: d^2 < 2^40, the sum < 2^62)
 //   a_tsx  max, a_fst min   the first index as a u32 within the slice
 //                           (monotone in the global index)
-// a duration >= 2^20 us (rare) counts in a_cs, adds d to a_s1b and d^2 as
-// lo32 into a_s2 and hi32 into a_s2h.  Written out in the unpacked partial
-// format (s2 split into lo32 / hi32 limbs).
+// (every record's duration is < 2^20: wider ones are escapes).  Written out in
+// the unpacked partial format (s2 split into lo32 / hi32 limbs).
 constexpr int K3RT = 256;
 constexpr uint32_t K3RB = 64;  // runs per wave batch (one per lane)
-constexpr uint32_t K3_SMALL_D = 1u << 20;
+#ifndef KMZ_K3_COND
+#define KMZ_K3_COND 1  // max / min atomics only when a plain read says they move
+#endif
+// one record into the LDS accumulators: fi is its index within the slice /
+// item (PACK) or its global index
 template <bool PACK>
-__global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
-                                                  uint32_t ntiles, uint32_t S, uint32_t G, uint64_t index_base,
-                                                  unsigned long long *__restrict__ part) {
-  constexpr uint32_t A = PACK ? 1 : K3R;  // (the unpacked arrays)
-  constexpr uint32_t B = PACK ? K3R : 1;  // (the packed arrays)
-  __shared__ unsigned long long a_cnt[A], a_s1[A], a_s2a[A], a_s2b[A], a_tsx[K3R], a_fst[A];
-  __shared__ unsigned long long a_cs[B], a_s2[B], a_s1b[B], a_s2h[B];
-  __shared__ uint32_t a_fst32[B];
+__device__ __forceinline__ void k3_accumulate(uint64_t x, uint64_t tsx, uint64_t fi, unsigned long long *a0,
+                                              unsigned long long *a1, unsigned long long *a2, unsigned long long *a3,
+                                              unsigned long long *a_tsx, unsigned long long *a_fst,
+                                              uint32_t *a_fst32) {
+  const uint32_t kl = k3_rec_g(x);
+  const uint64_t d = k3_rec_d(x), dd = d * d;
+  if (PACK) {
+    atomicAdd(&a0[kl], (1ull << 42) + d);
+    atomicAdd(&a1[kl], (unsigned long long)dd);
+  } else {
+    atomicAdd(&a0[kl], 1ull);
+    atomicAdd(&a1[kl], (unsigned long long)d);
+    atomicAdd(&a2[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
+    atomicAdd(&a3[kl], (unsigned long long)(dd >> 32));
+  }
+#if KMZ_K3_COND
+  // max and min only move one way: a plain LDS read that already dominates
+  // this record makes its atomic a no-op, so it is skipped (a stale read can
+  // only cost an unneeded atomic)
+  if (tsx > a_tsx[kl]) atomicMax(&a_tsx[kl], (unsigned long long)tsx);
+  if (PACK) {
+    if ((uint32_t)fi < a_fst32[kl]) atomicMin(&a_fst32[kl], (uint32_t)fi);
+  } else {
+    if (fi < a_fst[kl]) atomicMin(&a_fst[kl], (unsigned long long)fi);
+  }
+#else
+  atomicMax(&a_tsx[kl], (unsigned long long)tsx);
+  if (PACK)
+    atomicMin(&a_fst32[kl], (uint32_t)fi);
+  else
+    atomicMin(&a_fst[kl], (unsigned long long)fi);
+#endif
+}
+
+template <bool PACK>
+__global__ void __launch_bounds__(K3RT) k3_reduce(const uint64_t *__restrict__ pool, const uint32_t *__restrict__ dir,
+                                                  const uint64_t *__restrict__ tbase, uint32_t ntiles, uint32_t S,
+                                                  uint32_t G, uint64_t index_base, unsigned long long *__restrict__ part) {
+  __shared__ unsigned long long acc[6 * K3R];
   constexpr uint32_t NW = K3RT / 64;
   __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB];  // per wave: run starts in the batch, pool offsets
+  __shared__ uint64_t r_tb[NW][K3RB];                    // ... and the runs' time bases
+  unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
+                     *a_fst = acc + 5 * K3R;
+  uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
   const uint32_t s = blockIdx.x, p = blockIdx.y;
-  for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
-    a_tsx[k] = 0;
-    if (PACK) {
-      a_cs[k] = a_s2[k] = a_s1b[k] = a_s2h[k] = 0;
-      a_fst32[k] = ~0u;
-    } else {
-      a_cnt[k] = a_s1[k] = a_s2a[k] = a_s2b[k] = 0;
-      a_fst[k] = ~0ull;
-    }
-  }
+  for (uint32_t k = threadIdx.x; k < 6 * K3R; k += K3RT) acc[k] = k < 5 * K3R ? 0ull : ~0ull;
   __syncthreads();
   const uint32_t tps = (ntiles + S - 1) / S;
   const uint32_t *row = dir + ((uint64_t)p * S + s) * tps;  // this slice's tiles, in order
@@ -247,10 +357,11 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
     const uint32_t total = __shfl(incl, 63, 64);
     r_pre[w][lane] = incl - c;
     r_off[w][lane] = (uint32_t)(k < ntiles ? k : 0) * K3T + o;  // (ntiles * K3T < 2^32: n < 2^32)
+    r_tb[w][lane] = c ? tbase[k] : 0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     for (uint32_t q0 = 0; q0 < total; q0 += 64 * U) {
-      Rec xr[U];
+      uint64_t xr[U];
       uint32_t run[U];
       bool v[U];
 #pragma unroll
@@ -267,33 +378,15 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
         if (!v[u]) continue;
-        const uint32_t kl = xr[u].w & (K3R - 1);
-        const uint64_t d = xr[u].d, dd = d * d;
-        if (PACK) {
-          if (d < K3_SMALL_D) {
-            atomicAdd(&a_cs[kl], (1ull << 42) + d);
-            atomicAdd(&a_s2[kl], (unsigned long long)dd);
-          } else {  // (rare)
-            atomicAdd(&a_cs[kl], 1ull << 42);
-            atomicAdd(&a_s1b[kl], (unsigned long long)d);
-            atomicAdd(&a_s2[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
-            atomicAdd(&a_s2h[kl], (unsigned long long)(dd >> 32));
-          }
-          atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
-          // this slice's tiles are s, s + S, ...: (k - s) / S numbers them
-          const uint32_t m = (uint32_t)((k0 - s) / S) + run[u] * (uint32_t)(step / S);
-          atomicMin(&a_fst32[kl], m * K3T + (xr[u].w >> 10));
-        } else {
-          atomicAdd(&a_cnt[kl], 1ull);
-          atomicAdd(&a_s1[kl], (unsigned long long)d);
-          atomicAdd(&a_s2a[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
-          atomicAdd(&a_s2b[kl], (unsigned long long)(dd >> 32));
-          atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
-          atomicMin(&a_fst[kl], (unsigned long long)(index_base + (k0 + run[u] * step) * K3T + (xr[u].w >> 10)));
-        }
+        const uint64_t tsx = r_tb[w][run[u]] + k3_rec_toff(xr[u]);
+        // this slice's tiles are s, s + S, ...: (k - s) / S numbers them
+        const uint64_t fi = PACK ? (uint64_t)(((uint32_t)((k0 - s) / S) + run[u] * (uint32_t)(step / S)) * K3T +
+                                              k3_rec_li(xr[u]))
+                                 : index_base + (k0 + run[u] * step) * K3T + k3_rec_li(xr[u]);
+        k3_accumulate<PACK>(xr[u], tsx, fi, a0, a1, a2, a3, a_tsx, a_fst, a_fst32);
       }
     }
-    __builtin_amdgcn_wave_barrier();  // r_pre / r_off are rewritten by the next batch
+    __builtin_amdgcn_wave_barrier();  // r_pre / r_off / r_tb are rewritten by the next batch
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
@@ -301,19 +394,19 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const Rec *__restrict__ pool, 
     if (g >= G) break;
     unsigned long long *b = part + (uint64_t)s * 6 * G + g;
     if (PACK) {
-      const unsigned long long cs = a_cs[k], s2 = a_s2[k];
+      const unsigned long long cs = a0[k], s2 = a1[k];
       const uint32_t f = a_fst32[k];
       b[0] = cs >> 42;
-      b[G] = (cs & ((1ull << 42) - 1)) + a_s1b[k];
+      b[G] = cs & ((1ull << 42) - 1);
       b[2ull * G] = s2 & 0xFFFFFFFFull;
-      b[3ull * G] = (s2 >> 32) + a_s2h[k];
+      b[3ull * G] = s2 >> 32;
       b[4ull * G] = a_tsx[k];
       b[5ull * G] = f == ~0u ? ~0ull : index_base + ((uint64_t)s + (uint64_t)(f / K3T) * S) * K3T + f % K3T;
     } else {
-      b[0] = a_cnt[k];
-      b[G] = a_s1[k];
-      b[2ull * G] = a_s2a[k] & 0xFFFFFFFFull;  // (canonical limbs when this is the last word: S = 1)
-      b[3ull * G] = a_s2b[k] + (a_s2a[k] >> 32);
+      b[0] = a0[k];
+      b[G] = a1[k];
+      b[2ull * G] = a2[k] & 0xFFFFFFFFull;  // (canonical limbs when this is the last word: S = 1)
+      b[3ull * G] = a3[k] + (a2[k] >> 32);
       b[4ull * G] = a_tsx[k];
       b[5ull * G] = a_fst[k];
     }
@@ -403,9 +496,10 @@ __global__ void __launch_bounds__(1024) k3_plan(const uint32_t *__restrict__ tot
 // record loop is instantiated for each accumulator form and chosen once per
 // workgroup (as the fixed-slice k3_reduce<PACK> is compiled), not per record.
 template <bool PACK>
-__device__ __forceinline__ void k3_reduce_items(const Rec *__restrict__ pool, const uint32_t *__restrict__ row,
-                                                uint64_t tb, uint64_t te, uint64_t index_base, unsigned long long *acc,
-                                                uint32_t (*r_pre)[K3RB], uint32_t (*r_off)[K3RB]) {
+__device__ __forceinline__ void k3_reduce_items(const uint64_t *__restrict__ pool, const uint32_t *__restrict__ row,
+                                                const uint64_t *__restrict__ tbase, uint64_t tb, uint64_t te,
+                                                uint64_t index_base, unsigned long long *acc, uint32_t (*r_pre)[K3RB],
+                                                uint32_t (*r_off)[K3RB], uint64_t (*r_tb)[K3RB]) {
   constexpr uint32_t NW = K3RT / 64;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
@@ -426,10 +520,11 @@ __device__ __forceinline__ void k3_reduce_items(const Rec *__restrict__ pool, co
     const uint32_t total = __shfl(incl, 63, 64);
     r_pre[w][lane] = incl - c;
     r_off[w][lane] = (uint32_t)(k < te ? k : 0) * K3T + o;
+    r_tb[w][lane] = c ? tbase[k] : 0;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     for (uint32_t q0 = 0; q0 < total; q0 += 64 * U) {
-      Rec xr[U];
+      uint64_t xr[U];
       uint32_t run[U];
       bool v[U];
 #pragma unroll
@@ -446,42 +541,26 @@ __device__ __forceinline__ void k3_reduce_items(const Rec *__restrict__ pool, co
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
         if (!v[u]) continue;
-        const uint32_t kl = xr[u].w & (K3R - 1);
-        const uint64_t d = xr[u].d, dd = d * d;
         const uint64_t tile = k0 + run[u];
-        if (PACK) {
-          if (d < K3_SMALL_D) {
-            atomicAdd(&a0[kl], (1ull << 42) + d);
-            atomicAdd(&a1[kl], (unsigned long long)dd);
-          } else {  // (rare)
-            atomicAdd(&a0[kl], 1ull << 42);
-            atomicAdd(&a2[kl], (unsigned long long)d);
-            atomicAdd(&a1[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
-            atomicAdd(&a3[kl], (unsigned long long)(dd >> 32));
-          }
-          atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
-          atomicMin(&a_fst32[kl], (uint32_t)(tile - tb) * K3T + (xr[u].w >> 10));
-        } else {
-          atomicAdd(&a0[kl], 1ull);
-          atomicAdd(&a1[kl], (unsigned long long)d);
-          atomicAdd(&a2[kl], (unsigned long long)(dd & 0xFFFFFFFFull));
-          atomicAdd(&a3[kl], (unsigned long long)(dd >> 32));
-          atomicMax(&a_tsx[kl], (unsigned long long)xr[u].tsx);
-          atomicMin(&a_fst[kl], (unsigned long long)(index_base + tile * K3T + (xr[u].w >> 10)));
-        }
+        const uint64_t tsx = r_tb[w][run[u]] + k3_rec_toff(xr[u]);
+        const uint64_t fi = PACK ? (uint64_t)((uint32_t)(tile - tb) * K3T + k3_rec_li(xr[u]))
+                                 : index_base + tile * K3T + k3_rec_li(xr[u]);
+        k3_accumulate<PACK>(xr[u], tsx, fi, a0, a1, a2, a3, a_tsx, a_fst, a_fst32);
       }
     }
-    __builtin_amdgcn_wave_barrier();  // r_pre / r_off are rewritten by the next batch
+    __builtin_amdgcn_wave_barrier();  // r_pre / r_off / r_tb are rewritten by the next batch
   }
 }
 
-__global__ void __launch_bounds__(K3RT) k3_reduce_bal(const Rec *__restrict__ pool, const uint32_t *__restrict__ dir,
-                                                      uint32_t ntiles, uint32_t P, const uint32_t *__restrict__ item_off,
+__global__ void __launch_bounds__(K3RT) k3_reduce_bal(const uint64_t *__restrict__ pool, const uint32_t *__restrict__ dir,
+                                                      const uint64_t *__restrict__ tbase, uint32_t ntiles, uint32_t P,
+                                                      const uint32_t *__restrict__ item_off,
                                                       uint32_t G, uint64_t index_base, uint32_t upk,
                                                       unsigned long long *__restrict__ part) {
   __shared__ unsigned long long acc[6 * K3R];
   constexpr uint32_t NW = K3RT / 64;
   __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB], wred[NW];
+  __shared__ uint64_t r_tb[NW][K3RB];
   const uint32_t item = blockIdx.x;
   if (item >= item_off[P]) return;  // (the grid is an upper bound; uniform over the workgroup)
   uint32_t lo = 0, hi = P;  // the partition: item_off[p] <= item < item_off[p + 1]
@@ -511,14 +590,14 @@ __global__ void __launch_bounds__(K3RT) k3_reduce_bal(const Rec *__restrict__ po
   uint32_t tot = 0;
   for (uint32_t k = 0; k < NW; ++k) tot += wred[k];
   const bool pack = tot < (1u << 22) && !upk;  // (upk: test knob)
-  // packed: cs, s2, s1b, s2h, tsx, fst32 (u32) -- unpacked: cnt, s1, s2a, s2b, tsx, fst
+  // packed: cs, s2, -, -, tsx, fst32 (u32) -- unpacked: cnt, s1, s2a, s2b, tsx, fst
   unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
                      *a_fst = acc + 5 * K3R;
   uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
   if (pack)
-    k3_reduce_items<true>(pool, row, tb, te, index_base, acc, r_pre, r_off);
+    k3_reduce_items<true>(pool, row, tbase, tb, te, index_base, acc, r_pre, r_off, r_tb);
   else
-    k3_reduce_items<false>(pool, row, tb, te, index_base, acc, r_pre, r_off);
+    k3_reduce_items<false>(pool, row, tbase, tb, te, index_base, acc, r_pre, r_off, r_tb);
   __syncthreads();
   unsigned long long *b = part + (uint64_t)item * 6 * K3R;
   for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
@@ -527,9 +606,9 @@ __global__ void __launch_bounds__(K3RT) k3_reduce_bal(const Rec *__restrict__ po
       const unsigned long long cs = a0[k], s2 = a1[k];
       const uint32_t f = a_fst32[k];
       b[k] = cs >> 42;
-      b[K3R + k] = (cs & ((1ull << 42) - 1)) + a2[k];
+      b[K3R + k] = cs & ((1ull << 42) - 1);
       b[2 * K3R + k] = s2 & 0xFFFFFFFFull;
-      b[3 * K3R + k] = (s2 >> 32) + a3[k];
+      b[3 * K3R + k] = s2 >> 32;
       b[4 * K3R + k] = a_tsx[k];
       b[5 * K3R + k] = f == ~0u ? ~0ull : index_base + tb * K3T + f;
     } else {
@@ -706,9 +785,10 @@ void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape
                        unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp) {
   if (!n || !n_ep) return;
   const uint32_t G = n_ep * n_status, P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
+  uint64_t *rec = static_cast<uint64_t *>(pool);
   hipLaunchKernelGGL(k3_produce, dim3(ntiles), dim3(K3PT), 0, s, kind, shape, status, dur, ts, n, ep_of_shape,
-                     n_shapes, n_ep, n_status, P, ntiles, S, (ntiles + S - 1) / S, (Rec *)pool, dir, counters,
-                     tile_tmp);
+                     n_shapes, n_ep, n_status, P, ntiles, S, (ntiles + S - 1) / S, rec, dir, k3_tbase(pool, n),
+                     k3_esc(pool, n), counters, tile_tmp);
   hipLaunchKernelGGL(k_tile_sum, dim3(std::max<uint32_t>(1, tile_sum_blocks(ntiles))), dim3(1024), 0, s, tile_tmp, ntiles, 1u, 1u,
                      n_server, 99u);
 }
@@ -724,12 +804,12 @@ void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base
   // in-slice first indices fit their fields)
   // one slice: its partials are the group partials ([6][G], the same layout)
   unsigned long long *dst = S == 1 ? grp : part;
+  const uint64_t *rec = static_cast<const uint64_t *>(pool);
+  const uint64_t *tb = k3_tbase(const_cast<void *>(pool), n);
   if (KMZ_K3_PACK && (uint64_t)((ntiles + S - 1) / S) * K3T < (1ull << 22))
-    hipLaunchKernelGGL(k3_reduce<true>, dim3(S, P), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, S, G, index_base,
-                       dst);
+    hipLaunchKernelGGL(k3_reduce<true>, dim3(S, P), dim3(K3RT), 0, s, rec, dir, tb, ntiles, S, G, index_base, dst);
   else
-    hipLaunchKernelGGL(k3_reduce<false>, dim3(S, P), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, S, G,
-                       index_base, dst);
+    hipLaunchKernelGGL(k3_reduce<false>, dim3(S, P), dim3(K3RT), 0, s, rec, dir, tb, ntiles, S, G, index_base, dst);
   if (S > 1)
     hipLaunchKernelGGL(k3_combine, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part, S,
                        G, grp);
@@ -768,8 +848,9 @@ void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_
   const uint32_t slots = std::min<uint32_t>(K3_ITEMS, 2 * k3_resident());
   const uint32_t nitems = slots > P + 256 ? slots - P : 256;
   hipLaunchKernelGGL(k3_plan, dim3(1), dim3(1024), 0, s, tot, P, ntiles, nitems, item_off);
-  hipLaunchKernelGGL(k3_reduce_bal, dim3(k3_bal_items(G)), dim3(K3RT), 0, s, (const Rec *)pool, dir, ntiles, P, item_off,
-                     G, index_base, unpacked ? 1u : 0u, part);
+  hipLaunchKernelGGL(k3_reduce_bal, dim3(k3_bal_items(G)), dim3(K3RT), 0, s, static_cast<const uint64_t *>(pool), dir,
+                     k3_tbase(const_cast<void *>(pool), n), ntiles, P, item_off, G, index_base, unpacked ? 1u : 0u,
+                     part);
   hipLaunchKernelGGL(k3_combine_bal, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part,
                      item_off, G, grp);
 }
@@ -779,7 +860,27 @@ uint32_t k3_bal_items(uint32_t G) { return K3_ITEMS + (G + K3R - 1) / K3R; }  //
 uint64_t k3_bal_part_bytes(uint32_t G) { return (uint64_t)k3_bal_items(G) * 6 * K3R * 8; }
 uint32_t k3_partitions(uint32_t G) { return (G + K3R - 1) / K3R; }
 uint32_t k3_pmax() { return K3PMAX; }
-uint64_t k3_pool_bytes(uint32_t n) { return (uint64_t)((n + K3T - 1) / K3T) * K3T * sizeof(Rec); }
+// the record pool: [tile][K3T] records, then each tile's time base (u64), then
+// the escape list (u32 span indices, as many as spans at worst)
+uint64_t k3_pool_bytes(uint32_t n) {
+  const uint64_t nt = (n + K3T - 1) / K3T;
+  return nt * K3T * 8 + nt * 8 + ((uint64_t)n + 4) * 4;
+}
+uint64_t *k3_tbase(void *pool, uint32_t n) { return static_cast<uint64_t *>(pool) + (uint64_t)((n + K3T - 1) / K3T) * K3T; }
+uint32_t *k3_esc(void *pool, uint32_t n) {
+  return reinterpret_cast<uint32_t *>(k3_tbase(pool, n) + (n + K3T - 1) / K3T);
+}
+
+void launch_k3_escapes(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
+                       const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
+                       uint32_t n_shapes, uint32_t n_status, uint64_t index_base, void *pool,
+                       const unsigned int *counters, unsigned long long *E, uint32_t G, unsigned long long *grp) {
+  if (!n || !G) return;
+  hipLaunchKernelGGL(k3_escape, dim3(256), dim3(256), 0, s, kind, shape, status, dur, ts, ep_of_shape, n_shapes,
+                     n_status, index_base, k3_esc(pool, n), counters, E, G);
+  hipLaunchKernelGGL(k3_escape_fold, dim3(std::min<uint32_t>((G + 255) / 256, 2048)), dim3(256), 0, s, counters, E, G,
+                     grp);
+}
 uint32_t k3_tiles(uint32_t n) { return (n + K3T - 1) / K3T; }
 uint64_t k3_dir_words(uint32_t n, uint32_t P, uint32_t S) {
   const uint64_t nt = k3_tiles(n);

@@ -93,6 +93,16 @@ void launch_add_base(hipStream_t s, uint64_t *v, uint64_t n, uint64_t base) {
   if (n && base) hipLaunchKernelGGL(k_add_base, dim3(grid_of(n)), dim3(256), 0, s, v, n, base);
 }
 
+// v[i] = base + i
+__global__ void __launch_bounds__(256) k_iota(unsigned long long *__restrict__ v, uint64_t n, uint64_t base) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    v[i] = base + i;
+}
+
+void launch_iota(hipStream_t s, unsigned long long *v, uint64_t n, uint64_t base) {
+  if (n) hipLaunchKernelGGL(k_iota, dim3(grid_of(n)), dim3(256), 0, s, v, n, base);
+}
+
 void launch_remap_index(hipStream_t s, unsigned long long *v, uint64_t n, uint32_t stride, uint32_t shift,
                         const uint64_t *lstart, const uint64_t *gstart, uint64_t nruns) {
   if (n && nruns)

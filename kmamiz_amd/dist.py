@@ -69,7 +69,7 @@ def merge_endpoint_partials(e: torch.Tensor, n_ep: int) -> torch.Tensor:
 
 
 def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: torch.Tensor, engine=None,
-              digest: int = 0, group=None, check_ids: bool = True):
+              digest: int = 0, group=None, check_ids: bool = True, exact: bool = True):
     """The whole per-step merge: one fixed-size MAX all-reduce that makes the
     ranks agree (group/endpoint counts, the id-table digest, the unresolved
     parent count) before any size-dependent collective, the sharding guards,
@@ -105,20 +105,38 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
     agree = torch.tensor([G, -G, E, -E, dg, -dg, nu, 1 if refused else 0], dtype=torch.int64, device=dev)
     dist.all_reduce(agree, op=dist.ReduceOp.MAX, group=group)
     a = agree.tolist()
-    if a[7]:
-        if isinstance(check_ids, IdGuard):
-            check_ids.abandon()  # its exchange was posted before the run: drain it on every rank
-        raise refused or ShardingError("another rank's shard has repeated span ids: sharding is not exact, "
-                                       "run unsharded")
     if a[0] != -a[1] or a[2] != -a[3] or a[4] != -a[5]:
+        if isinstance(check_ids, IdGuard):
+            check_ids.abandon()
         raise ShardingError("ranks merged partials over different endpoint/status id tables "
                             "(assign global ids with shard.exchange_tables)")
-    if a[6] > 0:
-        _check_shards(engine, nu, int(a[6]), dev, group)
-    if isinstance(check_ids, IdGuard):  # started before the run: its exchange overlapped it
-        check_ids.finish()
-    elif engine is not None and check_ids:
-        check_repeated_ids(engine, dev, group)
+    # the sharding guards: a span-id map that crosses shards (an id repeated
+    # inside a shard or across shards, a parent in another shard) makes the
+    # per-shard dependency results differ from the reference's global Map
+    # (Traces.ts:117-143).  With an engine the merge stays exact: the whole
+    # batch's dependency pass is re-run on one rank (_unsharded_deps); without
+    # one, or with ``exact=False``, every rank raises ShardingError.
+    crossed = bool(a[7])
+    if crossed and isinstance(check_ids, IdGuard):
+        check_ids.abandon()  # its exchange was posted before the run: drain it on every rank
+    if not crossed and a[6] > 0:
+        crossed = _check_shards(engine, nu, int(a[6]), dev, group, raise_=not exact)
+    if not crossed:
+        if isinstance(check_ids, IdGuard):  # started before the run: its exchange overlapped it
+            crossed = check_ids.finish(raise_=not exact)
+        elif engine is not None and check_ids:
+            crossed = IdGuard(engine, dev, group).start().finish(raise_=not exact)
+    if crossed and (engine is None or not exact):
+        raise refused or ShardingError("another rank's shard has repeated span ids: sharding is not exact, "
+                                       "run unsharded")
+    if crossed:
+        # the stats are exact per shard (realtime rows keep repeated ids,
+        # Traces.ts:28-31) and merge as usual; the dependency results come
+        # from one pass over the whole batch
+        if G:
+            _merge_groups_only(p, G, group)
+        _unsharded_deps(engine, e, E, dev, group)
+        return None
     if G:
         dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM, group=group)  # modular: exact for u64
     ming = p[5 * G : 6 * G]
@@ -217,9 +235,11 @@ class IdGuard:
             self.work.wait()
         self.work = self.send = self.recv = None
 
-    def finish(self) -> None:
+    def finish(self, raise_: bool = True) -> bool:
+        """-> True when some span id is in two shards (ShardingError instead
+        with ``raise_``)."""
         if self.world == 1:
-            return
+            return False
         if self.work is None:
             self.start()
         self.work.wait()
@@ -234,9 +254,10 @@ class IdGuard:
         flag = torch.tensor([1 if rep else 0], dtype=torch.int64, device=self.dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
         self.work = self.send = self.recv = None
-        if int(flag.item()):
+        if int(flag.item()) and raise_:
             raise ShardingError("a span id occurs in two shards: the reference's global span map would merge them "
                                 "(Traces.ts:117-123); run unsharded")
+        return bool(int(flag.item()))
 
 
 def check_repeated_ids(engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None) -> None:
@@ -285,9 +306,10 @@ def _unresolved(engine) -> int:
         raise
 
 
-def _check_shards(engine, nu: int, mu: int, dev, group=None) -> None:
+def _check_shards(engine, nu: int, mu: int, dev, group=None, raise_: bool = True) -> bool:
     """Exchange the unresolved parent ids (padded to the largest list) and
-    count, on every rank, how many of them are span ids of its own shard."""
+    count, on every rank, how many of them are span ids of its own shard.
+    -> True when some are (ShardingError instead with ``raise_``)."""
     mine = torch.zeros(mu, dtype=torch.int64, device=dev)
     if nu:
         engine.unresolved_parents(mine.data_ptr(), mu, mine.is_cuda)
@@ -295,8 +317,101 @@ def _check_shards(engine, nu: int, mu: int, dev, group=None) -> None:
     found = torch.tensor([engine.count_ids(allu.data_ptr(), allu.numel(), allu.is_cuda)], dtype=torch.int64,
                          device=dev)
     dist.all_reduce(found, op=dist.ReduceOp.SUM, group=group)
-    if int(found.item()):
+    if int(found.item()) and raise_:
         raise ShardingError(f"{int(found.item())} parent ids of one shard are spans of another: shard by whole traces")
+    return bool(int(found.item()))
+
+
+def _merge_groups_only(p: torch.Tensor, G: int, group=None) -> None:
+    """merge_group_partials on ``group``: SUM of the moments, MAX / MIN fields."""
+    dist.all_reduce(p[: 4 * G], op=dist.ReduceOp.SUM, group=group)
+    ts = _as_signed_order(p[4 * G : 5 * G])
+    dist.all_reduce(ts, op=dist.ReduceOp.MAX, group=group)
+    p[4 * G : 5 * G] = _as_signed_order(ts)
+    first = p[5 * G :]
+    first = torch.where(first == -1, torch.full_like(first, _I64_MAX), first)
+    dist.all_reduce(first, op=dist.ReduceOp.MIN, group=group)
+    p[5 * G :] = torch.where(first == _I64_MAX, torch.full_like(first, -1), first)
+
+
+def _bcast(t: torch.Tensor, dev, group=None) -> torch.Tensor:
+    """Broadcast a host tensor from rank 0 on ``dev``'s backend (device
+    tensors under RCCL); returns it on the host."""
+    if dev.type == "cpu":
+        dist.broadcast(t, src=0, group=group)
+        return t
+    d = t.to(dev)
+    dist.broadcast(d, src=0, group=group)
+    return d.cpu()
+
+
+def _unsharded_deps(engine, e: torch.Tensor, E: int, dev, group=None) -> None:
+    """The exact merge of shards whose span-id map crosses shards: rank 0
+    gathers every shard's columns (placed at their global flatten positions,
+    kmz_get_global_index) and shape tables, runs the dependency pass of the
+    whole batch on a second context of its GPU -- the reference's one global
+    Map (Traces.ts:117-143) -- and broadcasts its endpoint partials and edge
+    keys, which replace every rank's own (``e`` in place; the engine's edge
+    set by kmz_set_triples).  Cost: the batch's columns (35 B/span) to rank 0
+    and one unsharded dependency pass there, only when a guard fires."""
+    import numpy as np
+
+    from . import _lib as L
+    from .engine import Engine, ShapeTable, SpanBatch
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    b = engine.spans()
+    tab = engine.shape_table()
+    mine = {"gidx": engine.global_index(), "sid": b.span_id, "pid": b.parent_id, "kind": b.kind, "shape": b.shape,
+            "status": b.status, "dur": b.duration, "ts": b.timestamp,
+            "tab": (np.asarray(tab.rt_ep, np.uint32), np.asarray(tab.tag_ep, np.uint32),
+                    np.asarray(tab.dep_ep, np.uint32), int(tab.n_rt_ep), int(tab.n_tag_ep), int(tab.n_dep_ep),
+                    int(tab.n_status))}
+    parts = [None] * world
+    dist.all_gather_object(parts, mine, group=group)
+    W = 2 * E  # endpoint partial words: [max ts] E, [min first row] E
+    head = torch.zeros(W + 1, dtype=torch.int64)  # endpoint partials, then the key count
+    keys2 = np.zeros(0, np.uint64)
+    if rank == 0:
+        N = sum(len(x["gidx"]) for x in parts)
+        cols = {k: np.zeros(N, dt) for k, dt in (("sid", np.uint64), ("pid", np.uint64), ("kind", np.uint8),
+                                                  ("shape", np.uint32), ("status", np.uint16), ("dur", np.uint32),
+                                                  ("ts", np.int64))}
+        soff, tabs = 0, []
+        for x in parts:  # shard r's shape s is shape soff_r + s of the whole batch
+            g = np.asarray(x["gidx"], np.int64)
+            for k in cols:
+                cols[k][g] = np.asarray(x[k]) + (np.uint32(soff) if k == "shape" else 0)
+            tabs.append(x["tab"])
+            soff += len(x["tab"][2])
+        table = ShapeTable(*(np.concatenate([t[j] for t in tabs]) for j in range(3)),
+                           *(max(t[j] for t in tabs) for j in range(3, 7)))
+        whole = SpanBatch(cols["sid"], cols["pid"], cols["kind"], cols["shape"], cols["status"], cols["dur"],
+                          cols["ts"], 0)
+        e2 = Engine(torch.cuda.current_device())
+        try:
+            e2.load(whole, table)
+            e2.run(L.RUN_DEPS)
+            ew = e2.partials_words(L.PART_ENDPOINTS)
+            ep2 = np.zeros(max(1, ew), np.uint64)
+            e2.export_partials(L.PART_ENDPOINTS, ep2.ctypes.data, ew, False)
+            keys2 = np.asarray(e2.triples(sort=False), np.uint64)
+        finally:
+            e2.close()
+        if ew != W:
+            raise ShardingError(f"the unsharded pass has {ew // 2} endpoints, the shards {E}")
+        head[:W] = torch.from_numpy(ep2[:W].view(np.int64))
+        head[W] = len(keys2)
+    head = _bcast(head, dev, group)
+    nk = int(head[W].item())
+    kt = torch.zeros(max(1, nk), dtype=torch.int64)
+    if rank == 0 and nk:
+        kt[:nk] = torch.from_numpy(keys2.view(np.int64))
+    kt = _bcast(kt, dev, group)
+    e[:W] = head[:W].to(e.device)
+    kh = np.ascontiguousarray(kt[:nk].numpy().view(np.uint64))
+    engine.set_triples(kh.ctypes.data, nk, False)
 
 
 def merge_edge_keys(keys: torch.Tensor, group=None) -> torch.Tensor:

@@ -99,6 +99,7 @@ class Engine:
         self.n_dep_ep = 0
         self.n_status = 1
         self._pinned = {}  # name -> (ptr, bytes): reused page-locked result buffers
+        self._shapes = None  # the loaded batch's ShapeTable (or a synthetic config number)
 
     def close(self):
         if getattr(self, "ctx", None):
@@ -147,6 +148,7 @@ class Engine:
         self.index_base = batch.index_base
         self.n_dep_ep = shapes.n_dep_ep
         self.n_status = max(1, shapes.n_status)
+        self._shapes = shapes
 
     # ---- K1 on the device: Zipkin JSON -> columns (kmz_json_parse) -------------
     def json_parse(self, data=None, ptr: Optional[int] = None, length: int = 0, device: bool = False):
@@ -196,6 +198,7 @@ class Engine:
         self.index_base = index_base
         self.n_dep_ep = shapes.n_dep_ep
         self.n_status = max(1, shapes.n_status)
+        self._shapes = shapes
 
     def spans(self) -> SpanBatch:
         """The loaded batch's columns, copied to the host (kmz_get_spans)."""
@@ -217,6 +220,7 @@ class Engine:
         self.n = n.value
         self.n_dep_ep = d.n_endpoints
         self.n_status = d.n_status
+        self._shapes = config
         return self.n
 
     def load_synthetic_shard(self, config: int, seed: int, trace_begin: int, trace_end: int, world: int,
@@ -234,7 +238,29 @@ class Engine:
         self.index_base = 0
         self.n_dep_ep = d.n_endpoints
         self.n_status = d.n_status
+        self._shapes = config
         return self.n
+
+    def shape_table(self):
+        """The ShapeTable the loaded batch is indexed by."""
+        if isinstance(self._shapes, int):
+            from . import synth
+
+            return synth.shape_table(self._shapes)
+        return self._shapes
+
+    def global_index(self) -> np.ndarray:
+        """Global flatten index (Traces.ts:29) of every loaded span, as the
+        run's results report them (kmz_get_global_index)."""
+        out = np.zeros(max(1, self.n), np.uint64)
+        L.check(self.ctx, self._lib.kmz_get_global_index(self.ctx, L.ptr(out), len(out), L.MEM_HOST))
+        return out[: self.n]
+
+    def set_triples(self, src_ptr: int, n: int, device: bool):
+        """Replace the run's edge set with n keys (kmz_set_triples)."""
+        self.gen += 1
+        L.check(self.ctx, self._lib.kmz_set_triples(self.ctx, C.c_void_p(src_ptr) if n else None, n,
+                                                    L.MEM_DEVICE if device else L.MEM_HOST))
 
     def set_index_map(self, local_start: np.ndarray, global_start: np.ndarray):
         """Local -> global flatten-index runs of a non-contiguous shard

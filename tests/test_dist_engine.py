@@ -97,8 +97,33 @@ def test_two_rank_merge_equals_single_engine():
         assert r[4] == exp_tail
 
 
-def _cross_worker(rank, world, port, q):
-    """Rank 1's batch has a span whose parentId is a span of rank 0's shard."""
+def _crossing_batches(case, world):
+    """Per rank: the host batch of its traces, with the span-id map crossing
+    shards as ``case`` says -- "parent": rank 1 has a span whose parentId is a
+    span of rank 0's shard; "repeat": the last rank reuses one span id of rank
+    0's shard (a leaf SERVER span: no parent link crosses); "inner": the last
+    rank repeats one of its own span ids (its run takes the span-table path);
+    "none": clean shards."""
+    from kmamiz_amd import synth
+
+    ntr = 900 if case != "parent" else 700
+    cut = [ntr * r // world for r in range(world + 1)] if case != "parent" else [0, 300, 700][: world + 1]
+    out = []
+    b0, _ = synth.host_batch(synth.MESH, cut[0], cut[1])
+    for rank in range(world):
+        batch, _ = synth.host_batch(synth.MESH, cut[rank], cut[rank + 1])
+        if case == "parent" and rank == 1:
+            roots = np.nonzero(batch.parent_id == 0)[0]
+            batch.parent_id[roots[3]] = b0.span_id[10]  # a parent on the other shard
+        if case in ("repeat", "inner") and rank == world - 1:
+            kids = set(batch.parent_id.tolist())
+            leaf = next(i for i in range(len(batch)) if batch.kind[i] == 1 and int(batch.span_id[i]) not in kids)
+            batch.span_id[leaf] = b0.span_id[len(b0) - 1] if case == "repeat" else batch.span_id[leaf - 7]
+        out.append(batch)
+    return out
+
+
+def _crossing_worker(rank, world, port, q, case, exact):
     import torch
     import torch.distributed as dist
 
@@ -110,15 +135,9 @@ def _cross_worker(rank, world, port, q):
         from kmamiz_amd import dist as kdist
         from kmamiz_amd import synth
 
-        cut = [0, 300, 700]
-        table = synth.shape_table(synth.MESH)
-        b0, _ = synth.host_batch(synth.MESH, cut[0], cut[1])
-        batch, _ = synth.host_batch(synth.MESH, cut[rank], cut[rank + 1])
-        if rank == 1:
-            roots = np.nonzero(batch.parent_id == 0)[0]
-            batch.parent_id[roots[3]] = b0.span_id[10]  # a parent on the other shard
+        batch = _crossing_batches(case, world)[rank]
         e = Engine(0)
-        e.load(batch, table)
+        e.load(batch, synth.shape_table(synth.MESH))
         e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
         gw, ew, tw = (e.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
         g = torch.zeros(gw, dtype=torch.int64)
@@ -127,98 +146,96 @@ def _cross_worker(rank, world, port, q):
         e.export_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
         e.export_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
         e.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, False)
-        nu = e.unresolved_parents()
         try:
-            kdist.merge_all(g, gw // 6, ep, ew // 2, t[:tw], engine=e)
-            q.put((rank, nu, "merged"))
+            kdist.merge_all(g, gw // 6, ep, ew // 2, t[:tw], engine=e, exact=exact)
         except kdist.ShardingError:
-            q.put((rank, nu, "refused"))
+            q.put((rank, "refused", None, None, None))
+            return
+        e.import_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
+        e.import_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
+        e.finalize()
+        groups, keys, eps = e.fetch()
+        q.put((rank, "merged", groups.tobytes(), np.sort(keys).tobytes(), eps.tobytes()))
         e.close()
-    except Exception as ex:  # surfaced by the parent
-        q.put((rank, -1, repr(ex)))
+    except Exception:  # surfaced by the parent
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None, None))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.gpu
-def test_cross_shard_parent_is_refused():
-    """a parent link across shards would be joined by the
-    reference's global span map; merge_all's guard finds it on both ranks."""
+def _run_crossing(case, world, exact=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_cross_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_crossing_worker, args=(r, world, port, q, case, exact)) for r in range(world)]
     for p in ps:
         p.start()
-    res = sorted(q.get(timeout=180) for _ in range(2))
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
     for p in ps:
         p.join(timeout=60)
-    assert res[0] == (0, 0, "refused"), res
-    assert res[1] == (1, 1, "refused"), res
+    return res
 
 
-def _repeat_worker(rank, world, port, q, repeat):
-    """The last rank's batch reuses one span id of rank 0's shard (a leaf
-    SERVER span, so no parent link crosses shards)."""
-    import torch
-    import torch.distributed as dist
+def _whole_batch_expected(case, world):
+    """One engine over the whole batch (the reference's single global span
+    map), and the C oracle's edge keys and endpoints of the same batch."""
+    from kmamiz_amd import Engine, SpanBatch
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+    from oracle import c_oracle
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parts = _crossing_batches(case, world)
+    cols = {f: np.concatenate([getattr(b, f) for b in parts]) for f in ("span_id", "parent_id", "kind", "shape",
+                                                                      "status", "duration", "timestamp")}
+    whole = SpanBatch(index_base=0, **cols)
+    table = synth.shape_table(synth.MESH)
+    e = Engine(0)
     try:
-        from kmamiz_amd import Engine
-        from kmamiz_amd import _lib as L
-        from kmamiz_amd import dist as kdist
-        from kmamiz_amd import synth
-
-        ntr = 900
-        cut = [ntr * r // world for r in range(world + 1)]
-        table = synth.shape_table(synth.MESH)
-        b0, _ = synth.host_batch(synth.MESH, 0, 1)
-        batch, _ = synth.host_batch(synth.MESH, cut[rank], cut[rank + 1])
-        if repeat and rank == world - 1:
-            kids = set(batch.parent_id.tolist())
-            leaf = next(i for i in range(len(batch)) if batch.kind[i] == 1 and int(batch.span_id[i]) not in kids)
-            batch.span_id[leaf] = b0.span_id[len(b0) - 1]
-        e = Engine(0)
-        e.load(batch, table)
+        e.load(whole, table)
         e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
-        gw, ew, tw = (e.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
-        g = torch.zeros(gw, dtype=torch.int64)
-        ep = torch.zeros(ew, dtype=torch.int64)
-        t = torch.zeros(max(1, tw), dtype=torch.int64)
-        e.export_partials(L.PART_GROUPS, g.data_ptr(), gw, False)
-        e.export_partials(L.PART_ENDPOINTS, ep.data_ptr(), ew, False)
-        e.export_partials(L.PART_TRIPLES, t.data_ptr(), tw, False)
-        try:
-            kdist.merge_all(g, gw // 6, ep, ew // 2, t[:tw], engine=e)
-            q.put((rank, "merged"))
-        except kdist.ShardingError:
-            q.put((rank, "refused"))
-        e.close()
-    except Exception as ex:  # surfaced by the parent
-        q.put((rank, repr(ex)))
+        g, k, ep = e.fetch()
+        exp = (g.tobytes(), np.sort(k).tobytes(), ep.tobytes())
     finally:
-        dist.destroy_process_group()
+        e.close()
+    okeys, oep, _ = c_oracle.deps(whole, table.dep_ep, table.n_dep_ep)
+    return exp, okeys, oep
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_cross_shard_repeated_span_id_is_refused(world):
-    """SURVEY.md 8e's global duplicate check: a span id present in two shards
-    (Traces.ts:117-123 keeps one row for it) makes merge_all refuse on every
-    rank; the same shards without the repeat merge."""
-    for repeat, want in ((False, "merged"), (True, "refused")):
-        ctx = mp.get_context("spawn")
-        q = ctx.Queue()
-        port = _port()
-        ps = [ctx.Process(target=_repeat_worker, args=(r, world, port, q, repeat)) for r in range(world)]
-        for p in ps:
-            p.start()
-        res = sorted(q.get(timeout=180) for _ in range(world))
-        for p in ps:
-            p.join(timeout=60)
-        assert [r[1] for r in res] == [want] * world, res
+@pytest.mark.parametrize("case,world", [("parent", 2), ("repeat", 2), ("repeat", 3), ("inner", 2)])
+def test_crossing_shards_merge_exactly(case, world):
+    """SURVEY.md 8e / Traces.ts:117-143: the reference keys ONE Map by span id
+    over the whole batch, so a parent in another shard, an id in two shards or
+    an id repeated inside one shard changes rows and edges that per-shard runs
+    cannot see.  merge_all's guards find it on every rank and the merge stays
+    exact (one unsharded dependency pass on rank 0, broadcast): every rank ends
+    with the single-engine result over the whole batch, bit for bit, whose
+    edges and endpoints equal the C oracle's."""
+    res = _run_crossing(case, world)
+    for r in res:
+        assert r[1] == "merged", r[1]
+    exp, okeys, oep = _whole_batch_expected(case, world)
+    assert np.array_equal(np.frombuffer(exp[1], np.uint64), okeys)
+    from kmamiz_amd import _lib as L
+
+    eps = np.frombuffer(exp[2], L.ENDPOINT_DTYPE)
+    assert np.array_equal(eps["has_row"] != 0, oep["has_row"])
+    assert np.array_equal(eps["first_row"][oep["has_row"]], oep["first"][oep["has_row"]])
+    for r in res:
+        assert r[2] == exp[0]
+        assert r[3] == exp[1]
+        assert r[4] == exp[2]
+
+
+@pytest.mark.gpu
+def test_crossing_shards_refused_without_exact():
+    """exact=False keeps the old contract: every rank raises ShardingError
+    (and a clean batch merges either way)."""
+    assert [r[1] for r in _run_crossing("parent", 2, exact=False)] == ["refused"] * 2
+    assert [r[1] for r in _run_crossing("repeat", 3, exact=False)] == ["refused"] * 3
+    assert [r[1] for r in _run_crossing("none", 2, exact=False)] == ["merged"] * 2
 
 
 # ---------------------------------------------------------------------------
