@@ -216,13 +216,26 @@ def main():
         is_5xx = np.array([str(x).startswith("5") for x in synth.STATUSES[:n_status]], dtype=bool)
         eng.set_service_map(tag_sid, len(sid_names), is_5xx)  # the groups' services, for kmz_service_sums
 
+    phases = {}  # (KMZ_BENCH_TRACE: host wall time per step phase)
+
+    def mark(name, t):
+        now = time.perf_counter()
+        phases[name] = phases.get(name, 0.0) + (now - t)
+        return now
+
     def service_tail():
+        tp = time.perf_counter()
         t = run_tail(eng, tmaps)  # reads the edge keys where the run left them, in HBM
+        tp = mark("tail_run", tp)
         state["metrics"] = t.metrics()
+        tp = mark("tail_metrics", tp)
         # RiskAnalyzer.RealtimeRisk: the per-service sums over the combined
         # groups on the device (kmz_service_sums, bit-equal to the host's row
         # sums), the rest over the ~10^3 services on the host
-        state["risk"] = realtime_risk_from_sums(t, sid_names, *eng.service_sums())
+        sums = eng.service_sums()
+        tp = mark("service_sums", tp)
+        state["risk"] = realtime_risk_from_sums(t, sid_names, *sums)
+        mark("risk", tp)
 
     def step():
         # N > 1: the repeated-span-id guard routes this batch's ids and posts
@@ -230,7 +243,9 @@ def main():
         tg = time.perf_counter()
         guard = kdist.IdGuard(eng, dev).start() if world > 1 else None
         state["guard_start_s"] = state.get("guard_start_s", 0.0) + (time.perf_counter() - tg)
+        tp = time.perf_counter()
         eng.run(flags)
+        tp = mark("run", tp)
         if world > 1:
             gw = eng.partials_words(L.PART_GROUPS)
             ew = eng.partials_words(L.PART_ENDPOINTS)
@@ -252,6 +267,7 @@ def main():
         elif not args.no_fetch:  # the three result sets, one synchronisation (with the tail
             # on, the edge keys stay in HBM for kmz_tail_run: the service tail is the output)
             state["groups"], state["keys"], state["endpoints"] = eng.fetch(keys=not tail_on)
+            mark("fetch", tp)
         if tail_on:
             service_tail()
 
@@ -269,6 +285,7 @@ def main():
 
     barrier()
     state["guard_start_s"] = 0.0
+    phases.clear()
     t0 = time.perf_counter()
     marks = []
     for _ in range(args.steps):
@@ -278,6 +295,7 @@ def main():
     t1 = time.perf_counter()
     if os.environ.get("KMZ_BENCH_TRACE"):  # diagnostic: per-step wall times
         print("step ms:", [round((b - a) * 1e3, 3) for a, b in zip([t0] + marks, marks + [t1])], file=sys.stderr)
+        print("phase ms/step:", {k: round(v / args.steps * 1e3, 4) for k, v in phases.items()}, file=sys.stderr)
     eng.set_profiling(False)
     ktimes = eng.kernel_times(reset=True)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev if world > 1 else "cpu")

@@ -704,9 +704,8 @@ static int run_join(kmz_ctx *c, bool *ok) {
   // size; bit 7: never, for comparison)
   if (n == 0 || !cert_plan(n, &pl, !(c->ablate2 & 128u), (c->ablate2 & 64u) != 0) || c->table_hint || (c->ablate & 32))
     return KMZ_OK;
-  const size_t nsub = (size_t)1 << (pl.B1 + pl.B2);
   if (ensure(c, c->dp, (size_t)(n + 1) * 4) || ensure(c, c->cpool1, cert_pool1_words(n) * 8) ||
-      ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) ||
+      ensure(c, c->cpool2, cert_pool2_bytes(pl)) || ensure(c, c->ccur, cert_cur_words(pl) * 4) ||
       ensure(c, c->cdir, cert_dir_entries(n, pl) * 2))
     return KMZ_E_HIP;
   unsigned int *cnt = P<unsigned int>(c->counters);
@@ -715,7 +714,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
   {
     Timed t(c, KMZ_K_MEMSET);
     FillArgs f;
-    f.add(cur2, nsub * 4, 0);
+    f.add(cur2, cert_cur_words(pl) * 4, 0);
     f.add(c->mkey.p, (size_t)c->mcap * 8, 0);
     f.add(c->mval.p, (size_t)c->mcap * 4, 0xFF);  // ids not in the batch: NONE
     launch_fill(c->stream, f);
@@ -832,22 +831,23 @@ static int run_shape_stats(kmz_ctx *c) {
     const bool bal = S > 1 && !(c->ablate & (1u << 14));
     const uint32_t Sd = bal ? 1u : S;  // the directory's slices ([partition][tile] for the balanced reduce)
     if (ensure(c, c->k3pool, k3_pool_bytes(n)) || ensure(c, c->k3dir, (k3_dir_words(n, Pp, Sd) + k3_plan_words(Pp) + 1) * 4) ||
-        ensure(c, c->k3part, bal ? k3_bal_part_bytes((uint32_t)Gs) : (size_t)S * 6 * Gs * 8) ||
+        ensure(c, c->k3part, bal ? k3_bal_part_bytes((uint32_t)Gs) : k3_slice_part_bytes((uint32_t)Gs, S)) ||
         ensure(c, c->tile_tmp, (size_t)nt * 16))
       return KMZ_E_HIP;
     {
       Timed t(c, KMZ_K_STATS);
       launch_k3_produce(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_shapes,
-                        c->n_status, Sd, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp));
+                        c->n_status, Sd, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp),
+                        c->index_base, E + 5 * Gs);
     }
     {
       Timed t(c, KMZ_K_REDUCE);
       if (bal)
-        launch_k3_reduce_bal(c->stream, n, (uint32_t)Gs, c->index_base, c->k3pool.p, P<uint32_t>(c->k3dir),
+        launch_k3_reduce_bal(c->stream, n, (uint32_t)Gs, E + 5 * Gs, c->k3pool.p, P<uint32_t>(c->k3dir),
                              P<uint32_t>(c->k3dir) + k3_dir_words(n, Pp, 1), P<unsigned long long>(c->k3part), sg,
                              (c->ablate & (1u << 15)) != 0);  // (bit 15, test knob: unpacked accumulators)
       else
-        launch_k3_reduce(c->stream, n, (uint32_t)Gs, c->index_base, c->k3pool.p, P<uint32_t>(c->k3dir),
+        launch_k3_reduce(c->stream, n, (uint32_t)Gs, E + 5 * Gs, c->k3pool.p, P<uint32_t>(c->k3dir),
                          P<unsigned long long>(c->k3part), S, sg);
       launch_k3_escapes(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_status,
                         c->index_base, c->k3pool.p, cnt, E, (uint32_t)Gs, sg);
@@ -916,7 +916,6 @@ static int run_fused(kmz_ctx *c, bool links) {
   CertPlan pl;  // (the plan fused_eligible accepted: same arguments)
   if (!cert_plan(n, &pl, true, (c->ablate2 & 64u) != 0) || pl.B1 != 6)
     return fail(c, KMZ_E_STATE, "fused join + walk: certificate plan is not the kernel's 2^6 pass-1 binning");
-  const size_t nsub = (size_t)1 << (pl.B1 + pl.B2);
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
   unsigned long long *st = P<unsigned long long>(c->stats64);
@@ -939,7 +938,7 @@ static int run_fused(kmz_ctx *c, bool links) {
     return fail(c, KMZ_E_ARG, "fused join + walk: list sizes past 2^32");
   void *old_ctab = c->ctab.p;
   if (ensure(c, c->dp, (size_t)(n + 1) * 4) || ensure(c, c->cpool1, cert_pool1_words(n) * 8) ||
-      ensure(c, c->cpool2, nsub * pl.cap2 * 8) || ensure(c, c->ccur, nsub * 4) ||
+      ensure(c, c->cpool2, cert_pool2_bytes(pl)) || ensure(c, c->ccur, cert_cur_words(pl) * 4) ||
       ensure(c, c->cdir, cert_dir_entries(n, pl) * 2) || ensure(c, c->mkey, (size_t)c->mcap * 8) ||
       ensure(c, c->mval, (size_t)c->mcap * 4) || ensure(c, c->ctab, c->ccap * CHAIN_ENTRY_BYTES) ||
       ensure(c, c->ctile, (size_t)chain_tiles(n) * 16) || ensure(c, c->plist, (size_t)(n + 1) * 4) ||
@@ -952,7 +951,7 @@ static int run_fused(kmz_ctx *c, bool links) {
   {
     Timed t(c, KMZ_K_MEMSET);
     FillArgs f;
-    f.add(cur2, nsub * 4, 0);
+    f.add(cur2, cert_cur_words(pl) * 4, 0);
     f.add(c->mkey.p, (size_t)c->mcap * 8, 0);
     f.add(c->mval.p, (size_t)c->mcap * 4, 0xFF);  // ids not in the batch: NONE
     if (c->ctab_dirty) f.add(c->ctab.p, c->ccap * CHAIN_ENTRY_BYTES, 0);
@@ -2293,12 +2292,12 @@ int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32
   if (n >= 0xFFFFFFFFull || !cert_plan((uint32_t)n, &pl, false))  // (k_cert_bin bins by 2^6)
     return fail(c, KMZ_E_UNSUPPORTED, "too many values for the certificate: check on the host");
   const uint32_t m = (uint32_t)n;
-  const size_t nsub = (size_t)1 << (pl.B1 + pl.B2);
   // (the guard's own certificate buffers: reusing the run's would resize them
   // between runs, changing the run's addresses -- and its hipGraph key -- every
   // multi-GPU step)
   if (ensure(c, c->rt_pool1, cert_pool1_words(m) * 8) || ensure(c, c->rt_dir, cert_dir_entries(m, pl) * 2) ||
-      ensure(c, c->rt_pool2, nsub * pl.cap2 * 8) || ensure(c, c->rt_cur, nsub * 4) || ensure(c, c->rt_ctr, C_COUNT * 4))
+      ensure(c, c->rt_pool2, cert_pool2_bytes(pl)) || ensure(c, c->rt_cur, cert_cur_words(pl) * 4) ||
+      ensure(c, c->rt_ctr, C_COUNT * 4))
     return KMZ_E_HIP;
   const unsigned long long *src = reinterpret_cast<const unsigned long long *>(vals);
   if (mem != KMZ_MEM_DEVICE) {
@@ -2309,7 +2308,7 @@ int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32
   unsigned int *cnt = P<unsigned int>(c->rt_ctr);
   unsigned int *cur2 = P<unsigned int>(c->rt_cur);
   HIPCHK(c, hipMemsetAsync(cnt, 0, C_COUNT * 4, c->stream));
-  HIPCHK(c, hipMemsetAsync(cur2, 0, nsub * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(cur2, 0, cert_cur_words(pl) * 4, c->stream));
   launch_cert_bin(c->stream, src, m, P<unsigned long long>(c->rt_pool1), P<uint16_t>(c->rt_dir));
   launch_cert_split(c->stream, m, P<unsigned long long>(c->rt_pool1), P<uint16_t>(c->rt_dir), pl,
                     P<unsigned long long>(c->rt_pool2), cur2, cnt);

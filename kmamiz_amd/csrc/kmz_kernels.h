@@ -82,16 +82,20 @@ void launch_synth_fill(hipStream_t s, int config, uint64_t seed, uint64_t t0, ui
 void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
                        const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
                        uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint32_t S, unsigned int *counters,
-                       unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp);
+                       unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp,
+                       uint64_t index_base, unsigned long long *first);
 // balanced K3 reduce (directory [partition][tile], i.e. produced with S = 1):
 // plan = k3_plan_words(P) u32 scratch, part = k3_bal_part_bytes(G)
-void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
+void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, const unsigned long long *first, const void *pool,
                           const uint32_t *dir, uint32_t *plan, unsigned long long *part, unsigned long long *grp,
                           bool unpacked = false);
 uint32_t k3_bal_items(uint32_t G);
 uint32_t k3_plan_words(uint32_t P);
 uint64_t k3_bal_part_bytes(uint32_t G);
-void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, uint64_t index_base, const void *pool,
+uint64_t k3_slice_part_bytes(uint32_t G, uint32_t S);
+// `first`: the groups' first indices, kept by produce (the escape block's
+// first-index words)
+void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, const unsigned long long *first, const void *pool,
                       const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp);
 // small key spaces (G <= 1024): per-chunk LDS partials, part = [k3_small_blocks(n)][6][G] u64
 uint32_t k3_small_blocks(uint32_t n);
@@ -227,7 +231,14 @@ void launch_remap_index(hipStream_t s, unsigned long long *v, uint64_t n, uint32
 // window parent join + uniqueness certificate (kmz_join.hip)
 struct CertPlan {
   uint32_t B1, B2, cap2, chunks;  // 2^B1 pass-1 bins, 2^B2 sub-bins per bin
+  // past 2^29 ids a single pass 2 would write runs of ~2 records: pass 2 then
+  // splits into 2^B2 and a second split pass into 2^B3 more (0: no third level)
+  uint32_t B3 = 0, cap3 = 0, chunks3 = 0;
 };
+// the certificate's pass-2 pool (bytes: level 2, then level 3) and sub-bin
+// counters (u32 words) for a plan
+uint64_t cert_pool2_bytes(const CertPlan &pl);
+uint64_t cert_cur_words(const CertPlan &pl);
 // wide: pass 1 may use 2^8 bins (the window join; the guard's k_cert_bin
 // always bins by 2^6); force_wide: 2^8 bins at any size (test knob)
 bool cert_plan(uint32_t n, CertPlan *pl, bool wide = true, bool force_wide = false);
