@@ -310,6 +310,11 @@ int kmz_set_triples(kmz_ctx *ctx, const uint64_t *keys, uint64_t n, int mem);
 int kmz_finalize(kmz_ctx *ctx);
 /* host-side finalisation of one partial (same arithmetic as the device) */
 void kmz_finalize_host(const uint64_t *partials, uint64_t n_groups, kmz_group *out);
+/* out[i] = exp(in[i]) by the C library's exp, element by element: the host
+ * finish of RiskAnalyzer's SigmoidAdj (Normalizer.ts:32-41) over the services
+ * in one call instead of one interpreter call per service (the same libm exp
+ * Python's math.exp calls, so the results are bit-identical) */
+void kmz_host_exp(const double *in, double *out, uint64_t n);
 
 /* ---- multi-GPU sharding guard ---------------------------- */
 /* Sharding by whole traces equals the reference's global span map

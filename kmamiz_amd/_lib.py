@@ -192,6 +192,7 @@ SIGNATURES = [
     ("kmz_service_sums", C.c_int, [_P, _P, C.c_uint64]),
     ("kmz_finalize", C.c_int, [_P]),
     ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
+    ("kmz_host_exp", None, [_P, _P, C.c_uint64]),
     ("kmz_host_alloc", _P, [C.c_uint64]),
     ("kmz_host_free", None, [_P]),
     ("kmz_set_profiling", C.c_int, [_P, C.c_int]),

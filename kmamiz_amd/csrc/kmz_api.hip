@@ -84,11 +84,11 @@ struct kmz_ctx {
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
   // service tail (kmz_tail.hip): maps, link set, detail table, pair set, pair table, outputs
   DevBuf tl_svc, tl_cls, tl_lsvc, tl_lset, tl_akey, tl_aval, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs,
-      tl_cnt, tl_fkey, tl_fval, tl_sstat, tl_rel;
+      tl_cnt, tl_fkey, tl_fval, tl_sstat, tl_rel, tl_lbkt, tl_lbn;
   uint32_t tl_n_ep = 0, tl_n_cls = 0, tl_n_svc = 0, tl_n_dist = 64, tl_deep = 0;
   uint32_t tl_rel_dist = 0;  // distances in the last run's relying table (0: not complete, use the details)
   bool tl_map = false, tl_ran = false;
-  uint64_t tl_acap = 0, tl_pacap = 0, tl_lcap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0;
+  uint64_t tl_acap = 0, tl_pacap = 0, tl_lcap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0, tl_bcap = 0;
   DevBuf tl_sfirst;              // per service: first row (k_tail_service_rows)
   void *tl_host = nullptr;       // pinned: the tail's counters, per-service stats, relying table, first rows
   size_t tl_host_bytes = 0;
@@ -346,7 +346,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
-                    &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
+                    &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->tl_lbkt, &c->tl_lbn, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
                     &c->o_key, &c->o_val, &c->o_out,
                     &c->o_rts, &c->o_rsh, &c->j_buf, &c->j_elem, &c->j_state, &c->j_jsc, &c->j_mask,
                     &c->j_cnt, &c->j_off, &c->j_csc, &c->j_small, &c->j_starts, &c->j_slices, &c->j_tslot,
@@ -837,18 +837,19 @@ static int run_shape_stats(kmz_ctx *c) {
     {
       Timed t(c, KMZ_K_STATS);
       launch_k3_produce(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_shapes,
-                        c->n_status, Sd, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp),
-                        c->index_base, E + 5 * Gs);
+                        c->n_status, Sd, cnt, nsrv, c->k3pool.p, P<uint32_t>(c->k3dir), P<uint32_t>(c->tile_tmp));
     }
     {
       Timed t(c, KMZ_K_REDUCE);
       if (bal)
-        launch_k3_reduce_bal(c->stream, n, (uint32_t)Gs, E + 5 * Gs, c->k3pool.p, P<uint32_t>(c->k3dir),
+        launch_k3_reduce_bal(c->stream, n, (uint32_t)Gs, c->k3pool.p, P<uint32_t>(c->k3dir),
                              P<uint32_t>(c->k3dir) + k3_dir_words(n, Pp, 1), P<unsigned long long>(c->k3part), sg,
                              (c->ablate & (1u << 15)) != 0);  // (bit 15, test knob: unpacked accumulators)
       else
-        launch_k3_reduce(c->stream, n, (uint32_t)Gs, E + 5 * Gs, c->k3pool.p, P<uint32_t>(c->k3dir),
+        launch_k3_reduce(c->stream, n, (uint32_t)Gs, c->k3pool.p, P<uint32_t>(c->k3dir),
                          P<unsigned long long>(c->k3part), S, sg);
+      launch_k3_first(c->stream, c->kind, c->shape, c->status, n, nullptr, c->n_shapes, c->n_status, c->index_base,
+                      (uint32_t)Gs, sg, cnt);
       launch_k3_escapes(c->stream, c->kind, c->shape, c->status, c->dur, c->ts, n, nullptr, c->n_shapes, c->n_status,
                         c->index_base, c->k3pool.p, cnt, E, (uint32_t)Gs, sg);
     }
@@ -2021,12 +2022,19 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
   // <= 1/2, cache-resident when the keys repeat), or by the worst case (two
   // link keys and one pair per edge key) on the first run; grown on overflow
   if (!c->tl_lcap) c->tl_lcap = pow2_at_least(4 * nt + 64);
+  // link-key buckets: two link keys per edge key at most, spread by a hash
+  // (mean + 25 % + 512 per bucket); grown on overflow
+  const uint32_t nbk = tail_buckets();
+  c->tl_bcap = std::max<uint64_t>(c->tl_bcap, (2 * nt / nbk) * 5 / 4 + 512);
   if (!c->tl_pcap) c->tl_pcap = pow2_at_least(2 * nt + 64);
   if (!c->tl_acap) c->tl_acap = pow2_at_least(nt / 2 + 4096);
   if (!c->tl_pacap) c->tl_pacap = pow2_at_least(nt / 4 + 4096);
   for (int attempt = 0;; ++attempt) {
     const uint64_t acap = c->tl_acap, pacap = c->tl_pacap, lcap = c->tl_lcap, pcap = c->tl_pcap;
-    if (ensure(c, c->tl_lset, lcap * 8) || ensure(c, c->tl_akey, acap * 8) || ensure(c, c->tl_aval, acap * 16) ||
+    const uint64_t bcap = c->tl_bcap;
+    if (bcap >= 0xFFFFFFFFull) return fail(c, KMZ_E_OVERFLOW, "service tail buckets");
+    if (ensure(c, c->tl_lbkt, bcap * nbk * 8) || ensure(c, c->tl_lbn, (size_t)nbk * 4) ||
+        ensure(c, c->tl_lset, lcap * 8) || ensure(c, c->tl_akey, acap * 8) || ensure(c, c->tl_aval, acap * 16) ||
         ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
         ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
         ensure(c, c->tl_fkey, acap * 8) || ensure(c, c->tl_fval, acap * 4) ||
@@ -2056,6 +2064,7 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       f.add(c->tl_pval.p, pacap * 4, 0);
       f.add(c->tl_hasin.p, c->tl_n_ep ? c->tl_n_ep : 1, 0);
       f.add(c->tl_cnt.p, 64, 0);
+      g.add(c->tl_lbn.p, (size_t)nbk * 4, 0);
       g.add(c->tl_fkey.p, acap * 8, 0);
       g.add(c->tl_fval.p, acap * 4, 0);
       if (c->tl_n_svc) {
@@ -2071,6 +2080,7 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       Timed t(c, KMZ_K_TAIL);
       launch_tail(c->stream, P<unsigned long long>(c->trip_out), st + S_TRIP_OUT, nt, P<uint32_t>(c->tl_svc),
                   P<uint32_t>(c->tl_cls), P<uint32_t>(c->tl_lsvc), P<uint32_t>(c->tl_svc), c->tl_n_ep, c->tl_n_cls,
+                  P<unsigned long long>(c->tl_lbkt), (uint32_t)bcap, P<uint32_t>(c->tl_lbn),
                   P<unsigned long long>(c->tl_lset), lcap, P<unsigned long long>(c->tl_akey), P<uint32_t>(c->tl_aval),
                   acap, P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey),
                   P<uint32_t>(c->tl_pval), pacap, P<uint8_t>(c->tl_hasin), P<unsigned long long>(c->tl_fkey),
@@ -2105,6 +2115,7 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       c->tl_pacap = std::max(c->tl_pacap * 4, pow2_at_least(nt / 4 + 4096));
       c->tl_lcap = std::max(c->tl_lcap * 4, pow2_at_least(4 * nt + 64));
       c->tl_pcap = std::max(c->tl_pcap * 4, pow2_at_least(2 * nt + 64));
+      c->tl_bcap *= 2;
       continue;
     }
     const uint64_t won_l = (uint32_t)h[4], won_p = (uint32_t)(h[4] >> 32);
@@ -2344,6 +2355,11 @@ void kmz_finalize_host(const uint64_t *p, uint64_t G, kmz_group *out) {
     finalize_moments(p[g], p[G + g], p[2 * G + g], p[3 * G + g], &r.mean, &r.cv);
     out[g] = r;
   }
+}
+
+void kmz_host_exp(const double *in, double *out, uint64_t n) {
+#pragma clang loop vectorize(disable)  // (the scalar libm exp: no vector math library)
+  for (uint64_t i = 0; i < n; ++i) out[i] = exp(in[i]);
 }
 
 void *kmz_host_alloc(uint64_t bytes) {

@@ -587,13 +587,9 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
 // Chain interning stages few keys (new chains only): k_chain_settle inserts
 // them in place, which is cheaper at that volume.
 constexpr uint32_t KP_T = 256, KP_PER = 16, KP_STEP = KP_T * KP_PER;  // 4096 keys per step
-// With KMZ_KP_DEDUP, a step's compact keys are first put in an 8192-slot LDS
-// set and the repeats dropped (a key that finds no slot in 16 probes, or
-// equals the empty marker, is kept: k_key_slice dedups whatever arrives)
-#ifndef KMZ_KP_DEDUP
-#define KMZ_KP_DEDUP 0
-#endif
-constexpr uint32_t KP_DSET = KMZ_KP_DEDUP ? 8192 : 1, KP_DEMPTY = 0xFFFFFFFFu;
+// (Measured and dropped: each step's keys first put in an 8192-slot LDS set
+// and the repeats dropped before the slice sort -- k_key_part + k_key_slice
+// 2.63 -> 3.10 ms on config 5: few repeats fall inside one 4096-key step.)
 
 // exclusive prefix sum of v[0..m) in LDS (m <= 4 * KP_T), by the whole workgroup
 __device__ __forceinline__ void kp_scan(uint32_t *__restrict__ v, uint32_t m, uint32_t *__restrict__ wsum) {
@@ -638,8 +634,6 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
   const KT *__restrict__ stage = static_cast<const KT *>(stage_v);
   KT *__restrict__ bucket = static_cast<KT *>(bucket_v);
   __shared__ KT sorted[KP_STEP];  // 32 KB (16 KB compact)
-  __shared__ uint32_t dset[C ? KP_DSET : 1];
-  constexpr bool DD = C && KMZ_KP_DEDUP;
   __shared__ uint32_t hist[1u << KB2_MAX], off[1u << KB2_MAX], base[1u << KB2_MAX], wsum[KP_T / 64];
   static_assert((1u << KB2_MAX) <= 4 * KP_T, "kp_scan covers the slices of a coarse bin");
   const uint32_t nf = 1u << lb2;
@@ -690,30 +684,11 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
     seek();
     load();  // (in flight during the LDS work below)
     for (uint32_t x = threadIdx.x; x < nf; x += KP_T) hist[x] = 0;
-    if (DD)
-      for (uint32_t x = threadIdx.x; x < KP_DSET; x += KP_T) dset[x] = KP_DEMPTY;
     __syncthreads();
     uint32_t f[KP_PER], rk[KP_PER];
-    bool keep[KP_PER];
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j) {
-      keep[j] = j * KP_T + threadIdx.x < nv;
-      if (DD && keep[j] && (uint32_t)k[j] != KP_DEMPTY) {
-        uint32_t h = ((uint32_t)k[j] * 0x9E3779B1u) >> 19;
-        for (uint32_t z = 0; z < 16; ++z) {
-          const uint32_t cur = atomicCAS(&dset[h], KP_DEMPTY, (uint32_t)k[j]);
-          if (cur == KP_DEMPTY) break;
-          if (cur == (uint32_t)k[j]) {
-            keep[j] = false;  // (an equal key of this step went first)
-            break;
-          }
-          h = (h + 1) & (KP_DSET - 1);
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < (int)KP_PER; ++j) {
-      const bool v = keep[j];
+      const bool v = j * KP_T + threadIdx.x < nv;
       f[j] = fine(k[j]);
       rk[j] = v ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
     }
@@ -727,7 +702,7 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
     kp_scan(off, nf, wsum);
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j)
-      if (keep[j]) sorted[off[f[j]] + rk[j]] = k[j];
+      if (j * KP_T + threadIdx.x < nv) sorted[off[f[j]] + rk[j]] = k[j];
     __syncthreads();
     // consecutive threads -> consecutive slots of one slice's bucket
     const uint32_t nz = off[nf - 1] + hist[nf - 1];

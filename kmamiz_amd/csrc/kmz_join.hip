@@ -26,9 +26,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <mutex>
-
-#include <algorithm>
 
 #include "kmz_joinw.h"
 
@@ -510,159 +507,6 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
 }
 
-// KMZ_CERT_PERSIST=1: the persistent pass 2 below (A/B variant; 104 VGPRs at
-// 1024 threads: one workgroup per CU, whose next chunk's gather overlaps the
-// current chunk's work)
-#ifndef KMZ_CERT_PERSIST
-#define KMZ_CERT_PERSIST 0
-#endif
-// pass 2: for one bin, the runs of TPC tiles (a chunk of <= CERT_CHUNK
-// records) -> 2^B2 sub-bins (dynamic LDS: CERT_CHUNK u64 staging + 2 * 2^B2
-// u32).  Persistent: a workgroup takes the items (bin, chunk) blockIdx.x,
-// + gridDim.x, ...; the next item's directory is read and its records are
-// gathered into registers before the current item is ranked, reserved,
-// staged and written, so the gather's latency overlaps that work.  (Reserving
-// four sub-bins per 64-bit atomic, as 16-bit fields, measured 0.59 against
-// 0.57 ms on config 3: the per-sub-bin reservations are not what bounds this
-// pass.  PQ = 16, i.e. runs twice as long per sub-bin, measured slower: 0.59
-// against 0.55 ms.)  With 2^8 pass-1 bins (B1 = 8, batches past ~10^8 ids) a
-// chunk takes 4x the tiles (tile runs of ~8 records).  A record finds its tile
-// run by a binary search over the run starts.
-constexpr uint32_t CS_T = 1024;  // threads of a pass-2 workgroup
-template <int PQ, uint32_t B1>
-__global__ void __launch_bounds__(CS_T) k_cert_split_p(const unsigned long long *__restrict__ pool1,
-                                                     const uint16_t *__restrict__ jdir, uint32_t n, uint32_t chunks,
-                                                     uint32_t B2, unsigned long long *__restrict__ pool2,
-                                                     uint32_t cap2, unsigned int *__restrict__ cur2,
-                                                     unsigned int *__restrict__ counters) {
-  constexpr uint32_t BINS = 1u << B1;
-  constexpr uint32_t CH = PQ * 1024, PER = CH / CS_T;
-  // ~32 ids per tile run at 64 bins, ~8 at 256
-  constexpr uint32_t TPC = (PQ * 24) << (B1 - CERT_B1);
-  static_assert(TPC <= 2 * CS_T && CH % CS_T == 0, "tile runs per thread");
-  extern __shared__ uint64_t dyn[];
-  __shared__ uint32_t wsum[16], tcnt[TPC], toff[TPC];
-  uint64_t *stg = dyn;
-  const uint32_t M = 1u << B2;  // (<= CS_T: cert_plan keeps B2 <= 9)
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(dyn + CH), *base = cnt + M;
-  const uint32_t ntiles = join_tiles(n), items = BINS * chunks;
-  const uint32_t sh = 64 - B1 - B2;
-  // item `it`'s tile runs: tcnt := each run's position in the chunk, toff :=
-  // its offset in its tile; returns the chunk's record count (every thread)
-  auto plan_item = [&](uint32_t it) -> uint32_t {
-    const uint32_t b = it / chunks, T0 = (it % chunks) * TPC;
-    const uint32_t nt = T0 < ntiles ? min(TPC, ntiles - T0) : 0;
-    for (uint32_t j = threadIdx.x; j < TPC; j += CS_T) {
-      uint32_t c = 0, o = 0;
-      if (it < items && j < nt) {
-        const uint32_t t = T0 + j;
-        const uint32_t tsize = min(JT, n - t * JT);
-        o = jdir[(uint64_t)t * BINS + b];
-        const uint32_t e = b + 1 < BINS ? jdir[(uint64_t)t * BINS + b + 1] : tsize;
-        c = e - o;
-      }
-      tcnt[j] = c;
-      toff[j] = o;
-    }
-    __syncthreads();
-    const uint32_t last = tcnt[TPC - 1];
-    block_scan_lds(tcnt, TPC, wsum);  // (ends with a barrier)
-    return tcnt[TPC - 1] + last;
-  };
-  // gather item `it`'s records (cn of them) into registers: every load in flight at once
-  auto gather = [&](uint32_t it, uint32_t cn, uint64_t(&h)[PER]) {
-    const uint32_t T0 = (it % chunks) * TPC, nt = T0 < ntiles ? min(TPC, ntiles - T0) : 0;
-#pragma unroll
-    for (int q = 0; q < (int)PER; ++q) {
-      const uint32_t e = q * CS_T + threadIdx.x;
-      h[q] = 0;
-      if (e < cn) {
-        uint32_t lo = 0;  // the last run starting at or before e (empty runs share the next one's start)
-#pragma unroll
-        for (uint32_t step = 512; step; step >>= 1)
-          if (lo + step < nt && tcnt[lo + step] <= e) lo += step;
-        h[q] = pool1[(uint64_t)(T0 + lo) * JT + toff[lo] + (e - tcnt[lo])];
-      }
-    }
-  };
-  uint32_t it = blockIdx.x;
-  uint32_t cn = plan_item(it);
-  if (cn > CH) {  // cannot happen for hashed ids short of ~20 sigma
-    if (threadIdx.x == 0) atomicOr(&counters[C_CERT], CERT_OVF);
-    cn = 0;
-  }
-  uint64_t h[PER], hn[PER];
-  gather(it, cn, h);
-  for (; it < items; it += gridDim.x) {
-    // the next item: directory, then its gather (in flight during this item's work)
-    for (uint32_t k = threadIdx.x; k < M; k += CS_T) cnt[k] = 0;  // (ordered by plan_item's barriers)
-    const uint32_t nx = it + gridDim.x;
-    uint32_t cnn = plan_item(nx);
-    if (cnn > CH) {
-      if (threadIdx.x == 0) atomicOr(&counters[C_CERT], CERT_OVF);
-      cnn = 0;
-    }
-    gather(nx, nx < items ? cnn : 0, hn);
-    const uint32_t b = it / chunks;
-    uint32_t rk[PER];
-#pragma unroll
-    for (int q = 0; q < (int)PER; ++q) {
-      const uint32_t e = q * CS_T + threadIdx.x;
-      rk[q] = e < cn ? atomicAdd(&cnt[(uint32_t)(h[q] >> sh) & (M - 1)], 1u) : 0;
-    }
-    __syncthreads();
-    // each sub-bin's global run, reserved with one device atomic; the returned
-    // base is stored to LDS only after the scan and the LDS scatter below, so
-    // the atomic's round trip overlaps them (barriers here wait for LDS only)
-    uint32_t rb = 0;
-    {
-      const uint32_t c = threadIdx.x < M ? cnt[threadIdx.x] : 0;
-      if (c) rb = atomicAdd(&cur2[(b << B2) | threadIdx.x], c);
-    }
-    block_scan_lds(cnt, M, wsum);  // cnt := local offsets (its first barrier orders the read above)
-#pragma unroll
-    for (int q = 0; q < (int)PER; ++q) {
-      const uint32_t e = q * CS_T + threadIdx.x;
-      if (e < cn) stg[cnt[(uint32_t)(h[q] >> sh) & (M - 1)] + rk[q]] = h[q];
-    }
-    if (threadIdx.x < M) base[threadIdx.x] = rb;
-    __syncthreads();
-    bool ovf = false;
-    for (uint32_t e = threadIdx.x; e < cn; e += CS_T) {
-      const uint64_t x = stg[e];
-      const uint32_t sb = (uint32_t)(x >> sh) & (M - 1);
-      const uint32_t pos = base[sb] + e - cnt[sb];
-      if (pos < cap2)
-        pool2[(uint64_t)((b << B2) | sb) * cap2 + pos] = x;
-      else
-        ovf = true;
-    }
-    if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
-    __syncthreads();  // (stg, cnt and base are reused by the next item)
-#pragma unroll
-    for (int q = 0; q < (int)PER; ++q) h[q] = hn[q];
-    cn = cnn;
-  }
-}
-
-// resident workgroups of a kernel (CUs x occupancy at `threads` and `lds`
-// bytes of dynamic LDS), queried once per device and kernel slot
-static uint32_t resident_grid(int slot, const void *fn, int threads, size_t lds, uint32_t fallback) {
-  static std::mutex mu;
-  static uint32_t cached[4][64] = {{0}};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return fallback;
-  std::lock_guard<std::mutex> lk(mu);
-  if (!cached[slot][dev]) {
-    int cus = 0, occ = 0;
-    cached[slot][dev] = fallback;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, threads, lds) == hipSuccess && occ > 0)
-      cached[slot][dev] = (uint32_t)cus * (uint32_t)occ;
-  }
-  return cached[slot][dev];
-}
-
 // pass 2b (past 2^29 ids): each level-2 sub-bin, CERT_CHUNK records at a
 // time, split again by the next B3 hash bits.  A single pass 2 into the
 // 2^12 sub-bins 10^9 ids need wrote runs of ~2 records per chunk and sub-bin
@@ -738,88 +582,79 @@ constexpr uint32_t CK_OVF = 1024;           // overflow ids (8 KB)
 constexpr int CCT = 512;                    // threads per pass-3 workgroup (two per CU)
 constexpr int CK_PER = 12;                  // ids per thread: sub-bins <= CCT * CK_PER = 6144 (cert_plan)
 static_assert(CCT * CK_PER >= CERT_SET * 3 / 4, "a sub-bin must fit the workgroup's registers");
-// Persistent: a workgroup takes sub-bins sb, sb + gridDim.x, ... and loads the
-// next sub-bin's ids into registers while it checks the current one (the
-// one-sub-bin-per-workgroup form waited on its loads with nothing to overlap
-// them).
+// (A persistent form that loads the next sub-bin's ids while checking the
+// current one measured slower: 0.31 against 0.275 ms on config 3.)
 __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__restrict__ pool, uint32_t cap,
-                                                   const unsigned int *__restrict__ cur, uint32_t nsb,
+                                                   const unsigned int *__restrict__ cur, uint32_t cur_stride,
                                                    unsigned int *__restrict__ counters) {
   __shared__ ulonglong2 bkt2[CK_NB * CK_S / 2];
   __shared__ uint32_t bcnt[CK_NB];
   __shared__ unsigned long long ovf[CK_OVF];
   __shared__ uint32_t novf;
   unsigned long long *bkt = reinterpret_cast<unsigned long long *>(bkt2);
-  bool dup = false, lost = false;
-  uint64_t hn[CK_PER];
-  auto load = [&](uint32_t sb) {
-    const uint32_t m = sb < nsb ? min(cur[sb], cap) : 0;
-    const unsigned long long *src = pool + (uint64_t)min(sb, nsb - 1) * cap;
+  const uint32_t sb = blockIdx.x;
+  const uint32_t m = min(cur[(uint64_t)sb * cur_stride], cap);
+  if (m == 0) return;
+  const unsigned long long *src = pool + (uint64_t)sb * cap;
+  uint64_t h[CK_PER];
 #pragma unroll
-    for (int q = 0; q < CK_PER; ++q) {
-      const uint32_t e = q * CCT + threadIdx.x;
-      hn[q] = e < m ? src[e] : 0;
+  for (int q = 0; q < CK_PER; ++q) {  // every load in flight while the counters are cleared
+    const uint32_t e = q * CCT + threadIdx.x;
+    h[q] = e < m ? src[e] : 0;
+  }
+  for (uint32_t k = threadIdx.x; k < CK_NB; k += CCT) bcnt[k] = 0;
+  if (threadIdx.x == 0) novf = 0;
+  __syncthreads();
+  bool lost = false;
+#pragma unroll
+  for (int q = 0; q < CK_PER; ++q) {
+    if (h[q] == 0) continue;  // padding (and cert_hash(0) == 0: span id 0, reported as F_ZERO_ID)
+    const uint32_t b = (uint32_t)h[q] & (CK_NB - 1);
+    const uint32_t slot = atomicAdd(&bcnt[b], 1u);
+    if (slot < CK_S) {
+      bkt[b * CK_S + slot] = h[q];
+    } else {
+      const uint32_t o = atomicAdd(&novf, 1u);
+      if (o < CK_OVF) ovf[o] = h[q];
+      else lost = true;
     }
-  };
-  load(blockIdx.x);
-  for (uint32_t sb = blockIdx.x; sb < nsb; sb += gridDim.x) {
-    uint64_t h[CK_PER];
+  }
+  __syncthreads();
+  bool dup = false;
+  // pairs within each bucket's slots
+  for (uint32_t b = threadIdx.x; b < CK_NB; b += CCT) {
+    const uint32_t c = min(bcnt[b], CK_S);
+    if (c < 2) continue;
+    uint64_t x[CK_S];
+    // a bucket is 64 B (16 banks): read in lane order, lanes b, b+4, b+8,
+    // b+12 of a 16-lane group would hit the same four banks (4-way conflict on
+    // every ds_read_b128); rotating each lane's start by b/4 spreads a group
+    // over all 64 banks.  (Slot order does not matter to the pair test.)
+    const uint32_t rot = (b >> 2) & 3;
 #pragma unroll
-    for (int q = 0; q < CK_PER; ++q) h[q] = hn[q];
-    load(sb + gridDim.x);  // (in flight during this sub-bin's check)
-    for (uint32_t k = threadIdx.x; k < CK_NB; k += CCT) bcnt[k] = 0;
-    if (threadIdx.x == 0) novf = 0;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < CK_PER; ++q) {
-      if (h[q] == 0) continue;  // padding (and cert_hash(0) == 0: span id 0, reported as F_ZERO_ID)
-      const uint32_t b = (uint32_t)h[q] & (CK_NB - 1);
-      const uint32_t slot = atomicAdd(&bcnt[b], 1u);
-      if (slot < CK_S) {
-        bkt[b * CK_S + slot] = h[q];
-      } else {
-        const uint32_t o = atomicAdd(&novf, 1u);
-        if (o < CK_OVF) ovf[o] = h[q];
-        else lost = true;
-      }
+    for (uint32_t j = 0; j < CK_S; j += 2) {
+      const uint32_t jj = (((j >> 1) + rot) & 3) << 1;
+      const ulonglong2 v = bkt2[(b * CK_S + jj) / 2];
+      x[j] = v.x;
+      x[j + 1] = v.y;
     }
-    __syncthreads();
-    // pairs within each bucket's slots
-    for (uint32_t b = threadIdx.x; b < CK_NB; b += CCT) {
-      const uint32_t c = min(bcnt[b], CK_S);
-      if (c < 2) continue;
-      uint64_t x[CK_S];
-      // a bucket is 64 B (16 banks): read in lane order, lanes b, b+4, b+8,
-      // b+12 of a 16-lane group would hit the same four banks (4-way conflict
-      // on every ds_read_b128); rotating each lane's start by b/4 spreads a
-      // group over all 64 banks.  (Slot order does not matter to the pair test.)
-      const uint32_t rot = (b >> 2) & 3;
+    // (x[] holds the slots in rotated order; slot s of the bucket is valid iff s < c)
+    bool ok[CK_S];
 #pragma unroll
-      for (uint32_t j = 0; j < CK_S; j += 2) {
-        const uint32_t jj = (((j >> 1) + rot) & 3) << 1;
-        const ulonglong2 v = bkt2[(b * CK_S + jj) / 2];
-        x[j] = v.x;
-        x[j + 1] = v.y;
-      }
-      // (x[] holds the slots in rotated order; slot s of the bucket is valid iff s < c)
-      bool ok[CK_S];
+    for (uint32_t j = 0; j < CK_S; ++j) ok[j] = (((((j >> 1) + rot) & 3) << 1) | (j & 1)) < c;
 #pragma unroll
-      for (uint32_t j = 0; j < CK_S; ++j) ok[j] = (((((j >> 1) + rot) & 3) << 1) | (j & 1)) < c;
+    for (uint32_t i = 0; i < CK_S; ++i)
 #pragma unroll
-      for (uint32_t i = 0; i < CK_S; ++i)
+      for (uint32_t j = i + 1; j < CK_S; ++j) dup |= ok[i] && ok[j] && x[i] == x[j];
+  }
+  // overflow ids: against their bucket's slots and the later overflow ids
+  const uint32_t no = min(novf, CK_OVF);
+  for (uint32_t o = threadIdx.x; o < no; o += CCT) {
+    const uint64_t v = ovf[o];
+    const uint32_t b = (uint32_t)v & (CK_NB - 1);
 #pragma unroll
-        for (uint32_t j = i + 1; j < CK_S; ++j) dup |= ok[i] && ok[j] && x[i] == x[j];
-    }
-    // overflow ids: against their bucket's slots and the later overflow ids
-    const uint32_t no = min(novf, CK_OVF);
-    for (uint32_t o = threadIdx.x; o < no; o += CCT) {
-      const uint64_t v = ovf[o];
-      const uint32_t b = (uint32_t)v & (CK_NB - 1);
-#pragma unroll
-      for (uint32_t j = 0; j < CK_S; ++j) dup |= bkt[b * CK_S + j] == v;  // (a full bucket: all 8 slots written)
-      for (uint32_t t = o + 1; t < no; ++t) dup |= ovf[t] == v;
-    }
-    __syncthreads();  // (the next sub-bin clears and refills the buckets)
+    for (uint32_t j = 0; j < CK_S; ++j) dup |= bkt[b * CK_S + j] == v;  // (a full bucket: all 8 slots written)
+    for (uint32_t t = o + 1; t < no; ++t) dup |= ovf[t] == v;
   }
   if (dup) atomicOr(&counters[C_CERT], CERT_DUP);
   if (lost) atomicOr(&counters[C_CERT], CERT_OVF);
@@ -997,29 +832,13 @@ void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const 
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
                        const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters) {
   if (!n) return;
-  if (!KMZ_CERT_PERSIST) {
-    const size_t lds = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B2) * 4;
-    if (pl.B1 == CERT_B1W)
-      hipLaunchKernelGGL((k_cert_split<CERT_PQ, CERT_B1W>), dim3((1u << CERT_B1W) * pl.chunks), dim3(1024), lds, s,
-                         pool1, jdir, n, pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
-    else
-      hipLaunchKernelGGL((k_cert_split<CERT_PQ, CERT_B1>), dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir,
-                         n, pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
-  } else {
-  // (dynamic LDS sized for the largest M, so the occupancy query holds for every plan)
-  const size_t lds = CERT_PQ * 1024 * 8 + (size_t)2 * CS_T * 4;
-  if (pl.B1 == CERT_B1W) {
-    const uint32_t items = (1u << CERT_B1W) * pl.chunks;
-    const void *fn = (const void *)k_cert_split_p<CERT_PQ, CERT_B1W>;
-    hipLaunchKernelGGL((k_cert_split_p<CERT_PQ, CERT_B1W>), dim3(std::min(items, resident_grid(1, fn, CS_T, lds, 512))),
-                       dim3(CS_T), lds, s, pool1, jdir, n, pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
-  } else {
-    const uint32_t items = CERT_BINS * pl.chunks;
-    const void *fn = (const void *)k_cert_split_p<CERT_PQ, CERT_B1>;
-    hipLaunchKernelGGL((k_cert_split_p<CERT_PQ, CERT_B1>), dim3(std::min(items, resident_grid(2, fn, CS_T, lds, 512))),
-                       dim3(CS_T), lds, s, pool1, jdir, n, pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
-  }
-  }
+  const size_t lds = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B2) * 4;
+  if (pl.B1 == CERT_B1W)
+    hipLaunchKernelGGL((k_cert_split<CERT_PQ, CERT_B1W>), dim3((1u << CERT_B1W) * pl.chunks), dim3(1024), lds, s, pool1,
+                       jdir, n, pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
+  else
+    hipLaunchKernelGGL((k_cert_split<CERT_PQ, CERT_B1>), dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n,
+                       pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
   if (pl.B3) {  // level 3: after level 2 in the same pool and counter block
     const uint32_t n2 = 1u << (pl.B1 + pl.B2);
     const size_t lds3 = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B3) * 4;
@@ -1032,14 +851,11 @@ void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
                        const unsigned int *cur2, unsigned int *counters) {
   if (!n) return;
-  if (pl.B3) {
-    const uint32_t nsb = 1u << (pl.B1 + pl.B2 + pl.B3);
-    hipLaunchKernelGGL(k_cert_check, dim3(std::min(nsb, resident_grid(0, (const void *)k_cert_check, CCT, 0, 512))), dim3(CCT), 0, s, pool2 + cert_level2_words(pl),
-                       pl.cap3, cur2 + (1u << (pl.B1 + pl.B2)), nsb, counters);
-  } else {
-    const uint32_t nsb = 1u << (pl.B1 + pl.B2);
-    hipLaunchKernelGGL(k_cert_check, dim3(std::min(nsb, resident_grid(0, (const void *)k_cert_check, CCT, 0, 512))), dim3(CCT), 0, s, pool2, pl.cap2, cur2, nsb, counters);
-  }
+  if (pl.B3)
+    hipLaunchKernelGGL(k_cert_check, dim3(1u << (pl.B1 + pl.B2 + pl.B3)), dim3(CCT), 0, s,
+                       pool2 + cert_level2_words(pl), pl.cap3, cur2 + (1u << (pl.B1 + pl.B2)), 1u, counters);
+  else
+    hipLaunchKernelGGL(k_cert_check, dim3(1u << (pl.B1 + pl.B2)), dim3(CCT), 0, s, pool2, pl.cap2, cur2, 1u, counters);
 }
 
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,

@@ -39,7 +39,7 @@ struct DupEntry {
 };
 
 // up to FILL_MAX buffer fills (byte value each) in one launch (k_fill)
-constexpr uint32_t FILL_MAX = 8;
+constexpr uint32_t FILL_MAX = 12;
 struct FillArgs {
   void *p[FILL_MAX];
   uint64_t bytes[FILL_MAX];
@@ -47,6 +47,7 @@ struct FillArgs {
   uint32_t n = 0;
   void add(void *ptr, uint64_t nbytes, uint32_t byte) {
     if (!nbytes) return;
+    if (n >= FILL_MAX) __builtin_trap();  // (a programming error: never corrupt the launch arguments)
     p[n] = ptr;
     bytes[n] = nbytes;
     val[n] = byte;
@@ -82,20 +83,22 @@ void launch_synth_fill(hipStream_t s, int config, uint64_t seed, uint64_t t0, ui
 void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
                        const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
                        uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint32_t S, unsigned int *counters,
-                       unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp,
-                       uint64_t index_base, unsigned long long *first);
+                       unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp);
 // balanced K3 reduce (directory [partition][tile], i.e. produced with S = 1):
 // plan = k3_plan_words(P) u32 scratch, part = k3_bal_part_bytes(G)
-void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, const unsigned long long *first, const void *pool,
+void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, const void *pool,
                           const uint32_t *dir, uint32_t *plan, unsigned long long *part, unsigned long long *grp,
                           bool unpacked = false);
 uint32_t k3_bal_items(uint32_t G);
 uint32_t k3_plan_words(uint32_t P);
 uint64_t k3_bal_part_bytes(uint32_t G);
 uint64_t k3_slice_part_bytes(uint32_t G, uint32_t S);
-// `first`: the groups' first indices, kept by produce (the escape block's
-// first-index words)
-void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, const unsigned long long *first, const void *pool,
+// the reduce leaves each group's first 16-span block; launch_k3_first turns it
+// into the first span index (before launch_k3_escapes)
+void launch_k3_first(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status, uint32_t n,
+                     const uint32_t *ep_of_shape, uint32_t n_shapes, uint32_t n_status, uint64_t index_base,
+                     uint32_t G, unsigned long long *grp, unsigned int *counters);
+void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, const void *pool,
                       const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp);
 // small key spaces (G <= 1024): per-chunk LDS partials, part = [k3_small_blocks(n)][6][G] u64
 uint32_t k3_small_blocks(uint32_t n);
@@ -192,13 +195,18 @@ void launch_collapse_endpoints(hipStream_t s, const unsigned long long *sg, uint
                                unsigned long long *ep_ts, unsigned long long *ep_first, unsigned int *counters);
 
 // service-level tail over the compacted edge keys (kmz_tail.hip)
+// link keys are bucketed first: lbkt = tail_buckets() x bcap u64, lbn =
+// tail_buckets() u32 counters (zeroed); lset is the fallback set for a bucket
+// whose distinct keys overflow its LDS set
+uint32_t tail_buckets();
 void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned long long *n_keys, uint64_t n_max,
                  const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
-                 uint32_t n_ep, uint32_t n_cls, unsigned long long *lset, uint64_t lcap, unsigned long long *akey,
-                 uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
-                 uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned long long *fkey, uint32_t *fval,
-                 uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
-                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts, uint32_t knobs = 0);
+                 uint32_t n_ep, uint32_t n_cls, unsigned long long *lbkt, uint32_t bcap, uint32_t *lbn,
+                 unsigned long long *lset, uint64_t lcap, unsigned long long *akey, uint32_t *aval, uint64_t acap,
+                 unsigned long long *pset, uint64_t pcap, unsigned long long *pkey, uint32_t *pval, uint64_t pacap,
+                 uint8_t *hasin, unsigned long long *fkey, uint32_t *fval, uint64_t fcap, uint32_t *sstat,
+                 uint32_t *rel, uint32_t n_dist, unsigned int *counters, uint32_t *links_out, uint32_t *pairs_out,
+                 unsigned long long *out_counts, uint32_t knobs = 0);
 // per service: rows / gateway into sstat slots 6 / 7, first row into sfirst (after launch_tail)
 void launch_tail_service_rows(hipStream_t s, const unsigned long long *epf, const uint32_t *svc, const uint8_t *hasin,
                               uint32_t n_ep, uint32_t *sstat, unsigned long long *sfirst);

@@ -60,21 +60,24 @@ __device__ __forceinline__ uint32_t block_excl_scan_pairs(const uint32_t *cnt, u
 // ===========================================================================
 // one SERVER span's record: 8 bytes
 //   bits  0-9   group within its partition (K3R = 1024 groups per partition)
-//   bits 10-29  duration (us, < 2^20)
-//   bits 30-63  timestamp - the tile's least SERVER timestamp (us, < 2^34: 4.7 h)
+//   bits 10-16  the span's 16-span block within the tile (index / 16)
+//   bits 17-36  duration (us, < 2^20)
+//   bits 37-63  timestamp - the tile's least SERVER timestamp (us, < 2^27: 134 s)
 // (16-byte records {timestamp, duration, group | index} until round 3: the
-// record round trip was half of K3's HBM traffic.)  The record carries no span
-// index: a group's first index (a min over its spans) is kept by produce in
-// the first-index word of the escape block E, a plain read then a device
-// atomicMin only when the read says it moves (tiles run in about index order,
-// so after the first tiles the read settles it; a stale read only costs an
-// atomic).  Room for an index would have cost the group bits: 256-group
-// partitions made the runs per (tile, partition) four times shorter and the
-// directory four times larger, and the reduce slower than with 16-byte
-// records.  A span whose duration or time offset does not fit is an escape:
-// produce lists its index, k3_escape adds it into E with device atomics, and
-// k3_escape_fold folds E into the group partials.  Escapes are rare (requests
-// of a second or more).
+// record round trip was half of K3's HBM traffic.)  The reduce keeps a group's
+// first block; k3_first_fix then finds the group's first span inside that
+// block (16 spans read per group), so the first index stays exact without
+// the 11 index bits, which would have cost the group bits (256-group
+// partitions made the runs per (tile, partition) four times shorter, the
+// directory four times larger and the reduce slower than with 16-byte
+// records) or the timestamp's range (the synthetic meshes spread a tile's
+// traces over 30 s).  (A first index kept by produce with a device atomicMin
+// behind a plain read cost 0.2 ms at 10^8 spans: the read sees its XCD's
+// stale L2 copy, so nearly every span took the atomic.)  A span whose
+// duration or time offset does not fit is an escape: produce lists its index,
+// k3_escape adds it into a block of escape partials with device atomics, and
+// k3_escape_fold folds that block into the group partials.  Escapes are rare
+// (requests of a second or more; a tile spread over more than two minutes).
 #ifndef KMZ_K3T
 #define KMZ_K3T 2048
 #endif
@@ -82,16 +85,22 @@ constexpr uint32_t K3T = KMZ_K3T;  // spans per tile
 constexpr uint32_t K3R = 1024;    // groups per partition
 constexpr uint32_t K3PMAX = 256;  // partitions (G <= 2^18)
 constexpr int K3PT = K3T / 4;     // producer threads (four spans each)
-constexpr uint32_t K3_GB = 10, K3_DB = 20, K3_TB = 34;
-constexpr uint32_t K3F = 5;  // fields of the reduce's partials: count, sum d, sum d^2 (two limbs), max timestamp
-static_assert(K3R == (1u << K3_GB) && K3_GB + K3_DB + K3_TB == 64, "record fields");
+constexpr uint32_t K3_GB = 10, K3_CB = 7, K3_DB = 20, K3_TB = 27;
+constexpr uint32_t K3BS = K3T >> K3_CB;  // spans per block (16)
+constexpr uint32_t K3F = 6;  // partial fields: count, sum d, sum d^2 (two limbs), max timestamp, first block
+static_assert(K3R == (1u << K3_GB) && K3_GB + K3_CB + K3_DB + K3_TB == 64 && K3BS * (1u << K3_CB) == K3T,
+              "record fields");
 static_assert(K3PT <= 1024, "producer threads");
-__device__ __forceinline__ uint64_t k3_rec(uint32_t gl, uint32_t d, uint64_t toff) {
-  return (uint64_t)gl | ((uint64_t)d << K3_GB) | (toff << (64 - K3_TB));
+__device__ __forceinline__ uint64_t k3_rec(uint32_t gl, uint32_t li, uint32_t d, uint64_t toff) {
+  return (uint64_t)gl | ((uint64_t)(li / K3BS) << K3_GB) | ((uint64_t)d << (K3_GB + K3_CB)) | (toff << (64 - K3_TB));
 }
 __device__ __forceinline__ uint32_t k3_rec_g(uint64_t x) { return (uint32_t)x & (K3R - 1); }
-__device__ __forceinline__ uint32_t k3_rec_d(uint64_t x) { return (uint32_t)(x >> K3_GB) & ((1u << K3_DB) - 1); }
+__device__ __forceinline__ uint32_t k3_rec_blk(uint64_t x) { return (uint32_t)(x >> K3_GB) & ((1u << K3_CB) - 1); }
+__device__ __forceinline__ uint32_t k3_rec_d(uint64_t x) {
+  return (uint32_t)(x >> (K3_GB + K3_CB)) & ((1u << K3_DB) - 1);
+}
 __device__ __forceinline__ uint64_t k3_rec_toff(uint64_t x) { return x >> (64 - K3_TB); }
+constexpr uint32_t K3_BPT = 1u << K3_CB;  // blocks per tile
 
 __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ kind, const uint32_t *__restrict__ shape,
                                                    const uint16_t *__restrict__ status, const uint32_t *__restrict__ dur,
@@ -101,8 +110,7 @@ __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ k
                                                    uint32_t S, uint32_t tps, uint64_t *__restrict__ pool,
                                                    uint32_t *__restrict__ dir, uint64_t *__restrict__ tbase,
                                                    uint32_t *__restrict__ esc, unsigned int *__restrict__ counters,
-                                                   uint32_t *__restrict__ tile_servers, uint64_t index_base,
-                                                   unsigned long long *first) {
+                                                   uint32_t *__restrict__ tile_servers) {
   __shared__ uint32_t cnt[K3PMAX], off[K3PMAX];
   __shared__ uint32_t wave_tot[K3PT / 64 + 1];
   __shared__ unsigned long long wmin[K3PT / 64];
@@ -136,38 +144,29 @@ __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ k
   __syncthreads();
   uint64_t base = ~0ull;
   for (int k = 0; k < K3PT / 64; ++k) base = min(base, (uint64_t)wmin[k]);
-  uint32_t pp[PER], rr[PER], gq[PER];
+  uint32_t pp[PER], rr[PER];
   uint64_t rec[PER];
-  unsigned long long fq[PER];
   uint32_t servers = 0, flags = 0;
-  // the groups first (their first-index words are read while the tile is ranked)
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    gq[k] = NONE;
-    if (t0 + k * K3PT + threadIdx.x < n && kd[k] == KIND_SERVER) {
-      ++servers;
-      const uint32_t ep = sh[k] < n_shapes ? (ep_of_shape ? ep_of_shape[sh[k]] : sh[k]) : NONE;  // null map: by shape
-      if (ep >= n_ep || st[k] >= n_status)
-        flags |= F_RANGE;
-      else
-        gq[k] = ep * n_status + st[k];
-    }
-    fq[k] = gq[k] != NONE ? first[gq[k]] : 0ull;
-  }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const uint32_t li = k * K3PT + threadIdx.x;
     pp[k] = NONE;
     bool escape = false;
-    if (gq[k] != NONE) {
-      const uint32_t g = gq[k];
-      const uint64_t toff = ((uint64_t)tv[k] ^ TS_BIAS) - base;
-      if (du[k] < (1u << K3_DB) && toff < (1ull << K3_TB)) {
-        pp[k] = g / K3R;
-        rec[k] = k3_rec(g % K3R, du[k], toff);
-        rr[k] = atomicAdd(&cnt[pp[k]], 1u);
+    if (t0 + li < n && kd[k] == KIND_SERVER) {
+      ++servers;
+      const uint32_t ep = sh[k] < n_shapes ? (ep_of_shape ? ep_of_shape[sh[k]] : sh[k]) : NONE;  // null map: by shape
+      if (ep >= n_ep || st[k] >= n_status) {
+        flags |= F_RANGE;
       } else {
-        escape = true;
+        const uint32_t g = ep * n_status + st[k];
+        const uint64_t toff = ((uint64_t)tv[k] ^ TS_BIAS) - base;
+        if (du[k] < (1u << K3_DB) && toff < (1ull << K3_TB)) {
+          pp[k] = g / K3R;
+          rec[k] = k3_rec(g % K3R, li, du[k], toff);
+          rr[k] = atomicAdd(&cnt[pp[k]], 1u);
+        } else {
+          escape = true;
+        }
       }
     }
     // escapes: one list reservation per wave
@@ -180,12 +179,6 @@ __global__ void __launch_bounds__(K3PT) k3_produce(const uint8_t *__restrict__ k
     }
   }
   if (flags) atomicOr(&counters[C_FLAGS], flags);
-  // first indices: a device atomic only where the plain read says it moves
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const unsigned long long gi = index_base + t0 + k * K3PT + threadIdx.x;
-    if (gq[k] != NONE && gi < fq[k]) atomicMin(&first[gq[k]], gi);
-  }
   __syncthreads();
   uint32_t total = block_excl_scan_pairs<K3PT>(cnt, off, P, wave_tot);
   // directory: [partition][slice][tile within the slice], so a reduce
@@ -294,24 +287,27 @@ static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32
 // per lane in flight); a record finds its run by a binary search over the
 // wave's 64 run starts in LDS.
 //
-// PACK (a slice holds < 2^22 records: ceil(ntiles / S) * K3T < 2^22): three
-// LDS atomics per record instead of five --
+// PACK (a slice holds < 2^22 records: ceil(ntiles / S) * K3T < 2^22): four
+// LDS atomics per record instead of six --
 //   a_cs  += 2^42 + d       count in bits 42..63, sum of durations < 2^20 in
 //                           bits 0..41 (< 2^22 of them: no carry)
 //   a_s2  += d^2            (d < 2^20: d^2 < 2^40, the sum < 2^62)
-//   a_tsx  max
+//   a_tsx  max, a_fst min   the first block as a u32 within the slice / item
 // (every record's duration is < 2^20: wider ones are escapes).  Written out in
-// the unpacked partial format (s2 split into lo32 / hi32 limbs).  The first
-// index is not the reduce's: produce keeps it (k3_produce, `first`).
+// the unpacked partial format (s2 split into lo32 / hi32 limbs, the first
+// block global); k3_first_fix turns blocks into span indices.
 constexpr int K3RT = 256;
 constexpr uint32_t K3RB = 64;  // runs per wave batch (one per lane)
 #ifndef KMZ_K3_COND
-#define KMZ_K3_COND 1  // the max atomic only when a plain read says it moves
+#define KMZ_K3_COND 1  // max / min atomics only when a plain read says they move
 #endif
+// one record into the LDS accumulators: fb is its block within the slice /
+// item (PACK) or its global block
 template <bool PACK>
-__device__ __forceinline__ void k3_accumulate(uint64_t x, uint64_t tsx, unsigned long long *a0, unsigned long long *a1,
-                                              unsigned long long *a2, unsigned long long *a3,
-                                              unsigned long long *a_tsx) {
+__device__ __forceinline__ void k3_accumulate(uint64_t x, uint64_t tsx, uint64_t fb, unsigned long long *a0,
+                                              unsigned long long *a1, unsigned long long *a2, unsigned long long *a3,
+                                              unsigned long long *a_tsx, unsigned long long *a_fst,
+                                              uint32_t *a_fst32) {
   const uint32_t kl = k3_rec_g(x);
   const uint64_t d = k3_rec_d(x), dd = d * d;
   if (PACK) {
@@ -324,19 +320,28 @@ __device__ __forceinline__ void k3_accumulate(uint64_t x, uint64_t tsx, unsigned
     atomicAdd(&a3[kl], (unsigned long long)(dd >> 32));
   }
 #if KMZ_K3_COND
-  // the max only moves up: a plain LDS read that already dominates this
-  // record makes its atomic a no-op, so it is skipped (a stale read can only
-  // cost an unneeded atomic)
+  // max and min only move one way: a plain LDS read that already dominates
+  // this record makes its atomic a no-op, so it is skipped (a stale read can
+  // only cost an unneeded atomic)
   if (tsx > a_tsx[kl]) atomicMax(&a_tsx[kl], (unsigned long long)tsx);
+  if (PACK) {
+    if ((uint32_t)fb < a_fst32[kl]) atomicMin(&a_fst32[kl], (uint32_t)fb);
+  } else {
+    if (fb < a_fst[kl]) atomicMin(&a_fst[kl], (unsigned long long)fb);
+  }
 #else
   atomicMax(&a_tsx[kl], (unsigned long long)tsx);
+  if (PACK)
+    atomicMin(&a_fst32[kl], (uint32_t)fb);
+  else
+    atomicMin(&a_fst[kl], (unsigned long long)fb);
 #endif
 }
 
 // one accumulator block out: packed or unpacked LDS sums -> the K3F partial
-// fields at b[f * stride]
+// fields at b[f * stride] (the first block: `fst`, already global)
 template <bool PACK>
-__device__ __forceinline__ void k3_write_partial(const unsigned long long *acc, uint32_t k,
+__device__ __forceinline__ void k3_write_partial(const unsigned long long *acc, uint32_t k, unsigned long long fst,
                                                  unsigned long long *__restrict__ b, uint64_t stride) {
   if (PACK) {
     const unsigned long long cs = acc[k], s2 = acc[K3R + k];
@@ -351,20 +356,22 @@ __device__ __forceinline__ void k3_write_partial(const unsigned long long *acc, 
     b[3 * stride] = acc[3 * K3R + k] + (acc[2 * K3R + k] >> 32);
   }
   b[4 * stride] = acc[4 * K3R + k];
+  b[5 * stride] = fst;
 }
 
 template <bool PACK>
 __global__ void __launch_bounds__(K3RT) k3_reduce(const uint64_t *__restrict__ pool, const uint32_t *__restrict__ dir,
                                                   const uint64_t *__restrict__ tbase, uint32_t ntiles, uint32_t S,
-                                                  uint32_t G, const unsigned long long *__restrict__ first,
-                                                  unsigned long long *__restrict__ part) {
+                                                  uint32_t G, unsigned long long *__restrict__ part) {
   __shared__ unsigned long long acc[K3F * K3R];
   constexpr uint32_t NW = K3RT / 64;
   __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB];  // per wave: run starts in the batch, pool offsets
   __shared__ uint64_t r_tb[NW][K3RB];                    // ... and the runs' time bases
-  unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R;
+  unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
+                     *a_fst = acc + 5 * K3R;
+  uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
   const uint32_t s = blockIdx.x, p = blockIdx.y;
-  for (uint32_t k = threadIdx.x; k < K3F * K3R; k += K3RT) acc[k] = 0ull;
+  for (uint32_t k = threadIdx.x; k < K3F * K3R; k += K3RT) acc[k] = k < 5 * K3R ? 0ull : ~0ull;
   __syncthreads();
   const uint32_t tps = (ntiles + S - 1) / S;
   const uint32_t *row = dir + ((uint64_t)p * S + s) * tps;  // this slice's tiles, in order
@@ -405,8 +412,14 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const uint64_t *__restrict__ p
         xr[u] = pool[v[u] ? r_off[w][j] + (q - r_pre[w][j]) : 0];
       }
 #pragma unroll
-      for (uint32_t u = 0; u < U; ++u)
-        if (v[u]) k3_accumulate<PACK>(xr[u], r_tb[w][run[u]] + k3_rec_toff(xr[u]), a0, a1, a2, a3, a_tsx);
+      for (uint32_t u = 0; u < U; ++u) {
+        if (!v[u]) continue;
+        // this slice's tiles are s, s + S, ...: (k - s) / S numbers them
+        const uint64_t fb = PACK ? (uint64_t)(((uint32_t)((k0 - s) / S) + run[u] * (uint32_t)(step / S)) * K3_BPT +
+                                              k3_rec_blk(xr[u]))
+                                 : (k0 + run[u] * step) * K3_BPT + k3_rec_blk(xr[u]);
+        k3_accumulate<PACK>(xr[u], r_tb[w][run[u]] + k3_rec_toff(xr[u]), fb, a0, a1, a2, a3, a_tsx, a_fst, a_fst32);
+      }
     }
     __builtin_amdgcn_wave_barrier();  // r_pre / r_off / r_tb are rewritten by the next batch
   }
@@ -415,8 +428,10 @@ __global__ void __launch_bounds__(K3RT) k3_reduce(const uint64_t *__restrict__ p
     uint64_t g = (uint64_t)p * K3R + k;
     if (g >= G) break;
     unsigned long long *b = part + (uint64_t)s * K3F * G + g;
-    k3_write_partial<PACK>(acc, k, b, G);
-    if (S == 1) b[5ull * G] = first[g];  // (one slice: these are the group partials)
+    const uint32_t f = a_fst32[k];
+    const unsigned long long fst =
+        PACK ? (f == ~0u ? ~0ull : ((uint64_t)s + (uint64_t)(f / K3_BPT) * S) * K3_BPT + f % K3_BPT) : a_fst[k];
+    k3_write_partial<PACK>(acc, k, fst, b, G);
   }
 }
 
@@ -508,7 +523,9 @@ __device__ __forceinline__ void k3_reduce_items(const uint64_t *__restrict__ poo
                                                 uint32_t (*r_off)[K3RB], uint64_t (*r_tb)[K3RB]) {
   constexpr uint32_t NW = K3RT / 64;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R;
+  unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
+                     *a_fst = acc + 5 * K3R;
+  uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
   constexpr uint32_t U = 4;
   for (uint64_t k0 = tb + (uint64_t)w * K3RB; k0 < te; k0 += (uint64_t)NW * K3RB) {
     const uint64_t k = k0 + lane;  // this lane's run: tile k
@@ -543,8 +560,13 @@ __device__ __forceinline__ void k3_reduce_items(const uint64_t *__restrict__ poo
         xr[u] = pool[v[u] ? r_off[w][jj] + (q - r_pre[w][jj]) : 0];
       }
 #pragma unroll
-      for (uint32_t u = 0; u < U; ++u)
-        if (v[u]) k3_accumulate<PACK>(xr[u], r_tb[w][run[u]] + k3_rec_toff(xr[u]), a0, a1, a2, a3, a_tsx);
+      for (uint32_t u = 0; u < U; ++u) {
+        if (!v[u]) continue;
+        const uint64_t tile = k0 + run[u];
+        const uint64_t fb = PACK ? (uint64_t)((uint32_t)(tile - tb) * K3_BPT + k3_rec_blk(xr[u]))
+                                 : tile * K3_BPT + k3_rec_blk(xr[u]);
+        k3_accumulate<PACK>(xr[u], r_tb[w][run[u]] + k3_rec_toff(xr[u]), fb, a0, a1, a2, a3, a_tsx, a_fst, a_fst32);
+      }
     }
     __builtin_amdgcn_wave_barrier();  // r_pre / r_off / r_tb are rewritten by the next batch
   }
@@ -582,12 +604,12 @@ __global__ void __launch_bounds__(K3RT) k3_reduce_bal(const uint64_t *__restrict
   }
   for (int o = 32; o > 0; o >>= 1) nrec += __shfl_xor(nrec, o, 64);
   if (lane == 0) wred[w] = nrec;
-  for (uint32_t k = threadIdx.x; k < K3F * K3R; k += K3RT) acc[k] = 0ull;
+  for (uint32_t k = threadIdx.x; k < K3F * K3R; k += K3RT) acc[k] = k < 5 * K3R ? 0ull : ~0ull;
   __syncthreads();
   uint32_t tot = 0;
   for (uint32_t k = 0; k < NW; ++k) tot += wred[k];
   const bool pack = tot < (1u << 22) && !upk;  // (upk: test knob)
-  // packed: cs, s2, -, -, tsx -- unpacked: cnt, s1, s2a, s2b, tsx
+  // packed: cs, s2, -, -, tsx, fst32 (u32) -- unpacked: cnt, s1, s2a, s2b, tsx, fst
   if (pack)
     k3_reduce_items<true>(pool, row, tbase, tb, te, acc, r_pre, r_off, r_tb);
   else
@@ -596,21 +618,22 @@ __global__ void __launch_bounds__(K3RT) k3_reduce_bal(const uint64_t *__restrict
   unsigned long long *b = part + (uint64_t)item * K3F * K3R;
   for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {
     if ((uint64_t)p * K3R + k >= G) break;
-    if (pack)
-      k3_write_partial<true>(acc, k, b + k, K3R);
-    else
-      k3_write_partial<false>(acc, k, b + k, K3R);
+    if (pack) {
+      const uint32_t f = reinterpret_cast<const uint32_t *>(acc + 5 * K3R)[k];
+      k3_write_partial<true>(acc, k, f == ~0u ? ~0ull : tb * K3_BPT + f, b + k, K3R);
+    } else {
+      k3_write_partial<false>(acc, k, acc[5 * K3R + k], b + k, K3R);
+    }
   }
 }
 
-// the items of each partition folded; the first index from produce
+// the items of each partition folded (the first block: k3_first_fix next)
 __global__ void __launch_bounds__(256) k3_combine_bal(const unsigned long long *__restrict__ part,
                                                       const uint32_t *__restrict__ item_off, uint32_t G,
-                                                      const unsigned long long *__restrict__ first,
                                                       unsigned long long *__restrict__ grp) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
     const uint32_t p = g / K3R, k = g % K3R;
-    unsigned long long c = 0, s1 = 0, s2a = 0, s2b = 0, tsx = 0;
+    unsigned long long c = 0, s1 = 0, s2a = 0, s2b = 0, tsx = 0, fst = ~0ull;
     for (uint32_t it = item_off[p]; it < item_off[p + 1]; ++it) {
       const unsigned long long *b = part + (uint64_t)it * K3F * K3R + k;
       c += b[0];
@@ -618,21 +641,21 @@ __global__ void __launch_bounds__(256) k3_combine_bal(const unsigned long long *
       s2a += b[2 * K3R];
       s2b += b[3 * K3R];
       tsx = max(tsx, b[4 * K3R]);
+      fst = min(fst, b[5 * K3R]);
     }
     grp[g] = c;
     grp[G + g] = s1;
     grp[2ull * G + g] = s2a & 0xFFFFFFFFull;  // canonical limbs: S2 = s2a + 2^32 s2b with s2a < 2^32,
     grp[3ull * G + g] = s2b + (s2a >> 32);     // whatever split the items' sums had
     grp[4ull * G + g] = tsx;
-    grp[5ull * G + g] = first[g];
+    grp[5ull * G + g] = fst;
   }
 }
 
 __global__ void __launch_bounds__(256) k3_combine(const unsigned long long *__restrict__ part, uint32_t S, uint32_t G,
-                                                  const unsigned long long *__restrict__ first,
                                                   unsigned long long *__restrict__ grp) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
-    unsigned long long c = 0, s1 = 0, s2a = 0, s2b = 0, tsx = 0;
+    unsigned long long c = 0, s1 = 0, s2a = 0, s2b = 0, tsx = 0, fst = ~0ull;
     for (uint32_t s = 0; s < S; ++s) {
       const unsigned long long *b = part + (uint64_t)s * K3F * G + g;
       c += b[0];
@@ -640,13 +663,43 @@ __global__ void __launch_bounds__(256) k3_combine(const unsigned long long *__re
       s2a += b[2ull * G];
       s2b += b[3ull * G];
       tsx = max(tsx, b[4ull * G]);
+      fst = min(fst, b[5ull * G]);
     }
     grp[g] = c;
     grp[G + g] = s1;
     grp[2ull * G + g] = s2a & 0xFFFFFFFFull;  // (canonical limbs, as k3_combine_bal)
     grp[3ull * G + g] = s2b + (s2a >> 32);
     grp[4ull * G + g] = tsx;
-    grp[5ull * G + g] = first[g];
+    grp[5ull * G + g] = fst;
+  }
+}
+
+// a group's first block -> its first span: the first SERVER span of the
+// block in the group (one exists: the block's record came from it; an
+// escaped span of the group earlier in the block is found the same way)
+__global__ void __launch_bounds__(256) k3_first_fix(const uint8_t *__restrict__ kind,
+                                                    const uint32_t *__restrict__ shape,
+                                                    const uint16_t *__restrict__ status, uint32_t n,
+                                                    const uint32_t *__restrict__ ep_of_shape, uint32_t n_shapes,
+                                                    uint32_t n_status, uint64_t index_base, uint32_t G,
+                                                    unsigned long long *__restrict__ grp,
+                                                    unsigned int *__restrict__ counters) {
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
+    const unsigned long long blk = grp[5ull * G + g];
+    if (blk == ~0ull) continue;
+    const uint64_t i0 = blk * K3BS;
+    unsigned long long f = ~0ull;
+    for (uint32_t j = 0; j < K3BS && i0 + j < n; ++j) {
+      const uint64_t i = i0 + j;
+      if (kind[i] != KIND_SERVER || shape[i] >= n_shapes) continue;
+      const uint32_t ep = ep_of_shape ? ep_of_shape[shape[i]] : shape[i];
+      if ((uint64_t)ep * n_status + status[i] == g) {
+        f = index_base + i;
+        break;
+      }
+    }
+    if (f == ~0ull) atomicOr(&counters[C_FLAGS], F_RANGE);  // (cannot happen for a well-formed run)
+    grp[5ull * G + g] = f;
   }
 }
 
@@ -764,20 +817,19 @@ void launch_k3_small(hipStream_t s, const uint8_t *kind, const uint32_t *shape, 
 void launch_k3_produce(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,
                        const uint32_t *dur, const int64_t *ts, uint32_t n, const uint32_t *ep_of_shape,
                        uint32_t n_shapes, uint32_t n_ep, uint32_t n_status, uint32_t S, unsigned int *counters,
-                       unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp,
-                       uint64_t index_base, unsigned long long *first) {
+                       unsigned long long *n_server, void *pool, uint32_t *dir, uint32_t *tile_tmp) {
   if (!n || !n_ep) return;
   const uint32_t G = n_ep * n_status, P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
   uint64_t *rec = static_cast<uint64_t *>(pool);
   hipLaunchKernelGGL(k3_produce, dim3(ntiles), dim3(K3PT), 0, s, kind, shape, status, dur, ts, n, ep_of_shape,
                      n_shapes, n_ep, n_status, P, ntiles, S, (ntiles + S - 1) / S, rec, dir, k3_tbase(pool, n),
-                     k3_esc(pool, n), counters, tile_tmp, index_base, first);
+                     k3_esc(pool, n), counters, tile_tmp);
   hipLaunchKernelGGL(k_tile_sum, dim3(std::max<uint32_t>(1, tile_sum_blocks(ntiles))), dim3(1024), 0, s, tile_tmp, ntiles, 1u, 1u,
                      n_server, 99u);
 }
 
-void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, const unsigned long long *first, const void *pool,
-                      const uint32_t *dir, unsigned long long *part, uint32_t S, unsigned long long *grp) {
+void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, const void *pool, const uint32_t *dir,
+                      unsigned long long *part, uint32_t S, unsigned long long *grp) {
   if (!n || !G) return;
   const uint32_t P = (G + K3R - 1) / K3R, ntiles = (n + K3T - 1) / K3T;
 #ifndef KMZ_K3_PACK
@@ -785,18 +837,17 @@ void launch_k3_reduce(hipStream_t s, uint32_t n, uint32_t G, const unsigned long
 #endif
   // packed accumulators while a slice's records stay below 2^22 (counts and
   // in-slice first indices fit their fields)
-  // one slice: its partials are the group partials ([6][G]: the reduce's five
-  // fields, then the first index)
+  // one slice: its partials are the group partials ([6][G], the same layout)
   unsigned long long *dst = S == 1 ? grp : part;
   const uint64_t *rec = static_cast<const uint64_t *>(pool);
   const uint64_t *tb = k3_tbase(const_cast<void *>(pool), n);
   if (KMZ_K3_PACK && (uint64_t)((ntiles + S - 1) / S) * K3T < (1ull << 22))
-    hipLaunchKernelGGL(k3_reduce<true>, dim3(S, P), dim3(K3RT), 0, s, rec, dir, tb, ntiles, S, G, first, dst);
+    hipLaunchKernelGGL(k3_reduce<true>, dim3(S, P), dim3(K3RT), 0, s, rec, dir, tb, ntiles, S, G, dst);
   else
-    hipLaunchKernelGGL(k3_reduce<false>, dim3(S, P), dim3(K3RT), 0, s, rec, dir, tb, ntiles, S, G, first, dst);
+    hipLaunchKernelGGL(k3_reduce<false>, dim3(S, P), dim3(K3RT), 0, s, rec, dir, tb, ntiles, S, G, dst);
   if (S > 1)
     hipLaunchKernelGGL(k3_combine, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part, S,
-                       G, first, grp);
+                       G, grp);
 }
 
 // workgroups of k3_reduce_bal the device keeps resident (CUs x occupancy),
@@ -819,7 +870,7 @@ static uint32_t k3_resident() {
 }
 
 // balanced: per-partition record counts, the item plan, one workgroup per item
-void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, const unsigned long long *first, const void *pool,
+void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, const void *pool,
                           const uint32_t *dir, uint32_t *plan, unsigned long long *part, unsigned long long *grp,
                           bool unpacked) {
   if (!n || !G) return;
@@ -835,7 +886,7 @@ void launch_k3_reduce_bal(hipStream_t s, uint32_t n, uint32_t G, const unsigned 
   hipLaunchKernelGGL(k3_reduce_bal, dim3(k3_bal_items(G)), dim3(K3RT), 0, s, static_cast<const uint64_t *>(pool), dir,
                      k3_tbase(const_cast<void *>(pool), n), ntiles, P, item_off, G, unpacked ? 1u : 0u, part);
   hipLaunchKernelGGL(k3_combine_bal, dim3((G + 255) / 256 < 2048 ? (G + 255) / 256 : 2048), dim3(256), 0, s, part,
-                     item_off, G, first, grp);
+                     item_off, G, grp);
 }
 
 uint32_t k3_plan_words(uint32_t P) { return P * K3_PSUM_SPLIT + P + 1; }
@@ -853,6 +904,14 @@ uint64_t k3_pool_bytes(uint32_t n) {
 uint64_t *k3_tbase(void *pool, uint32_t n) { return static_cast<uint64_t *>(pool) + (uint64_t)((n + K3T - 1) / K3T) * K3T; }
 uint32_t *k3_esc(void *pool, uint32_t n) {
   return reinterpret_cast<uint32_t *>(k3_tbase(pool, n) + (n + K3T - 1) / K3T);
+}
+
+void launch_k3_first(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status, uint32_t n,
+                     const uint32_t *ep_of_shape, uint32_t n_shapes, uint32_t n_status, uint64_t index_base,
+                     uint32_t G, unsigned long long *grp, unsigned int *counters) {
+  if (!n || !G) return;
+  hipLaunchKernelGGL(k3_first_fix, dim3(std::min<uint32_t>((G + 255) / 256, 2048)), dim3(256), 0, s, kind, shape,
+                     status, n, ep_of_shape, n_shapes, n_status, index_base, G, grp, counters);
 }
 
 void launch_k3_escapes(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint16_t *status,

@@ -24,10 +24,11 @@
 //
 // where cls = interned (uniqueServiceName, method, labelName) and svc =
 // interned uniqueServiceName of an endpoint (host-supplied maps: the label map
-// is the host's, as in EndpointDependencies.label()).  A link key that wins its
-// slot in the link set adds itself to its (svc, lsvc(cls), d) detail counters
-// in the same step (count, dependingBy, dependingOn), so duplicates cost one
-// probe and no second pass runs.  Cohesion needs, per service, the distinct
+// is the host's, as in EndpointDependencies.label()).  The link keys are
+// bucketed by hash (k_tail_part) and each bucket deduplicated in LDS
+// (k_tail_dedup); a key's first occurrence adds itself to its (svc,
+// lsvc(cls), d) detail counters (count, dependingBy, dependingOn).  Cohesion
+// needs, per service, the distinct
 // (consumer service, consumed endpoint) pairs at distance 1: the pair set
 // (desc, usn[anc]) does the same on its own winners.  `hasin` marks rows with
 // a non-empty dependingBy (a service with a row without one is a gateway,
@@ -110,64 +111,54 @@ __device__ __forceinline__ void detail_add(uint64_t dk, uint32_t cnt, uint32_t b
 
 constexpr uint32_t TAIL_LAGG = 1024;  // per-workgroup LDS detail slots (20 KB)
 // Link keys repeat: config 5's 2.7e7 link keys per step hold ~5e4 distinct
-// ones.  A workgroup remembers the link / pair keys it has already put in the
-// global sets (direct-mapped LDS caches); a key found there is in its set, so
-// it is not a first occurrence and needs no global probe.  (A slot overwritten
-// by another key only costs a probe.)
-constexpr uint32_t TAIL_LSEEN = 2048, TAIL_PSEEN = 512;
-#ifndef KMZ_TAIL_U
-#define KMZ_TAIL_U 4
-#endif
-constexpr int TAIL_U = KMZ_TAIL_U;  // edge keys per thread and step
+// ones, spread so evenly over the edge keys that a per-workgroup LDS cache of
+// 2048 keys caught few of them (every miss a probe of the global link set:
+// 1.0 of the tail's 1.35 ms).  So the link keys are partitioned first: pass A
+// (k_tail_part) derives them from the edge keys and writes each into one of
+// TAIL_P buckets by its hash (an LDS counting sort per 2048 edge keys, one
+// reservation per bucket and step); pass B (k_tail_dedup) takes one bucket
+// per workgroup, where every occurrence of a link key lands, and dedups it in
+// an LDS set -- a key that wins there is a first occurrence of the run.
+// Cohesion pairs stay in pass A (a direct-mapped LDS cache in front of the
+// global pair set: they are few).
+constexpr uint32_t TAIL_P = 1024;               // link-key buckets
+constexpr uint32_t TAIL_PSEEN = 512;
+constexpr uint32_t TA_T = 256, TA_U = 8;         // pass A: threads, edge keys per thread and step
+constexpr uint32_t TA_STEP = TA_T * TA_U;        // 2048 edge keys, <= 4096 link keys per step
+constexpr uint32_t TB_T = 256, TB_SET = 4096;    // pass B: threads, LDS set slots (32 KB)
+__device__ __forceinline__ uint32_t tail_bucket(uint64_t lk) { return (uint32_t)(mix64(lk) >> 54); }  // 10 bits
+static_assert(TAIL_P == 1024, "tail_bucket takes 10 bits");
 
 // link key: svc << 40 | cls << 16 | type << 15 | d   (type 1 = SERVER / dependingOn)
 // detail key: svc << 40 | lsvc << 16 | d
 // pair key: (desc + 1) << 32 | consumer usn;  pair detail key: (svc + 1) << 32 | consumer usn
-__global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__restrict__ keys,
+__global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__restrict__ keys,
                                                     const unsigned long long *__restrict__ n_keys,
                                                     const uint32_t *__restrict__ svc, const uint32_t *__restrict__ cls,
-                                                    const uint32_t *__restrict__ lsvc_of_cls,
                                                     const uint32_t *__restrict__ usn, uint32_t n_ep, uint32_t n_cls,
-                                                    unsigned long long *__restrict__ lset, uint64_t lcap,
-                                                    unsigned long long *__restrict__ akey, uint32_t *__restrict__ aval,
-                                                    uint64_t acap, unsigned long long *__restrict__ pset,
+                                                    unsigned long long *__restrict__ lbkt, uint32_t bcap,
+                                                    uint32_t *__restrict__ lbn, unsigned long long *__restrict__ pset,
                                                     uint64_t pcap, unsigned long long *__restrict__ pkey,
                                                     uint32_t *__restrict__ pval, uint64_t pacap,
-                                                    uint8_t *__restrict__ hasin, unsigned long long *__restrict__ fkey,
-                                                    uint32_t *__restrict__ fval, uint64_t fcap,
-                                                    uint32_t *__restrict__ sstat, uint32_t *__restrict__ rel,
-                                                    uint32_t n_dist, unsigned int *__restrict__ counters,
-                                                    uint32_t knobs) {
+                                                    uint8_t *__restrict__ hasin, uint32_t *__restrict__ sstat,
+                                                    unsigned int *__restrict__ counters, uint32_t knobs) {
   const uint64_t n = *n_keys;
-  uint32_t flags = 0, won_l = 0, won_p = 0;  // first occurrences in the link / pair sets (sizes the next run's sets)
-  // winners' details are summed in LDS first (hot (service, linked service,
-  // distance) entries see one global update per workgroup, not one per link)
-  __shared__ unsigned long long lkey[TAIL_LAGG];
-  __shared__ uint32_t lval[TAIL_LAGG][3];
-  __shared__ unsigned long long lseen[TAIL_LSEEN], pseen[TAIL_PSEEN];
-  for (uint32_t x = threadIdx.x; x < TAIL_LSEEN; x += blockDim.x) lseen[x] = 0;
-  for (uint32_t x = threadIdx.x; x < TAIL_PSEEN; x += blockDim.x) pseen[x] = 0;
-  for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += blockDim.x) {
-    lkey[x] = 0;
-    lval[x][0] = lval[x][1] = lval[x][2] = 0;
-  }
-  __syncthreads();
-  // TAIL_U keys per thread and step: their loads and table gathers are issued
-  // together (the per-key chain of dependent loads is what bounds this kernel)
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += TAIL_U * stride) {
-    uint64_t kq[TAIL_U];
+  __shared__ unsigned long long stg[2 * TA_STEP];  // 32 KB
+  __shared__ uint32_t hist[TAIL_P], base[TAIL_P], wsum[TA_T / 64 + 1];
+  __shared__ unsigned long long pseen[TAIL_PSEEN];
+  for (uint32_t x = threadIdx.x; x < TAIL_PSEEN; x += TA_T) pseen[x] = 0;
+  uint32_t flags = 0, won_p = 0;
+  for (uint64_t s0 = (uint64_t)blockIdx.x * TA_STEP; s0 < n; s0 += (uint64_t)gridDim.x * TA_STEP) {
+    uint64_t kq[TA_U];
 #pragma unroll
-    for (int u = 0; u < TAIL_U; ++u) {
-      const uint64_t i = i0 + u * stride;
+    for (int u = 0; u < (int)TA_U; ++u) {
+      const uint64_t i = s0 + u * TA_T + threadIdx.x;
       kq[u] = i < n ? keys[i] : 0;
     }
-    uint32_t cq_a[TAIL_U], cq_s[TAIL_U], sv_a[TAIL_U], sv_s[TAIL_U], us_a[TAIL_U];
-    bool okq[TAIL_U];
+    uint32_t cq_a[TA_U], cq_s[TA_U], sv_a[TA_U], sv_s[TA_U], us_a[TA_U];
 #pragma unroll
-    for (int u = 0; u < TAIL_U; ++u) {
+    for (int u = 0; u < (int)TA_U; ++u) {
       const uint32_t a = (uint32_t)(kq[u] >> 40), s = (uint32_t)(kq[u] >> 16) & 0xFFFFFFu;
-      okq[u] = i0 + u * stride < n;
       const bool in = a < n_ep && s < n_ep;
       cq_a[u] = in ? cls[a] : NONE;
       cq_s[u] = in ? cls[s] : NONE;
@@ -175,9 +166,14 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
       sv_s[u] = in ? svc[s] : 0;
       us_a[u] = in ? usn[a] : 0;
     }
+    for (uint32_t x = threadIdx.x; x < TAIL_P; x += TA_T) hist[x] = 0;
+    __syncthreads();
+    uint64_t lk[2 * TA_U];
+    uint32_t rk[2 * TA_U];
 #pragma unroll
-    for (int u = 0; u < TAIL_U; ++u) {
-      if (!okq[u]) continue;
+    for (int u = 0; u < (int)TA_U; ++u) {
+      lk[2 * u] = lk[2 * u + 1] = 0;
+      if (s0 + u * TA_T + threadIdx.x >= n) continue;
       const uint64_t k = kq[u];
       const uint32_t a = (uint32_t)(k >> 40), s = (uint32_t)(k >> 16) & 0xFFFFFFu, d = (uint32_t)(k >> 1) & 0x7FFFu;
       const bool on = (k & 1) != 0;
@@ -186,35 +182,10 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
         continue;
       }
       if (!hasin[s]) hasin[s] = 1;  // (read first: ~10^7 keys share ~10^4 bytes)
-      // desc's row: (anc, d) in dependingBy
-      uint32_t side = 0;
-      uint64_t lk[2];
-      lk[side++] = ((uint64_t)sv_s[u] << 40) | ((uint64_t)cq_a[u] << 16) | d;
-      if (on) lk[side++] = ((uint64_t)sv_a[u] << 40) | ((uint64_t)cq_s[u] << 16) | (1u << 15) | d;
-      if (knobs & 1) side = 0;  // (diagnostic knob: no link keys -- timing only, wrong results)
-      for (uint32_t t = 0; t < side; ++t) {
-        unsigned long long &seen = lseen[(uint32_t)(lk[t] * 0x9E3779B97F4A7C15ull >> 53) & (TAIL_LSEEN - 1)];
-        if (seen == lk[t]) continue;  // put in the set by this workgroup already
-        const bool won = tail_set_put(lset, lcap, lk[t], &flags);
-        seen = lk[t];  // (in the set now, whoever won)
-        if (!won) continue;
-        ++won_l;
-        const uint32_t c = (uint32_t)(lk[t] >> 16) & 0xFFFFFFu;
-        const uint64_t dk = (lk[t] & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
-        const uint32_t ty = (uint32_t)(lk[t] >> 15) & 1u;  // dependingBy (CLIENT) / dependingOn (SERVER)
-        uint32_t h = (uint32_t)(mix64(dk) & (TAIL_LAGG - 1));
-        bool done = false;
-        for (uint32_t z = 0; z < 16; ++z) {
-          const unsigned long long cur = atomicCAS(&lkey[h], 0ull, (unsigned long long)dk);
-          if (cur == 0 || cur == dk) {
-            atomicAdd(&lval[h][0], 1u);
-            atomicAdd(&lval[h][1 + ty], 1u);
-            done = true;
-            break;
-          }
-          h = (h + 1) & (TAIL_LAGG - 1);
-        }
-        if (!done) detail_add(dk, 1u, ty == 0, ty == 1, akey, aval, acap, fkey, fval, fcap, sstat, &flags);
+      if (!(knobs & 1)) {  // (diagnostic knob 1: no link keys -- timing only, wrong results)
+        // desc's row: (anc, d) in dependingBy; anc's row, when on: (desc, d) in dependingOn
+        lk[2 * u] = ((uint64_t)sv_s[u] << 40) | ((uint64_t)cq_a[u] << 16) | d;
+        if (on) lk[2 * u + 1] = ((uint64_t)sv_a[u] << 40) | ((uint64_t)cq_s[u] << 16) | (1u << 15) | d;
       }
       // cohesion: (consumer service, consumed endpoint) at distance 1
       bool pwon = false;
@@ -235,20 +206,144 @@ __global__ void __launch_bounds__(256) k_tail_links(const unsigned long long *__
         }
       }
     }
+#pragma unroll
+    for (int j = 0; j < (int)(2 * TA_U); ++j) rk[j] = lk[j] ? atomicAdd(&hist[tail_bucket(lk[j])], 1u) : 0;
+    __syncthreads();
+    // each bucket's run of this step: one reservation, the local offsets by a scan
+    for (uint32_t x = threadIdx.x; x < TAIL_P; x += TA_T) {
+      const uint32_t h = hist[x];
+      base[x] = h ? atomicAdd(&lbn[x], h) : 0;
+    }
+    {  // exclusive scan of hist (TAIL_P = 4 per thread)
+      const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+      uint32_t v[4], run = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = run;
+        run += hist[4 * threadIdx.x + j];
+      }
+      uint32_t x = run;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+      }
+      if (lane == 63) wsum[w] = x;
+      __syncthreads();
+      uint32_t before = x - run;
+      for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+      if (threadIdx.x == TA_T - 1) wsum[TA_T / 64] = before + run;  // the step's link keys
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hist[4 * threadIdx.x + j] = before + v[j];  // hist := offsets
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < (int)(2 * TA_U); ++j)
+      if (lk[j]) stg[hist[tail_bucket(lk[j])] + rk[j]] = lk[j];
+    __syncthreads();
+    const uint32_t tot = wsum[TA_T / 64];
+    for (uint32_t e = threadIdx.x; e < tot; e += TA_T) {
+      const uint64_t x = stg[e];
+      const uint32_t b = tail_bucket(x);
+      const uint32_t pos = base[b] + e - hist[b];
+      if (pos < bcap)
+        lbkt[(uint64_t)b * bcap + pos] = x;
+      else
+        flags |= F_TRIPLE_OVERFLOW;  // (the host repeats the tail with larger buckets)
+    }
+    __syncthreads();  // (stg, hist and base are reused by the next step)
   }
-  __syncthreads();  // this workgroup's details -> the global table
-  for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += blockDim.x)
-    if (lkey[x]) detail_add(lkey[x], lval[x][0], lval[x][1], lval[x][2], akey, aval, acap, fkey, fval, fcap, sstat,
-                            &flags);
   if (flags) atomicOr(&counters[C_FLAGS], flags);
-  for (int o = 32; o > 0; o >>= 1) {
-    won_l += __shfl_xor(won_l, o, 64);
-    won_p += __shfl_xor(won_p, o, 64);
+  for (int o = 32; o > 0; o >>= 1) won_p += __shfl_xor(won_p, o, 64);
+  if ((threadIdx.x & 63) == 0 && won_p) atomicAdd(&counters[9], won_p);  // (u32 word 9 of the tail's counter block)
+}
+
+// pass B: bucket b's link keys -> first occurrences -> details.  A key that
+// finds no LDS slot in 64 probes (more than ~3000 distinct keys in one bucket)
+// goes to the global link set, which decides for it exactly.
+__global__ void __launch_bounds__(TB_T) k_tail_dedup(const unsigned long long *__restrict__ lbkt, uint32_t bcap,
+                                                     const uint32_t *__restrict__ lbn,
+                                                     const uint32_t *__restrict__ lsvc_of_cls,
+                                                     unsigned long long *__restrict__ lset, uint64_t lcap,
+                                                     unsigned long long *__restrict__ akey, uint32_t *__restrict__ aval,
+                                                     uint64_t acap, unsigned long long *__restrict__ fkey,
+                                                     uint32_t *__restrict__ fval, uint64_t fcap,
+                                                     uint32_t *__restrict__ sstat, unsigned int *__restrict__ counters) {
+  __shared__ unsigned long long set[TB_SET];
+  __shared__ unsigned long long lkey[TAIL_LAGG];
+  __shared__ uint32_t lval[TAIL_LAGG][3];
+  uint32_t flags = 0, won_l = 0;
+  for (uint32_t b = blockIdx.x; b < TAIL_P; b += gridDim.x) {
+    for (uint32_t x = threadIdx.x; x < TB_SET; x += TB_T) set[x] = 0;
+    for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += TB_T) {
+      lkey[x] = 0;
+      lval[x][0] = lval[x][1] = lval[x][2] = 0;
+    }
+    __syncthreads();
+    const uint32_t m = min(lbn[b], bcap);
+    const unsigned long long *src = lbkt + (uint64_t)b * bcap;
+    for (uint32_t e0 = 0; e0 < m; e0 += 4 * TB_T) {
+      uint64_t xq[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t e = e0 + u * TB_T + threadIdx.x;
+        xq[u] = e < m ? src[e] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t lk = xq[u];
+        if (!lk) continue;
+        uint32_t h = (uint32_t)mix64(lk) & (TB_SET - 1);  // (the bucket took the top bits)
+        int won = -1;  // -1: undecided in LDS
+        for (uint32_t z = 0; z < 64; ++z) {
+          const unsigned long long cur = set[h];
+          if (cur == lk) {
+            won = 0;
+            break;
+          }
+          if (cur == 0) {
+            const unsigned long long was = atomicCAS(&set[h], 0ull, (unsigned long long)lk);
+            if (was == 0) {
+              won = 1;
+              break;
+            }
+            if (was == lk) {
+              won = 0;
+              break;
+            }
+          }
+          h = (h + 1) & (TB_SET - 1);
+        }
+        if (won < 0) won = tail_set_put(lset, lcap, lk, &flags) ? 1 : 0;
+        if (!won) continue;
+        ++won_l;
+        const uint32_t c = (uint32_t)(lk >> 16) & 0xFFFFFFu, d = (uint32_t)lk & 0x7FFFu;
+        const uint64_t dk = (lk & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
+        const uint32_t ty = (uint32_t)(lk >> 15) & 1u;  // dependingBy (CLIENT) / dependingOn (SERVER)
+        uint32_t q = (uint32_t)(mix64(dk) & (TAIL_LAGG - 1));
+        bool done = false;
+        for (uint32_t z = 0; z < 16; ++z) {
+          const unsigned long long cur = atomicCAS(&lkey[q], 0ull, (unsigned long long)dk);
+          if (cur == 0 || cur == dk) {
+            atomicAdd(&lval[q][0], 1u);
+            atomicAdd(&lval[q][1 + ty], 1u);
+            done = true;
+            break;
+          }
+          q = (q + 1) & (TAIL_LAGG - 1);
+        }
+        if (!done) detail_add(dk, 1u, ty == 0, ty == 1, akey, aval, acap, fkey, fval, fcap, sstat, &flags);
+      }
+    }
+    __syncthreads();  // this bucket's details -> the global table
+    for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += TB_T)
+      if (lkey[x]) detail_add(lkey[x], lval[x][0], lval[x][1], lval[x][2], akey, aval, acap, fkey, fval, fcap, sstat,
+                              &flags);
+    __syncthreads();
   }
-  if ((threadIdx.x & 63) == 0 && (won_l | won_p)) {
-    atomicAdd(&counters[8], won_l);  // (u32 words 8 and 9 of the tail's counter block)
-    atomicAdd(&counters[9], won_p);
-  }
+  if (flags) atomicOr(&counters[C_FLAGS], flags);
+  for (int o = 32; o > 0; o >>= 1) won_l += __shfl_xor(won_l, o, 64);
+  if ((threadIdx.x & 63) == 0 && won_l) atomicAdd(&counters[8], won_l);  // (u32 word 8 of the tail's counter block)
 }
 
 // aggregation tables -> dense kmz_tail_detail (MODE 0) / kmz_tail_pair (MODE 1)
@@ -415,17 +510,21 @@ void launch_service_sums(hipStream_t s, const kmz_group *grp, uint32_t n_status,
   hipLaunchKernelGGL(k_service_sums, dim3((n_sid + 3) / 4), dim3(256), 0, s, grp, n_status, off, eps, is5, n_sid, out);
 }
 
+uint32_t tail_buckets() { return TAIL_P; }
+
 void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned long long *n_keys, uint64_t n_max,
                  const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
-                 uint32_t n_ep, uint32_t n_cls, unsigned long long *lset, uint64_t lcap, unsigned long long *akey,
-                 uint32_t *aval, uint64_t acap, unsigned long long *pset, uint64_t pcap, unsigned long long *pkey,
-                 uint32_t *pval, uint64_t pacap, uint8_t *hasin, unsigned long long *fkey, uint32_t *fval,
-                 uint64_t fcap, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
-                 uint32_t *links_out, uint32_t *pairs_out, unsigned long long *out_counts, uint32_t knobs) {
-  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + 255) / 256, 1024));
-  hipLaunchKernelGGL(k_tail_links, dim3(g), dim3(256), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls,
-                     lset, lcap, akey, aval, acap, pset, pcap, pkey, pval, pacap, hasin, fkey, fval, fcap, sstat, rel,
-                     n_dist, counters, knobs);
+                 uint32_t n_ep, uint32_t n_cls, unsigned long long *lbkt, uint32_t bcap, uint32_t *lbn,
+                 unsigned long long *lset, uint64_t lcap, unsigned long long *akey, uint32_t *aval, uint64_t acap,
+                 unsigned long long *pset, uint64_t pcap, unsigned long long *pkey, uint32_t *pval, uint64_t pacap,
+                 uint8_t *hasin, unsigned long long *fkey, uint32_t *fval, uint64_t fcap, uint32_t *sstat,
+                 uint32_t *rel, uint32_t n_dist, unsigned int *counters, uint32_t *links_out, uint32_t *pairs_out,
+                 unsigned long long *out_counts, uint32_t knobs) {
+  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + TA_STEP - 1) / TA_STEP, 2048));
+  hipLaunchKernelGGL(k_tail_part, dim3(g), dim3(TA_T), 0, s, keys, n_keys, svc, cls, usn, n_ep, n_cls, lbkt, bcap, lbn,
+                     pset, pcap, pkey, pval, pacap, hasin, sstat, counters, knobs);
+  hipLaunchKernelGGL(k_tail_dedup, dim3(TAIL_P), dim3(TB_T), 0, s, lbkt, bcap, lbn, lsvc_of_cls, lset, lcap, akey, aval,
+                     acap, fkey, fval, fcap, sstat, counters);
   const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((acap + 255) / 256, TAIL_COMPACT_BLOCKS));
   hipLaunchKernelGGL(k_tail_compact<0>, dim3(ga), dim3(256), 0, s, akey, aval, acap, links_out, out_counts, rel, n_dist,
                      counters);

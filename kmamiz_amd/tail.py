@@ -425,9 +425,13 @@ def realtime_risk_from_sums(tail: ServiceTail, sid_names: Sequence[str], order_i
     k = len(order_ids)
     with np.errstate(divide="ignore", invalid="ignore"):
         rel = np.where(cnt != 0, wsum / np.where(cnt != 0, cnt, 1.0), math.nan)
-        # SigmoidAdj (Normalizer.ts:32-41): the libm exp of risk.py, element by element
+        # SigmoidAdj (Normalizer.ts:32-41): the libm exp of risk.py (math.exp),
+        # element by element, in one call (kmz_host_exp)
         z = 2 * math.log(3)
-        rel_norm = to_precise(1 / (1 + np.array([math.exp(x) for x in (-z * (rel - 1.5)).tolist()], dtype=np.float64)))
+        arg = np.ascontiguousarray(-z * (rel - 1.5), dtype=np.float64)
+        ex = np.empty_like(arg)
+        L.lib().kmz_host_exp(L.ptr(arg), L.ptr(ex), len(arg))
+        rel_norm = to_precise(1 / (1 + ex))
         total = float(cnt.sum())
         npro = (cnt / total) * (1 - MP) + MP
         nerr = (err / cnt) * (1 - MP) + MP

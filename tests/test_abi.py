@@ -95,3 +95,21 @@ def test_synthetic_host_generator_deterministic():
     srv = full.kind == 1
     assert all(kinds[p] == 2 for p in full.parent_id[srv].tolist())
     assert np.all(full.kind[full.parent_id == 0] == 2)
+
+
+def test_host_exp_is_math_exp():
+    """kmz_host_exp (the risk finish's SigmoidAdj exponentials in one call)
+    returns Python's math.exp bit for bit: both are the C library's exp."""
+    import math
+
+    from kmamiz_amd import _lib
+
+    rng = np.random.default_rng(7)
+    x = np.concatenate([rng.normal(0, 3, 4000), rng.uniform(-700, 700, 4000),
+                        [0.0, -0.0, 1e-300, -745.2, 709.7, math.inf, -math.inf, math.nan]])
+    out = np.empty_like(x)
+    _lib.lib().kmz_host_exp(_lib.ptr(x), _lib.ptr(out), len(x))
+    ref = np.array([math.inf if v > 709.78 else math.exp(v) for v in x.tolist()])  # (math.exp raises on overflow)
+    fin = ~np.isnan(ref)
+    assert np.array_equal(np.isnan(out), ~fin)
+    assert np.array_equal(out[fin].view(np.uint64), ref[fin].view(np.uint64))

@@ -73,7 +73,7 @@ def test_two_rank_merge_equals_single_engine():
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=180) for _ in range(2)]
+    res = [q.get(timeout=150) for _ in range(2)]
     for p in ps:
         p.join(timeout=60)
     for r in res:
@@ -176,7 +176,7 @@ def _run_crossing(case, world, exact=True):
     ps = [ctx.Process(target=_crossing_worker, args=(r, world, port, q, case, exact)) for r in range(world)]
     for p in ps:
         p.start()
-    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    res = sorted((q.get(timeout=150) for _ in range(world)), key=lambda r: r[0])
     for p in ps:
         p.join(timeout=60)
     return res
@@ -294,7 +294,7 @@ def test_json_shards_merge_equals_c_oracle(world):
     ps = [ctx.Process(target=_json_shard_worker, args=(r, world, port, q, 400)) for r in range(world)]
     for p in ps:
         p.start()
-    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    res = sorted((q.get(timeout=150) for _ in range(world)), key=lambda r: r[0])
     for p in ps:
         p.join(timeout=60)
     for r in res:
