@@ -82,13 +82,14 @@ struct kmz_ctx {
   uint64_t imap_n = 0;     // 0: contiguous batch (index_base + i)
   DevBuf ctile;           // K4 per-workgroup stats (apart from K3's tile_tmp: the two run concurrently)
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
-  // service tail (kmz_tail.hip): maps, link set, detail table, pair set, pair table, outputs
-  DevBuf tl_svc, tl_cls, tl_lsvc, tl_lset, tl_akey, tl_aval, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs,
-      tl_cnt, tl_fkey, tl_fval, tl_sstat, tl_rel, tl_lbkt, tl_lbn;
+  // service tail (kmz_tail.hip): maps, pair set / table, outputs, link-key buckets
+  DevBuf tl_svc, tl_cls, tl_lsvc, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs, tl_cnt, tl_sstat, tl_rel,
+      tl_lbkt, tl_lbn;
   uint32_t tl_n_ep = 0, tl_n_cls = 0, tl_n_svc = 0, tl_n_dist = 64, tl_deep = 0;
   uint32_t tl_rel_dist = 0;  // distances in the last run's relying table (0: not complete, use the details)
   bool tl_map = false, tl_ran = false;
-  uint64_t tl_acap = 0, tl_pacap = 0, tl_lcap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0, tl_bcap = 0;
+  uint64_t tl_acap = 0, tl_pacap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0, tl_bcap = 0;
+  uint32_t tl_bbits = 0;  // link-key buckets: 2^tl_bbits
   DevBuf tl_sfirst;              // per service: first row (k_tail_service_rows)
   void *tl_host = nullptr;       // pinned: the tail's counters, per-service stats, relying table, first rows
   size_t tl_host_bytes = 0;
@@ -344,8 +345,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
                     &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
-                    &c->tl_lset, &c->tl_akey, &c->tl_aval, &c->tl_pset, &c->tl_pkey, &c->tl_pval,
-                    &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt, &c->tl_fkey, &c->tl_fval,
+                    &c->tl_pset, &c->tl_pkey, &c->tl_pval,
+                    &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt,
                     &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->tl_lbkt, &c->tl_lbn, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
                     &c->o_key, &c->o_val, &c->o_out,
                     &c->o_rts, &c->o_rsh, &c->j_buf, &c->j_elem, &c->j_state, &c->j_jsc, &c->j_mask,
@@ -2018,26 +2019,24 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
   }
   // link keys <= 2 per edge key (load <= 1/2); pairs <= 1 per edge key; the
   // detail / pair tables start smaller and grow on overflow
-  // link / pair sets: sized by the previous run's first occurrences (load
-  // <= 1/2, cache-resident when the keys repeat), or by the worst case (two
-  // link keys and one pair per edge key) on the first run; grown on overflow
-  if (!c->tl_lcap) c->tl_lcap = pow2_at_least(4 * nt + 64);
-  // link-key buckets: two link keys per edge key at most, spread by a hash
-  // (mean + 25 % + 512 per bucket); grown on overflow
-  const uint32_t nbk = tail_buckets();
-  c->tl_bcap = std::max<uint64_t>(c->tl_bcap, (2 * nt / nbk) * 5 / 4 + 512);
+  // pair set: sized by the previous run's first occurrences (load <= 1/2), or
+  // by the worst case (one pair per edge key) on the first run; grown on overflow
+  if (!c->tl_bbits) c->tl_bbits = 11;
   if (!c->tl_pcap) c->tl_pcap = pow2_at_least(2 * nt + 64);
   if (!c->tl_acap) c->tl_acap = pow2_at_least(nt / 2 + 4096);
   if (!c->tl_pacap) c->tl_pacap = pow2_at_least(nt / 4 + 4096);
   for (int attempt = 0;; ++attempt) {
-    const uint64_t acap = c->tl_acap, pacap = c->tl_pacap, lcap = c->tl_lcap, pcap = c->tl_pcap;
+    const uint64_t acap = c->tl_acap, pacap = c->tl_pacap, pcap = c->tl_pcap;
+    // link-key buckets: two link keys per edge key at most, spread by a hash
+    // of their (service, linked service) pair (1.5 x the mean + 4096 per
+    // bucket: hot pairs weigh some buckets); grown on overflow
+    const uint32_t bits = c->tl_bbits, nbk = 1u << bits;
+    c->tl_bcap = std::max<uint64_t>(c->tl_bcap, ((2 * nt) >> bits) * 3 / 2 + 4096);
     const uint64_t bcap = c->tl_bcap;
     if (bcap >= 0xFFFFFFFFull) return fail(c, KMZ_E_OVERFLOW, "service tail buckets");
     if (ensure(c, c->tl_lbkt, bcap * nbk * 8) || ensure(c, c->tl_lbn, (size_t)nbk * 4) ||
-        ensure(c, c->tl_lset, lcap * 8) || ensure(c, c->tl_akey, acap * 8) || ensure(c, c->tl_aval, acap * 16) ||
         ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
         ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
-        ensure(c, c->tl_fkey, acap * 8) || ensure(c, c->tl_fval, acap * 4) ||
         ensure(c, c->tl_sstat, (size_t)c->tl_n_svc * 32) || ensure(c, c->tl_rel, (size_t)c->tl_n_svc * c->tl_n_dist * 4) ||
         ensure(c, c->tl_sfirst, (size_t)c->tl_n_svc * 8 + 8))
       return KMZ_E_HIP;
@@ -2055,37 +2054,29 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
     }
     {
       Timed t(c, KMZ_K_MEMSET);
-      FillArgs f, g;
-      f.add(c->tl_lset.p, lcap * 8, 0);
-      f.add(c->tl_akey.p, acap * 8, 0);
-      f.add(c->tl_aval.p, acap * 16, 0);
+      FillArgs f;
       f.add(c->tl_pset.p, pcap * 8, 0);
       f.add(c->tl_pkey.p, pacap * 8, 0);
       f.add(c->tl_pval.p, pacap * 4, 0);
       f.add(c->tl_hasin.p, c->tl_n_ep ? c->tl_n_ep : 1, 0);
       f.add(c->tl_cnt.p, 64, 0);
-      g.add(c->tl_lbn.p, (size_t)nbk * 4, 0);
-      g.add(c->tl_fkey.p, acap * 8, 0);
-      g.add(c->tl_fval.p, acap * 4, 0);
+      f.add(c->tl_lbn.p, (size_t)nbk * 4, 0);
       if (c->tl_n_svc) {
-        g.add(c->tl_sstat.p, (size_t)c->tl_n_svc * 32, 0);
-        g.add(c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4, 0);
-        g.add(c->tl_sfirst.p, (size_t)c->tl_n_svc * 8, 0xFF);
+        f.add(c->tl_sstat.p, (size_t)c->tl_n_svc * 32, 0);
+        f.add(c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4, 0);
+        f.add(c->tl_sfirst.p, (size_t)c->tl_n_svc * 8, 0xFF);
       }
       launch_fill(c->stream, f);
-      launch_fill(c->stream, g);
     }
     unsigned long long *cnt64 = P<unsigned long long>(c->tl_cnt);  // [0] flags (u32), [1] details, [2] pairs
     {
       Timed t(c, KMZ_K_TAIL);
       launch_tail(c->stream, P<unsigned long long>(c->trip_out), st + S_TRIP_OUT, nt, P<uint32_t>(c->tl_svc),
                   P<uint32_t>(c->tl_cls), P<uint32_t>(c->tl_lsvc), P<uint32_t>(c->tl_svc), c->tl_n_ep, c->tl_n_cls,
-                  P<unsigned long long>(c->tl_lbkt), (uint32_t)bcap, P<uint32_t>(c->tl_lbn),
-                  P<unsigned long long>(c->tl_lset), lcap, P<unsigned long long>(c->tl_akey), P<uint32_t>(c->tl_aval),
-                  acap, P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey),
-                  P<uint32_t>(c->tl_pval), pacap, P<uint8_t>(c->tl_hasin), P<unsigned long long>(c->tl_fkey),
-                  P<uint32_t>(c->tl_fval), acap, P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), nd_run,
-                  P<unsigned int>(c->tl_cnt), P<uint32_t>(c->tl_det), P<uint32_t>(c->tl_pairs), cnt64 + 1,
+                  bits, P<unsigned long long>(c->tl_lbkt), (uint32_t)bcap, P<uint32_t>(c->tl_lbn),
+                  P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey), P<uint32_t>(c->tl_pval),
+                  pacap, P<uint8_t>(c->tl_hasin), P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), nd_run,
+                  P<unsigned int>(c->tl_cnt), P<kmz_tail_detail>(c->tl_det), acap, P<uint32_t>(c->tl_pairs), cnt64 + 1,
                   // diagnostic knobs (timing only, wrong results): KMZ_ABLATE bit 7 skips the
                   // link keys, bit 12 the cohesion pairs
                   ((c->ablate >> 7) & 1u) | (((c->ablate >> 12) & 1u) << 1));
@@ -2105,26 +2096,30 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
-    unsigned long long h[5];
+    unsigned long long h[6];
     memcpy(h, hh, sizeof(h));
     const uint32_t fl = (uint32_t)h[0];
     if (fl & F_RANGE) return fail(c, KMZ_E_RANGE, "edge key endpoint outside the tail map");
-    if (fl & F_TRIPLE_OVERFLOW) {
+    const bool bucket_full = (uint32_t)h[5] != 0;  // (u32 word 10) a bucket outgrew its LDS tables
+    if ((fl & F_TRIPLE_OVERFLOW) || bucket_full) {
       if (attempt >= 3) return fail(c, KMZ_E_OVERFLOW, "service tail table overflow");
-      c->tl_acap = std::max(c->tl_acap * 4, pow2_at_least(nt / 2 + 4096));
-      c->tl_pacap = std::max(c->tl_pacap * 4, pow2_at_least(nt / 4 + 4096));
-      c->tl_lcap = std::max(c->tl_lcap * 4, pow2_at_least(4 * nt + 64));
-      c->tl_pcap = std::max(c->tl_pcap * 4, pow2_at_least(2 * nt + 64));
-      c->tl_bcap *= 2;
+      if (bucket_full) {
+        if (c->tl_bbits >= tail_bucket_bits_max()) return fail(c, KMZ_E_OVERFLOW, "service tail: too many link keys");
+        ++c->tl_bbits;
+      }
+      if (fl & F_TRIPLE_OVERFLOW) {
+        c->tl_acap = std::max(c->tl_acap * 4, pow2_at_least(nt / 2 + 4096));
+        c->tl_pacap = std::max(c->tl_pacap * 4, pow2_at_least(nt / 4 + 4096));
+        c->tl_pcap = std::max(c->tl_pcap * 4, pow2_at_least(2 * nt + 64));
+        c->tl_bcap *= 2;
+      }
       continue;
     }
-    const uint64_t won_l = (uint32_t)h[4], won_p = (uint32_t)(h[4] >> 32);
-    c->tl_lcap = pow2_at_least(2 * won_l + 4096);  // the next run's sets (this run's keys at load <= 1/2)
-    c->tl_pcap = pow2_at_least(2 * won_p + 4096);
-    // the detail / pair tables at load <= 1/2 of this run's counts for the
-    // next run (they start at nt / 2 and nt / 4 slots: config 5 has ~10^5
-    // details for 1.4e7 edge keys, and every slot is filled and scanned per
-    // run); a larger next batch overflows and repeats the tail 4x larger
+    const uint64_t won_p = (uint32_t)(h[4] >> 32);
+    c->tl_pcap = pow2_at_least(2 * won_p + 4096);  // the next run's pair set (this run's pairs at load <= 1/2)
+    // the detail output / pair tables at 2x this run's counts for the next
+    // run (they start at nt / 2 and nt / 4); a larger next batch overflows and
+    // repeats the tail 4x larger
     c->tl_acap = pow2_at_least(2 * h[1] + 4096);
     c->tl_pacap = pow2_at_least(2 * h[2] + 4096);
     c->tl_nd = h[1];

@@ -85,49 +85,60 @@ __device__ __forceinline__ uint64_t tail_agg_slot(unsigned long long *__restrict
   return cap;
 }
 
-// add (count, dependingBy, dependingOn) to the detail dk in the global table;
-// the first link of a type there also counts into the service's ACS
-// (distance 1, RiskAnalyzer.ts:150-166) and instability (any distance,
-// EndpointDependencies.ts:618-628) counters
-__device__ __forceinline__ void detail_add(uint64_t dk, uint32_t cnt, uint32_t by, uint32_t on,
-                                           unsigned long long *__restrict__ akey, uint32_t *__restrict__ aval,
-                                           uint64_t acap, unsigned long long *__restrict__ fkey,
-                                           uint32_t *__restrict__ fval, uint64_t fcap, uint32_t *__restrict__ sstat,
-                                           uint32_t *flags) {
-  const uint64_t p = tail_agg_slot(akey, acap, dk, flags);
-  if (p == acap) return;
-  const uint32_t sv = (uint32_t)(dk >> 40), d = (uint32_t)dk & 0xFFFFu;
-  atomicAdd(&aval[4 * p + 0], cnt);
-  for (uint32_t ty = 0; ty < 2; ++ty) {
-    const uint32_t v = ty ? on : by;
-    if (!v || atomicAdd(&aval[4 * p + 1 + ty], v)) continue;
-    if (d == 1) atomicAdd(&sstat[8 * sv + TS_AIS + ty], 1u);
-    const uint64_t q = tail_agg_slot(fkey, fcap, (dk >> 16) + 1, flags);  // (svc, lsvc)
-    if (q == fcap) continue;
-    const uint32_t was = atomicOr(&fval[q], 1u << ty);
-    if (!(was & (1u << ty))) atomicAdd(&sstat[8 * sv + TS_NBY + ty], 1u);
-  }
-}
-
-constexpr uint32_t TAIL_LAGG = 1024;  // per-workgroup LDS detail slots (20 KB)
-// Link keys repeat: config 5's 2.7e7 link keys per step hold ~5e4 distinct
-// ones, spread so evenly over the edge keys that a per-workgroup LDS cache of
-// 2048 keys caught few of them (every miss a probe of the global link set:
-// 1.0 of the tail's 1.35 ms).  So the link keys are partitioned first: pass A
-// (k_tail_part) derives them from the edge keys and writes each into one of
-// TAIL_P buckets by its hash (an LDS counting sort per 2048 edge keys, one
-// reservation per bucket and step); pass B (k_tail_dedup) takes one bucket
-// per workgroup, where every occurrence of a link key lands, and dedups it in
-// an LDS set -- a key that wins there is a first occurrence of the run.
-// Cohesion pairs stay in pass A (a direct-mapped LDS cache in front of the
-// global pair set: they are few).
-constexpr uint32_t TAIL_P = 1024;               // link-key buckets
-constexpr uint32_t TAIL_PSEEN = 512;
-constexpr uint32_t TA_T = 256, TA_U = 8;         // pass A: threads, edge keys per thread and step
+// Link keys repeat, but not enough for a cache: config 5's 2.7e7 link keys
+// per step (1e8 spans) hold a few million distinct ones (1.3e6 of 6.6e6 at
+// 4.5e6 spans), and their details (service, linked service, distance) nearly
+// as many (9.1e5 there).  The round-3 k_tail_links put every link key in a
+// global set behind a per-workgroup LDS cache and added every first
+// occurrence into a global detail table: millions of dependent device-scope
+// probes and atomics (1.35 ms, waves waiting on memory 78 % of their cycles).
+// Here both dedups stay in LDS by partitioning on the (service, linked
+// service) pair -- every link key, detail and pair flag of a pair lands in one
+// bucket:
+//   k_tail_part   per edge key its link keys, minus those its workgroup has
+//                 already emitted (a direct-mapped LDS filter: hot keys), into
+//                 one of 2^bits buckets by a hash of (service, linked service)
+//                 -- an LDS counting sort per 2048 edge keys, one reservation
+//                 per bucket and step; cohesion pairs into the pair set.
+//   k_tail_dedup  one 1024-thread workgroup per bucket: its link keys into an
+//                 LDS set; each distinct key into its detail (LDS table:
+//                 count, dependingBy, dependingOn) and its pair's flags (a
+//                 by / on link at any distance / at distance 1); the details
+//                 written out as kmz_tail_detail records (one reservation per
+//                 bucket) with their relying-factor sums, each pair's flags
+//                 added to its service's counters.
+// A bucket whose LDS tables are too small, or an output that is full, flags
+// the run and the host repeats the tail with twice the buckets (or a larger
+// output): exact either way.
+constexpr uint32_t TA_T = 512, TA_U = 4;         // pass A: threads, edge keys per thread and step
 constexpr uint32_t TA_STEP = TA_T * TA_U;        // 2048 edge keys, <= 4096 link keys per step
-constexpr uint32_t TB_T = 256, TB_SET = 4096;    // pass B: threads, LDS set slots (32 KB)
-__device__ __forceinline__ uint32_t tail_bucket(uint64_t lk) { return (uint32_t)(mix64(lk) >> 54); }  // 10 bits
-static_assert(TAIL_P == 1024, "tail_bucket takes 10 bits");
+constexpr uint32_t TA_SEEN = 4096;               // pass A: LDS filter of emitted link keys (32 KB)
+constexpr uint32_t TAIL_PSEEN = 512;
+constexpr uint32_t TAIL_BMAX = 12;               // buckets: 2^11 (2^12 after an overflow)
+constexpr uint32_t TB_T = 1024;                  // pass B: one workgroup per CU
+constexpr uint32_t TB_LSET = 8192, TB_DSET = 4096, TB_PSET = 1024;  // LDS: 64 + 80 + 12 KB
+// a link key's (service, linked service) pair and its bucket
+__device__ __forceinline__ uint32_t tail_bucket(uint64_t pair, uint32_t bits) {
+  return (uint32_t)(mix64(pair ^ 0x2545F4914F6CDD1Dull) >> (64 - bits));
+}
+__device__ __forceinline__ uint64_t link_pair(uint64_t lk, const uint32_t *__restrict__ lsvc_of_cls) {
+  return ((lk >> 40) << 24) | lsvc_of_cls[(uint32_t)(lk >> 16) & 0xFFFFFFu];  // svc << 24 | lsvc
+}
+// insert k (nonzero) into an LDS open-addressing table of 2^lb slots -> its
+// slot, or ~0u when 64 probes find no room
+__device__ __forceinline__ uint32_t lds_slot(unsigned long long *tab, uint32_t lb, uint64_t k) {
+  uint32_t h = (uint32_t)mix64(k) & ((1u << lb) - 1);
+  for (uint32_t z = 0; z < 64; ++z) {
+    const unsigned long long cur = tab[h];
+    if (cur == k) return h;
+    if (cur == 0) {
+      const unsigned long long was = atomicCAS(&tab[h], 0ull, (unsigned long long)k);
+      if (was == 0 || was == k) return h;
+    }
+    h = (h + 1) & ((1u << lb) - 1);
+  }
+  return ~0u;
+}
 
 // link key: svc << 40 | cls << 16 | type << 15 | d   (type 1 = SERVER / dependingOn)
 // detail key: svc << 40 | lsvc << 16 | d
@@ -135,18 +146,23 @@ static_assert(TAIL_P == 1024, "tail_bucket takes 10 bits");
 __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__restrict__ keys,
                                                     const unsigned long long *__restrict__ n_keys,
                                                     const uint32_t *__restrict__ svc, const uint32_t *__restrict__ cls,
+                                                    const uint32_t *__restrict__ lsvc_of_cls,
                                                     const uint32_t *__restrict__ usn, uint32_t n_ep, uint32_t n_cls,
-                                                    unsigned long long *__restrict__ lbkt, uint32_t bcap,
-                                                    uint32_t *__restrict__ lbn, unsigned long long *__restrict__ pset,
-                                                    uint64_t pcap, unsigned long long *__restrict__ pkey,
-                                                    uint32_t *__restrict__ pval, uint64_t pacap,
-                                                    uint8_t *__restrict__ hasin, uint32_t *__restrict__ sstat,
-                                                    unsigned int *__restrict__ counters, uint32_t knobs) {
+                                                    uint32_t bits, unsigned long long *__restrict__ lbkt,
+                                                    uint32_t bcap, uint32_t *__restrict__ lbn,
+                                                    unsigned long long *__restrict__ pset, uint64_t pcap,
+                                                    unsigned long long *__restrict__ pkey, uint32_t *__restrict__ pval,
+                                                    uint64_t pacap, uint8_t *__restrict__ hasin,
+                                                    uint32_t *__restrict__ sstat, unsigned int *__restrict__ counters,
+                                                    uint32_t knobs) {
   const uint64_t n = *n_keys;
+  const uint32_t nb = 1u << bits;
   __shared__ unsigned long long stg[2 * TA_STEP];  // 32 KB
-  __shared__ uint32_t hist[TAIL_P], base[TAIL_P], wsum[TA_T / 64 + 1];
-  __shared__ unsigned long long pseen[TAIL_PSEEN];
+  __shared__ uint32_t hist[1u << TAIL_BMAX], base[1u << TAIL_BMAX], wsum[TA_T / 64 + 1];
+  __shared__ unsigned long long pseen[TAIL_PSEEN], lseen[TA_SEEN];
+  __shared__ uint16_t bk[2 * TA_STEP];  // each staged key's bucket
   for (uint32_t x = threadIdx.x; x < TAIL_PSEEN; x += TA_T) pseen[x] = 0;
+  for (uint32_t x = threadIdx.x; x < TA_SEEN; x += TA_T) lseen[x] = 0;
   uint32_t flags = 0, won_p = 0;
   for (uint64_t s0 = (uint64_t)blockIdx.x * TA_STEP; s0 < n; s0 += (uint64_t)gridDim.x * TA_STEP) {
     uint64_t kq[TA_U];
@@ -166,10 +182,10 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
       sv_s[u] = in ? svc[s] : 0;
       us_a[u] = in ? usn[a] : 0;
     }
-    for (uint32_t x = threadIdx.x; x < TAIL_P; x += TA_T) hist[x] = 0;
+    for (uint32_t x = threadIdx.x; x < nb; x += TA_T) hist[x] = 0;
     __syncthreads();
     uint64_t lk[2 * TA_U];
-    uint32_t rk[2 * TA_U];
+    uint32_t rk[2 * TA_U], lb[2 * TA_U];
 #pragma unroll
     for (int u = 0; u < (int)TA_U; ++u) {
       lk[2 * u] = lk[2 * u + 1] = 0;
@@ -186,6 +202,16 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
         // desc's row: (anc, d) in dependingBy; anc's row, when on: (desc, d) in dependingOn
         lk[2 * u] = ((uint64_t)sv_s[u] << 40) | ((uint64_t)cq_a[u] << 16) | d;
         if (on) lk[2 * u + 1] = ((uint64_t)sv_a[u] << 40) | ((uint64_t)cq_s[u] << 16) | (1u << 15) | d;
+        // emitted by this workgroup already: drop (a lossy filter; pass B dedups exactly)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (!lk[2 * u + t]) continue;
+          unsigned long long &e = lseen[(uint32_t)(lk[2 * u + t] * 0x9E3779B97F4A7C15ull >> 52) & (TA_SEEN - 1)];
+          if (e == lk[2 * u + t])
+            lk[2 * u + t] = 0;
+          else
+            e = lk[2 * u + t];
+        }
       }
       // cohesion: (consumer service, consumed endpoint) at distance 1
       bool pwon = false;
@@ -207,21 +233,20 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
       }
     }
 #pragma unroll
-    for (int j = 0; j < (int)(2 * TA_U); ++j) rk[j] = lk[j] ? atomicAdd(&hist[tail_bucket(lk[j])], 1u) : 0;
+    for (int j = 0; j < (int)(2 * TA_U); ++j) {
+      lb[j] = lk[j] ? tail_bucket(link_pair(lk[j], lsvc_of_cls), bits) : 0;
+      rk[j] = lk[j] ? atomicAdd(&hist[lb[j]], 1u) : 0;
+    }
     __syncthreads();
     // each bucket's run of this step: one reservation, the local offsets by a scan
-    for (uint32_t x = threadIdx.x; x < TAIL_P; x += TA_T) {
+    for (uint32_t x = threadIdx.x; x < nb; x += TA_T) {
       const uint32_t h = hist[x];
       base[x] = h ? atomicAdd(&lbn[x], h) : 0;
     }
-    {  // exclusive scan of hist (TAIL_P = 4 per thread)
-      const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-      uint32_t v[4], run = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = run;
-        run += hist[4 * threadIdx.x + j];
-      }
+    {  // exclusive scan of hist (nb / TA_T per thread)
+      const uint32_t per = nb / TA_T, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+      uint32_t run = 0;
+      for (uint32_t j = 0; j < per; ++j) run += hist[per * threadIdx.x + j];
       uint32_t x = run;
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
@@ -233,21 +258,27 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
       for (uint32_t k = 0; k < w; ++k) before += wsum[k];
       if (threadIdx.x == TA_T - 1) wsum[TA_T / 64] = before + run;  // the step's link keys
       __syncthreads();
-#pragma unroll
-      for (int j = 0; j < 4; ++j) hist[4 * threadIdx.x + j] = before + v[j];  // hist := offsets
+      for (uint32_t j = 0; j < per; ++j) {  // hist := offsets
+        const uint32_t c = hist[per * threadIdx.x + j];
+        hist[per * threadIdx.x + j] = before;
+        before += c;
+      }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < (int)(2 * TA_U); ++j)
-      if (lk[j]) stg[hist[tail_bucket(lk[j])] + rk[j]] = lk[j];
+      if (lk[j]) {
+        const uint32_t at = hist[lb[j]] + rk[j];
+        stg[at] = lk[j];
+        bk[at] = (uint16_t)lb[j];
+      }
     __syncthreads();
     const uint32_t tot = wsum[TA_T / 64];
     for (uint32_t e = threadIdx.x; e < tot; e += TA_T) {
-      const uint64_t x = stg[e];
-      const uint32_t b = tail_bucket(x);
+      const uint32_t b = bk[e];
       const uint32_t pos = base[b] + e - hist[b];
       if (pos < bcap)
-        lbkt[(uint64_t)b * bcap + pos] = x;
+        lbkt[(uint64_t)b * bcap + pos] = stg[e];
       else
         flags |= F_TRIPLE_OVERFLOW;  // (the host repeats the tail with larger buckets)
     }
@@ -258,30 +289,38 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
   if ((threadIdx.x & 63) == 0 && won_p) atomicAdd(&counters[9], won_p);  // (u32 word 9 of the tail's counter block)
 }
 
-// pass B: bucket b's link keys -> first occurrences -> details.  A key that
-// finds no LDS slot in 64 probes (more than ~3000 distinct keys in one bucket)
-// goes to the global link set, which decides for it exactly.
+// pass B: bucket b -> its distinct link keys -> details (written out) and
+// pair flags (into the services' counters)
+constexpr uint32_t PF_BY = 1, PF_ON = 2, PF_BY1 = 4, PF_ON1 = 8;
 __global__ void __launch_bounds__(TB_T) k_tail_dedup(const unsigned long long *__restrict__ lbkt, uint32_t bcap,
-                                                     const uint32_t *__restrict__ lbn,
+                                                     const uint32_t *__restrict__ lbn, uint32_t bits,
                                                      const uint32_t *__restrict__ lsvc_of_cls,
-                                                     unsigned long long *__restrict__ lset, uint64_t lcap,
-                                                     unsigned long long *__restrict__ akey, uint32_t *__restrict__ aval,
-                                                     uint64_t acap, unsigned long long *__restrict__ fkey,
-                                                     uint32_t *__restrict__ fval, uint64_t fcap,
-                                                     uint32_t *__restrict__ sstat, unsigned int *__restrict__ counters) {
-  __shared__ unsigned long long set[TB_SET];
-  __shared__ unsigned long long lkey[TAIL_LAGG];
-  __shared__ uint32_t lval[TAIL_LAGG][3];
-  uint32_t flags = 0, won_l = 0;
-  for (uint32_t b = blockIdx.x; b < TAIL_P; b += gridDim.x) {
-    for (uint32_t x = threadIdx.x; x < TB_SET; x += TB_T) set[x] = 0;
-    for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += TB_T) {
-      lkey[x] = 0;
-      lval[x][0] = lval[x][1] = lval[x][2] = 0;
+                                                     kmz_tail_detail *__restrict__ dout, uint64_t dcap,
+                                                     unsigned long long *__restrict__ dcount,
+                                                     uint32_t *__restrict__ sstat, uint32_t *__restrict__ rel,
+                                                     uint32_t n_dist, unsigned int *__restrict__ counters) {
+  __shared__ unsigned long long lset[TB_LSET], dkey[TB_DSET], pkey[TB_PSET];
+  __shared__ uint32_t dval[3][TB_DSET], pflag[TB_PSET];
+  __shared__ uint32_t s_full, s_nd, s_won;
+  __shared__ unsigned long long s_base;
+  constexpr uint32_t LB = 13, DB = 12, PB = 10;
+  static_assert((1u << LB) == TB_LSET && (1u << DB) == TB_DSET && (1u << PB) == TB_PSET, "LDS table sizes");
+  uint32_t flags = 0;
+  for (uint32_t b = blockIdx.x; b < (1u << bits); b += gridDim.x) {
+    for (uint32_t x = threadIdx.x; x < TB_LSET; x += TB_T) lset[x] = 0;
+    for (uint32_t x = threadIdx.x; x < TB_DSET; x += TB_T) {
+      dkey[x] = 0;
+      dval[0][x] = dval[1][x] = dval[2][x] = 0;
     }
+    for (uint32_t x = threadIdx.x; x < TB_PSET; x += TB_T) {
+      pkey[x] = 0;
+      pflag[x] = 0;
+    }
+    if (threadIdx.x == 0) s_full = s_nd = s_won = 0;
     __syncthreads();
     const uint32_t m = min(lbn[b], bcap);
     const unsigned long long *src = lbkt + (uint64_t)b * bcap;
+    // 1. the bucket's link keys into the LDS set
     for (uint32_t e0 = 0; e0 < m; e0 += 4 * TB_T) {
       uint64_t xq[4];
 #pragma unroll
@@ -290,60 +329,94 @@ __global__ void __launch_bounds__(TB_T) k_tail_dedup(const unsigned long long *_
         xq[u] = e < m ? src[e] : 0;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint64_t lk = xq[u];
+      for (int u = 0; u < 4; ++u)
+        if (xq[u] && lds_slot(lset, LB, xq[u]) == ~0u) s_full = 1;
+    }
+    __syncthreads();
+    // 2. each distinct link key: its detail and its pair's flags
+    uint32_t won = 0;
+    if (!s_full) {
+      for (uint32_t x = threadIdx.x; x < TB_LSET; x += TB_T) {
+        const uint64_t lk = lset[x];
         if (!lk) continue;
-        uint32_t h = (uint32_t)mix64(lk) & (TB_SET - 1);  // (the bucket took the top bits)
-        int won = -1;  // -1: undecided in LDS
-        for (uint32_t z = 0; z < 64; ++z) {
-          const unsigned long long cur = set[h];
-          if (cur == lk) {
-            won = 0;
-            break;
-          }
-          if (cur == 0) {
-            const unsigned long long was = atomicCAS(&set[h], 0ull, (unsigned long long)lk);
-            if (was == 0) {
-              won = 1;
-              break;
-            }
-            if (was == lk) {
-              won = 0;
-              break;
-            }
-          }
-          h = (h + 1) & (TB_SET - 1);
-        }
-        if (won < 0) won = tail_set_put(lset, lcap, lk, &flags) ? 1 : 0;
-        if (!won) continue;
-        ++won_l;
+        ++won;
         const uint32_t c = (uint32_t)(lk >> 16) & 0xFFFFFFu, d = (uint32_t)lk & 0x7FFFu;
-        const uint64_t dk = (lk & ~((1ull << 40) - 1)) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
         const uint32_t ty = (uint32_t)(lk >> 15) & 1u;  // dependingBy (CLIENT) / dependingOn (SERVER)
-        uint32_t q = (uint32_t)(mix64(dk) & (TAIL_LAGG - 1));
-        bool done = false;
-        for (uint32_t z = 0; z < 16; ++z) {
-          const unsigned long long cur = atomicCAS(&lkey[q], 0ull, (unsigned long long)dk);
-          if (cur == 0 || cur == dk) {
-            atomicAdd(&lval[q][0], 1u);
-            atomicAdd(&lval[q][1 + ty], 1u);
-            done = true;
-            break;
-          }
-          q = (q + 1) & (TAIL_LAGG - 1);
+        const uint64_t pr = ((lk >> 40) << 24) | lsvc_of_cls[c];
+        const uint64_t dk = ((lk >> 40) << 40) | ((uint64_t)lsvc_of_cls[c] << 16) | d;
+        const uint32_t q = lds_slot(dkey, DB, dk + 1);  // (+1: the key of svc 0, lsvc 0, d 0 is never 0 in LDS)
+        const uint32_t r = lds_slot(pkey, PB, pr + 1);
+        if (q == ~0u || r == ~0u) {
+          s_full = 1;
+          continue;
         }
-        if (!done) detail_add(dk, 1u, ty == 0, ty == 1, akey, aval, acap, fkey, fval, fcap, sstat, &flags);
+        atomicAdd(&dval[0][q], 1u);
+        atomicAdd(&dval[1 + ty][q], 1u);
+        atomicOr(&pflag[r], (ty ? PF_ON : PF_BY) | (d == 1 ? (ty ? PF_ON1 : PF_BY1) : 0u));
       }
     }
-    __syncthreads();  // this bucket's details -> the global table
-    for (uint32_t x = threadIdx.x; x < TAIL_LAGG; x += TB_T)
-      if (lkey[x]) detail_add(lkey[x], lval[x][0], lval[x][1], lval[x][2], akey, aval, acap, fkey, fval, fcap, sstat,
-                              &flags);
+    __syncthreads();
+    if (s_full) {  // (uniform) a table too small for this bucket: the host redoes the tail with more buckets
+      if (threadIdx.x == 0) atomicOr(&counters[10], 1u);
+    } else {
+      for (int o = 32; o > 0; o >>= 1) won += __shfl_xor(won, o, 64);
+      if ((threadIdx.x & 63) == 0 && won) atomicAdd(&s_won, won);
+      // 3. the details out (one reservation), the pairs into the services' counters
+      uint32_t nd = 0;
+      for (uint32_t x = threadIdx.x; x < TB_DSET; x += TB_T) nd += dkey[x] != 0;
+      for (int o = 32; o > 0; o >>= 1) nd += __shfl_xor(nd, o, 64);
+      if ((threadIdx.x & 63) == 0 && nd) atomicAdd(&s_nd, nd);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        s_base = s_nd ? atomicAdd(dcount, (unsigned long long)s_nd) : 0;
+        if (s_won) atomicAdd(&counters[8], s_won);  // (u32 word 8: distinct link keys)
+        s_nd = 0;
+      }
+      __syncthreads();
+      for (uint32_t x = threadIdx.x; x < TB_DSET; x += TB_T) {
+        const unsigned long long k = dkey[x];
+        if (!k) continue;
+        const uint64_t dk = k - 1;
+        const uint64_t at = s_base + atomicAdd(&s_nd, 1u);
+        const uint32_t sv = (uint32_t)(dk >> 40), d = (uint32_t)dk & 0xFFFFu;
+        if (at < dcap) {
+          kmz_tail_detail r;
+          r.svc = sv;
+          r.lsvc = (uint32_t)(dk >> 16) & 0xFFFFFFu;
+          r.distance = d;
+          r.count = dval[0][x];
+          r.depending_by = dval[1][x];
+          r.depending_on = dval[2][x];
+          dout[at] = r;
+        } else {
+          flags |= F_TRIPLE_OVERFLOW;
+        }
+        // RelyingFactor: sum of dependingBy / distance (RiskAnalyzer.ts:124-137),
+        // per (service, distance) -- one add per detail, not per link key
+        if (dval[1][x]) {
+          if (d < n_dist)
+            atomicAdd(&rel[(uint64_t)sv * n_dist + d], dval[1][x]);
+          else
+            atomicMax(&counters[6], d);  // deeper than the dense table: the host uses the details
+        }
+      }
+      // a service's instability counts its linked services with a by / on link
+      // (EndpointDependencies.ts:618-628), its ACS those at distance 1
+      // (RiskAnalyzer.ts:150-166): every (service, linked service) pair is in
+      // this bucket only
+      for (uint32_t x = threadIdx.x; x < TB_PSET; x += TB_T) {
+        const uint32_t f = pflag[x];
+        if (!f) continue;
+        const uint32_t sv = (uint32_t)((pkey[x] - 1) >> 24);
+        if (f & PF_BY) atomicAdd(&sstat[8 * sv + TS_NBY], 1u);
+        if (f & PF_ON) atomicAdd(&sstat[8 * sv + TS_NON], 1u);
+        if (f & PF_BY1) atomicAdd(&sstat[8 * sv + TS_AIS], 1u);
+        if (f & PF_ON1) atomicAdd(&sstat[8 * sv + TS_ADS], 1u);
+      }
+    }
     __syncthreads();
   }
   if (flags) atomicOr(&counters[C_FLAGS], flags);
-  for (int o = 32; o > 0; o >>= 1) won_l += __shfl_xor(won_l, o, 64);
-  if ((threadIdx.x & 63) == 0 && won_l) atomicAdd(&counters[8], won_l);  // (u32 word 8 of the tail's counter block)
 }
 
 // aggregation tables -> dense kmz_tail_detail (MODE 0) / kmz_tail_pair (MODE 1)
@@ -510,24 +583,21 @@ void launch_service_sums(hipStream_t s, const kmz_group *grp, uint32_t n_status,
   hipLaunchKernelGGL(k_service_sums, dim3((n_sid + 3) / 4), dim3(256), 0, s, grp, n_status, off, eps, is5, n_sid, out);
 }
 
-uint32_t tail_buckets() { return TAIL_P; }
+uint32_t tail_bucket_bits_max() { return TAIL_BMAX; }
 
 void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned long long *n_keys, uint64_t n_max,
                  const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
-                 uint32_t n_ep, uint32_t n_cls, unsigned long long *lbkt, uint32_t bcap, uint32_t *lbn,
-                 unsigned long long *lset, uint64_t lcap, unsigned long long *akey, uint32_t *aval, uint64_t acap,
+                 uint32_t n_ep, uint32_t n_cls, uint32_t bits, unsigned long long *lbkt, uint32_t bcap, uint32_t *lbn,
                  unsigned long long *pset, uint64_t pcap, unsigned long long *pkey, uint32_t *pval, uint64_t pacap,
-                 uint8_t *hasin, unsigned long long *fkey, uint32_t *fval, uint64_t fcap, uint32_t *sstat,
-                 uint32_t *rel, uint32_t n_dist, unsigned int *counters, uint32_t *links_out, uint32_t *pairs_out,
-                 unsigned long long *out_counts, uint32_t knobs) {
-  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + TA_STEP - 1) / TA_STEP, 2048));
-  hipLaunchKernelGGL(k_tail_part, dim3(g), dim3(TA_T), 0, s, keys, n_keys, svc, cls, usn, n_ep, n_cls, lbkt, bcap, lbn,
-                     pset, pcap, pkey, pval, pacap, hasin, sstat, counters, knobs);
-  hipLaunchKernelGGL(k_tail_dedup, dim3(TAIL_P), dim3(TB_T), 0, s, lbkt, bcap, lbn, lsvc_of_cls, lset, lcap, akey, aval,
-                     acap, fkey, fval, fcap, sstat, counters);
-  const uint32_t ga = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((acap + 255) / 256, TAIL_COMPACT_BLOCKS));
-  hipLaunchKernelGGL(k_tail_compact<0>, dim3(ga), dim3(256), 0, s, akey, aval, acap, links_out, out_counts, rel, n_dist,
-                     counters);
+                 uint8_t *hasin, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
+                 kmz_tail_detail *links_out, uint64_t dcap, uint32_t *pairs_out, unsigned long long *out_counts,
+                 uint32_t knobs) {
+  // (a few workgroups per CU, each over many steps: the LDS filter sees more of the hot keys)
+  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + TA_STEP - 1) / TA_STEP, 512));
+  hipLaunchKernelGGL(k_tail_part, dim3(g), dim3(TA_T), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls, bits,
+                     lbkt, bcap, lbn, pset, pcap, pkey, pval, pacap, hasin, sstat, counters, knobs);
+  hipLaunchKernelGGL(k_tail_dedup, dim3(1u << bits), dim3(TB_T), 0, s, lbkt, bcap, lbn, bits, lsvc_of_cls, links_out,
+                     dcap, out_counts, sstat, rel, n_dist, counters);
   const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pacap + 255) / 256, TAIL_COMPACT_BLOCKS));
   hipLaunchKernelGGL(k_tail_compact<1>, dim3(gp), dim3(256), 0, s, pkey, pval, pacap, pairs_out, out_counts + 1, rel,
                      n_dist, counters);
