@@ -2028,13 +2028,14 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
   for (int attempt = 0;; ++attempt) {
     const uint64_t acap = c->tl_acap, pacap = c->tl_pacap, pcap = c->tl_pcap;
     // link-key buckets: two link keys per edge key at most, spread by a hash
-    // of their (service, linked service) pair (1.5 x the mean + 4096 per
-    // bucket: hot pairs weigh some buckets); grown on overflow
-    const uint32_t bits = c->tl_bbits, nbk = 1u << bits;
-    c->tl_bcap = std::max<uint64_t>(c->tl_bcap, ((2 * nt) >> bits) * 3 / 2 + 4096);
-    const uint64_t bcap = c->tl_bcap;
-    if (bcap >= 0xFFFFFFFFull) return fail(c, KMZ_E_OVERFLOW, "service tail buckets");
-    if (ensure(c, c->tl_lbkt, bcap * nbk * 8) || ensure(c, c->tl_lbn, (size_t)nbk * 4) ||
+    // of their (service, linked service) pair, each pass-A workgroup writing
+    // its own slab of every bucket (2 x its mean share + 64: hot pairs weigh
+    // some buckets); grown on overflow
+    const uint32_t bits = c->tl_bbits, nbk = 1u << bits, nwg = tail_part_grid(nt);
+    c->tl_bcap = std::max<uint64_t>(c->tl_bcap, (2 * nt) / ((uint64_t)nbk * nwg) * 2 + 64);
+    const uint64_t slab = c->tl_bcap;
+    if (slab >= 0xFFFFFFFFull) return fail(c, KMZ_E_OVERFLOW, "service tail buckets");
+    if (ensure(c, c->tl_lbkt, slab * nbk * nwg * 8) || ensure(c, c->tl_lbn, (size_t)nbk * nwg * 4) ||
         ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
         ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
         ensure(c, c->tl_sstat, (size_t)c->tl_n_svc * 32) || ensure(c, c->tl_rel, (size_t)c->tl_n_svc * c->tl_n_dist * 4) ||
@@ -2060,7 +2061,6 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       f.add(c->tl_pval.p, pacap * 4, 0);
       f.add(c->tl_hasin.p, c->tl_n_ep ? c->tl_n_ep : 1, 0);
       f.add(c->tl_cnt.p, 64, 0);
-      f.add(c->tl_lbn.p, (size_t)nbk * 4, 0);
       if (c->tl_n_svc) {
         f.add(c->tl_sstat.p, (size_t)c->tl_n_svc * 32, 0);
         f.add(c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4, 0);
@@ -2073,7 +2073,7 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
       Timed t(c, KMZ_K_TAIL);
       launch_tail(c->stream, P<unsigned long long>(c->trip_out), st + S_TRIP_OUT, nt, P<uint32_t>(c->tl_svc),
                   P<uint32_t>(c->tl_cls), P<uint32_t>(c->tl_lsvc), P<uint32_t>(c->tl_svc), c->tl_n_ep, c->tl_n_cls,
-                  bits, P<unsigned long long>(c->tl_lbkt), (uint32_t)bcap, P<uint32_t>(c->tl_lbn),
+                  bits, P<unsigned long long>(c->tl_lbkt), (uint32_t)slab, P<uint32_t>(c->tl_lbn),
                   P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey), P<uint32_t>(c->tl_pval),
                   pacap, P<uint8_t>(c->tl_hasin), P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), nd_run,
                   P<unsigned int>(c->tl_cnt), P<kmz_tail_detail>(c->tl_det), acap, P<uint32_t>(c->tl_pairs), cnt64 + 1,

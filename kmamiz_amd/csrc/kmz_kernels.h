@@ -195,15 +195,17 @@ void launch_collapse_endpoints(hipStream_t s, const unsigned long long *sg, uint
                                unsigned long long *ep_ts, unsigned long long *ep_first, unsigned int *counters);
 
 // service-level tail over the compacted edge keys (kmz_tail.hip)
-// link keys are bucketed by their (service, linked service) pair first: lbkt
-// = 2^bits x bcap u64, lbn = 2^bits u32 counters (zeroed), bits <=
-// tail_bucket_bits_max(); details are written to links_out (dcap records,
-// count in out_counts[0]); counters word 10 set: a bucket outgrew its LDS
-// tables (redo with more buckets)
+// link keys are bucketed by their (service, linked service) pair first, each
+// pass-A workgroup into its own slab of every bucket: lbkt = 2^bits x
+// tail_part_grid(n_max) x slab u64, lbn = as many u32 fills (written by the
+// kernel); bits = tail_bucket_bits_max() or one less; details are written
+// to links_out (dcap records, count in out_counts[0]); counters word 10 set:
+// a bucket outgrew its LDS tables (redo with more buckets)
 uint32_t tail_bucket_bits_max();
+uint32_t tail_part_grid(uint64_t n_max);
 void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned long long *n_keys, uint64_t n_max,
                  const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
-                 uint32_t n_ep, uint32_t n_cls, uint32_t bits, unsigned long long *lbkt, uint32_t bcap, uint32_t *lbn,
+                 uint32_t n_ep, uint32_t n_cls, uint32_t bits, unsigned long long *lbkt, uint32_t slab, uint32_t *lbn,
                  unsigned long long *pset, uint64_t pcap, unsigned long long *pkey, uint32_t *pval, uint64_t pacap,
                  uint8_t *hasin, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
                  kmz_tail_detail *links_out, uint64_t dcap, uint32_t *pairs_out, unsigned long long *out_counts,

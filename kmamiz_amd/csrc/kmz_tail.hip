@@ -98,31 +98,33 @@ __device__ __forceinline__ uint64_t tail_agg_slot(unsigned long long *__restrict
 //   k_tail_part   per edge key its link keys, minus those its workgroup has
 //                 already emitted (a direct-mapped LDS filter: hot keys), into
 //                 one of 2^bits buckets by a hash of (service, linked service)
-//                 -- an LDS counting sort per 2048 edge keys, one reservation
-//                 per bucket and step; cohesion pairs into the pair set.
-//   k_tail_dedup  one 1024-thread workgroup per bucket: its link keys into an
+//                 -- an LDS counting sort per 2048 edge keys; every workgroup
+//                 owns a slab of each bucket and counts its fill in LDS (one
+//                 device atomic per bucket and step on 2^11 shared counters
+//                 was 1.2e7 contended atomics per run); cohesion pairs into
+//                 the pair set.
+//   k_tail_dedup  one 1024-thread workgroup per bucket: its link keys (the
+//                 workgroups' slabs, located by a scan of their fills) into an
 //                 LDS set; each distinct key into its detail (LDS table:
 //                 count, dependingBy, dependingOn) and its pair's flags (a
 //                 by / on link at any distance / at distance 1); the details
 //                 written out as kmz_tail_detail records (one reservation per
 //                 bucket) with their relying-factor sums, each pair's flags
 //                 added to its service's counters.
-// A bucket whose LDS tables are too small, or an output that is full, flags
-// the run and the host repeats the tail with twice the buckets (or a larger
-// output): exact either way.
+// A bucket whose LDS tables are too small, a full slab or an output that is
+// full flags the run and the host repeats the tail with twice the buckets (or
+// larger slabs or output): exact either way.
 constexpr uint32_t TA_T = 512, TA_U = 4;         // pass A: threads, edge keys per thread and step
 constexpr uint32_t TA_STEP = TA_T * TA_U;        // 2048 edge keys, <= 4096 link keys per step
-constexpr uint32_t TA_SEEN = 4096;               // pass A: LDS filter of emitted link keys (32 KB)
+constexpr uint32_t TA_SEEN = 2048;               // pass A: LDS filter of emitted link keys (16 KB)
 constexpr uint32_t TAIL_PSEEN = 512;
 constexpr uint32_t TAIL_BMAX = 12;               // buckets: 2^11 (2^12 after an overflow)
 constexpr uint32_t TB_T = 1024;                  // pass B: one workgroup per CU
-constexpr uint32_t TB_LSET = 8192, TB_DSET = 4096, TB_PSET = 1024;  // LDS: 64 + 80 + 12 KB
+constexpr uint32_t TB_LSET = 8192, TB_DSET = 2048, TB_PSET = 2048;  // LDS: 64 + 40 + 24 KB
+constexpr uint32_t TA_GRID = 512;                // pass A workgroups (slabs per bucket)
 // a link key's (service, linked service) pair and its bucket
 __device__ __forceinline__ uint32_t tail_bucket(uint64_t pair, uint32_t bits) {
   return (uint32_t)(mix64(pair ^ 0x2545F4914F6CDD1Dull) >> (64 - bits));
-}
-__device__ __forceinline__ uint64_t link_pair(uint64_t lk, const uint32_t *__restrict__ lsvc_of_cls) {
-  return ((lk >> 40) << 24) | lsvc_of_cls[(uint32_t)(lk >> 16) & 0xFFFFFFu];  // svc << 24 | lsvc
 }
 // insert k (nonzero) into an LDS open-addressing table of 2^lb slots -> its
 // slot, or ~0u when 64 probes find no room
@@ -143,26 +145,28 @@ __device__ __forceinline__ uint32_t lds_slot(unsigned long long *tab, uint32_t l
 // link key: svc << 40 | cls << 16 | type << 15 | d   (type 1 = SERVER / dependingOn)
 // detail key: svc << 40 | lsvc << 16 | d
 // pair key: (desc + 1) << 32 | consumer usn;  pair detail key: (svc + 1) << 32 | consumer usn
+template <uint32_t BITS>
 __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__restrict__ keys,
                                                     const unsigned long long *__restrict__ n_keys,
                                                     const uint32_t *__restrict__ svc, const uint32_t *__restrict__ cls,
                                                     const uint32_t *__restrict__ lsvc_of_cls,
                                                     const uint32_t *__restrict__ usn, uint32_t n_ep, uint32_t n_cls,
-                                                    uint32_t bits, unsigned long long *__restrict__ lbkt,
-                                                    uint32_t bcap, uint32_t *__restrict__ lbn,
+                                                    unsigned long long *__restrict__ lbkt, uint32_t slab,
+                                                    uint32_t *__restrict__ lbn,
                                                     unsigned long long *__restrict__ pset, uint64_t pcap,
                                                     unsigned long long *__restrict__ pkey, uint32_t *__restrict__ pval,
                                                     uint64_t pacap, uint8_t *__restrict__ hasin,
                                                     uint32_t *__restrict__ sstat, unsigned int *__restrict__ counters,
                                                     uint32_t knobs) {
   const uint64_t n = *n_keys;
-  const uint32_t nb = 1u << bits;
+  constexpr uint32_t nb = 1u << BITS, bits = BITS;
   __shared__ unsigned long long stg[2 * TA_STEP];  // 32 KB
-  __shared__ uint32_t hist[1u << TAIL_BMAX], base[1u << TAIL_BMAX], wsum[TA_T / 64 + 1];
+  __shared__ uint32_t hist[nb], fill[nb], wsum[TA_T / 64 + 1];  // this step's offsets; the slabs' fill
   __shared__ unsigned long long pseen[TAIL_PSEEN], lseen[TA_SEEN];
   __shared__ uint16_t bk[2 * TA_STEP];  // each staged key's bucket
   for (uint32_t x = threadIdx.x; x < TAIL_PSEEN; x += TA_T) pseen[x] = 0;
   for (uint32_t x = threadIdx.x; x < TA_SEEN; x += TA_T) lseen[x] = 0;
+  for (uint32_t x = threadIdx.x; x < nb; x += TA_T) fill[x] = 0;
   uint32_t flags = 0, won_p = 0;
   for (uint64_t s0 = (uint64_t)blockIdx.x * TA_STEP; s0 < n; s0 += (uint64_t)gridDim.x * TA_STEP) {
     uint64_t kq[TA_U];
@@ -233,16 +237,11 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
       }
     }
 #pragma unroll
-    for (int j = 0; j < (int)(2 * TA_U); ++j) {
-      lb[j] = lk[j] ? tail_bucket(link_pair(lk[j], lsvc_of_cls), bits) : 0;
+    for (int j = 0; j < (int)(2 * TA_U); ++j) {  // (the bucket: the key's (service, linked service) pair)
+      lb[j] = lk[j] ? tail_bucket(((lk[j] >> 40) << 24) | lsvc_of_cls[(uint32_t)(lk[j] >> 16) & 0xFFFFFFu], bits) : 0;
       rk[j] = lk[j] ? atomicAdd(&hist[lb[j]], 1u) : 0;
     }
     __syncthreads();
-    // each bucket's run of this step: one reservation, the local offsets by a scan
-    for (uint32_t x = threadIdx.x; x < nb; x += TA_T) {
-      const uint32_t h = hist[x];
-      base[x] = h ? atomicAdd(&lbn[x], h) : 0;
-    }
     {  // exclusive scan of hist (nb / TA_T per thread)
       const uint32_t per = nb / TA_T, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
       uint32_t run = 0;
@@ -276,14 +275,18 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
     const uint32_t tot = wsum[TA_T / 64];
     for (uint32_t e = threadIdx.x; e < tot; e += TA_T) {
       const uint32_t b = bk[e];
-      const uint32_t pos = base[b] + e - hist[b];
-      if (pos < bcap)
-        lbkt[(uint64_t)b * bcap + pos] = stg[e];
+      const uint32_t pos = fill[b] + e - hist[b];  // (this workgroup's slab of bucket b)
+      if (pos < slab)
+        lbkt[((uint64_t)b * gridDim.x + blockIdx.x) * slab + pos] = stg[e];
       else
-        flags |= F_TRIPLE_OVERFLOW;  // (the host repeats the tail with larger buckets)
+        flags |= F_TRIPLE_OVERFLOW;  // (the host repeats the tail with larger slabs)
     }
-    __syncthreads();  // (stg, hist and base are reused by the next step)
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < nb; x += TA_T)  // the slabs' fill after this step
+      fill[x] += (x + 1 < nb ? hist[x + 1] : tot) - hist[x];
+    __syncthreads();  // (stg and hist are reused by the next step)
   }
+  for (uint32_t x = threadIdx.x; x < nb; x += TA_T) lbn[(uint64_t)x * gridDim.x + blockIdx.x] = fill[x];
   if (flags) atomicOr(&counters[C_FLAGS], flags);
   for (int o = 32; o > 0; o >>= 1) won_p += __shfl_xor(won_p, o, 64);
   if ((threadIdx.x & 63) == 0 && won_p) atomicAdd(&counters[9], won_p);  // (u32 word 9 of the tail's counter block)
@@ -292,8 +295,8 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
 // pass B: bucket b -> its distinct link keys -> details (written out) and
 // pair flags (into the services' counters)
 constexpr uint32_t PF_BY = 1, PF_ON = 2, PF_BY1 = 4, PF_ON1 = 8;
-__global__ void __launch_bounds__(TB_T) k_tail_dedup(const unsigned long long *__restrict__ lbkt, uint32_t bcap,
-                                                     const uint32_t *__restrict__ lbn, uint32_t bits,
+__global__ void __launch_bounds__(TB_T) k_tail_dedup(const unsigned long long *__restrict__ lbkt, uint32_t slab,
+                                                     const uint32_t *__restrict__ lbn, uint32_t nwg, uint32_t bits,
                                                      const uint32_t *__restrict__ lsvc_of_cls,
                                                      kmz_tail_detail *__restrict__ dout, uint64_t dcap,
                                                      unsigned long long *__restrict__ dcount,
@@ -303,7 +306,8 @@ __global__ void __launch_bounds__(TB_T) k_tail_dedup(const unsigned long long *_
   __shared__ uint32_t dval[3][TB_DSET], pflag[TB_PSET];
   __shared__ uint32_t s_full, s_nd, s_won;
   __shared__ unsigned long long s_base;
-  constexpr uint32_t LB = 13, DB = 12, PB = 10;
+  __shared__ uint32_t soff[TA_GRID + 1], wsum[TB_T / 64];  // the slabs' fills -> their offsets in the bucket
+  constexpr uint32_t LB = 13, DB = 11, PB = 11;
   static_assert((1u << LB) == TB_LSET && (1u << DB) == TB_DSET && (1u << PB) == TB_PSET, "LDS table sizes");
   uint32_t flags = 0;
   for (uint32_t b = blockIdx.x; b < (1u << bits); b += gridDim.x) {
@@ -317,16 +321,39 @@ __global__ void __launch_bounds__(TB_T) k_tail_dedup(const unsigned long long *_
       pflag[x] = 0;
     }
     if (threadIdx.x == 0) s_full = s_nd = s_won = 0;
+    {  // exclusive scan of the nwg slab fills (nwg <= TB_T: one per thread)
+      const uint32_t c = threadIdx.x < nwg ? min(lbn[(uint64_t)b * nwg + threadIdx.x], slab) : 0;
+      const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+      uint32_t x = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+      }
+      if (lane == 63) wsum[w] = x;
+      __syncthreads();
+      uint32_t before = x - c;
+      for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+      if (threadIdx.x < nwg) soff[threadIdx.x] = before;
+      if (threadIdx.x == TB_T - 1) soff[nwg] = before + c;
+    }
     __syncthreads();
-    const uint32_t m = min(lbn[b], bcap);
-    const unsigned long long *src = lbkt + (uint64_t)b * bcap;
-    // 1. the bucket's link keys into the LDS set
+    const uint32_t m = soff[nwg];
+    const unsigned long long *src = lbkt + (uint64_t)b * nwg * slab;
+    // 1. the bucket's link keys into the LDS set (entry e: slab w with
+    // soff[w] <= e < soff[w + 1], by a binary search)
     for (uint32_t e0 = 0; e0 < m; e0 += 4 * TB_T) {
       uint64_t xq[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t e = e0 + u * TB_T + threadIdx.x;
-        xq[u] = e < m ? src[e] : 0;
+        xq[u] = 0;
+        if (e < m) {
+          uint32_t lo = 0;
+#pragma unroll
+          for (uint32_t step = TA_GRID / 2; step; step >>= 1)
+            if (lo + step < nwg && soff[lo + step] <= e) lo += step;
+          xq[u] = src[(uint64_t)lo * slab + (e - soff[lo])];
+        }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -584,19 +611,27 @@ void launch_service_sums(hipStream_t s, const kmz_group *grp, uint32_t n_status,
 }
 
 uint32_t tail_bucket_bits_max() { return TAIL_BMAX; }
+uint32_t tail_part_grid(uint64_t n_max) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + TA_STEP - 1) / TA_STEP, TA_GRID));
+}
 
 void launch_tail(hipStream_t s, const unsigned long long *keys, const unsigned long long *n_keys, uint64_t n_max,
                  const uint32_t *svc, const uint32_t *cls, const uint32_t *lsvc_of_cls, const uint32_t *usn,
-                 uint32_t n_ep, uint32_t n_cls, uint32_t bits, unsigned long long *lbkt, uint32_t bcap, uint32_t *lbn,
+                 uint32_t n_ep, uint32_t n_cls, uint32_t bits, unsigned long long *lbkt, uint32_t slab, uint32_t *lbn,
                  unsigned long long *pset, uint64_t pcap, unsigned long long *pkey, uint32_t *pval, uint64_t pacap,
                  uint8_t *hasin, uint32_t *sstat, uint32_t *rel, uint32_t n_dist, unsigned int *counters,
                  kmz_tail_detail *links_out, uint64_t dcap, uint32_t *pairs_out, unsigned long long *out_counts,
                  uint32_t knobs) {
-  // (a few workgroups per CU, each over many steps: the LDS filter sees more of the hot keys)
-  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_max + TA_STEP - 1) / TA_STEP, 512));
-  hipLaunchKernelGGL(k_tail_part, dim3(g), dim3(TA_T), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep, n_cls, bits,
-                     lbkt, bcap, lbn, pset, pcap, pkey, pval, pacap, hasin, sstat, counters, knobs);
-  hipLaunchKernelGGL(k_tail_dedup, dim3(1u << bits), dim3(TB_T), 0, s, lbkt, bcap, lbn, bits, lsvc_of_cls, links_out,
+  // (a few workgroups per CU, each over many steps: the LDS filter sees more
+  // of the hot keys; lbkt / lbn are sized for tail_part_grid(n_max) slabs)
+  const uint32_t g = tail_part_grid(n_max);
+  if (bits == TAIL_BMAX)
+    hipLaunchKernelGGL(k_tail_part<TAIL_BMAX>, dim3(g), dim3(TA_T), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn, n_ep,
+                       n_cls, lbkt, slab, lbn, pset, pcap, pkey, pval, pacap, hasin, sstat, counters, knobs);
+  else
+    hipLaunchKernelGGL(k_tail_part<TAIL_BMAX - 1>, dim3(g), dim3(TA_T), 0, s, keys, n_keys, svc, cls, lsvc_of_cls, usn,
+                       n_ep, n_cls, lbkt, slab, lbn, pset, pcap, pkey, pval, pacap, hasin, sstat, counters, knobs);
+  hipLaunchKernelGGL(k_tail_dedup, dim3(1u << bits), dim3(TB_T), 0, s, lbkt, slab, lbn, g, bits, lsvc_of_cls, links_out,
                      dcap, out_counts, sstat, rel, n_dist, counters);
   const uint32_t gp = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((pacap + 255) / 256, TAIL_COMPACT_BLOCKS));
   hipLaunchKernelGGL(k_tail_compact<1>, dim3(gp), dim3(256), 0, s, pkey, pval, pacap, pairs_out, out_counts + 1, rel,

@@ -443,8 +443,16 @@ def realtime_risk_from_sums(tail: ServiceTail, sid_names: Sequence[str], order_i
     rf = tail.relying_factor()[sv].astype(np.float64)
     ais, ads = tail._acs()
     acs = (ais * ads)[sv].astype(np.float64)
-    by_locale = np.argsort(tail.maps.rank("locale")[sv], kind="stable")
-    by_code = sv[np.argsort(tail.maps.rank("code")[sv], kind="stable")]
+    # (the present services rarely change between ticks: their two orders are
+    # kept on the maps for the last set seen)
+    memo = tail.maps.__dict__.setdefault("_order_memo", {})
+    sk = sv.tobytes()
+    if memo.get("key") != sk:
+        memo.clear()
+        memo["key"] = sk
+        memo["orders"] = (np.argsort(tail.maps.rank("locale")[sv], kind="stable"),
+                          sv[np.argsort(tail.maps.rank("code")[sv], kind="stable")])
+    by_locale, by_code = memo["orders"]
     raw = _fixed_ratio(rf[by_locale]) + _fixed_ratio(acs[by_locale])
     if replicas:
         rep = {}
