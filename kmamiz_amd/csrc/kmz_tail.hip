@@ -168,13 +168,21 @@ __global__ void __launch_bounds__(TA_T) k_tail_part(const unsigned long long *__
   for (uint32_t x = threadIdx.x; x < TA_SEEN; x += TA_T) lseen[x] = 0;
   for (uint32_t x = threadIdx.x; x < nb; x += TA_T) fill[x] = 0;
   uint32_t flags = 0, won_p = 0;
+  // the next step's edge keys are loaded while this step is sorted and written
+  uint64_t kn[TA_U];
+  auto load = [&](uint64_t s1) {
+#pragma unroll
+    for (int u = 0; u < (int)TA_U; ++u) {
+      const uint64_t i = s1 + u * TA_T + threadIdx.x;
+      kn[u] = i < n ? keys[i] : 0;
+    }
+  };
+  load((uint64_t)blockIdx.x * TA_STEP);
   for (uint64_t s0 = (uint64_t)blockIdx.x * TA_STEP; s0 < n; s0 += (uint64_t)gridDim.x * TA_STEP) {
     uint64_t kq[TA_U];
 #pragma unroll
-    for (int u = 0; u < (int)TA_U; ++u) {
-      const uint64_t i = s0 + u * TA_T + threadIdx.x;
-      kq[u] = i < n ? keys[i] : 0;
-    }
+    for (int u = 0; u < (int)TA_U; ++u) kq[u] = kn[u];
+    load(s0 + (uint64_t)gridDim.x * TA_STEP);
     uint32_t cq_a[TA_U], cq_s[TA_U], sv_a[TA_U], sv_s[TA_U], us_a[TA_U];
 #pragma unroll
     for (int u = 0; u < (int)TA_U; ++u) {
@@ -341,20 +349,27 @@ __global__ void __launch_bounds__(TB_T) k_tail_dedup(const unsigned long long *_
     const unsigned long long *src = lbkt + (uint64_t)b * nwg * slab;
     // 1. the bucket's link keys into the LDS set (entry e: slab w with
     // soff[w] <= e < soff[w + 1], by a binary search)
-    for (uint32_t e0 = 0; e0 < m; e0 += 4 * TB_T) {
-      uint64_t xq[4];
+    uint64_t xn[4];  // the next chunk's keys load while this chunk's are inserted
+    auto load = [&](uint32_t e0) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t e = e0 + u * TB_T + threadIdx.x;
-        xq[u] = 0;
+        xn[u] = 0;
         if (e < m) {
           uint32_t lo = 0;
 #pragma unroll
           for (uint32_t step = TA_GRID / 2; step; step >>= 1)
             if (lo + step < nwg && soff[lo + step] <= e) lo += step;
-          xq[u] = src[(uint64_t)lo * slab + (e - soff[lo])];
+          xn[u] = src[(uint64_t)lo * slab + (e - soff[lo])];
         }
       }
+    };
+    load(0);
+    for (uint32_t e0 = 0; e0 < m; e0 += 4 * TB_T) {
+      uint64_t xq[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xq[u] = xn[u];
+      load(e0 + 4 * TB_T);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (xq[u] && lds_slot(lset, LB, xq[u]) == ~0u) s_full = 1;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# rocprofv3 kernel stats of one bench config: tools/r04_prof.sh TAG CONFIG [extra bench args]
+# rocprofv3 kernel stats of one bench config: tools/prof_stats.sh TAG CONFIG [extra bench args]
 export TMPDIR=/tmp
 TAG=${1:-r04}; CFG=${2:-mesh}; shift 2
 mkdir -p gpurun_out/${TAG}_prof_${CFG}
