@@ -742,13 +742,21 @@ __global__ void __launch_bounds__(KS_T) k_key_slice(const void *__restrict__ buc
     for (uint32_t x = threadIdx.x; x < ESLICE / 2; x += KS_T) l[x] = g[x];
     __syncthreads();
     const KT *src = bucket + (uint64_t)b * bcap;
+    // the next chunk's keys load while this chunk's are inserted
+    KT kn[KS_PER];
+    auto load = [&](uint32_t x1) {
+#pragma unroll
+      for (int j = 0; j < (int)KS_PER; ++j) {
+        const uint32_t i = x1 + j * KS_T + threadIdx.x;
+        kn[j] = i < m ? src[i] : (KT)0;
+      }
+    };
+    load(0);
     for (uint32_t x0 = 0; x0 < m; x0 += KS_T * KS_PER) {
       KT k[KS_PER];
 #pragma unroll
-      for (int j = 0; j < (int)KS_PER; ++j) {
-        const uint32_t i = x0 + j * KS_T + threadIdx.x;
-        k[j] = i < m ? src[i] : (KT)0;
-      }
+      for (int j = 0; j < (int)KS_PER; ++j) k[j] = kn[j];
+      load(x0 + KS_T * KS_PER);
 #pragma unroll
       for (int j = 0; j < (int)KS_PER; ++j) {
         if (x0 + j * KS_T + threadIdx.x >= m || (flags & F_TRIPLE_OVERFLOW)) continue;  // (a full slice: the run is repeated larger)
