@@ -63,10 +63,13 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE_WAVES) k4_tile(const uint8_t *__
   }
   chain_lds_init(L);
   if (threadIdx.x == 0) wcount = 0;
-  // each slot's endpoint and SERVER element hash (k_chain_etab)
+  // each non-CLIENT slot's endpoint and SERVER element hash (k_chain_etab;
+  // a CLIENT slot's record holds neither, so half the window skips the gather)
   uint3 e[WPW];
 #pragma unroll
-  for (int q = 0; q < WPW; ++q) e[q] = *reinterpret_cast<const uint3 *>(etab + (sh[q] < n_shapes ? sh[q] : 0));
+  for (int q = 0; q < WPW; ++q)
+    e[q] = k[q] == KIND_CLIENT ? make_uint3(0, 0, 0)
+                               : *reinterpret_cast<const uint3 *>(etab + (sh[q] < n_shapes ? sh[q] : 0));
   // window -> LDS records {element hash, endpoint, local contracted parent | kind << 16}
   bool other = false;  // a span neither SERVER nor CLIENT in the window (rows' lastUsage path)
 #pragma unroll
