@@ -154,7 +154,8 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
   };
   auto gather_ep = [&]() {
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) e[q] = etab[sh[q] < n_shapes ? sh[q] : 0];
+    for (int q = 0; q < CPW; ++q)  // (a CLIENT slot's record holds no endpoint: no gather)
+      e[q] = k[q] == KIND_CLIENT ? make_uint4(0, 0, 0, 0) : etab[sh[q] < n_shapes ? sh[q] : 0];
   };
   if (threadIdx.x == 0) dcnt = wcnt = wcount = 0;
   if (threadIdx.x < (1u << KB1_MAX)) lbin[threadIdx.x] = 0;
