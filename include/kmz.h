@@ -247,6 +247,17 @@ int kmz_get_span_links(kmz_ctx *ctx, uint32_t *cparent, uint64_t *rowpos, uint64
  * Pinned (page-locked) output buffers copy fastest. */
 int kmz_fetch(kmz_ctx *ctx, kmz_group *groups, uint64_t groups_cap, uint64_t *triples, uint64_t triples_cap,
               uint64_t *n_triples, kmz_endpoint *endpoints, uint64_t endpoints_cap);
+/* kmz_fetch in two halves, for a loop over consecutive batches: _begin takes
+ * a device copy of the run's three result sets (on the run's stream, so the
+ * next kmz_run may overwrite its own buffers at once) and queues their copies
+ * to the host on a transfer stream of the context; _end waits for them and
+ * fills `endpoints`.  The next batch's kernels run while the results of this
+ * one cross PCIe.  The output buffers must stay valid and untouched until
+ * _end; a _begin while one is open ends that one first.  *n_triples is set
+ * by _begin. */
+int kmz_fetch_begin(kmz_ctx *ctx, kmz_group *groups, uint64_t groups_cap, uint64_t *triples, uint64_t triples_cap,
+                    uint64_t *n_triples, kmz_endpoint *endpoints, uint64_t endpoints_cap);
+int kmz_fetch_end(kmz_ctx *ctx);
 
 /* ---- reduced graph in exact order ------------------- */
 /* The cache layer holds EndpointDependencies reduced to one merged row per
@@ -457,6 +468,11 @@ void kmz_host_free(void *p);
 #define KMZ_K_JOINWALK 16 /* K2 + K4 fused: k_join_chain (join, contraction, chain walk) */
 #define KMZ_K_COUNT 17
 int kmz_set_profiling(kmz_ctx *ctx, int on);
+/* time only the kernel ids whose bit is set in mask (1 << KMZ_K_*; 0 = off).
+ * Each timed id costs an event pair on the stream, and each event record a
+ * short pipeline gap before the next launch: a benchmark that prices one
+ * kernel times only that one (bench.py). */
+int kmz_set_profiling_mask(kmz_ctx *ctx, uint32_t mask);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);
 

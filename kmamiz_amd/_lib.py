@@ -167,6 +167,8 @@ SIGNATURES = [
     ("kmz_json_known", C.c_int, [_P, _P, _P]),
     ("kmz_json_forget", C.c_int, [_P]),
     ("kmz_fetch", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64]),
+    ("kmz_fetch_begin", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64]),
+    ("kmz_fetch_end", C.c_int, [_P]),
     ("kmz_group_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_endpoint_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_partials_size", C.c_int, [_P, C.c_int, C.POINTER(C.c_uint64)]),
@@ -196,6 +198,7 @@ SIGNATURES = [
     ("kmz_host_alloc", _P, [C.c_uint64]),
     ("kmz_host_free", None, [_P]),
     ("kmz_set_profiling", C.c_int, [_P, C.c_int]),
+    ("kmz_set_profiling_mask", C.c_int, [_P, C.c_uint32]),
     ("kmz_kernel_times", C.c_int, [_P, _P, _P, C.c_int]),
     ("kmz_synth_describe", C.c_int, [C.c_int, C.POINTER(SynthDesc)]),
     ("kmz_synth_load", C.c_int, [_P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),

@@ -150,7 +150,18 @@ struct kmz_ctx {
   bool overlap = false;  // this run uses the side stream
 
   // profiling
+  // kmz_fetch_begin / _end: transfer stream, snapshot of the results, the open fetch
+  hipStream_t xfer = nullptr;
+  hipEvent_t ev_snap = nullptr;
+  DevBuf f_grp, f_trip, f_ep;
+  void *fhep = nullptr;
+  size_t fhep_bytes = 0;
+  bool fetch_open = false;
+  kmz_endpoint *f_eps = nullptr;
+  uint32_t f_ndep = 0;
+
   bool prof = false;
+  uint32_t prof_mask = 0;  // kernel ids timed while prof (kmz_set_profiling_mask)
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
   double ms[KMZ_K_COUNT] = {0};
@@ -208,15 +219,16 @@ hipEvent_t ev_get(kmz_ctx *c) {
 struct Timed {
   kmz_ctx *c;
   EventPair ep;
-  Timed(kmz_ctx *ctx, int k) : c(ctx) {
-    if (!c->prof) return;
+  bool on;
+  Timed(kmz_ctx *ctx, int k) : c(ctx), on(ctx->prof && ((ctx->prof_mask >> k) & 1u)) {
+    if (!on) return;
     ep.kernel = k;
     ep.a = ev_get(c);
     ep.b = ev_get(c);
     hipEventRecord(ep.a, c->stream);
   }
   ~Timed() {
-    if (!c->prof) return;
+    if (!on) return;
     hipEventRecord(ep.b, c->stream);
     c->pending.push_back(ep);
   }
@@ -335,6 +347,7 @@ void kmz_destroy(kmz_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
+  if (c->xfer) hipStreamSynchronize(c->xfer);
   harvest(c);
   for (auto e : c->pool) hipEventDestroy(e);
   DevBuf *bufs[] = {&c->in_sid, &c->in_pid,    &c->in_kind,  &c->in_shape,  &c->in_status, &c->in_dur,
@@ -351,13 +364,16 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->o_key, &c->o_val, &c->o_out,
                     &c->o_rts, &c->o_rsh, &c->j_buf, &c->j_elem, &c->j_state, &c->j_jsc, &c->j_mask,
                     &c->j_cnt, &c->j_off, &c->j_csc, &c->j_small, &c->j_starts, &c->j_slices, &c->j_tslot,
-                    &c->j_stab, &c->j_ttab, &c->j_reps, &c->j_smap, &c->j_tmap};
+                    &c->j_stab, &c->j_ttab, &c->j_reps, &c->j_smap, &c->j_tmap, &c->f_grp, &c->f_trip, &c->f_ep};
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   for (auto &g : c->graphs)
     if (g.exec) hipGraphExecDestroy(g.exec);
   if (c->hpin) hipHostFree(c->hpin);
   if (c->hep) hipHostFree(c->hep);
+  if (c->fhep) hipHostFree(c->fhep);
+  if (c->xfer) hipStreamDestroy(c->xfer);
+  if (c->ev_snap) hipEventDestroy(c->ev_snap);
   if (c->tl_host) hipHostFree(c->tl_host);
   if (c->side) {
     hipStreamSynchronize(c->side);
@@ -1738,27 +1754,67 @@ int kmz_get_triples(kmz_ctx *c, uint64_t *out, uint64_t cap, uint64_t *n_out) {
   return kmz_fetch(c, nullptr, 0, out, cap, n_out, nullptr, 0);
 }
 
-int kmz_fetch(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint64_t tcap, uint64_t *n_trip,
-              kmz_endpoint *eps, uint64_t ecap) {
+namespace {
+
+// kmz_fetch's argument checks; the edge-key count from the run's read-back
+int fetch_check(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint64_t tcap, uint64_t *n_trip,
+                kmz_endpoint *eps, uint64_t ecap, uint64_t *nt) {
   if (!c) return KMZ_E_ARG;
   const bool want_deps = trip || n_trip || eps;
   if (groups && !(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
   if (want_deps && !(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
   if (groups && gcap < c->G) return fail(c, KMZ_E_ARG, "output too small");
   if (eps && ecap < c->n_dep) return fail(c, KMZ_E_ARG, "output too small");
-  uint64_t nt = 0;
+  *nt = 0;
   if (want_deps) {
     if (c->hpin_valid) {
-      nt = reinterpret_cast<const unsigned long long *>(reinterpret_cast<const unsigned int *>(c->hpin) + C_COUNT)[S_TRIP_OUT];
+      *nt = reinterpret_cast<const unsigned long long *>(reinterpret_cast<const unsigned int *>(c->hpin) + C_COUNT)[S_TRIP_OUT];
     } else {
       unsigned long long s[S_COUNT];
       HIPCHK(c, hipMemcpyAsync(s, c->stats64.p, sizeof(s), hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
-      nt = s[S_TRIP_OUT];
+      *nt = s[S_TRIP_OUT];
     }
-    if (n_trip) *n_trip = nt;
-    if (trip && tcap < nt) return fail(c, KMZ_E_ARG, "output too small");
+    if (n_trip) *n_trip = *nt;
+    if (trip && tcap < *nt) return fail(c, KMZ_E_ARG, "output too small");
   }
+  return KMZ_OK;
+}
+
+// per endpoint {last timestamp ^ bias, first row << 1 | internal} -> kmz_endpoint
+void endpoints_from(const uint64_t *h, uint32_t n_dep, kmz_endpoint *eps) {
+  for (uint32_t e = 0; e < n_dep; ++e) {
+    const uint64_t tsx = h[e], f = h[n_dep + e];
+    eps[e].last_ts = tsx == 0 ? INT64_MIN : (int64_t)(tsx ^ TS_BIAS);
+    eps[e].has_row = f != ~0ull;
+    eps[e].first_row = f == ~0ull ? ~0ull : (f >> 1);
+    eps[e].external = f == ~0ull ? 0u : (uint32_t)((f & 1) == 0);
+  }
+}
+
+int pinned_staging(kmz_ctx *c, void *&p, size_t &have, size_t bytes) {
+  if (have >= bytes) return KMZ_OK;
+  if (p) hipHostFree(p);
+  p = nullptr;
+  have = 0;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    p = nullptr;
+    return fail(c, KMZ_E_HIP, "hipHostMalloc (endpoint staging)");
+  }
+  have = bytes;
+  return KMZ_OK;
+}
+
+}  // namespace
+
+int kmz_fetch(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint64_t tcap, uint64_t *n_trip,
+              kmz_endpoint *eps, uint64_t ecap) {
+  if (c && c->fetch_open) {
+    const int r = kmz_fetch_end(c);
+    if (r) return r;
+  }
+  uint64_t nt = 0;
+  if (int r = fetch_check(c, groups, gcap, trip, tcap, n_trip, eps, ecap, &nt)) return r;
   bool any = false;
   if (groups && c->G) {
     HIPCHK(c, hipMemcpyAsync(groups, c->grp_final.p, (size_t)c->G * sizeof(kmz_group), hipMemcpyDeviceToHost, c->stream));
@@ -1770,30 +1826,56 @@ int kmz_fetch(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint
   }
   const size_t eb = (size_t)c->n_dep * 16;
   if (eps && c->n_dep) {
-    if (c->hep_bytes < eb) {
-      if (c->hep) hipHostFree(c->hep);
-      c->hep = nullptr;
-      c->hep_bytes = 0;
-      if (hipHostMalloc(&c->hep, eb, hipHostMallocDefault) != hipSuccess) {
-        c->hep = nullptr;
-        return fail(c, KMZ_E_HIP, "hipHostMalloc (endpoint staging)");
-      }
-      c->hep_bytes = eb;
-    }
+    if (int r = pinned_staging(c, c->hep, c->hep_bytes, eb)) return r;
     HIPCHK(c, hipMemcpyAsync(c->hep, c->epp.p, eb, hipMemcpyDeviceToHost, c->stream));
     any = true;
   }
   if (any) HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (eps) {
-    const uint64_t *h = reinterpret_cast<const uint64_t *>(c->hep);
-    for (uint32_t e = 0; e < c->n_dep; ++e) {
-      const uint64_t tsx = h[e], f = h[c->n_dep + e];
-      eps[e].last_ts = tsx == 0 ? INT64_MIN : (int64_t)(tsx ^ TS_BIAS);
-      eps[e].has_row = f != ~0ull;
-      eps[e].first_row = f == ~0ull ? ~0ull : (f >> 1);
-      eps[e].external = f == ~0ull ? 0u : (uint32_t)((f & 1) == 0);
-    }
+  if (eps) endpoints_from(reinterpret_cast<const uint64_t *>(c->hep), c->n_dep, eps);
+  return KMZ_OK;
+}
+
+int kmz_fetch_begin(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint64_t tcap, uint64_t *n_trip,
+                    kmz_endpoint *eps, uint64_t ecap) {
+  if (c && c->fetch_open) {
+    const int r = kmz_fetch_end(c);
+    if (r) return r;
   }
+  uint64_t nt = 0;
+  if (int r = fetch_check(c, groups, gcap, trip, tcap, n_trip, eps, ecap, &nt)) return r;
+  if (!c->xfer) {
+    HIPCHK(c, hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_snap, hipEventDisableTiming));
+  }
+  const size_t gb = groups ? (size_t)c->G * sizeof(kmz_group) : 0, tb = trip ? (size_t)nt * 8 : 0,
+               eb = eps ? (size_t)c->n_dep * 16 : 0;
+  // the device copy: the next run is free to overwrite the results at once
+  if (ensure(c, c->f_grp, gb) || ensure(c, c->f_trip, tb) || ensure(c, c->f_ep, eb))
+    return fail(c, KMZ_E_HIP, "hipMalloc (fetch snapshot)");
+  if (eb) {
+    if (int r = pinned_staging(c, c->fhep, c->fhep_bytes, eb)) return r;
+  }
+  if (gb) HIPCHK(c, hipMemcpyAsync(c->f_grp.p, c->grp_final.p, gb, hipMemcpyDeviceToDevice, c->stream));
+  if (tb) HIPCHK(c, hipMemcpyAsync(c->f_trip.p, c->trip_out.p, tb, hipMemcpyDeviceToDevice, c->stream));
+  if (eb) HIPCHK(c, hipMemcpyAsync(c->f_ep.p, c->epp.p, eb, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_snap, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->xfer, c->ev_snap, 0));
+  if (gb) HIPCHK(c, hipMemcpyAsync(groups, c->f_grp.p, gb, hipMemcpyDeviceToHost, c->xfer));
+  if (tb) HIPCHK(c, hipMemcpyAsync(trip, c->f_trip.p, tb, hipMemcpyDeviceToHost, c->xfer));
+  if (eb) HIPCHK(c, hipMemcpyAsync(c->fhep, c->f_ep.p, eb, hipMemcpyDeviceToHost, c->xfer));
+  c->fetch_open = true;
+  c->f_eps = eps;
+  c->f_ndep = eb ? c->n_dep : 0;
+  return KMZ_OK;
+}
+
+int kmz_fetch_end(kmz_ctx *c) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->fetch_open) return KMZ_OK;
+  c->fetch_open = false;
+  HIPCHK(c, hipStreamSynchronize(c->xfer));
+  if (c->f_eps && c->f_ndep) endpoints_from(reinterpret_cast<const uint64_t *>(c->fhep), c->f_ndep, c->f_eps);
+  c->f_eps = nullptr;
   return KMZ_OK;
 }
 
@@ -2367,9 +2449,12 @@ void kmz_host_free(void *p) {
   if (p) (void)hipHostFree(p);
 }
 
-int kmz_set_profiling(kmz_ctx *c, int on) {
+int kmz_set_profiling(kmz_ctx *c, int on) { return kmz_set_profiling_mask(c, on ? (1u << KMZ_K_COUNT) - 1 : 0u); }
+
+int kmz_set_profiling_mask(kmz_ctx *c, uint32_t mask) {
   if (!c) return KMZ_E_ARG;
-  c->prof = on != 0;
+  c->prof_mask = mask & ((1u << KMZ_K_COUNT) - 1);
+  c->prof = c->prof_mask != 0;
   // create the timing events now, and record each once (the first record of
   // an event allocates its completion signal: ~0.5 ms, not inside a timed run)
   std::vector<hipEvent_t> tmp;

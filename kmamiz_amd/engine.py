@@ -333,6 +333,35 @@ class Engine:
                                               len(e) if deps else 0))
         return g, t, e
 
+    def fetch_begin(self, groups: bool = True, deps: bool = True, keys: bool = True):
+        """First half of ``fetch`` for a loop over consecutive batches
+        (kmz_fetch_begin): the results of the last run are copied on the
+        device and queued to the host on a transfer stream, so the next run's
+        kernels overlap the copies.  ``fetch_end()`` returns them.  The pinned
+        buffers alternate between two sets: a result stays valid until the
+        second fetch after it."""
+        info = self.info()
+        keys = keys and deps
+        slot = self._fslot = getattr(self, "_fslot", 0) ^ 1
+        g = self._pinned_array(f"groups{slot}", info["n_groups"], L.GROUP_DTYPE) if groups else None
+        t = self._pinned_array(f"triples{slot}", info["n_triples"], np.uint64) if keys else None
+        e = np.zeros(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE) if deps else None
+        n = C.c_uint64()
+        L.check(self.ctx, self._lib.kmz_fetch_begin(self.ctx, L.ptr(g) if groups else None, len(g) if groups else 0,
+                                                    L.ptr(t) if keys else None, len(t) if keys else 0,
+                                                    C.byref(n) if deps else None, L.ptr(e) if deps else None,
+                                                    len(e) if deps else 0))
+        self._fopen = (g, t, e)
+        return self._fopen
+
+    def fetch_end(self):
+        """-> (groups, triples, endpoints) of the open ``fetch_begin`` (None
+        if none is open), after its copies have landed."""
+        out = getattr(self, "_fopen", None)
+        L.check(self.ctx, self._lib.kmz_fetch_end(self.ctx))
+        self._fopen = None
+        return out
+
     def span_links(self):
         cp = np.zeros(self.n, dtype=np.uint32)
         rp = np.zeros(self.n, dtype=np.uint64)
@@ -451,8 +480,17 @@ class Engine:
         return order, out["wsum"][order], out["count"][order], out["err"][order]
 
     # ---- profiling -------------------------------------------------------------
-    def set_profiling(self, on: bool):
-        L.check(self.ctx, self._lib.kmz_set_profiling(self.ctx, 1 if on else 0))
+    def set_profiling(self, on):
+        """True / False: time every kernel id, or none.  A collection of
+        names from ``_lib.KERNELS``: time only those (each timed id adds an
+        event pair, i.e. launch gaps, to the run)."""
+        if isinstance(on, bool) or on is None:
+            L.check(self.ctx, self._lib.kmz_set_profiling(self.ctx, 1 if on else 0))
+        else:
+            mask = 0
+            for k in on:
+                mask |= 1 << L.KERNELS.index(k)
+            L.check(self.ctx, self._lib.kmz_set_profiling_mask(self.ctx, mask))
 
     def kernel_times(self, reset: bool = False) -> dict:
         ms = np.zeros(len(L.KERNELS), dtype=np.float64)

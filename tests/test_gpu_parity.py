@@ -1353,3 +1353,45 @@ def test_graph_replay_equals_direct_runs(config, ntr):
     finally:
         on.close()
         off.close()
+
+
+def test_pipelined_fetch_equals_fetch(engine):
+    """kmz_fetch_begin / _end (bench.py's loop: one batch's results cross PCIe
+    while the next batch's kernels run) return what kmz_fetch returns for each
+    batch, although the next run overwrites the device results before _end."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS
+    ranges = ((0, 3000), (3000, 5200))
+    want = []
+    for a, b in ranges:
+        engine.load_synthetic(synth.MESH, synth.SEED, a, b)
+        engine.run(flags)
+        g, k, e = engine.fetch()
+        want.append((g.copy(), np.sort(k), e.copy()))
+    assert want[0][0].tobytes() != want[1][0].tobytes()
+    engine.load_synthetic(synth.MESH, synth.SEED, *ranges[0])
+    engine.run(flags)
+    engine.fetch_begin()
+    engine.load_synthetic(synth.MESH, synth.SEED, *ranges[1])
+    engine.run(flags)  # (overwrites the first batch's device results)
+
+    def same(got, i):
+        g, k, e = got
+        wg, wk, we = want[i]
+        assert g.tobytes() == wg.tobytes()
+        assert np.array_equal(np.sort(k), wk)
+        assert e.tobytes() == we.tobytes()
+
+    same(engine.fetch_end(), 0)
+    first = engine.fetch_begin()
+    engine.run(flags)  # a run while the second batch's copies are in flight
+    engine.fetch_begin()  # (a _begin ends the open fetch first)
+    same(first, 1)
+    same(engine.fetch_end(), 1)
+    assert engine.fetch_end() is None
+    # without keys (the service tail's fetch) and without deps
+    engine.fetch_begin(keys=False)
+    g, k, e = engine.fetch_end()
+    assert k is None and g.tobytes() == want[1][0].tobytes() and e.tobytes() == want[1][2].tobytes()
