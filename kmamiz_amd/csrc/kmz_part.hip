@@ -298,6 +298,9 @@ static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32
 // block global); k3_first_fix turns blocks into span indices.
 constexpr int K3RT = 256;
 constexpr uint32_t K3RB = 64;  // runs per wave batch (one per lane)
+#ifndef KMZ_K3_U
+#define KMZ_K3_U 4  // records per lane in flight in k3_reduce_bal's record loop
+#endif
 #ifndef KMZ_K3_COND
 #define KMZ_K3_COND 1  // max / min atomics only when a plain read says they move
 #endif
@@ -526,10 +529,14 @@ __device__ __forceinline__ void k3_reduce_items(const uint64_t *__restrict__ poo
   unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
                      *a_fst = acc + 5 * K3R;
   uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
-  constexpr uint32_t U = 4;
+  constexpr uint32_t U = KMZ_K3_U;
+  // each batch's directory words are loaded during the batch before it
+  uint32_t xn = tb + (uint64_t)w * K3RB + lane < te ? row[tb + (uint64_t)w * K3RB + lane] : 0;
   for (uint64_t k0 = tb + (uint64_t)w * K3RB; k0 < te; k0 += (uint64_t)NW * K3RB) {
     const uint64_t k = k0 + lane;  // this lane's run: tile k
-    const uint32_t x = k < te ? row[k] : 0;
+    const uint32_t x = xn;
+    const uint64_t kn = k + (uint64_t)NW * K3RB;
+    xn = kn < te ? row[kn] : 0;
     const uint32_t o = x >> 16;
     const uint32_t c = (o + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;
     uint32_t incl = c;

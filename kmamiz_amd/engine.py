@@ -325,7 +325,7 @@ class Engine:
         keys = keys and deps
         g = self._pinned_array("groups", info["n_groups"], L.GROUP_DTYPE) if groups else None
         t = self._pinned_array("triples", info["n_triples"], np.uint64) if keys else None
-        e = np.zeros(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE) if deps else None
+        e = np.empty(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE) if deps else None  # (kmz_fetch sets every entry)
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_fetch(self.ctx, L.ptr(g) if groups else None, len(g) if groups else 0,
                                               L.ptr(t) if keys else None, len(t) if keys else 0,
@@ -345,7 +345,7 @@ class Engine:
         slot = self._fslot = getattr(self, "_fslot", 0) ^ 1
         g = self._pinned_array(f"groups{slot}", info["n_groups"], L.GROUP_DTYPE) if groups else None
         t = self._pinned_array(f"triples{slot}", info["n_triples"], np.uint64) if keys else None
-        e = np.zeros(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE) if deps else None
+        e = np.empty(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE) if deps else None  # (set by kmz_fetch_end)
         n = C.c_uint64()
         L.check(self.ctx, self._lib.kmz_fetch_begin(self.ctx, L.ptr(g) if groups else None, len(g) if groups else 0,
                                                     L.ptr(t) if keys else None, len(t) if keys else 0,
