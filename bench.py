@@ -486,9 +486,10 @@ def main():
                 "step_frac": round(pipe_bytes / (secs / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "overhead_bytes": overhead,
                 "kernels": per_kernel,
-                "kernels_source": ("a profiled pass of the same --steps steps before the timed region; in the timed "
-                                   f"region only {dom}'s events ({kname}, `achieved`)" if args.kernel_times == "split"
-                                   else "every kernel's events inside the timed region"),
+                "kernels_source": ("a profiled pass of the same --steps steps before the timed region, every kernel "
+                                   "timed and on one stream; in the timed region (side-stream overlap on) only "
+                                   f"{dom}'s events ({kname}, `achieved`)" if args.kernel_times == "split"
+                                   else "every kernel's events inside the timed region (one stream)"),
                 "units": units,
             },
             "cpu_baseline": cpu,

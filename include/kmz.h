@@ -471,7 +471,9 @@ int kmz_set_profiling(kmz_ctx *ctx, int on);
 /* time only the kernel ids whose bit is set in mask (1 << KMZ_K_*; 0 = off).
  * Each timed id costs an event pair on the stream, and each event record a
  * short pipeline gap before the next launch: a benchmark that prices one
- * kernel times only that one (bench.py). */
+ * kernel times only that one (bench.py).  While more than one id is timed,
+ * runs keep every kernel on one stream (no side-stream overlap), so that each
+ * kernel's time is its own. */
 int kmz_set_profiling_mask(kmz_ctx *ctx, uint32_t mask);
 /* ms[KMZ_K_COUNT] accumulated since the last reset, calls[KMZ_K_COUNT] */
 int kmz_kernel_times(kmz_ctx *ctx, double *ms, uint64_t *calls, int reset);

@@ -1607,17 +1607,21 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
   c->k4_now = (flags & KMZ_RUN_DEPS) ? k4_direct(c) : false;
   for (int attempt = 0; attempt < 8; ++attempt) {
     // K3 (+ the certificate, see run_join) on the side stream while the main
-    // stream joins and walks (KMZ_ABLATE bit 25: serial, for comparison)
-    // Only small batches (< 2^23 spans) overlap: they are launch- and
-    // latency-bound (Bookinfo 1M: 0.369 -> 0.323 ms/step).  At 10^8 spans every
-    // kernel fills the GPU by itself, overlap buys <= 3 % (mesh 5.29 -> 5.12 ms)
-    // or loses (config 5: 19.6 -> 25.7 ms), and it blurs the per-kernel
-    // roofline accounting (profiles/r01_overlap_ab/).  KMZ_ABLATE bit 27 forces it.
-    // Below 2^17 spans (a 2 500-trace tick) the second stream's fork / join
-    // costs more than the overlap gives: Bookinfo 164 -> 149 us, mesh
-    // 320 -> 300 us per run serial (tools/bench_tick.py).
+    // stream joins and walks (KMZ_ABLATE bit 25: serial, for comparison).
+    // Small batches are launch- and latency-bound (Bookinfo 1M: 0.369 -> 0.323
+    // ms/step).  At 10^8 spans the kernels of round 1 each filled the GPU and
+    // overlap bought <= 3 % or lost (profiles/r01_overlap_ab/); since round 4
+    // the VALU-bound join shares the CUs with the memory-bound K3, and the
+    // latency-bound walk with the certificate: mesh 3.96 -> 3.76, config 5
+    // 8.56 -> 8.43 ms/step (profiles/r04/ab/overlap/).  Below 2^17 spans (a
+    // 2 500-trace tick) the second stream's fork / join costs more than the
+    // overlap gives: Bookinfo 164 -> 149 us, mesh 320 -> 300 us per run serial
+    // (tools/bench_tick.py).  While more than one kernel id is timed
+    // (kmz_set_profiling_mask) runs stay on one stream, so that each kernel's
+    // time is its own.  KMZ_ABLATE bit 27 forces the overlap.
+    const bool timing_many = c->prof && (c->prof_mask & (c->prof_mask - 1));
     c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25)) &&
-                 ((c->n >= (1ull << 17) && c->n < (1ull << 23)) || (c->ablate & (1u << 27)));
+                 ((c->n >= (1ull << 17) && !timing_many) || (c->ablate & (1u << 27)));
     int r = run_enqueue_graphed(c, flags, links, h, s64);
     if (r) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
