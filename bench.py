@@ -233,20 +233,33 @@ def main():
         return now
 
     def service_tail():
+        # the device half: what reads this run's buffers (the edge keys where
+        # the run left them in HBM; the combined groups)
         tp = time.perf_counter()
-        t = run_tail(eng, tmaps)  # reads the edge keys where the run left them, in HBM
+        t = run_tail(eng, tmaps)
         tp = mark("tail_run", tp)
-        state["metrics"] = t.metrics()
-        tp = mark("tail_metrics", tp)
         # RiskAnalyzer.RealtimeRisk: the per-service sums over the combined
         # groups on the device (kmz_service_sums, bit-equal to the host's row
         # sums), the rest over the ~10^3 services on the host
         sums = eng.service_sums()
-        tp = mark("service_sums", tp)
+        mark("service_sums", tp)
+        state["tail_host"] = (t, sums)
+
+    def tail_host():
+        # the host half (metrics, risk): pure host work on what the device half
+        # read back, done while the next step's run is on the GPU
+        if "tail_host" not in state:
+            return
+        t, sums = state.pop("tail_host")
+        tp = time.perf_counter()
+        state["metrics"] = t.metrics()
+        tp = mark("tail_metrics", tp)
         state["risk"] = realtime_risk_from_sums(t, sid_names, *sums)
         mark("risk", tp)
 
     def fetch_done():
+        if tail_on:
+            tail_host()
         out = eng.fetch_end()
         if out is not None:
             state["groups"], state["keys"], state["endpoints"] = out
@@ -258,7 +271,11 @@ def main():
         guard = kdist.IdGuard(eng, dev).start() if world > 1 else None
         state["guard_start_s"] = state.get("guard_start_s", 0.0) + (time.perf_counter() - tg)
         tp = time.perf_counter()
-        eng.run(flags)
+        eng.run_begin(flags)
+        if tail_on:
+            tail_host()  # the previous step's host finish, beside this step's kernels
+            tp = mark("run_begin+tail_host", tp)
+        eng.run_end()
         tp = mark("run", tp)
         if world > 1:
             gw = eng.partials_words(L.PART_GROUPS)

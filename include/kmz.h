@@ -224,6 +224,13 @@ int kmz_load(kmz_ctx *ctx, const kmz_spans *spans, const kmz_shapes *shapes, int
 
 /* ---- compute (asynchronous on the context stream) ------------------------ */
 int kmz_run(kmz_ctx *ctx, uint32_t flags);
+/* kmz_run in two halves: _begin validates and enqueues the run (with its
+ * read-back) and returns at once; _end waits for it, repeats it where a table
+ * must grow or a seed change, and publishes its results.  Between the two the
+ * caller may do host work (e.g. the previous batch's service-tail finish);
+ * every other call on the context fails with KMZ_E_STATE until _end. */
+int kmz_run_begin(kmz_ctx *ctx, uint32_t flags);
+int kmz_run_end(kmz_ctx *ctx);
 
 /* ---- results (synchronise the stream) ------------------------------------- */
 int kmz_get_info(kmz_ctx *ctx, kmz_info *out);

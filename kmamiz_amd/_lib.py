@@ -153,6 +153,8 @@ SIGNATURES = [
     ("kmz_sync", C.c_int, [_P]),
     ("kmz_load", C.c_int, [_P, C.POINTER(Spans), C.POINTER(Shapes), C.c_int]),
     ("kmz_run", C.c_int, [_P, C.c_uint32]),
+    ("kmz_run_begin", C.c_int, [_P, C.c_uint32]),
+    ("kmz_run_end", C.c_int, [_P]),
     ("kmz_get_info", C.c_int, [_P, C.POINTER(Info)]),
     ("kmz_get_groups", C.c_int, [_P, _P, C.c_uint64]),
     ("kmz_get_endpoints", C.c_int, [_P, _P, C.c_uint64]),

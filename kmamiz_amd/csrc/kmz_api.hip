@@ -157,6 +157,9 @@ struct kmz_ctx {
   void *fhep = nullptr;
   size_t fhep_bytes = 0;
   bool fetch_open = false;
+  // kmz_run_begin / _end: a run enqueued and not yet waited for
+  bool run_open = false;
+  uint32_t run_flags = 0;
   kmz_endpoint *f_eps = nullptr;
   uint32_t f_ndep = 0;
 
@@ -174,6 +177,8 @@ int fail(kmz_ctx *c, int code, const std::string &msg) {
   if (c) c->err = msg;
   return code;
 }
+
+int run_busy(kmz_ctx *c) { return fail(c, KMZ_E_STATE, "a run is open: kmz_run_end first"); }
 
 #define HIPCHK(c, x)                                                                        \
   do {                                                                                      \
@@ -346,6 +351,7 @@ kmz_ctx *kmz_create(int device, void *stream) {
 void kmz_destroy(kmz_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
+  if (c->side) hipStreamSynchronize(c->side);
   hipStreamSynchronize(c->stream);
   if (c->xfer) hipStreamSynchronize(c->xfer);
   harvest(c);
@@ -389,6 +395,7 @@ const char *kmz_last_error(kmz_ctx *c) { return c ? c->err.c_str() : "null conte
 
 int kmz_sync(kmz_ctx *c) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   harvest(c);
   return KMZ_OK;
@@ -415,6 +422,7 @@ static int load_shapes(kmz_ctx *c, const kmz_shapes *sh) {
 
 int kmz_load(kmz_ctx *c, const kmz_spans *s, const kmz_shapes *sh, int where) {
   if (!c || !s) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   hipSetDevice(c->device);
   if (s->n >= 0xFFFFFFFFull) return fail(c, KMZ_E_ARG, "batch too large (n must be < 2^32-1)");
   if (s->n && (!s->span_id || !s->parent_id || !s->kind || !s->shape || !s->status || !s->duration || !s->timestamp))
@@ -539,6 +547,7 @@ int json_keys(kmz_ctx *c, const char *json, int mem, uint32_t nf, const std::vec
 
 int kmz_json_known(kmz_ctx *c, uint32_t *shape_of_raw, uint32_t *status_of_raw) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->j_ready) return fail(c, KMZ_E_STATE, "kmz_json_known before a successful kmz_json_parse");
   for (size_t k = 0; shape_of_raw && k < c->j_skeys.size(); ++k) {
     auto it = c->j_known_s.find(c->j_skeys[k]);
@@ -553,6 +562,7 @@ int kmz_json_known(kmz_ctx *c, uint32_t *shape_of_raw, uint32_t *status_of_raw) 
 
 int kmz_json_forget(kmz_ctx *c) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   c->j_known_s.clear();
   c->j_known_t.clear();
   return KMZ_OK;
@@ -561,6 +571,7 @@ int kmz_json_forget(kmz_ctx *c) {
 int kmz_json_parse(kmz_ctx *c, const char *json, uint64_t len, int mem, uint64_t *n_spans, uint32_t *n_shapes,
                    uint32_t *n_statuses) {
   if (!c || (!json && len) || !n_spans || !n_shapes || !n_statuses) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   hipSetDevice(c->device);
   c->j_ready = false;
   c->loaded = false;  // the context's columns are rewritten
@@ -662,6 +673,7 @@ int kmz_json_parse(kmz_ctx *c, const char *json, uint64_t len, int mem, uint64_t
 
 int kmz_json_fields(kmz_ctx *c, uint64_t *shape_fields, uint64_t *status_fields) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->j_ready) return fail(c, KMZ_E_STATE, "kmz_json_fields before a successful kmz_json_parse");
   if (shape_fields && !c->j_sfields.empty()) memcpy(shape_fields, c->j_sfields.data(), c->j_sfields.size() * 8);
   if (status_fields && !c->j_tfields.empty()) memcpy(status_fields, c->j_tfields.data(), c->j_tfields.size() * 8);
@@ -671,6 +683,7 @@ int kmz_json_fields(kmz_ctx *c, uint64_t *shape_fields, uint64_t *status_fields)
 int kmz_json_load(kmz_ctx *c, const uint32_t *shape_of_raw, const uint32_t *status_of_raw, const kmz_shapes *shapes,
                   uint64_t index_base) {
   if (!c || !shapes) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->j_ready) return fail(c, KMZ_E_STATE, "kmz_json_load before a successful kmz_json_parse");
   const size_t ns = c->j_sslots.size(), nt = c->j_tslots.size();
   if ((ns && !shape_of_raw) || (nt && !status_of_raw)) return KMZ_E_ARG;
@@ -1370,6 +1383,7 @@ static int run_dep_order(kmz_ctx *c, uint64_t n_keys, bool dups) {
 int kmz_get_dep_entries(kmz_ctx *c, kmz_dep_entry *out, uint64_t cap, uint64_t *n_out, int64_t *row_ts,
                         uint32_t *row_shape, uint64_t row_cap) {
   if (!c || !n_out) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & KMZ_RUN_DEP_ORDER)) return fail(c, KMZ_E_STATE, "run with KMZ_RUN_DEPS|KMZ_RUN_DEP_ORDER first");
   *n_out = c->o_n;
   if (out && cap < c->o_n) return fail(c, KMZ_E_ARG, "output too small");
@@ -1402,6 +1416,7 @@ static int remap_results(kmz_ctx *c, uint32_t flags, bool links) {
 
 int kmz_set_index_map(kmz_ctx *c, const uint64_t *local_start, const uint64_t *global_start, uint64_t n_runs) {
   if (!c || (n_runs && (!local_start || !global_start))) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_set_index_map before kmz_load");
   if (n_runs == 0) {
     c->imap_n = 0;
@@ -1587,8 +1602,36 @@ static int run_enqueue_graphed(kmz_ctx *c, uint32_t flags, bool links, unsigned 
   return KMZ_OK;
 }
 
+// one attempt of a run: the stream layout, then every launch and the read-back
+static int run_attempt(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, unsigned long long *s64) {
+  const uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
+  // K3 (+ the certificate, see run_join) on the side stream while the main
+  // stream joins and walks (KMZ_ABLATE bit 25: serial, for comparison).
+  // Small batches are launch- and latency-bound (Bookinfo 1M: 0.369 -> 0.323
+  // ms/step).  At 10^8 spans the kernels of round 1 each filled the GPU and
+  // overlap bought <= 3 % or lost (profiles/r01_overlap_ab/); since round 4
+  // the VALU-bound join shares the CUs with the memory-bound K3, and the
+  // latency-bound walk with the certificate: mesh 3.96 -> 3.76, config 5
+  // 8.56 -> 8.43 ms/step (profiles/r04/ab/overlap/).  Below 2^17 spans (a
+  // 2 500-trace tick) the second stream's fork / join costs more than the
+  // overlap gives: Bookinfo 164 -> 149 us, mesh 320 -> 300 us per run serial
+  // (tools/bench_tick.py).  While more than one kernel id is timed
+  // (kmz_set_profiling_mask) runs stay on one stream, so that each kernel's
+  // time is its own.  KMZ_ABLATE bit 27 forces the overlap.
+  const bool timing_many = c->prof && (c->prof_mask & (c->prof_mask - 1));
+  c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25)) &&
+               ((c->n >= (1ull << 17) && !timing_many) || (c->ablate & (1u << 27)));
+  return run_enqueue_graphed(c, flags, links, h, s64);
+}
+
 int kmz_run(kmz_ctx *c, uint32_t flags) {
+  const int r = kmz_run_begin(c, flags);
+  return r ? r : kmz_run_end(c);
+}
+
+int kmz_run_begin(kmz_ctx *c, uint32_t flags) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return fail(c, KMZ_E_STATE, "kmz_run_begin while a run is open (kmz_run_end first)");
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_run before kmz_load");
   uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
   if (smode == (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG)) return fail(c, KMZ_E_ARG, "choose one stats identity per run");
@@ -1605,25 +1648,27 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
   unsigned int *h = reinterpret_cast<unsigned int *>(c->hpin);
   unsigned long long *s64 = reinterpret_cast<unsigned long long *>(h + C_COUNT);
   c->k4_now = (flags & KMZ_RUN_DEPS) ? k4_direct(c) : false;
+  if (int r = run_attempt(c, flags, links, h, s64)) return r;
+  c->run_open = true;
+  c->run_flags = flags;
+  return KMZ_OK;
+}
+
+// waits for the run's read-back; a run that must grow a table or change a
+// seed is repeated here (each repeat enqueued and waited for in turn)
+int kmz_run_end(kmz_ctx *c) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->run_open) return fail(c, KMZ_E_STATE, "kmz_run_end without kmz_run_begin");
+  c->run_open = false;
+  const uint32_t flags = c->run_flags;
+  const bool links = (flags & (KMZ_RUN_SPAN_LINKS | KMZ_RUN_DEP_ORDER)) != 0;
+  unsigned int *h = reinterpret_cast<unsigned int *>(c->hpin);
+  unsigned long long *s64 = reinterpret_cast<unsigned long long *>(h + C_COUNT);
   for (int attempt = 0; attempt < 8; ++attempt) {
-    // K3 (+ the certificate, see run_join) on the side stream while the main
-    // stream joins and walks (KMZ_ABLATE bit 25: serial, for comparison).
-    // Small batches are launch- and latency-bound (Bookinfo 1M: 0.369 -> 0.323
-    // ms/step).  At 10^8 spans the kernels of round 1 each filled the GPU and
-    // overlap bought <= 3 % or lost (profiles/r01_overlap_ab/); since round 4
-    // the VALU-bound join shares the CUs with the memory-bound K3, and the
-    // latency-bound walk with the certificate: mesh 3.96 -> 3.76, config 5
-    // 8.56 -> 8.43 ms/step (profiles/r04/ab/overlap/).  Below 2^17 spans (a
-    // 2 500-trace tick) the second stream's fork / join costs more than the
-    // overlap gives: Bookinfo 164 -> 149 us, mesh 320 -> 300 us per run serial
-    // (tools/bench_tick.py).  While more than one kernel id is timed
-    // (kmz_set_profiling_mask) runs stay on one stream, so that each kernel's
-    // time is its own.  KMZ_ABLATE bit 27 forces the overlap.
-    const bool timing_many = c->prof && (c->prof_mask & (c->prof_mask - 1));
-    c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25)) &&
-                 ((c->n >= (1ull << 17) && !timing_many) || (c->ablate & (1u << 27)));
-    int r = run_enqueue_graphed(c, flags, links, h, s64);
-    if (r) return r;
+    if (attempt > 0) {
+      int r = run_attempt(c, flags, links, h, s64);
+      if (r) return r;
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     harvest(c);
     if (h[C_FLAGS] & F_CTAB_DIRTY) c->ctab_dirty = true;
@@ -1702,6 +1747,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
 
 int kmz_get_graph_stats(kmz_ctx *c, uint64_t *launches, uint32_t *cached) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (launches) *launches = c->graph_launches;
   if (cached) {
     uint32_t k = 0;
@@ -1713,6 +1759,7 @@ int kmz_get_graph_stats(kmz_ctx *c, uint64_t *launches, uint32_t *cached) {
 
 int kmz_get_info(kmz_ctx *c, kmz_info *out) {
   if (!c || !out) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   unsigned int hb[C_COUNT];
   unsigned long long sb[S_COUNT];
   const unsigned int *h = hb;
@@ -1742,6 +1789,7 @@ int kmz_get_info(kmz_ctx *c, kmz_info *out) {
 
 int kmz_get_groups(kmz_ctx *c, kmz_group *out, uint64_t cap) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
   if (cap < c->G) return fail(c, KMZ_E_ARG, "output too small");
   if (c->G) HIPCHK(c, hipMemcpyAsync(out, c->grp_final.p, (size_t)c->G * sizeof(kmz_group), hipMemcpyDeviceToHost, c->stream));
@@ -1755,6 +1803,7 @@ int kmz_get_endpoints(kmz_ctx *c, kmz_endpoint *out, uint64_t cap) {
 
 int kmz_get_triples(kmz_ctx *c, uint64_t *out, uint64_t cap, uint64_t *n_out) {
   if (!c || !n_out) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   return kmz_fetch(c, nullptr, 0, out, cap, n_out, nullptr, 0);
 }
 
@@ -1813,6 +1862,7 @@ int pinned_staging(kmz_ctx *c, void *&p, size_t &have, size_t bytes) {
 
 int kmz_fetch(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint64_t tcap, uint64_t *n_trip,
               kmz_endpoint *eps, uint64_t ecap) {
+  if (c && c->run_open) return run_busy(c);
   if (c && c->fetch_open) {
     const int r = kmz_fetch_end(c);
     if (r) return r;
@@ -1841,6 +1891,7 @@ int kmz_fetch(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint
 
 int kmz_fetch_begin(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint64_t tcap, uint64_t *n_trip,
                     kmz_endpoint *eps, uint64_t ecap) {
+  if (c && c->run_open) return run_busy(c);
   if (c && c->fetch_open) {
     const int r = kmz_fetch_end(c);
     if (r) return r;
@@ -1875,6 +1926,7 @@ int kmz_fetch_begin(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip
 
 int kmz_fetch_end(kmz_ctx *c) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->fetch_open) return KMZ_OK;
   c->fetch_open = false;
   HIPCHK(c, hipStreamSynchronize(c->xfer));
@@ -1886,6 +1938,7 @@ int kmz_fetch_end(kmz_ctx *c) {
 int kmz_get_spans(kmz_ctx *c, uint64_t *span_id, uint64_t *parent_id, uint8_t *kind, uint32_t *shape,
                   uint16_t *status, uint32_t *duration, int64_t *timestamp, uint64_t cap) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->loaded) return fail(c, KMZ_E_STATE, "no batch loaded");
   if (cap < c->n) return fail(c, KMZ_E_ARG, "output too small");
   const uint64_t n = c->n;
@@ -1904,6 +1957,7 @@ int kmz_get_spans(kmz_ctx *c, uint64_t *span_id, uint64_t *parent_id, uint8_t *k
 
 int kmz_get_span_links(kmz_ctx *c, uint32_t *cparent, uint64_t *rowpos, uint64_t cap) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & KMZ_RUN_DEPS) || !c->links) return fail(c, KMZ_E_STATE, "run with KMZ_RUN_DEPS|KMZ_RUN_SPAN_LINKS first");
   if (cap < c->n) return fail(c, KMZ_E_ARG, "output too small");
   if (c->n) {
@@ -1916,6 +1970,7 @@ int kmz_get_span_links(kmz_ctx *c, uint32_t *cparent, uint64_t *rowpos, uint64_t
 
 int kmz_group_partials(kmz_ctx *c, void **dev_ptr, uint64_t *n_groups) {
   if (!c || !dev_ptr || !n_groups) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
   *dev_ptr = c->grp.p;
   *n_groups = c->G;
@@ -1924,6 +1979,7 @@ int kmz_group_partials(kmz_ctx *c, void **dev_ptr, uint64_t *n_groups) {
 
 int kmz_endpoint_partials(kmz_ctx *c, void **dev_ptr, uint64_t *n_ep) {
   if (!c || !dev_ptr || !n_ep) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
   *dev_ptr = c->epp.p;
   *n_ep = c->n_dep;
@@ -1932,6 +1988,7 @@ int kmz_endpoint_partials(kmz_ctx *c, void **dev_ptr, uint64_t *n_ep) {
 
 int kmz_partials_size(kmz_ctx *c, int which, uint64_t *words) {
   if (!c || !words) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (which == KMZ_PART_GROUPS) {
     if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
     *words = 6ull * c->G;
@@ -1955,6 +2012,7 @@ int kmz_partials_size(kmz_ctx *c, int which, uint64_t *words) {
 }
 
 int kmz_partials_copy(kmz_ctx *c, int which, void *buf, uint64_t words, int mem, int direction) {
+  if (c && c->run_open) return run_busy(c);
   uint64_t need = 0;
   int r = kmz_partials_size(c, which, &need);
   if (r) return r;
@@ -1976,6 +2034,7 @@ int kmz_partials_copy(kmz_ctx *c, int which, void *buf, uint64_t words, int mem,
 // replace: the keys become the edge set (kmz_set_triples), else they join it
 static int merge_or_set_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, int mem, bool replace) {
   if (!c || (n && !keys)) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
   uint64_t nl = 0;
   int r = kmz_partials_size(c, KMZ_PART_TRIPLES, &nl);
@@ -2033,6 +2092,7 @@ static int merge_or_set_triples(kmz_ctx *c, const uint64_t *keys, uint64_t n, in
 
 int kmz_get_global_index(kmz_ctx *c, uint64_t *out, uint64_t cap, int mem) {
   if (!c || (c->n && !out)) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_get_global_index before kmz_load");
   if (cap < c->n) return fail(c, KMZ_E_ARG, "output too small");
   unsigned long long *dst = reinterpret_cast<unsigned long long *>(out);
@@ -2065,6 +2125,7 @@ static uint64_t pow2_at_least(uint64_t x) {
 
 int kmz_tail_map_set(kmz_ctx *c, const kmz_tail_map *m) {
   if (!c || !m || !m->svc || !m->cls || (m->n_cls && !m->lsvc)) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   const uint32_t lim = 1u << 24;
   if (m->n_svc >= lim || m->n_cls >= lim || m->n_lsvc >= lim || m->n_ep >= lim) return fail(c, KMZ_E_ARG, "tail ids must be < 2^24");
   for (uint32_t e = 0; e < m->n_ep; ++e)
@@ -2090,6 +2151,7 @@ int kmz_tail_map_set(kmz_ctx *c, const kmz_tail_map *m) {
 
 int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
   if (!c->tl_map) return fail(c, KMZ_E_STATE, "kmz_tail_map_set first");
   if (c->tl_n_ep != c->n_dep) return fail(c, KMZ_E_ARG, "tail map size differs from the dependency endpoints");
@@ -2226,6 +2288,7 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
 int kmz_tail_service_stats(kmz_ctx *c, uint32_t *stats, uint64_t scap, uint32_t *by_dist, uint64_t dcap,
                            uint32_t *n_dist) {
   if (!c || !n_dist) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
   *n_dist = c->tl_rel_dist;
   const uint64_t ns = (uint64_t)c->tl_n_svc * 8, nd = (uint64_t)c->tl_n_svc * c->tl_rel_dist;
@@ -2238,6 +2301,7 @@ int kmz_tail_service_stats(kmz_ctx *c, uint32_t *stats, uint64_t scap, uint32_t 
 
 int kmz_tail_service_first(kmz_ctx *c, uint64_t *first, uint64_t cap) {
   if (!c || (!first && cap)) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
   if (cap < c->tl_n_svc) return fail(c, KMZ_E_ARG, "output too small");
   if (c->tl_n_svc) memcpy(first, static_cast<const char *>(c->tl_host) + 64 + (size_t)c->tl_n_svc * 32, (size_t)c->tl_n_svc * 8);
@@ -2247,6 +2311,7 @@ int kmz_tail_service_first(kmz_ctx *c, uint64_t *first, uint64_t cap) {
 int kmz_service_map_set(kmz_ctx *c, const uint32_t *sid_of_ep, uint32_t n_ep, uint32_t n_sid, const uint8_t *is_5xx,
                         uint32_t n_status) {
   if (!c || (n_ep && !sid_of_ep) || (n_status && !is_5xx) || !n_status) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   std::vector<uint32_t> off((size_t)n_sid + 1, 0), eps(n_ep);
   for (uint32_t e = 0; e < n_ep; ++e) {
     if (sid_of_ep[e] >= n_sid) return fail(c, KMZ_E_RANGE, "service id out of range");
@@ -2271,6 +2336,7 @@ int kmz_service_map_set(kmz_ctx *c, const uint32_t *sid_of_ep, uint32_t n_ep, ui
 
 int kmz_service_sums(kmz_ctx *c, kmz_service_sum *out, uint64_t cap) {
   if (!c || (!out && cap)) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->sv_map) return fail(c, KMZ_E_STATE, "kmz_service_map_set first");
   if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
   if ((uint64_t)c->sv_n_ep * c->sv_n_status != c->G) return fail(c, KMZ_E_ARG, "service map size differs from the groups");
@@ -2287,6 +2353,7 @@ int kmz_service_sums(kmz_ctx *c, kmz_service_sum *out, uint64_t cap) {
 int kmz_tail_get(kmz_ctx *c, kmz_tail_detail *det, uint64_t dcap, kmz_tail_pair *pairs, uint64_t pcap,
                  uint8_t *has_in, uint64_t hcap) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
   if ((det && dcap < c->tl_nd) || (pairs && pcap < c->tl_np) || (has_in && hcap < c->tl_n_ep))
     return fail(c, KMZ_E_ARG, "output too small");
@@ -2301,6 +2368,7 @@ int kmz_tail_get(kmz_ctx *c, kmz_tail_detail *det, uint64_t dcap, kmz_tail_pair 
 
 int kmz_unresolved_parents(kmz_ctx *c, uint64_t *ids, uint64_t cap, uint64_t *n_out, int mem) {
   if (!c || !n_out) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
   if (!(c->path & 1)) return fail(c, KMZ_E_UNSUPPORTED, "span-table path: no per-span parent resolution to export");
   if (c->hpin_valid && reinterpret_cast<const unsigned int *>(c->hpin)[C_MISS] == 0) {
@@ -2334,6 +2402,7 @@ int kmz_unresolved_parents(kmz_ctx *c, uint64_t *ids, uint64_t cap, uint64_t *n_
 
 int kmz_count_ids(kmz_ctx *c, const uint64_t *ids, uint64_t n, int mem, uint64_t *found) {
   if (!c || !found || (n && !ids)) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_count_ids before kmz_load");
   uint64_t cap = 1024;
   while (cap < 2 * n + 64) cap *= 2;
@@ -2357,6 +2426,7 @@ int kmz_count_ids(kmz_ctx *c, const uint64_t *ids, uint64_t n, int mem, uint64_t
 
 int kmz_route_ids(kmz_ctx *c, uint32_t world, uint64_t *out, uint64_t cap, int mem, uint64_t *counts) {
   if (!c || !counts || world == 0 || (c->n && !out)) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_route_ids before kmz_load");
   if (cap < c->n) return fail(c, KMZ_E_ARG, "output too small");
   const uint32_t n = (uint32_t)c->n;
@@ -2378,6 +2448,7 @@ int kmz_route_ids(kmz_ctx *c, uint32_t world, uint64_t *out, uint64_t cap, int m
 
 int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32_t *repeated) {
   if (!c || !repeated || (n && !vals)) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   *repeated = 0;
   if (n < 2) return KMZ_OK;
   CertPlan pl;
@@ -2419,6 +2490,7 @@ int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32
 
 int kmz_finalize(kmz_ctx *c) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
   {
     Timed t(c, KMZ_K_FINAL);
@@ -2457,6 +2529,7 @@ int kmz_set_profiling(kmz_ctx *c, int on) { return kmz_set_profiling_mask(c, on 
 
 int kmz_set_profiling_mask(kmz_ctx *c, uint32_t mask) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   c->prof_mask = mask & ((1u << KMZ_K_COUNT) - 1);
   c->prof = c->prof_mask != 0;
   // create the timing events now, and record each once (the first record of
@@ -2475,6 +2548,7 @@ int kmz_set_profiling_mask(kmz_ctx *c, uint32_t mask) {
 
 int kmz_kernel_times(kmz_ctx *c, double *ms, uint64_t *calls, int reset) {
   if (!c) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   int r = kmz_sync(c);
   if (r) return r;
   for (int k = 0; k < KMZ_K_COUNT; ++k) {
@@ -2536,6 +2610,7 @@ static int synth_base(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64
 
 int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t t1, uint64_t *n_out) {
   if (!c || t1 < t0) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   kmz_synth_desc d;
   if (kmz_synth_describe(config, &d)) return fail(c, KMZ_E_ARG, "unknown synthetic config");
   hipSetDevice(c->device);
@@ -2599,6 +2674,7 @@ int kmz_synth_load(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t 
 int kmz_synth_load_shard(kmz_ctx *c, int config, uint64_t seed, uint64_t t0, uint64_t t1, uint32_t world,
                          uint32_t rank, uint64_t *n_out) {
   if (!c || t1 < t0 || world == 0 || rank >= world) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
   kmz_synth_desc d;
   if (kmz_synth_describe(config, &d)) return fail(c, KMZ_E_ARG, "unknown synthetic config");
   hipSetDevice(c->device);

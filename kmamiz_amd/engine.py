@@ -282,6 +282,16 @@ class Engine:
         self.gen += 1
         L.check(self.ctx, self._lib.kmz_run(self.ctx, flags))
 
+    def run_begin(self, flags: int):
+        """``run`` in two halves (kmz_run_begin / _end): the run is enqueued
+        here, the caller's host work between the two overlaps its kernels, and
+        ``run_end`` waits for it.  No other engine call in between."""
+        self.gen += 1
+        L.check(self.ctx, self._lib.kmz_run_begin(self.ctx, flags))
+
+    def run_end(self):
+        L.check(self.ctx, self._lib.kmz_run_end(self.ctx))
+
     def sync(self):
         L.check(self.ctx, self._lib.kmz_sync(self.ctx))
 

@@ -1395,3 +1395,30 @@ def test_pipelined_fetch_equals_fetch(engine):
     engine.fetch_begin(keys=False)
     g, k, e = engine.fetch_end()
     assert k is None and g.tobytes() == want[1][0].tobytes() and e.tobytes() == want[1][2].tobytes()
+
+
+def test_run_begin_end_equals_run(engine):
+    """kmz_run_begin / _end (host work between the two overlaps the run's
+    kernels) give kmz_run's results; any other call while the run is open is
+    refused, and so is an _end without a _begin."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS
+    engine.load_synthetic(synth.MESH, synth.SEED, 0, 4000)
+    engine.run(flags)
+    g, k, e = engine.fetch()
+    want = (g.copy(), np.sort(k), e.copy(), engine.info())
+    engine.run_begin(flags)
+    with pytest.raises(Exception, match="run is open"):
+        engine.info()
+    with pytest.raises(Exception, match="run is open"):
+        engine.fetch()
+    with pytest.raises(Exception):
+        engine.run_begin(flags)
+    engine.run_end()
+    g, k, e = engine.fetch()
+    assert g.tobytes() == want[0].tobytes() and np.array_equal(np.sort(k), want[1]) and e.tobytes() == want[2].tobytes()
+    assert engine.info() == want[3]
+    with pytest.raises(Exception, match="without kmz_run_begin"):
+        engine.run_end()
