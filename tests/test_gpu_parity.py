@@ -1422,3 +1422,27 @@ def test_run_begin_end_equals_run(engine):
     assert engine.info() == want[3]
     with pytest.raises(Exception, match="without kmz_run_begin"):
         engine.run_end()
+
+
+def test_fetch_begin_pageable_and_runtime_copies(engine):
+    """kmz_fetch_begin into pageable host arrays (the runtime's copies, not
+    k_copy_out's pinned path) returns kmz_fetch's result sets."""
+    import ctypes as C
+
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    engine.load_synthetic(synth.MESH, synth.SEED, 100, 2600)
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    wg, wk, we = engine.fetch()
+    wg, wk, we = wg.copy(), np.sort(wk), we.copy()
+    g = np.empty(len(wg), dtype=L.GROUP_DTYPE)
+    k = np.empty(len(wk), dtype=np.uint64)
+    e = np.empty(len(we), dtype=L.ENDPOINT_DTYPE)
+    n = C.c_uint64()
+    lib = L.lib()
+    L.check(engine.ctx, lib.kmz_fetch_begin(engine.ctx, L.ptr(g), len(g), L.ptr(k), len(k), C.byref(n), L.ptr(e),
+                                            len(e)))
+    L.check(engine.ctx, lib.kmz_fetch_end(engine.ctx))
+    assert n.value == len(wk)
+    assert g.tobytes() == wg.tobytes() and np.array_equal(np.sort(k), wk) and e.tobytes() == we.tobytes()
