@@ -141,7 +141,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile)
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -1845,6 +1845,16 @@ void endpoints_from(const uint64_t *h, uint32_t n_dep, kmz_endpoint *eps) {
   }
 }
 
+// the device address of page-locked host memory (hipHostMalloc / registered), else null
+void *host_pinned_dev(void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // (pageable memory: not an error of the fetch)
+    return nullptr;
+  }
+  return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+}
+
 int pinned_staging(kmz_ctx *c, void *&p, size_t &have, size_t bytes) {
   if (have >= bytes) return KMZ_OK;
   if (p) hipHostFree(p);
@@ -1915,9 +1925,22 @@ int kmz_fetch_begin(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip
   if (eb) HIPCHK(c, hipMemcpyAsync(c->f_ep.p, c->epp.p, eb, hipMemcpyDeviceToDevice, c->stream));
   HIPCHK(c, hipEventRecord(c->ev_snap, c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->xfer, c->ev_snap, 0));
-  if (gb) HIPCHK(c, hipMemcpyAsync(groups, c->f_grp.p, gb, hipMemcpyDeviceToHost, c->xfer));
-  if (tb) HIPCHK(c, hipMemcpyAsync(trip, c->f_trip.p, tb, hipMemcpyDeviceToHost, c->xfer));
-  if (eb) HIPCHK(c, hipMemcpyAsync(c->fhep, c->f_ep.p, eb, hipMemcpyDeviceToHost, c->xfer));
+  // to page-locked host memory by the DMA engines (hipMemcpyDeviceToDeviceNoCU
+  // on the buffer's device address): the runtime's device-to-host copy is a
+  // blit kernel over the whole GPU whose waves wait on PCIe, and the next
+  // run's first kernels waited ~0.13 ms for it.  Pageable memory, or KMZ_ABLATE2
+  // bit 9 (for comparison): the runtime's copy.
+  const void *from[3] = {c->f_grp.p, c->f_trip.p, c->f_ep.p};
+  void *to[3] = {groups, trip, c->fhep};
+  const size_t nb[3] = {gb, tb, eb};
+  for (int k = 0; k < 3; ++k) {
+    if (!nb[k]) continue;
+    void *dev = (c->ablate2 & (1u << 9)) ? nullptr : host_pinned_dev(to[k]);
+    if (dev)
+      HIPCHK(c, hipMemcpyAsync(dev, from[k], nb[k], hipMemcpyDeviceToDeviceNoCU, c->xfer));
+    else
+      HIPCHK(c, hipMemcpyAsync(to[k], from[k], nb[k], hipMemcpyDeviceToHost, c->xfer));
+  }
   c->fetch_open = true;
   c->f_eps = eps;
   c->f_ndep = eb ? c->n_dep : 0;
