@@ -20,12 +20,18 @@ for f in glob.glob(os.path.join(sys.argv[1], "**", "*counter_collection.csv"), r
             acc[d] += float(r["Counter_Value"]) * 1024
             names[d] = r["Kernel_Name"].split("(")[0]
 known = {"k_stream": 1 << 30, "k_rand": 50000000 * 16}
-kinds = ["stream (1 GiB, coalesced 16-B words)", "random 16-B reads, 64 MiB table", "random 16-B reads, 1 GiB table"]
 rows = []
-for i, d in enumerate(sorted(acc)):
+nrand = 0
+for d in sorted(acc):
     k = names[d]
-    base = known["k_stream" if "stream" in k else "k_rand"]
-    rows.append({"launch": i, "kernel": k, "access": kinds[i % 3], "fetch_size_bytes": acc[d],
-                 "known_bytes": base, "ratio": round(acc[d] / base, 3),
-                 "bytes_per_16B_read": round(acc[d] / (base / 16), 1)})
+    if k.startswith("__amd"):
+        continue  # (the buffers' fills)
+    if "stream" in k:
+        access, base = "stream (1 GiB, coalesced 16-B words)", known["k_stream"]
+    else:
+        access = ["random 16-B reads, 64 MiB table", "random 16-B reads, 1 GiB table"][nrand % 2]
+        base = known["k_rand"]
+        nrand += 1
+    rows.append({"dispatch": d, "kernel": k, "access": access, "fetch_size_bytes": acc[d], "known_bytes": base,
+                 "ratio": round(acc[d] / base, 3), "bytes_per_16B_read": round(acc[d] / (base / 16), 1)})
 print(json.dumps(rows, indent=1))
