@@ -79,7 +79,11 @@ def traffic_of(kernel, config, n_local):
             continue
         # (template instances, e.g. k4_chain<false>, count as their kernel)
         ks = [v for name, v in t.get("kernels", {}).items() if name.split("<")[0] == kernel]
-        return (sum(v["traffic_bytes"] for v in ks), os.path.basename(f)) if ks else None
+        if not ks:
+            return None
+        lower = sum(v.get("traffic_lower_bytes", 0) for v in ks) if all("traffic_lower_bytes" in v for v in ks) else None
+        hits = [v["l2_hit_rate"] for v in ks if "l2_hit_rate" in v]
+        return (sum(v["traffic_bytes"] for v in ks), os.path.basename(f), lower, hits[0] if len(hits) == 1 else None)
     return None
 
 
@@ -492,7 +496,13 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(d["gbs"] / HBM_PEAK_GBS, 4),
+                # HBM-side bytes per launch from the PMC passes: 2 x FETCH_SIZE +
+                # WRITE_SIZE (every read request 128 B: the upper figure), and
+                # FETCH_SIZE + WRITE_SIZE (every request 64 B, as a random 16-B
+                # probe registers: the lower one); the L2 hit rate of its requests
                 "traffic": (tr[0] if tr else None),
+                "traffic_lower": (tr[2] if tr else None),
+                "l2_hit_rate": (tr[3] if tr else None),
                 "traffic_source": (f"profiles/{tr[1]} (build {build_id()})" if tr else
                                    f"no PMC pass of build {build_id()} on this workload committed"),
                 "pipeline_bytes": pipe_bytes,

@@ -358,6 +358,14 @@ int kmz_count_ids(kmz_ctx *ctx, const uint64_t *ids, uint64_t n, int mem, uint64
  * plans for, or a bucket overflow): the caller checks another way. */
 int kmz_route_ids(kmz_ctx *ctx, uint32_t world, uint64_t *out, uint64_t cap, int mem, uint64_t *counts);
 int kmz_id_repeats(kmz_ctx *ctx, const uint64_t *vals, uint64_t n, int mem, uint32_t *repeated);
+/* kmz_route_ids into fixed segments, with no host round trip: out holds
+ * `world` segments of `seg` words; segment r's word 0 is the number of values
+ * routed to rank r and its words 1 .. min(count, seg - 1) those values (a
+ * count >= seg means the segment overflowed: the caller exchanges exactly).
+ * With device memory the routing is only enqueued on the context's stream,
+ * so an all-to-all of equal segments can be posted behind it at once
+ * (dist.IdGuard; Traces.ts:117-123 is the semantics the check protects). */
+int kmz_route_ids_fixed(kmz_ctx *ctx, uint32_t world, uint64_t seg, uint64_t *out, int mem);
 
 /* ---- traceId sharding (shard = h(traceId) mod G) ------------ */
 /* The shard of a trace, from its traceId string (the reference dedups and

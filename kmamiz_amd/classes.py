@@ -730,14 +730,29 @@ class EndpointDependencies:
 
         if self._native is None:
             raise ValueError("service_tail() needs an engine-backed result")
-        if self._cutoff != 0:
-            raise NotImplementedError("service_tail() runs on the unfiltered edge set; with "
-                                      "DEPRECATED_ENDPOINT_THRESHOLD set use toReduced() (filtered) and the host tail")
         nat = self._native
         eng = nat.eng
         if eng.gen != nat.gen:  # the engine ran something else since: this batch's dependency pass again
             eng = nat.traces._load()
             eng.run(L.RUN_DEPS)
+        if self._cutoff != 0:
+            # DEPRECATED_ENDPOINT_THRESHOLD set: the tail of the constructor-
+            # filtered graph (EndpointDependencies.ts:44-74).  The filtered edge
+            # keys replace the run's edge set (kmz_set_triples) and the stale
+            # endpoints lose their rows (first-row partial -> none), so the
+            # kernels see exactly the kept rows; the engine no longer holds this
+            # run afterwards (its gen moved: a later call runs the pass again).
+            keys, eps = self.reduced()
+            stale = (nat.endpoints["has_row"] != 0) & (eps["has_row"] == 0)
+            if stale.any() or len(keys) != len(nat.triples):
+                ew = eng.partials_words(L.PART_ENDPOINTS)
+                part = np.zeros(max(1, ew), np.uint64)
+                eng.export_partials(L.PART_ENDPOINTS, part.ctypes.data, ew, False)
+                n_ep = ew // 2
+                part[n_ep:][np.nonzero(stale[:n_ep])[0]] = np.uint64(L.NONE64)  # [min first row] half
+                eng.import_partials(L.PART_ENDPOINTS, part.ctypes.data, ew, False)
+                kh = np.ascontiguousarray(keys, dtype=np.uint64)
+                eng.set_triples(kh.ctypes.data, len(kh), False)
         return run_tail(eng, maps_from_dictionary(nat.dict, labelMap), eng.endpoints())
 
     def toReduced(self, reg=None):

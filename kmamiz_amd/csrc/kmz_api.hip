@@ -104,6 +104,7 @@ struct kmz_ctx {
   bool chain_ran = false;   // this run's dependency graph came from k4_chain's chain interning
   bool walk_once = false;   // a K4 wait ran out (F_SPIN): this run is redone on the exact per-row walk
   bool k4_now = false;      // this kmz_run's K4 mode (direct enumeration), decided once per call
+  bool dep_valid = false;   // every shape's dependency endpoint is < n_dep (chain elements by shape)
   // hipGraphs of a whole run for small batches (launch-bound): a run whose
   // launch sequence (kmz_run key) repeats is captured once and replayed
   struct RunGraph {
@@ -141,7 +142,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines)
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -410,6 +411,10 @@ static int load_shapes(kmz_ctx *c, const kmz_shapes *sh) {
   c->n_tag = sh->n_tag_ep;
   c->n_dep = sh->n_dep_ep;
   c->n_status = sh->n_status;
+  // (the walk's chain elements may be shapes -- each maps to one endpoint in
+  // range, and a shape id fits an edge key's 24 bits below NONE's)
+  c->dep_valid = sh->n_shapes < 0xFFFFFFu;
+  for (uint32_t s = 0; s < sh->n_shapes && c->dep_valid; ++s) c->dep_valid = sh->dep_ep[s] < sh->n_dep_ep;
   size_t b = (size_t)sh->n_shapes * 4;
   if (ensure(c, c->d_rt, b) || ensure(c, c->d_tag, b) || ensure(c, c->d_dep, b)) return KMZ_E_HIP;
   if (b) {
@@ -1089,6 +1094,7 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     launch_fill(c->stream, f);
   }
   c->ctab_dirty = true;  // until this run's slots are cleared below
+  const bool w8 = !(c->ablate2 & 1024u), by_shape = w8 && c->dep_valid && !(c->ablate2 & 2048u);
   {
     ChainRun a;
     a.ts = c->ts;
@@ -1112,21 +1118,33 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     a.seed = c->sig_seed;
     // (test knob 24 forces sig collisions on the first seed only)
     a.ablate = c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24));
+    // k4_tile8 (8-byte window records; KMZ_ABLATE2 bit 10: the 16-byte
+    // k4_tile, for comparison).  Its chain elements are shapes when the
+    // dependency table maps every shape into range (bit 11: endpoints
+    // anyway): no gather before the window is built; the leaders map their
+    // keys' shapes to endpoints
+    a.id_ep = by_shape ? P<uint32_t>(c->d_dep) : nullptr;
+    a.n_ids = c->n_shapes;
     Timed t(c, KMZ_K_WALK);
-    launch_chain_tile(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep), c->n_shapes,
-                      P<uint4>(c->cetab), P<uint32_t>(c->ctile), a);
+    if (w8)
+      launch_chain_tile8(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep), c->n_shapes,
+                         P<uint32_t>(c->ctile), a);
+    else
+      launch_chain_tile(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep), c->n_shapes,
+                        P<uint4>(c->cetab), P<uint32_t>(c->ctile), a);
   }
   {
     Timed t(c, KMZ_K_SETTLE);
     launch_chain_settle_list(c->stream, nt, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
                              P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), (uint32_t)stot,
-                             P<unsigned long long>(c->kdefer), (uint32_t)dtot, gpos, (uint32_t)gtot, c->ablate);
+                             P<unsigned long long>(c->kdefer), (uint32_t)dtot, gpos, (uint32_t)gtot, c->ablate,
+                             by_shape ? P<uint32_t>(c->d_dep) : nullptr, c->n_shapes);
   }
   {
     Timed t(c, KMZ_K_PEND);
     launch_chain_pend(c->stream, P<uint32_t>(c->plist), n + 1, c->kind, c->shape, c->ts, P<uint32_t>(c->cparent), n,
                       P<uint32_t>(c->d_dep), c->n_shapes, c->n_dep, c->sig_seed, c->ctab.p, c->ccap,
-                      P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, (uint32_t)gtot, false, c->ablate);
+                      P<unsigned long long>(c->trip), c->tcap, epp, cnt, st, gpos, (uint32_t)gtot, false, c->ablate, by_shape);
   }
   if (c->overlap) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_k3, 0));  // the shape-level K3 partials
   {
@@ -2466,6 +2484,29 @@ int kmz_route_ids(kmz_ctx *c, uint32_t world, uint64_t *out, uint64_t cap, int m
   HIPCHK(c, hipMemcpyAsync(counts, c->rt_tot.p, (size_t)world * 8, hipMemcpyDeviceToHost, c->stream));
   if (mem != KMZ_MEM_DEVICE && n) HIPCHK(c, hipMemcpyAsync(out, dst, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return KMZ_OK;
+}
+
+int kmz_route_ids_fixed(kmz_ctx *c, uint32_t world, uint64_t seg, uint64_t *out, int mem) {
+  if (!c || world == 0 || seg < 2 || !out) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
+  if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_route_ids_fixed before kmz_load");
+  const uint32_t n = (uint32_t)c->n;
+  if (ensure(c, c->rt_hist, (size_t)route_chunks(n) * world * 4) || ensure(c, c->rt_tot, (size_t)world * 8))
+    return KMZ_E_HIP;
+  unsigned long long *dst = reinterpret_cast<unsigned long long *>(out);
+  const size_t words = (size_t)world * seg;
+  if (mem != KMZ_MEM_DEVICE) {
+    if (ensure(c, c->rt_out, words * 8)) return KMZ_E_HIP;
+    dst = P<unsigned long long>(c->rt_out);
+  }
+  if (!launch_route(c->stream, c->sid, n, world, P<uint32_t>(c->rt_hist), P<unsigned long long>(c->rt_tot), dst, seg))
+    return fail(c, KMZ_E_ARG, "world must be 1..1024");
+  HIPCHK(c, hipGetLastError());
+  if (mem != KMZ_MEM_DEVICE) {  // (host memory: copied back; device memory: enqueued only)
+    HIPCHK(c, hipMemcpyAsync(out, dst, words * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   return KMZ_OK;
 }
 

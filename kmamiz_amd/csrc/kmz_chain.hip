@@ -447,7 +447,7 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
           if (w01[q].y != ps[q]) flags |= F_SIG;
           continue;
         }
-        uint32_t h = (uint32_t)(sg[q] >> 32) & (IMAP - 1);
+        uint32_t h = (uint32_t)(sig_place(sg[q]) >> 32) & (IMAP - 1);
         hslot[q] = IMAP;  // a leader without a map slot (map full)
         for (uint32_t t = 0; t < 8; ++t) {
           const unsigned long long kk = atomicCAS(&imap_sig[h], 0ull, (unsigned long long)sg[q]);
@@ -838,7 +838,9 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
                                                      unsigned int *__restrict__ counters,
                                                      unsigned long long *__restrict__ stats64,
                                                      uint32_t *__restrict__ gpos, uint32_t gcap, bool direct,
-                                                     uint32_t spin) {
+                                                     uint32_t spin, bool by_shape) {
+  // by_shape: the run's chain elements are shapes (k4_tile8 on a dependency
+  // table that maps every shape into range), as the tile kernel's
   const uint32_t m = min(counters[C_PLIST], pcap);
   uint32_t flags = 0;
   for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < m; x += gridDim.x * blockDim.x) {
@@ -849,7 +851,7 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     const bool on = ki == KIND_SERVER;
     if (es >= n_ep && on) flags |= F_RANGE;
     // fold hashes of the span's ancestry and of its parent's (suffix) ancestry
-    uint64_t acc = sig_elem(es, on, seed), pacc = 0;
+    uint64_t acc = sig_elem(by_shape ? (sh < n_shapes ? sh : NONE) : es, on, seed), pacc = 0;
     uint32_t d = 0;
     bool bad = false;
     const uint32_t a = cparent[i];
@@ -866,7 +868,7 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
         break;
       }
       const uint32_t sa = shape[cur];
-      const uint32_t ea = sa < n_shapes ? dep_ep[sa] : NONE;
+      const uint32_t ea = sa < n_shapes ? (by_shape ? sa : dep_ep[sa]) : NONE;
       const uint64_t el = sig_elem(ea, kind[cur] == KIND_SERVER, seed);
       acc = sig_step(acc, el);
       pacc = d == 1 ? el : sig_step(pacc, el);
@@ -1086,10 +1088,11 @@ void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, cons
                        const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
-                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct, uint32_t ablate) {
+                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct, uint32_t ablate,
+                       bool by_shape) {
   hipLaunchKernelGGL(k4_chain_pend, dim3(1024), dim3(256), 0, s, plist, pcap, kind, shape, ts, cparent, n, dep_ep,
                      n_shapes, n_ep, seed, reinterpret_cast<unsigned long long *>(ctab), ccap, trip, tcap, ep_ts,
-                     counters, stats64, gpos, gcap, direct, spin_bound(ablate));
+                     counters, stats64, gpos, gcap, direct, spin_bound(ablate), by_shape);
 }
 
 }  // namespace kmz

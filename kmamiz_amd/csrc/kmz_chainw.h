@@ -30,8 +30,17 @@ __device__ __forceinline__ uint8_t kf_kind(uint8_t b) { return b & 3; }
 __device__ __forceinline__ uint8_t kf_st(uint8_t b) { return b >> 2; }
 __device__ __forceinline__ uint8_t kf_make(uint8_t kind, uint8_t st) { return (uint8_t)(kind | (st << 2)); }
 
+// A chain element's 64-bit value: an injective function of (endpoint, on) --
+// one 32 x 64-bit multiply by an odd constant of (endpoint << 1 | on) ^ seed
+// (endpoints past 2^30 are all "none") -- cheap enough that the walk computes
+// it per step from the endpoint instead of reading it from LDS (the walk's
+// window records are 8 bytes).  Injectivity is what the chain table's
+// exactness argument needs (kmz_chain.hip); the odd multiplier spreads the
+// bits the table's home slot is taken from.  (Until round 5: mix64, two 64-bit
+// multiplies, kept in 16-byte LDS records.)
 __host__ __device__ __forceinline__ uint64_t sig_elem(uint32_t ep, bool on, uint64_t seed) {
-  return mix64((((uint64_t)ep << 1) | (on ? 1ull : 0ull)) ^ seed);
+  const uint32_t x = (((ep < EPK_NONE ? ep : EPK_NONE) << 1) | (on ? 1u : 0u)) ^ (uint32_t)seed;
+  return (uint64_t)x * 0x9E3779B97F4A7C15ull;
 }
 constexpr uint64_t ROOT_SIG = ~0ull;  // the "parent sig" of a root
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, uint32_t r) {
@@ -44,9 +53,8 @@ __device__ __forceinline__ uint64_t sig_step(uint64_t acc, uint64_t el) {
   return ((acc << SIG_R) | (acc >> (64 - SIG_R))) ^ el;
 }
 // The finish is an xor with a depth and seed constant: a bijection for each
-// depth, which is all the exactness argument needs.  The fold is already an
-// xor of rotated mix64 outputs (uniform bits), so no further mixing is needed
-// for the table's placement; a final mix64 (two 64-bit multiplies per sig,
+// depth, which is all the exactness argument needs.  Placement mixes once
+// more (sig_place); a final mix64 of both sigs (two 64-bit multiplies per sig,
 // two sigs per span) cost 4 % of k4_chain (mesh 1.33 against 1.28 ms).
 // 0 marks an unwritten word and ROOT_SIG a root's parent: a sig equal to
 // either is treated as a collision (another seed)
@@ -59,9 +67,15 @@ __device__ __forceinline__ uint64_t sig_final(uint64_t acc, uint32_t d, uint64_t
   if (z == 0 || z == ROOT_SIG) *flags |= F_SIG;
   return z;
 }
-// home slot: the sig's high bits (ccap is a power of two: mulhi64(sig, ccap))
+// Placement of a sig (the chain table's home slot, the walk's LDS leader
+// map): an xorshift and one multiply, so that every bit of the sig reaches the
+// top bits -- the fold of Fibonacci-hashed elements leaves some low-quality
+// bits (low bits of a product) rotated into the top ones.  Placement only:
+// identity is the whole sig.
+__device__ __forceinline__ uint64_t sig_place(uint64_t sig) { return (sig ^ (sig >> 29)) * 0xBF58476D1CE4E5B9ull; }
+// home slot: the placement's high bits (ccap is a power of two)
 __device__ __forceinline__ uint64_t cslot(uint64_t sig, uint64_t ccap) {
-  return sig >> (64 - __builtin_ctzll(ccap));
+  return sig_place(sig) >> (64 - __builtin_ctzll(ccap));
 }
 
 __device__ __forceinline__ uint64_t edge_key(uint32_t ea, uint32_t es, uint32_t d, bool on) {

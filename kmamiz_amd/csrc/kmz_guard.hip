@@ -89,9 +89,12 @@ __global__ void __launch_bounds__(RT_T) k_route_hist(const uint64_t *__restrict_
   for (uint32_t r = threadIdx.x; r < world; r += RT_T) hist[(uint64_t)blockIdx.x * world + r] = h[r];
 }
 
-// hist[chunk][owner] -> exclusive output offsets (owner-major); tot[owner] = its count
+// hist[chunk][owner] -> exclusive output offsets (owner-major); tot[owner] = its count.
+// fixed (segw > 0): offsets within the owner's own segment of segw words,
+// whose word 0 gets the count (kmz_route_ids_fixed: no counts exchange)
 __global__ void __launch_bounds__(RT_T) k_route_scan(uint32_t *__restrict__ hist, uint32_t nchunks, uint32_t world,
-                                                     unsigned long long *__restrict__ tot) {
+                                                     unsigned long long *__restrict__ tot, uint64_t segw,
+                                                     unsigned long long *__restrict__ out) {
   __shared__ unsigned long long seg[RT_MAXW];
   for (uint32_t r = threadIdx.x; r < world; r += RT_T) {
     unsigned long long a = 0;
@@ -102,7 +105,9 @@ __global__ void __launch_bounds__(RT_T) k_route_scan(uint32_t *__restrict__ hist
     }
     seg[r] = a;
     tot[r] = a;
+    if (segw) out[(uint64_t)r * segw] = a;
   }
+  if (segw) return;  // (segments are the owners' own: no global offsets)
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long a = 0;
@@ -119,26 +124,30 @@ __global__ void __launch_bounds__(RT_T) k_route_scan(uint32_t *__restrict__ hist
 
 __global__ void __launch_bounds__(RT_T) k_route_scatter(const uint64_t *__restrict__ sid, uint32_t n, uint32_t chunk,
                                                         uint32_t world, const uint32_t *__restrict__ off,
-                                                        unsigned long long *__restrict__ out) {
+                                                        unsigned long long *__restrict__ out, uint64_t segw) {
   __shared__ uint32_t cur[RT_MAXW];
   for (uint32_t r = threadIdx.x; r < world; r += RT_T) cur[r] = off[(uint64_t)blockIdx.x * world + r];
   __syncthreads();
   const uint32_t b = blockIdx.x * chunk, e = min(n, b + chunk);
   for (uint32_t i = b + threadIdx.x; i < e; i += RT_T) {  // (order inside a segment is free: the check is a set test)
     const uint64_t h = id_hash(sid[i]);
-    out[atomicAdd(&cur[id_owner(h, world)], 1u)] = h;
+    const uint32_t r = id_owner(h, world), x = atomicAdd(&cur[r], 1u);
+    if (!segw)
+      out[x] = h;
+    else if (x + 1 < segw)  // (a full segment: its count says so, the exchange is redone exactly)
+      out[(uint64_t)r * segw + 1 + x] = h;
   }
 }
 
 uint32_t route_chunks(uint32_t n) { return std::max<uint32_t>(1, std::min<uint32_t>(1024, (n + 4095) / 4096)); }
 
 bool launch_route(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint32_t *hist,
-                  unsigned long long *tot, unsigned long long *out) {
+                  unsigned long long *tot, unsigned long long *out, uint64_t segw) {
   if (world == 0 || world > RT_MAXW) return false;
   const uint32_t g = route_chunks(n), chunk = (n + g - 1) / g;
   hipLaunchKernelGGL(k_route_hist, dim3(g), dim3(RT_T), 0, s, sid, n, chunk, world, hist);
-  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(RT_T), 0, s, hist, g, world, tot);
-  if (n) hipLaunchKernelGGL(k_route_scatter, dim3(g), dim3(RT_T), 0, s, sid, n, chunk, world, hist, out);
+  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(RT_T), 0, s, hist, g, world, tot, segw, out);
+  if (n) hipLaunchKernelGGL(k_route_scatter, dim3(g), dim3(RT_T), 0, s, sid, n, chunk, world, hist, out, segw);
   return true;
 }
 

@@ -12,6 +12,19 @@ namespace kmz {
 constexpr uint8_t KIND_SERVER = KMZ_KIND_SERVER;
 constexpr uint8_t KIND_CLIENT = KMZ_KIND_CLIENT;
 
+// A window slot's packed (kind, element id) word (k4_tile8's 8-byte records):
+// kind in bits 30-31, the id in bits 0-29 -- the span's shape, or its
+// dependency endpoint -- and EPK_NONE for none (a CLIENT span, an unknown
+// shape).  Edge keys hold endpoints in 24 bits, so every endpoint id fits.
+constexpr uint32_t EPK_NONE = 0x3FFFFFFFu;
+__host__ __device__ __forceinline__ uint32_t epk_pack(uint32_t kind, uint32_t ep) {
+  return ((kind & 3u) << 30) | (ep < EPK_NONE ? ep : EPK_NONE);
+}
+__host__ __device__ __forceinline__ uint32_t epk_kind(uint32_t e) { return e >> 30; }
+__host__ __device__ __forceinline__ uint32_t epk_ep(uint32_t e) {
+  return (e & EPK_NONE) == EPK_NONE ? NONE : (e & EPK_NONE);
+}
+
 // u32 device counters
 enum {
   C_FLAGS = 0,
@@ -169,13 +182,17 @@ void launch_chain_settle_list(hipStream_t s, uint32_t nt, void *ctab, uint64_t c
                               uint64_t tcap, unsigned int *counters, const uint32_t *tile_stats,
                               unsigned long long *stats64, const unsigned long long *stage, uint32_t scap,
                               const unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap,
-                              uint32_t ablate = 0);
+                              uint32_t ablate = 0, const uint32_t *id_ep = nullptr, uint32_t n_ids = 0);
 // K4 chain interning, one workgroup per tile (kmz_walk.hip); same global
 // lists as the fused kernel (settled by launch_chain_settle_list over walk_tiles)
 struct ChainRun;
 uint32_t walk_tiles(uint32_t n);
 void launch_chain_tile(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint32_t *cparent, uint32_t n,
                        const uint32_t *dep_ep, uint32_t n_shapes, uint4 *etab, uint32_t *tile_stats, const ChainRun &a);
+// k4_tile8: 8-byte window records; chain elements by shape (a.id_ep set: the
+// dependency table maps every shape into range) or by endpoint (gathered)
+void launch_chain_tile8(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint32_t *cparent, uint32_t n,
+                        const uint32_t *dep_ep, uint32_t n_shapes, uint32_t *tile_stats, const ChainRun &a);
 // zero the chain-table entries this run wrote (instead of a memset of the table)
 void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
                         const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);
@@ -186,7 +203,8 @@ void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, cons
                        const uint32_t *dep_ep,
                        uint32_t n_shapes, uint32_t n_ep, uint64_t seed, void *ctab, uint64_t ccap,
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned int *counters,
-                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct, uint32_t ablate = 0);
+                       unsigned long long *stats64, uint32_t *gpos, uint32_t gcap, bool direct, uint32_t ablate = 0,
+                       bool by_shape = false);
 // shape-level K3 partials -> endpoint groups / dependency-endpoint records
 void launch_collapse_groups(hipStream_t s, const unsigned long long *sg, uint32_t n_shapes, uint32_t S,
                             const uint32_t *map, uint32_t n_ep, unsigned long long *grp, unsigned int *counters);
@@ -224,7 +242,7 @@ void launch_unresolved(hipStream_t s, const uint64_t *pid, const uint32_t *dp, u
 // hist [route_chunks(n) * world] u32 scratch, tot [world] counts
 uint32_t route_chunks(uint32_t n);
 bool launch_route(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint32_t *hist,
-                  unsigned long long *tot, unsigned long long *out);
+                  unsigned long long *tot, unsigned long long *out, uint64_t segw = 0);
 void launch_ids_count(hipStream_t s, const unsigned long long *ids, uint64_t m, unsigned long long *set, uint64_t cap,
                       const uint64_t *sid, uint32_t n, unsigned long long *found);
 

@@ -296,10 +296,16 @@ static inline uint32_t tile_sum_blocks(uint32_t ntiles) { return std::min<uint32
 // (every record's duration is < 2^20: wider ones are escapes).  Written out in
 // the unpacked partial format (s2 split into lo32 / hi32 limbs, the first
 // block global); k3_first_fix turns blocks into span indices.
-constexpr int K3RT = 256;
+#ifndef KMZ_K3RT
+#define KMZ_K3RT 256
+#endif
+constexpr int K3RT = KMZ_K3RT;  // balanced-reduce threads per workgroup
 constexpr uint32_t K3RB = 64;  // runs per wave batch (one per lane)
 #ifndef KMZ_K3_U
 #define KMZ_K3_U 4  // records per lane in flight in k3_reduce_bal's record loop
+#endif
+#ifndef KMZ_K3_SEARCH
+#define KMZ_K3_SEARCH 0  // 1: round 4's binary search for a record's run (A/B)
 #endif
 #ifndef KMZ_K3_COND
 #define KMZ_K3_COND 1  // max / min atomics only when a plain read says they move
@@ -523,7 +529,8 @@ template <bool PACK>
 __device__ __forceinline__ void k3_reduce_items(const uint64_t *__restrict__ pool, const uint32_t *__restrict__ row,
                                                 const uint64_t *__restrict__ tbase, uint64_t tb, uint64_t te,
                                                 unsigned long long *acc, uint32_t (*r_pre)[K3RB],
-                                                uint32_t (*r_off)[K3RB], uint64_t (*r_tb)[K3RB]) {
+                                                uint32_t (*r_off)[K3RB], uint64_t (*r_tb)[K3RB],
+                                                uint8_t (*r_tile)[K3RB], unsigned long long *r_mask) {
   constexpr uint32_t NW = K3RT / 64;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned long long *a0 = acc, *a1 = acc + K3R, *a2 = acc + 2 * K3R, *a3 = acc + 3 * K3R, *a_tsx = acc + 4 * K3R,
@@ -546,30 +553,58 @@ __device__ __forceinline__ void k3_reduce_items(const uint64_t *__restrict__ poo
       if (lane >= (uint32_t)d) incl += y;
     }
     const uint32_t total = __shfl(incl, 63, 64);
-    r_pre[w][lane] = incl - c;
-    r_off[w][lane] = (uint32_t)(k < te ? k : 0) * K3T + o;
-    r_tb[w][lane] = c ? tbase[k] : 0;
+    // the non-empty runs, compacted (so that no two share a start): run i's
+    // start, pool offset, time base and tile
+    const uint64_t ne = __ballot(c != 0);
+    const uint32_t ci = __popcll(ne & ((1ull << lane) - 1)), pre = incl - c;
+    if (c) {
+      r_pre[w][ci] = pre;
+      r_off[w][ci] = (uint32_t)k * K3T + o;
+      r_tb[w][ci] = tbase[k];
+      r_tile[w][ci] = lane;
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // a record's run without a search: per 64 records [b, b + 64), the runs
+    // starting inside set their bit of a start mask (lane i holds compacted
+    // run i's start); run(q) = (runs starting before b) + popcount of the
+    // mask's bits <= q - b, minus one
+    const uint32_t nr = (uint32_t)__popcll(ne);
+    const uint32_t mypre = lane < nr ? r_pre[w][lane] : 0xFFFFFFFFu;
     for (uint32_t q0 = 0; q0 < total; q0 += 64 * U) {
       uint64_t xr[U];
       uint32_t run[U];
       bool v[U];
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
-        const uint32_t q = q0 + u * 64 + lane;
+        const uint32_t b = q0 + u * 64, q = b + lane;
         v[u] = q < total;
+#if KMZ_K3_SEARCH  // (round 4: a binary search over the run starts, six dependent LDS reads)
         uint32_t jj = 0;
 #pragma unroll
-        for (uint32_t b = 32; b; b >>= 1)
-          if (r_pre[w][jj + b] <= q) jj += b;
+        for (uint32_t bb = 32; bb; bb >>= 1)
+          if (jj + bb < nr && r_pre[w][jj + bb] <= q) jj += bb;
+#else
+        const uint32_t sft = mypre - b;  // (wraps for runs starting before b)
+        // the wave's start mask in LDS: cleared by lane 0, one OR per run
+        // starting in [b, b + 64), read back by every lane (one wave's LDS
+        // operations complete in order)
+        if (lane == 0) r_mask[w] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (sft < 64) atomicOr(&r_mask[w], 1ull << sft);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const uint64_t m = r_mask[w];
+        const uint32_t before = (uint32_t)__popcll(__ballot(mypre < b));
+        uint32_t jj = before + (uint32_t)__popcll(m & (~0ull >> (63 - lane))) - 1;
+        jj = v[u] ? jj : 0;  // (a lane past the records: any run, its load is not used)
+#endif
         run[u] = jj;
         xr[u] = pool[v[u] ? r_off[w][jj] + (q - r_pre[w][jj]) : 0];
       }
 #pragma unroll
       for (uint32_t u = 0; u < U; ++u) {
         if (!v[u]) continue;
-        const uint64_t tile = k0 + run[u];
+        const uint64_t tile = k0 + r_tile[w][run[u]];
         const uint64_t fb = PACK ? (uint64_t)((uint32_t)(tile - tb) * K3_BPT + k3_rec_blk(xr[u]))
                                  : tile * K3_BPT + k3_rec_blk(xr[u]);
         k3_accumulate<PACK>(xr[u], r_tb[w][run[u]] + k3_rec_toff(xr[u]), fb, a0, a1, a2, a3, a_tsx, a_fst, a_fst32);
@@ -587,6 +622,8 @@ __global__ void __launch_bounds__(K3RT) k3_reduce_bal(const uint64_t *__restrict
   constexpr uint32_t NW = K3RT / 64;
   __shared__ uint32_t r_pre[NW][K3RB], r_off[NW][K3RB], wred[NW];
   __shared__ uint64_t r_tb[NW][K3RB];
+  __shared__ uint8_t r_tile[NW][K3RB];
+  __shared__ unsigned long long r_mask[NW];
   const uint32_t item = blockIdx.x;
   if (item >= item_off[P]) return;  // (the grid is an upper bound; uniform over the workgroup)
   uint32_t lo = 0, hi = P;  // the partition: item_off[p] <= item < item_off[p + 1]
@@ -618,9 +655,9 @@ __global__ void __launch_bounds__(K3RT) k3_reduce_bal(const uint64_t *__restrict
   const bool pack = tot < (1u << 22) && !upk;  // (upk: test knob)
   // packed: cs, s2, -, -, tsx, fst32 (u32) -- unpacked: cnt, s1, s2a, s2b, tsx, fst
   if (pack)
-    k3_reduce_items<true>(pool, row, tbase, tb, te, acc, r_pre, r_off, r_tb);
+    k3_reduce_items<true>(pool, row, tbase, tb, te, acc, r_pre, r_off, r_tb, r_tile, r_mask);
   else
-    k3_reduce_items<false>(pool, row, tbase, tb, te, acc, r_pre, r_off, r_tb);
+    k3_reduce_items<false>(pool, row, tbase, tb, te, acc, r_pre, r_off, r_tb, r_tile, r_mask);
   __syncthreads();
   unsigned long long *b = part + (uint64_t)item * K3F * K3R;
   for (uint32_t k = threadIdx.x; k < K3R; k += K3RT) {

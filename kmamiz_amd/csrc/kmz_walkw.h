@@ -4,9 +4,9 @@
 // (k4_tile, kmz_walk.hip).  See kmz_chain.hip for the chain table and its
 // exactness argument; the reference walk is Traces.ts:138-208.
 //
-// Input: the window as 16-byte LDS records {element hash lo, hi, endpoint,
-// window-local contracted parent | kind << 16} (W_NONE root, W_OUT outside the
-// window, W_CYC a CLIENT loop) and the tile's non-CLIENT spans compacted into
+// Input: the window as LDS records (Rec16 / Rec8 below: element hash or
+// endpoint, window-local contracted parent | kind << 16; W_NONE root, W_OUT
+// outside the window, W_CYC a CLIENT loop) and the tile's non-CLIENT spans compacted into
 // `wlist` (tile-local indices).  Per round every thread takes TW of them:
 //   walk     a Horner fold over the LDS element hashes of the ancestors (the
 //            depth is the step count; the loop runs while any lane walks);
@@ -48,7 +48,25 @@ struct ChainRun {
   uint32_t n_ep;
   uint64_t index_base, seed;
   uint32_t ablate;
+  // the records' element ids are shapes (k4_tile8 on a dependency table that
+  // maps every shape into range): id_ep maps one to its endpoint where a key
+  // or an endpoint update needs it; null: the ids are endpoints
+  const uint32_t *id_ep = nullptr;
+  uint32_t n_ids = 0;  // (shape ids: n_shapes; an id past it is NONE)
 };
+
+// an edge key over shape ids -> the same key over their dependency endpoints
+// (an id past n_ids -- NONE's 24 bits -- stays as it is, as NONE did)
+__device__ __forceinline__ uint64_t key_ids_to_eps(uint64_t key, const uint32_t *__restrict__ id_ep, uint32_t n_ids) {
+  const uint32_t ia = (uint32_t)(key >> 40), id = (uint32_t)(key >> 16) & 0xFFFFFFu;
+  const uint64_t ea = ia < n_ids ? id_ep[ia] : ia, ed = id < n_ids ? id_ep[id] : id;
+  return (ea << 40) | (ed << 16) | (key & 0xFFFFull);
+}
+
+// a record id's dependency endpoint (NONE stays NONE)
+__device__ __forceinline__ uint32_t run_ep(const ChainRun &a, uint32_t id) {
+  return (a.id_ep && id != NONE) ? a.id_ep[id] : id;
+}
 
 // per-round LDS of the walk: the leader map and the list reservations
 struct ChainLds {
@@ -61,15 +79,39 @@ __device__ __forceinline__ void chain_lds_init(ChainLds &L) {
   if (threadIdx.x < 3) L.l_need[threadIdx.x] = 0;
 }
 
+// Window records.  Rec16 (the fused join + walk): {element lo, element hi,
+// endpoint, window parent | kind << 16}.  Rec8 (k4_tile, round 5): {epk
+// (kind << 30 | endpoint), window parent | kind << 16}; the element is
+// computed per step from the endpoint (sig_elem: one multiply), so the record
+// is half the LDS and one ds_read_b64.  Both give the same elements.
+struct Rec16 {
+  using T = uint4;
+  static __device__ __forceinline__ uint32_t kind(const T &r) { return (r.w >> 16) & 3; }
+  static __device__ __forceinline__ uint32_t ep(const T &r) { return r.z; }
+  static __device__ __forceinline__ uint32_t parent(const T &r) { return r.w & 0xFFFF; }
+  static __device__ __forceinline__ uint64_t elem(const T &r, uint64_t) { return (uint64_t)r.y << 32 | r.x; }
+};
+struct Rec8 {  // (the id: a shape, or an endpoint)
+  using T = uint2;
+  static __device__ __forceinline__ uint32_t kind(const T &r) { return (r.y >> 16) & 3; }
+  static __device__ __forceinline__ uint32_t ep(const T &r) { return epk_ep(r.x); }
+  static __device__ __forceinline__ uint32_t parent(const T &r) { return r.y & 0xFFFF; }
+  static __device__ __forceinline__ uint64_t elem(const T &r, uint64_t seed) {
+    return sig_elem(r.x & EPK_NONE, ((r.y >> 16) & 3) == KIND_SERVER, seed);
+  }
+};
+
 // All rounds of one tile.  W: window slots (an index >= W is not a window
-// slot); NT: threads of the workgroup; TW: walkers per thread and round.  The
-// caller has published lrec / wlist / m with a barrier; this returns after a
-// barrier (the window may be rewritten).
-template <uint32_t W, int NT, int TW>
-__device__ __forceinline__ void chain_walk_rounds(const uint4 *__restrict__ lrec, const uint16_t *__restrict__ wlist,
-                                                  uint32_t m, uint32_t w0, uint32_t toff, bool any_other, ChainLds &L,
-                                                  const ChainRun a, uint32_t &rows, uint32_t &rel, uint32_t &maxd,
-                                                  uint32_t &fresh_n, uint32_t &flags) {
+// slot); NT: threads of the workgroup; TW: walkers per thread and round; R:
+// the record layout.  The caller has published lrec / wlist / m with a
+// barrier; this returns after a barrier (the window may be rewritten).
+template <uint32_t W, int NT, int TW, class R = Rec16>
+__device__ __forceinline__ void chain_walk_rounds(const typename R::T *__restrict__ lrec,
+                                                  const uint16_t *__restrict__ wlist, uint32_t m, uint32_t w0,
+                                                  uint32_t toff, bool any_other, ChainLds &L, const ChainRun a,
+                                                  uint32_t &rows, uint32_t &rel, uint32_t &maxd, uint32_t &fresh_n,
+                                                  uint32_t &flags) {
+  using RT = typename R::T;
   const uint32_t spin = spin_bound(a.ablate);
   const bool hash_on = !(a.ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
   for (uint32_t r0 = 0; r0 < m; r0 += TW * NT) {
@@ -82,10 +124,10 @@ __device__ __forceinline__ void chain_walk_rounds(const uint4 *__restrict__ lrec
       const bool on = idx < m;
       const uint32_t jl = on ? toff + wlist[idx] : W - 1;
       jq[q] = jl;
-      const uint4 r = lrec[jl];
-      kq[q] = (r.w >> 16) & 3;
-      myep[q] = r.z;
-      sg[q] = (uint64_t)r.y << 32 | r.x;  // the element hash until the walk is done
+      const RT r = lrec[jl];
+      kq[q] = R::kind(r);
+      myep[q] = R::ep(r);
+      sg[q] = R::elem(r, a.seed);  // the element hash until the walk is done
       acc[q] = 0;
       dd[q] = 0;
       wa[q] = W_NONE;
@@ -96,8 +138,9 @@ __device__ __forceinline__ void chain_walk_rounds(const uint4 *__restrict__ lrec
       }
       st[q] = S_DONE;
       if (!hash_on) continue;
-      if (kq[q] == KIND_SERVER && r.z >= a.n_ep) flags |= F_RANGE;
-      wa[q] = r.w & 0xFFFF;
+      // (ids that are shapes are in range whenever they are not NONE)
+      if (kq[q] == KIND_SERVER && (a.id_ep ? myep[q] == NONE : myep[q] >= a.n_ep)) flags |= F_RANGE;
+      wa[q] = R::parent(r);
     }
     // the TW walks of a thread step together: TW independent LDS reads in
     // flight per step, then branch-free updates (compiled without the
@@ -109,23 +152,24 @@ __device__ __forceinline__ void chain_walk_rounds(const uint4 *__restrict__ lrec
 #pragma unroll
         for (int q = 0; q < TW; ++q) go |= wa[q] < W;
         if (__ballot(go) == 0) break;
-        uint4 r[TW];
+        RT r[TW];
 #pragma unroll
         for (int q = 0; q < TW; ++q) r[q] = lrec[wa[q] < W ? wa[q] : 0];
 #pragma unroll
         for (int q = 0; q < TW; ++q) {
           const bool act = wa[q] < W;
-          const uint64_t nacc = sig_step(acc[q], (uint64_t)r[q].y << 32 | r[q].x);
-          if (OTHER && act && kq[q] == KIND_SERVER && ((r[q].w >> 16) & 3) != KIND_SERVER) {
+          const uint64_t nacc = sig_step(acc[q], R::elem(r[q], a.seed));
+          if (OTHER && act && kq[q] == KIND_SERVER && R::kind(r[q]) != KIND_SERVER) {
             // (rare) a non-SERVER ancestor of a row: its lastUsage
-            if (r[q].z < a.n_ep)
-              atomicMax(&a.ep_ts[r[q].z], (unsigned long long)((uint64_t)a.ts[w0 + wa[q]] ^ TS_BIAS));
+            const uint32_t e = run_ep(a, R::ep(r[q]));
+            if (e < a.n_ep)
+              atomicMax(&a.ep_ts[e], (unsigned long long)((uint64_t)a.ts[w0 + wa[q]] ^ TS_BIAS));
             else
               flags |= F_RANGE;
           }
           acc[q] = act ? nacc : acc[q];
           dd[q] = act ? it + 1 : dd[q];
-          wa[q] = act ? (r[q].w & 0xFFFF) : wa[q];
+          wa[q] = act ? R::parent(r[q]) : wa[q];
         }
       }
     };
@@ -177,7 +221,7 @@ __device__ __forceinline__ void chain_walk_rounds(const uint4 *__restrict__ lrec
         if (w01[q].y != ps[q]) flags |= F_SIG;
         continue;
       }
-      uint32_t h = (uint32_t)(sg[q] >> 32) & (IMAP - 1);
+      uint32_t h = (uint32_t)(sig_place(sg[q]) >> 32) & (IMAP - 1);
       hslot[q] = IMAP;  // a leader without a map slot (map full)
       for (uint32_t t = 0; t < 8; ++t) {
         const unsigned long long kk = atomicCAS(&L.imap_sig[h], 0ull, (unsigned long long)sg[q]);
@@ -250,17 +294,19 @@ __device__ __forceinline__ void chain_walk_rounds(const uint4 *__restrict__ lrec
         const uint32_t d = dd[q];
         if (os[q]) {  // the row's keys (ancestor k, row endpoint, k, ancestor is SERVER)
           const uint64_t base = (uint64_t)L.l_base[0] + os[q] - 1;
-          uint32_t an = lrec[jq[q]].w & 0xFFFF;
+          // (shape ids: the keys are staged over shapes and mapped to
+          // endpoints by k_chain_settle_list -- no gather in the walk)
+          uint32_t an = R::parent(lrec[jq[q]]);
           for (uint32_t kk = 1; kk <= d; ++kk) {
-            const uint4 r = lrec[an];
-            const uint64_t key = edge_key(r.z, myep[q], kk, ((r.w >> 16) & 3) == KIND_SERVER);
+            const RT r = lrec[an];
+            const uint64_t key = edge_key(R::ep(r), myep[q], kk, R::kind(r) == KIND_SERVER);
             if (base + kk - 1 < a.scap) {
               a.stage[base + kk - 1] = key;
             } else {
-              edge_insert(key, a.trip, a.tcap, &flags);
+              edge_insert(a.id_ep ? key_ids_to_eps(key, a.id_ep, a.n_ids) : key, a.trip, a.tcap, &flags);
               flags |= F_STAGE_FULL;
             }
-            an = r.w & 0xFFFF;
+            an = R::parent(r);
           }
         }
         if (cvq[q] == 0) {  // won the slot (published above)

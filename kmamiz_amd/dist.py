@@ -120,7 +120,14 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
     if crossed and isinstance(check_ids, IdGuard):
         check_ids.abandon()  # its exchange was posted before the run: drain it on every rank
     if not crossed and a[6] > 0:
-        crossed = _check_shards(engine, nu, int(a[6]), dev, group, raise_=not exact)
+        try:
+            crossed = _check_shards(engine, nu, int(a[6]), dev, group, raise_=not exact)
+        except ShardingError:
+            if isinstance(check_ids, IdGuard):
+                check_ids.abandon()
+            raise
+        if crossed and isinstance(check_ids, IdGuard):
+            check_ids.abandon()  # posted before the run: drained before the exact merge's collectives
     if not crossed:
         if isinstance(check_ids, IdGuard):  # started before the run: its exchange overlapped it
             crossed = check_ids.finish(raise_=not exact)
@@ -188,13 +195,27 @@ def route_ids_np(span_ids: np.ndarray, world: int):
     return h[order], np.bincount(own, minlength=world).astype(np.int64)
 
 
+# agreed fixed-segment size of IdGuard's exchange per (group, world): set on
+# every rank from the same all-reduced maximum in IdGuard.finish
+_ID_SEG: dict = {}
+
+
 class IdGuard:
     """The cross-shard repeated-span-id check (check_repeated_ids) split in
-    two, so that its all-to-all overlaps the run: ``start()`` routes this
-    rank's id hashes (kmz_route_ids, on the engine's stream) and posts the
-    exchange asynchronously; ``finish()`` waits for it, runs the uniqueness
-    certificate over what this rank received (kmz_id_repeats) and agrees on
-    the verdict (a MAX all-reduce), raising ShardingError on a repeat."""
+    two, so that its all-to-all overlaps the run.
+
+    ``start()`` routes this rank's id hashes and posts the exchange.  Once the
+    ranks have agreed on a segment size (the previous finish()), the routing
+    writes fixed segments (kmz_route_ids_fixed: each owner's count, then its
+    values) and the exchange is an all-to-all of equal segments, so start()
+    only enqueues: no counts exchange and no stream synchronisation before the
+    run (under RCCL the all-to-all is posted on device tensors behind the
+    routing; under gloo, CPU-only, the copy and the exchange wait for
+    finish()).  The first call, and any step whose segment overflowed on some
+    rank, use the exact protocol: the counts all-to-all, then the values with
+    those split sizes.  ``finish()`` runs the uniqueness certificate over what
+    this rank received (kmz_id_repeats) and agrees on the verdict and the next
+    segment size in one MAX all-reduce, raising ShardingError on a repeat."""
 
     def __init__(self, engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None):
         self.engine, self.group, self.span_ids = engine, group, span_ids
@@ -203,11 +224,36 @@ class IdGuard:
         self.on_dev = (engine is not None and dev is not None and torch.device(dev).type == "cuda"
                        and dist.get_backend(group) == "nccl")
         self.dev = torch.device(dev) if self.on_dev else torch.device("cpu")
-        self.work = None
+        # (gloo with the engine on a GPU: the routing is still enqueued on the device)
+        self.route_dev = (torch.device(dev) if engine is not None and dev is not None
+                          and torch.device(dev).type == "cuda" else None)
+        self.key = (id(group) if group is not None else None, self.world)
+        self.work = self.fixed = self.pending = None
 
     def start(self) -> "IdGuard":
         if self.world == 1:
             return self
+        seg = _ID_SEG.get(self.key) if self.engine is not None else None
+        if seg is not None:
+            self.fixed = seg
+            if self.route_dev is not None:  # enqueued on the engine's stream, no wait
+                send = torch.empty(self.world * seg, dtype=torch.int64, device=self.route_dev)
+                self.engine.route_ids_fixed(self.world, seg, send.data_ptr(), True)
+            else:
+                send = torch.empty(self.world * seg, dtype=torch.int64)
+                self.engine.route_ids_fixed(self.world, seg, send.data_ptr(), False)
+            if self.on_dev:
+                self.recv = torch.empty_like(send)
+                self.send = send
+                self.work = dist.all_to_all_single(self.recv, send, group=self.group, async_op=True)
+            else:
+                self.pending = send  # (gloo: copied and exchanged in finish)
+            return self
+        return self._start_counts()
+
+    def _start_counts(self) -> "IdGuard":
+        """The exact protocol: counts first, then the values with those splits."""
+        self.fixed = None
         if self.engine is not None:
             n = int(self.engine.n)
             send = torch.empty(max(1, n), dtype=torch.int64, device=self.dev)
@@ -223,6 +269,7 @@ class IdGuard:
         rc = rcnt.tolist()
         self.recv = torch.empty(max(1, sum(rc)), dtype=torch.int64, device=self.dev)
         self.m = sum(rc)
+        self.maxc = max(rc) if rc else 0
         self.send = send  # (kept alive until the exchange is done)
         self.work = dist.all_to_all_single(self.recv[: self.m], send, output_split_sizes=rc, input_split_sizes=counts,
                                            group=self.group, async_op=True)
@@ -233,31 +280,64 @@ class IdGuard:
         this when the merge is refused before the guard's verdict)."""
         if self.work is not None:
             self.work.wait()
-        self.work = self.send = self.recv = None
+        if self.pending is not None:  # (gloo, fixed segments: the exchange every rank still posts)
+            send = self.pending.cpu()
+            dist.all_to_all_single(torch.empty_like(send), send, group=self.group)
+        self.work = self.send = self.recv = self.pending = None
+
+    def _received(self):
+        """-> (this rank's received values, the largest count any source sent
+        it, whether some source's segment overflowed)."""
+        if self.fixed is None:
+            self.work.wait()
+            return self.recv[: self.m], self.maxc, False
+        seg = self.fixed
+        if self.pending is not None:
+            send = self.pending.cpu()  # (waits for the routing on the engine's stream)
+            self.pending = None
+            self.recv = torch.empty_like(send)
+            dist.all_to_all_single(self.recv, send, group=self.group)
+        else:
+            self.work.wait()
+        r = self.recv.view(self.world, seg)
+        cnt = r[:, 0]
+        maxc = int(cnt.max().item())
+        if maxc >= seg:
+            return None, maxc, True
+        keep = torch.arange(seg - 1, device=r.device)[None, :] < cnt[:, None]
+        return r[:, 1:][keep], maxc, False
 
     def finish(self, raise_: bool = True) -> bool:
         """-> True when some span id is in two shards (ShardingError instead
         with ``raise_``)."""
         if self.world == 1:
             return False
-        if self.work is None:
+        if self.work is None and self.pending is None:
             self.start()
-        self.work.wait()
-        recv = self.recv[: self.m]
-        if self.on_dev:
-            torch.cuda.current_stream(self.dev).synchronize()  # (the engine's stream may not be torch's)
+        recv, maxc, over = self._received()
         rep = None
-        if self.engine is not None and recv.numel():
-            rep = self.engine.id_repeats(recv.data_ptr(), recv.numel(), self.on_dev)
-        if rep is None:  # host check (no engine, or the certificate could not decide)
-            rep = bool(recv.numel()) and torch.unique(recv).numel() != recv.numel()
-        flag = torch.tensor([1 if rep else 0], dtype=torch.int64, device=self.dev)
+        if not over:
+            if self.on_dev:
+                torch.cuda.current_stream(self.dev).synchronize()  # (the engine's stream may not be torch's)
+            if self.engine is not None and recv.numel():
+                rep = self.engine.id_repeats(recv.data_ptr(), recv.numel(), self.on_dev)
+            if rep is None:  # host check (no engine, or the certificate could not decide)
+                rep = bool(recv.numel()) and torch.unique(recv).numel() != recv.numel()
+        # one MAX all-reduce: the verdict, any overflow, the largest count (the
+        # next step's segment size, the same on every rank)
+        flag = torch.tensor([1 if rep else 0, 1 if over else 0, maxc], dtype=torch.int64, device=self.dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        f = flag.tolist()
         self.work = self.send = self.recv = None
-        if int(flag.item()) and raise_:
+        if self.engine is not None:
+            _ID_SEG[self.key] = int(f[2] * 1.125) + 1025
+        if f[1]:  # a segment overflowed somewhere: this step exactly, every rank
+            self._start_counts()
+            return self.finish(raise_)
+        if f[0] and raise_:
             raise ShardingError("a span id occurs in two shards: the reference's global span map would merge them "
                                 "(Traces.ts:117-123); run unsharded")
-        return bool(int(flag.item()))
+        return bool(f[0])
 
 
 def check_repeated_ids(engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None) -> None:
@@ -338,10 +418,10 @@ def _bcast(t: torch.Tensor, dev, group=None) -> torch.Tensor:
     """Broadcast a host tensor from rank 0 on ``dev``'s backend (device
     tensors under RCCL); returns it on the host."""
     if dev.type == "cpu":
-        dist.broadcast(t, src=0, group=group)
+        dist.broadcast(t, group=group, group_src=0)
         return t
     d = t.to(dev)
-    dist.broadcast(d, src=0, group=group)
+    dist.broadcast(d, group=group, group_src=0)
     return d.cpu()
 
 
@@ -354,56 +434,46 @@ def _unsharded_deps(engine, e: torch.Tensor, E: int, dev, group=None) -> None:
     keys, which replace every rank's own (``e`` in place; the engine's edge
     set by kmz_set_triples).  Cost: the batch's columns (35 B/span) to rank 0
     and one unsharded dependency pass there, only when a guard fires."""
-    import numpy as np
-
-    from . import _lib as L
-    from .engine import Engine, ShapeTable, SpanBatch
-
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    b = engine.spans()
-    tab = engine.shape_table()
-    mine = {"gidx": engine.global_index(), "sid": b.span_id, "pid": b.parent_id, "kind": b.kind, "shape": b.shape,
-            "status": b.status, "dur": b.duration, "ts": b.timestamp,
-            "tab": (np.asarray(tab.rt_ep, np.uint32), np.asarray(tab.tag_ep, np.uint32),
-                    np.asarray(tab.dep_ep, np.uint32), int(tab.n_rt_ep), int(tab.n_tag_ep), int(tab.n_dep_ep),
-                    int(tab.n_status))}
-    parts = [None] * world
-    dist.all_gather_object(parts, mine, group=group)
+    try:
+        b = engine.spans()
+        tab = engine.shape_table()
+        mine = {"gidx": engine.global_index(), "sid": b.span_id, "pid": b.parent_id, "kind": b.kind,
+                "shape": b.shape, "status": b.status, "dur": b.duration, "ts": b.timestamp,
+                "tab": (np.asarray(tab.rt_ep, np.uint32), np.asarray(tab.tag_ep, np.uint32),
+                        np.asarray(tab.dep_ep, np.uint32), int(tab.n_rt_ep), int(tab.n_tag_ep), int(tab.n_dep_ep),
+                        int(tab.n_status))}
+    except Exception as ex:  # noqa: BLE001 (a shard that cannot send its columns fails the pass on rank 0)
+        mine = {"error": f"rank {rank}: {ex}"}
+    # only rank 0 needs the columns: gather, not all-gather (an all-gather
+    # would copy every shard to every rank)
+    parts = [None] * world if rank == 0 else None
+    dist.gather_object(mine, parts, group=group, group_dst=0)
+    del mine
     W = 2 * E  # endpoint partial words: [max ts] E, [min first row] E
-    head = torch.zeros(W + 1, dtype=torch.int64)  # endpoint partials, then the key count
+    # endpoint partials, the key count, then a status word: rank 0 reports its
+    # own failure through the broadcast every rank waits in, so that no rank is
+    # left blocked when rank 0 raises (an error on rank 0 -> ShardingError on all)
+    head = torch.zeros(W + 2, dtype=torch.int64)
     keys2 = np.zeros(0, np.uint64)
+    err = None
     if rank == 0:
-        N = sum(len(x["gidx"]) for x in parts)
-        cols = {k: np.zeros(N, dt) for k, dt in (("sid", np.uint64), ("pid", np.uint64), ("kind", np.uint8),
-                                                  ("shape", np.uint32), ("status", np.uint16), ("dur", np.uint32),
-                                                  ("ts", np.int64))}
-        soff, tabs = 0, []
-        for x in parts:  # shard r's shape s is shape soff_r + s of the whole batch
-            g = np.asarray(x["gidx"], np.int64)
-            for k in cols:
-                cols[k][g] = np.asarray(x[k]) + (np.uint32(soff) if k == "shape" else 0)
-            tabs.append(x["tab"])
-            soff += len(x["tab"][2])
-        table = ShapeTable(*(np.concatenate([t[j] for t in tabs]) for j in range(3)),
-                           *(max(t[j] for t in tabs) for j in range(3, 7)))
-        whole = SpanBatch(cols["sid"], cols["pid"], cols["kind"], cols["shape"], cols["status"], cols["dur"],
-                          cols["ts"], 0)
-        e2 = Engine(torch.cuda.current_device())
         try:
-            e2.load(whole, table)
-            e2.run(L.RUN_DEPS)
-            ew = e2.partials_words(L.PART_ENDPOINTS)
-            ep2 = np.zeros(max(1, ew), np.uint64)
-            e2.export_partials(L.PART_ENDPOINTS, ep2.ctypes.data, ew, False)
-            keys2 = np.asarray(e2.triples(sort=False), np.uint64)
-        finally:
-            e2.close()
-        if ew != W:
-            raise ShardingError(f"the unsharded pass has {ew // 2} endpoints, the shards {E}")
-        head[:W] = torch.from_numpy(ep2[:W].view(np.int64))
-        head[W] = len(keys2)
+            bad = [x["error"] for x in parts if "error" in x]
+            if bad:
+                raise ShardingError("; ".join(bad))
+            keys2 = _unsharded_pass(parts, head, W)
+        except Exception as ex:  # noqa: BLE001 (re-raised below, on every rank)
+            err = ex
+            head.zero_()
+            head[W + 1] = 1
+        parts = None
     head = _bcast(head, dev, group)
+    if int(head[W + 1].item()):
+        if err is not None:
+            raise ShardingError(f"the unsharded dependency pass failed on rank 0: {err}") from err
+        raise ShardingError("the unsharded dependency pass failed on rank 0")
     nk = int(head[W].item())
     kt = torch.zeros(max(1, nk), dtype=torch.int64)
     if rank == 0 and nk:
@@ -412,6 +482,58 @@ def _unsharded_deps(engine, e: torch.Tensor, E: int, dev, group=None) -> None:
     e[:W] = head[:W].to(e.device)
     kh = np.ascontiguousarray(kt[:nk].numpy().view(np.uint64))
     engine.set_triples(kh.ctypes.data, nk, False)
+
+
+def _unsharded_pass(parts, head: torch.Tensor, W: int) -> np.ndarray:
+    """Rank 0's half of _unsharded_deps: place every shard's spans at their
+    global flatten positions (relative to the batch's first position, which
+    is not 0 for any batch after the first), run the dependency pass of the
+    whole batch on a second engine context, write its endpoint partials and
+    key count into ``head`` and return the keys."""
+    from . import _lib as L
+    from .engine import Engine, ShapeTable, SpanBatch
+
+    N = sum(len(x["gidx"]) for x in parts)
+    nonempty = [np.asarray(x["gidx"], np.int64) for x in parts if len(x["gidx"])]
+    base = min(int(g.min()) for g in nonempty) if nonempty else 0
+    top = max(int(g.max()) for g in nonempty) + 1 if nonempty else 0
+    if top - base != N:  # the shards together must be one contiguous batch
+        raise ShardingError(f"the shards' global positions span [{base}, {top}) for {N} spans")
+    cols = {k: np.zeros(N, dt) for k, dt in (("sid", np.uint64), ("pid", np.uint64), ("kind", np.uint8),
+                                              ("shape", np.uint32), ("status", np.uint16), ("dur", np.uint32),
+                                              ("ts", np.int64))}
+    filled = np.zeros(N, np.bool_)
+    soff, tabs = 0, []
+    for x in parts:  # shard r's shape s is shape soff_r + s of the whole batch
+        g = np.asarray(x["gidx"], np.int64) - base
+        filled[g] = True
+        for k in cols:
+            cols[k][g] = np.asarray(x[k]) + (np.uint32(soff) if k == "shape" else 0)
+        tabs.append(x["tab"])
+        soff += len(x["tab"][2])
+    if not filled.all():
+        raise ShardingError("two shards claim the same global position")
+    table = ShapeTable(*(np.concatenate([t[j] for t in tabs]) for j in range(3)),
+                       *(max(t[j] for t in tabs) for j in range(3, 7)))
+    # index_base = the batch's first global position: first rows stay global
+    whole = SpanBatch(cols["sid"], cols["pid"], cols["kind"], cols["shape"], cols["status"], cols["dur"],
+                      cols["ts"], base)
+    del cols
+    e2 = Engine(torch.cuda.current_device())
+    try:
+        e2.load(whole, table)
+        e2.run(L.RUN_DEPS)
+        ew = e2.partials_words(L.PART_ENDPOINTS)
+        ep2 = np.zeros(max(1, ew), np.uint64)
+        e2.export_partials(L.PART_ENDPOINTS, ep2.ctypes.data, ew, False)
+        keys2 = np.asarray(e2.triples(sort=False), np.uint64)
+    finally:
+        e2.close()
+    if ew != W:
+        raise ShardingError(f"the unsharded pass has {ew // 2} endpoints, the shards {W // 2}")
+    head[:W] = torch.from_numpy(ep2[:W].view(np.int64))
+    head[W] = len(keys2)
+    return keys2
 
 
 def merge_edge_keys(keys: torch.Tensor, group=None) -> torch.Tensor:

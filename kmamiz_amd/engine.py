@@ -449,6 +449,13 @@ class Engine:
                                                   L.MEM_DEVICE if device else L.MEM_HOST, L.ptr(counts)))
         return [int(x) for x in counts[:world]]
 
+    def route_ids_fixed(self, world: int, seg: int, dst_ptr: int, device: bool) -> None:
+        """kmz_route_ids_fixed: ``world`` segments of ``seg`` words (count,
+        then the values) at dst; with device memory only enqueued on the
+        engine's stream (no host round trip)."""
+        L.check(self.ctx, self._lib.kmz_route_ids_fixed(self.ctx, world, seg, C.c_void_p(dst_ptr),
+                                                        L.MEM_DEVICE if device else L.MEM_HOST))
+
     def id_repeats(self, src_ptr: int, n: int, device: bool) -> Optional[bool]:
         """Whether any of the n routed values occurs twice (kmz_id_repeats);
         None when the certificate cannot decide (the caller checks another way)."""

@@ -305,3 +305,31 @@ def test_node_worker_with_filter(tmp_path):
     assert r.returncode == 0, r.stderr
     for k, (g, e) in enumerate(zip(json.loads(r.stdout), exp)):
         assert g == e[0], k
+
+
+@pytest.mark.gpu
+def test_gpu_service_tail_with_filter(engine):
+    """service_tail() with DEPRECATED_ENDPOINT_THRESHOLD set: the GPU tail of
+    the constructor-filtered graph (stale rows gone, stale endpoints stripped
+    from the kept rows' lists, EndpointDependencies.ts:44-74) == the oracle's
+    service metrics of EndpointDependencies([]).combineWith(newDep).trim()
+    under the same threshold and clock, in ticks where endpoints go stale."""
+    from kmamiz_amd import Traces
+
+    windows, nows = _retimed_windows()
+    stale_seen = 0
+    with Pinned() as p:
+        for k, (w, now) in enumerate(zip(windows, nows)):
+            p.now = now + (k % 2) * 2 * HOUR_US // 1000  # every other tick: the whole window is stale
+            win = Traces(copy.deepcopy(w), engine=engine).toEndpointDependencies()
+            red = O.strip_undef(O.EndpointDependencies([]).combineWith(
+                O.Traces(copy.deepcopy(w)).toEndpointDependencies()).trim().toJSON())
+            od = O.EndpointDependencies(red)
+            tail = win.service_tail()
+            inst = tail.instability()
+            assert inst == od.toServiceInstability(), k
+            assert tail.coupling() == od.toServiceCoupling(), k
+            stale_seen += len(red) < len(O.strip_undef(O.Traces(copy.deepcopy(w)).toEndpointDependencies().toJSON()))
+            # the filtered edge set replaced the run's: a second call runs the pass again, same answer
+            assert win.service_tail().instability() == inst, k
+    assert stale_seen > 0

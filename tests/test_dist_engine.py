@@ -97,17 +97,19 @@ def test_two_rank_merge_equals_single_engine():
         assert r[4] == exp_tail
 
 
-def _crossing_batches(case, world):
+def _crossing_batches(case, world, t0=0):
     """Per rank: the host batch of its traces, with the span-id map crossing
     shards as ``case`` says -- "parent": rank 1 has a span whose parentId is a
     span of rank 0's shard; "repeat": the last rank reuses one span id of rank
     0's shard (a leaf SERVER span: no parent link crosses); "inner": the last
     rank repeats one of its own span ids (its run takes the span-table path);
-    "none": clean shards."""
+    "none": clean shards.  ``t0``: the batch's first trace (a batch after the
+    first starts at a global flatten position > 0)."""
     from kmamiz_amd import synth
 
     ntr = 900 if case != "parent" else 700
     cut = [ntr * r // world for r in range(world + 1)] if case != "parent" else [0, 300, 700][: world + 1]
+    cut = [t0 + c for c in cut]
     out = []
     b0, _ = synth.host_batch(synth.MESH, cut[0], cut[1])
     for rank in range(world):
@@ -127,7 +129,7 @@ def _crossing_batches(case, world):
     return out
 
 
-def _crossing_worker(rank, world, port, q, case, exact):
+def _crossing_worker(rank, world, port, q, case, exact, t0=0):
     import torch
     import torch.distributed as dist
 
@@ -139,7 +141,7 @@ def _crossing_worker(rank, world, port, q, case, exact):
         from kmamiz_amd import dist as kdist
         from kmamiz_amd import synth
 
-        batch = _crossing_batches(case, world)[rank]
+        batch = _crossing_batches(case, world, t0)[rank]
         e = Engine(0)
         e.load(batch, synth.shape_table(synth.MESH))
         e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
@@ -169,11 +171,11 @@ def _crossing_worker(rank, world, port, q, case, exact):
         dist.destroy_process_group()
 
 
-def _run_crossing(case, world, exact=True):
+def _run_crossing(case, world, exact=True, t0=0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_crossing_worker, args=(r, world, port, q, case, exact)) for r in range(world)]
+    ps = [ctx.Process(target=_crossing_worker, args=(r, world, port, q, case, exact, t0)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted((q.get(timeout=150) for _ in range(world)), key=lambda r: r[0])
@@ -182,7 +184,7 @@ def _run_crossing(case, world, exact=True):
     return res
 
 
-def _whole_batch_expected(case, world):
+def _whole_batch_expected(case, world, t0=0):
     """One engine over the whole batch (the reference's single global span
     map), and the C oracle's edge keys and endpoints of the same batch."""
     from kmamiz_amd import Engine, SpanBatch
@@ -190,10 +192,10 @@ def _whole_batch_expected(case, world):
     from kmamiz_amd import synth
     from oracle import c_oracle
 
-    parts = _crossing_batches(case, world)
+    parts = _crossing_batches(case, world, t0)
     cols = {f: np.concatenate([getattr(b, f) for b in parts]) for f in ("span_id", "parent_id", "kind", "shape",
                                                                       "status", "duration", "timestamp")}
-    whole = SpanBatch(index_base=0, **cols)
+    whole = SpanBatch(index_base=parts[0].index_base, **cols)
     table = synth.shape_table(synth.MESH)
     e = Engine(0)
     try:
@@ -208,18 +210,20 @@ def _whole_batch_expected(case, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,world", [("parent", 2), ("repeat", 2), ("repeat", 3), ("inner", 2)])
-def test_crossing_shards_merge_exactly(case, world):
+@pytest.mark.parametrize("case,world,t0", [("parent", 2, 0), ("repeat", 2, 0), ("repeat", 3, 0), ("inner", 2, 0),
+                                          ("repeat", 2, 1000), ("parent", 2, 500)])
+def test_crossing_shards_merge_exactly(case, world, t0):
     """SURVEY.md 8e / Traces.ts:117-143: the reference keys ONE Map by span id
     over the whole batch, so a parent in another shard, an id in two shards or
     an id repeated inside one shard changes rows and edges that per-shard runs
     cannot see.  merge_all's guards find it on every rank and the merge stays
     exact (one unsharded dependency pass on rank 0, broadcast): every rank ends
     with the single-engine result over the whole batch, bit for bit, whose
-    edges and endpoints equal the C oracle's."""
-    res = _run_crossing(case, world)
+    edges and endpoints equal the C oracle's.  ``t0`` > 0: a batch that does
+    not start at global position 0 (the first rows stay global)."""
+    res = _run_crossing(case, world, t0=t0)
     assert [r[1] for r in res] == ["merged"] * world, [r[1] for r in res]
-    exp, okeys, oep = _whole_batch_expected(case, world)
+    exp, okeys, oep = _whole_batch_expected(case, world, t0)
     assert np.array_equal(np.frombuffer(exp[1], np.uint64), okeys)
     from kmamiz_amd import _lib as L
 

@@ -65,3 +65,102 @@ def test_id_repeats_past_1e8_values(engine):
     assert engine.id_repeats(v.data_ptr(), m, True) is True
     del v
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("device", [False, True])
+def test_route_ids_fixed_equals_host_mirror(engine, world, device):
+    """kmz_route_ids_fixed: segment r = [count_r, its hashes] (word 0 the true
+    count even past the segment: an overflowed segment says so)."""
+    from kmamiz_amd import dist as kdist
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(synth.MESH, 0, 3000)
+    engine.load(batch, synth.shape_table(synth.MESH))
+    h, c = kdist.route_ids_np(batch.span_id, world)
+    for seg in (int(c.max()) + 1 + 7, max(2, int(c.max()) // 2)):
+        out = torch.zeros(world * seg, dtype=torch.int64, device="cuda" if device else "cpu")
+        engine.route_ids_fixed(world, seg, out.data_ptr(), device)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint64).reshape(world, seg)
+        assert got[:, 0].tolist() == c.tolist()
+        o = 0
+        for r in range(world):
+            k = min(int(c[r]), seg - 1)
+            mine = h[o : o + int(c[r])]
+            if k == int(c[r]):  # complete segment: exactly its hashes
+                assert np.array_equal(np.sort(got[r, 1 : 1 + k]), np.sort(mine))
+            else:  # overflowed: a subset of them
+                assert np.isin(got[r, 1:], mine).all()
+            o += int(c[r])
+
+
+def _guard_worker(rank, world, port, q, dev_kind):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kmamiz_amd import Engine
+        from kmamiz_amd import dist as kdist
+        from kmamiz_amd import synth
+
+        e = Engine(0)
+        dev = torch.device("cuda", 0) if dev_kind == "cuda" else torch.device("cpu")
+        cut = [0, 400, 900, 1300][: world + 1]
+        b0, _ = synth.host_batch(synth.MESH, cut[0], cut[1])
+        out = []
+        # steps: clean (exact protocol, first), clean (fixed segments), a
+        # repeat across shards (fixed), clean with a forced tiny segment
+        # (overflow -> the exact protocol, same step), a repeat after it
+        for step, (rep, tiny) in enumerate([(False, False), (False, False), (True, False), (False, True),
+                                            (True, False)]):
+            batch, _ = synth.host_batch(synth.MESH, cut[rank], cut[rank + 1])
+            if rep and rank == world - 1:
+                batch.span_id[len(batch) - 1] = b0.span_id[5]
+            e.load(batch, synth.shape_table(synth.MESH))
+            if tiny:
+                kdist._ID_SEG[(None, world)] = 4
+            g = kdist.IdGuard(e, dev).start()
+            fixed = g.fixed is not None
+            got = g.finish(raise_=False)
+            out.append((fixed, got))
+        q.put((rank, out))
+        e.close()
+    except Exception:
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,dev_kind", [(2, "cpu"), (3, "cuda")])
+def test_id_guard_fixed_segments_over_steps(world, dev_kind):
+    """IdGuard across steps (dist.py): the first step exchanges counts, later
+    ones fixed segments with no host round trip in start(); a repeat across
+    shards is found either way, and a step whose segment overflows (forced
+    here) is redone exactly on every rank."""
+    import multiprocessing as mp
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_guard_worker, args=(r, world, port, q, dev_kind)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=200) for _ in range(world)), key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert isinstance(r[1], list), r[1]
+        fixed = [x[0] for x in r[1]]
+        found = [x[1] for x in r[1]]
+        assert fixed == [False, True, True, True, True]
+        assert found == [False, False, True, False, True]

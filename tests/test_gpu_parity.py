@@ -8,6 +8,7 @@
 * size-independent properties at BASELINE.json's full sizes.
 """
 import math
+import os
 import random
 
 import numpy as np
@@ -273,6 +274,64 @@ def test_wide_durations_vs_c_oracle(engine, ntr):
     b2 = SpanBatch(batch.span_id, batch.parent_id, batch.kind, batch.shape, batch.status,
                    d.astype(batch.duration.dtype), batch.timestamp, batch.index_base)
     _compare_synth(engine, b2, synth.shape_table(3))
+
+
+@pytest.mark.parametrize("ntr", [3000, 40000])
+def test_chain_elements_by_shape_with_shared_endpoints(engine, ntr):
+    """k4_tile8 interns chains over shapes when the dependency table maps
+    every shape into range (kmz_walk.hip): exact whatever the table, only
+    fewer repeats where shapes share an endpoint.  Here every mesh endpoint
+    gets a second shape (s + n and s map to endpoint s) and a third of the
+    spans move to it; rows, relations, edge keys and endpoints equal the C
+    oracle and the same run with chain elements by endpoint (KMZ_ABLATE2 bit
+    11); the shape chains outnumber the endpoint chains.  (Fresh engines with
+    chain interning forced and the fused kernel off, so that k4_tile8 runs at
+    both sizes.)"""
+    from kmamiz_amd import Engine
+    from kmamiz_amd import synth
+    from kmamiz_amd.engine import ShapeTable, SpanBatch
+
+    batch, _ = synth.host_batch(3, 0, ntr)
+    t = synth.shape_table(3)
+    n = len(t.dep_ep)
+    rng = np.random.default_rng(5)
+    shape = batch.shape.copy()
+    shape[rng.random(len(shape)) < 1 / 3] += np.uint32(n)
+    two = lambda x: np.concatenate([np.asarray(x, np.uint32)] * 2)  # noqa: E731
+    table = ShapeTable(two(t.rt_ep), two(t.tag_ep), two(t.dep_ep), t.n_rt_ep, t.n_tag_ep, t.n_dep_ep, t.n_status)
+    b2 = SpanBatch(batch.span_id, batch.parent_id, batch.kind, shape, batch.status, batch.duration, batch.timestamp,
+                   batch.index_base)
+    out = []
+    for bits2 in (1 << 4, (1 << 4) | (1 << 11)):
+        os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"] = str(1 << 29), str(bits2)
+        try:
+            e = Engine(0)
+        finally:
+            del os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"]
+        try:
+            info = _compare_synth(e, b2, table)
+            out.append((info, e.triples().copy(), e.endpoints().tobytes()))
+        finally:
+            e.close()
+    (by_shape, k1, p1), (by_ep, k2, p2) = out
+    assert np.array_equal(k1, k2) and p1 == p2
+    assert by_shape["path"] & 32 and by_ep["path"] & 32  # (k4_tile8 both times)
+    assert by_shape["n_chains"] > by_ep["n_chains"] > 0
+
+
+def test_chain_elements_by_endpoint_when_a_shape_is_out_of_range(engine):
+    """A dependency table with an entry past n_dep (a shape no span uses) keeps
+    the walk on endpoint elements (gathered per slot): same results as the
+    C oracle."""
+    from kmamiz_amd import synth
+    from kmamiz_amd.engine import ShapeTable
+
+    batch, _ = synth.host_batch(3, 0, 3000)
+    t = synth.shape_table(3)
+    dep = np.concatenate([np.asarray(t.dep_ep, np.uint32), np.array([t.n_dep_ep + 7], np.uint32)])
+    ext = lambda x: np.concatenate([np.asarray(x, np.uint32), np.zeros(1, np.uint32)])  # noqa: E731
+    table = ShapeTable(ext(t.rt_ep), ext(t.tag_ep), dep, t.n_rt_ep, t.n_tag_ep, t.n_dep_ep, t.n_status)
+    _compare_synth(engine, batch, table)
 
 
 def test_synthetic_shard_base_vs_c_oracle(engine):

@@ -37,14 +37,33 @@ def main():
         for _ in range(3):
             eng.route_ids(world, buf.data_ptr(), n, True)
         route = (time.perf_counter() - t) / 3
+        # fixed segments (IdGuard's steady state: no counts exchange, no sync)
+        seg = int(n / world * 1.125) + 1025
+        fbuf = torch.empty(world * seg, dtype=torch.int64, device="cuda")
+        eng.route_ids_fixed(world, seg, fbuf.data_ptr(), True)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(3):
+            eng.route_ids_fixed(world, seg, fbuf.data_ptr(), True)
+        torch.cuda.synchronize()
+        route_fixed = (time.perf_counter() - t) / 3
+        del fbuf
+        # what an owner receives: ~n values (hash-uniform owners, equal shards)
         assert eng.id_repeats(buf.data_ptr(), n, True) is False
         t = time.perf_counter()
         for _ in range(3):
             eng.id_repeats(buf.data_ptr(), n, True)
         check = (time.perf_counter() - t) / 3
+        # the exchange over xGMI (not timed on one GPU): each rank sends
+        # (world-1)/world of its 8-B hashes, one direct link per peer at
+        # ~153 GB/s (MI355X_MICROARCH.md), all links at once
+        peer_bytes = 8 * n / world
         out["worlds"][world] = {"spans_rank0": n, "step_ms": round(step * 1e3, 3), "route_ms": round(route * 1e3, 3),
+                                "route_fixed_ms": round(route_fixed * 1e3, 3),
                                 "certificate_ms": round(check * 1e3, 3),
-                                "all_to_all_bytes_per_rank": 8 * n}
+                                "all_to_all_bytes_per_rank": int(8 * n * (world - 1) / world),
+                                "all_to_all_ms_projected": round(peer_bytes / 153e9 * 1e3, 3),
+                                "guard_ms_projected": round((route_fixed + check) * 1e3 + peer_bytes / 153e9 * 1e3, 3)}
         del buf
         torch.cuda.empty_cache()
     eng.close()
