@@ -239,6 +239,12 @@ class IdGuard:
             if self.route_dev is not None:  # enqueued on the engine's stream, no wait
                 send = torch.empty(self.world * seg, dtype=torch.int64, device=self.route_dev)
                 self.engine.route_ids_fixed(self.world, seg, send.data_ptr(), True)
+                if self.on_dev and getattr(self.engine, "stream", None) != torch.cuda.current_stream(
+                        self.route_dev).cuda_stream:
+                    # (the exchange is ordered behind torch's stream: an engine
+                    # on a stream of its own is waited for here; the bench's
+                    # engine runs on torch's stream and needs no wait)
+                    self.engine.sync()
             else:
                 send = torch.empty(self.world * seg, dtype=torch.int64)
                 self.engine.route_ids_fixed(self.world, seg, send.data_ptr(), False)
@@ -281,6 +287,8 @@ class IdGuard:
         if self.work is not None:
             self.work.wait()
         if self.pending is not None:  # (gloo, fixed segments: the exchange every rank still posts)
+            if self.route_dev is not None:
+                self.engine.sync()
             send = self.pending.cpu()
             dist.all_to_all_single(torch.empty_like(send), send, group=self.group)
         self.work = self.send = self.recv = self.pending = None
@@ -293,7 +301,9 @@ class IdGuard:
             return self.recv[: self.m], self.maxc, False
         seg = self.fixed
         if self.pending is not None:
-            send = self.pending.cpu()  # (waits for the routing on the engine's stream)
+            if self.route_dev is not None:
+                self.engine.sync()  # (the routing ran on the engine's stream, not torch's)
+            send = self.pending.cpu()
             self.pending = None
             self.recv = torch.empty_like(send)
             dist.all_to_all_single(self.recv, send, group=self.group)

@@ -92,6 +92,7 @@ class Engine:
     def __init__(self, device: int = 0, stream: Optional[int] = None):
         self._lib = L.lib()
         self.ctx = self._lib.kmz_create(device, C.c_void_p(stream) if stream else None)
+        self.stream = stream  # (the hipStream_t handle it launches on; None: its own)
         if not self.ctx:
             raise RuntimeError(f"kmz_create({device}) failed: no HIP device visible (the engine has no CPU path)")
         self.n = 0
