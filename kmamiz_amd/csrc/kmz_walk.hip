@@ -145,12 +145,18 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE8_WAVES) k4_tile8(const uint8_t *
   uint32_t flags = 0;
   uint32_t c[WPW], e[WPW];
   uint8_t k[WPW];
+  // (the window's columns from workgroup-uniform bases, so that every load
+  // takes a 32-bit lane offset: no 64-bit address arithmetic per slot)
+  const uint32_t *__restrict__ cpw = cparent + w0;
+  const uint8_t *__restrict__ kw = kind + w0;
+  const uint32_t *__restrict__ sw = shape + w0;
+  const uint32_t last = n - 1 - w0;
 #pragma unroll
   for (int q = 0; q < WPW; ++q) {  // clamped, unconditional: every load in flight together
-    const uint32_t j = min(w0 + q * WTT + threadIdx.x, n - 1);
-    c[q] = cparent[j];
-    k[q] = kind[j];
-    e[q] = shape[j];
+    const uint32_t j = min((uint32_t)(q * WTT) + threadIdx.x, last);
+    c[q] = cpw[j];
+    k[q] = kw[j];
+    e[q] = sw[j];
   }
 #pragma unroll
   for (int q = 0; q < WPW; ++q) {
@@ -167,8 +173,11 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE8_WAVES) k4_tile8(const uint8_t *
   for (int q = 0; q < WPW; ++q) {
     const uint32_t jl = q * WTT + threadIdx.x;
     if (jl >= wn) continue;
-    const uint32_t cp =
-        c[q] == NONE ? W_NONE : (c[q] == CYC ? W_CYC : ((c[q] >= w0 && c[q] < w1) ? c[q] - w0 : W_OUT));
+    // (branch-free: in-window offset, else W_OUT; NONE and CYC on top)
+    const uint32_t rel = c[q] - w0;
+    uint32_t cp = rel < wn ? rel : (uint32_t)W_OUT;
+    cp = c[q] == NONE ? (uint32_t)W_NONE : cp;
+    cp = c[q] == CYC ? (uint32_t)W_CYC : cp;
     lrec[jl] = make_uint2(e[q], cp | ((uint32_t)(k[q] & 3) << 16));
     other |= (k[q] & 3) != KIND_SERVER && k[q] != KIND_CLIENT;
   }
