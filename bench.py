@@ -196,7 +196,11 @@ def main():
     per_trace = synth.count_spans(config, 0, sample_tr) / sample_tr
     n_traces = max(1, int(round(target / per_trace)))
 
-    stream = torch.cuda.current_stream()
+    # one stream for torch, the collectives and the engine: a stream of its
+    # own (torch's default stream has handle 0, which kmz_create would take
+    # for "create your own" -- a non-blocking stream unordered with torch's)
+    stream = torch.cuda.Stream(device=local)
+    torch.cuda.set_stream(stream)
     eng = Engine(local, stream=stream.cuda_stream)
     if world > 1:  # this rank's traces: shard(traceId) == rank, global flatten indices
         n_local = eng.load_synthetic_shard(config, synth.SEED, 0, n_traces, world, rank)
@@ -205,6 +209,12 @@ def main():
     progress(f"loaded {n_local} spans")
     digest = synth.table_digest(config)  # every rank indexes partials by the same synthetic id tables
     flags = L.RUN_STATS_TAG | L.RUN_DEPS
+    if world > 1:
+        # every step's id guard (IdGuard, below) routes and checks every span
+        # id of every shard, this rank's own included: the run skips its own
+        # uniqueness certificate (a repeat anywhere sends the merge to the
+        # exact unsharded pass)
+        flags |= L.RUN_NO_CERT
     dev = torch.device("cuda", local)
     state = {}
     tail_on = args.tail == "on" or (args.tail == "auto" and config == synth.POWER)

@@ -75,6 +75,14 @@ extern "C" {
 #define KMZ_RUN_DEPS 4u      /* dependency graph (Traces.ts:112-211) */
 #define KMZ_RUN_SPAN_LINKS 8u/* keep per-span links for kmz_get_span_links */
 #define KMZ_RUN_DEP_ORDER 16u /* with DEPS: the entry order of the reduced graph (kmz_get_dep_entries) */
+/* with DEPS: no uniqueness certificate in the run (the window-join path,
+ * whatever the ids).  Only for a caller that checks this batch's span ids for
+ * repeats itself, over a superset of them -- the multi-GPU guard routes every
+ * span id of every shard, its own included, to an owner that checks them
+ * (kmz_route_ids_fixed + kmz_id_repeats_seg_begin): a repeat inside the shard
+ * makes this run's dependency results wrong, and the guard's verdict sends
+ * the merge to the exact unsharded pass (dist.merge_all). */
+#define KMZ_RUN_NO_CERT 32u
 
 /* where a kmz_load buffer lives */
 #define KMZ_MEM_HOST 0
@@ -366,6 +374,18 @@ int kmz_id_repeats(kmz_ctx *ctx, const uint64_t *vals, uint64_t n, int mem, uint
  * so an all-to-all of equal segments can be posted behind it at once
  * (dist.IdGuard; Traces.ts:117-123 is the semantics the check protects). */
 int kmz_route_ids_fixed(kmz_ctx *ctx, uint32_t world, uint64_t seg, uint64_t *out, int mem);
+/* kmz_id_repeats over the fixed segments an all-to-all of
+ * kmz_route_ids_fixed outputs delivered (device memory, `world` segments of
+ * `seg` words as received), without compacting them first, ENQUEUED on
+ * `stream` (a hipStream_t; NULL: the context's stream) -- the stream that
+ * waits for the exchange, so that the check runs beside this rank's own run.
+ * The segments stay untouched until kmz_id_repeats_seg_end, which waits for
+ * it: *max_count = the largest count any source sent (>= seg: a segment
+ * overflowed, *repeated is then 0 and meaningless: exchange exactly), else
+ * *repeated as kmz_id_repeats.  One open check per context; kmz_id_repeats
+ * is refused while it is open. */
+int kmz_id_repeats_seg_begin(kmz_ctx *ctx, const uint64_t *segs, uint32_t world, uint64_t seg, void *stream);
+int kmz_id_repeats_seg_end(kmz_ctx *ctx, uint32_t *repeated, uint64_t *max_count);
 
 /* ---- traceId sharding (shard = h(traceId) mod G) ------------ */
 /* The shard of a trace, from its traceId string (the reference dedups and

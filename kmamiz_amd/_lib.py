@@ -21,6 +21,7 @@ NONE32 = 0xFFFFFFFF
 NONE64 = 0xFFFFFFFFFFFFFFFF
 
 RUN_STATS_RT, RUN_STATS_TAG, RUN_DEPS, RUN_SPAN_LINKS, RUN_DEP_ORDER = 1, 2, 4, 8, 16
+RUN_NO_CERT = 32  # the multi-GPU guard checks the ids (kmz.h KMZ_RUN_NO_CERT)
 MEM_HOST, MEM_DEVICE = 0, 1
 
 ERRORS = {
@@ -185,6 +186,8 @@ SIGNATURES = [
     ("kmz_route_ids_fixed", C.c_int, [_P, C.c_uint32, C.c_uint64, _P, C.c_int]),
     ("kmz_get_graph_stats", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     ("kmz_id_repeats", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.POINTER(C.c_uint32)]),
+    ("kmz_id_repeats_seg_begin", C.c_int, [_P, _P, C.c_uint32, C.c_uint64, _P]),
+    ("kmz_id_repeats_seg_end", C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     ("kmz_trace_shard", C.c_uint32, [C.c_char_p, C.c_uint64, C.c_uint32]),
     ("kmz_set_index_map", C.c_int, [_P, _P, _P, C.c_uint64]),
     ("kmz_get_global_index", C.c_int, [_P, _P, C.c_uint64, C.c_int]),

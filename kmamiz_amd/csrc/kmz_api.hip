@@ -65,6 +65,13 @@ struct kmz_ctx {
   DevBuf gd_out, gd_in, gd_set, gd_cnt;  // sharding guard (kmz_guard.hip)
   DevBuf rt_hist, rt_tot, rt_out, rt_ctr;  // cross-shard repeated-id guard: routing scratch, certificate counters
   DevBuf rt_pool1, rt_dir, rt_pool2, rt_cur;  // ... and its own certificate buffers (the run's stay as the run left them)
+  DevBuf rt_tsz;                               // ... segment tile sizes (kmz_id_repeats_seg_begin)
+  // kmz_id_repeats_seg_begin/_end: the open check's stream, segment size, plan
+  // and pinned read-back (counters, then the largest count)
+  bool rs_open = false;
+  hipStream_t rs_stream = nullptr;
+  uint64_t rs_seg = 0;
+  void *rs_pin = nullptr;
   // device JSON ingest (kmz_json.hip)
   DevBuf j_buf, j_elem, j_state, j_jsc, j_mask, j_cnt, j_off, j_csc, j_small, j_starts, j_slices, j_tslot, j_stab,
       j_ttab, j_reps, j_smap, j_tmap;
@@ -130,6 +137,7 @@ struct kmz_ctx {
   uint32_t dcap = 1024;
   uint32_t scap = 1u << 15;  // K4 staged keys per persistent workgroup (grown when it overflows)
   uint32_t mcap = 1u << 16;   // window-join miss table slots (grown on F_MISS_OVERFLOW)
+  bool no_cert = false;       // KMZ_RUN_NO_CERT: the caller's guard checks the ids (no certificate in the run)
   bool table_hint = false;    // the loaded batch failed the uniqueness certificate: go to the table path
   void *hpin = nullptr;       // pinned host copy of counters + stats64 (one read-back per run)
   bool hpin_valid = false;    // hpin holds the last completed run's values
@@ -142,7 +150,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -364,7 +372,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->rt_tsz, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt,
                     &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->tl_lbkt, &c->tl_lbn, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
@@ -372,11 +380,13 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->o_rts, &c->o_rsh, &c->j_buf, &c->j_elem, &c->j_state, &c->j_jsc, &c->j_mask,
                     &c->j_cnt, &c->j_off, &c->j_csc, &c->j_small, &c->j_starts, &c->j_slices, &c->j_tslot,
                     &c->j_stab, &c->j_ttab, &c->j_reps, &c->j_smap, &c->j_tmap, &c->f_grp, &c->f_trip, &c->f_ep};
+  if (c->rs_open && c->rs_stream) hipStreamSynchronize(c->rs_stream);  // (an open guard check reads its buffers)
   for (DevBuf *b : bufs)
     if (b->p) hipFree(b->p);
   for (auto &g : c->graphs)
     if (g.exec) hipGraphExecDestroy(g.exec);
   if (c->hpin) hipHostFree(c->hpin);
+  if (c->rs_pin) hipHostFree(c->rs_pin);
   if (c->hep) hipHostFree(c->hep);
   if (c->fhep) hipHostFree(c->fhep);
   if (c->xfer) hipStreamDestroy(c->xfer);
@@ -734,10 +744,25 @@ int kmz_json_load(kmz_ctx *c, const uint32_t *shape_of_raw, const uint32_t *stat
 static int run_join(kmz_ctx *c, bool *ok) {
   const uint32_t n = (uint32_t)c->n;
   *ok = false;
+  // The certificate beside the join and the walk only while the chain table
+  // fits the 256 MB MALL: then the walk's probes leave HBM to the certificate
+  // (measured: mesh 5.21 -> 5.12 ms, Bookinfo 0.385 -> 0.323 ms); a chain
+  // table in HBM (config 5, 4 GB) and the certificate slow each other down
+  // (19.3 -> 25.7 ms)
+  const bool cert_side = c->overlap && !(c->ablate & (1u << 26)) && c->ccap * CHAIN_ENTRY_BYTES <= (256ull << 20);
+  // (KMZ_ABLATE2 bit 13, for comparison: the certificate from the start of
+  // the run -- pass 1 by its own kernel, k_cert_bin over the span ids, on the
+  // side stream, none in the join -- so that it runs beside the join too.
+  // Measured slower on config 3: 3.81 against 3.59 ms; the certificate's
+  // workgroups take CUs from the VALU-bound join, while beside the walk,
+  // whose probes wait on the MALL, they fill idle issue slots;
+  // profiles/r05/ab/early/.)
+  const bool early = cert_side && !c->no_cert && (c->ablate2 & 8192u);
   CertPlan pl;
   // (KMZ_ABLATE2 bit 6, test knob: the certificate's 2^8 pass-1 bins at any
-  // size; bit 7: never, for comparison)
-  if (n == 0 || !cert_plan(n, &pl, !(c->ablate2 & 128u), (c->ablate2 & 64u) != 0) || c->table_hint || (c->ablate & 32))
+  // size; bit 7: never, for comparison.  k_cert_bin bins by 2^6.)
+  if (n == 0 || !cert_plan(n, &pl, !early && !(c->ablate2 & 128u), !early && (c->ablate2 & 64u) != 0) ||
+      c->table_hint || (c->ablate & 32))
     return KMZ_OK;
   if (ensure(c, c->dp, (size_t)(n + 1) * 4) || ensure(c, c->cpool1, cert_pool1_words(n) * 8) ||
       ensure(c, c->cpool2, cert_pool2_bytes(pl)) || ensure(c, c->ccur, cert_cur_words(pl) * 4) ||
@@ -746,39 +771,60 @@ static int run_join(kmz_ctx *c, bool *ok) {
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
   if (ensure(c, c->mkey, (size_t)c->mcap * 8) || ensure(c, c->mval, (size_t)c->mcap * 4)) return KMZ_E_HIP;
+  if (early) {  // (behind the side stream's K3: the main stream waits for that one near the end)
+    c->stream = c->side;
+    {
+      Timed t(c, KMZ_K_MEMSET);
+      FillArgs f;
+      f.add(cur2, cert_cur_words(pl) * 4, 0);
+      launch_fill(c->stream, f);
+    }
+    {
+      Timed t(c, KMZ_K_CERT);
+      launch_cert_bin(c->stream, reinterpret_cast<const unsigned long long *>(c->sid), n,
+                      P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir));
+      launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
+                        P<unsigned long long>(c->cpool2), cur2, cnt);
+    }
+    {
+      Timed t(c, KMZ_K_CHECK);
+      launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
+    }
+    c->stream = c->main;
+  }
   {
     Timed t(c, KMZ_K_MEMSET);
     FillArgs f;
-    f.add(cur2, cert_cur_words(pl) * 4, 0);
+    if (!early) f.add(cur2, cert_cur_words(pl) * 4, 0);
     f.add(c->mkey.p, (size_t)c->mcap * 8, 0);
     f.add(c->mval.p, (size_t)c->mcap * 4, 0xFF);  // ids not in the batch: NONE
     launch_fill(c->stream, f);
   }
   {
     Timed t(c, KMZ_K_JOIN);
+    // (no pass 1 in the join -- bit 6 of its knobs -- when the certificate
+    // bins on its own or KMZ_RUN_NO_CERT leaves it to the caller)
     launch_join(c->stream, c->sid, c->pid, c->kind, n, P<uint32_t>(c->cparent), P<uint32_t>(c->dp),
-                P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, pl, c->ablate);
+                P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, pl,
+                c->ablate | (c->no_cert || early ? 64u : 0u));
   }
-  // ... only while the chain table fits the 256 MB MALL: then the walk's
-  // probes leave HBM to the certificate (measured: mesh 5.21 -> 5.12 ms,
-  // Bookinfo 0.385 -> 0.323 ms); a chain table in HBM (config 5, 4 GB) and
-  // the certificate slow each other down (19.3 -> 25.7 ms)
-  const bool cert_side = c->overlap && !(c->ablate & (1u << 26)) && c->ccap * CHAIN_ENTRY_BYTES <= (256ull << 20);
-  if (cert_side) {  // the certificate checks the join's ids beside the chain walk (read after the run)
-    HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
-    c->stream = c->side;
+  if (!early && !c->no_cert) {
+    if (cert_side) {  // the certificate checks the join's ids beside the chain walk (read after the run)
+      HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
+      c->stream = c->side;
+    }
+    {
+      Timed t(c, KMZ_K_CERT);
+      launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
+                        P<unsigned long long>(c->cpool2), cur2, cnt);
+    }
+    {
+      Timed t(c, KMZ_K_CHECK);
+      launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
+    }
+    c->stream = c->main;
   }
-  {
-    Timed t(c, KMZ_K_CERT);
-    launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
-                      P<unsigned long long>(c->cpool2), cur2, cnt);
-  }
-  {
-    Timed t(c, KMZ_K_CHECK);
-    launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
-  }
-  c->stream = c->main;
   {
     // parents outside the window / chains leaving it: these kernels read the
     // join's counters and return at once when there is nothing to do, so the
@@ -1009,19 +1055,21 @@ static int run_fused(kmz_ctx *c, bool links) {
   }
   // the certificate beside the settle (small batches), as run_join
   const bool cert_side = c->overlap && !(c->ablate & (1u << 26)) && c->ccap * CHAIN_ENTRY_BYTES <= (256ull << 20);
-  if (cert_side) {
+  if (cert_side && !c->no_cert) {
     HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
     c->stream = c->side;
   }
-  {
-    Timed t(c, KMZ_K_CERT);
-    launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
-                      P<unsigned long long>(c->cpool2), cur2, cnt);
-  }
-  {
-    Timed t(c, KMZ_K_CHECK);
-    launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
+  if (!c->no_cert) {  // (KMZ_RUN_NO_CERT: the fused kernel's pass 1 still runs, unread)
+    {
+      Timed t(c, KMZ_K_CERT);
+      launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
+                        P<unsigned long long>(c->cpool2), cur2, cnt);
+    }
+    {
+      Timed t(c, KMZ_K_CHECK);
+      launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
+    }
   }
   c->stream = c->main;
   {
@@ -1666,6 +1714,7 @@ int kmz_run_begin(kmz_ctx *c, uint32_t flags) {
   unsigned int *h = reinterpret_cast<unsigned int *>(c->hpin);
   unsigned long long *s64 = reinterpret_cast<unsigned long long *>(h + C_COUNT);
   c->k4_now = (flags & KMZ_RUN_DEPS) ? k4_direct(c) : false;
+  c->no_cert = (flags & KMZ_RUN_NO_CERT) != 0;
   if (int r = run_attempt(c, flags, links, h, s64)) return r;
   c->run_open = true;
   c->run_flags = flags;
@@ -2500,8 +2549,12 @@ int kmz_route_ids_fixed(kmz_ctx *c, uint32_t world, uint64_t seg, uint64_t *out,
     if (ensure(c, c->rt_out, words * 8)) return KMZ_E_HIP;
     dst = P<unsigned long long>(c->rt_out);
   }
-  if (!launch_route(c->stream, c->sid, n, world, P<uint32_t>(c->rt_hist), P<unsigned long long>(c->rt_tot), dst, seg))
-    return fail(c, KMZ_E_ARG, "world must be 1..1024");
+  // (KMZ_ABLATE2 bit 12, for comparison: the histogram / scan / scatter form)
+  const bool ok = (c->ablate2 & 4096u)
+                      ? launch_route(c->stream, c->sid, n, world, P<uint32_t>(c->rt_hist),
+                                     P<unsigned long long>(c->rt_tot), dst, seg)
+                      : launch_route_fixed(c->stream, c->sid, n, world, seg, P<unsigned long long>(c->rt_tot), dst);
+  if (!ok) return fail(c, KMZ_E_ARG, "world must be 1..1024");
   HIPCHK(c, hipGetLastError());
   if (mem != KMZ_MEM_DEVICE) {  // (host memory: copied back; device memory: enqueued only)
     HIPCHK(c, hipMemcpyAsync(out, dst, words * 8, hipMemcpyDeviceToHost, c->stream));
@@ -2513,6 +2566,7 @@ int kmz_route_ids_fixed(kmz_ctx *c, uint32_t world, uint64_t seg, uint64_t *out,
 int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32_t *repeated) {
   if (!c || !repeated || (n && !vals)) return KMZ_E_ARG;
   if (c->run_open) return run_busy(c);
+  if (c->rs_open) return fail(c, KMZ_E_STATE, "kmz_id_repeats while kmz_id_repeats_seg_begin is open");
   *repeated = 0;
   if (n < 2) return KMZ_OK;
   CertPlan pl;
@@ -2544,6 +2598,67 @@ int kmz_id_repeats(kmz_ctx *c, const uint64_t *vals, uint64_t n, int mem, uint32
   unsigned int h[C_COUNT];
   HIPCHK(c, hipMemcpyAsync(h, cnt, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (h[C_CERT] & CERT_DUP) {
+    *repeated = 1;
+    return KMZ_OK;
+  }
+  if (h[C_CERT] & CERT_OVF) return fail(c, KMZ_E_UNSUPPORTED, "certificate overflow: check on the host");
+  return KMZ_OK;
+}
+
+// The guard's certificate straight over the fixed segments an all-to-all
+// delivered (IdGuard): no compaction of the segments first, and enqueued only,
+// on the caller's stream (the one that waits for the exchange), so that it
+// runs beside the rank's own run; kmz_id_repeats_seg_end waits for it.
+int kmz_id_repeats_seg_begin(kmz_ctx *c, const uint64_t *segs, uint32_t world, uint64_t seg, void *stream) {
+  if (!c || !segs || world == 0 || seg < 2) return KMZ_E_ARG;
+  if (c->rs_open) return fail(c, KMZ_E_STATE, "kmz_id_repeats_seg_begin while one is open");
+  hipSetDevice(c->device);
+  const uint64_t jt = cert_pool1_words(1);  // (values per pass-1 tile)
+  const uint64_t tps = (seg - 1 + jt - 1) / jt, tiles = tps * world;
+  CertPlan pl;
+  if (tiles * jt >= 0xFFFFFFFFull || !cert_plan((uint32_t)(tiles * jt), &pl, false))
+    return fail(c, KMZ_E_UNSUPPORTED, "too many values for the certificate: check on the host");
+  const uint32_t m = (uint32_t)(tiles * jt);  // (an upper bound: the plan's pools are sized for it)
+  if (ensure(c, c->rt_pool1, cert_pool1_words(m) * 8) || ensure(c, c->rt_dir, cert_dir_entries(m, pl) * 2) ||
+      ensure(c, c->rt_pool2, cert_pool2_bytes(pl)) || ensure(c, c->rt_cur, cert_cur_words(pl) * 4) ||
+      ensure(c, c->rt_ctr, C_COUNT * 4 + 8) || ensure(c, c->rt_tsz, tiles * 2))
+    return KMZ_E_HIP;
+  if (!c->rs_pin && hipHostMalloc(&c->rs_pin, C_COUNT * 4 + 8, hipHostMallocDefault) != hipSuccess) {
+    c->rs_pin = nullptr;
+    return fail(c, KMZ_E_HIP, "hipHostMalloc (guard read-back)");
+  }
+  hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+  unsigned int *cnt = P<unsigned int>(c->rt_ctr);
+  unsigned long long *maxc = reinterpret_cast<unsigned long long *>(cnt + C_COUNT);
+  static_assert(C_COUNT * 4 % 8 == 0, "the largest count follows the counters");
+  unsigned int *cur2 = P<unsigned int>(c->rt_cur);
+  HIPCHK(c, hipMemsetAsync(cnt, 0, C_COUNT * 4 + 8, s));
+  HIPCHK(c, hipMemsetAsync(cur2, 0, cert_cur_words(pl) * 4, s));
+  const unsigned long long *src = reinterpret_cast<const unsigned long long *>(segs);
+  launch_cert_bin_seg(s, src, world, seg, (uint32_t)tps, P<unsigned long long>(c->rt_pool1), P<uint16_t>(c->rt_dir),
+                      P<uint16_t>(c->rt_tsz), maxc);
+  launch_cert_split(s, m, P<unsigned long long>(c->rt_pool1), P<uint16_t>(c->rt_dir), pl,
+                    P<unsigned long long>(c->rt_pool2), cur2, cnt, P<uint16_t>(c->rt_tsz));
+  launch_cert_check(s, m, pl, P<unsigned long long>(c->rt_pool2), cur2, cnt);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->rs_pin, cnt, C_COUNT * 4 + 8, hipMemcpyDeviceToHost, s));
+  c->rs_stream = s;
+  c->rs_seg = seg;
+  c->rs_open = true;
+  return KMZ_OK;
+}
+
+int kmz_id_repeats_seg_end(kmz_ctx *c, uint32_t *repeated, uint64_t *max_count) {
+  if (!c || !repeated || !max_count) return KMZ_E_ARG;
+  if (!c->rs_open) return fail(c, KMZ_E_STATE, "kmz_id_repeats_seg_end without kmz_id_repeats_seg_begin");
+  c->rs_open = false;
+  HIPCHK(c, hipStreamSynchronize(c->rs_stream));
+  const unsigned int *h = reinterpret_cast<const unsigned int *>(c->rs_pin);
+  const uint64_t mc = *reinterpret_cast<const unsigned long long *>(h + C_COUNT);
+  *max_count = mc;
+  *repeated = 0;
+  if (mc >= c->rs_seg) return KMZ_OK;  // a segment overflowed: the caller redoes the exchange exactly
   if (h[C_CERT] & CERT_DUP) {
     *repeated = 1;
     return KMZ_OK;

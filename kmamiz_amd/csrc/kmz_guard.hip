@@ -139,6 +139,62 @@ __global__ void __launch_bounds__(RT_T) k_route_scatter(const uint64_t *__restri
   }
 }
 
+// Fixed segments in one pass (kmz_route_ids_fixed): each workgroup holds its
+// 4096 hashes in registers, ranks them per owner with LDS atomics, reserves
+// each owner's run in that owner's segment with one device atomic, and writes
+// them; a last tiny kernel stores the counts into the segments' word 0.  8 B
+// read + 8 B written per id (the hist/scan/scatter form reads the ids twice).
+constexpr uint32_t RF_PT = 16, RF_CH = RT_T * RF_PT;
+
+__global__ void __launch_bounds__(RT_T) k_route_fixed(const uint64_t *__restrict__ sid, uint32_t n, uint32_t world,
+                                                      uint64_t segw, unsigned long long *__restrict__ cur,
+                                                      unsigned long long *__restrict__ out) {
+  __shared__ uint32_t h[RT_MAXW];
+  __shared__ unsigned long long base[RT_MAXW];
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T) h[r] = 0;
+  const uint32_t b = blockIdx.x * RF_CH;
+  uint64_t v[RF_PT];
+#pragma unroll
+  for (int q = 0; q < (int)RF_PT; ++q) {  // every load in flight before the first hash
+    const uint32_t i = b + q * RT_T + threadIdx.x;
+    v[q] = i < n ? sid[i] : 0;
+  }
+  __syncthreads();
+  uint32_t ow[RF_PT], rk[RF_PT];
+#pragma unroll
+  for (int q = 0; q < (int)RF_PT; ++q) {
+    const uint32_t i = b + q * RT_T + threadIdx.x;
+    v[q] = id_hash(v[q]);
+    ow[q] = id_owner(v[q], world);
+    rk[q] = i < n ? atomicAdd(&h[ow[q]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T)
+    if (h[r]) base[r] = atomicAdd(&cur[r], (unsigned long long)h[r]);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < (int)RF_PT; ++q) {
+    const uint32_t i = b + q * RT_T + threadIdx.x;
+    const unsigned long long x = base[ow[q]] + rk[q];
+    if (i < n && x + 1 < segw) out[(uint64_t)ow[q] * segw + 1 + x] = v[q];  // (full: its count says so)
+  }
+}
+
+__global__ void __launch_bounds__(RT_T) k_route_counts(uint32_t world, uint64_t segw,
+                                                       const unsigned long long *__restrict__ cur,
+                                                       unsigned long long *__restrict__ out) {
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T) out[(uint64_t)r * segw] = cur[r];
+}
+
+bool launch_route_fixed(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint64_t segw,
+                        unsigned long long *cur, unsigned long long *out) {
+  if (world == 0 || world > RT_MAXW || segw < 2) return false;
+  hipMemsetAsync(cur, 0, (size_t)world * 8, s);
+  if (n) hipLaunchKernelGGL(k_route_fixed, dim3((n + RF_CH - 1) / RF_CH), dim3(RT_T), 0, s, sid, n, world, segw, cur, out);
+  hipLaunchKernelGGL(k_route_counts, dim3(1), dim3(RT_T), 0, s, world, segw, cur, out);
+  return true;
+}
+
 uint32_t route_chunks(uint32_t n) { return std::max<uint32_t>(1, std::min<uint32_t>(1024, (n + 4095) / 4096)); }
 
 bool launch_route(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint32_t *hist,

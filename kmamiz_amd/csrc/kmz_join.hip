@@ -344,18 +344,19 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
 // still a bijection): the routing fixed the top bits of the values a rank
 // receives, and the bins need them uniform.  Same tile-major layout as
 // k_join_window's pass 1 (pool1, jdir).
-__global__ void __launch_bounds__(JTT) k_cert_bin(const unsigned long long *__restrict__ v, uint32_t n,
-                                                  unsigned long long *__restrict__ pool1, uint16_t *__restrict__ jdir) {
+// One tile of pass 1: cnt (<= JT) values from v into pool1 tile `tile`, its
+// bin starts into jdir.
+__device__ __forceinline__ void cert_bin_tile(const unsigned long long *__restrict__ v, uint32_t cnt, uint32_t tile,
+                                              unsigned long long *__restrict__ pool1, uint16_t *__restrict__ jdir) {
   constexpr uint32_t NW = JTT / 64, PT = JT / JTT;
   __shared__ uint64_t stg[JT];
   __shared__ uint32_t wcnt[CERT_BINS * NW], wsum[NW];
-  const uint32_t t0 = blockIdx.x * JT, t1 = min(n, t0 + JT);
   for (uint32_t e = threadIdx.x; e < CERT_BINS * NW; e += JTT) wcnt[e] = 0;
   uint64_t hv[PT];
 #pragma unroll
   for (int q = 0; q < (int)PT; ++q) {
-    const uint32_t i = t0 + q * JTT + threadIdx.x;
-    hv[q] = i < t1 ? cert_hash(v[i]) : 0;
+    const uint32_t i = q * JTT + threadIdx.x;
+    hv[q] = i < cnt ? cert_hash(v[i]) : 0;
   }
   __syncthreads();
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -363,7 +364,7 @@ __global__ void __launch_bounds__(JTT) k_cert_bin(const unsigned long long *__re
   uint32_t rk[PT];
 #pragma unroll
   for (int q = 0; q < (int)PT; ++q) {
-    const bool ok = t0 + q * JTT + threadIdx.x < t1;
+    const bool ok = q * JTT + threadIdx.x < cnt;
     const uint32_t bin = (uint32_t)(hv[q] >> (64 - CERT_B1));
     const uint64_t peers = match6(bin, __ballot(ok));
     uint32_t prior = 0;
@@ -373,18 +374,49 @@ __global__ void __launch_bounds__(JTT) k_cert_bin(const unsigned long long *__re
   }
   __syncthreads();
   block_scan_lds(wcnt, CERT_BINS * NW, wsum);
-  if (threadIdx.x < CERT_BINS) jdir[(uint64_t)blockIdx.x * CERT_BINS + threadIdx.x] = (uint16_t)wcnt[threadIdx.x * NW];
+  if (threadIdx.x < CERT_BINS) jdir[(uint64_t)tile * CERT_BINS + threadIdx.x] = (uint16_t)wcnt[threadIdx.x * NW];
 #pragma unroll
   for (int q = 0; q < (int)PT; ++q)
-    if (t0 + q * JTT + threadIdx.x < t1) stg[wcnt[(uint32_t)(hv[q] >> (64 - CERT_B1)) * NW + w] + rk[q]] = hv[q];
+    if (q * JTT + threadIdx.x < cnt) stg[wcnt[(uint32_t)(hv[q] >> (64 - CERT_B1)) * NW + w] + rk[q]] = hv[q];
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) pool1[(uint64_t)t0 + e] = stg[e];
+  for (uint32_t e = threadIdx.x; e < cnt; e += JTT) pool1[(uint64_t)tile * JT + e] = stg[e];
+}
+
+__global__ void __launch_bounds__(JTT) k_cert_bin(const unsigned long long *__restrict__ v, uint32_t n,
+                                                  unsigned long long *__restrict__ pool1, uint16_t *__restrict__ jdir) {
+  const uint32_t t0 = blockIdx.x * JT;
+  cert_bin_tile(v + t0, min(n - t0, JT), blockIdx.x, pool1, jdir);
+}
+
+// The same over the guard's fixed segments as received (kmz_id_repeats_seg):
+// segment r = [count, values...] of segw words; tps tiles per segment, tile
+// sizes (a segment's last tiles short or empty) into tsz for the split.  The
+// largest count any source sent (the next segment size; >= segw: it
+// overflowed) into *maxc.
+__global__ void __launch_bounds__(JTT) k_cert_bin_seg(const unsigned long long *__restrict__ segs, uint32_t world,
+                                                      uint64_t segw, uint32_t tps,
+                                                      unsigned long long *__restrict__ pool1,
+                                                      uint16_t *__restrict__ jdir, uint16_t *__restrict__ tsz,
+                                                      unsigned long long *__restrict__ maxc) {
+  const uint32_t r = blockIdx.x / tps, lt = blockIdx.x % tps;
+  const unsigned long long c = segs[(uint64_t)r * segw];
+  const uint64_t have = c < segw - 1 ? c : segw - 1, b0 = (uint64_t)lt * JT;
+  const uint32_t cnt = have > b0 ? (uint32_t)min<uint64_t>(JT, have - b0) : 0u;
+  if (lt == 0 && threadIdx.x == 0) atomicMax(maxc, c);
+  if (threadIdx.x == 0) tsz[blockIdx.x] = (uint16_t)cnt;
+  cert_bin_tile(segs + (uint64_t)r * segw + 1 + b0, cnt, blockIdx.x, pool1, jdir);
 }
 
 void launch_cert_bin(hipStream_t s, const unsigned long long *v, uint32_t n, unsigned long long *pool1,
                      uint16_t *jdir) {
   if (!n) return;
   hipLaunchKernelGGL(k_cert_bin, dim3(join_tiles(n)), dim3(JTT), 0, s, v, n, pool1, jdir);
+}
+
+void launch_cert_bin_seg(hipStream_t s, const unsigned long long *segs, uint32_t world, uint64_t segw, uint32_t tps,
+                         unsigned long long *pool1, uint16_t *jdir, uint16_t *tsz, unsigned long long *maxc) {
+  hipLaunchKernelGGL(k_cert_bin_seg, dim3(world * tps), dim3(JTT), 0, s, segs, world, segw, tps, pool1, jdir, tsz,
+                     maxc);
 }
 
 // pass 2: for one bin, the runs of TPC tiles -> 2^B2 sub-bins (dynamic LDS:
@@ -400,7 +432,8 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
                                                      const uint16_t *__restrict__ jdir, uint32_t n, uint32_t chunks,
                                                      uint32_t B2, unsigned long long *__restrict__ pool2,
                                                      uint32_t cap2, unsigned int *__restrict__ cur2,
-                                                     unsigned int *__restrict__ counters) {
+                                                     unsigned int *__restrict__ counters,
+                                                     const uint16_t *__restrict__ tsz) {
   constexpr uint32_t BINS = 1u << B1;
   // ~32 ids per tile run at 64 bins, ~8 at 256
   constexpr uint32_t CERT_CHUNK = PQ * 1024, CERT_TPC = (PQ * 24) << (B1 - CERT_B1);
@@ -422,7 +455,7 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
     uint32_t o = 0;
     if (threadIdx.x < nt) {
       const uint32_t t = T0 + threadIdx.x;
-      const uint32_t tsize = min(JT, n - t * JT);
+      const uint32_t tsize = tsz ? tsz[t] : min(JT, n - t * JT);  // (tsz: the guard's segment tiles)
       o = jdir[(uint64_t)t * BINS + b];
       const uint32_t e = b + 1 < BINS ? jdir[(uint64_t)t * BINS + b + 1] : tsize;
       c = e - o;
@@ -836,15 +869,16 @@ void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const 
 }
 
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
-                       const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters) {
+                       const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters,
+                       const uint16_t *tsz) {
   if (!n) return;
   const size_t lds = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B2) * 4;
   if (pl.B1 == CERT_B1W)
     hipLaunchKernelGGL((k_cert_split<CERT_PQ, CERT_B1W>), dim3((1u << CERT_B1W) * pl.chunks), dim3(1024), lds, s, pool1,
-                       jdir, n, pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
+                       jdir, n, pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters, tsz);
   else
     hipLaunchKernelGGL((k_cert_split<CERT_PQ, CERT_B1>), dim3(CERT_BINS * pl.chunks), dim3(1024), lds, s, pool1, jdir, n,
-                       pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters);
+                       pl.chunks, pl.B2, pool2, pl.cap2, cur2, counters, tsz);
   if (pl.B3) {  // level 3: after level 2 in the same pool and counter block
     const uint32_t n2 = 1u << (pl.B1 + pl.B2);
     const size_t lds3 = CERT_PQ * 1024 * 8 + (size_t)2 * (1u << pl.B3) * 4;

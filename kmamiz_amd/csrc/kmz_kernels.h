@@ -243,6 +243,10 @@ void launch_unresolved(hipStream_t s, const uint64_t *pid, const uint32_t *dp, u
 uint32_t route_chunks(uint32_t n);
 bool launch_route(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint32_t *hist,
                   unsigned long long *tot, unsigned long long *out, uint64_t segw = 0);
+// ... into fixed segments of segw words in one pass over the ids (no
+// histogram pass): cur [world] u64 scratch (zeroed here)
+bool launch_route_fixed(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint64_t segw,
+                        unsigned long long *cur, unsigned long long *out);
 void launch_ids_count(hipStream_t s, const unsigned long long *ids, uint64_t m, unsigned long long *set, uint64_t cap,
                       const uint64_t *sid, uint32_t n, unsigned long long *found);
 
@@ -277,13 +281,19 @@ __host__ __device__ uint32_t join_tiles(uint32_t n);
 void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
                  uint32_t *cparent, uint32_t *dp, unsigned long long *pool1, uint16_t *jdir, unsigned int *counters,
                  const CertPlan &pl, uint32_t ablate = 0);
+// tsz: per-tile sizes (the guard's segment tiles, launch_cert_bin_seg); null: dense tiles of n values
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
-                       const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters);
+                       const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters,
+                       const uint16_t *tsz = nullptr);
 void launch_cert_check(hipStream_t s, uint32_t n, const CertPlan &pl, const unsigned long long *pool2,
                        const unsigned int *cur2, unsigned int *counters);
 // pass 1 of the certificate over a plain value array (cross-shard id guard)
 void launch_cert_bin(hipStream_t s, const unsigned long long *v, uint32_t n, unsigned long long *pool1,
                      uint16_t *jdir);
+// ... over fixed segments as received (count word, values): tps tiles per
+// segment, their sizes into tsz, the largest count into *maxc (atomicMax)
+void launch_cert_bin_seg(hipStream_t s, const unsigned long long *segs, uint32_t world, uint64_t segw, uint32_t tps,
+                         unsigned long long *pool1, uint16_t *jdir, uint16_t *tsz, unsigned long long *maxc);
 void launch_miss(hipStream_t s, const uint64_t *sid, const uint64_t *pid, uint32_t *dp, uint32_t n,
                  unsigned long long *mkey, uint32_t *mval, uint32_t mcap, const unsigned int *counters);
 void launch_pend(hipStream_t s, const uint8_t *kind, const uint32_t *dp, uint32_t n, uint32_t *cparent,

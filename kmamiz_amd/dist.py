@@ -34,6 +34,14 @@ _BIAS = -(1 << 63)  # flips the sign bit: u64 order <-> i64 order
 _I64_MAX = (1 << 63) - 1
 
 
+def _engine_reads(engine, t: torch.Tensor) -> None:
+    """Before the engine reads a device tensor that torch (or a collective on
+    torch's stream) produced: wait for torch's stream unless the engine
+    launches on that same stream."""
+    if t.is_cuda and getattr(engine, "stream", None) != torch.cuda.current_stream(t.device).cuda_stream:
+        torch.cuda.current_stream(t.device).synchronize()
+
+
 def _as_signed_order(x: torch.Tensor) -> torch.Tensor:
     return torch.bitwise_xor(x, torch.tensor(_BIAS, dtype=torch.int64, device=x.device))
 
@@ -165,6 +173,7 @@ def merge_all(p: torch.Tensor, n_groups: int, e: torch.Tensor, n_ep: int, keys: 
     e[E : 2 * E] = torch.where(fe == _I64_MAX, torch.full_like(fe, -1), fe)
     allk = _gather_padded(keys, nk, world, group)
     if engine is not None:
+        _engine_reads(engine, allk)
         engine.merge_triples(allk.data_ptr(), allk.numel(), keys.is_cuda)
         return None
     u = torch.unique(allk)
@@ -198,6 +207,16 @@ def route_ids_np(span_ids: np.ndarray, world: int):
 # agreed fixed-segment size of IdGuard's exchange per (group, world): set on
 # every rank from the same all-reduced maximum in IdGuard.finish
 _ID_SEG: dict = {}
+# per device: the stream IdGuard's certificate runs on (it waits for the
+# exchange there, beside the rank's own run)
+_GUARD_STREAMS: dict = {}
+
+
+def _guard_stream(dev: torch.device):
+    s = _GUARD_STREAMS.get(dev.index)
+    if s is None:
+        s = _GUARD_STREAMS[dev.index] = torch.cuda.Stream(dev)
+    return s
 
 
 class IdGuard:
@@ -213,9 +232,18 @@ class IdGuard:
     routing; under gloo, CPU-only, the copy and the exchange wait for
     finish()).  The first call, and any step whose segment overflowed on some
     rank, use the exact protocol: the counts all-to-all, then the values with
-    those split sizes.  ``finish()`` runs the uniqueness certificate over what
-    this rank received (kmz_id_repeats) and agrees on the verdict and the next
-    segment size in one MAX all-reduce, raising ShardingError on a repeat."""
+    those split sizes.  Under RCCL with fixed segments start() also enqueues
+    the uniqueness certificate over the segments as they arrive
+    (kmz_id_repeats_seg_begin) on a stream of its own that waits for the
+    exchange, so the check runs beside this rank's run too; ``finish()`` waits
+    for its verdict (elsewhere it runs the certificate over what this rank
+    received: kmz_id_repeats_seg_* or kmz_id_repeats) and agrees on the
+    verdict and the next segment size in one MAX all-reduce, raising
+    ShardingError on a repeat.
+
+    Every span id of every shard, the owner's own included, is routed and
+    checked, so a repeat inside one shard is found too: a run covered by a
+    guard may skip its own certificate (KMZ_RUN_NO_CERT)."""
 
     def __init__(self, engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None):
         self.engine, self.group, self.span_ids = engine, group, span_ids
@@ -229,6 +257,7 @@ class IdGuard:
                           and torch.device(dev).type == "cuda" else None)
         self.key = (id(group) if group is not None else None, self.world)
         self.work = self.fixed = self.pending = None
+        self.seg_open = False  # kmz_id_repeats_seg_begin enqueued, not yet ended
 
     def start(self) -> "IdGuard":
         if self.world == 1:
@@ -252,6 +281,15 @@ class IdGuard:
                 self.recv = torch.empty_like(send)
                 self.send = send
                 self.work = dist.all_to_all_single(self.recv, send, group=self.group, async_op=True)
+                # the certificate over the segments as they arrive, on the
+                # guard's stream behind the exchange (no host wait): it runs
+                # beside this rank's run, finish() reads its verdict
+                gs = _guard_stream(self.route_dev)
+                with torch.cuda.stream(gs):
+                    self.work.wait()
+                self.recv.record_stream(gs)
+                self.engine.id_repeats_seg_begin(self.recv.data_ptr(), self.world, seg, gs.cuda_stream)
+                self.seg_open = True
             else:
                 self.pending = send  # (gloo: copied and exchanged in finish)
             return self
@@ -284,6 +322,9 @@ class IdGuard:
     def abandon(self) -> None:
         """Wait for a posted exchange without checking it (every rank calls
         this when the merge is refused before the guard's verdict)."""
+        if self.seg_open:  # (its certificate reads the received segments: wait for it)
+            self.seg_open = False
+            self.engine.id_repeats_seg_end()
         if self.work is not None:
             self.work.wait()
         if self.pending is not None:  # (gloo, fixed segments: the exchange every rank still posts)
@@ -317,22 +358,50 @@ class IdGuard:
         keep = torch.arange(seg - 1, device=r.device)[None, :] < cnt[:, None]
         return r[:, 1:][keep], maxc, False
 
+    def _seg_verdict(self):
+        """Fixed segments, engine on a GPU: the certificate over the segments
+        as received (kmz_id_repeats_seg_*; under gloo the exchange runs here on
+        the host and the segments go to the device first).  -> (repeated, the
+        largest count any source sent, whether a segment overflowed)."""
+        seg = self.fixed
+        if not self.seg_open:
+            self.engine.sync()  # (the routing ran on the engine's stream)
+            send = self.pending.cpu()
+            self.pending = None
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=self.group)
+            self.recv = recv.to(self.route_dev)
+            self.engine.id_repeats_seg_begin(self.recv.data_ptr(), self.world, seg,
+                                             torch.cuda.current_stream(self.route_dev).cuda_stream)
+        self.seg_open = False
+        rep, maxc = self.engine.id_repeats_seg_end()
+        over = maxc >= seg
+        if rep is None and not over:  # the certificate could not decide: compact and check on the host
+            r = self.recv.view(self.world, seg)
+            keep = torch.arange(seg - 1, device=r.device)[None, :] < r[:, :1]
+            v = r[:, 1:][keep]
+            rep = bool(v.numel()) and torch.unique(v).numel() != v.numel()
+        return rep, maxc, over
+
     def finish(self, raise_: bool = True) -> bool:
         """-> True when some span id is in two shards (ShardingError instead
         with ``raise_``)."""
         if self.world == 1:
             return False
-        if self.work is None and self.pending is None:
+        if self.work is None and self.pending is None and not self.seg_open:
             self.start()
-        recv, maxc, over = self._received()
-        rep = None
-        if not over:
-            if self.on_dev:
-                torch.cuda.current_stream(self.dev).synchronize()  # (the engine's stream may not be torch's)
-            if self.engine is not None and recv.numel():
-                rep = self.engine.id_repeats(recv.data_ptr(), recv.numel(), self.on_dev)
-            if rep is None:  # host check (no engine, or the certificate could not decide)
-                rep = bool(recv.numel()) and torch.unique(recv).numel() != recv.numel()
+        if self.fixed is not None and self.engine is not None and self.route_dev is not None:
+            rep, maxc, over = self._seg_verdict()
+        else:
+            recv, maxc, over = self._received()
+            rep = None
+            if not over:
+                if self.on_dev:
+                    torch.cuda.current_stream(self.dev).synchronize()  # (the engine's stream may not be torch's)
+                if self.engine is not None and recv.numel():
+                    rep = self.engine.id_repeats(recv.data_ptr(), recv.numel(), self.on_dev)
+                if rep is None:  # host check (no engine, or the certificate could not decide)
+                    rep = bool(recv.numel()) and torch.unique(recv).numel() != recv.numel()
         # one MAX all-reduce: the verdict, any overflow, the largest count (the
         # next step's segment size, the same on every rank)
         flag = torch.tensor([1 if rep else 0, 1 if over else 0, maxc], dtype=torch.int64, device=self.dev)
@@ -404,6 +473,7 @@ def _check_shards(engine, nu: int, mu: int, dev, group=None, raise_: bool = True
     if nu:
         engine.unresolved_parents(mine.data_ptr(), mu, mine.is_cuda)
     allu = _gather_padded(mine, mu, dist.get_world_size(group), group)
+    _engine_reads(engine, allu)
     found = torch.tensor([engine.count_ids(allu.data_ptr(), allu.numel(), allu.is_cuda)], dtype=torch.int64,
                          device=dev)
     dist.all_reduce(found, op=dist.ReduceOp.SUM, group=group)

@@ -92,7 +92,9 @@ class Engine:
     def __init__(self, device: int = 0, stream: Optional[int] = None):
         self._lib = L.lib()
         self.ctx = self._lib.kmz_create(device, C.c_void_p(stream) if stream else None)
-        self.stream = stream  # (the hipStream_t handle it launches on; None: its own)
+        # (the hipStream_t handle it launches on; None: its own -- a handle of 0,
+        # torch's default stream, also means its own, unordered with torch's)
+        self.stream = stream if stream else None
         if not self.ctx:
             raise RuntimeError(f"kmz_create({device}) failed: no HIP device visible (the engine has no CPU path)")
         self.n = 0
@@ -467,6 +469,24 @@ class Engine:
             return None
         L.check(self.ctx, rc)
         return bool(r.value)
+
+    def id_repeats_seg_begin(self, segs_ptr: int, world: int, seg: int, stream: int = 0) -> None:
+        """kmz_id_repeats_seg_begin: the certificate over ``world`` received
+        fixed segments of ``seg`` words (device memory), enqueued on
+        ``stream`` (a hipStream_t handle; 0: the engine's stream)."""
+        L.check(self.ctx, self._lib.kmz_id_repeats_seg_begin(self.ctx, C.c_void_p(segs_ptr), world, seg,
+                                                             C.c_void_p(stream) if stream else None))
+
+    def id_repeats_seg_end(self):
+        """-> (repeated: Optional[bool], max_count: int) (kmz_id_repeats_seg_end);
+        repeated is None when the certificate cannot decide, and meaningless
+        when max_count >= seg (a segment overflowed)."""
+        r, m = C.c_uint32(), C.c_uint64()
+        rc = self._lib.kmz_id_repeats_seg_end(self.ctx, C.byref(r), C.byref(m))
+        if rc == L.E_UNSUPPORTED:
+            return None, int(m.value)
+        L.check(self.ctx, rc)
+        return bool(r.value), int(m.value)
 
     def graph_stats(self):
         """(runs replayed from hipGraphs so far, graphs held) (kmz_get_graph_stats)."""

@@ -129,7 +129,7 @@ def _crossing_batches(case, world, t0=0):
     return out
 
 
-def _crossing_worker(rank, world, port, q, case, exact, t0=0):
+def _crossing_worker(rank, world, port, q, case, exact, t0=0, no_cert=False):
     import torch
     import torch.distributed as dist
 
@@ -144,7 +144,9 @@ def _crossing_worker(rank, world, port, q, case, exact, t0=0):
         batch = _crossing_batches(case, world, t0)[rank]
         e = Engine(0)
         e.load(batch, synth.shape_table(synth.MESH))
-        e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+        # (no_cert: the run skips its own certificate, merge_all's id guard
+        # covers every shard's ids -- a repeat inside one shard included)
+        e.run(L.RUN_STATS_TAG | L.RUN_DEPS | (L.RUN_NO_CERT if no_cert else 0))
         gw, ew, tw = (e.partials_words(w) for w in (L.PART_GROUPS, L.PART_ENDPOINTS, L.PART_TRIPLES))
         g = torch.zeros(gw, dtype=torch.int64)
         ep = torch.zeros(ew, dtype=torch.int64)
@@ -171,11 +173,12 @@ def _crossing_worker(rank, world, port, q, case, exact, t0=0):
         dist.destroy_process_group()
 
 
-def _run_crossing(case, world, exact=True, t0=0):
+def _run_crossing(case, world, exact=True, t0=0, no_cert=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_crossing_worker, args=(r, world, port, q, case, exact, t0)) for r in range(world)]
+    ps = [ctx.Process(target=_crossing_worker, args=(r, world, port, q, case, exact, t0, no_cert))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = sorted((q.get(timeout=150) for _ in range(world)), key=lambda r: r[0])
@@ -210,9 +213,12 @@ def _whole_batch_expected(case, world, t0=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,world,t0", [("parent", 2, 0), ("repeat", 2, 0), ("repeat", 3, 0), ("inner", 2, 0),
-                                          ("repeat", 2, 1000), ("parent", 2, 500)])
-def test_crossing_shards_merge_exactly(case, world, t0):
+@pytest.mark.parametrize("case,world,t0,no_cert", [("parent", 2, 0, False), ("repeat", 2, 0, False),
+                                                  ("repeat", 3, 0, False), ("inner", 2, 0, False),
+                                                  ("repeat", 2, 1000, False), ("parent", 2, 500, False),
+                                                  ("inner", 2, 0, True), ("repeat", 3, 0, True),
+                                                  ("none", 2, 0, True)])
+def test_crossing_shards_merge_exactly(case, world, t0, no_cert):
     """SURVEY.md 8e / Traces.ts:117-143: the reference keys ONE Map by span id
     over the whole batch, so a parent in another shard, an id in two shards or
     an id repeated inside one shard changes rows and edges that per-shard runs
@@ -220,8 +226,11 @@ def test_crossing_shards_merge_exactly(case, world, t0):
     exact (one unsharded dependency pass on rank 0, broadcast): every rank ends
     with the single-engine result over the whole batch, bit for bit, whose
     edges and endpoints equal the C oracle's.  ``t0`` > 0: a batch that does
-    not start at global position 0 (the first rows stay global)."""
-    res = _run_crossing(case, world, t0=t0)
+    not start at global position 0 (the first rows stay global).  ``no_cert``:
+    the runs skip their own uniqueness certificate (KMZ_RUN_NO_CERT, the
+    multi-GPU bench's setting) and the id guard alone finds the repeat --
+    inside one shard too, whose window-join result it replaces."""
+    res = _run_crossing(case, world, t0=t0, no_cert=no_cert)
     assert [r[1] for r in res] == ["merged"] * world, [r[1] for r in res]
     exp, okeys, oep = _whole_batch_expected(case, world, t0)
     assert np.array_equal(np.frombuffer(exp[1], np.uint64), okeys)

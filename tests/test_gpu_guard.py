@@ -164,3 +164,63 @@ def test_id_guard_fixed_segments_over_steps(world, dev_kind):
         found = [x[1] for x in r[1]]
         assert fixed == [False, True, True, True, True]
         assert found == [False, False, True, False, True]
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_id_repeats_seg_over_received_segments(engine, world):
+    """kmz_id_repeats_seg_begin/_end over fixed segments as an all-to-all
+    delivers them (count word, values, stale words past the count), enqueued
+    on a stream of its own: distinct values pass, one repeat inside a segment
+    or across two is found, an overflowed segment reports its count."""
+    from kmamiz_amd import dist as kdist
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(synth.MESH, 0, 3000)
+    engine.load(batch, synth.shape_table(synth.MESH))
+    h, c = kdist.route_ids_np(batch.span_id, world)
+    seg = int(c.max()) + 1 + 4100  # slack past a pass-1 tile: short and empty tiles in every segment
+    out = torch.full((world * seg,), -1, dtype=torch.int64, device="cuda")  # stale words: never read
+    engine.route_ids_fixed(world, seg, out.data_ptr(), True)
+    torch.cuda.synchronize()
+    gs = torch.cuda.Stream()
+
+    def verdict(buf, s):
+        torch.cuda.synchronize()
+        engine.id_repeats_seg_begin(buf.data_ptr(), world, s, gs.cuda_stream)
+        return engine.id_repeats_seg_end()
+
+    assert verdict(out, seg) == (False, int(c.max()))
+    r = out.view(world, seg)
+    last = world - 1
+    k = int(c[last])
+    save = r[last, k].item()
+    r[last, k] = r[last, 1]  # inside the last segment
+    assert verdict(out, seg) == (True, int(c.max()))
+    r[last, k] = save
+    if world > 1:
+        r[last, k] = r[0, 1]  # across segments (two sources sent one value)
+        assert verdict(out, seg) == (True, int(c.max()))
+        r[last, k] = save
+    assert verdict(out, seg) == (False, int(c.max()))
+    small = max(2, int(c.max()) // 2)  # overflowed: the count says so
+    o2 = torch.zeros(world * small, dtype=torch.int64, device="cuda")
+    engine.route_ids_fixed(world, small, o2.data_ptr(), True)
+    rep, maxc = verdict(o2, small)
+    assert maxc == int(c.max()) and maxc >= small
+
+
+def test_no_cert_run_equals_certified_run(engine):
+    """KMZ_RUN_NO_CERT (a run covered by the multi-GPU id guard) changes no
+    result on a batch with unique ids."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(synth.MESH, 0, 4000)
+    engine.load(batch, synth.shape_table(synth.MESH))
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    g0, k0, e0 = engine.fetch()
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS | L.RUN_NO_CERT)
+    g1, k1, e1 = engine.fetch()
+    assert g0.tobytes() == g1.tobytes()
+    assert np.array_equal(np.sort(k0), np.sort(k1))
+    assert e0.tobytes() == e1.tobytes()

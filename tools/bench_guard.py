@@ -1,9 +1,21 @@
 """Cost of the cross-shard repeated-id guard on one GPU:
-rank 0's shard of config 4 at world 2/4/8 (kmz_synth_load_shard), the routing
-of its span-id hashes (kmz_route_ids, into device memory) and the certificate
-over as many values as an owner receives (kmz_id_repeats, device memory),
-timed over repeats, beside the shard's own step (kmz_run).  The all-to-all
-itself is not timed here (one GPU).  Prints one JSON object."""
+rank 0's shard of config 4 at world 2/4/8 (kmz_synth_load_shard).  Timed over
+repeats, on the engine's stream = torch's (as bench.py):
+  step_ms           the shard's own step with its certificate (kmz_run)
+  step_nocert_ms    ... with KMZ_RUN_NO_CERT (the multi-GPU setting: the
+                    guard checks every shard's ids, the run checks none)
+  route_fixed_ms    kmz_route_ids_fixed, one pass (and route_fixed_hist_ms,
+                    the histogram / scan / scatter form, KMZ_ABLATE2 bit 12)
+  seg_certificate_ms  kmz_id_repeats_seg_begin/_end over world segments as
+                    an owner receives them, alone
+  guarded_step_ms   the whole guarded step as bench.py runs it at N > 1, with
+                    the all-to-all stood in for by a device copy of the
+                    segments on a stream of its own: routing, then the run
+                    (no certificate) beside the copy + the segment
+                    certificate on the guard's stream, then its verdict
+The exchange over xGMI itself is not timed here (one GPU): its projection
+is the bytes each rank sends over its peer links at ~153 GB/s each.  Prints
+one JSON object."""
 import json
 import os
 import sys
@@ -11,6 +23,18 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def _timed(fn, reps=3):
+    import torch
+
+    fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps * 1e3
 
 
 def main():
@@ -22,51 +46,64 @@ def main():
 
     ntr = 36578450  # 1e9 mesh spans (config 4)
     out = {"metric": "sharding guard cost per step, rank 0 of config 4", "unit": "ms", "worlds": {}}
-    eng = Engine(0)
+    stream = torch.cuda.Stream()  # (as bench.py: torch's current stream and the engine's, not handle 0)
+    torch.cuda.set_stream(stream)
+    eng = Engine(0, stream=stream.cuda_stream)
+    os.environ["KMZ_ABLATE2"] = str(4096)
+    eng_hist = Engine(0, stream=stream.cuda_stream)  # (the histogram routing form, for comparison)
+    del os.environ["KMZ_ABLATE2"]
+    gs = torch.cuda.Stream()
+    cs = torch.cuda.Stream()
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS
     for world in (2, 4, 8):
         n = eng.load_synthetic_shard(synth.MESH, synth.SEED, 0, ntr, world, 0)
-        buf = torch.empty(n, dtype=torch.int64, device="cuda")
-        eng.run(L.RUN_STATS_TAG | L.RUN_DEPS)
-        t = time.perf_counter()
-        for _ in range(3):
-            eng.run(L.RUN_STATS_TAG | L.RUN_DEPS)
-        step = (time.perf_counter() - t) / 3
-        eng.route_ids(world, buf.data_ptr(), n, True)
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        for _ in range(3):
-            eng.route_ids(world, buf.data_ptr(), n, True)
-        route = (time.perf_counter() - t) / 3
-        # fixed segments (IdGuard's steady state: no counts exchange, no sync)
+        step = _timed(lambda: eng.run(flags))
+        step_nc = _timed(lambda: eng.run(flags | L.RUN_NO_CERT))
         seg = int(n / world * 1.125) + 1025
-        fbuf = torch.empty(world * seg, dtype=torch.int64, device="cuda")
-        eng.route_ids_fixed(world, seg, fbuf.data_ptr(), True)
+        send = torch.empty(world * seg, dtype=torch.int64, device="cuda")
+        recv = torch.empty_like(send)
+        route = _timed(lambda: eng.route_ids_fixed(world, seg, send.data_ptr(), True))
+        eng_hist.load_synthetic_shard(synth.MESH, synth.SEED, 0, ntr, world, 0)
+        route_hist = _timed(lambda: eng_hist.route_ids_fixed(world, seg, send.data_ptr(), True))
+        eng_hist.load(synth.host_batch(synth.MESH, 0, 10)[0], synth.shape_table(synth.MESH))  # (free its columns)
+        eng.route_ids_fixed(world, seg, send.data_ptr(), True)
+        recv.copy_(send)
         torch.cuda.synchronize()
-        t = time.perf_counter()
-        for _ in range(3):
-            eng.route_ids_fixed(world, seg, fbuf.data_ptr(), True)
-        torch.cuda.synchronize()
-        route_fixed = (time.perf_counter() - t) / 3
-        del fbuf
-        # what an owner receives: ~n values (hash-uniform owners, equal shards)
-        assert eng.id_repeats(buf.data_ptr(), n, True) is False
-        t = time.perf_counter()
-        for _ in range(3):
-            eng.id_repeats(buf.data_ptr(), n, True)
-        check = (time.perf_counter() - t) / 3
-        # the exchange over xGMI (not timed on one GPU): each rank sends
-        # (world-1)/world of its 8-B hashes, one direct link per peer at
-        # ~153 GB/s (MI355X_MICROARCH.md), all links at once
+
+        def seg_cert():
+            eng.id_repeats_seg_begin(recv.data_ptr(), world, seg, 0)
+            rep, _ = eng.id_repeats_seg_end()
+            assert rep is False
+
+        cert = _timed(seg_cert)
+
+        def guarded():
+            eng.route_ids_fixed(world, seg, send.data_ptr(), True)
+            cs.wait_stream(stream)
+            with torch.cuda.stream(cs):
+                recv.copy_(send)  # (stands in for the all-to-all)
+            gs.wait_stream(cs)
+            eng.id_repeats_seg_begin(recv.data_ptr(), world, seg, gs.cuda_stream)
+            eng.run_begin(flags | L.RUN_NO_CERT)
+            eng.run_end()
+            rep, _ = eng.id_repeats_seg_end()
+            assert rep is False
+
+        guarded_ms = _timed(guarded)
         peer_bytes = 8 * n / world
-        out["worlds"][world] = {"spans_rank0": n, "step_ms": round(step * 1e3, 3), "route_ms": round(route * 1e3, 3),
-                                "route_fixed_ms": round(route_fixed * 1e3, 3),
-                                "certificate_ms": round(check * 1e3, 3),
+        a2a = peer_bytes / 153e9 * 1e3
+        out["worlds"][world] = {"spans_rank0": n, "step_ms": round(step, 3), "step_nocert_ms": round(step_nc, 3),
+                                "route_fixed_ms": round(route, 3), "route_fixed_hist_ms": round(route_hist, 3),
+                                "seg_certificate_ms": round(cert, 3), "guarded_step_ms": round(guarded_ms, 3),
                                 "all_to_all_bytes_per_rank": int(8 * n * (world - 1) / world),
-                                "all_to_all_ms_projected": round(peer_bytes / 153e9 * 1e3, 3),
-                                "guard_ms_projected": round((route_fixed + check) * 1e3 + peer_bytes / 153e9 * 1e3, 3)}
-        del buf
+                                "all_to_all_ms_projected": round(a2a, 3),
+                                # the guard's cost on the step: what the guarded step adds to the
+                                # shard's certified step (the exchange overlaps the run)
+                                "guard_ms_measured": round(guarded_ms - step, 3)}
+        del send, recv
         torch.cuda.empty_cache()
     eng.close()
+    eng_hist.close()
     print(json.dumps(out))
 
 
