@@ -150,11 +150,16 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin)
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
   hipStream_t main = nullptr, side = nullptr;
+  // the certificate's own side stream (from the end of the join: not queued
+  // behind K3 on `side`), its completion event, and whether this run used it
+  hipStream_t side2 = nullptr;
+  hipEvent_t ev_cert = nullptr;
+  bool cert2 = false;
   hipEvent_t ev_fork = nullptr, ev_k3 = nullptr, ev_join = nullptr, ev_done = nullptr;
   bool overlap = false;  // this run uses the side stream
 
@@ -201,6 +206,7 @@ int ensure(kmz_ctx *c, DevBuf &b, size_t bytes) {
   if (b.p) {  // (both streams may still use it)
     hipStreamSynchronize(c->stream);
     if (c->side) hipStreamSynchronize(c->side);
+    if (c->side2) hipStreamSynchronize(c->side2);
     if (c->main && c->main != c->stream) hipStreamSynchronize(c->main);
     hipFree(b.p);
     b.p = nullptr;
@@ -334,6 +340,8 @@ kmz_ctx *kmz_create(int device, void *stream) {
     c->own_stream = true;
   }
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_cert, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_k3, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -361,6 +369,7 @@ void kmz_destroy(kmz_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->side) hipStreamSynchronize(c->side);
+  if (c->side2) hipStreamSynchronize(c->side2);
   hipStreamSynchronize(c->stream);
   if (c->xfer) hipStreamSynchronize(c->xfer);
   harvest(c);
@@ -396,7 +405,11 @@ void kmz_destroy(kmz_ctx *c) {
     hipStreamSynchronize(c->side);
     hipStreamDestroy(c->side);
   }
-  for (hipEvent_t e : {c->ev_fork, c->ev_k3, c->ev_join, c->ev_done})
+  if (c->side2) {
+    hipStreamSynchronize(c->side2);
+    hipStreamDestroy(c->side2);
+  }
+  for (hipEvent_t e : {c->ev_fork, c->ev_k3, c->ev_join, c->ev_done, c->ev_cert})
     if (e) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
@@ -810,9 +823,13 @@ static int run_join(kmz_ctx *c, bool *ok) {
   }
   if (!early && !c->no_cert) {
     if (cert_side) {  // the certificate checks the join's ids beside the chain walk (read after the run)
+      // on a stream of its own, from the end of the join, not behind K3 on
+      // the side stream (KMZ_ABLATE2 bit 14: behind it, for comparison)
+      hipStream_t cs = (c->ablate2 & 16384u) ? c->side : c->side2;
       HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
-      HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_join, 0));
-      c->stream = c->side;
+      HIPCHK(c, hipStreamWaitEvent(cs, c->ev_join, 0));
+      c->stream = cs;
+      c->cert2 = cs == c->side2;
     }
     {
       Timed t(c, KMZ_K_CERT);
@@ -1173,13 +1190,15 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     // keys' shapes to endpoints
     a.id_ep = by_shape ? P<uint32_t>(c->d_dep) : nullptr;
     a.n_ids = c->n_shapes;
-    Timed t(c, KMZ_K_WALK);
-    if (w8)
-      launch_chain_tile8(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep), c->n_shapes,
-                         P<uint32_t>(c->ctile), a);
-    else
-      launch_chain_tile(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep), c->n_shapes,
-                        P<uint4>(c->cetab), P<uint32_t>(c->ctile), a);
+    {
+      Timed t(c, KMZ_K_WALK);
+      if (w8)
+        launch_chain_tile8(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
+                           c->n_shapes, P<uint32_t>(c->ctile), a);
+      else
+        launch_chain_tile(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
+                          c->n_shapes, P<uint4>(c->cetab), P<uint32_t>(c->ctile), a);
+    }
   }
   {
     Timed t(c, KMZ_K_SETTLE);
@@ -1533,6 +1552,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   const uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
   c->sstats = false;
   c->chain_ran = false;
+  c->cert2 = false;
   HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4 + S_COUNT * 8, c->stream));
   int r;
   c->main = c->stream;
@@ -1551,12 +1571,19 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     c->stream = c->main;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     hipStreamIsCapturing(c->main, &cs);
-    if (c->overlap && cs == hipStreamCaptureStatusNone) hipStreamSynchronize(c->side);
+    if (c->overlap && cs == hipStreamCaptureStatusNone) {
+      hipStreamSynchronize(c->side);
+      hipStreamSynchronize(c->side2);
+    }
     return r;
   }
   if (c->overlap) {  // everything queued on the side stream, before the read-back
     HIPCHK(c, hipEventRecord(c->ev_done, c->side));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
+  }
+  if (c->cert2) {  // ... and on the certificate's
+    HIPCHK(c, hipEventRecord(c->ev_cert, c->side2));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_cert, 0));
   }
   static_assert(C_COUNT * 4 % 8 == 0, "the statistics follow the counters in one buffer and in hpin");
   (void)s64;
