@@ -150,7 +150,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own)
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -160,6 +160,10 @@ struct kmz_ctx {
   hipStream_t side2 = nullptr;
   hipEvent_t ev_cert = nullptr;
   bool cert2 = false;
+  // a chain table past the MALL (config 5): the certificate waits for the
+  // end of the walk and runs beside the settle (launch_cert_deferred)
+  bool cert_defer = false;
+  CertPlan cert_pl{};
   hipEvent_t ev_fork = nullptr, ev_k3 = nullptr, ev_join = nullptr, ev_done = nullptr;
   bool overlap = false;  // this run uses the side stream
 
@@ -751,6 +755,35 @@ int kmz_json_load(kmz_ctx *c, const uint32_t *shape_of_raw, const uint32_t *stat
   return KMZ_OK;
 }
 
+// The certificate split + check deferred by run_join (a chain table past the
+// MALL, config 5): on side2 from here, i.e. beside the settle's probe-bound
+// k_key_part / k_key_slice instead of between the join and the walk (the
+// walk's HBM-resident chain table and the certificate slow each other down).
+static int launch_cert_deferred(kmz_ctx *c) {
+  if (!c->cert_defer) return KMZ_OK;
+  c->cert_defer = false;
+  const uint32_t n = (uint32_t)c->n;
+  const CertPlan &pl = c->cert_pl;
+  unsigned int *cnt = P<unsigned int>(c->counters);
+  unsigned int *cur2 = P<unsigned int>(c->ccur);
+  HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_join, 0));
+  hipStream_t keep = c->stream;
+  c->stream = c->side2;
+  c->cert2 = true;
+  {
+    Timed t(c, KMZ_K_CERT);
+    launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
+                      P<unsigned long long>(c->cpool2), cur2, cnt);
+  }
+  {
+    Timed t(c, KMZ_K_CHECK);
+    launch_cert_check(c->stream, n, pl, P<unsigned long long>(c->cpool2), cur2, cnt);
+  }
+  c->stream = keep;
+  return KMZ_OK;
+}
+
 // K1': window join + uniqueness certificate.  *ok = false when the batch
 // needs the global table (a repeated span id, or a batch too large for the
 // certificate's two partition levels).
@@ -821,7 +854,14 @@ static int run_join(kmz_ctx *c, bool *ok) {
                 P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, pl,
                 c->ablate | (c->no_cert || early ? 64u : 0u));
   }
-  if (!early && !c->no_cert) {
+  // (KMZ_ABLATE2 bit 15, for comparison: with a chain table past the MALL
+  // the certificate beside the settle instead of on the main stream between
+  // the join and the walk.  Config 5: 8.31 against 8.00 ms, the settle's
+  // probes and the certificate slow each other down; profiles/r05/ab/defer/)
+  if (!early && !c->no_cert && !cert_side && c->overlap && (c->ablate2 & 32768u)) {
+    c->cert_defer = true;
+    c->cert_pl = pl;
+  } else if (!early && !c->no_cert) {
     if (cert_side) {  // the certificate checks the join's ids beside the chain walk (read after the run)
       // on a stream of its own, from the end of the join, not behind K3 on
       // the side stream (KMZ_ABLATE2 bit 14: behind it, for comparison)
@@ -1200,6 +1240,7 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
                           c->n_shapes, P<uint4>(c->cetab), P<uint32_t>(c->ctile), a);
     }
   }
+  if (int r2 = launch_cert_deferred(c)) return r2;
   {
     Timed t(c, KMZ_K_SETTLE);
     launch_chain_settle_list(c->stream, nt, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
@@ -1343,6 +1384,7 @@ static int run_deps(kmz_ctx *c, bool links) {
                    // (test knob 24 forces sig collisions on the first seed only)
                    c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)), cmode);
     }
+    if (int r2 = launch_cert_deferred(c)) return r2;
     {
       Timed t(c, KMZ_K_SETTLE);
       launch_chain_settle(c->stream, n, direct, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
@@ -1553,6 +1595,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   c->sstats = false;
   c->chain_ran = false;
   c->cert2 = false;
+  c->cert_defer = false;
   HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4 + S_COUNT * 8, c->stream));
   int r;
   c->main = c->stream;
@@ -1577,6 +1620,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     }
     return r;
   }
+  if ((r = launch_cert_deferred(c))) return r;  // (a path with no walk after the join)
   if (c->overlap) {  // everything queued on the side stream, before the read-back
     HIPCHK(c, hipEventRecord(c->ev_done, c->side));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
