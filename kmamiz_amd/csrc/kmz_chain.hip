@@ -590,6 +590,15 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
 // Chain interning stages few keys (new chains only): k_chain_settle inserts
 // them in place, which is cheaper at that volume.
 constexpr uint32_t KP_T = 256, KP_PER = 16, KP_STEP = KP_T * KP_PER;  // 4096 keys per step
+// a direct-mapped LDS cache of the keys this workgroup already wrote out
+// (its runs are all of one coarse bin: the grid is a multiple of 2^lb1), so a
+// key that recurs across its runs -- config 5's power-law head -- is written
+// once: the edge set is a set, and a key found in the cache was written by the
+// thread that put it there
+#ifndef KMZ_KP_CACHE
+#define KMZ_KP_CACHE 2048
+#endif
+constexpr uint32_t KP_CACHE = KMZ_KP_CACHE;
 // (Measured and dropped: each step's keys first put in an 8192-slot LDS set
 // and the repeats dropped before the slice sort -- k_key_part + k_key_slice
 // 2.63 -> 3.10 ms on config 5: few repeats fall inside one 4096-key step.)
@@ -632,11 +641,13 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
                                                    uint32_t lb2, void *__restrict__ bucket_v,
                                                    uint64_t bcap, uint32_t *__restrict__ bucket_n,
                                                    unsigned long long *__restrict__ trip, uint64_t tcap,
-                                                   unsigned int *__restrict__ counters) {
+                                                   unsigned int *__restrict__ counters, bool dedup) {
   using KT = typename std::conditional<C, uint32_t, unsigned long long>::type;
   const KT *__restrict__ stage = static_cast<const KT *>(stage_v);
   KT *__restrict__ bucket = static_cast<KT *>(bucket_v);
   __shared__ KT sorted[KP_STEP];  // 32 KB (16 KB compact)
+  __shared__ unsigned long long kcache[KP_CACHE];  // 16 KB: (coarse bin, residual) or the whole key; ~0 = empty
+  for (uint32_t x = threadIdx.x; x < KP_CACHE; x += KP_T) kcache[x] = ~0ull;
   __shared__ uint32_t hist[1u << KB2_MAX], off[1u << KB2_MAX], base[1u << KB2_MAX], wsum[KP_T / 64];
   static_assert((1u << KB2_MAX) <= 4 * KP_T, "kp_scan covers the slices of a coarse bin");
   const uint32_t nf = 1u << lb2;
@@ -689,11 +700,21 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
     for (uint32_t x = threadIdx.x; x < nf; x += KP_T) hist[x] = 0;
     __syncthreads();
     uint32_t f[KP_PER], rk[KP_PER];
+    bool keep[KP_PER];
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j) {
-      const bool v = j * KP_T + threadIdx.x < nv;
+      keep[j] = j * KP_T + threadIdx.x < nv;
+      if (dedup && keep[j]) {
+        const uint64_t e = C ? (((uint64_t)c << 32) | (uint64_t)k[j]) : (uint64_t)k[j];
+        const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+        const uint32_t slot = (lo ^ (lo >> 11) ^ (lo >> 22) ^ hi ^ (hi >> 11)) & (KP_CACHE - 1);
+        if (kcache[slot] == e)
+          keep[j] = false;
+        else
+          kcache[slot] = e;
+      }
       f[j] = fine(k[j]);
-      rk[j] = v ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
+      rk[j] = keep[j] ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice
     }
     __syncthreads();
     for (uint32_t x = threadIdx.x; x < nf; x += KP_T) {
@@ -705,7 +726,7 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
     kp_scan(off, nf, wsum);
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j)
-      if (j * KP_T + threadIdx.x < nv) sorted[off[f[j]] + rk[j]] = k[j];
+      if (keep[j]) sorted[off[f[j]] + rk[j]] = k[j];
     __syncthreads();
     // consecutive threads -> consecutive slots of one slice's bucket
     const uint32_t nz = off[nf - 1] + hist[nf - 1];
@@ -1022,7 +1043,7 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
                          unsigned long long *bucket, uint64_t bcap, uint32_t *bucket_n,
                          const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
-                         uint32_t gcap, uint32_t ablate, bool cmode) {
+                         uint32_t gcap, uint32_t ablate, bool cmode, uint32_t ablate2) {
   if (!chain_tiles(n)) return;
   const uint32_t g = chain_grid(n);
   uint32_t lb1, lb2;
@@ -1034,14 +1055,16 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
   const uint32_t nsl = (uint32_t)(tcap / ESLICE), nruns = g << lb1;
   if (direct) {
     const uint32_t gp = std::min<uint32_t>(nruns, 8192), gs = std::min<uint32_t>(nsl, 8192);
+    // the key cache needs one coarse bin per workgroup (KMZ_ABLATE2 bit 16: off, for comparison)
+    const bool dedup = !(ablate2 & 65536u) && gp % (1u << lb1) == 0;
     if (cmode) {
       hipLaunchKernelGGL(k_key_part<true>, dim3(gp), dim3(KP_T), 0, s, (const void *)stage, scap >> lb1, stage_n,
-                         nruns, lb1, lb2, (void *)bucket, bcap, bucket_n, trip, tcap, counters);
+                         nruns, lb1, lb2, (void *)bucket, bcap, bucket_n, trip, tcap, counters, dedup);
       hipLaunchKernelGGL(k_key_slice<true>, dim3(gs), dim3(KS_T), 0, s, (const void *)bucket, bcap, bucket_n, nsl,
                          lb1 + lb2, trip, tcap, counters);
     } else {
       hipLaunchKernelGGL(k_key_part<false>, dim3(gp), dim3(KP_T), 0, s, (const void *)stage, scap >> lb1, stage_n,
-                         nruns, lb1, lb2, (void *)bucket, bcap, bucket_n, trip, tcap, counters);
+                         nruns, lb1, lb2, (void *)bucket, bcap, bucket_n, trip, tcap, counters, dedup);
       hipLaunchKernelGGL(k_key_slice<false>, dim3(gs), dim3(KS_T), 0, s, (const void *)bucket, bcap, bucket_n, nsl,
                          lb1 + lb2, trip, tcap, counters);
     }

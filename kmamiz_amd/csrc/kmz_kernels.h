@@ -163,7 +163,7 @@ void launch_chain_settle(hipStream_t s, uint32_t n, bool direct, void *ctab, uin
                          const unsigned long long *stage, uint32_t scap, const uint32_t *stage_n,
                          unsigned long long *bucket, uint64_t bcap, uint32_t *bucket_n,
                          const unsigned long long *defer, uint32_t dcap, const uint32_t *defer_n, uint32_t *gpos,
-                         uint32_t gcap, uint32_t ablate = 0, bool cmode = false);
+                         uint32_t gcap, uint32_t ablate = 0, bool cmode = false, uint32_t ablate2 = 0);
 // per shape: dependency endpoint + SERVER element hash under `seed` (the walk's gather table)
 void launch_chain_etab(hipStream_t s, const uint32_t *dep_ep, uint32_t n_shapes, uint64_t seed, uint4 *etab);
 // K2 + K4 fused over one LDS window, chain interning (kmz_fuse.hip); its
