@@ -150,7 +150,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -1599,15 +1599,24 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4 + S_COUNT * 8, c->stream));
   int r;
   c->main = c->stream;
-  if (c->overlap) {
+  // (KMZ_ABLATE2 bit 17, for comparison: K3 on the main stream between the
+  // join and the walk -- run_deps runs the shape-level K3 before its walk --
+  // instead of beside the join on the side stream)
+  const bool k3_mid = smode && (flags & KMZ_RUN_DEPS) && (c->ablate2 & 131072u);
+  if (c->overlap && !k3_mid) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
     c->stream = c->side;
   }
-  r = smode ? run_stats(c, smode) : 0;
-  if (c->overlap) {
+  r = smode && !k3_mid ? run_stats(c, smode) : 0;
+  if (c->overlap && !k3_mid) {
     c->stream = c->main;
     HIPCHK(c, hipEventRecord(c->ev_k3, c->side));
+  }
+  if (c->overlap && k3_mid) {  // (nothing on the side stream before the certificate: the waits pass at once)
+    HIPCHK(c, hipEventRecord(c->ev_k3, c->main));
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->main));
+    HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
   }
   if (r) return r;
   if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, links))) {
@@ -1621,6 +1630,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     return r;
   }
   if ((r = launch_cert_deferred(c))) return r;  // (a path with no walk after the join)
+  if (k3_mid && (r = run_stats(c, smode))) return r;  // (its shape level ran inside run_deps)
   if (c->overlap) {  // everything queued on the side stream, before the read-back
     HIPCHK(c, hipEventRecord(c->ev_done, c->side));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));

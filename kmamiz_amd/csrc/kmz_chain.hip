@@ -595,10 +595,12 @@ constexpr uint32_t KP_T = 256, KP_PER = 16, KP_STEP = KP_T * KP_PER;  // 4096 ke
 // key that recurs across its runs -- config 5's power-law head -- is written
 // once: the edge set is a set, and a key found in the cache was written by the
 // thread that put it there
-#ifndef KMZ_KP_CACHE
-#define KMZ_KP_CACHE 2048
+// 16 KB: 4096 32-bit residuals (compact staging), else 2048 whole keys
+// (2048 whole keys measured against 1024 and 4096: 7.50 against 7.67 / 7.74
+// ms on config 5, the larger cache costing occupancy)
+#ifndef KMZ_KP_CACHE_BYTES
+#define KMZ_KP_CACHE_BYTES 16384
 #endif
-constexpr uint32_t KP_CACHE = KMZ_KP_CACHE;
 // (Measured and dropped: each step's keys first put in an 8192-slot LDS set
 // and the repeats dropped before the slice sort -- k_key_part + k_key_slice
 // 2.63 -> 3.10 ms on config 5: few repeats fall inside one 4096-key step.)
@@ -646,8 +648,10 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
   const KT *__restrict__ stage = static_cast<const KT *>(stage_v);
   KT *__restrict__ bucket = static_cast<KT *>(bucket_v);
   __shared__ KT sorted[KP_STEP];  // 32 KB (16 KB compact)
-  __shared__ unsigned long long kcache[KP_CACHE];  // 16 KB: (coarse bin, residual) or the whole key; ~0 = empty
-  for (uint32_t x = threadIdx.x; x < KP_CACHE; x += KP_T) kcache[x] = ~0ull;
+  // the cache: residuals of this workgroup's coarse bin, or whole keys; all ones = empty
+  constexpr uint32_t KP_CACHE = KMZ_KP_CACHE_BYTES / sizeof(KT);
+  __shared__ KT kcache[KP_CACHE];
+  for (uint32_t x = threadIdx.x; x < KP_CACHE; x += KP_T) kcache[x] = (KT)~0ull;
   __shared__ uint32_t hist[1u << KB2_MAX], off[1u << KB2_MAX], base[1u << KB2_MAX], wsum[KP_T / 64];
   static_assert((1u << KB2_MAX) <= 4 * KP_T, "kp_scan covers the slices of a coarse bin");
   const uint32_t nf = 1u << lb2;
@@ -704,14 +708,14 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
 #pragma unroll
     for (int j = 0; j < (int)KP_PER; ++j) {
       keep[j] = j * KP_T + threadIdx.x < nv;
-      if (dedup && keep[j]) {
-        const uint64_t e = C ? (((uint64_t)c << 32) | (uint64_t)k[j]) : (uint64_t)k[j];
+      if (dedup && keep[j] && k[j] != (KT)~0ull) {  // (one coarse bin per workgroup: the residual is the key)
+        const uint64_t e = (uint64_t)k[j];
         const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
-        const uint32_t slot = (lo ^ (lo >> 11) ^ (lo >> 22) ^ hi ^ (hi >> 11)) & (KP_CACHE - 1);
-        if (kcache[slot] == e)
+        const uint32_t slot = (lo ^ (lo >> 12) ^ (lo >> 24) ^ hi ^ (hi >> 12)) & (KP_CACHE - 1);
+        if (kcache[slot] == k[j])
           keep[j] = false;
         else
-          kcache[slot] = e;
+          kcache[slot] = k[j];
       }
       f[j] = fine(k[j]);
       rk[j] = keep[j] ? atomicAdd(&hist[f[j]], 1u) : 0;  // rank within its slice

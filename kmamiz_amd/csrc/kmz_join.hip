@@ -58,15 +58,29 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
                                                      unsigned int *__restrict__ counters, uint32_t ablate) {
   constexpr uint32_t NW = JTT / 64, BINS = 1u << B1;
   __shared__ uint64_t lsid[JW];
-  __shared__ uint4 lbkt[JB];  // later: staging of the tile's hashed ids
-  // the buckets' fill counts (insert phase), then the certificate's per-wave
-  // bin counts (pass 1)
-  __shared__ uint32_t lcw[JB > BINS * NW ? JB : BINS * NW];
-  uint32_t *const lcnt = lcw, *const wcnt = lcw;
+  // the window's LDS hash (kmz_joinw.h jh8): per bucket 8 entries (local
+  // index + 1, u16) and their 8-bit fingerprints in one u64, so that a lookup
+  // tests all 8 with a few 32-bit operations (a zero-byte test) instead of
+  // decoding 16 packed entries; fill counts four per word (a bucket past 255
+  // ids -- repeated ids only -- spills into its neighbour's count: that only
+  // costs lookups, which compare whole ids, a miss, resolved by the
+  // semi-join).  After the lookups
+  // the entries become the certificate's staging and the fingerprints its
+  // per-wave bin counters (pass 1)
+  __shared__ uint4 lidx[JB];
+  __shared__ unsigned long long lfp[JB];
+  __shared__ uint32_t lcnt4[JB / 4];
+  uint32_t *const wcnt = reinterpret_cast<uint32_t *>(lfp);
+  constexpr uint32_t WCAP = JB * 2;  // u32 words of the pass-1 counters
+  static_assert(BINS * NW <= WCAP, "pass-1 counters fit the fingerprint words");
+  // per window slot: its parent's local index (12 bits, or X_NONE / X_MISS)
+  // | X_CLIENT when the slot itself is a CLIENT span (no separate kind array:
+  // 2.5 KB of LDS, the third workgroup per CU)
   __shared__ uint16_t ldp[JW];
-  __shared__ uint8_t lkind[JW];
+  constexpr uint32_t X_NONE = 0xFFF, X_MISS = 0xFFE, X_CLIENT = 0x8000;
+  static_assert(JW < X_MISS, "local indices stay below the markers");
   __shared__ uint32_t wsum[NW];
-  __shared__ uint16_t stash[JSTASH];
+  __shared__ uint32_t stash[JSTASH];  // fingerprint << 16 | local index + 1
   __shared__ uint32_t nstash;
   constexpr int PW = JW / JTT, PT = JT / JTT;
   const uint32_t t0 = blockIdx.x * JT, t1 = min(n, t0 + JT);
@@ -74,10 +88,8 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   const bool dbg_t = (ablate & (1u << 23)) != 0;
   unsigned long long tprev = 0, tacc[6] = {0, 0, 0, 0, 0, 0};
   KMZ_JSTAMP(0);
-  for (uint32_t k = threadIdx.x; k < JB; k += JTT) {
-    lbkt[k] = make_uint4(0, 0, 0, 0);
-    lcnt[k] = 0;
-  }
+  for (uint32_t k = threadIdx.x; k < JB; k += JTT) lfp[k] = 0;
+  for (uint32_t k = threadIdx.x; k < JB / 4; k += JTT) lcnt4[k] = 0;
   if (threadIdx.x == 0) nstash = 0;
   // one round of window loads (ids, kinds, parent ids), all in flight together
   uint64_t s[PW], p[PW];
@@ -99,44 +111,36 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
 #pragma unroll
   for (int q = 0; q < PW; ++q) {
     const uint32_t jl = q * JTT + threadIdx.x;
-    hs[q] = jfold(s[q]);
-    if (w0 + jl < w1) {
-      lsid[jl] = s[q];
-      lkind[jl] = k[q];
-    }
+    hs[q] = jh8(jfold(s[q]));
+    if (w0 + jl < w1) lsid[jl] = s[q];
   }
   __syncthreads();
   KMZ_JSTAMP(0);
   bool ovf = false;
-  if (!(ablate & 256)) {  // insert: the emptier of the two buckets, else the other, else the stash
-    // (in lockstep over the thread's PW ids: the bucket counts, then the
-    // slot claims, each step's LDS operations in flight together)
-    uint32_t bq[PW], sq[PW];
+  uint8_t *const lfp8 = reinterpret_cast<uint8_t *>(lfp);
+  uint16_t *const lidx16 = reinterpret_cast<uint16_t *>(lidx);
+  if (!(ablate & 256)) {  // insert: a slot of the id's bucket, else the stash
+    // (in lockstep over the thread's PW ids: the slot claims in flight together)
+    uint32_t sq[PW];
     bool iq[PW];
 #pragma unroll
     for (int q = 0; q < PW; ++q) {
       iq[q] = w0 + q * JTT + threadIdx.x < w1 && s[q] != 0;
-      const uint32_t b1 = jb1(hs[q]), b2 = jb2(hs[q]);
-      bq[q] = lcnt[b1] <= lcnt[b2] ? b1 : b2;
+      const uint32_t b = jbk8(hs[q]), sh = (b & 3) * 8;
+      sq[q] = iq[q] ? (atomicAdd(&lcnt4[b >> 2], 1u << sh) >> sh) & 0xFF : 0u;
     }
-#pragma unroll
-    for (int q = 0; q < PW; ++q) sq[q] = iq[q] ? atomicAdd(&lcnt[bq[q]], 1u) : 0u;
 #pragma unroll
     for (int q = 0; q < PW; ++q) {
       const uint32_t jl = q * JTT + threadIdx.x;
       if (!iq[q]) continue;
-      uint32_t b = bq[q], slot = sq[q];
-      if (slot >= 8) {  // (rare) the other bucket
-        b = b ^ jb1(hs[q]) ^ jb2(hs[q]);
-        slot = atomicAdd(&lcnt[b], 1u);
-      }
-      const uint16_t e = (uint16_t)((jfp(hs[q]) << 12) | (jl + 1));
-      if (slot < 8) {
-        reinterpret_cast<uint16_t *>(&lbkt[b])[slot] = e;
+      const uint32_t b = jbk8(hs[q]);
+      if (sq[q] < 8) {
+        lfp8[b * 8 + sq[q]] = (uint8_t)jfp8(hs[q]);
+        lidx16[b * 8 + sq[q]] = (uint16_t)(jl + 1);
       } else {
         const uint32_t t = atomicAdd(&nstash, 1u);
         if (t < JSTASH)
-          stash[t] = e;
+          stash[t] = (jfp8(hs[q]) << 16) | (jl + 1);
         else
           ovf = true;  // this tile cannot answer: the table path runs
       }
@@ -147,40 +151,34 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   const uint32_t ns = min(nstash, JSTASH);
   // window parents: tile spans, and CLIENT spans of the halo (chains pass
   // through them).  The PW lookups of a thread go in lockstep, each step's
-  // LDS reads in flight together: both buckets; the first fingerprint
-  // candidate's entry; its id.  Further candidates (a fingerprint collision)
-  // and the stash are the rare tail.
-  uint32_t cq[PW], hq[PW], eq[PW];
+  // LDS reads in flight together: the bucket's fingerprints; the first
+  // candidate's entry; its id.  Further candidates (an 8-bit fingerprint
+  // collision) and the stash are the rare tail.
+  uint32_t hq[PW], eq[PW];
+  uint64_t cq[PW];
   bool nq[PW];
   uint16_t rq[PW];
 #pragma unroll
   for (int q = 0; q < PW; ++q) {
     const uint32_t jl = q * JTT + threadIdx.x, j = w0 + jl;
     nq[q] = j < w1 && p[q] != 0 && ((j >= t0 && j < t1) || k[q] == KIND_CLIENT) && !(ablate & 512);
-    rq[q] = nq[q] ? L_MISS : L_NONE;
-    hq[q] = jfold(p[q]);
-    const uint32_t f = jfp(hq[q]);
-    const uint4 x = lbkt[nq[q] ? jb1(hq[q]) : 0], y = lbkt[nq[q] ? jb2(hq[q]) : 0];
-    const uint32_t c[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-    // candidates: entries with the fingerprint (two per word, SWAR; empty
-    // entries have fingerprint 0, which no id has)
-    const uint32_t pat = (f << 12) | (f << 28);
-    uint32_t cand = 0;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const uint32_t v = c[t], z = v ^ pat;
-      cand |= ((z & 0xF000u) == 0 ? 1u : 0u) << (2 * t);
-      cand |= ((z & 0xF0000000u) == 0 ? 1u : 0u) << (2 * t + 1);
-    }
+    rq[q] = nq[q] ? X_MISS : X_NONE;
+    hq[q] = jh8(jfold(p[q]));
+    const uint64_t w = lfp[nq[q] ? jbk8(hq[q]) : 0];
+    uint32_t pat = jfp8(hq[q]);
+    pat |= pat << 8;
+    pat |= pat << 16;
+    // exact zero-byte test of fingerprints ^ pattern: bit 7 of a byte of
+    // ~y & 0x80.. is set iff that byte matched (no carry crosses a byte)
+    const uint32_t xl = (uint32_t)w ^ pat, xh = (uint32_t)(w >> 32) ^ pat;
+    const uint32_t yl = ((xl & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | xl;
+    const uint32_t yh = ((xh & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | xh;
+    const uint64_t cand = ((uint64_t)(~yh & 0x80808080u) << 32) | (uint64_t)(~yl & 0x80808080u);
     cq[q] = nq[q] ? cand : 0;
   }
-  const uint16_t *lbkt16 = reinterpret_cast<const uint16_t *>(lbkt);
 #pragma unroll
-  for (int q = 0; q < PW; ++q) {  // the first candidate's entry (local index + 1)
-    const uint32_t t = __builtin_ctz(cq[q] | 0x10000u);
-    const uint32_t b = t < 8 ? jb1(hq[q]) : jb2(hq[q]);
-    eq[q] = cq[q] ? lbkt16[b * 8 + (t & 7)] & 0xFFF : 0;
-  }
+  for (int q = 0; q < PW; ++q)  // the first candidate's entry (local index + 1)
+    eq[q] = cq[q] ? lidx16[jbk8(hq[q]) * 8 + (__builtin_ctzll(cq[q]) >> 3)] : 0;
 #pragma unroll
   for (int q = 0; q < PW; ++q) {  // its id
     const bool hit = eq[q] && lsid[eq[q] ? eq[q] - 1 : 0] == p[q];
@@ -193,24 +191,24 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
     const uint32_t jl = q * JTT + threadIdx.x;
     if (w0 + jl >= w1) continue;
     uint32_t r = rq[q];
-    uint32_t cand = cq[q];
+    uint64_t cand = cq[q];
     while (cand) {  // (rare) further candidates
-      const uint32_t t = __builtin_ctz(cand);
+      const uint32_t t = __builtin_ctzll(cand) >> 3;
       cand &= cand - 1;
-      const uint32_t en = lbkt16[(t < 8 ? jb1(hq[q]) : jb2(hq[q])) * 8 + (t & 7)] & 0xFFF;
+      const uint32_t en = lidx16[jbk8(hq[q]) * 8 + t];
       if (lsid[en - 1] == p[q]) {
         r = en - 1;
         break;
       }
     }
-    if (nq[q] && r == L_MISS) {
-      const uint32_t f = jfp(hq[q]);
+    if (nq[q] && r == X_MISS) {
+      const uint32_t f = jfp8(hq[q]);
       for (uint32_t t = 0; t < ns; ++t) {
         const uint32_t en = stash[t];
-        if ((en >> 12) == f && lsid[(en & 4095) - 1] == p[q]) r = (en & 4095) - 1;
+        if ((en >> 16) == f && lsid[(en & 0xFFFF) - 1] == p[q]) r = (en & 0xFFFF) - 1;
       }
     }
-    ldp[jl] = (uint16_t)r;
+    ldp[jl] = (uint16_t)(r | (k[q] == KIND_CLIENT ? X_CLIENT : 0u));
   }
   if (ovf) atomicOr(&counters[C_CERT], CERT_OVF);
   __syncthreads();
@@ -225,31 +223,32 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
     for (int q = 0; q < PT; ++q) {
       const uint32_t i = t0 + q * JTT + threadIdx.x, il = i - w0;
       const bool ok = i < t1;
-      d0[q] = ok ? ldp[il] : L_NONE;
-      act[q] = ok && lkind[il] != KIND_CLIENT;
+      const uint32_t e0 = ok ? ldp[il] : X_NONE;
+      d0[q] = e0 & 0xFFF;
+      act[q] = ok && !(e0 & X_CLIENT);
       j[q] = d0[q];
       cp[q] = NONE;
       hops[q] = 0;
     }
     for (;;) {
       bool any = false;
-      uint8_t kj[PT];
+      uint32_t ej[PT];
 #pragma unroll
-      for (int q = 0; q < PT; ++q) kj[q] = (act[q] && j[q] < JW) ? lkind[j[q]] : 0;
+      for (int q = 0; q < PT; ++q) ej[q] = (act[q] && j[q] < JW) ? ldp[j[q]] : 0;
 #pragma unroll
       for (int q = 0; q < PT; ++q) {
         if (!act[q]) continue;
         if (j[q] >= JW) {  // markers (a compare, not a switch: see Window::next in kmz_part.hip)
-          cp[q] = j[q] == L_NONE ? NONE : PEND;
+          cp[q] = j[q] == X_NONE ? NONE : PEND;
           act[q] = false;
-        } else if (kj[q] != KIND_CLIENT) {
+        } else if (!(ej[q] & X_CLIENT)) {
           cp[q] = w0 + j[q];
           act[q] = false;
         } else if (++hops[q] > MAX_DEPTH) {
           cp[q] = CYC;
           act[q] = false;
         } else {
-          j[q] = ldp[j[q]];
+          j[q] = ej[q] & 0xFFF;
           any = true;
         }
       }
@@ -261,8 +260,8 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
       hv[q] = 0;
       if (i >= t1) continue;
       cparent[i] = cp[q];
-      dp[i] = d0[q] == L_NONE ? NONE : (d0[q] == L_MISS ? MISSV : w0 + d0[q]);
-      miss += d0[q] == L_MISS;
+      dp[i] = d0[q] == X_NONE ? NONE : (d0[q] == X_MISS ? MISSV : w0 + d0[q]);
+      miss += d0[q] == X_MISS;
       pend += cp[q] == PEND;
       const uint64_t key = lsid[i - w0];
       zero += key == 0;
@@ -285,18 +284,19 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   // from per-wave bin counters (LDS atomics with return), or where the LDS
   // has no room for them (2^8 bins) from wave ballots.
   for (uint32_t e = threadIdx.x; e < BINS * NW; e += JTT) wcnt[e] = 0;
-  __syncthreads();  // lbkt free from here on
-  uint64_t *stg = reinterpret_cast<uint64_t *>(lbkt);
+  __syncthreads();  // the hash entries are free from here on
+  uint64_t *stg = reinterpret_cast<uint64_t *>(lidx);
+  static_assert(JB * 16 >= JT * 8, "the hash entries hold the tile's certificate staging");
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1;
   uint32_t rk[PT];
 #if KMZ_RANK_ATOMIC
-  if constexpr (2 * BINS * NW <= (sizeof(lcw) / sizeof(uint32_t))) {
+  if constexpr (2 * BINS * NW <= WCAP) {
     // wave-major counters (a wave's 64 lanes spread over the banks; the
     // order within a bin is immaterial to the certificate), transposed to
     // bin-major for the scan.  The 6 ballots per span this replaces were an
     // eighth of the kernel's VALU instructions.
-    uint32_t *const wmaj = lcw + BINS * NW;
+    uint32_t *const wmaj = wcnt + BINS * NW;
     for (uint32_t e = threadIdx.x; e < BINS * NW; e += JTT) wmaj[e] = 0;
     __syncthreads();
 #pragma unroll

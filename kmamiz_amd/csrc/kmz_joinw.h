@@ -78,6 +78,13 @@ __device__ __forceinline__ uint32_t jb2(uint32_t x) { return (x * 0x85EBCA77u) >
 // compares fingerprints only
 __device__ __forceinline__ uint32_t jfp(uint32_t x) { return max(((x * 0x9E3779B1u) >> 18) & 0xF, 1u); }
 
+// k_join_window's hash: one 32-bit multiply of the folded id; the bucket is
+// its top 10 bits, the 8-bit fingerprint (1..255: an empty slot's byte is 0)
+// the next 8
+__device__ __forceinline__ uint32_t jh8(uint32_t x) { return x * 0x9E3779B1u; }
+__device__ __forceinline__ uint32_t jbk8(uint32_t h) { return h >> 22; }
+__device__ __forceinline__ uint32_t jfp8(uint32_t h) { return max((h >> 14) & 0xFFu, 1u); }
+
 // lanes of this wave whose `v` (B bits) equals mine, among `valid` lanes
 template <int B>
 __device__ __forceinline__ uint64_t match_bits(uint32_t v, uint64_t valid) {
