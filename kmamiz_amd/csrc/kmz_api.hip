@@ -150,7 +150,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -164,6 +164,7 @@ struct kmz_ctx {
   // end of the walk and runs beside the settle (launch_cert_deferred)
   bool cert_defer = false;
   CertPlan cert_pl{};
+  bool k3_late = false;  // the shape-level K3 on the main stream after the chain walk (run_chain_tiles)
   hipEvent_t ev_fork = nullptr, ev_k3 = nullptr, ev_join = nullptr, ev_done = nullptr;
   bool overlap = false;  // this run uses the side stream
 
@@ -1241,6 +1242,8 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     }
   }
   if (int r2 = launch_cert_deferred(c)) return r2;
+  if (c->k3_late && !c->sstats)
+    if (int r2 = run_shape_stats(c)) return r2;
   {
     Timed t(c, KMZ_K_SETTLE);
     launch_chain_settle_list(c->stream, nt, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
@@ -1309,7 +1312,7 @@ static int run_deps(kmz_ctx *c, bool links) {
   if (ensure(c, c->trip, c->tcap * 8) || ensure(c, c->trip_out, c->tcap * 8)) return KMZ_E_HIP;
   if (dups == 0 && !(c->ablate & 16) && !c->walk_once && !c->k4_now && !(c->ablate2 & 256u)) {
     // unique span ids, chain interning: one workgroup per tile (kmz_walk.hip)
-    if (!c->sstats && (r = run_shape_stats(c))) return r;
+    if (!c->sstats && !c->k3_late && (r = run_shape_stats(c))) return r;
     return run_chain_tiles(c, links, joined);
   }
   if (dups == 0 && !(c->ablate & 16) && !c->walk_once) {
@@ -1602,7 +1605,16 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   // (KMZ_ABLATE2 bit 17, for comparison: K3 on the main stream between the
   // join and the walk -- run_deps runs the shape-level K3 before its walk --
   // instead of beside the join on the side stream)
-  const bool k3_mid = smode && (flags & KMZ_RUN_DEPS) && (c->ablate2 & 131072u);
+  // On the chain-tile path K3 runs on the main stream after the walk
+  // (run_chain_tiles), so that the join has the CUs to itself and the
+  // certificate's split, which cannot share a CU with the walk, shares them
+  // with K3 instead: mesh 3.39 -> 3.36 ms (profiles/r05/ab/k3late, wide).
+  // KMZ_ABLATE2 bit 18: beside the join on the side stream, for comparison
+  // (and elsewhere: config 5's direct walk measured 7.58 against 7.44 ms
+  // with K3 on the main stream, profiles/r05/ab/k3mid5)
+  c->k3_late = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate2 & 262144u) && !c->k4_now && !fused_eligible(c) &&
+               !(c->ablate & 16) && !(c->ablate2 & 256u);
+  const bool k3_mid = smode && (flags & KMZ_RUN_DEPS) && ((c->ablate2 & 131072u) || c->k3_late);
   if (c->overlap && !k3_mid) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
