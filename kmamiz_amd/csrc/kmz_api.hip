@@ -155,8 +155,12 @@ struct kmz_ctx {
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
   hipStream_t main = nullptr, side = nullptr;
-  // the certificate's own side stream (from the end of the join: not queued
-  // behind K3 on `side`), its completion event, and whether this run used it
+  // the certificate's side stream: `side` when K3 is not on it this run (the
+  // chain-tile path, K3 after the walk); else a second one, created on first
+  // use (a run's streams stay within HIP's default 4 hardware queues: a
+  // fifth shares one, measured 0.206 against 0.192 ms on Bookinfo), its
+  // completion event, and whether this run used it
+  bool k3_on_side = false;
   hipStream_t side2 = nullptr;
   hipEvent_t ev_cert = nullptr;
   bool cert2 = false;
@@ -345,7 +349,6 @@ kmz_ctx *kmz_create(int device, void *stream) {
     c->own_stream = true;
   }
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_cert, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_k3, hipEventDisableTiming) != hipSuccess ||
@@ -756,6 +759,14 @@ int kmz_json_load(kmz_ctx *c, const uint32_t *shape_of_raw, const uint32_t *stat
   return KMZ_OK;
 }
 
+// the stream the certificate runs on beside the walk (see kmz_ctx::side2);
+// nullptr if the second stream cannot be created
+static hipStream_t cert_stream(kmz_ctx *c) {
+  if (!c->k3_on_side) return c->side;
+  if (!c->side2 && hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess) c->side2 = nullptr;
+  return c->side2;
+}
+
 // The certificate split + check deferred by run_join (a chain table past the
 // MALL, config 5): on side2 from here, i.e. beside the settle's probe-bound
 // k_key_part / k_key_slice instead of between the join and the walk (the
@@ -767,11 +778,13 @@ static int launch_cert_deferred(kmz_ctx *c) {
   const CertPlan &pl = c->cert_pl;
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
+  hipStream_t cs = cert_stream(c);
+  if (!cs) return fail(c, KMZ_E_HIP, "hipStreamCreateWithFlags (certificate stream)");
   HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
-  HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_join, 0));
+  HIPCHK(c, hipStreamWaitEvent(cs, c->ev_join, 0));
   hipStream_t keep = c->stream;
-  c->stream = c->side2;
-  c->cert2 = true;
+  c->stream = cs;
+  c->cert2 = cs == c->side2;
   {
     Timed t(c, KMZ_K_CERT);
     launch_cert_split(c->stream, n, P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), pl,
@@ -866,7 +879,8 @@ static int run_join(kmz_ctx *c, bool *ok) {
     if (cert_side) {  // the certificate checks the join's ids beside the chain walk (read after the run)
       // on a stream of its own, from the end of the join, not behind K3 on
       // the side stream (KMZ_ABLATE2 bit 14: behind it, for comparison)
-      hipStream_t cs = (c->ablate2 & 16384u) ? c->side : c->side2;
+      hipStream_t cs = (c->ablate2 & 16384u) ? c->side : cert_stream(c);
+      if (!cs) return fail(c, KMZ_E_HIP, "hipStreamCreateWithFlags (certificate stream)");
       HIPCHK(c, hipEventRecord(c->ev_join, c->stream));
       HIPCHK(c, hipStreamWaitEvent(cs, c->ev_join, 0));
       c->stream = cs;
@@ -1615,6 +1629,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   c->k3_late = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate2 & 262144u) && !c->k4_now && !fused_eligible(c) &&
                !(c->ablate & 16) && !(c->ablate2 & 256u);
   const bool k3_mid = smode && (flags & KMZ_RUN_DEPS) && ((c->ablate2 & 131072u) || c->k3_late);
+  c->k3_on_side = c->overlap && smode && !k3_mid;
   if (c->overlap && !k3_mid) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
@@ -1637,7 +1652,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     hipStreamIsCapturing(c->main, &cs);
     if (c->overlap && cs == hipStreamCaptureStatusNone) {
       hipStreamSynchronize(c->side);
-      hipStreamSynchronize(c->side2);
+      if (c->side2) hipStreamSynchronize(c->side2);
     }
     return r;
   }
