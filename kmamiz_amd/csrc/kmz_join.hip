@@ -651,7 +651,10 @@ __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__
     const uint32_t b = (uint32_t)h[q] & (CK_NB - 1);
     const uint32_t slot = atomicAdd(&bcnt[b], 1u);
     if (slot < CK_S) {
-      bkt[b * CK_S + slot] = h[q];
+      // slot s of bucket b at position s ^ ((b >> 1) & 7): a bucket's 64 B
+      // cover 16 of the 32 banks a ds_write_b64 group sees, so without the
+      // swizzle the first slots of all buckets land on the same few banks
+      bkt[b * CK_S + (slot ^ ((b >> 1) & 7))] = h[q];
     } else {
       const uint32_t o = atomicAdd(&novf, 1u);
       if (o < CK_OVF) ovf[o] = h[q];
@@ -669,7 +672,7 @@ __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__
     // b+12 of a 16-lane group would hit the same four banks (4-way conflict on
     // every ds_read_b128); rotating each lane's start by b/4 spreads a group
     // over all 64 banks.  (Slot order does not matter to the pair test.)
-    const uint32_t rot = (b >> 2) & 3;
+    const uint32_t rot = (b >> 2) & 3, sw = (b >> 1) & 7;
 #pragma unroll
     for (uint32_t j = 0; j < CK_S; j += 2) {
       const uint32_t jj = (((j >> 1) + rot) & 3) << 1;
@@ -677,10 +680,11 @@ __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__
       x[j] = v.x;
       x[j + 1] = v.y;
     }
-    // (x[] holds the slots in rotated order; slot s of the bucket is valid iff s < c)
+    // (x[] holds the positions in rotated order; position p holds slot p ^ sw,
+    // valid iff that slot < c)
     bool ok[CK_S];
 #pragma unroll
-    for (uint32_t j = 0; j < CK_S; ++j) ok[j] = (((((j >> 1) + rot) & 3) << 1) | (j & 1)) < c;
+    for (uint32_t j = 0; j < CK_S; ++j) ok[j] = ((((((j >> 1) + rot) & 3) << 1) | (j & 1)) ^ sw) < c;
 #pragma unroll
     for (uint32_t i = 0; i < CK_S; ++i)
 #pragma unroll
