@@ -678,6 +678,9 @@ __global__ void __launch_bounds__(256) k3_combine_bal(const unsigned long long *
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
     const uint32_t p = g / K3R, k = g % K3R;
     unsigned long long c = 0, s1 = 0, s2a = 0, s2b = 0, tsx = 0, fst = ~0ull;
+    // (unrolled: a hot partition has many items, and one item's six loads at
+    // a time left the kernel waiting on one round trip per item)
+#pragma unroll 4
     for (uint32_t it = item_off[p]; it < item_off[p + 1]; ++it) {
       const unsigned long long *b = part + (uint64_t)it * K3F * K3R + k;
       c += b[0];
