@@ -1786,15 +1786,16 @@ static int run_attempt(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   // overlap bought <= 3 % or lost (profiles/r01_overlap_ab/); since round 4
   // the VALU-bound join shares the CUs with the memory-bound K3, and the
   // latency-bound walk with the certificate: mesh 3.96 -> 3.76, config 5
-  // 8.56 -> 8.43 ms/step (profiles/r04/ab/overlap/).  Below 2^17 spans (a
+  // 8.56 -> 8.43 ms/step (profiles/r04/ab/overlap/).  Below 2^18 spans (a
   // 2 500-trace tick) the second stream's fork / join costs more than the
   // overlap gives: Bookinfo 164 -> 149 us, mesh 320 -> 300 us per run serial
-  // (tools/bench_tick.py).  While more than one kernel id is timed
+  // (tools/bench_tick.py); config 5's tick (1.4*10^5 spans) 833 -> 805 us per
+  // tick serial (profiles/r05/m3/tick.json).  While more than one kernel id is timed
   // (kmz_set_profiling_mask) runs stay on one stream, so that each kernel's
   // time is its own.  KMZ_ABLATE bit 27 forces the overlap.
   const bool timing_many = c->prof && (c->prof_mask & (c->prof_mask - 1));
   c->overlap = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate & (1u << 25)) &&
-               ((c->n >= (1ull << 17) && !timing_many) || (c->ablate & (1u << 27)));
+               ((c->n >= (1ull << 18) && !timing_many) || (c->ablate & (1u << 27)));
   return run_enqueue_graphed(c, flags, links, h, s64);
 }
 
