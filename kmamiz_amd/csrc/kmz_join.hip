@@ -49,6 +49,16 @@ __device__ unsigned long long g_join_dbg[16];  // diagnostic phase clocks (KMZ_A
 
 // (A persistent form of this kernel, the next tile's window loaded while the
 // current tile contracts and bins, measured 1.62 against 1.18 ms on config 3.)
+// Its window: the tile and KH spans either side.  A parent further out is a
+// MISS (the semi-join), a chain leaving the window PEND (k_pend): slower for
+// those spans, never a different answer.  (KH = 128: mesh 3.328 -> 3.310 ms,
+// config 5 7.31 -> 8.22 ms, its longer traces leaving more parents outside;
+// profiles/r05/ab/halo, halop.)
+#ifndef KMZ_JOIN_HALO
+#define KMZ_JOIN_HALO 256
+#endif
+constexpr uint32_t KH = KMZ_JOIN_HALO, KW = JT + 2 * KH;
+static_assert(KW <= JW, "the window hash is sized for JW slots");
 template <uint32_t B1>
 __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restrict__ sid, const uint64_t *__restrict__ pid,
                                                      const uint8_t *__restrict__ kind, uint32_t n,
@@ -57,7 +67,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
                                                      uint16_t *__restrict__ jdir,
                                                      unsigned int *__restrict__ counters, uint32_t ablate) {
   constexpr uint32_t NW = JTT / 64, BINS = 1u << B1;
-  __shared__ uint64_t lsid[JW];
+  __shared__ uint64_t lsid[KW];
   // the window's LDS hash (kmz_joinw.h jh8): per bucket 8 entries (local
   // index + 1, u16) and their 8-bit fingerprints in one u64, so that a lookup
   // tests all 8 with a few 32-bit operations (a zero-byte test) instead of
@@ -76,15 +86,15 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   // per window slot: its parent's local index (12 bits, or X_NONE / X_MISS)
   // | X_CLIENT when the slot itself is a CLIENT span (no separate kind array:
   // 2.5 KB of LDS, the third workgroup per CU)
-  __shared__ uint16_t ldp[JW];
+  __shared__ uint16_t ldp[KW];
   constexpr uint32_t X_NONE = 0xFFF, X_MISS = 0xFFE, X_CLIENT = 0x8000;
-  static_assert(JW < X_MISS, "local indices stay below the markers");
+  static_assert(KW < X_MISS, "local indices stay below the markers");
   __shared__ uint32_t wsum[NW];
   __shared__ uint32_t stash[JSTASH];  // fingerprint << 16 | local index + 1
   __shared__ uint32_t nstash;
-  constexpr int PW = JW / JTT, PT = JT / JTT;
+  constexpr int PW = (KW + JTT - 1) / JTT, PT = JT / JTT;  // (slots past KW: w0 + jl >= w1)
   const uint32_t t0 = blockIdx.x * JT, t1 = min(n, t0 + JT);
-  const uint32_t w0 = t0 > JH ? t0 - JH : 0, w1 = min(n, t1 + JH);
+  const uint32_t w0 = t0 > KH ? t0 - KH : 0, w1 = min(n, t1 + KH);
   const bool dbg_t = (ablate & (1u << 23)) != 0;
   unsigned long long tprev = 0, tacc[6] = {0, 0, 0, 0, 0, 0};
   KMZ_JSTAMP(0);
@@ -234,11 +244,11 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
       bool any = false;
       uint32_t ej[PT];
 #pragma unroll
-      for (int q = 0; q < PT; ++q) ej[q] = (act[q] && j[q] < JW) ? ldp[j[q]] : 0;
+      for (int q = 0; q < PT; ++q) ej[q] = (act[q] && j[q] < KW) ? ldp[j[q]] : 0;
 #pragma unroll
       for (int q = 0; q < PT; ++q) {
         if (!act[q]) continue;
-        if (j[q] >= JW) {  // markers (a compare, not a switch: see Window::next in kmz_part.hip)
+        if (j[q] >= KW) {  // markers (a compare, not a switch: see Window::next in kmz_part.hip)
           cp[q] = j[q] == X_NONE ? NONE : PEND;
           act[q] = false;
         } else if (!(ej[q] & X_CLIENT)) {
