@@ -150,7 +150,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream)
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream), bit 20 = the run's counters zeroed by hipMemsetAsync (not k_fill)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -1613,7 +1613,17 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   c->chain_ran = false;
   c->cert2 = false;
   c->cert_defer = false;
-  HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4 + S_COUNT * 8, c->stream));
+  // (by our fill kernel, not hipMemsetAsync: the runtime's fill is a blit
+  // kernel that waited behind the previous fetch's device-to-host blit on the
+  // transfer stream, ~0.13 ms at the head of every pipelined step;
+  // KMZ_ABLATE2 bit 20: the runtime's fill, for comparison)
+  if (c->ablate2 & (1u << 20)) {
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4 + S_COUNT * 8, c->stream));
+  } else {
+    FillArgs f;
+    f.add(c->counters.p, C_COUNT * 4 + S_COUNT * 8, 0);
+    launch_fill(c->stream, f);
+  }
   int r;
   c->main = c->stream;
   // (KMZ_ABLATE2 bit 17, for comparison: K3 on the main stream between the

@@ -85,7 +85,10 @@ constexpr uint32_t KB1_MAX = 8, KB2_MAX = 8;
 // the cache they overfill their slice's bucket.
 // (4096 keys measured on config 5: k_key_part + k_key_slice 2.61 -> 2.49 ms,
 // but the direct walk 2.00 -> 2.85 ms)
-constexpr uint32_t KCACHE = 1024;
+#ifndef KMZ_KCACHE
+#define KMZ_KCACHE 1024
+#endif
+constexpr uint32_t KCACHE = KMZ_KCACHE;
 // where the next tile's endpoint gather is issued: 0 after the probes' check
 // (round 3: mesh walk 1.11 -> 1.08 ms, two A/B runs, tools/r03_var.sh), 1
 // before the probes (round 2's choice), 2 at the tile's end (1.09-1.11)
