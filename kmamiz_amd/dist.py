@@ -288,8 +288,11 @@ class IdGuard:
                 with torch.cuda.stream(gs):
                     self.work.wait()
                 self.recv.record_stream(gs)
-                self.engine.id_repeats_seg_begin(self.recv.data_ptr(), self.world, seg, gs.cuda_stream)
-                self.seg_open = True
+                try:
+                    self.engine.id_repeats_seg_begin(self.recv.data_ptr(), self.world, seg, gs.cuda_stream)
+                    self.seg_open = True
+                except Exception:  # noqa: BLE001 (the certificate cannot take it: finish() checks by compaction)
+                    self.seg_open = False
             else:
                 self.pending = send  # (gloo: copied and exchanged in finish)
             return self
@@ -390,7 +393,8 @@ class IdGuard:
             return False
         if self.work is None and self.pending is None and not self.seg_open:
             self.start()
-        if self.fixed is not None and self.engine is not None and self.route_dev is not None:
+        if (self.fixed is not None and self.engine is not None and self.route_dev is not None
+                and (self.seg_open or self.pending is not None)):
             rep, maxc, over = self._seg_verdict()
         else:
             recv, maxc, over = self._received()
