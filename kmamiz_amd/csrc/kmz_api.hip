@@ -2673,7 +2673,7 @@ int kmz_route_ids_fixed(kmz_ctx *c, uint32_t world, uint64_t seg, uint64_t *out,
                       ? launch_route(c->stream, c->sid, n, world, P<uint32_t>(c->rt_hist),
                                      P<unsigned long long>(c->rt_tot), dst, seg)
                       : launch_route_fixed(c->stream, c->sid, n, world, seg, P<unsigned long long>(c->rt_tot), dst);
-  if (!ok) return fail(c, KMZ_E_ARG, "world must be 1..1024");
+  if (!ok) return world > 1024 ? fail(c, KMZ_E_ARG, "world must be 1..1024") : fail(c, KMZ_E_HIP, "kmz_route_ids_fixed launch");
   HIPCHK(c, hipGetLastError());
   if (mem != KMZ_MEM_DEVICE) {  // (host memory: copied back; device memory: enqueued only)
     HIPCHK(c, hipMemcpyAsync(out, dst, words * 8, hipMemcpyDeviceToHost, c->stream));

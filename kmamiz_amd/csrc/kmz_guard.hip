@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(RT_T) k_route_counts(uint32_t world, uint64_t 
 bool launch_route_fixed(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint64_t segw,
                         unsigned long long *cur, unsigned long long *out) {
   if (world == 0 || world > RT_MAXW || segw < 2) return false;
-  hipMemsetAsync(cur, 0, (size_t)world * 8, s);
+  if (hipMemsetAsync(cur, 0, (size_t)world * 8, s) != hipSuccess) return false;
   if (n) hipLaunchKernelGGL(k_route_fixed, dim3((n + RF_CH - 1) / RF_CH), dim3(RT_T), 0, s, sid, n, world, segw, cur, out);
   hipLaunchKernelGGL(k_route_counts, dim3(1), dim3(RT_T), 0, s, world, segw, cur, out);
   return true;
