@@ -169,6 +169,7 @@ struct kmz_ctx {
   bool cert_defer = false;
   CertPlan cert_pl{};
   bool k3_late = false;  // the shape-level K3 on the main stream after the chain walk (run_chain_tiles)
+  bool epp_filled = false;  // this run's endpoint partials were filled with its counters (run_enqueue)
   hipEvent_t ev_fork = nullptr, ev_k3 = nullptr, ev_join = nullptr, ev_done = nullptr;
   bool overlap = false;  // this run uses the side stream
 
@@ -1300,7 +1301,7 @@ static int run_deps(kmz_ctx *c, bool links) {
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned long long *st = P<unsigned long long>(c->stats64);
   unsigned long long *epp = P<unsigned long long>(c->epp);
-  {
+  if (!c->epp_filled) {  // (run_enqueue fills it with the counters)
     Timed t(c, KMZ_K_MEMSET);
     FillArgs f;
     f.add(epp, (size_t)c->n_dep * 8, 0);
@@ -1617,11 +1618,20 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   // kernel that waited behind the previous fetch's device-to-host blit on the
   // transfer stream, ~0.13 ms at the head of every pipelined step;
   // KMZ_ABLATE2 bit 20: the runtime's fill, for comparison)
+  // (with DEPS, the endpoint partials' fill rides in the same launch)
+  c->epp_filled = false;
   if (c->ablate2 & (1u << 20)) {
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, C_COUNT * 4 + S_COUNT * 8, c->stream));
   } else {
     FillArgs f;
     f.add(c->counters.p, C_COUNT * 4 + S_COUNT * 8, 0);
+    if (flags & KMZ_RUN_DEPS) {
+      if (ensure(c, c->epp, (size_t)(c->n_dep + 1) * 16)) return KMZ_E_HIP;
+      unsigned long long *epp = P<unsigned long long>(c->epp);
+      f.add(epp, (size_t)c->n_dep * 8, 0);
+      f.add(epp + c->n_dep, (size_t)c->n_dep * 8, 0xFF);
+      c->epp_filled = true;
+    }
     launch_fill(c->stream, f);
   }
   int r;
@@ -2106,9 +2116,17 @@ int kmz_fetch_begin(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip
   if (eb) {
     if (int r = pinned_staging(c, c->fhep, c->fhep_bytes, eb)) return r;
   }
-  if (gb) HIPCHK(c, hipMemcpyAsync(c->f_grp.p, c->grp_final.p, gb, hipMemcpyDeviceToDevice, c->stream));
-  if (tb) HIPCHK(c, hipMemcpyAsync(c->f_trip.p, c->trip_out.p, tb, hipMemcpyDeviceToDevice, c->stream));
-  if (eb) HIPCHK(c, hipMemcpyAsync(c->f_ep.p, c->epp.p, eb, hipMemcpyDeviceToDevice, c->stream));
+  {  // (one copy kernel; the runtime's copies where a range is not 8-byte aligned)
+    CopyArgs cp;
+    cp.add(c->grp_final.p, c->f_grp.p, gb);
+    cp.add(c->trip_out.p, c->f_trip.p, tb);
+    cp.add(c->epp.p, c->f_ep.p, eb);
+    if (!launch_copy8(c->stream, cp)) {
+      if (gb) HIPCHK(c, hipMemcpyAsync(c->f_grp.p, c->grp_final.p, gb, hipMemcpyDeviceToDevice, c->stream));
+      if (tb) HIPCHK(c, hipMemcpyAsync(c->f_trip.p, c->trip_out.p, tb, hipMemcpyDeviceToDevice, c->stream));
+      if (eb) HIPCHK(c, hipMemcpyAsync(c->f_ep.p, c->epp.p, eb, hipMemcpyDeviceToDevice, c->stream));
+    }
+  }
   HIPCHK(c, hipEventRecord(c->ev_snap, c->stream));
   HIPCHK(c, hipStreamWaitEvent(c->xfer, c->ev_snap, 0));
   // to page-locked host memory by the DMA engines (hipMemcpyDeviceToDeviceNoCU

@@ -68,6 +68,23 @@ struct FillArgs {
   }
 };
 void launch_fill(hipStream_t s, const FillArgs &a);
+// up to 4 device copies (8-byte multiples, 8-byte aligned) in one launch;
+// false (nothing launched) if a range is not
+struct CopyArgs {
+  const void *src[4];
+  void *dst[4];
+  uint64_t bytes[4];
+  uint32_t n = 0;
+  void add(const void *from, void *to, uint64_t nbytes) {
+    if (!nbytes) return;
+    if (n >= 4) __builtin_trap();
+    src[n] = from;
+    dst[n] = to;
+    bytes[n] = nbytes;
+    ++n;
+  }
+};
+bool launch_copy8(hipStream_t s, const CopyArgs &a);
 
 void launch_build(hipStream_t s, const uint64_t *sid, uint32_t n, unsigned long long *table, uint64_t cap,
                   DupEntry *dups, uint32_t dup_cap, unsigned int *counters);

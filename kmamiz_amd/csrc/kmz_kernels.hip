@@ -763,6 +763,30 @@ __global__ void __launch_bounds__(256) k_fill(FillArgs a) {
   }
 }
 
+// up to 4 device-to-device copies of 8-byte-multiple, 8-byte-aligned ranges in
+// one launch (kmz_fetch_begin's snapshot: one launch instead of three blits
+// on the critical path of a pipelined step)
+__global__ void __launch_bounds__(256) k_copy8(CopyArgs a) {
+  const uint32_t k = blockIdx.y;
+  if (k >= a.n) return;
+  const unsigned long long *__restrict__ src = static_cast<const unsigned long long *>(a.src[k]);
+  unsigned long long *__restrict__ dst = static_cast<unsigned long long *>(a.dst[k]);
+  const uint64_t n8 = a.bytes[k] / 8;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+bool launch_copy8(hipStream_t s, const CopyArgs &a) {
+  if (!a.n) return true;
+  uint64_t mx = 0;
+  for (uint32_t k = 0; k < a.n; ++k) {
+    if ((a.bytes[k] | (uintptr_t)a.src[k] | (uintptr_t)a.dst[k]) & 7) return false;
+    mx = std::max<uint64_t>(mx, a.bytes[k]);
+  }
+  const uint32_t gx = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((mx / 8 + 255) / 256, 1024));
+  hipLaunchKernelGGL(k_copy8, dim3(gx, a.n), dim3(256), 0, s, a);
+  return true;
+}
+
 void launch_fill(hipStream_t s, const FillArgs &a) {
   if (!a.n) return;
   uint64_t mx = 0;
