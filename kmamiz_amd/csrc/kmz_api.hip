@@ -112,6 +112,9 @@ struct kmz_ctx {
   bool walk_once = false;   // a K4 wait ran out (F_SPIN): this run is redone on the exact per-row walk
   bool k4_now = false;      // this kmz_run's K4 mode (direct enumeration), decided once per call
   bool dep_valid = false;   // every shape's dependency endpoint is < n_dep (chain elements by shape)
+  uint64_t shape_gen = 0;   // counts shape-table loads (load_shapes)
+  uint64_t alloc_gen = 0;   // counts device allocations (ensure)
+  uint64_t etab_key = 0;    // (shape table, seed, buffer) the walk's gather table cetab holds; 0: none
   // hipGraphs of a whole run for small batches (launch-bound): a run whose
   // launch sequence (kmz_run key) repeats is captured once and replayed
   struct RunGraph {
@@ -225,6 +228,7 @@ int ensure(kmz_ctx *c, DevBuf &b, size_t bytes) {
   hipError_t e = hipMalloc(&b.p, bytes);
   if (e != hipSuccess) return fail(c, KMZ_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
   b.bytes = bytes;
+  ++c->alloc_gen;
   return 0;
 }
 
@@ -445,6 +449,7 @@ static int load_shapes(kmz_ctx *c, const kmz_shapes *sh) {
   c->n_status = sh->n_status;
   // (the walk's chain elements may be shapes -- each maps to one endpoint in
   // range, and a shape id fits an edge key's 24 bits below NONE's)
+  ++c->shape_gen;
   c->dep_valid = sh->n_shapes < 0xFFFFFFu;
   for (uint32_t s = 0; s < sh->n_shapes && c->dep_valid; ++s) c->dep_valid = sh->dep_ep[s] < sh->n_dep_ep;
   size_t b = (size_t)sh->n_shapes * 4;
@@ -766,6 +771,17 @@ static hipStream_t cert_stream(kmz_ctx *c) {
   if (!c->k3_on_side) return c->side;
   if (!c->side2 && hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess) c->side2 = nullptr;
   return c->side2;
+}
+
+// whether cetab already holds this shape table's gather table under this seed
+// (k_chain_etab is then skipped: one launch less per run); marks it as held.
+// Never under run graphs (a replay must not depend on what an earlier run left).
+static bool etab_cached(kmz_ctx *c) {
+  const uint64_t key = (mix64(c->shape_gen * 0x9E3779B97F4A7C15ull ^ c->sig_seed ^ (c->alloc_gen << 40)) ^
+                        (uint64_t)(uintptr_t)c->cetab.p ^ c->n_shapes) | 1;
+  const bool ok = key == c->etab_key && !(c->ablate & (1u << 13));
+  c->etab_key = (c->ablate & (1u << 13)) ? 0 : key;
+  return ok;
 }
 
 // The certificate split + check deferred by run_join (a chain table past the
@@ -1124,7 +1140,7 @@ static int run_fused(kmz_ctx *c, bool links) {
                       (uint32_t)stot, P<unsigned long long>(c->kdefer), (uint32_t)dtot, gpos, (uint32_t)gtot,
                       P<uint4>(c->cetab),
                       // (test knob 24 forces sig collisions on the first seed only)
-                      c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)));
+                      c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)), n > 0 && etab_cached(c));
   }
   // the certificate beside the settle (small batches), as run_join
   const bool cert_side = c->overlap && !(c->ablate & (1u << 26)) && c->ccap * CHAIN_ENTRY_BYTES <= (256ull << 20);
@@ -1400,7 +1416,8 @@ static int run_deps(kmz_ctx *c, bool links) {
                    scap, P<uint32_t>(c->kstage_n), P<unsigned long long>(c->kdefer), dcap, P<uint32_t>(c->kdefer_n),
                    wpos, wcap, P<uint32_t>(c->kwpos_n), P<uint4>(c->cetab), direct,
                    // (test knob 24 forces sig collisions on the first seed only)
-                   c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)), cmode);
+                   c->sig_seed == SIG_SEED0 ? c->ablate : (c->ablate & ~(1u << 24)), cmode,
+                   n > 0 && etab_cached(c));
     }
     if (int r2 = launch_cert_deferred(c)) return r2;
     {

@@ -1008,7 +1008,7 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint32_t pcap, unsigned int *counters, uint32_t *wg_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
                   uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
-                  uint4 *etab, bool direct, uint32_t ablate, bool cmode) {
+                  uint4 *etab, bool direct, uint32_t ablate, bool cmode, bool etab_ok) {
   const uint32_t nt = chain_tiles(n);
   if (!nt) return;
   uint32_t lb1, lb2;
@@ -1019,7 +1019,7 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
   }
   const uint32_t g = chain_grid(n);
   unsigned long long *tab = reinterpret_cast<unsigned long long *>(ctab);
-  launch_chain_etab(s, dep_ep, n_shapes, seed, etab);
+  if (!etab_ok) launch_chain_etab(s, dep_ep, n_shapes, seed, etab);  // (etab_ok: this shape table's, this seed's)
   if (direct)
     hipLaunchKernelGGL(k4_chain<true>, dim3(g), dim3(CTT), 0, s, kind, shape, ts, cparent, n, etab, n_shapes, n_ep,
                        index_base, seed, tab, ccap, trip, tcap, ep_ts, rowpos, plist, pcap, counters, wg_stats, stage,

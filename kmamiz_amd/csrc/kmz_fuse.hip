@@ -443,9 +443,9 @@ void launch_join_chain(hipStream_t s, const uint64_t *sid, const uint64_t *pid, 
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned long long *rowpos,
                        uint32_t *plist, uint32_t pcap, uint32_t *tile_stats, unsigned long long *stage, uint32_t scap,
                        unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap, uint4 *etab,
-                       uint32_t ablate) {
+                       uint32_t ablate, bool etab_ok) {
   if (!n) return;
-  launch_chain_etab(s, dep_ep, n_shapes, seed, etab);
+  if (!etab_ok) launch_chain_etab(s, dep_ep, n_shapes, seed, etab);  // (etab_ok: this shape table's, this seed's)
   hipLaunchKernelGGL(k_join_chain, dim3(join_tiles(n)), dim3(JTT), 0, s, sid, pid, kind, shape, ts, n, etab, n_shapes,
                      n_ep, index_base, seed, cparent, dp, pool1, jdir, counters,
                      reinterpret_cast<unsigned long long *>(ctab), ccap, trip, tcap, ep_ts, rowpos, plist, pcap,

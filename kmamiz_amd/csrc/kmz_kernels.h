@@ -163,7 +163,7 @@ void launch_chain(hipStream_t s, const uint8_t *kind, const uint32_t *shape, con
                   uint32_t pcap, unsigned int *counters, uint32_t *tile_stats, unsigned long long *stats64,
                   unsigned long long *stage, uint32_t scap, uint32_t *stage_n, unsigned long long *defer,
                   uint32_t dcap, uint32_t *defer_n, uint32_t *wpos, uint32_t wcap, uint32_t *wpos_n,
-                  uint4 *etab, bool direct, uint32_t ablate = 0, bool cmode = false);
+                  uint4 *etab, bool direct, uint32_t ablate = 0, bool cmode = false, bool etab_ok = false);
 uint32_t chain_grid(uint32_t n);
 // coarse bins per tile workgroup (2^lb1) and slices per coarse bin (2^lb2) of
 // an edge set of tcap slots; false if tcap is not ESLICE * a power of two
@@ -193,7 +193,7 @@ void launch_join_chain(hipStream_t s, const uint64_t *sid, const uint64_t *pid, 
                        unsigned long long *trip, uint64_t tcap, unsigned long long *ep_ts, unsigned long long *rowpos,
                        uint32_t *plist, uint32_t pcap, uint32_t *tile_stats, unsigned long long *stage, uint32_t scap,
                        unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap, uint4 *etab,
-                       uint32_t ablate = 0);
+                       uint32_t ablate = 0, bool etab_ok = false);
 // (nt: the tile kernel's tiles, whose tile_stats rows are summed)
 void launch_chain_settle_list(hipStream_t s, uint32_t nt, void *ctab, uint64_t ccap, unsigned long long *trip,
                               uint64_t tcap, unsigned int *counters, const uint32_t *tile_stats,
