@@ -625,6 +625,39 @@ def test_sig_collision_is_detected_and_retried(engine, separate):
     assert _info_results(a[2]) == _info_results(b[2])
 
 
+@pytest.mark.parametrize("config,ntr,knob2", [(2, 30000, 0), (3, 4000, 16), (5, 20000, 0), (3, 20000, 0)])
+def test_gather_table_kept_across_runs(config, ntr, knob2):
+    """The walk's per-shape gather table (k_chain_etab) is built once per shape
+    table and seed and kept by later runs of the same engine (kmz_api.hip
+    etab_cached): repeated runs of one loaded batch -- the fused join + walk
+    (config 2), k4_chain (KMZ_ABLATE2 bit 4 at 4000 traces), config 5's
+    direct walk -- equal the C oracle every time; after a reload with another
+    config's shape table the table is rebuilt; under the collision knob the
+    retried seed's table is the one kept."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    def check(e, cfg):
+        batch, _ = synth.host_batch(cfg, 0, ntr)
+        table = synth.shape_table(cfg)
+        okeys, _, ocnt = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+        e.load_synthetic(cfg, synth.SEED, 0, ntr)
+        for _ in range(3):
+            e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+            assert np.array_equal(np.sort(e.triples()), np.sort(okeys))
+            assert e.info()["n_rows"] == ocnt["rows"]
+
+    other = 5 if config != 5 else 2
+    for knob in (0, 1 << 24):
+        e = _engine_with2(knob, knob2)
+        try:
+            check(e, config)
+            check(e, other)  # another shape table on the same engine
+            check(e, config)
+        finally:
+            e.close()
+
+
 SPIN_TINY_DEFER = 1 << 10  # KMZ_ABLATE: 4 deferred chain checks per workgroup (in-place chain_put waits)
 SPIN_NO_WAIT = 1 << 11     # KMZ_ABLATE: every chain-table wait "runs out" at once (F_SPIN)
 FORCE_INTERNING = 1 << 29  # KMZ_ABLATE: K4 chain interning even where auto mode would enumerate
