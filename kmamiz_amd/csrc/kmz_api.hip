@@ -153,7 +153,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream), bit 20 = the run's counters zeroed by hipMemsetAsync (not k_fill)
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream), bit 20 = the run's counters zeroed by hipMemsetAsync (not k_fill), bit 21 = on the direct walk, K3 beside the join on the side stream (not from the end of the walk, beside the settle)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -171,6 +171,9 @@ struct kmz_ctx {
   // end of the walk and runs beside the settle (launch_cert_deferred)
   bool cert_defer = false;
   CertPlan cert_pl{};
+  bool k3_settle = false;  // K3 on the side stream from the end of the direct walk (run_enqueue)
+  bool k3_ran = false;     // ... and it has been enqueued
+  uint32_t k3_mode = 0;    // this run's K3 mode (run_stats)
   bool k3_late = false;  // the shape-level K3 on the main stream after the chain walk (run_chain_tiles)
   bool epp_filled = false;  // this run's endpoint partials were filled with its counters (run_enqueue)
   hipEvent_t ev_fork = nullptr, ev_k3 = nullptr, ev_join = nullptr, ev_done = nullptr;
@@ -961,6 +964,8 @@ static int run_table(kmz_ctx *c) {
 
 // K3 once per batch over (shape x status); every grouping the path needs is a
 // union of these groups (k_collapse_groups / k_collapse_endpoints).
+static int run_stats(kmz_ctx *c, uint32_t mode);
+
 static int run_shape_stats(kmz_ctx *c) {
   const uint32_t n = (uint32_t)c->n;
   const uint64_t Gs = (uint64_t)c->n_shapes * c->n_status;
@@ -1348,7 +1353,7 @@ static int run_deps(kmz_ctx *c, bool links) {
   }
   if (dups == 0 && !(c->ablate & 16) && !c->walk_once) {
     // unique span ids: rows are the SERVER spans; chain interning (kmz_chain.hip)
-    if (!c->sstats && (r = run_shape_stats(c))) return r;
+    if (!c->sstats && !c->k3_settle && (r = run_shape_stats(c))) return r;
     const uint32_t nt = chain_tiles(n);
     const bool direct = c->k4_now;
     // per persistent workgroup: staged keys (of candidate new chains, or of
@@ -1420,6 +1425,16 @@ static int run_deps(kmz_ctx *c, bool links) {
                    n > 0 && etab_cached(c));
     }
     if (int r2 = launch_cert_deferred(c)) return r2;
+    if (c->k3_settle) {  // K3 beside the settle (run_enqueue)
+      HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+      HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      c->stream = c->side;
+      const int r2 = run_stats(c, c->k3_mode);
+      c->stream = c->main;
+      if (r2) return r2;
+      HIPCHK(c, hipEventRecord(c->ev_k3, c->side));
+      c->k3_ran = true;
+    }
     {
       Timed t(c, KMZ_K_SETTLE);
       launch_chain_settle(c->stream, n, direct, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
@@ -1665,7 +1680,15 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
   // with K3 on the main stream, profiles/r05/ab/k3mid5)
   c->k3_late = smode && (flags & KMZ_RUN_DEPS) && !(c->ablate2 & 262144u) && !c->k4_now && !fused_eligible(c) &&
                !(c->ablate & 16) && !(c->ablate2 & 256u);
-  const bool k3_mid = smode && (flags & KMZ_RUN_DEPS) && ((c->ablate2 & 131072u) || c->k3_late);
+  // On the direct walk (config 5) K3 runs on the side stream from the end of
+  // the walk, beside the settle, so that the join has the CUs to itself:
+  // 7.28-7.31 -> 7.15-7.19 ms (profiles/r05/ab/k3s, k3s2; KMZ_ABLATE2 bit 21:
+  // beside the join, for comparison)
+  c->k3_settle = c->overlap && smode && (flags & KMZ_RUN_DEPS) && !(c->ablate2 & (1u << 21)) && !c->k3_late &&
+                 c->k4_now && !fused_eligible(c) && !(c->ablate & 16);
+  c->k3_ran = false;
+  c->k3_mode = smode;
+  const bool k3_mid = smode && (flags & KMZ_RUN_DEPS) && ((c->ablate2 & 131072u) || c->k3_late || c->k3_settle);
   c->k3_on_side = c->overlap && smode && !k3_mid;
   if (c->overlap && !k3_mid) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
@@ -1694,7 +1717,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     return r;
   }
   if ((r = launch_cert_deferred(c))) return r;  // (a path with no walk after the join)
-  if (k3_mid && (r = run_stats(c, smode))) return r;  // (its shape level ran inside run_deps)
+  if (k3_mid && !c->k3_ran && (r = run_stats(c, smode))) return r;  // (its shape level ran inside run_deps)
   if (c->overlap) {  // everything queued on the side stream, before the read-back
     HIPCHK(c, hipEventRecord(c->ev_done, c->side));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_done, 0));
