@@ -112,7 +112,8 @@ struct kmz_ctx {
   bool walk_once = false;   // a K4 wait ran out (F_SPIN): this run is redone on the exact per-row walk
   bool k4_now = false;      // this kmz_run's K4 mode (direct enumeration), decided once per call
   bool dep_valid = false;   // every shape's dependency endpoint is < n_dep (chain elements by shape)
-  uint64_t shape_gen = 0;   // counts shape-table loads (load_shapes)
+  uint64_t shape_gen = 0;   // counts shape tables whose dependency endpoints differ from the last (load_shapes)
+  std::vector<uint32_t> dep_host;  // the last table's dependency endpoints
   uint64_t alloc_gen = 0;   // counts device allocations (ensure)
   uint64_t etab_key = 0;    // (shape table, seed, buffer) the walk's gather table cetab holds; 0: none
   // hipGraphs of a whole run for small batches (launch-bound): a run whose
@@ -204,7 +205,10 @@ struct kmz_ctx {
 namespace {
 
 int fail(kmz_ctx *c, int code, const std::string &msg) {
-  if (c) c->err = msg;
+  if (c) {
+    c->err = msg;
+    c->etab_key = 0;  // (after any failure the walk's gather table is rebuilt)
+  }
   return code;
 }
 
@@ -452,7 +456,13 @@ static int load_shapes(kmz_ctx *c, const kmz_shapes *sh) {
   c->n_status = sh->n_status;
   // (the walk's chain elements may be shapes -- each maps to one endpoint in
   // range, and a shape id fits an edge key's 24 bits below NONE's)
-  ++c->shape_gen;
+  // (a reload of the same dependency endpoints -- every kmz_load of a realtime
+  // tick -- keeps the walk's gather table, etab_cached)
+  if (c->dep_host.size() != sh->n_shapes ||
+      (sh->n_shapes && memcmp(c->dep_host.data(), sh->dep_ep, (size_t)sh->n_shapes * 4) != 0)) {
+    c->dep_host.assign(sh->dep_ep, sh->dep_ep + sh->n_shapes);
+    ++c->shape_gen;
+  }
   c->dep_valid = sh->n_shapes < 0xFFFFFFu;
   for (uint32_t s = 0; s < sh->n_shapes && c->dep_valid; ++s) c->dep_valid = sh->dep_ep[s] < sh->n_dep_ep;
   size_t b = (size_t)sh->n_shapes * 4;
