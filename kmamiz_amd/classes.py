@@ -725,7 +725,18 @@ class EndpointDependencies:
     def service_tail(self, labelMap: Optional[Dict[str, str]] = None):
         """Scale form of the service-level tail (tail.ServiceTail) of the
         reduced graph ``EndpointDependencies([]).combineWith(self).trim()``,
-        computed on the GPU from the edge keys (kmz_tail_run)."""
+        computed on the GPU from the edge keys (kmz_tail_run).
+
+        Side effect with DEPRECATED_ENDPOINT_THRESHOLD set: the filtered edge
+        keys and endpoint partials are written into the engine that holds the
+        run (kmz_set_triples, kmz_partials_copy), so the engine no longer holds
+        the unfiltered run.  Results already taken from the run (rows,
+        reduced(), toReduced(): host copies) are unaffected; a later call that
+        needs the device state -- another result's service_tail(), this one
+        unfiltered included -- sees the moved ``gen`` and runs the batch's
+        dependency pass again first (correct, at the cost of one pass).  Only
+        the stale endpoints' first-row half is cleared: the tail reads rows
+        (has_row, first row) and never a last-usage timestamp."""
         from .tail import maps_from_dictionary, run_tail
 
         if self._native is None:

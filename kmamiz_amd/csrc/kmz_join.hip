@@ -71,10 +71,15 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   // the window's LDS hash (kmz_joinw.h jh8): per bucket 8 entries (local
   // index + 1, u16) and their 8-bit fingerprints in one u64, so that a lookup
   // tests all 8 with a few 32-bit operations (a zero-byte test) instead of
-  // decoding 16 packed entries; fill counts four per word (a bucket past 255
-  // ids -- repeated ids only -- spills into its neighbour's count: that only
-  // costs lookups, which compare whole ids, a miss, resolved by the
-  // semi-join).  After the lookups
+  // decoding 16 packed entries; fill counts are bytes, four per word.  A
+  // bucket's count wraps past 255 ids (its carry lands in the neighbour's
+  // byte), and an insert that then reads 0..7 would write a slot already
+  // written -- two threads could leave a fingerprint of one id beside the
+  // index of another.  No tile ever answers from such a table: 256 ids in one
+  // bucket put >= 248 of them past its 8 slots, i.e. past the 64-entry stash,
+  // which sets `ovf` (CERT_OVF): the run is redone on the table path.  (Below the
+  // wrap, a lookup compares whole ids, so a fingerprint collision only costs
+  // a further candidate.)  After the lookups
   // the entries become the certificate's staging and the fingerprints its
   // per-wave bin counters (pass 1)
   __shared__ uint4 lidx[JB];

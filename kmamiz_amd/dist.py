@@ -205,7 +205,8 @@ def route_ids_np(span_ids: np.ndarray, world: int):
 
 
 # agreed fixed-segment size of IdGuard's exchange per (group, world): set on
-# every rank from the same all-reduced maximum in IdGuard.finish
+# every rank from the same all-reduced maximum in IdGuard.finish; each entry
+# keeps its group object (IdGuard._seg_size)
 _ID_SEG: dict = {}
 # per device: the stream IdGuard's certificate runs on (it waits for the
 # exchange there, beside the rank's own run)
@@ -245,24 +246,47 @@ class IdGuard:
     checked, so a repeat inside one shard is found too: a run covered by a
     guard may skip its own certificate (KMZ_RUN_NO_CERT)."""
 
-    def __init__(self, engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None):
+    def __init__(self, engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None, *,
+                 world: Optional[int] = None, backend: Optional[str] = None):
+        # (world / backend: given only by a single-process test that stands in
+        # for the collectives, _a2a and _agree; otherwise the group's)
         self.engine, self.group, self.span_ids = engine, group, span_ids
-        self.world = dist.get_world_size(group)
+        self.world = world if world is not None else dist.get_world_size(group)
+        backend = backend if backend is not None else dist.get_backend(group)
         # device tensors under RCCL; host tensors under gloo (its all-to-all is CPU-only)
         self.on_dev = (engine is not None and dev is not None and torch.device(dev).type == "cuda"
-                       and dist.get_backend(group) == "nccl")
+                       and backend == "nccl")
         self.dev = torch.device(dev) if self.on_dev else torch.device("cpu")
         # (gloo with the engine on a GPU: the routing is still enqueued on the device)
         self.route_dev = (torch.device(dev) if engine is not None and dev is not None
                           and torch.device(dev).type == "cuda" else None)
-        self.key = (id(group) if group is not None else None, self.world)
+        self.gobj = group if group is not None or world is not None else dist.distributed_c10d._get_default_group()
         self.work = self.fixed = self.pending = None
         self.seg_open = False  # kmz_id_repeats_seg_begin enqueued, not yet ended
+
+    # the guard's collectives (a single-process test overrides both)
+    def _a2a(self, out, inp, out_splits=None, in_splits=None, async_op=False):
+        return dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                      group=self.group, async_op=async_op)
+
+    def _agree(self, flag: torch.Tensor) -> None:
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+
+    def _seg_size(self) -> Optional[int]:
+        """The segment size every rank agreed on in this group's last finish(),
+        or None (no finish() yet: the counts protocol).  The entry holds the
+        group object itself and is used only while that very object is the
+        group, so a destroyed group whose id() a new group reuses, or a
+        re-initialised default group, starts over with the counts protocol on
+        every rank (ranks that disagreed here would post different
+        all-to-alls and hang under RCCL)."""
+        e = _ID_SEG.get((id(self.gobj), self.world))
+        return e[1] if e is not None and e[0] is self.gobj else None
 
     def start(self) -> "IdGuard":
         if self.world == 1:
             return self
-        seg = _ID_SEG.get(self.key) if self.engine is not None else None
+        seg = self._seg_size() if self.engine is not None else None
         if seg is not None:
             self.fixed = seg
             if self.route_dev is not None:  # enqueued on the engine's stream, no wait
@@ -280,7 +304,7 @@ class IdGuard:
             if self.on_dev:
                 self.recv = torch.empty_like(send)
                 self.send = send
-                self.work = dist.all_to_all_single(self.recv, send, group=self.group, async_op=True)
+                self.work = self._a2a(self.recv, send, async_op=True)
                 # the certificate over the segments as they arrive, on the
                 # guard's stream behind the exchange (no host wait): it runs
                 # beside this rank's run, finish() reads its verdict
@@ -312,14 +336,13 @@ class IdGuard:
             counts = c.tolist()
         cnt = torch.tensor(counts, dtype=torch.int64, device=self.dev)
         rcnt = torch.empty_like(cnt)
-        dist.all_to_all_single(rcnt, cnt, group=self.group)
+        self._a2a(rcnt, cnt)
         rc = rcnt.tolist()
         self.recv = torch.empty(max(1, sum(rc)), dtype=torch.int64, device=self.dev)
         self.m = sum(rc)
         self.maxc = max(rc) if rc else 0
         self.send = send  # (kept alive until the exchange is done)
-        self.work = dist.all_to_all_single(self.recv[: self.m], send, output_split_sizes=rc, input_split_sizes=counts,
-                                           group=self.group, async_op=True)
+        self.work = self._a2a(self.recv[: self.m], send, rc, counts, async_op=True)
         return self
 
     def abandon(self) -> None:
@@ -334,7 +357,7 @@ class IdGuard:
             if self.route_dev is not None:
                 self.engine.sync()
             send = self.pending.cpu()
-            dist.all_to_all_single(torch.empty_like(send), send, group=self.group)
+            self._a2a(torch.empty_like(send), send)
         self.work = self.send = self.recv = self.pending = None
 
     def _received(self):
@@ -350,7 +373,7 @@ class IdGuard:
             send = self.pending.cpu()
             self.pending = None
             self.recv = torch.empty_like(send)
-            dist.all_to_all_single(self.recv, send, group=self.group)
+            self._a2a(self.recv, send)
         else:
             self.work.wait()
         r = self.recv.view(self.world, seg)
@@ -372,12 +395,19 @@ class IdGuard:
             send = self.pending.cpu()
             self.pending = None
             recv = torch.empty_like(send)
-            dist.all_to_all_single(recv, send, group=self.group)
+            self._a2a(recv, send)
             self.recv = recv.to(self.route_dev)
-            self.engine.id_repeats_seg_begin(self.recv.data_ptr(), self.world, seg,
-                                             torch.cuda.current_stream(self.route_dev).cuda_stream)
-        self.seg_open = False
-        rep, maxc = self.engine.id_repeats_seg_end()
+            try:
+                self.engine.id_repeats_seg_begin(self.recv.data_ptr(), self.world, seg,
+                                                 torch.cuda.current_stream(self.route_dev).cuda_stream)
+                self.seg_open = True
+            except Exception:  # noqa: BLE001 (the certificate cannot take it: compaction below, and every rank still agrees)
+                self.seg_open = False
+        if self.seg_open:
+            self.seg_open = False
+            rep, maxc = self.engine.id_repeats_seg_end()
+        else:
+            rep, maxc = None, int(self.recv.view(self.world, seg)[:, 0].max().item())
         over = maxc >= seg
         if rep is None and not over:  # the certificate could not decide: compact and check on the host
             r = self.recv.view(self.world, seg)
@@ -409,11 +439,11 @@ class IdGuard:
         # one MAX all-reduce: the verdict, any overflow, the largest count (the
         # next step's segment size, the same on every rank)
         flag = torch.tensor([1 if rep else 0, 1 if over else 0, maxc], dtype=torch.int64, device=self.dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        self._agree(flag)
         f = flag.tolist()
         self.work = self.send = self.recv = None
         if self.engine is not None:
-            _ID_SEG[self.key] = int(f[2] * 1.125) + 1025
+            _ID_SEG[(id(self.gobj), self.world)] = (self.gobj, int(f[2] * 1.125) + 1025)
         if f[1]:  # a segment overflowed somewhere: this step exactly, every rank
             self._start_counts()
             return self.finish(raise_)

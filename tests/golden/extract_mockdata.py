@@ -45,6 +45,7 @@ const Utils = {{ ObjectToInterfaceString: (o) => "__schema__" + JSON.stringify(o
 WANT = {
     "MockData.ts": [
         "MockTrace",
+        "MockEndpointDependencies",
         "MockTracePDAS",
         "MockRlDataPDAS",
         "MockEndpointDependenciesPDAS",

@@ -22,6 +22,7 @@ import os
 import shutil
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import ROOT
@@ -82,6 +83,25 @@ class Pinned:
         settings.set_clock(None)
         O.DEPRECATED_THRESHOLD_MS = 0
         O.DATE_NOW = None
+
+
+class Unfiltered:
+    """Inside a Pinned block: DEPRECATED_ENDPOINT_THRESHOLD unset for the
+    oracle and the product alike, restored on exit (the clock stays)."""
+
+    def __enter__(self):
+        from kmamiz_amd import settings
+
+        self.ms = O.DEPRECATED_THRESHOLD_MS
+        settings.set_deprecated_threshold(None)
+        O.DEPRECATED_THRESHOLD_MS = 0
+        return self
+
+    def __exit__(self, *exc):
+        from kmamiz_amd import settings
+
+        settings.set_deprecated_threshold(THRESHOLD)
+        O.DEPRECATED_THRESHOLD_MS = self.ms
 
 
 def _row(name, last, by=(), on=()):
@@ -332,4 +352,17 @@ def test_gpu_service_tail_with_filter(engine):
             stale_seen += len(red) < len(O.strip_undef(O.Traces(copy.deepcopy(w)).toEndpointDependencies().toJSON()))
             # the filtered edge set replaced the run's: a second call runs the pass again, same answer
             assert win.service_tail().instability() == inst, k
+            # an unfiltered consumer of the same run after the
+            # filtered tail (the engine's state moved): the unfiltered graph's
+            # tail and reduced form, as the oracle computes them unfiltered
+            with Unfiltered():
+                from kmamiz_amd.classes import EndpointDependencies
+
+                unf = EndpointDependencies(_native=win._native)
+                ured = O.strip_undef(O.EndpointDependencies([]).combineWith(
+                    O.Traces(copy.deepcopy(w)).toEndpointDependencies()).trim().toJSON())
+                uod = O.EndpointDependencies(ured)
+                assert unf.service_tail().instability() == uod.toServiceInstability(), k
+                assert unf.service_tail().coupling() == uod.toServiceCoupling(), k
+                assert np.array_equal(np.sort(unf.reduced()[0]), np.sort(win._native.triples)), k
     assert stale_seen > 0

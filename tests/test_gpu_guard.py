@@ -121,9 +121,10 @@ def _guard_worker(rank, world, port, q, dev_kind):
             if rep and rank == world - 1:
                 batch.span_id[len(batch) - 1] = b0.span_id[5]
             e.load(batch, synth.shape_table(synth.MESH))
-            if tiny:
-                kdist._ID_SEG[(None, world)] = 4
-            g = kdist.IdGuard(e, dev).start()
+            g = kdist.IdGuard(e, dev)
+            if tiny:  # (the agreed size, forced: the entry keeps its group object)
+                kdist._ID_SEG[(id(g.gobj), world)] = (g.gobj, 4)
+            g.start()
             fixed = g.fixed is not None
             got = g.finish(raise_=False)
             out.append((fixed, got))
@@ -224,3 +225,112 @@ def test_no_cert_run_equals_certified_run(engine):
     assert g0.tobytes() == g1.tobytes()
     assert np.array_equal(np.sort(k0), np.sort(k1))
     assert e0.tobytes() == e1.tobytes()
+
+
+class _LoopGuard:
+    """IdGuard's RCCL branch (dist.py IdGuard.start: device routing, the
+    all-to-all posted behind it, the segment certificate on the guard's stream
+    waiting for the exchange) on one process: the all-to-all is stood in for
+    by a copy of the routed segments on a stream of its own -- optionally
+    appending the first value of segment ``inject[0]`` to segment
+    ``inject[1]``, as if another source had sent it too -- and the MAX
+    all-reduce by the identity.  Built as a subclass at call time (the module
+    imports torch.distributed lazily)."""
+
+    @staticmethod
+    def make(engine, inject=None):
+        from kmamiz_amd import dist as kdist
+
+        class G(kdist.IdGuard):
+            def __init__(self):
+                super().__init__(engine, torch.device("cuda", 0), world=2, backend="nccl")
+                self.inject = inject
+                self.xs = torch.cuda.Stream()
+
+            def _a2a(self, out, inp, out_splits=None, in_splits=None, async_op=False):
+                self.xs.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.xs):
+                    out.copy_(inp)  # (identity: this rank's segments stand in for what the sources sent)
+                    if self.inject is not None and out_splits is None and self.fixed is not None:
+                        r = out.view(self.world, self.fixed)
+                        a, b = self.inject
+                        pos = (r[b, 0] + 1).clamp(max=self.fixed - 1).view(1)
+                        r[b].index_copy_(0, pos, r[a, 1].view(1))
+                        r[b, 0] += 1
+                ev = torch.cuda.Event()
+                ev.record(self.xs)
+                inp.record_stream(self.xs)
+                out.record_stream(self.xs)
+
+                class Work:
+                    def wait(self):
+                        torch.cuda.current_stream().wait_event(ev)
+
+                w = Work()
+                if not async_op:
+                    w.wait()
+                return w
+
+            def _agree(self, flag):
+                pass
+
+        return G()
+
+
+def test_id_guard_device_wiring_single_process():
+    """the RCCL branch of IdGuard.start/finish as the multi-GPU
+    bench wires it (one explicit stream for torch and the engine, the run
+    without its own certificate beside the guard), on one process: the first
+    step exchanges counts, later ones fixed segments whose certificate is
+    enqueued on the guard stream (seg_open); a repeat inside the shard and one
+    across two sources' segments are found, clean steps pass, and when
+    kmz_id_repeats_seg_begin fails start() falls back to finish()'s
+    compaction check with the same verdicts."""
+    from kmamiz_amd import Engine
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import dist as kdist
+    from kmamiz_amd import synth
+
+    stream = torch.cuda.Stream()
+    prev = torch.cuda.current_stream()
+    torch.cuda.set_stream(stream)
+    e = Engine(0, stream=stream.cuda_stream)
+    try:
+        table = synth.shape_table(synth.MESH)
+        kdist._ID_SEG.pop((id(None), 2), None)  # (this process's stand-in group: no agreed size yet)
+        clean, _ = synth.host_batch(synth.MESH, 0, 3000)
+        rep_in, _ = synth.host_batch(synth.MESH, 0, 3000)
+        rep_in.span_id[len(rep_in) - 1] = rep_in.span_id[5]
+
+        def step(batch, inject=None, fail_seg=False):
+            e.load(batch, table)
+            g = _LoopGuard.make(e, inject)
+            if fail_seg:
+                def boom(*a, **k):
+                    raise RuntimeError("KMZ_E_UNSUPPORTED (test)")
+                e.id_repeats_seg_begin = boom
+            try:
+                g.start()
+                e.run(L.RUN_STATS_TAG | L.RUN_DEPS | L.RUN_NO_CERT)  # beside the guard, as the bench runs
+                opened = g.seg_open
+                fixed = g.fixed is not None
+                got = g.finish(raise_=False)
+            finally:
+                if fail_seg:
+                    del e.id_repeats_seg_begin
+            return fixed, opened, got
+
+        assert step(clean) == (False, False, False)  # first step: counts protocol
+        assert step(clean) == (True, True, False)  # fixed segments, certificate on the guard stream
+        assert step(rep_in) == (True, True, True)  # a repeat inside this shard
+        assert step(clean, inject=(0, 1)) == (True, True, True)  # one value from two sources
+        assert step(clean, inject=(1, 0)) == (True, True, True)
+        assert step(clean) == (True, True, False)
+        # kmz_id_repeats_seg_begin failing: start() leaves it closed, finish() compacts
+        assert step(clean, fail_seg=True) == (True, False, False)
+        assert step(rep_in, fail_seg=True) == (True, False, True)
+        assert step(clean, inject=(0, 1), fail_seg=True) == (True, False, True)
+        assert step(clean) == (True, True, False)
+    finally:
+        e.close()
+        torch.cuda.set_stream(prev)
