@@ -146,7 +146,7 @@ typedef struct kmz_info {
                            bit 3 k_walk redo after a chain-table wait ran out (F_SPIN),
                            bit 4 join and chain walk fused in one kernel (k_join_chain),
                            bit 5 chain interning by one workgroup per tile (k4_tile; else
-                           the persistent k4_chain) */
+                           the persistent k4_chain), bit 6 that tile kernel is k4_tile9 */
   uint64_t n_chains;    /* distinct interned ancestor chains (chain-interning path) */
 } kmz_info;
 

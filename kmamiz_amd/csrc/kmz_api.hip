@@ -154,7 +154,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream), bit 20 = the run's counters zeroed by hipMemsetAsync (not k_fill), bit 21 = on the direct walk, K3 beside the join on the side stream (not from the end of the walk, beside the settle)
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream), bit 20 = the run's counters zeroed by hipMemsetAsync (not k_fill), bit 21 = on the direct walk, K3 beside the join on the side stream (not from the end of the walk, beside the settle), bit 22 = chain interning on k4_tile8 (not k4_tile9)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -1247,6 +1247,9 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
   }
   c->ctab_dirty = true;  // until this run's slots are cleared below
   const bool w8 = !(c->ablate2 & 1024u), by_shape = w8 && c->dep_valid && !(c->ablate2 & 2048u);
+  // k4_tile9 where the ids fit its 19-bit record field (KMZ_ABLATE2 bit 22:
+  // k4_tile8, for comparison)
+  const bool w9 = w8 && !(c->ablate2 & (1u << 22)) && chain_tile9_fits(by_shape ? c->n_shapes : c->n_dep);
   {
     ChainRun a;
     a.ts = c->ts;
@@ -1279,7 +1282,10 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     a.n_ids = c->n_shapes;
     {
       Timed t(c, KMZ_K_WALK);
-      if (w8)
+      if (w9)
+        launch_chain_tile9(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
+                           c->n_shapes, P<uint32_t>(c->ctile), a);
+      else if (w8)
         launch_chain_tile8(c->stream, c->kind, c->shape, P<uint32_t>(c->cparent), n, P<uint32_t>(c->d_dep),
                            c->n_shapes, P<uint32_t>(c->ctile), a);
       else
@@ -1314,7 +1320,7 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     launch_chain_clear_list(c->stream, c->ctab.p, gpos, (uint32_t)gtot, cnt);
   }
   c->ctab_dirty = false;  // (set again after the run if the list overflowed: F_CTAB_DIRTY)
-  c->path = (joined ? 1 : 0) | 2 | 32;
+  c->path = (joined ? 1 : 0) | 2 | 32 | (w9 ? 64 : 0);
   c->chain_ran = true;
   c->k4_direct_ran = false;
   c->k4_lb1 = 0;

@@ -210,6 +210,12 @@ void launch_chain_tile(hipStream_t s, const uint8_t *kind, const uint32_t *shape
 // dependency table maps every shape into range) or by endpoint (gathered)
 void launch_chain_tile8(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint32_t *cparent, uint32_t n,
                         const uint32_t *dep_ep, uint32_t n_shapes, uint32_t *tile_stats, const ChainRun &a);
+// k4_tile9 (round 6): k4_tile8's chains with the element hashes kept in LDS
+// and sentinel-terminated walks; ids (shapes, or gathered endpoints) below
+// 2^19 - 1 (chain_tile9_fits)
+bool chain_tile9_fits(uint32_t n_ids);
+void launch_chain_tile9(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint32_t *cparent, uint32_t n,
+                        const uint32_t *dep_ep, uint32_t n_shapes, uint32_t *tile_stats, const ChainRun &a);
 // zero the chain-table entries this run wrote (instead of a memset of the table)
 void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
                         const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);

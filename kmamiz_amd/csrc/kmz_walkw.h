@@ -101,6 +101,179 @@ struct Rec8 {  // (the id: a shape, or an endpoint)
   }
 };
 
+// a window slot as the leaders' key staging reads it: its id (endpoint or
+// shape; NONE for none), kind and window parent
+struct AncRec {
+  uint32_t ep, kind, parent;
+};
+
+// The probe, check, leaders and row counts of one round, after the walk
+// (shared by the walk kernels).  Per walker slot q: st (S_PUT: probe the chain
+// sg with parent sig ps; S_PEND: its ancestry leaves the window; S_DONE:
+// nothing to probe), kq (KIND_CLIENT: an empty walker slot), the depth dd, the
+// window slot jq and the id myep; anc(x) gives window slot x's AncRec.
+template <int NT, int TW, class Anc>
+__device__ __forceinline__ void chain_round_tail(uint64_t (&sg)[TW], const uint64_t (&ps)[TW], uint8_t (&st)[TW],
+                                                 const uint8_t (&kq)[TW], const uint32_t (&dd)[TW],
+                                                 const uint32_t (&jq)[TW], const uint32_t (&myep)[TW], uint32_t w0,
+                                                 Anc anc, ChainLds &L, const ChainRun &a, uint32_t &rows,
+                                                 uint32_t &rel, uint32_t &maxd, uint32_t &fresh_n, uint32_t &flags) {
+  const uint32_t spin = spin_bound(a.ablate);
+  ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
+  uint64_t pos[TW];
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    const bool pr = st[q] == S_PUT;
+    pos[q] = pr ? cslot(sg[q], a.ccap) : 0;
+    w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]) : make_ulonglong2(0, 0);
+  }
+  // check what the probes found; one leader per distinct unknown sig
+  uint32_t hslot[TW];
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    hslot[q] = IMAP + 1;  // not an insert
+    if (st[q] != S_PUT) continue;
+    for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
+      pos[q] = pos[q] + 1 == a.ccap ? 0 : pos[q] + 1;
+      w01[q] = *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
+    }
+    st[q] = S_DONE;
+    if (w01[q].x == sg[q] && w01[q].y != 0) {
+      if (w01[q].y != ps[q]) flags |= F_SIG;
+      continue;
+    }
+    uint32_t h = (uint32_t)(sig_place(sg[q]) >> 32) & (IMAP - 1);
+    hslot[q] = IMAP;  // a leader without a map slot (map full)
+    for (uint32_t t = 0; t < 8; ++t) {
+      const unsigned long long kk = atomicCAS(&L.imap_sig[h], 0ull, (unsigned long long)sg[q]);
+      if (kk == 0) {
+        L.imap_psig[h] = ps[q];
+        hslot[q] = h;
+        break;
+      }
+      if (kk == sg[q]) {
+        hslot[q] = h | 0x80000000u;
+        break;
+      }
+      h = (h + 1) & (IMAP - 1);
+    }
+  }
+  if (a.ablate & (1u << 18))  // diagnostic knob: probe but no inserts
+#pragma unroll
+    for (int q = 0; q < TW; ++q) hslot[q] = IMAP + 1;
+  __syncthreads();
+  // followers compare with their leader; leaders claim the probed slot (one
+  // CAS) and publish at once (a lane that waits on another workgroup's
+  // unpublished entry must never hold back, in its own wave, a publish that
+  // workgroup may wait on).  Their list entries are reserved in LDS, then in
+  // the global lists with one atomic per list and workgroup.
+  unsigned long long cvq[TW];
+  uint32_t os[TW], ol[TW];
+  bool lead[TW];
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    lead[q] = false;
+    os[q] = ol[q] = 0;
+    cvq[q] = 0;
+    if (hslot[q] > IMAP) {
+      if (hslot[q] != IMAP + 1) {
+        const uint32_t h = hslot[q] & (IMAP - 1);
+        if (L.imap_psig[h] != ps[q]) flags |= F_SIG;
+      }
+      continue;
+    }
+    lead[q] = true;
+    unsigned long long *en = a.ctab + 2 * pos[q];
+    cvq[q] = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
+    if (cvq[q] == 0) atomicExch(&en[1], (unsigned long long)ps[q]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  bool anyl = false;
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    if (!lead[q]) continue;
+    anyl = true;
+    // a row whose chain this leader inserted (or lost to another chain: the
+    // deferred check may insert it) stages its keys; one that joined the
+    // same chain leaves them to the winner (knob 19: diagnostic, none)
+    if (kq[q] == KIND_SERVER && dd[q] && cvq[q] != sg[q] && !(a.ablate & (1u << 19)))
+      os[q] = atomicAdd(&L.l_need[0], dd[q]) + 1;
+    ol[q] = atomicAdd(&L.l_need[cvq[q] == 0 ? 1 : 2], 1u);
+  }
+  if (__syncthreads_or(anyl)) {
+    if (threadIdx.x < 3) {
+      const uint32_t need = L.l_need[threadIdx.x];
+      L.l_base[threadIdx.x] =
+          need ? atomicAdd(&a.counters[threadIdx.x == 0 ? C_FSTAGE : (threadIdx.x == 1 ? C_WPOS : C_FDEFER)], need)
+               : 0;
+      L.l_need[threadIdx.x] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < TW; ++q) {
+      if (!lead[q]) continue;
+      const uint32_t d = dd[q];
+      if (os[q]) {  // the row's keys (ancestor k, row endpoint, k, ancestor is SERVER)
+        const uint64_t base = (uint64_t)L.l_base[0] + os[q] - 1;
+        // (shape ids: the keys are staged over shapes and mapped to
+        // endpoints by k_chain_settle_list -- no gather in the walk)
+        uint32_t an = anc(jq[q]).parent;
+        for (uint32_t kk = 1; kk <= d; ++kk) {
+          const AncRec r = anc(an);
+          const uint64_t key = edge_key(r.ep, myep[q], kk, r.kind == KIND_SERVER);
+          if (base + kk - 1 < a.scap) {
+            a.stage[base + kk - 1] = key;
+          } else {
+            edge_insert(a.id_ep ? key_ids_to_eps(key, a.id_ep, a.n_ids) : key, a.trip, a.tcap, &flags);
+            flags |= F_STAGE_FULL;
+          }
+          an = r.parent;
+        }
+      }
+      if (cvq[q] == 0) {  // won the slot (published above)
+        ++fresh_n;
+        const uint64_t x = (uint64_t)L.l_base[1] + ol[q];
+        if (x < a.gcap)
+          a.gpos[x] = (uint32_t)pos[q];
+        else
+          flags |= F_CTAB_DIRTY;
+      } else {  // joined an unpublished entry, or lost the slot to another chain
+        const uint64_t x = (uint64_t)L.l_base[2] + ol[q];
+        if (x < a.dcap) {
+          *reinterpret_cast<ulonglong2 *>(a.defer + 2 * x) = make_ulonglong2(sg[q], ps[q]);
+        } else {
+          int rr = 0;
+          for (uint32_t t = 0; t < spin && rr == 0; ++t)
+            rr = chain_put(a.ctab, a.ccap, sg[q], ps[q], &flags, a.gpos, a.gcap, a.counters);
+          if (rr == 0) flags |= F_SPIN;  // unchecked: the run is redone on the exact walk
+          fresh_n += rr == 1;
+        }
+      }
+    }
+  }
+  // per walker: row counts, pending list, rowpos
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    if (kq[q] == KIND_CLIENT) continue;  // (an empty walker slot)
+    const uint32_t i = w0 + jq[q];
+    const bool pending = st[q] == S_PEND;
+    uint64_t rp = NONE64;
+    if (kq[q] == KIND_SERVER) {
+      rp = a.index_base + i;
+      if (!pending) {
+        ++rows;
+        rel += dd[q];
+        maxd = max(maxd, dd[q]);
+      }
+    }
+    if (pending) {
+      const uint32_t x = atomicAdd(&a.counters[C_PLIST], 1u);
+      if (x < a.pcap) a.plist[x] = i;
+    }
+    if (a.rowpos_out) a.rowpos_out[i] = rp;
+  }
+}
+
 // All rounds of one tile.  W: window slots (an index >= W is not a window
 // slot); NT: threads of the workgroup; TW: walkers per thread and round; R:
 // the record layout.  The caller has published lrec / wlist / m with a
@@ -112,7 +285,6 @@ __device__ __forceinline__ void chain_walk_rounds(const typename R::T *__restric
                                                   uint32_t &rows, uint32_t &rel, uint32_t &maxd, uint32_t &fresh_n,
                                                   uint32_t &flags) {
   using RT = typename R::T;
-  const uint32_t spin = spin_bound(a.ablate);
   const bool hash_on = !(a.ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
   for (uint32_t r0 = 0; r0 < m; r0 += TW * NT) {
     uint64_t sg[TW], ps[TW], acc[TW];
@@ -198,159 +370,10 @@ __device__ __forceinline__ void chain_walk_rounds(const typename R::T *__restric
       }
       if (!(a.ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
-    ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
-    uint64_t pos[TW];
-#pragma unroll
-    for (int q = 0; q < TW; ++q) {
-      const bool pr = st[q] == S_PUT;
-      pos[q] = pr ? cslot(sg[q], a.ccap) : 0;
-      w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]) : make_ulonglong2(0, 0);
-    }
-    // check what the probes found; one leader per distinct unknown sig
-    uint32_t hslot[TW];
-#pragma unroll
-    for (int q = 0; q < TW; ++q) {
-      hslot[q] = IMAP + 1;  // not an insert
-      if (st[q] != S_PUT) continue;
-      for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
-        pos[q] = pos[q] + 1 == a.ccap ? 0 : pos[q] + 1;
-        w01[q] = *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
-      }
-      st[q] = S_DONE;
-      if (w01[q].x == sg[q] && w01[q].y != 0) {
-        if (w01[q].y != ps[q]) flags |= F_SIG;
-        continue;
-      }
-      uint32_t h = (uint32_t)(sig_place(sg[q]) >> 32) & (IMAP - 1);
-      hslot[q] = IMAP;  // a leader without a map slot (map full)
-      for (uint32_t t = 0; t < 8; ++t) {
-        const unsigned long long kk = atomicCAS(&L.imap_sig[h], 0ull, (unsigned long long)sg[q]);
-        if (kk == 0) {
-          L.imap_psig[h] = ps[q];
-          hslot[q] = h;
-          break;
-        }
-        if (kk == sg[q]) {
-          hslot[q] = h | 0x80000000u;
-          break;
-        }
-        h = (h + 1) & (IMAP - 1);
-      }
-    }
-    if (a.ablate & (1u << 18))  // diagnostic knob: probe but no inserts
-#pragma unroll
-      for (int q = 0; q < TW; ++q) hslot[q] = IMAP + 1;
-    __syncthreads();
-    // followers compare with their leader; leaders claim the probed slot (one
-    // CAS) and publish at once (a lane that waits on another workgroup's
-    // unpublished entry must never hold back, in its own wave, a publish that
-    // workgroup may wait on).  Their list entries are reserved in LDS, then in
-    // the global lists with one atomic per list and workgroup.
-    unsigned long long cvq[TW];
-    uint32_t os[TW], ol[TW];
-    bool lead[TW];
-#pragma unroll
-    for (int q = 0; q < TW; ++q) {
-      lead[q] = false;
-      os[q] = ol[q] = 0;
-      cvq[q] = 0;
-      if (hslot[q] > IMAP) {
-        if (hslot[q] != IMAP + 1) {
-          const uint32_t h = hslot[q] & (IMAP - 1);
-          if (L.imap_psig[h] != ps[q]) flags |= F_SIG;
-        }
-        continue;
-      }
-      lead[q] = true;
-      unsigned long long *en = a.ctab + 2 * pos[q];
-      cvq[q] = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
-      if (cvq[q] == 0) atomicExch(&en[1], (unsigned long long)ps[q]);
-    }
-    __builtin_amdgcn_wave_barrier();
-    bool anyl = false;
-#pragma unroll
-    for (int q = 0; q < TW; ++q) {
-      if (!lead[q]) continue;
-      anyl = true;
-      // a row whose chain this leader inserted (or lost to another chain: the
-      // deferred check may insert it) stages its keys; one that joined the
-      // same chain leaves them to the winner (knob 19: diagnostic, none)
-      if (kq[q] == KIND_SERVER && dd[q] && cvq[q] != sg[q] && !(a.ablate & (1u << 19)))
-        os[q] = atomicAdd(&L.l_need[0], dd[q]) + 1;
-      ol[q] = atomicAdd(&L.l_need[cvq[q] == 0 ? 1 : 2], 1u);
-    }
-    if (__syncthreads_or(anyl)) {
-      if (threadIdx.x < 3) {
-        const uint32_t need = L.l_need[threadIdx.x];
-        L.l_base[threadIdx.x] =
-            need ? atomicAdd(&a.counters[threadIdx.x == 0 ? C_FSTAGE : (threadIdx.x == 1 ? C_WPOS : C_FDEFER)], need)
-                 : 0;
-        L.l_need[threadIdx.x] = 0;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int q = 0; q < TW; ++q) {
-        if (!lead[q]) continue;
-        const uint32_t d = dd[q];
-        if (os[q]) {  // the row's keys (ancestor k, row endpoint, k, ancestor is SERVER)
-          const uint64_t base = (uint64_t)L.l_base[0] + os[q] - 1;
-          // (shape ids: the keys are staged over shapes and mapped to
-          // endpoints by k_chain_settle_list -- no gather in the walk)
-          uint32_t an = R::parent(lrec[jq[q]]);
-          for (uint32_t kk = 1; kk <= d; ++kk) {
-            const RT r = lrec[an];
-            const uint64_t key = edge_key(R::ep(r), myep[q], kk, R::kind(r) == KIND_SERVER);
-            if (base + kk - 1 < a.scap) {
-              a.stage[base + kk - 1] = key;
-            } else {
-              edge_insert(a.id_ep ? key_ids_to_eps(key, a.id_ep, a.n_ids) : key, a.trip, a.tcap, &flags);
-              flags |= F_STAGE_FULL;
-            }
-            an = R::parent(r);
-          }
-        }
-        if (cvq[q] == 0) {  // won the slot (published above)
-          ++fresh_n;
-          const uint64_t x = (uint64_t)L.l_base[1] + ol[q];
-          if (x < a.gcap)
-            a.gpos[x] = (uint32_t)pos[q];
-          else
-            flags |= F_CTAB_DIRTY;
-        } else {  // joined an unpublished entry, or lost the slot to another chain
-          const uint64_t x = (uint64_t)L.l_base[2] + ol[q];
-          if (x < a.dcap) {
-            *reinterpret_cast<ulonglong2 *>(a.defer + 2 * x) = make_ulonglong2(sg[q], ps[q]);
-          } else {
-            int rr = 0;
-            for (uint32_t t = 0; t < spin && rr == 0; ++t)
-              rr = chain_put(a.ctab, a.ccap, sg[q], ps[q], &flags, a.gpos, a.gcap, a.counters);
-            if (rr == 0) flags |= F_SPIN;  // unchecked: the run is redone on the exact walk
-            fresh_n += rr == 1;
-          }
-        }
-      }
-    }
-    // per walker: row counts, pending list, rowpos
-#pragma unroll
-    for (int q = 0; q < TW; ++q) {
-      if (kq[q] == KIND_CLIENT) continue;  // (an empty walker slot)
-      const uint32_t i = w0 + jq[q];
-      const bool pending = st[q] == S_PEND;
-      uint64_t rp = NONE64;
-      if (kq[q] == KIND_SERVER) {
-        rp = a.index_base + i;
-        if (!pending) {
-          ++rows;
-          rel += dd[q];
-          maxd = max(maxd, dd[q]);
-        }
-      }
-      if (pending) {
-        const uint32_t x = atomicAdd(&a.counters[C_PLIST], 1u);
-        if (x < a.pcap) a.plist[x] = i;
-      }
-      if (a.rowpos_out) a.rowpos_out[i] = rp;
-    }
+    chain_round_tail<NT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
+      const RT r = lrec[x];
+      return AncRec{R::ep(r), R::kind(r), R::parent(r)};
+    }, L, a, rows, rel, maxd, fresh_n, flags);
     __syncthreads();  // (wlist / imap reads of this round before the next round's leaders)
   }
 }

@@ -319,6 +319,49 @@ def test_chain_elements_by_shape_with_shared_endpoints(engine, ntr):
     assert by_shape["n_chains"] > by_ep["n_chains"] > 0
 
 
+@pytest.mark.parametrize("config,ntr,variant", [(2, 30000, "plain"), (3, 4000, "plain"), (3, 40000, "plain"),
+                                                (3, 40000, "by_endpoint"), (3, 20000, "other_kinds"),
+                                                (5, 2000, "plain"), (5, 20000, "plain"), (5, 6000, "other_kinds")])
+def test_tile9_equals_tile8_and_oracle(config, ntr, variant):
+    """k4_tile9 (element hashes in LDS, sentinel-terminated walks, kmz_walk.hip)
+    against k4_tile8 (KMZ_ABLATE2 bit 22) and the C oracle: the same rows,
+    relations, depths, edge keys, endpoints and interned chains.  Variants:
+    chain elements by endpoint (KMZ_ABLATE2 bit 11: the gathered ids), and
+    5 % of the spans turned into kind-0 spans (neither SERVER nor CLIENT: the
+    walk's lastUsage branch, Traces.ts:192-208).  Chain interning forced and
+    the fused kernel off, so that the tile kernels run at every size."""
+    from kmamiz_amd import Engine
+    from kmamiz_amd import synth
+    from kmamiz_amd.engine import SpanBatch
+
+    batch, _ = synth.host_batch(config, 0, ntr)
+    table = synth.shape_table(config)
+    if variant == "other_kinds":
+        kind = batch.kind.copy()
+        rng = np.random.default_rng(9)
+        kind[(rng.random(len(kind)) < 0.05) & (kind == 1)] = 0
+        batch = SpanBatch(batch.span_id, batch.parent_id, kind, batch.shape, batch.status, batch.duration,
+                          batch.timestamp, batch.index_base)
+    odeps = c_oracle.deps(batch, table.dep_ep, table.n_dep_ep)
+    base2 = (1 << 4) | ((1 << 11) if variant == "by_endpoint" else 0)
+    out = []
+    for bits2 in (base2, base2 | (1 << 22)):
+        os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"] = str(1 << 29), str(bits2)
+        try:
+            e = Engine(0)
+        finally:
+            del os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"]
+        try:
+            info = _compare_synth(e, batch, table, odeps)
+            out.append((info, e.triples().copy(), e.endpoints().tobytes()))
+        finally:
+            e.close()
+    (i9, k9, p9), (i8, k8, p8) = out
+    assert i9["path"] & 96 == 96 and i8["path"] & 96 == 32  # k4_tile9, then k4_tile8
+    assert np.array_equal(k9, k8) and p9 == p8
+    assert i9["n_chains"] == i8["n_chains"] > 0
+
+
 def test_chain_elements_by_endpoint_when_a_shape_is_out_of_range(engine):
     """A dependency table with an entry past n_dep (a shape no span uses) keeps
     the walk on endpoint elements (gathered per slot): same results as the

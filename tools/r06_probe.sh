@@ -1,17 +1,30 @@
 #!/bin/bash
-# Round-6 first probe on the box: (a) k4_tile8's VALU / SALU / LDS instructions
-# per wave under the phase knobs (KMZ_ABLATE bit 16: window + row counts only;
-# bit 17: + walk and sigs; bit 18: + probes, no inserts; 0: all), config 3 at
-# 10^8 spans; (b) rocprofv3 kernel traces of the realtime tick (Bookinfo and
-# mesh, direct and graphed); (c) tools/bench_tick.py.
+# Round-6 GPU cycle: (1) the GPU suite (messy batches deselected); (2) mesh
+# bench A/B, k4_tile9 (default) against k4_tile8 (KMZ_ABLATE2 bit 22);
+# (3) the walk's instruction counters per wave for both, under the phase knobs
+# (KMZ_ABLATE bit 16: window + row counts only; bit 17: + walk and sigs; 0:
+# all), config 3 at 10^8 spans; (4) rocprofv3 kernel traces of the realtime
+# tick (Bookinfo and mesh, direct and graphed) and tools/bench_tick.py.
+# usage: tools/r06_probe.sh [skip-tests]
 set -o pipefail
 export TMPDIR=/tmp
 D=gpurun_out/r06probe
 mkdir -p $D
-for a in 0 65536 131072 262144; do
-  KMZ_ABLATE=$a timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-    --kernel-include-regex "k4_tile8" --kernel-trace --output-format csv -d $D/knob_$a -o walk -- \
-    python3 tools/ab/ablate.py child 3650000 > $D/knob_$a.log 2>&1 || exit 1
+if [ "$1" != skip-tests ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+    --deselect tests/test_gpu_parity.py::test_messy_batches_vs_oracle > $D/tests.log 2>&1
+  rc=$?
+  tail -3 $D/tests.log
+  [ $rc -eq 0 ] || exit 1
+fi
+bash tools/ab/ab_env.sh w9 "--steps 10 --warmup 3" 2 t9=base t8=base:KMZ_ABLATE2=4194304 || exit 1
+python3 tools/ab/abread.py gpurun_out/ab_w9
+for v in 0 4194304; do
+  for a in 0 65536 131072; do
+    KMZ_ABLATE=$a KMZ_ABLATE2=$v timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+      --kernel-include-regex "k4_tile" --kernel-trace --output-format csv -d $D/knob_${v}_$a -o walk -- \
+      python3 tools/ab/ablate.py child 3650000 > $D/knob_${v}_$a.log 2>&1 || exit 1
+  done
 done
 for c in bookinfo mesh; do
   for m in direct graph; do
