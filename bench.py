@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 #   stats  k3_produce     K3 (read ep/status/kind/dur/ts)       19 B/span
 #   reduce k3_reduce      K3 second pass: the partitioned records it must
 #                         read (dur 4 + ts 8 + key/index 4)      16 B/SERVER span
-#   walk   k4_tile8       K4 traversal (k4_tile, k4_chain: knobs / direct)  12 B/relation
+#   walk   k4_tile9       K4 traversal (k4_tile8, k4_tile, k4_chain: knobs / direct)  12 B/relation
 #   cert   k_cert_split   uniqueness certificate: one radix split of the
 #                         8-B hashed span id (read + write)      16 B/span
 #   check  k_cert_check   certificate check: one read of it       8 B/span
@@ -402,9 +402,11 @@ def main():
     # certificate's and the reduce's extra passes are overhead, not 8d work
     pipe_bytes = (57 + 19) * n_local + 12 * A
     overhead = {k: per_kernel[k]["alg_bytes"] for k in ("cert", "check", "reduce", "tail") if k in per_kernel}
-    # (the walk: k4_tile8 for chain interning, kmz_info.path bit 5 -- k4_tile
-    # with KMZ_ABLATE2 bit 10; the persistent k4_chain otherwise)
-    tile = "k4_tile" if int(os.environ.get("KMZ_ABLATE2", "0"), 0) & 1024 else "k4_tile8"
+    # (the walk: k4_tile9 for chain interning, kmz_info.path bits 5 + 6 --
+    # k4_tile8 with KMZ_ABLATE2 bit 22, k4_tile with bit 10; the persistent
+    # k4_chain otherwise)
+    tile = ("k4_tile" if int(os.environ.get("KMZ_ABLATE2", "0"), 0) & 1024
+            else ("k4_tile9" if info.get("path", 0) & 64 else "k4_tile8"))
     kname = {"join": "k_join_window", "stats": "k3_produce" if "reduce" in per_kernel else "k_stats",
              "reduce": "k3_reduce_bal", "walk": tile if info.get("path", 0) & 32 else "k4_chain",
              "cert": "k_cert_split", "check": "k_cert_check", "tail": "k_tail_part", "joinwalk": "k_join_chain"}[dom]

@@ -638,6 +638,57 @@ constexpr int CK_PER = 6144 / CCT;          // ids per thread: sub-bins <= CCT *
 static_assert(CCT * CK_PER >= CERT_SET * 3 / 4, "a sub-bin must fit the workgroup's registers");
 // (A persistent form that loads the next sub-bin's ids while checking the
 // current one measured slower: 0.31 against 0.275 ms on config 3.)
+#ifndef KMZ_CK_CAS
+#define KMZ_CK_CAS 0
+#endif
+#if KMZ_CK_CAS
+// (variant) the same check as an open-addressing LDS set: each id claims
+// the first free slot from its home (the hash's low 13 bits) by an LDS
+// compare-and-swap; finding itself there is a repeat.  8192 slots for at most
+// 6144 ids: a free slot always exists, so every probe sequence ends.
+constexpr uint32_t CK_SET = 8192;
+__global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__restrict__ pool, uint32_t cap,
+                                                   const unsigned int *__restrict__ cur, uint32_t cur_stride,
+                                                   unsigned int *__restrict__ counters) {
+  __shared__ unsigned long long tab[CK_SET];
+  const uint32_t sb = blockIdx.x;
+  const uint32_t m = min(cur[(uint64_t)sb * cur_stride], cap);
+  if (m == 0) return;
+  const unsigned long long *src = pool + (uint64_t)sb * cap;
+  uint64_t h[CK_PER];
+#pragma unroll
+  for (int q = 0; q < CK_PER; ++q) {  // every load in flight while the set is cleared
+    const uint32_t e = q * CCT + threadIdx.x;
+    h[q] = e < m ? src[e] : 0;
+  }
+  for (uint32_t k = threadIdx.x; k < CK_SET / 2; k += CCT) reinterpret_cast<ulonglong2 *>(tab)[k] = make_ulonglong2(0, 0);
+  __syncthreads();
+  bool dup = false, lost = m > CCT * CK_PER;
+  uint32_t pos[CK_PER];
+  bool live[CK_PER];
+#pragma unroll
+  for (int q = 0; q < CK_PER; ++q) {
+    pos[q] = (uint32_t)h[q] & (CK_SET - 1);
+    live[q] = h[q] != 0;  // padding (and cert_hash(0) == 0: span id 0, reported as F_ZERO_ID)
+  }
+  // the thread's ids in lockstep: one CAS each per step, all in flight together
+  for (uint32_t z = 0; z < CK_SET; ++z) {
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < CK_PER; ++q) {
+      if (!live[q]) continue;
+      const unsigned long long o = atomicCAS(&tab[pos[q]], 0ull, (unsigned long long)h[q]);
+      dup |= o == h[q];
+      live[q] = o != 0 && o != h[q];
+      pos[q] = (pos[q] + 1) & (CK_SET - 1);
+      any |= live[q];
+    }
+    if (!any) break;
+  }
+  if (dup) atomicOr(&counters[C_CERT], CERT_DUP);
+  if (lost) atomicOr(&counters[C_CERT], CERT_OVF);
+}
+#else
 __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__restrict__ pool, uint32_t cap,
                                                    const unsigned int *__restrict__ cur, uint32_t cur_stride,
                                                    unsigned int *__restrict__ counters) {
@@ -717,6 +768,7 @@ __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__
   if (dup) atomicOr(&counters[C_CERT], CERT_DUP);
   if (lost) atomicOr(&counters[C_CERT], CERT_OVF);
 }
+#endif
 
 // ---- MISS parents: semi-join of the missing parent ids against all span ids
 __device__ __forceinline__ uint64_t mslot(uint64_t key, uint32_t mcap) { return slot_of(key ^ 0x7F4A7C159E3779B9ull, mcap); }

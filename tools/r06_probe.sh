@@ -19,6 +19,16 @@ if [ "$1" != skip-tests ]; then
 fi
 bash tools/ab/ab_env.sh w9 "--steps 10 --warmup 3" 2 t9=base t8=base:KMZ_ABLATE2=4194304 || exit 1
 python3 tools/ab/abread.py gpurun_out/ab_w9
+# the certificate check as an LDS compare-and-swap set (libkmz_ckcas.so, -DKMZ_CK_CAS=1)
+KMZ_LIB_VARIANT=ckcas timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_guard.py -m gpu -x -q \
+  --timeout 200 --timeout-method thread -p no:cacheprovider \
+  -k "certificate or repeated or id_repeats or structured or synthetic_vs or seg or guard" > $D/tests_ckcas.log 2>&1
+rc=$?
+tail -2 $D/tests_ckcas.log
+if [ $rc -eq 0 ]; then
+  bash tools/ab/ab_env.sh ck "--steps 10 --warmup 3" 2 t9=base ckcas=ckcas || exit 1
+  python3 tools/ab/abread.py gpurun_out/ab_ck
+fi
 for v in 0 4194304; do
   for a in 0 65536 131072; do
     KMZ_ABLATE=$a KMZ_ABLATE2=$v timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
