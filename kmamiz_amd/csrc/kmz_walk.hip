@@ -230,6 +230,146 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #ifndef KMZ_TILE9_WAVES
 #define KMZ_TILE9_WAVES 7
 #endif
+
+// k4_tile9's probe / claim / lists (against chain_round_tail: fewer dependent
+// round trips per workgroup).  A walker whose probe finds its chain checks
+// the parent sig; one that finds the home slot empty claims it with one CAS
+// (no LDS leader map: two walkers of a workgroup with the same new chain,
+// 0.4 % of them, both CAS and the second defers); the winner publishes its
+// parent sig and stages its keys.  Its list entries are placed by an LDS add
+// in the workgroup's own region of each list (WG_STAGE keys, WG_POS claimed
+// slots: no device atomic and no barrier between the claim and the writes);
+// past the region a device atomic reserves them in the global list.  A claim
+// that lost the slot, or a chain found unpublished, goes to the deferred
+// checks (global list, as before).  need[0] / need[1]: the workgroup's key /
+// claim counts so far (its region holds the first ones).
+template <int NT, int TW, class Anc>
+__device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint64_t (&ps)[TW], uint8_t (&st)[TW],
+                                                  const uint8_t (&kq)[TW], const uint32_t (&dd)[TW],
+                                                  const uint32_t (&jq)[TW], const uint32_t (&myep)[TW], uint32_t w0,
+                                                  Anc anc, uint32_t *need, const ChainRun &a, uint32_t &rows,
+                                                  uint32_t &rel, uint32_t &maxd, uint32_t &fresh_n, uint32_t &flags) {
+  const uint32_t spin = spin_bound(a.ablate);
+  ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
+  uint64_t pos[TW];
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    const bool pr = st[q] == S_PUT;
+    pos[q] = pr ? cslot(sg[q], a.ccap) : 0;
+    w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]) : make_ulonglong2(0, 0);
+  }
+  bool lead[TW], dfr[TW];
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    lead[q] = dfr[q] = false;
+    if (st[q] != S_PUT) continue;
+    for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
+      pos[q] = pos[q] + 1 == a.ccap ? 0 : pos[q] + 1;
+      w01[q] = *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
+    }
+    st[q] = S_DONE;
+    if (w01[q].x == sg[q]) {
+      if (w01[q].y == 0)
+        dfr[q] = true;  // found, not yet published: checked by the settle
+      else if (w01[q].y != ps[q])
+        flags |= F_SIG;
+      continue;
+    }
+    if (a.ablate & (1u << 18)) continue;  // diagnostic knob: probe but no inserts
+    lead[q] = true;  // an empty slot (or PROBE_MAX other chains: the CAS fails, the settle inserts)
+  }
+  // the claims, all in flight together; a winner publishes at once
+  unsigned long long cvq[TW];
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    cvq[q] = 0;
+    if (!lead[q]) continue;
+    unsigned long long *en = a.ctab + 2 * pos[q];
+    cvq[q] = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
+    if (cvq[q] == 0) atomicExch(&en[1], (unsigned long long)ps[q]);
+  }
+  const uint32_t blk = blockIdx.x;
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    if (!lead[q] && !dfr[q]) continue;
+    const uint32_t d = dd[q];
+    if (lead[q] && cvq[q] == 0) {  // won the slot: it is cleared after the run
+      ++fresh_n;
+      const uint32_t o = atomicAdd(&need[1], 1u);
+      if (o < WG_POS) {
+        a.wgpos[(uint64_t)blk * WG_POS + o] = (uint32_t)pos[q];
+      } else {
+        const uint32_t x = atomicAdd(&a.counters[C_WPOS], 1u);
+        if (x < a.gcap)
+          a.gpos[x] = (uint32_t)pos[q];
+        else
+          flags |= F_CTAB_DIRTY;
+      }
+    }
+    // a row whose chain this walker inserted (or lost to another chain: the
+    // deferred check may insert it) stages its keys (ancestor k, row id, k,
+    // ancestor is SERVER); one that joined the same chain leaves them to the
+    // winner (knob 19: diagnostic, none)
+    if (lead[q] && kq[q] == KIND_SERVER && d && cvq[q] != sg[q] && !(a.ablate & (1u << 19))) {
+      const uint32_t o = atomicAdd(&need[0], d);
+      unsigned long long *dst;
+      uint64_t cap;
+      if (o + d <= WG_STAGE) {
+        dst = a.wstage + (uint64_t)blk * WG_STAGE + o;
+        cap = d;
+      } else {
+        const uint32_t b = atomicAdd(&a.counters[C_FSTAGE], d);
+        dst = a.stage + b;
+        cap = b < a.scap ? a.scap - b : 0;
+      }
+      uint32_t an = anc(jq[q]).parent;
+      for (uint32_t kk = 1; kk <= d; ++kk) {
+        const AncRec r = anc(an);
+        const uint64_t key = edge_key(r.ep, myep[q], kk, r.kind == KIND_SERVER);
+        if (kk - 1 < cap) {
+          dst[kk - 1] = key;
+        } else {
+          edge_insert(a.id_ep ? key_ids_to_eps(key, a.id_ep, a.n_ids) : key, a.trip, a.tcap, &flags);
+          flags |= F_STAGE_FULL;
+        }
+        an = r.parent;
+      }
+    }
+    if (dfr[q] || cvq[q] != 0) {  // found unpublished, joined an unpublished claim, or lost the slot
+      const uint32_t x = atomicAdd(&a.counters[C_FDEFER], 1u);
+      if (x < a.dcap) {
+        *reinterpret_cast<ulonglong2 *>(a.defer + 2 * (uint64_t)x) = make_ulonglong2(sg[q], ps[q]);
+      } else {
+        int rr = 0;
+        for (uint32_t t = 0; t < spin && rr == 0; ++t)
+          rr = chain_put(a.ctab, a.ccap, sg[q], ps[q], &flags, a.gpos, a.gcap, a.counters);
+        if (rr == 0) flags |= F_SPIN;  // unchecked: the run is redone on the exact walk
+        fresh_n += rr == 1;
+      }
+    }
+  }
+  // per walker: row counts, pending list, rowpos
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    if (kq[q] == KIND_CLIENT) continue;  // (an empty walker slot)
+    const uint32_t i = w0 + jq[q];
+    const bool pending = st[q] == S_PEND;
+    uint64_t rp = NONE64;
+    if (kq[q] == KIND_SERVER) {
+      rp = a.index_base + i;
+      if (!pending) {
+        ++rows;
+        rel += dd[q];
+        maxd = max(maxd, dd[q]);
+      }
+    }
+    if (pending) {
+      const uint32_t x = atomicAdd(&a.counters[C_PLIST], 1u);
+      if (x < a.pcap) a.plist[x] = i;
+    }
+    if (a.rowpos_out) a.rowpos_out[i] = rp;
+  }
+}
 template <bool BY_SHAPE>
 __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *__restrict__ kind,
                                                                  const uint32_t *__restrict__ shape,
@@ -240,7 +380,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   __shared__ uint64_t lel[W9];  // element hash (0 on the sentinels)
   __shared__ uint32_t lpk[W9];  // window parent | kind << 11 | id << 13
   __shared__ uint16_t wlist[WT];
-  __shared__ ChainLds L;
+  __shared__ uint32_t need[2];  // the workgroup's staged keys and claimed slots (chain_round_tail9)
   __shared__ uint32_t wcnt[WPT][NW];
   __shared__ uint32_t red[NW][4];
   const uint32_t t0 = blockIdx.x * WT, t1 = min(n, t0 + WT);
@@ -260,7 +400,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     k[q] = kw[j];
     e[q] = sw[j];
   }
-  chain_lds_init(L);
+  if (threadIdx.x < 2) need[threadIdx.x] = 0;
   if (threadIdx.x < 3) {
     lpk[WW + threadIdx.x] = (WW + threadIdx.x) | ((uint32_t)KIND_CLIENT << P9_BITS) | (ID9_NONE << (P9_BITS + 2));
     lel[WW + threadIdx.x] = 0;
@@ -399,11 +539,15 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
       }
       if (!(a.ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
-    chain_round_tail<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
+    chain_round_tail9<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
       const uint32_t pk = lpk[x];
       return AncRec{p9_id(pk), p9_kind(pk), p9_parent(pk)};
-    }, L, a, rows, rel, maxd, fresh_n, flags);
-    __syncthreads();  // (wlist / imap reads of this round before the next round's leaders)
+    }, need, a, rows, rel, maxd, fresh_n, flags);
+  }
+  __syncthreads();  // (the workgroup's list counts are final)
+  if (threadIdx.x == 0) {
+    a.wn[blockIdx.x] = need[0];
+    a.wn[a.ntiles + blockIdx.x] = need[1];
   }
   if (flags) atomicOr(&a.counters[C_FLAGS], flags);
   chain_tile_stats<WTT>(rows, rel, maxd, fresh_n, red, tile_stats);
