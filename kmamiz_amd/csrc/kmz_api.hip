@@ -155,7 +155,7 @@ struct kmz_ctx {
   uint32_t ep_mode = 0;  // which ep table the groups use
   bool links = false;
   uint32_t ablate = 0;  // diagnostic knobs (KMZ_ABLATE env), never set in production
-  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream), bit 20 = the run's counters zeroed by hipMemsetAsync (not k_fill), bit 21 = on the direct walk, K3 beside the join on the side stream (not from the end of the walk, beside the settle), bit 22 = chain interning on k4_tile8 (not k4_tile9)
+  uint32_t ablate2 = 0;  // more knobs (KMZ_ABLATE2): bit 0 = 8-byte key staging (no compact keys), bit 1 = 2^20-slot edge set, bits 2/3 = chain table load <= 1/2 / 1/4, bit 4 = join + walk never fused, bit 5 = fused at any size, bit 6 = 2^8 certificate bins at any size, bit 7 = never, bit 8 = chain interning on the persistent k4_chain (not k4_tile), bit 9 = kmz_fetch_begin's copies to the host by the runtime's blit (not the DMA engines), bit 10 = chain interning on the 16-byte-record k4_tile (not k4_tile8), bit 11 = k4_tile8's chain elements by endpoint even where the table would allow shapes, bit 12 = kmz_route_ids_fixed by histogram / scan / scatter (not one pass), bit 13 = the certificate from the start of the run beside the join (pass 1 by k_cert_bin), bit 14 = the certificate behind K3 on the side stream (not on a stream of its own), bit 15 = with a chain table past the MALL, the certificate beside the settle (not on the main stream between the join and the walk), bit 16 = k_key_part without its LDS cache of written keys, bit 17 = K3 on the main stream between the join and the walk, bit 18 = K3 beside the join on the side stream on the chain-tile path too (not after the walk on the main stream), bit 20 = the run's counters zeroed by hipMemsetAsync (not k_fill), bit 21 = on the direct walk, K3 beside the join on the side stream (not from the end of the walk, beside the settle), bit 22 = chain interning on k4_tile8 (not k4_tile9), bit 23 = no run graphs (as KMZ_HIPGRAPH=0)
 
   // side stream: K3 and the uniqueness certificate run beside the join and the
   // chain walk (they share no buffers; fork/join by events)
@@ -196,6 +196,9 @@ struct kmz_ctx {
   uint32_t f_ndep = 0;
 
   bool prof = false;
+  // run graphs for batches below 2^23 spans (run_enqueue_graphed): on unless
+  // KMZ_HIPGRAPH=0 or KMZ_ABLATE2 bit 23
+  bool graphs = true;
   uint32_t prof_mask = 0;  // kernel ids timed while prof (kmz_set_profiling_mask)
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -372,7 +375,11 @@ kmz_ctx *kmz_create(int device, void *stream) {
   }
   if (const char *a = getenv("KMZ_ABLATE")) c->ablate = (uint32_t)strtoul(a, nullptr, 0);
   if (const char *a = getenv("KMZ_ABLATE2")) c->ablate2 = (uint32_t)strtoul(a, nullptr, 0);
-  if (const char *a = getenv("KMZ_HIPGRAPH")) if (atoi(a) == 1) c->ablate |= 1u << 13;  // opt-in run graphs
+  // run graphs: on by default (round 6); KMZ_HIPGRAPH=0 or KMZ_ABLATE2 bit 23
+  // turn them off, KMZ_ABLATE bit 13 (or KMZ_HIPGRAPH=1) keeps them on
+  if (const char *a = getenv("KMZ_HIPGRAPH")) c->graphs = atoi(a) != 0;
+  if (c->ablate2 & (1u << 23)) c->graphs = false;
+  if (c->ablate & (1u << 13)) c->graphs = true;
   if (c->ablate2 & 2u) c->tcap = 1ull << 20;  // test knob: an edge set large enough for compact staging from the start
   if (c->ablate & (1u << 30)) c->scap = 256;  // test knob: tiny key staging (overflow + growth paths)
   // counters (u32) and statistics (u64) in one allocation: one fill and one
@@ -793,8 +800,8 @@ static hipStream_t cert_stream(kmz_ctx *c) {
 static bool etab_cached(kmz_ctx *c) {
   const uint64_t key = (mix64(c->shape_gen * 0x9E3779B97F4A7C15ull ^ c->sig_seed ^ (c->alloc_gen << 40)) ^
                         (uint64_t)(uintptr_t)c->cetab.p ^ c->n_shapes) | 1;
-  const bool ok = key == c->etab_key && !(c->ablate & (1u << 13));
-  c->etab_key = (c->ablate & (1u << 13)) ? 0 : key;
+  const bool ok = key == c->etab_key && !c->graphs;
+  c->etab_key = c->graphs ? 0 : key;
   return ok;
 }
 
@@ -1788,14 +1795,16 @@ static uint64_t run_key(kmz_ctx *c, uint32_t flags) {
 }
 
 // Small batches (< 2^23 spans) are launch-bound: ~25 kernels and memsets per
-// run.  With KMZ_HIPGRAPH=1 (or KMZ_ABLATE bit 13) a run whose key was seen
-// on the previous run is captured into a hipGraph (stream capture, both
-// streams) and replayed while the key holds; the first run of a key (and any
-// run that grows a buffer) is enqueued directly, so a capture never
-// allocates.  Off by default: at a 2 500-trace tick the replays measured
-// 10-20 % slower than direct launches (tools/bench_tick.py).
+// run.  A run whose key was seen on the previous run is captured into a
+// hipGraph (stream capture, both streams) and replayed while the key holds;
+// the first run of a key (and any run that grows a buffer) is enqueued
+// directly, so a capture never allocates.  On by default since round 6: at
+// the 2 500-trace tick the replays measured faster than direct launches on
+// all three configs (round 5: 135 / 289 / 559 against 162 / 305 / 572 us per
+// run + fetch, Bookinfo / mesh / config 5); KMZ_HIPGRAPH=0 turns them off.
+// (Not while kernels are timed: the bench's live events keep them off.)
 static int run_enqueue_graphed(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, unsigned long long *s64) {
-  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && (c->ablate & (1u << 13)) &&
+  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && c->graphs &&
                         !c->table_hint && !c->walk_once && !(c->ablate & (32u | 16u));
   if (!eligible) return run_enqueue(c, flags, links, h, s64);
   const uint64_t key = run_key(c, flags);

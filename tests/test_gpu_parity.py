@@ -1451,7 +1451,7 @@ def test_headline_config5_vs_c_oracle_and_tail():
 # ---------------------------------------------------------------------------
 # hipGraph replay of small-batch runs (kmz_api.hip run_enqueue_graphed)
 # ---------------------------------------------------------------------------
-GRAPH_ON = 1 << 13  # KMZ_ABLATE: hipGraph capture / replay of small runs (KMZ_HIPGRAPH=1; off by default)
+GRAPH_OFF = 1 << 23  # KMZ_ABLATE2: no run graphs (KMZ_HIPGRAPH=0)
 
 
 def _run_results(e, flags):
@@ -1475,7 +1475,7 @@ def test_graph_replay_equals_direct_runs(config, ntr):
                                for f in batch.__dataclass_fields__})
     other.duration = other.duration[::-1].copy()
     other.timestamp = other.timestamp + 7
-    on, off = _engine_with(GRAPH_ON), _engine_with(0)
+    on, off = _engine_with(0), _engine_with2(0, GRAPH_OFF)  # (graphs on by default)
     try:
         for flags in (L.RUN_STATS_TAG | L.RUN_DEPS, L.RUN_STATS_RT | L.RUN_DEPS | L.RUN_SPAN_LINKS):
             for b in (batch, other, batch):

@@ -2,9 +2,9 @@
 takes up to 2 500 traces per 5-s tick (RealtimeWorkerImpl.ts:31-35).  Per tick
 on one GPU: kmz_load of the host columns (H2D) + kmz_run (stats + dependency
 graph) + kmz_fetch of the results, timed over many ticks, with the run's
-join + chain walk fused (default) or as two kernels, hipGraph replay on or
-off (KMZ_ABLATE bit 13).  Prints one JSON
-object; kernel launches per tick come from rocprofv3 (tools/tick_profile.sh).
+join + chain walk fused (default) or as two kernels, hipGraph replay on (the
+default since round 6) or off (KMZ_ABLATE2 bit 23).  Prints one JSON object;
+kernel traces of a tick come from rocprofv3 over tools/tick_trace.py.
 
     python tools/bench_tick.py [--traces 2500] [--ticks 200]
 """
@@ -36,10 +36,11 @@ def main():
         batch, _ = synth.host_batch(cfg, 0, args.traces)
         table = synth.shape_table(cfg)
         res = {"spans": len(batch)}
-        # default: direct launches, the join + chain walk fused (kmz_fuse.hip);
-        # separate: k_join_window + k4_chain (KMZ_ABLATE2 bit 4); graph: hipGraph
-        # replay (KMZ_ABLATE bit 13); serial: no side stream (bit 25)
-        for mode, knob, knob2 in (("default", 0, 0), ("separate", 0, 16), ("graph", 1 << 13, 0),
+        # default: hipGraph replay (since round 6), the join + chain walk fused
+        # (kmz_fuse.hip) where the batch allows; separate: k_join_window + the
+        # tile walk (KMZ_ABLATE2 bit 4); direct: launches one at a time
+        # (KMZ_ABLATE2 bit 23, = KMZ_HIPGRAPH=0); serial: no side stream (bit 25)
+        for mode, knob, knob2 in (("default", 0, 0), ("separate", 0, 16), ("direct", 0, 1 << 23),
                                   ("serial", 1 << 25, 0)):
             os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"] = str(knob), str(knob2)
             e = Engine(0)
