@@ -198,7 +198,7 @@ struct kmz_ctx {
   bool prof = false;
   // run graphs for batches below 2^23 spans (run_enqueue_graphed): on unless
   // KMZ_HIPGRAPH=0 or KMZ_ABLATE2 bit 23
-  bool graphs = true;
+  bool graphs_on = true;
   uint32_t prof_mask = 0;  // kernel ids timed while prof (kmz_set_profiling_mask)
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> pool;
@@ -377,9 +377,9 @@ kmz_ctx *kmz_create(int device, void *stream) {
   if (const char *a = getenv("KMZ_ABLATE2")) c->ablate2 = (uint32_t)strtoul(a, nullptr, 0);
   // run graphs: on by default (round 6); KMZ_HIPGRAPH=0 or KMZ_ABLATE2 bit 23
   // turn them off, KMZ_ABLATE bit 13 (or KMZ_HIPGRAPH=1) keeps them on
-  if (const char *a = getenv("KMZ_HIPGRAPH")) c->graphs = atoi(a) != 0;
-  if (c->ablate2 & (1u << 23)) c->graphs = false;
-  if (c->ablate & (1u << 13)) c->graphs = true;
+  if (const char *a = getenv("KMZ_HIPGRAPH")) c->graphs_on = atoi(a) != 0;
+  if (c->ablate2 & (1u << 23)) c->graphs_on = false;
+  if (c->ablate & (1u << 13)) c->graphs_on = true;
   if (c->ablate2 & 2u) c->tcap = 1ull << 20;  // test knob: an edge set large enough for compact staging from the start
   if (c->ablate & (1u << 30)) c->scap = 256;  // test knob: tiny key staging (overflow + growth paths)
   // counters (u32) and statistics (u64) in one allocation: one fill and one
@@ -800,8 +800,8 @@ static hipStream_t cert_stream(kmz_ctx *c) {
 static bool etab_cached(kmz_ctx *c) {
   const uint64_t key = (mix64(c->shape_gen * 0x9E3779B97F4A7C15ull ^ c->sig_seed ^ (c->alloc_gen << 40)) ^
                         (uint64_t)(uintptr_t)c->cetab.p ^ c->n_shapes) | 1;
-  const bool ok = key == c->etab_key && !c->graphs;
-  c->etab_key = c->graphs ? 0 : key;
+  const bool ok = key == c->etab_key && !c->graphs_on;
+  c->etab_key = c->graphs_on ? 0 : key;
   return ok;
 }
 
@@ -1804,7 +1804,7 @@ static uint64_t run_key(kmz_ctx *c, uint32_t flags) {
 // run + fetch, Bookinfo / mesh / config 5); KMZ_HIPGRAPH=0 turns them off.
 // (Not while kernels are timed: the bench's live events keep them off.)
 static int run_enqueue_graphed(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, unsigned long long *s64) {
-  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && c->graphs &&
+  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && c->graphs_on &&
                         !c->table_hint && !c->walk_once && !(c->ablate & (32u | 16u));
   if (!eligible) return run_enqueue(c, flags, links, h, s64);
   const uint64_t key = run_key(c, flags);
