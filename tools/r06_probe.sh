@@ -1,10 +1,11 @@
 #!/bin/bash
 # Round-6 GPU cycle: (1) the GPU suite (messy batches deselected); (2) mesh
-# bench A/B, k4_tile9 (default) against k4_tile8 (KMZ_ABLATE2 bit 22);
-# (3) the walk's instruction counters per wave for both, under the phase knobs
-# (KMZ_ABLATE bit 16: window + row counts only; bit 17: + walk and sigs; 0:
-# all), config 3 at 10^8 spans; (4) rocprofv3 kernel traces of the realtime
-# tick (Bookinfo and mesh, direct and graphed) and tools/bench_tick.py.
+# bench A/B, k4_tile9 (default, 7 workgroups per CU), the 8-per-CU build
+# (libkmz_t9w8.so) and k4_tile8 (KMZ_ABLATE2 bit 22); config 5 once each;
+# (3) the walk's instruction counters per wave under the phase knobs (KMZ_ABLATE
+# bit 16: window + row counts only; bit 17: + walk and sigs; 0: all), config 3
+# at 10^8 spans; (4) rocprofv3 kernel traces of the realtime tick (Bookinfo and
+# mesh, graphed and direct) and tools/bench_tick.py.
 # usage: tools/r06_probe.sh [skip-tests]
 set -o pipefail
 export TMPDIR=/tmp
@@ -17,23 +18,17 @@ if [ "$1" != skip-tests ]; then
   tail -3 $D/tests.log
   [ $rc -eq 0 ] || exit 1
 fi
-bash tools/ab/ab_env.sh w9 "--steps 10 --warmup 3" 2 t9=base t8=base:KMZ_ABLATE2=4194304 || exit 1
+bash tools/ab/ab_env.sh w9 "--steps 10 --warmup 3" 2 t9=base t9w8=t9w8 t8=base:KMZ_ABLATE2=4194304 || exit 1
 python3 tools/ab/abread.py gpurun_out/ab_w9
-# the certificate check as an LDS compare-and-swap set (libkmz_ckcas.so, -DKMZ_CK_CAS=1)
-KMZ_LIB_VARIANT=ckcas timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_guard.py -m gpu -x -q \
-  --timeout 200 --timeout-method thread -p no:cacheprovider \
-  -k "certificate or repeated or id_repeats or structured or synthetic_vs or seg or guard" > $D/tests_ckcas.log 2>&1
-rc=$?
-tail -2 $D/tests_ckcas.log
-if [ $rc -eq 0 ]; then
-  bash tools/ab/ab_env.sh ck "--steps 10 --warmup 3" 2 t9=base ckcas=ckcas || exit 1
-  python3 tools/ab/abread.py gpurun_out/ab_ck
-fi
-for v in 0 4194304; do
+bash tools/ab/ab_env.sh w9p "--config power --steps 10 --warmup 3" 1 t9=base t8=base:KMZ_ABLATE2=4194304 || exit 1
+python3 tools/ab/abread.py gpurun_out/ab_w9p
+bash tools/ab/ab_env.sh w9b "--config bookinfo --steps 200 --warmup 50" 2 graph=base direct=base:KMZ_HIPGRAPH=0 || exit 1
+python3 tools/ab/abread.py gpurun_out/ab_w9b
+for v in 0; do
   for a in 0 65536 131072; do
     KMZ_ABLATE=$a KMZ_ABLATE2=$v timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-      --kernel-include-regex "k4_tile" --kernel-trace --output-format csv -d $D/knob_${v}_$a -o walk -- \
-      python3 tools/ab/ablate.py child 3650000 > $D/knob_${v}_$a.log 2>&1 || exit 1
+      --kernel-include-regex "k4_tile" --kernel-trace --output-format csv -d $D/knobB_${v}_$a -o walk -- \
+      python3 tools/ab/ablate.py child 3650000 > $D/knobB_${v}_$a.log 2>&1 || exit 1
   done
 done
 for c in bookinfo mesh; do
