@@ -426,8 +426,8 @@ __global__ void __launch_bounds__(256) k_chain_settle_list(const unsigned long l
   // endpoint keys -- the gathers the walk left out)
   for (uint32_t x = t0; x < m; x += ts)
     edge_insert(id_ep ? key_ids_to_eps(stage[x], id_ep, n_ids) : stage[x], trip, tcap, &flags);
-  // k4_tile9's per-workgroup regions (wn[w]: the keys tile w needed, the
-  // first WG_STAGE of them in its region)
+  // k4_tile9's per-workgroup regions (wn[w]: the valid keys at the start of
+  // tile w's region; the rest of its keys are in the global list)
   if (wstage)
     for (uint64_t x = t0; x < (uint64_t)nwg * WG_STAGE; x += ts) {
       const uint32_t w = (uint32_t)(x / WG_STAGE), k = (uint32_t)(x % WG_STAGE);

@@ -242,7 +242,9 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 // past the region a device atomic reserves them in the global list.  A claim
 // that lost the slot, or a chain found unpublished, goes to the deferred
 // checks (global list, as before).  need[0] / need[1]: the workgroup's key /
-// claim counts so far (its region holds the first ones).
+// claim counts so far; need[2]: where the first key reservation that did not
+// fit the region started (its keys, and every later one's, went to the global
+// list), so the region's valid keys are the first min(need[0], need[2]).
 template <int NT, int TW, class Anc>
 __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint64_t (&ps)[TW], uint8_t (&st)[TW],
                                                   const uint8_t (&kq)[TW], const uint32_t (&dd)[TW],
@@ -317,7 +319,8 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
       if (o + d <= WG_STAGE) {
         dst = a.wstage + (uint64_t)blk * WG_STAGE + o;
         cap = d;
-      } else {
+      } else {  // (the region's valid keys end where the first reservation past it starts: need[2])
+        atomicMin(&need[2], o);
         const uint32_t b = atomicAdd(&a.counters[C_FSTAGE], d);
         dst = a.stage + b;
         cap = b < a.scap ? a.scap - b : 0;
@@ -380,7 +383,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   __shared__ uint64_t lel[W9];  // element hash (0 on the sentinels)
   __shared__ uint32_t lpk[W9];  // window parent | kind << 11 | id << 13
   __shared__ uint16_t wlist[WT];
-  __shared__ uint32_t need[2];  // the workgroup's staged keys and claimed slots (chain_round_tail9)
+  __shared__ uint32_t need[3];  // the workgroup's staged keys and claimed slots (chain_round_tail9)
   __shared__ uint32_t wcnt[WPT][NW];
   __shared__ uint32_t red[NW][4];
   const uint32_t t0 = blockIdx.x * WT, t1 = min(n, t0 + WT);
@@ -400,7 +403,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     k[q] = kw[j];
     e[q] = sw[j];
   }
-  if (threadIdx.x < 2) need[threadIdx.x] = 0;
+  if (threadIdx.x < 3) need[threadIdx.x] = threadIdx.x < 2 ? 0u : ~0u;
   if (threadIdx.x < 3) {
     lpk[WW + threadIdx.x] = (WW + threadIdx.x) | ((uint32_t)KIND_CLIENT << P9_BITS) | (ID9_NONE << (P9_BITS + 2));
     lel[WW + threadIdx.x] = 0;
@@ -546,7 +549,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   }
   __syncthreads();  // (the workgroup's list counts are final)
   if (threadIdx.x == 0) {
-    a.wn[blockIdx.x] = need[0];
+    a.wn[blockIdx.x] = min(need[0], need[2]);  // (the region's valid keys)
     a.wn[a.ntiles + blockIdx.x] = need[1];
   }
   if (flags) atomicOr(&a.counters[C_FLAGS], flags);
