@@ -55,9 +55,10 @@ struct ChainRun {
   uint32_t n_ids = 0;  // (shape ids: n_shapes; an id past it is NONE)
   // k4_tile9's per-workgroup lists (no device atomic to reserve them): tile w
   // stages up to WG_STAGE keys at wstage[w * WG_STAGE], claims up to WG_POS
-  // slots at wgpos[w * WG_POS], and writes the counts it needed to wn[w] /
-  // wn[ntiles + w]; what does not fit goes to the global lists above
-  unsigned long long *wstage = nullptr;
+  // slots at wgpos[w * WG_POS], defers up to WG_DEFER checks at
+  // wdefer[2 * w * WG_DEFER], and writes the counts to wn[w] / wn[ntiles + w]
+  // / wn[2 * ntiles + w]; what does not fit goes to the global lists above
+  unsigned long long *wstage = nullptr, *wdefer = nullptr;
   uint32_t *wgpos = nullptr;
   uint32_t *wn = nullptr;
   uint32_t ntiles = 0;
