@@ -230,6 +230,22 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #ifndef KMZ_TILE9_WAVES
 #define KMZ_TILE9_WAVES 7
 #endif
+// diagnostic phase clocks of k4_tile9 (a -DKMZ_T9_CLOCKS=1 build only):
+// s_memtime deltas seen by thread 0, summed over workgroups (kmz__debug_walk9)
+#ifndef KMZ_T9_CLOCKS
+#define KMZ_T9_CLOCKS 0
+#endif
+__device__ unsigned long long g_walk9_dbg[12];
+#if KMZ_T9_CLOCKS
+#define T9_STAMP(k)                                             \
+  {                                                             \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && t9prev) t9acc[k] += t_ - t9prev;    \
+    t9prev = t_;                                                \
+  }
+#else
+#define T9_STAMP(k)
+#endif
 
 // k4_tile9's probe / claim / lists (against chain_round_tail: fewer dependent
 // round trips per workgroup).  A walker whose probe finds its chain checks
@@ -251,7 +267,8 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
                                                   const uint8_t (&kq)[TW], const uint32_t (&dd)[TW],
                                                   const uint32_t (&jq)[TW], const uint32_t (&myep)[TW], uint32_t w0,
                                                   Anc anc, uint32_t *need, const ChainRun &a, uint32_t &rows,
-                                                  uint32_t &rel, uint32_t &maxd, uint32_t &fresh_n, uint32_t &flags) {
+                                                  uint32_t &rel, uint32_t &maxd, uint32_t &fresh_n, uint32_t &flags,
+                                                  unsigned long long *t9acc, unsigned long long &t9prev) {
   const uint32_t spin = spin_bound(a.ablate);
   ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
   uint64_t pos[TW];
@@ -281,6 +298,7 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
     if (a.ablate & (1u << 18)) continue;  // diagnostic knob: probe but no inserts
     lead[q] = true;  // an empty slot (or PROBE_MAX other chains: the CAS fails, the settle inserts)
   }
+  T9_STAMP(4);
   // the claims, all in flight together; a winner publishes at once
   unsigned long long cvq[TW];
 #pragma unroll
@@ -291,6 +309,10 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
     cvq[q] = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
     if (cvq[q] == 0) atomicExch(&en[1], (unsigned long long)ps[q]);
   }
+#if KMZ_T9_CLOCKS
+  if (__ballot(cvq[0] == 1234567 || cvq[TW - 1] == 1234567)) flags |= 0;  // (waits for the claims)
+#endif
+  T9_STAMP(5);
   const uint32_t blk = blockIdx.x;
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
@@ -358,6 +380,7 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
       }
     }
   }
+  T9_STAMP(6);
   // per walker: row counts, pending list, rowpos
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
@@ -379,6 +402,7 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
     }
     if (a.rowpos_out) a.rowpos_out[i] = rp;
   }
+  T9_STAMP(7);
 }
 template <bool BY_SHAPE>
 __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *__restrict__ kind,
@@ -397,6 +421,8 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   const uint32_t w0 = t0 > WH ? t0 - WH : 0, w1 = min(n, t1 + WH), wn = w1 - w0, toff = t0 - w0;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t flags = 0;
+  unsigned long long t9acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t9prev = 0;
+  T9_STAMP(0);
   uint32_t c[WPW], e[WPW];
   uint8_t k[WPW];
   const uint32_t *__restrict__ cpw = cparent + w0;
@@ -437,6 +463,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     other |= jl < wn && kk != KIND_SERVER && kk != KIND_CLIENT;
   }
   const bool any_other = __syncthreads_or(other);
+  T9_STAMP(0);
   // the tile's non-CLIENT spans -> wlist: a ballot per slot row, per-wave
   // counts in LDS, each lane's place from them and its rank in the ballot
   uint64_t mk[WPT];
@@ -465,6 +492,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     m += all;
   }
   __syncthreads();
+  T9_STAMP(1);
   uint32_t rows = 0, rel = 0, maxd = 0, fresh_n = 0;
   const bool hash_on = !(a.ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
   constexpr int TW = WTW;
@@ -527,6 +555,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
       walk(std::true_type{});
     else
       walk(std::false_type{});
+    T9_STAMP(2);
 #pragma unroll
     for (int q = 0; q < TW; ++q) {
       if (st[q] != S_DONE || !hash_on) {
@@ -549,10 +578,11 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
       }
       if (!(a.ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
+    T9_STAMP(3);
     chain_round_tail9<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
       const uint32_t pk = lpk[x];
       return AncRec{p9_id(pk), p9_kind(pk), p9_parent(pk)};
-    }, need, a, rows, rel, maxd, fresh_n, flags);
+    }, need, a, rows, rel, maxd, fresh_n, flags, t9acc, t9prev);
   }
   __syncthreads();  // (the workgroup's list counts are final)
   if (threadIdx.x == 0) {
@@ -561,7 +591,13 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     a.wn[2 * a.ntiles + blockIdx.x] = need[3];
   }
   if (flags) atomicOr(&a.counters[C_FLAGS], flags);
+  T9_STAMP(8);
   chain_tile_stats<WTT>(rows, rel, maxd, fresh_n, red, tile_stats);
+  T9_STAMP(9);
+#if KMZ_T9_CLOCKS
+  if (threadIdx.x == 0)
+    for (int kk = 0; kk < 10; ++kk) atomicAdd(&g_walk9_dbg[kk], t9acc[kk]);
+#endif
 }
 
 bool chain_tile9_fits(uint32_t n_ids) { return n_ids < ID9_NONE; }
@@ -599,3 +635,12 @@ void launch_chain_tile(hipStream_t s, const uint8_t *kind, const uint32_t *shape
 }
 
 }  // namespace kmz
+
+extern "C" int kmz__debug_walk9(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmz::g_walk9_dbg), sizeof(kmz::g_walk9_dbg)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[12] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(kmz::g_walk9_dbg), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}

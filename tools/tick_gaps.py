@@ -18,10 +18,12 @@ def ticks(path):
         for r in csv.DictReader(open(f)):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0]))
     rows.sort()
-    # a tick starts with kmz_load's copies: the runtime's copy kernels after a gap of > 20 us
+    # a tick starts with kmz_load's copies (the runtime's copy kernels) after
+    # the previous tick's run kernels; the fetch's copies end a tick
     out, cur = [], []
     for s, e, k in rows:
-        if cur and s - cur[-1][1] > 20000 and "copyBuffer" in k:
+        if cur and "copyBuffer" in k and "copyBuffer" not in cur[-1][2] and any("copyBuffer" in x[2] for x in cur[-3:]) is False \
+                and len(cur) > 8:
             out.append(cur)
             cur = []
         cur.append((s, e, k))
