@@ -232,6 +232,9 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #endif
 // diagnostic phase clocks of k4_tile9 (a -DKMZ_T9_CLOCKS=1 build only):
 // s_memtime deltas seen by thread 0, summed over workgroups (kmz__debug_walk9)
+#ifndef KMZ_T9_TAIL
+#define KMZ_T9_TAIL 1  // 0 (A/B build): k4_tile8's round tail (chain_round_tail) in k4_tile9
+#endif
 #ifndef KMZ_T9_CLOCKS
 #define KMZ_T9_CLOCKS 0
 #endif
@@ -415,6 +418,9 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   __shared__ uint32_t lpk[W9];  // window parent | kind << 11 | id << 13
   __shared__ uint16_t wlist[WT];
   __shared__ uint32_t need[4];  // the workgroup's staged keys, claimed slots and deferred checks (chain_round_tail9)
+#if !KMZ_T9_TAIL
+  __shared__ ChainLds L;
+#endif
   __shared__ uint32_t wcnt[WPT][NW];
   __shared__ uint32_t red[NW][4];
   const uint32_t t0 = blockIdx.x * WT, t1 = min(n, t0 + WT);
@@ -437,6 +443,9 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     e[q] = sw[j];
   }
   if (threadIdx.x < 4) need[threadIdx.x] = threadIdx.x == 2 ? ~0u : 0u;
+#if !KMZ_T9_TAIL
+  chain_lds_init(L);
+#endif
   if (threadIdx.x < 3) {
     lpk[WW + threadIdx.x] = (WW + threadIdx.x) | ((uint32_t)KIND_CLIENT << P9_BITS) | (ID9_NONE << (P9_BITS + 2));
     lel[WW + threadIdx.x] = 0;
@@ -579,10 +588,18 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
       if (!(a.ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
     T9_STAMP(3);
+#if KMZ_T9_TAIL
     chain_round_tail9<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
       const uint32_t pk = lpk[x];
       return AncRec{p9_id(pk), p9_kind(pk), p9_parent(pk)};
     }, need, a, rows, rel, maxd, fresh_n, flags, t9acc, t9prev);
+#else  // (A/B: k4_tile8's tail -- LDS leader map, lists reserved per workgroup with device atomics)
+    chain_round_tail<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
+      const uint32_t pk = lpk[x];
+      return AncRec{p9_id(pk), p9_kind(pk), p9_parent(pk)};
+    }, L, a, rows, rel, maxd, fresh_n, flags);
+    __syncthreads();
+#endif
   }
   __syncthreads();  // (the workgroup's list counts are final)
   if (threadIdx.x == 0) {
