@@ -235,6 +235,9 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #ifndef KMZ_T9_TAIL
 #define KMZ_T9_TAIL 1  // 0 (A/B build): k4_tile8's round tail (chain_round_tail) in k4_tile9
 #endif
+#ifndef KMZ_T9_LDSPAD
+#define KMZ_T9_LDSPAD 0
+#endif
 #ifndef KMZ_T9_CLOCKS
 #define KMZ_T9_CLOCKS 0
 #endif
@@ -420,6 +423,10 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   __shared__ uint32_t need[4];  // the workgroup's staged keys, claimed slots and deferred checks (chain_round_tail9)
 #if !KMZ_T9_TAIL
   __shared__ ChainLds L;
+#endif
+#if KMZ_T9_LDSPAD  // (A/B builds: LDS held back to cap the workgroups per CU)
+  __shared__ uint32_t ldspad[KMZ_T9_LDSPAD / 4];
+  if (threadIdx.x == 0) ldspad[(blockIdx.x * 7u) % (KMZ_T9_LDSPAD / 4)] = blockIdx.x;
 #endif
   __shared__ uint32_t wcnt[WPT][NW];
   __shared__ uint32_t red[NW][4];
