@@ -235,6 +235,9 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #ifndef KMZ_T9_TAIL
 #define KMZ_T9_TAIL 1  // 0 (A/B build): k4_tile8's round tail (chain_round_tail) in k4_tile9
 #endif
+#ifndef KMZ_T9_BAR
+#define KMZ_T9_BAR 0  // 1 (A/B build): workgroup barriers after the probes and after the claims, as k4_tile8's tail
+#endif
 #ifndef KMZ_T9_LDSPAD
 #define KMZ_T9_LDSPAD 0
 #endif
@@ -305,6 +308,9 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
     lead[q] = true;  // an empty slot (or PROBE_MAX other chains: the CAS fails, the settle inserts)
   }
   T9_STAMP(4);
+#if KMZ_T9_BAR
+  __syncthreads();
+#endif
   // the claims, all in flight together; a winner publishes at once
   unsigned long long cvq[TW];
 #pragma unroll
@@ -319,6 +325,9 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
   if (__ballot(cvq[0] == 1234567 || cvq[TW - 1] == 1234567)) flags |= 0;  // (waits for the claims)
 #endif
   T9_STAMP(5);
+#if KMZ_T9_BAR
+  __syncthreads();
+#endif
   const uint32_t blk = blockIdx.x;
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
