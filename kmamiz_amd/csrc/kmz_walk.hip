@@ -281,12 +281,17 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
   const uint32_t spin = spin_bound(a.ablate);
   ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
   uint64_t pos[TW];
+  // (unconditional loads, slot 0 for a walker that does not probe: the
+  // branchy form let the compiler wait for the first probe before issuing
+  // the second -- two round trips instead of one, walk 0.95 -> 1.35 ms)
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
-    const bool pr = st[q] == S_PUT;
-    pos[q] = pr ? cslot(sg[q], a.ccap) : 0;
-    w01[q] = pr ? *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]) : make_ulonglong2(0, 0);
+    pos[q] = st[q] == S_PUT ? cslot(sg[q], a.ccap) : 0;
+    w01[q] = *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
   }
+#pragma unroll
+  for (int q = 0; q < TW; ++q)
+    if (st[q] != S_PUT) w01[q] = make_ulonglong2(0, 0);
   bool lead[TW], dfr[TW];
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
