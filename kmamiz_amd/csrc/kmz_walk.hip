@@ -235,6 +235,9 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #ifndef KMZ_T9_TAIL
 #define KMZ_T9_TAIL 1  // 0 (A/B build): k4_tile8's round tail (chain_round_tail) in k4_tile9
 #endif
+#ifndef KMZ_T9_X
+#define KMZ_T9_X 0  // (timing-only A/B builds, wrong results) 1: no list writes, 2: no claims, 4: no probes
+#endif
 #ifndef KMZ_T9_BAR
 #define KMZ_T9_BAR 0  // 1 (A/B build): workgroup barriers after the probes and after the claims, as k4_tile8's tail
 #endif
@@ -287,7 +290,7 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
     pos[q] = st[q] == S_PUT ? cslot(sg[q], a.ccap) : 0;
-    w01[q] = *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
+    w01[q] = (KMZ_T9_X & 4) ? make_ulonglong2(sg[q], ps[q]) : *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
   }
 #pragma unroll
   for (int q = 0; q < TW; ++q)
@@ -323,6 +326,7 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
     cvq[q] = 0;
     if (!lead[q]) continue;
     unsigned long long *en = a.ctab + 2 * pos[q];
+    if (KMZ_T9_X & 2) continue;
     cvq[q] = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
     if (cvq[q] == 0) atomicExch(&en[1], (unsigned long long)ps[q]);
   }
@@ -336,7 +340,7 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
   const uint32_t blk = blockIdx.x;
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
-    if (!lead[q] && !dfr[q]) continue;
+    if ((!lead[q] && !dfr[q]) || (KMZ_T9_X & 1)) continue;
     const uint32_t d = dd[q];
     if (lead[q] && cvq[q] == 0) {  // won the slot: it is cleared after the run
       ++fresh_n;
