@@ -337,70 +337,120 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
 #if KMZ_T9_BAR
   __syncthreads();
 #endif
-  const uint32_t blk = blockIdx.x;
+  const uint32_t blk = blockIdx.x, lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1;  // (the lanes below this one)
+  // The list entries, reserved per wave: one LDS add for the wave's entries in
+  // the workgroup's region, and -- for a wave whose entries do not fit it --
+  // one device atomic for all of them in the global list.  (The workgroups
+  // that run first find nearly every chain new, ~480 claims and ~2000 keys
+  // each: a device atomic per walker on one counter serialised them, walk
+  // 0.67 -> 1.33 ms on the mesh.)  Every lane takes part in the ballots and
+  // shuffles; the per-walker work is predicated.
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
-    if ((!lead[q] && !dfr[q]) || (KMZ_T9_X & 1)) continue;
+    if (KMZ_T9_X & 1) break;
     const uint32_t d = dd[q];
-    if (lead[q] && cvq[q] == 0) {  // won the slot: it is cleared after the run
-      ++fresh_n;
-      const uint32_t o = atomicAdd(&need[1], 1u);
-      if (o < WG_POS) {
-        a.wgpos[(uint64_t)blk * WG_POS + o] = (uint32_t)pos[q];
-      } else {
-        const uint32_t x = atomicAdd(&a.counters[C_WPOS], 1u);
-        if (x < a.gcap)
-          a.gpos[x] = (uint32_t)pos[q];
-        else
-          flags |= F_CTAB_DIRTY;
+    const bool won = lead[q] && cvq[q] == 0;
+    fresh_n += won;
+    // claimed slots (cleared after the run)
+    {
+      const uint64_t mk = __ballot(won);
+      if (mk) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&need[1], (uint32_t)__popcll(mk));
+        base = __shfl(base, 0, 64);
+        const uint32_t o = base + (uint32_t)__popcll(mk & lt);
+        const uint64_t mo = __ballot(won && o >= WG_POS);
+        uint32_t gb = 0;
+        if (mo && lane == 0) gb = atomicAdd(&a.counters[C_WPOS], (uint32_t)__popcll(mo));
+        gb = __shfl(gb, 0, 64);
+        if (won) {
+          if (o < WG_POS) {
+            a.wgpos[(uint64_t)blk * WG_POS + o] = (uint32_t)pos[q];
+          } else {
+            const uint32_t x = gb + (uint32_t)__popcll(mo & lt);
+            if (x < a.gcap)
+              a.gpos[x] = (uint32_t)pos[q];
+            else
+              flags |= F_CTAB_DIRTY;
+          }
+        }
       }
     }
     // a row whose chain this walker inserted (or lost to another chain: the
     // deferred check may insert it) stages its keys (ancestor k, row id, k,
     // ancestor is SERVER); one that joined the same chain leaves them to the
     // winner (knob 19: diagnostic, none)
-    if (lead[q] && kq[q] == KIND_SERVER && d && cvq[q] != sg[q] && !(a.ablate & (1u << 19))) {
-      const uint32_t o = atomicAdd(&need[0], d);
+    const bool stg = lead[q] && kq[q] == KIND_SERVER && d && cvq[q] != sg[q] && !(a.ablate & (1u << 19));
+    if (__ballot(stg)) {
+      const uint32_t nd = stg ? d : 0u;
+      uint32_t incl = nd;  // the wave's inclusive scan of the key counts
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += y;
+      }
+      const uint32_t tot = __shfl(incl, 63, 64), pre = incl - nd;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&need[0], tot);
+      base = __shfl(base, 0, 64);
       unsigned long long *dst;
       uint64_t cap;
-      if (o + d <= WG_STAGE) {
-        dst = a.wstage + (uint64_t)blk * WG_STAGE + o;
-        cap = d;
+      if (base + tot <= WG_STAGE) {  // (wave-uniform)
+        dst = a.wstage + (uint64_t)blk * WG_STAGE + base + pre;
+        cap = nd;
       } else {  // (the region's valid keys end where the first reservation past it starts: need[2])
-        atomicMin(&need[2], o);
-        const uint32_t b = atomicAdd(&a.counters[C_FSTAGE], d);
-        dst = a.stage + b;
-        cap = b < a.scap ? a.scap - b : 0;
-      }
-      uint32_t an = anc(jq[q]).parent;
-      for (uint32_t kk = 1; kk <= d; ++kk) {
-        const AncRec r = anc(an);
-        const uint64_t key = edge_key(r.ep, myep[q], kk, r.kind == KIND_SERVER);
-        if (kk - 1 < cap) {
-          dst[kk - 1] = key;
-        } else {
-          edge_insert(a.id_ep ? key_ids_to_eps(key, a.id_ep, a.n_ids) : key, a.trip, a.tcap, &flags);
-          flags |= F_STAGE_FULL;
+        uint32_t gb = 0;
+        if (lane == 0) {
+          atomicMin(&need[2], base);
+          gb = atomicAdd(&a.counters[C_FSTAGE], tot);
         }
-        an = r.parent;
+        gb = __shfl(gb, 0, 64);
+        dst = a.stage + gb + pre;
+        cap = gb + pre < a.scap ? a.scap - (gb + pre) : 0;
+      }
+      if (stg) {
+        uint32_t an = anc(jq[q]).parent;
+        for (uint32_t kk = 1; kk <= d; ++kk) {
+          const AncRec r = anc(an);
+          const uint64_t key = edge_key(r.ep, myep[q], kk, r.kind == KIND_SERVER);
+          if (kk - 1 < cap) {
+            dst[kk - 1] = key;
+          } else {
+            edge_insert(a.id_ep ? key_ids_to_eps(key, a.id_ep, a.n_ids) : key, a.trip, a.tcap, &flags);
+            flags |= F_STAGE_FULL;
+          }
+          an = r.parent;
+        }
       }
     }
-    if (dfr[q] || cvq[q] != 0) {  // found unpublished, joined an unpublished claim, or lost the slot
-      // (the workgroup's region first: a hot new chain is found unpublished
-      // by many workgroups at once, and one device counter for all of them
-      // serialised the walk, 0.95 -> 1.40 ms on the mesh)
-      const uint32_t o = atomicAdd(&need[3], 1u);
-      const uint32_t x = o < WG_DEFER ? 0u : atomicAdd(&a.counters[C_FDEFER], 1u);
-      if (o < WG_DEFER) {
-        *reinterpret_cast<ulonglong2 *>(a.wdefer + 2 * ((uint64_t)blk * WG_DEFER + o)) = make_ulonglong2(sg[q], ps[q]);
-      } else if (x < a.dcap) {
-        *reinterpret_cast<ulonglong2 *>(a.defer + 2 * (uint64_t)x) = make_ulonglong2(sg[q], ps[q]);
-      } else {
-        int rr = 0;
-        for (uint32_t t = 0; t < spin && rr == 0; ++t)
-          rr = chain_put(a.ctab, a.ccap, sg[q], ps[q], &flags, a.gpos, a.gcap, a.counters);
-        if (rr == 0) flags |= F_SPIN;  // unchecked: the run is redone on the exact walk
-        fresh_n += rr == 1;
+    // deferred checks: found unpublished, joined an unpublished claim, or
+    // lost the slot to another chain
+    const bool dq = dfr[q] || cvq[q] != 0;
+    const uint64_t md = __ballot(dq);
+    if (md) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&need[3], (uint32_t)__popcll(md));
+      base = __shfl(base, 0, 64);
+      const uint32_t o = base + (uint32_t)__popcll(md & lt);
+      const uint64_t mo = __ballot(dq && o >= WG_DEFER);
+      uint32_t gb = 0;
+      if (mo && lane == 0) gb = atomicAdd(&a.counters[C_FDEFER], (uint32_t)__popcll(mo));
+      gb = __shfl(gb, 0, 64);
+      if (dq) {
+        const uint32_t x = gb + (uint32_t)__popcll(mo & lt);
+        if (o < WG_DEFER) {
+          *reinterpret_cast<ulonglong2 *>(a.wdefer + 2 * ((uint64_t)blk * WG_DEFER + o)) =
+              make_ulonglong2(sg[q], ps[q]);
+        } else if (x < a.dcap) {
+          *reinterpret_cast<ulonglong2 *>(a.defer + 2 * (uint64_t)x) = make_ulonglong2(sg[q], ps[q]);
+        } else {
+          int rr = 0;
+          for (uint32_t t = 0; t < spin && rr == 0; ++t)
+            rr = chain_put(a.ctab, a.ccap, sg[q], ps[q], &flags, a.gpos, a.gcap, a.counters);
+          if (rr == 0) flags |= F_SPIN;  // unchecked: the run is redone on the exact walk
+          fresh_n += rr == 1;
+        }
       }
     }
   }
