@@ -156,9 +156,12 @@ __global__ void __launch_bounds__(CTT, CHAIN_WAVES) k4_chain(
     }
   };
   auto gather_ep = [&]() {
+    // (every slot gathers -- a CLIENT slot entry 0, unused -- so that the
+    // loads carry no branch: a load under a branch made the compiler wait for
+    // it at the merge, which serialised the CPW gathers and the prefetch of the
+    // next tile behind them)
 #pragma unroll
-    for (int q = 0; q < CPW; ++q)  // (a CLIENT slot's record holds no endpoint: no gather)
-      e[q] = k[q] == KIND_CLIENT ? make_uint4(0, 0, 0, 0) : etab[sh[q] < n_shapes ? sh[q] : 0];
+    for (int q = 0; q < CPW; ++q) e[q] = etab[(k[q] != KIND_CLIENT && sh[q] < n_shapes) ? sh[q] : 0];
   };
   if (threadIdx.x == 0) dcnt = wcnt = wcount = 0;
   if (threadIdx.x < (1u << KB1_MAX)) lbin[threadIdx.x] = 0;

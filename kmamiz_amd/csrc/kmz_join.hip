@@ -469,10 +469,17 @@ __global__ void __launch_bounds__(1024) k_cert_split(const unsigned long long *_
   if (threadIdx.x < CERT_TPC) {
     uint32_t o = 0;
     if (threadIdx.x < nt) {
+      // (three unconditional loads, in flight together: a load under a branch
+      // -- tsz only for the guard's segment tiles, the next bin's offset only
+      // below the last bin -- made the compiler wait for it at the merge,
+      // before issuing the next)
       const uint32_t t = T0 + threadIdx.x;
-      const uint32_t tsize = tsz ? tsz[t] : min(JT, n - t * JT);  // (tsz: the guard's segment tiles)
-      o = jdir[(uint64_t)t * BINS + b];
-      const uint32_t e = b + 1 < BINS ? jdir[(uint64_t)t * BINS + b + 1] : tsize;
+      const uint16_t *row = jdir + (uint64_t)t * BINS;
+      o = row[b];
+      const uint32_t e1 = row[b + 1 < BINS ? b + 1 : b];
+      const uint32_t tz = (tsz ? tsz : jdir)[t];
+      const uint32_t tsize = tsz ? tz : min(JT, n - t * JT);  // (tsz: the guard's segment tiles)
+      const uint32_t e = b + 1 < BINS ? e1 : tsize;
       c = e - o;
     }
     tcnt[threadIdx.x] = c;

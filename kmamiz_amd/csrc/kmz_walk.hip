@@ -70,9 +70,8 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE_WAVES) k4_tile(const uint8_t *__
   // a CLIENT slot's record holds neither, so half the window skips the gather)
   uint3 e[WPW];
 #pragma unroll
-  for (int q = 0; q < WPW; ++q)
-    e[q] = k[q] == KIND_CLIENT ? make_uint3(0, 0, 0)
-                               : *reinterpret_cast<const uint3 *>(etab + (sh[q] < n_shapes ? sh[q] : 0));
+  for (int q = 0; q < WPW; ++q)  // (unconditional: a CLIENT slot gathers entry 0, unused; see k4_chain)
+    e[q] = *reinterpret_cast<const uint3 *>(etab + ((k[q] != KIND_CLIENT && sh[q] < n_shapes) ? sh[q] : 0));
   // window -> LDS records {element hash, endpoint, local contracted parent | kind << 16}
   bool other = false;  // a span neither SERVER nor CLIENT in the window (rows' lastUsage path)
 #pragma unroll
