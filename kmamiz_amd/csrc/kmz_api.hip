@@ -3194,3 +3194,29 @@ extern "C" int kmz__debug_k4(kmz_ctx *c, unsigned long long *out) {
   out[7] = 1ull << lb1;
   return KMZ_OK;
 }
+
+// diagnostic (tools/diag_lists.py): the chain walk's list use in the last run
+// -- the global lists' counts (staged keys, deferred checks, claimed slots,
+// pending spans) and, for k4_tile9, its per-workgroup regions' totals and
+// maxima (valid keys, claims, deferred checks)
+extern "C" int kmz__debug_chain_lists(kmz_ctx *c, unsigned long long *out) {
+  if (!c || !out) return KMZ_E_ARG;
+  unsigned int cnt[16];
+  if (hipMemcpy(cnt, c->counters.p, sizeof(cnt), hipMemcpyDeviceToHost) != hipSuccess) return KMZ_E_HIP;
+  out[0] = cnt[kmz::C_FSTAGE];
+  out[1] = cnt[kmz::C_FDEFER];
+  out[2] = cnt[kmz::C_WPOS];
+  out[3] = cnt[kmz::C_PLIST];
+  for (int k = 4; k < 10; ++k) out[k] = 0;
+  const uint32_t nt = kmz::walk_tiles((uint32_t)c->n);
+  if (c->wn9.p && c->wn9.bytes >= (size_t)nt * 12) {
+    std::vector<uint32_t> wn((size_t)nt * 3);
+    if (hipMemcpy(wn.data(), c->wn9.p, wn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return KMZ_E_HIP;
+    for (int f = 0; f < 3; ++f)
+      for (uint32_t w = 0; w < nt; ++w) {
+        out[4 + f] += wn[(size_t)f * nt + w];
+        out[7 + f] = std::max<unsigned long long>(out[7 + f], wn[(size_t)f * nt + w]);
+      }
+  }
+  return KMZ_OK;
+}
