@@ -277,9 +277,10 @@ template <int NT, int TW, class Anc>
 __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint64_t (&ps)[TW], uint8_t (&st)[TW],
                                                   const uint8_t (&kq)[TW], const uint32_t (&dd)[TW],
                                                   const uint32_t (&jq)[TW], const uint32_t (&myep)[TW], uint32_t w0,
-                                                  Anc anc, uint32_t *need, const ChainRun &a, uint32_t &rows,
-                                                  uint32_t &rel, uint32_t &maxd, uint32_t &fresh_n, uint32_t &flags,
-                                                  unsigned long long *t9acc, unsigned long long &t9prev) {
+                                                  Anc anc, uint32_t *need, ChainLds &L, uint32_t (&hf)[TW],
+                                                  const ChainRun &a, uint32_t &rows, uint32_t &rel, uint32_t &maxd,
+                                                  uint32_t &fresh_n, uint32_t &flags, unsigned long long *t9acc,
+                                                  unsigned long long &t9prev) {
   const uint32_t spin = spin_bound(a.ablate);
   ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
   uint64_t pos[TW];
@@ -304,15 +305,33 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
       w01[q] = *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
     }
     st[q] = S_DONE;
-    if (w01[q].x == sg[q]) {
-      if (w01[q].y == 0)
-        dfr[q] = true;  // found, not yet published: checked by the settle
-      else if (w01[q].y != ps[q])
-        flags |= F_SIG;
+    if (w01[q].x == sg[q] && w01[q].y != 0) {  // found and published: check it
+      if (w01[q].y != ps[q]) flags |= F_SIG;
       continue;
     }
     if (a.ablate & (1u << 18)) continue;  // diagnostic knob: probe but no inserts
-    lead[q] = true;  // an empty slot (or PROBE_MAX other chains: the CAS fails, the settle inserts)
+    // not found, or found unpublished: one leader per distinct sig in the
+    // workgroup (LDS map; a hot new chain repeats within a tile, and every
+    // repeat's CAS on one address, from every workgroup at once, serialised
+    // the walk, 0.95 -> 1.35 ms); a follower checks the leader's parent sig
+    // after the round's barrier (hf)
+    uint32_t h = (uint32_t)(sig_place(sg[q]) >> 32) & (IMAP - 1);
+    lead[q] = true;  // (a leader without a map slot when the map is full)
+    for (uint32_t t = 0; t < 8; ++t) {
+      const unsigned long long kk = atomicCAS(&L.imap_sig[h], 0ull, (unsigned long long)sg[q]);
+      if (kk == 0) {
+        L.imap_psig[h] = ps[q];
+        break;
+      }
+      if (kk == sg[q]) {
+        lead[q] = false;
+        hf[q] = h;
+        break;
+      }
+      h = (h + 1) & (IMAP - 1);
+    }
+    // a leader finding its chain unpublished defers the check (its CAS
+    // returns the sig: joined); one finding the slot empty claims it
   }
   T9_STAMP(4);
 #if KMZ_T9_BAR
@@ -488,9 +507,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   __shared__ uint32_t lpk[W9];  // window parent | kind << 11 | id << 13
   __shared__ uint16_t wlist[WT];
   __shared__ uint32_t need[4];  // the workgroup's staged keys, claimed slots and deferred checks (chain_round_tail9)
-#if !KMZ_T9_TAIL
-  __shared__ ChainLds L;
-#endif
+  __shared__ ChainLds L;  // (the leader map)
 #if KMZ_T9_LDSPAD  // (A/B builds: LDS held back to cap the workgroups per CU)
   __shared__ uint32_t ldspad[KMZ_T9_LDSPAD / 4];
   if (threadIdx.x == 0) ldspad[(blockIdx.x * 7u) % (KMZ_T9_LDSPAD / 4)] = blockIdx.x;
@@ -517,9 +534,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     e[q] = sw[j];
   }
   if (threadIdx.x < 4) need[threadIdx.x] = threadIdx.x == 2 ? ~0u : 0u;
-#if !KMZ_T9_TAIL
   chain_lds_init(L);
-#endif
   if (threadIdx.x < 3) {
     lpk[WW + threadIdx.x] = (WW + threadIdx.x) | ((uint32_t)KIND_CLIENT << P9_BITS) | (ID9_NONE << (P9_BITS + 2));
     lel[WW + threadIdx.x] = 0;
@@ -663,10 +678,17 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     }
     T9_STAMP(3);
 #if KMZ_T9_TAIL
+    uint32_t hf[TW];  // a follower's leader-map slot (IMAP + 1: none)
+#pragma unroll
+    for (int q = 0; q < TW; ++q) hf[q] = IMAP + 1;
     chain_round_tail9<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
       const uint32_t pk = lpk[x];
       return AncRec{p9_id(pk), p9_kind(pk), p9_parent(pk)};
-    }, need, a, rows, rel, maxd, fresh_n, flags, t9acc, t9prev);
+    }, need, L, hf, a, rows, rel, maxd, fresh_n, flags, t9acc, t9prev);
+    __syncthreads();  // (the leaders' parent sigs are in the map; it stays for a next round, as k4_tile8's)
+#pragma unroll
+    for (int q = 0; q < TW; ++q)
+      if (hf[q] <= IMAP && L.imap_psig[hf[q]] != ps[q]) flags |= F_SIG;
 #else  // (A/B: k4_tile8's tail -- LDS leader map, lists reserved per workgroup with device atomics)
     chain_round_tail<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
       const uint32_t pk = lpk[x];
