@@ -237,6 +237,11 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #ifndef KMZ_T9_X
 #define KMZ_T9_X 0  // (timing-only A/B builds, wrong results) 1: no list writes, 2: no claims, 4: no probes
 #endif
+#ifndef KMZ_WG_REGIONS
+#define KMZ_WG_REGIONS 1  // 0 (A/B build): k4_tile9's list entries all in the global lists
+#endif
+constexpr uint32_t R_STAGE = KMZ_WG_REGIONS ? WG_STAGE : 0, R_POS = KMZ_WG_REGIONS ? WG_POS : 0,
+                   R_DEFER = KMZ_WG_REGIONS ? WG_DEFER : 0;
 #ifndef KMZ_T9_BAR
 #define KMZ_T9_BAR 0  // 1 (A/B build): workgroup barriers after the probes and after the claims, as k4_tile8's tail
 #endif
@@ -378,12 +383,12 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
         if (lane == 0) base = atomicAdd(&need[1], (uint32_t)__popcll(mk));
         base = __shfl(base, 0, 64);
         const uint32_t o = base + (uint32_t)__popcll(mk & lt);
-        const uint64_t mo = __ballot(won && o >= WG_POS);
+        const uint64_t mo = __ballot(won && o >= R_POS);
         uint32_t gb = 0;
         if (mo && lane == 0) gb = atomicAdd(&a.counters[C_WPOS], (uint32_t)__popcll(mo));
         gb = __shfl(gb, 0, 64);
         if (won) {
-          if (o < WG_POS) {
+          if (o < R_POS) {
             a.wgpos[(uint64_t)blk * WG_POS + o] = (uint32_t)pos[q];
           } else {
             const uint32_t x = gb + (uint32_t)__popcll(mo & lt);
@@ -414,7 +419,7 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
       base = __shfl(base, 0, 64);
       unsigned long long *dst;
       uint64_t cap;
-      if (base + tot <= WG_STAGE) {  // (wave-uniform)
+      if (base + tot <= R_STAGE) {  // (wave-uniform)
         dst = a.wstage + (uint64_t)blk * WG_STAGE + base + pre;
         cap = nd;
       } else {  // (the region's valid keys end where the first reservation past it starts: need[2])
@@ -451,13 +456,13 @@ __device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint
       if (lane == 0) base = atomicAdd(&need[3], (uint32_t)__popcll(md));
       base = __shfl(base, 0, 64);
       const uint32_t o = base + (uint32_t)__popcll(md & lt);
-      const uint64_t mo = __ballot(dq && o >= WG_DEFER);
+      const uint64_t mo = __ballot(dq && o >= R_DEFER);
       uint32_t gb = 0;
       if (mo && lane == 0) gb = atomicAdd(&a.counters[C_FDEFER], (uint32_t)__popcll(mo));
       gb = __shfl(gb, 0, 64);
       if (dq) {
         const uint32_t x = gb + (uint32_t)__popcll(mo & lt);
-        if (o < WG_DEFER) {
+        if (o < R_DEFER) {
           *reinterpret_cast<ulonglong2 *>(a.wdefer + 2 * ((uint64_t)blk * WG_DEFER + o)) =
               make_ulonglong2(sg[q], ps[q]);
         } else if (x < a.dcap) {
