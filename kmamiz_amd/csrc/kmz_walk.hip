@@ -705,8 +705,8 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   __syncthreads();  // (the workgroup's list counts are final)
   if (threadIdx.x == 0) {
     a.wn[blockIdx.x] = min(need[0], need[2]);  // (the region's valid keys)
-    a.wn[a.ntiles + blockIdx.x] = need[1];
-    a.wn[2 * a.ntiles + blockIdx.x] = need[3];
+    a.wn[a.ntiles + blockIdx.x] = min(need[1], R_POS);
+    a.wn[2 * a.ntiles + blockIdx.x] = min(need[3], R_DEFER);
   }
   if (flags) atomicOr(&a.counters[C_FLAGS], flags);
   T9_STAMP(8);
