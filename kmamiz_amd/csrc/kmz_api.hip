@@ -89,7 +89,6 @@ struct kmz_ctx {
   uint64_t imap_n = 0;     // 0: contiguous batch (index_base + i)
   DevBuf ctile;           // K4 per-workgroup stats (apart from K3's tile_tmp: the two run concurrently)
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
-  DevBuf wstage9, wgpos9, wdefer9, wn9;  // k4_tile9's per-workgroup lists and their counts (ChainRun::wstage ...)
   // service tail (kmz_tail.hip): maps, pair set / table, outputs, link-key buckets
   DevBuf tl_svc, tl_cls, tl_lsvc, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs, tl_cnt, tl_sstat, tl_rel,
       tl_lbkt, tl_lbn;
@@ -409,7 +408,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->wstage9, &c->wgpos9, &c->wdefer9, &c->wn9, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->rt_tsz, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->rt_tsz, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt,
                     &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->tl_lbkt, &c->tl_lbn, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
@@ -1246,11 +1245,8 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     return KMZ_E_HIP;
   const bool w8 = !(c->ablate2 & 1024u), by_shape = w8 && c->dep_valid && !(c->ablate2 & 2048u);
   // k4_tile9 where the ids fit its 19-bit record field (KMZ_ABLATE2 bit 22:
-  // k4_tile8, for comparison); its per-workgroup lists
+  // k4_tile8, for comparison)
   const bool w9 = w8 && !(c->ablate2 & (1u << 22)) && chain_tile9_fits(by_shape ? c->n_shapes : c->n_dep);
-  if (w9 && (ensure(c, c->wstage9, (size_t)nt * WG_STAGE * 8) || ensure(c, c->wgpos9, (size_t)nt * WG_POS * 4) ||
-             ensure(c, c->wdefer9, (size_t)nt * WG_DEFER * 16) || ensure(c, c->wn9, (size_t)nt * 3 * 4)))
-    return KMZ_E_HIP;
   if (c->ctab.p != old_ctab) c->ctab_dirty = true;
   uint32_t *gpos = P<uint32_t>(c->kwpos);
   {
@@ -1291,13 +1287,6 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     // keys' shapes to endpoints
     a.id_ep = by_shape ? P<uint32_t>(c->d_dep) : nullptr;
     a.n_ids = c->n_shapes;
-    if (w9) {
-      a.wstage = P<unsigned long long>(c->wstage9);
-      a.wgpos = P<uint32_t>(c->wgpos9);
-      a.wdefer = P<unsigned long long>(c->wdefer9);
-      a.wn = P<uint32_t>(c->wn9);
-      a.ntiles = nt;
-    }
     {
       Timed t(c, KMZ_K_WALK);
       if (w9)
@@ -1319,9 +1308,7 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     launch_chain_settle_list(c->stream, nt, c->ctab.p, c->ccap, P<unsigned long long>(c->trip), c->tcap, cnt,
                              P<uint32_t>(c->ctile), st, P<unsigned long long>(c->kstage), (uint32_t)stot,
                              P<unsigned long long>(c->kdefer), (uint32_t)dtot, gpos, (uint32_t)gtot, c->ablate,
-                             by_shape ? P<uint32_t>(c->d_dep) : nullptr, c->n_shapes,
-                             w9 ? P<unsigned long long>(c->wstage9) : nullptr, w9 ? P<uint32_t>(c->wn9) : nullptr,
-                             w9 ? P<unsigned long long>(c->wdefer9) : nullptr);
+                             by_shape ? P<uint32_t>(c->d_dep) : nullptr, c->n_shapes);
   }
   {
     Timed t(c, KMZ_K_PEND);
@@ -1337,8 +1324,7 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
     launch_collapse_endpoints(c->stream, P<unsigned long long>(c->sgrp), c->n_shapes, c->n_status,
                               P<uint32_t>(c->d_dep), c->n_dep, P<uint32_t>(c->cparent), c->index_base, epp,
                               epp + c->n_dep, cnt);
-    launch_chain_clear_list(c->stream, c->ctab.p, gpos, (uint32_t)gtot, cnt, w9 ? P<uint32_t>(c->wgpos9) : nullptr,
-                            w9 ? P<uint32_t>(c->wn9) + nt : nullptr, w9 ? nt : 0u);
+    launch_chain_clear_list(c->stream, c->ctab.p, gpos, (uint32_t)gtot, cnt);
   }
   c->ctab_dirty = false;  // (set again after the run if the list overflowed: F_CTAB_DIRTY)
   c->path = (joined ? 1 : 0) | 2 | 32 | (w9 ? 64 : 0);
@@ -1789,8 +1775,7 @@ static uint64_t run_key(kmz_ctx *c, uint32_t flags) {
                     &c->trip, &c->trip_out, &c->counters, &c->stats64, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey, &c->mval,
                     &c->ctab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n, &c->cetab, &c->kbucket,
-                    &c->kbucket_n, &c->ctile, &c->kwpos, &c->kwpos_n, &c->wstage9, &c->wgpos9, &c->wdefer9,
-                    &c->wn9}) {
+                    &c->kbucket_n, &c->ctile, &c->kwpos, &c->kwpos_n}) {
     mix((uint64_t)(uintptr_t)b->p);
     mix(b->bytes);
   }
@@ -3195,10 +3180,9 @@ extern "C" int kmz__debug_k4(kmz_ctx *c, unsigned long long *out) {
   return KMZ_OK;
 }
 
-// diagnostic (tools/diag_lists.py): the chain walk's list use in the last run
-// -- the global lists' counts (staged keys, deferred checks, claimed slots,
-// pending spans) and, for k4_tile9, its per-workgroup regions' totals and
-// maxima (valid keys, claims, deferred checks)
+// diagnostic (tools/diag_lists.py): the chain walk's global lists in the last
+// run -- staged keys, deferred checks, claimed slots (outside the tile kernel's
+// per-workgroup reservations: all of them for k4_tile8/9), pending spans
 extern "C" int kmz__debug_chain_lists(kmz_ctx *c, unsigned long long *out) {
   if (!c || !out) return KMZ_E_ARG;
   unsigned int cnt[16];
@@ -3207,16 +3191,5 @@ extern "C" int kmz__debug_chain_lists(kmz_ctx *c, unsigned long long *out) {
   out[1] = cnt[kmz::C_FDEFER];
   out[2] = cnt[kmz::C_WPOS];
   out[3] = cnt[kmz::C_PLIST];
-  for (int k = 4; k < 10; ++k) out[k] = 0;
-  const uint32_t nt = kmz::walk_tiles((uint32_t)c->n);
-  if (c->wn9.p && c->wn9.bytes >= (size_t)nt * 12) {
-    std::vector<uint32_t> wn((size_t)nt * 3);
-    if (hipMemcpy(wn.data(), c->wn9.p, wn.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return KMZ_E_HIP;
-    for (int f = 0; f < 3; ++f)
-      for (uint32_t w = 0; w < nt; ++w) {
-        out[4 + f] += wn[(size_t)f * nt + w];
-        out[7 + f] = std::max<unsigned long long>(out[7 + f], wn[(size_t)f * nt + w]);
-      }
-  }
   return KMZ_OK;
 }

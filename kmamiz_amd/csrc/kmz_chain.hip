@@ -1106,14 +1106,9 @@ __global__ void __launch_bounds__(256) k_chain_clear(unsigned long long *__restr
                                                      const uint32_t *__restrict__ gpos, uint32_t gcap,
                                                      const unsigned int *__restrict__ counters) {
   auto clear = [&](uint32_t p) { *reinterpret_cast<ulonglong2 *>(ctab + 2 * (uint64_t)p) = make_ulonglong2(0, 0); };
-  if (wcap <= 256) {  // (many small regions, k4_tile9's: one thread per region slot)
-    for (uint64_t x = blockIdx.x * 256ull + threadIdx.x; x < (uint64_t)nwg * wcap; x += gridDim.x * 256ull)
-      if (x % wcap < min(wpos_n[x / wcap], wcap)) clear(wpos[x]);
-  } else {
-    for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
-      const uint32_t m = min(wpos_n[w], wcap);  // (a count past the region: the rest went to the global list)
-      for (uint32_t x = threadIdx.x; x < m; x += 256) clear(wpos[(uint64_t)w * wcap + x]);
-    }
+  for (uint32_t w = blockIdx.x; w < nwg; w += gridDim.x) {
+    const uint32_t m = min(wpos_n[w], wcap);
+    for (uint32_t x = threadIdx.x; x < m; x += 256) clear(wpos[(uint64_t)w * wcap + x]);
   }
   const uint32_t mg = min(counters[C_WPOS], gcap);
   for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < mg; x += gridDim.x * 256) clear(gpos[x]);
@@ -1127,11 +1122,9 @@ void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *w
                      wcap, wpos_n, g, gpos, gcap, counters);
 }
 
-void launch_chain_clear_list(hipStream_t s, void *ctab, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters,
-                             const uint32_t *wgpos, const uint32_t *wn_pos, uint32_t nwg) {
-  hipLaunchKernelGGL(k_chain_clear, dim3(1024), dim3(256), 0, s, reinterpret_cast<unsigned long long *>(ctab),
-                     wgpos ? wgpos : gpos, wgpos ? WG_POS : 0u, wgpos ? wn_pos : gpos, wgpos ? nwg : 0u, gpos, gcap,
-                     counters);
+void launch_chain_clear_list(hipStream_t s, void *ctab, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters) {
+  hipLaunchKernelGGL(k_chain_clear, dim3(1024), dim3(256), 0, s, reinterpret_cast<unsigned long long *>(ctab), gpos, 0u,
+                     gpos, 0u, gpos, gcap, counters);
 }
 
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,

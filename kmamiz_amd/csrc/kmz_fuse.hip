@@ -416,10 +416,7 @@ __global__ void __launch_bounds__(256) k_chain_settle_list(const unsigned long l
                                                            unsigned int *__restrict__ counters,
                                                            unsigned long long *__restrict__ stats64,
                                                            uint32_t *__restrict__ gpos, uint32_t gcap, uint32_t spin,
-                                                           const uint32_t *__restrict__ id_ep, uint32_t n_ids,
-                                                           const unsigned long long *__restrict__ wstage,
-                                                           const uint32_t *__restrict__ wn, uint32_t nwg,
-                                                           const unsigned long long *__restrict__ wdefer) {
+                                                           const uint32_t *__restrict__ id_ep, uint32_t n_ids) {
   const uint32_t m = min(counters[C_FSTAGE], scap), md = min(counters[C_FDEFER], dcap);
   const uint32_t t0 = blockIdx.x * 256 + threadIdx.x, ts = gridDim.x * 256;
   uint32_t flags = 0, fresh = 0;
@@ -427,14 +424,6 @@ __global__ void __launch_bounds__(256) k_chain_settle_list(const unsigned long l
   // endpoint keys -- the gathers the walk left out)
   for (uint32_t x = t0; x < m; x += ts)
     edge_insert(id_ep ? key_ids_to_eps(stage[x], id_ep, n_ids) : stage[x], trip, tcap, &flags);
-  // k4_tile9's per-workgroup regions (wn[w]: the valid keys at the start of
-  // tile w's region; the rest of its keys are in the global list)
-  if (wstage)
-    for (uint64_t x = t0; x < (uint64_t)nwg * WG_STAGE; x += ts) {
-      const uint32_t w = (uint32_t)(x / WG_STAGE), k = (uint32_t)(x % WG_STAGE);
-      if (k < wn[w] && k < WG_STAGE)
-        edge_insert(id_ep ? key_ids_to_eps(wstage[x], id_ep, n_ids) : wstage[x], trip, tcap, &flags);
-    }
   for (uint32_t x = t0; x < md; x += ts) {
     const unsigned long long *r = defer + 2 * (uint64_t)x;
     int rr = 0;
@@ -442,16 +431,6 @@ __global__ void __launch_bounds__(256) k_chain_settle_list(const unsigned long l
     if (rr == 0) flags |= F_SPIN;
     fresh += rr == 1;
   }
-  if (wdefer)  // (k4_tile9's per-workgroup deferred checks: wn[2 * nwg + w] of them, the first WG_DEFER in its region)
-    for (uint64_t x = t0; x < (uint64_t)nwg * WG_DEFER; x += ts) {
-      const uint32_t w = (uint32_t)(x / WG_DEFER), k = (uint32_t)(x % WG_DEFER);
-      if (k >= wn[2 * (uint64_t)nwg + w]) continue;
-      const unsigned long long *r = wdefer + 2 * x;
-      int rr = 0;
-      for (uint32_t t = 0; t < spin && rr == 0; ++t) rr = chain_put(ctab, ccap, r[0], r[1], &flags, gpos, gcap, counters);
-      if (rr == 0) flags |= F_SPIN;
-      fresh += rr == 1;
-    }
   if (flags) atomicOr(&counters[C_FLAGS], flags);
   for (int o = 32; o > 0; o >>= 1) fresh += __shfl_xor(fresh, o, 64);
   if ((threadIdx.x & 63) == 0 && fresh) atomicAdd(&stats64[S_CHAINS], (unsigned long long)fresh);
@@ -477,12 +456,11 @@ void launch_chain_settle_list(hipStream_t s, uint32_t nt, void *ctab, uint64_t c
                               uint64_t tcap, unsigned int *counters, const uint32_t *tile_stats,
                               unsigned long long *stats64, const unsigned long long *stage, uint32_t scap,
                               const unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap,
-                              uint32_t ablate, const uint32_t *id_ep, uint32_t n_ids, const unsigned long long *wstage,
-                              const uint32_t *wn, const unsigned long long *wdefer) {
+                              uint32_t ablate, const uint32_t *id_ep, uint32_t n_ids) {
   if (!nt) return;
   hipLaunchKernelGGL(k_chain_settle_list, dim3(std::min<uint32_t>(2048, std::max<uint32_t>(64, nt))), dim3(256), 0, s,
                      stage, scap, defer, dcap, trip, tcap, reinterpret_cast<unsigned long long *>(ctab), ccap, counters,
-                     stats64, gpos, gcap, spin_bound(ablate), id_ep, n_ids, wstage, wn, nt, wdefer);
+                     stats64, gpos, gcap, spin_bound(ablate), id_ep, n_ids);
   launch_tile_sum(s, tile_stats, nt, 4u, 4u, stats64 + S_ROWS, 2u);  // rows, rel, maxd, chains
 }
 

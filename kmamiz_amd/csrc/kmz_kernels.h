@@ -199,9 +199,7 @@ void launch_chain_settle_list(hipStream_t s, uint32_t nt, void *ctab, uint64_t c
                               uint64_t tcap, unsigned int *counters, const uint32_t *tile_stats,
                               unsigned long long *stats64, const unsigned long long *stage, uint32_t scap,
                               const unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap,
-                              uint32_t ablate = 0, const uint32_t *id_ep = nullptr, uint32_t n_ids = 0,
-                              const unsigned long long *wstage = nullptr, const uint32_t *wn = nullptr,
-                              const unsigned long long *wdefer = nullptr);
+                              uint32_t ablate = 0, const uint32_t *id_ep = nullptr, uint32_t n_ids = 0);
 // K4 chain interning, one workgroup per tile (kmz_walk.hip); same global
 // lists as the fused kernel (settled by launch_chain_settle_list over walk_tiles)
 struct ChainRun;
@@ -216,16 +214,13 @@ void launch_chain_tile8(hipStream_t s, const uint8_t *kind, const uint32_t *shap
 // and sentinel-terminated walks; ids (shapes, or gathered endpoints) below
 // 2^19 - 1 (chain_tile9_fits)
 bool chain_tile9_fits(uint32_t n_ids);
-constexpr uint32_t WG_STAGE = 64, WG_POS = 16, WG_DEFER = 16;  // k4_tile9's per-workgroup list capacities (ChainRun)
 void launch_chain_tile9(hipStream_t s, const uint8_t *kind, const uint32_t *shape, const uint32_t *cparent, uint32_t n,
                         const uint32_t *dep_ep, uint32_t n_shapes, uint32_t *tile_stats, const ChainRun &a);
 // zero the chain-table entries this run wrote (instead of a memset of the table)
 void launch_chain_clear(hipStream_t s, uint32_t n, void *ctab, const uint32_t *wpos, uint32_t wcap,
                         const uint32_t *wpos_n, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);
-// (the global list only: the fused kernel's claimed slots; with wgpos, also
-// k4_tile9's per-workgroup regions of nwg tiles, counts at wn_pos)
-void launch_chain_clear_list(hipStream_t s, void *ctab, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters,
-                             const uint32_t *wgpos = nullptr, const uint32_t *wn_pos = nullptr, uint32_t nwg = 0);
+// (the global list only: the fused kernel's claimed slots)
+void launch_chain_clear_list(hipStream_t s, void *ctab, const uint32_t *gpos, uint32_t gcap, const unsigned int *counters);
 void launch_chain_pend(hipStream_t s, const uint32_t *plist, uint32_t pcap, const uint8_t *kind,
                        const uint32_t *shape, const int64_t *ts, const uint32_t *cparent, uint32_t n,
                        const uint32_t *dep_ep,

@@ -229,278 +229,6 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #ifndef KMZ_TILE9_WAVES
 #define KMZ_TILE9_WAVES 7
 #endif
-// diagnostic phase clocks of k4_tile9 (a -DKMZ_T9_CLOCKS=1 build only):
-// s_memtime deltas seen by thread 0, summed over workgroups (kmz__debug_walk9)
-#ifndef KMZ_T9_TAIL
-#define KMZ_T9_TAIL 1  // 0 (A/B build): k4_tile8's round tail (chain_round_tail) in k4_tile9
-#endif
-#ifndef KMZ_T9_X
-#define KMZ_T9_X 0  // (timing-only A/B builds, wrong results) 1: no list writes, 2: no claims, 4: no probes
-#endif
-#ifndef KMZ_WG_REGIONS
-#define KMZ_WG_REGIONS 1  // 0 (A/B build): k4_tile9's list entries all in the global lists
-#endif
-constexpr uint32_t R_STAGE = KMZ_WG_REGIONS ? WG_STAGE : 0, R_POS = KMZ_WG_REGIONS ? WG_POS : 0,
-                   R_DEFER = KMZ_WG_REGIONS ? WG_DEFER : 0;
-#ifndef KMZ_T9_BAR
-#define KMZ_T9_BAR 0  // 1 (A/B build): workgroup barriers after the probes and after the claims, as k4_tile8's tail
-#endif
-#ifndef KMZ_T9_LDSPAD
-#define KMZ_T9_LDSPAD 0
-#endif
-#ifndef KMZ_T9_CLOCKS
-#define KMZ_T9_CLOCKS 0
-#endif
-__device__ unsigned long long g_walk9_dbg[12];
-#if KMZ_T9_CLOCKS
-#define T9_STAMP(k)                                             \
-  {                                                             \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    if (threadIdx.x == 0 && t9prev) t9acc[k] += t_ - t9prev;    \
-    t9prev = t_;                                                \
-  }
-#else
-#define T9_STAMP(k)
-#endif
-
-// k4_tile9's probe / claim / lists (against chain_round_tail: fewer dependent
-// round trips per workgroup).  A walker whose probe finds its chain checks
-// the parent sig; one that finds the home slot empty claims it with one CAS
-// (no LDS leader map: two walkers of a workgroup with the same new chain,
-// 0.4 % of them, both CAS and the second defers); the winner publishes its
-// parent sig and stages its keys.  Its list entries are placed by an LDS add
-// in the workgroup's own region of each list (WG_STAGE keys, WG_POS claimed
-// slots: no device atomic and no barrier between the claim and the writes);
-// past the region a device atomic reserves them in the global list.  A claim
-// that lost the slot, or a chain found unpublished, goes to the deferred
-// checks (global list, as before).  need[0] / need[1]: the workgroup's key /
-// claim counts so far; need[2]: where the first key reservation that did not
-// fit the region started (its keys, and every later one's, went to the global
-// list), so the region's valid keys are the first min(need[0], need[2]);
-// need[3]: deferred checks (the first WG_DEFER in the workgroup's region).
-template <int NT, int TW, class Anc>
-__device__ __forceinline__ void chain_round_tail9(uint64_t (&sg)[TW], const uint64_t (&ps)[TW], uint8_t (&st)[TW],
-                                                  const uint8_t (&kq)[TW], const uint32_t (&dd)[TW],
-                                                  const uint32_t (&jq)[TW], const uint32_t (&myep)[TW], uint32_t w0,
-                                                  Anc anc, uint32_t *need, ChainLds &L, uint32_t (&hf)[TW],
-                                                  const ChainRun &a, uint32_t &rows, uint32_t &rel, uint32_t &maxd,
-                                                  uint32_t &fresh_n, uint32_t &flags, unsigned long long *t9acc,
-                                                  unsigned long long &t9prev) {
-  const uint32_t spin = spin_bound(a.ablate);
-  ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
-  uint64_t pos[TW];
-  // (unconditional loads, slot 0 for a walker that does not probe: the
-  // branchy form let the compiler wait for the first probe before issuing
-  // the second -- two round trips instead of one, walk 0.95 -> 1.35 ms)
-#pragma unroll
-  for (int q = 0; q < TW; ++q) {
-    pos[q] = st[q] == S_PUT ? cslot(sg[q], a.ccap) : 0;
-    w01[q] = (KMZ_T9_X & 4) ? make_ulonglong2(sg[q], ps[q]) : *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
-  }
-#pragma unroll
-  for (int q = 0; q < TW; ++q)
-    if (st[q] != S_PUT) w01[q] = make_ulonglong2(0, 0);
-  bool lead[TW], dfr[TW];
-#pragma unroll
-  for (int q = 0; q < TW; ++q) {
-    lead[q] = dfr[q] = false;
-    if (st[q] != S_PUT) continue;
-    for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
-      pos[q] = pos[q] + 1 == a.ccap ? 0 : pos[q] + 1;
-      w01[q] = *reinterpret_cast<const ulonglong2 *>(a.ctab + 2 * pos[q]);
-    }
-    st[q] = S_DONE;
-    if (w01[q].x == sg[q] && w01[q].y != 0) {  // found and published: check it
-      if (w01[q].y != ps[q]) flags |= F_SIG;
-      continue;
-    }
-    if (a.ablate & (1u << 18)) continue;  // diagnostic knob: probe but no inserts
-    // not found, or found unpublished: one leader per distinct sig in the
-    // workgroup (LDS map; a hot new chain repeats within a tile, and every
-    // repeat's CAS on one address, from every workgroup at once, serialised
-    // the walk, 0.95 -> 1.35 ms); a follower checks the leader's parent sig
-    // after the round's barrier (hf)
-    uint32_t h = (uint32_t)(sig_place(sg[q]) >> 32) & (IMAP - 1);
-    lead[q] = true;  // (a leader without a map slot when the map is full)
-    for (uint32_t t = 0; t < 8; ++t) {
-      const unsigned long long kk = atomicCAS(&L.imap_sig[h], 0ull, (unsigned long long)sg[q]);
-      if (kk == 0) {
-        L.imap_psig[h] = ps[q];
-        break;
-      }
-      if (kk == sg[q]) {
-        lead[q] = false;
-        hf[q] = h;
-        break;
-      }
-      h = (h + 1) & (IMAP - 1);
-    }
-    // a leader finding its chain unpublished defers the check (its CAS
-    // returns the sig: joined); one finding the slot empty claims it
-  }
-  T9_STAMP(4);
-#if KMZ_T9_BAR
-  __syncthreads();
-#endif
-  // the claims, all in flight together; a winner publishes at once
-  unsigned long long cvq[TW];
-#pragma unroll
-  for (int q = 0; q < TW; ++q) {
-    cvq[q] = 0;
-    if (!lead[q]) continue;
-    unsigned long long *en = a.ctab + 2 * pos[q];
-    if (KMZ_T9_X & 2) continue;
-    cvq[q] = atomicCAS(&en[0], 0ull, (unsigned long long)sg[q]);
-    if (cvq[q] == 0) atomicExch(&en[1], (unsigned long long)ps[q]);
-  }
-#if KMZ_T9_CLOCKS
-  if (__ballot(cvq[0] == 1234567 || cvq[TW - 1] == 1234567)) flags |= 0;  // (waits for the claims)
-#endif
-  T9_STAMP(5);
-#if KMZ_T9_BAR
-  __syncthreads();
-#endif
-  const uint32_t blk = blockIdx.x, lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1;  // (the lanes below this one)
-  // The list entries, reserved per wave: one LDS add for the wave's entries in
-  // the workgroup's region, and -- for a wave whose entries do not fit it --
-  // one device atomic for all of them in the global list.  (The workgroups
-  // that run first find nearly every chain new, ~480 claims and ~2000 keys
-  // each: a device atomic per walker on one counter serialised them, walk
-  // 0.67 -> 1.33 ms on the mesh.)  Every lane takes part in the ballots and
-  // shuffles; the per-walker work is predicated.
-#pragma unroll
-  for (int q = 0; q < TW; ++q) {
-    if (KMZ_T9_X & 1) break;
-    const uint32_t d = dd[q];
-    const bool won = lead[q] && cvq[q] == 0;
-    fresh_n += won;
-    // claimed slots (cleared after the run)
-    {
-      const uint64_t mk = __ballot(won);
-      if (mk) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&need[1], (uint32_t)__popcll(mk));
-        base = __shfl(base, 0, 64);
-        const uint32_t o = base + (uint32_t)__popcll(mk & lt);
-        const uint64_t mo = __ballot(won && o >= R_POS);
-        uint32_t gb = 0;
-        if (mo && lane == 0) gb = atomicAdd(&a.counters[C_WPOS], (uint32_t)__popcll(mo));
-        gb = __shfl(gb, 0, 64);
-        if (won) {
-          if (o < R_POS) {
-            a.wgpos[(uint64_t)blk * WG_POS + o] = (uint32_t)pos[q];
-          } else {
-            const uint32_t x = gb + (uint32_t)__popcll(mo & lt);
-            if (x < a.gcap)
-              a.gpos[x] = (uint32_t)pos[q];
-            else
-              flags |= F_CTAB_DIRTY;
-          }
-        }
-      }
-    }
-    // a row whose chain this walker inserted (or lost to another chain: the
-    // deferred check may insert it) stages its keys (ancestor k, row id, k,
-    // ancestor is SERVER); one that joined the same chain leaves them to the
-    // winner (knob 19: diagnostic, none)
-    const bool stg = lead[q] && kq[q] == KIND_SERVER && d && cvq[q] != sg[q] && !(a.ablate & (1u << 19));
-    if (__ballot(stg)) {
-      const uint32_t nd = stg ? d : 0u;
-      uint32_t incl = nd;  // the wave's inclusive scan of the key counts
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= (uint32_t)o) incl += y;
-      }
-      const uint32_t tot = __shfl(incl, 63, 64), pre = incl - nd;
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&need[0], tot);
-      base = __shfl(base, 0, 64);
-      unsigned long long *dst;
-      uint64_t cap;
-      if (base + tot <= R_STAGE) {  // (wave-uniform)
-        dst = a.wstage + (uint64_t)blk * WG_STAGE + base + pre;
-        cap = nd;
-      } else {  // (the region's valid keys end where the first reservation past it starts: need[2])
-        uint32_t gb = 0;
-        if (lane == 0) {
-          atomicMin(&need[2], base);
-          gb = atomicAdd(&a.counters[C_FSTAGE], tot);
-        }
-        gb = __shfl(gb, 0, 64);
-        dst = a.stage + gb + pre;
-        cap = gb + pre < a.scap ? a.scap - (gb + pre) : 0;
-      }
-      if (stg) {
-        uint32_t an = anc(jq[q]).parent;
-        for (uint32_t kk = 1; kk <= d; ++kk) {
-          const AncRec r = anc(an);
-          const uint64_t key = edge_key(r.ep, myep[q], kk, r.kind == KIND_SERVER);
-          if (kk - 1 < cap) {
-            dst[kk - 1] = key;
-          } else {
-            edge_insert(a.id_ep ? key_ids_to_eps(key, a.id_ep, a.n_ids) : key, a.trip, a.tcap, &flags);
-            flags |= F_STAGE_FULL;
-          }
-          an = r.parent;
-        }
-      }
-    }
-    // deferred checks: found unpublished, joined an unpublished claim, or
-    // lost the slot to another chain
-    const bool dq = dfr[q] || cvq[q] != 0;
-    const uint64_t md = __ballot(dq);
-    if (md) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&need[3], (uint32_t)__popcll(md));
-      base = __shfl(base, 0, 64);
-      const uint32_t o = base + (uint32_t)__popcll(md & lt);
-      const uint64_t mo = __ballot(dq && o >= R_DEFER);
-      uint32_t gb = 0;
-      if (mo && lane == 0) gb = atomicAdd(&a.counters[C_FDEFER], (uint32_t)__popcll(mo));
-      gb = __shfl(gb, 0, 64);
-      if (dq) {
-        const uint32_t x = gb + (uint32_t)__popcll(mo & lt);
-        if (o < R_DEFER) {
-          *reinterpret_cast<ulonglong2 *>(a.wdefer + 2 * ((uint64_t)blk * WG_DEFER + o)) =
-              make_ulonglong2(sg[q], ps[q]);
-        } else if (x < a.dcap) {
-          *reinterpret_cast<ulonglong2 *>(a.defer + 2 * (uint64_t)x) = make_ulonglong2(sg[q], ps[q]);
-        } else {
-          int rr = 0;
-          for (uint32_t t = 0; t < spin && rr == 0; ++t)
-            rr = chain_put(a.ctab, a.ccap, sg[q], ps[q], &flags, a.gpos, a.gcap, a.counters);
-          if (rr == 0) flags |= F_SPIN;  // unchecked: the run is redone on the exact walk
-          fresh_n += rr == 1;
-        }
-      }
-    }
-  }
-  T9_STAMP(6);
-  // per walker: row counts, pending list, rowpos
-#pragma unroll
-  for (int q = 0; q < TW; ++q) {
-    if (kq[q] == KIND_CLIENT) continue;  // (an empty walker slot)
-    const uint32_t i = w0 + jq[q];
-    const bool pending = st[q] == S_PEND;
-    uint64_t rp = NONE64;
-    if (kq[q] == KIND_SERVER) {
-      rp = a.index_base + i;
-      if (!pending) {
-        ++rows;
-        rel += dd[q];
-        maxd = max(maxd, dd[q]);
-      }
-    }
-    if (pending) {
-      const uint32_t x = atomicAdd(&a.counters[C_PLIST], 1u);
-      if (x < a.pcap) a.plist[x] = i;
-    }
-    if (a.rowpos_out) a.rowpos_out[i] = rp;
-  }
-  T9_STAMP(7);
-}
 template <bool BY_SHAPE>
 __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *__restrict__ kind,
                                                                  const uint32_t *__restrict__ shape,
@@ -511,20 +239,13 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   __shared__ uint64_t lel[W9];  // element hash (0 on the sentinels)
   __shared__ uint32_t lpk[W9];  // window parent | kind << 11 | id << 13
   __shared__ uint16_t wlist[WT];
-  __shared__ uint32_t need[4];  // the workgroup's staged keys, claimed slots and deferred checks (chain_round_tail9)
-  __shared__ ChainLds L;  // (the leader map)
-#if KMZ_T9_LDSPAD  // (A/B builds: LDS held back to cap the workgroups per CU)
-  __shared__ uint32_t ldspad[KMZ_T9_LDSPAD / 4];
-  if (threadIdx.x == 0) ldspad[(blockIdx.x * 7u) % (KMZ_T9_LDSPAD / 4)] = blockIdx.x;
-#endif
+  __shared__ ChainLds L;
   __shared__ uint32_t wcnt[WPT][NW];
   __shared__ uint32_t red[NW][4];
   const uint32_t t0 = blockIdx.x * WT, t1 = min(n, t0 + WT);
   const uint32_t w0 = t0 > WH ? t0 - WH : 0, w1 = min(n, t1 + WH), wn = w1 - w0, toff = t0 - w0;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t flags = 0;
-  unsigned long long t9acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t9prev = 0;
-  T9_STAMP(0);
   uint32_t c[WPW], e[WPW];
   uint8_t k[WPW];
   const uint32_t *__restrict__ cpw = cparent + w0;
@@ -538,7 +259,6 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     k[q] = kw[j];
     e[q] = sw[j];
   }
-  if (threadIdx.x < 4) need[threadIdx.x] = threadIdx.x == 2 ? ~0u : 0u;
   chain_lds_init(L);
   if (threadIdx.x < 3) {
     lpk[WW + threadIdx.x] = (WW + threadIdx.x) | ((uint32_t)KIND_CLIENT << P9_BITS) | (ID9_NONE << (P9_BITS + 2));
@@ -566,7 +286,6 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     other |= jl < wn && kk != KIND_SERVER && kk != KIND_CLIENT;
   }
   const bool any_other = __syncthreads_or(other);
-  T9_STAMP(0);
   // the tile's non-CLIENT spans -> wlist: a ballot per slot row, per-wave
   // counts in LDS, each lane's place from them and its rank in the ballot
   uint64_t mk[WPT];
@@ -595,7 +314,6 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
     m += all;
   }
   __syncthreads();
-  T9_STAMP(1);
   uint32_t rows = 0, rel = 0, maxd = 0, fresh_n = 0;
   const bool hash_on = !(a.ablate & (1u << 16));  // diagnostic knob: no hashing / probing / inserting
   constexpr int TW = WTW;
@@ -658,7 +376,6 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
       walk(std::true_type{});
     else
       walk(std::false_type{});
-    T9_STAMP(2);
 #pragma unroll
     for (int q = 0; q < TW; ++q) {
       if (st[q] != S_DONE || !hash_on) {
@@ -681,41 +398,14 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
       }
       if (!(a.ablate & (1u << 17))) st[q] = S_PUT;  // diagnostic knob: hash only
     }
-    T9_STAMP(3);
-#if KMZ_T9_TAIL
-    uint32_t hf[TW];  // a follower's leader-map slot (IMAP + 1: none)
-#pragma unroll
-    for (int q = 0; q < TW; ++q) hf[q] = IMAP + 1;
-    chain_round_tail9<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
-      const uint32_t pk = lpk[x];
-      return AncRec{p9_id(pk), p9_kind(pk), p9_parent(pk)};
-    }, need, L, hf, a, rows, rel, maxd, fresh_n, flags, t9acc, t9prev);
-    __syncthreads();  // (the leaders' parent sigs are in the map; it stays for a next round, as k4_tile8's)
-#pragma unroll
-    for (int q = 0; q < TW; ++q)
-      if (hf[q] <= IMAP && L.imap_psig[hf[q]] != ps[q]) flags |= F_SIG;
-#else  // (A/B: k4_tile8's tail -- LDS leader map, lists reserved per workgroup with device atomics)
     chain_round_tail<WTT, TW>(sg, ps, st, kq, dd, jq, myep, w0, [&](uint32_t x) {
       const uint32_t pk = lpk[x];
       return AncRec{p9_id(pk), p9_kind(pk), p9_parent(pk)};
     }, L, a, rows, rel, maxd, fresh_n, flags);
-    __syncthreads();
-#endif
-  }
-  __syncthreads();  // (the workgroup's list counts are final)
-  if (threadIdx.x == 0) {
-    a.wn[blockIdx.x] = min(need[0], need[2]);  // (the region's valid keys)
-    a.wn[a.ntiles + blockIdx.x] = min(need[1], R_POS);
-    a.wn[2 * a.ntiles + blockIdx.x] = min(need[3], R_DEFER);
+    __syncthreads();  // (wlist / imap reads of this round before the next round's leaders)
   }
   if (flags) atomicOr(&a.counters[C_FLAGS], flags);
-  T9_STAMP(8);
   chain_tile_stats<WTT>(rows, rel, maxd, fresh_n, red, tile_stats);
-  T9_STAMP(9);
-#if KMZ_T9_CLOCKS
-  if (threadIdx.x == 0)
-    for (int kk = 0; kk < 10; ++kk) atomicAdd(&g_walk9_dbg[kk], t9acc[kk]);
-#endif
 }
 
 bool chain_tile9_fits(uint32_t n_ids) { return n_ids < ID9_NONE; }
@@ -753,12 +443,3 @@ void launch_chain_tile(hipStream_t s, const uint8_t *kind, const uint32_t *shape
 }
 
 }  // namespace kmz
-
-extern "C" int kmz__debug_walk9(unsigned long long *out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kmz::g_walk9_dbg), sizeof(kmz::g_walk9_dbg)) != hipSuccess) return -1;
-  if (reset) {
-    static const unsigned long long z[12] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(kmz::g_walk9_dbg), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}

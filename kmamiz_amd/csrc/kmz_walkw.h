@@ -53,15 +53,6 @@ struct ChainRun {
   // or an endpoint update needs it; null: the ids are endpoints
   const uint32_t *id_ep = nullptr;
   uint32_t n_ids = 0;  // (shape ids: n_shapes; an id past it is NONE)
-  // k4_tile9's per-workgroup lists (no device atomic to reserve them): tile w
-  // stages up to WG_STAGE keys at wstage[w * WG_STAGE], claims up to WG_POS
-  // slots at wgpos[w * WG_POS], defers up to WG_DEFER checks at
-  // wdefer[2 * w * WG_DEFER], and writes the counts to wn[w] / wn[ntiles + w]
-  // / wn[2 * ntiles + w]; what does not fit goes to the global lists above
-  unsigned long long *wstage = nullptr, *wdefer = nullptr;
-  uint32_t *wgpos = nullptr;
-  uint32_t *wn = nullptr;
-  uint32_t ntiles = 0;
 };
 
 // an edge key over shape ids -> the same key over their dependency endpoints

@@ -12,11 +12,10 @@ from kmamiz_amd import _lib as L  # noqa: E402
 ntr = int(sys.argv[1]) if len(sys.argv) > 1 else 3650000
 e = Engine(0)
 e.load_synthetic(synth.MESH, synth.SEED, 0, ntr)
-buf = (C.c_ulonglong * 10)()
+buf = (C.c_ulonglong * 4)()
 fn = L.lib().kmz__debug_chain_lists
 fn.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
-names = ["g_stage", "g_defer", "g_claims", "pending", "wg_keys", "wg_claims", "wg_defers", "max_keys", "max_claims",
-         "max_defers"]
+names = ["staged_keys", "deferred", "claims", "pending"]
 for k in range(3):
     e.run(L.RUN_STATS_TAG | L.RUN_DEPS)
     fn(e.ctx, buf)
