@@ -537,13 +537,25 @@ __device__ __forceinline__ void k3_reduce_items(const uint64_t *__restrict__ poo
                      *a_fst = acc + 5 * K3R;
   uint32_t *a_fst32 = reinterpret_cast<uint32_t *>(a_fst);
   constexpr uint32_t U = KMZ_K3_U;
-  // each batch's directory words are loaded during the batch before it
-  uint32_t xn = tb + (uint64_t)w * K3RB + lane < te ? row[tb + (uint64_t)w * K3RB + lane] : 0;
+  // each batch's directory words are loaded during the batch before it.
+  // (Every load here is unconditional, its index clamped into the item, and
+  // masked after: a load under a branch made the compiler wait for it at the
+  // merge -- the next batch's words right after their issue, the time base
+  // before the records -- three round trips per batch instead of one.)
+  if (te <= tb) return;  // (an empty item: nothing loaded)
+  const uint64_t tl = te - 1;  // the item's last tile
+  const uint64_t k00 = tb + (uint64_t)w * K3RB + lane;
+  uint32_t xn = row[k00 < te ? k00 : tl];
+  xn = k00 < te ? xn : 0;
   for (uint64_t k0 = tb + (uint64_t)w * K3RB; k0 < te; k0 += (uint64_t)NW * K3RB) {
     const uint64_t k = k0 + lane;  // this lane's run: tile k
     const uint32_t x = xn;
+    // (the time base first: its wait, counted in order, then leaves the next
+    // batch's directory word in flight)
+    const uint64_t tbk = tbase[k < te ? k : tl];
     const uint64_t kn = k + (uint64_t)NW * K3RB;
-    xn = kn < te ? row[kn] : 0;
+    xn = row[kn < te ? kn : tl];
+    xn = kn < te ? xn : 0;
     const uint32_t o = x >> 16;
     const uint32_t c = (o + (x & 0xFFFF) <= K3T) ? (x & 0xFFFF) : 0;
     uint32_t incl = c;
@@ -560,7 +572,7 @@ __device__ __forceinline__ void k3_reduce_items(const uint64_t *__restrict__ poo
     if (c) {
       r_pre[w][ci] = pre;
       r_off[w][ci] = (uint32_t)k * K3T + o;
-      r_tb[w][ci] = tbase[k];
+      r_tb[w][ci] = tbk;
       r_tile[w][ci] = lane;
     }
     __builtin_amdgcn_wave_barrier();
