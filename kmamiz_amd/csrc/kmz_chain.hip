@@ -757,7 +757,6 @@ __global__ void __launch_bounds__(KP_T) k_key_part(const void *__restrict__ stag
 }
 
 constexpr uint32_t KS_T = 1024, KS_PER = 8;  // 16 waves per slice, 8 keys per thread in flight
-static_assert(ESLICE / 2 % KS_T == 0, "a slice copies in whole rounds of the workgroup");
 template <bool C>
 __global__ void __launch_bounds__(KS_T) k_key_slice(const void *__restrict__ bucket_v, uint64_t bcap,
                                                     const uint32_t *__restrict__ bucket_n, uint32_t nsl, uint32_t ls,
@@ -772,25 +771,16 @@ __global__ void __launch_bounds__(KS_T) k_key_slice(const void *__restrict__ buc
     if (!m) continue;  // (uniform over the workgroup) the slice keeps what it holds
     ulonglong2 *g = reinterpret_cast<ulonglong2 *>(trip + (uint64_t)b * ESLICE);
     ulonglong2 *l = reinterpret_cast<ulonglong2 *>(tab);
-    {  // (the slice's loads all in flight: a rolled loop waited for each before the next)
-      constexpr int SP = ESLICE / 2 / KS_T;
-      ulonglong2 v[SP];
-#pragma unroll
-      for (int j = 0; j < SP; ++j) v[j] = g[j * KS_T + threadIdx.x];
-#pragma unroll
-      for (int j = 0; j < SP; ++j) l[j * KS_T + threadIdx.x] = v[j];
-    }
+    for (uint32_t x = threadIdx.x; x < ESLICE / 2; x += KS_T) l[x] = g[x];
     __syncthreads();
     const KT *src = bucket + (uint64_t)b * bcap;
-    // the next chunk's keys load while this chunk's are inserted (clamped,
-    // unconditional loads: no branch for the compiler to wait at)
+    // the next chunk's keys load while this chunk's are inserted
     KT kn[KS_PER];
     auto load = [&](uint32_t x1) {
 #pragma unroll
       for (int j = 0; j < (int)KS_PER; ++j) {
         const uint32_t i = x1 + j * KS_T + threadIdx.x;
-        const KT v = src[i < m ? i : m - 1];
-        kn[j] = i < m ? v : (KT)0;
+        kn[j] = i < m ? src[i] : (KT)0;
       }
     };
     load(0);
@@ -818,8 +808,7 @@ __global__ void __launch_bounds__(KS_T) k_key_slice(const void *__restrict__ buc
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < (int)(ESLICE / 2 / KS_T); ++j) g[j * KS_T + threadIdx.x] = l[j * KS_T + threadIdx.x];
+    for (uint32_t x = threadIdx.x; x < ESLICE / 2; x += KS_T) g[x] = l[x];
     __syncthreads();
   }
   if (flags) atomicOr(&counters[C_FLAGS], flags);
