@@ -229,6 +229,9 @@ __device__ __forceinline__ uint32_t p9_id(uint32_t pk) {
 #ifndef KMZ_TILE9_WAVES
 #define KMZ_TILE9_WAVES 7
 #endif
+#ifndef KMZ_TILE9_MAP
+#define KMZ_TILE9_MAP 128  // leader-map entries (16 B each); 256 spilled 2 VGPRs, walk 0.955 -> 0.946 ms at 128
+#endif
 template <bool BY_SHAPE>
 __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *__restrict__ kind,
                                                                  const uint32_t *__restrict__ shape,
@@ -239,7 +242,7 @@ __global__ void __launch_bounds__(WTT, KMZ_TILE9_WAVES) k4_tile9(const uint8_t *
   __shared__ uint64_t lel[W9];  // element hash (0 on the sentinels)
   __shared__ uint32_t lpk[W9];  // window parent | kind << 11 | id << 13
   __shared__ uint16_t wlist[WT];
-  __shared__ ChainLds L;
+  __shared__ ChainLdsT<KMZ_TILE9_MAP> L;
   __shared__ uint32_t wcnt[WPT][NW];
   __shared__ uint32_t red[NW][4];
   const uint32_t t0 = blockIdx.x * WT, t1 = min(n, t0 + WT);

@@ -68,14 +68,19 @@ __device__ __forceinline__ uint32_t run_ep(const ChainRun &a, uint32_t id) {
   return (a.id_ep && id != NONE) ? a.id_ep[id] : id;
 }
 
-// per-round LDS of the walk: the leader map and the list reservations
-struct ChainLds {
-  unsigned long long imap_sig[IMAP], imap_psig[IMAP];
+// per-round LDS of the walk: the leader map (M entries, a power of two) and
+// the list reservations
+template <uint32_t M>
+struct ChainLdsT {
+  static constexpr uint32_t MAP = M;
+  unsigned long long imap_sig[M], imap_psig[M];
   uint32_t l_need[3], l_base[3];  // a round's reservations in the global lists (stage, claimed, deferred)
 };
+using ChainLds = ChainLdsT<IMAP>;
 
-__device__ __forceinline__ void chain_lds_init(ChainLds &L) {
-  for (uint32_t x = threadIdx.x; x < IMAP; x += blockDim.x) L.imap_sig[x] = 0;
+template <uint32_t M>
+__device__ __forceinline__ void chain_lds_init(ChainLdsT<M> &L) {
+  for (uint32_t x = threadIdx.x; x < M; x += blockDim.x) L.imap_sig[x] = 0;
   if (threadIdx.x < 3) L.l_need[threadIdx.x] = 0;
 }
 
@@ -112,11 +117,11 @@ struct AncRec {
 // sg with parent sig ps; S_PEND: its ancestry leaves the window; S_DONE:
 // nothing to probe), kq (KIND_CLIENT: an empty walker slot), the depth dd, the
 // window slot jq and the id myep; anc(x) gives window slot x's AncRec.
-template <int NT, int TW, class Anc>
+template <int NT, int TW, class Anc, uint32_t M>
 __device__ __forceinline__ void chain_round_tail(uint64_t (&sg)[TW], const uint64_t (&ps)[TW], uint8_t (&st)[TW],
                                                  const uint8_t (&kq)[TW], const uint32_t (&dd)[TW],
                                                  const uint32_t (&jq)[TW], const uint32_t (&myep)[TW], uint32_t w0,
-                                                 Anc anc, ChainLds &L, const ChainRun &a, uint32_t &rows,
+                                                 Anc anc, ChainLdsT<M> &L, const ChainRun &a, uint32_t &rows,
                                                  uint32_t &rel, uint32_t &maxd, uint32_t &fresh_n, uint32_t &flags) {
   const uint32_t spin = spin_bound(a.ablate);
   ulonglong2 w01[TW];  // (sig, parent sig) of the probed slot
@@ -131,7 +136,7 @@ __device__ __forceinline__ void chain_round_tail(uint64_t (&sg)[TW], const uint6
   uint32_t hslot[TW];
 #pragma unroll
   for (int q = 0; q < TW; ++q) {
-    hslot[q] = IMAP + 1;  // not an insert
+    hslot[q] = M + 1;  // not an insert
     if (st[q] != S_PUT) continue;
     for (uint32_t z = 0; w01[q].x != sg[q] && w01[q].x != 0 && z < PROBE_MAX; ++z) {  // another chain's slot
       pos[q] = pos[q] + 1 == a.ccap ? 0 : pos[q] + 1;
@@ -142,8 +147,8 @@ __device__ __forceinline__ void chain_round_tail(uint64_t (&sg)[TW], const uint6
       if (w01[q].y != ps[q]) flags |= F_SIG;
       continue;
     }
-    uint32_t h = (uint32_t)(sig_place(sg[q]) >> 32) & (IMAP - 1);
-    hslot[q] = IMAP;  // a leader without a map slot (map full)
+    uint32_t h = (uint32_t)(sig_place(sg[q]) >> 32) & (M - 1);
+    hslot[q] = M;  // a leader without a map slot (map full)
     for (uint32_t t = 0; t < 8; ++t) {
       const unsigned long long kk = atomicCAS(&L.imap_sig[h], 0ull, (unsigned long long)sg[q]);
       if (kk == 0) {
@@ -155,12 +160,12 @@ __device__ __forceinline__ void chain_round_tail(uint64_t (&sg)[TW], const uint6
         hslot[q] = h | 0x80000000u;
         break;
       }
-      h = (h + 1) & (IMAP - 1);
+      h = (h + 1) & (M - 1);
     }
   }
   if (a.ablate & (1u << 18))  // diagnostic knob: probe but no inserts
 #pragma unroll
-    for (int q = 0; q < TW; ++q) hslot[q] = IMAP + 1;
+    for (int q = 0; q < TW; ++q) hslot[q] = M + 1;
   __syncthreads();
   // followers compare with their leader; leaders claim the probed slot (one
   // CAS) and publish at once (a lane that waits on another workgroup's
@@ -175,9 +180,9 @@ __device__ __forceinline__ void chain_round_tail(uint64_t (&sg)[TW], const uint6
     lead[q] = false;
     os[q] = ol[q] = 0;
     cvq[q] = 0;
-    if (hslot[q] > IMAP) {
-      if (hslot[q] != IMAP + 1) {
-        const uint32_t h = hslot[q] & (IMAP - 1);
+    if (hslot[q] > M) {
+      if (hslot[q] != M + 1) {
+        const uint32_t h = hslot[q] & (M - 1);
         if (L.imap_psig[h] != ps[q]) flags |= F_SIG;
       }
       continue;
