@@ -632,65 +632,112 @@ __global__ void __launch_bounds__(1024) k_cert_resplit(const unsigned long long 
 // so after one barrier each thread compares the pairs of its buckets' slots,
 // and each overflow id its bucket's slots and the other overflow ids.
 // cert_plan keeps a sub-bin at ~3 ids per bucket (a handful overflow).
-constexpr uint32_t CK_NB = 1024, CK_S = 8;  // buckets, slots per bucket (64 KB)
-constexpr uint32_t CK_OVF = 1024;           // overflow ids (8 KB)
-// threads per pass-3 workgroup: two workgroups per CU by LDS, so 1024
-// threads (six ids each) keep twice the waves of 512 (twelve ids each) in
-// flight: check 0.296 -> 0.257 ms on config 3 (profiles/r04/ab/cct/)
+constexpr uint32_t CK_NB = 1024, CK_S = 8;  // buckets, slots per bucket (32 KB of words; 64 KB of ids)
+#ifndef KMZ_CK_OVF
+#define KMZ_CK_OVF 256
+#endif
+constexpr uint32_t CK_OVF = KMZ_CK_OVF;     // overflow ids (2 KB)
+// threads per pass-3 workgroup: with 8-byte slots (76 KB of LDS, two
+// workgroups per CU) 1024 threads (six ids each) kept twice the waves of 512
+// in flight: check 0.296 -> 0.257 ms on config 3 (profiles/r04/ab/cct/).
+// With the 32-bit words (39 KB) four workgroups of 512 fit: 0.253 -> 0.238 ms
+// at 10^8, 2.41 -> 2.11 ms at 10^9 (profiles/r06/ab/ckfp2*; the words at
+// 1024 threads were slower than the 8-byte slots, 0.262 ms).
 #ifndef KMZ_CCT
-#define KMZ_CCT 1024
+#define KMZ_CCT 512
 #endif
 constexpr int CCT = KMZ_CCT;
 constexpr int CK_PER = 6144 / CCT;          // ids per thread: sub-bins <= CCT * CK_PER = 6144 (cert_plan)
 static_assert(CCT * CK_PER >= CERT_SET * 3 / 4, "a sub-bin must fit the workgroup's registers");
 // (A persistent form that loads the next sub-bin's ids while checking the
 // current one measured slower: 0.31 against 0.275 ms on config 3.)
-#ifndef KMZ_CK_CAS
-#define KMZ_CK_CAS 0
+#ifndef KMZ_CK_FP
+#define KMZ_CK_FP 1
 #endif
-#if KMZ_CK_CAS
-// (variant) the same check as an open-addressing LDS set: each id claims
-// the first free slot from its home (the hash's low 13 bits) by an LDS
-// compare-and-swap; finding itself there is a repeat.  8192 slots for at most
-// 6144 ids: a free slot always exists, so every probe sequence ends.
-constexpr uint32_t CK_SET = 8192;
+// (An open-addressing form -- each id claims the first free slot from its
+// home by an LDS compare-and-swap -- measured slower than the 8-slot buckets.)
+#if KMZ_CK_FP
+// The buckets hold 32-bit words instead of the ids: the 19 hash bits above
+// the bucket's 10 (a fingerprint) and the id's 13-bit position in the
+// sub-bin.  The pair test compares words' fingerprints; only a fingerprint
+// hit (~2^-19 per pair, a few hundred per 10^8 ids) reads the two ids back
+// from the pool and compares them whole, so the verdict stays exact.  Half
+// the LDS bytes written and read, and 32-bit compares.
+constexpr uint32_t CK_FPSH = 13;  // word = fp19 << 13 | position
+static_assert(CCT * CK_PER <= (1u << CK_FPSH), "positions fit the word");
+__device__ __forceinline__ uint32_t ck_fp(uint64_t h) { return (uint32_t)(h >> 10) & 0x7FFFFu; }
 __global__ void __launch_bounds__(CCT) k_cert_check(const unsigned long long *__restrict__ pool, uint32_t cap,
                                                    const unsigned int *__restrict__ cur, uint32_t cur_stride,
                                                    unsigned int *__restrict__ counters) {
-  __shared__ unsigned long long tab[CK_SET];
+  __shared__ uint4 bkt4[CK_NB * CK_S / 4];
+  __shared__ uint32_t bcnt[CK_NB];
+  __shared__ unsigned long long ovf[CK_OVF];
+  __shared__ uint32_t novf;
+  uint32_t *bkt = reinterpret_cast<uint32_t *>(bkt4);
   const uint32_t sb = blockIdx.x;
   const uint32_t m = min(cur[(uint64_t)sb * cur_stride], cap);
   if (m == 0) return;
   const unsigned long long *src = pool + (uint64_t)sb * cap;
   uint64_t h[CK_PER];
 #pragma unroll
-  for (int q = 0; q < CK_PER; ++q) {  // every load in flight while the set is cleared
+  for (int q = 0; q < CK_PER; ++q) {  // every load in flight while the counters are cleared
     const uint32_t e = q * CCT + threadIdx.x;
     h[q] = e < m ? src[e] : 0;
   }
-  for (uint32_t k = threadIdx.x; k < CK_SET / 2; k += CCT) reinterpret_cast<ulonglong2 *>(tab)[k] = make_ulonglong2(0, 0);
+  for (uint32_t k = threadIdx.x; k < CK_NB; k += CCT) bcnt[k] = 0;
+  if (threadIdx.x == 0) novf = 0;
   __syncthreads();
-  bool dup = false, lost = m > CCT * CK_PER;
-  uint32_t pos[CK_PER];
-  bool live[CK_PER];
+  bool lost = false;
 #pragma unroll
   for (int q = 0; q < CK_PER; ++q) {
-    pos[q] = (uint32_t)h[q] & (CK_SET - 1);
-    live[q] = h[q] != 0;  // padding (and cert_hash(0) == 0: span id 0, reported as F_ZERO_ID)
-  }
-  // the thread's ids in lockstep: one CAS each per step, all in flight together
-  for (uint32_t z = 0; z < CK_SET; ++z) {
-    bool any = false;
-#pragma unroll
-    for (int q = 0; q < CK_PER; ++q) {
-      if (!live[q]) continue;
-      const unsigned long long o = atomicCAS(&tab[pos[q]], 0ull, (unsigned long long)h[q]);
-      dup |= o == h[q];
-      live[q] = o != 0 && o != h[q];
-      pos[q] = (pos[q] + 1) & (CK_SET - 1);
-      any |= live[q];
+    if (h[q] == 0) continue;  // padding (and cert_hash(0) == 0: span id 0, reported as F_ZERO_ID)
+    const uint32_t b = (uint32_t)h[q] & (CK_NB - 1);
+    const uint32_t slot = atomicAdd(&bcnt[b], 1u);
+    if (slot < CK_S) {
+      // a bucket is 32 B (8 banks): slot s at position s ^ ((b >> 3) & 7), so
+      // the first slots of the buckets spread over all 64 banks
+      bkt[b * CK_S + (slot ^ ((b >> 3) & 7))] = (ck_fp(h[q]) << CK_FPSH) | (q * CCT + threadIdx.x);
+    } else {
+      const uint32_t o = atomicAdd(&novf, 1u);
+      if (o < CK_OVF) ovf[o] = h[q];
+      else lost = true;
     }
-    if (!any) break;
+  }
+  __syncthreads();
+  bool dup = false;
+  for (uint32_t b = threadIdx.x; b < CK_NB; b += CCT) {
+    const uint32_t c = min(bcnt[b], CK_S);
+    if (c < 2) continue;
+    // lanes b and b + 8 start on different halves of their buckets (same
+    // banks otherwise within a ds_read_b128 group)
+    const uint32_t r = (b >> 3) & 1, sw = (b >> 3) & 7;
+    const uint4 v0 = bkt4[b * 2 + r], v1 = bkt4[b * 2 + (r ^ 1)];
+    const uint32_t x[CK_S] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    bool ok[CK_S];
+#pragma unroll
+    for (uint32_t j = 0; j < CK_S; ++j) ok[j] = ((((j >> 2) ^ r) << 2 | (j & 3)) ^ sw) < c;
+    bool hit = false;
+#pragma unroll
+    for (uint32_t i = 0; i < CK_S; ++i)
+#pragma unroll
+      for (uint32_t j = i + 1; j < CK_S; ++j) hit |= ok[i] && ok[j] && ((x[i] ^ x[j]) >> CK_FPSH) == 0;
+    if (hit) {  // rare: confirm on the ids themselves
+      for (uint32_t i = 0; i < CK_S; ++i)
+        for (uint32_t j = i + 1; j < CK_S; ++j)
+          if (ok[i] && ok[j] && ((x[i] ^ x[j]) >> CK_FPSH) == 0)
+            dup |= src[x[i] & ((1u << CK_FPSH) - 1)] == src[x[j] & ((1u << CK_FPSH) - 1)];
+    }
+  }
+  // overflow ids: against their (full) bucket's words and the later overflow ids
+  const uint32_t no = min(novf, CK_OVF);
+  for (uint32_t o = threadIdx.x; o < no; o += CCT) {
+    const uint64_t v = ovf[o];
+    const uint32_t b = (uint32_t)v & (CK_NB - 1), f = ck_fp(v);
+    for (uint32_t j = 0; j < CK_S; ++j) {
+      const uint32_t w = bkt[b * CK_S + j];
+      if ((w >> CK_FPSH) == f) dup |= src[w & ((1u << CK_FPSH) - 1)] == v;
+    }
+    for (uint32_t t = o + 1; t < no; ++t) dup |= ovf[t] == v;
   }
   if (dup) atomicOr(&counters[C_CERT], CERT_DUP);
   if (lost) atomicOr(&counters[C_CERT], CERT_OVF);

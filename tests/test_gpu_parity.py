@@ -1208,6 +1208,45 @@ def test_certificate_massively_repeated_id(engine):
     assert info["n_dups"] > 0
 
 
+def _ids_of_hashes(h):
+    """Span ids whose kmz_common.h id_hash are the given uint64 values (its
+    inverse: undo the xorshift by 29, then the odd multiplier)."""
+    h = np.asarray(h, dtype=np.uint64)
+    x = h ^ (h >> np.uint64(29)) ^ (h >> np.uint64(58))
+    return x * np.uint64(pow(0x9E3779B97F4A7C15, -1, 1 << 64))
+
+
+@pytest.mark.parametrize("group", [2, 12])
+def test_certificate_fingerprint_collisions_are_not_repeats(engine, group):
+    """The check compares 19-bit fingerprints of the ids in one bucket and
+    reads the ids back only on a fingerprint hit.  Groups of distinct ids
+    whose hashes agree on every bit but one in the middle (same sub-bin,
+    bucket and fingerprint) must pass the certificate; with 12 a group also
+    overflows its bucket's 8 slots.  Then one group with a real repeat fails
+    it."""
+    from kmamiz_amd import synth
+    from kmamiz_amd import dist as kdist
+
+    batch, _ = synth.host_batch(3, 0, 40000)
+    parents = set(int(p) for p in batch.parent_id if p)
+    cand = np.array([i for i in range(len(batch)) if int(batch.span_id[i]) not in parents])
+    rng = np.random.default_rng(11 + group)
+    sel = rng.choice(cand, 600 - 600 % group, replace=False).reshape(-1, group)
+    base = rng.integers(1, 1 << 63, size=len(sel), dtype=np.uint64)
+    for g, b in zip(sel, base):
+        hs = b ^ (np.arange(group, dtype=np.uint64) << np.uint64(32))  # bits 32..35: outside every field
+        batch.span_id[g] = _ids_of_hashes(hs)
+    assert np.array_equal(kdist.id_hash_np(batch.span_id[sel[0]]), base[0] ^ (np.arange(group, dtype=np.uint64) << np.uint64(32)))
+    assert len(np.unique(batch.span_id)) == len(batch)
+    info = _compare_synth(engine, batch, synth.shape_table(3))
+    assert info["path"] & 1 and info["n_dups"] == 0
+    batch.span_id[sel[3][-1]] = batch.span_id[sel[3][0]]
+    engine._loaded_token = None
+    info = _compare_synth(engine, batch, synth.shape_table(3))
+    assert not (info["path"] & 1)
+    assert info["n_dups"] == 1
+
+
 # ---------------------------------------------------------------------------
 # traceId sharding: device shard generation + index map (SURVEY.md 8e)
 # ---------------------------------------------------------------------------
