@@ -374,6 +374,23 @@ int kmz_id_repeats(kmz_ctx *ctx, const uint64_t *vals, uint64_t n, int mem, uint
  * so an all-to-all of equal segments can be posted behind it at once
  * (dist.IdGuard; Traces.ts:117-123 is the semantics the check protects). */
 int kmz_route_ids_fixed(kmz_ctx *ctx, uint32_t world, uint64_t seg, uint64_t *out, int mem);
+/* kmz_route_ids_fixed folded into the next run (kmz_run / kmz_run_begin):
+ * arms it, nothing is enqueued here.  The run writes the same fixed segments
+ * into `out` (device memory, `world` * `seg` words) from its join's first
+ * certificate pass when the run has no certificate of its own
+ * (KMZ_RUN_NO_CERT) and world <= the pass's bins (64; 256 past ~10^8 spans),
+ * otherwise by kmz_route_ids_fixed's own pass inside the run; either way it
+ * records an event once the segments are complete (after the join, before
+ * the walk), so the exchange can start while the rest of the run executes.
+ * One-shot: the next run consumes it (a run repeated inside kmz_run_end does
+ * not route again).  Replaces the separate routing pass the guard ran before
+ * the run (the id_hash bins already computed there, Traces.ts:117-123). */
+int kmz_route_ids_join(kmz_ctx *ctx, uint32_t world, uint64_t seg, uint64_t *out);
+/* After kmz_run_begin of a run armed by kmz_route_ids_join: make `stream` (a
+ * hipStream_t; NULL: the context's) wait for its routing.  *in_join (may be
+ * NULL) = 1 when the join wrote the segments, 0 when the fallback pass did.
+ * KMZ_E_STATE when the last run routed nothing. */
+int kmz_route_wait(kmz_ctx *ctx, void *stream, int *in_join);
 /* kmz_id_repeats over the fixed segments an all-to-all of
  * kmz_route_ids_fixed outputs delivered (device memory, `world` segments of
  * `seg` words as received), without compacting them first, ENQUEUED on

@@ -184,6 +184,8 @@ SIGNATURES = [
     ("kmz_count_ids", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.POINTER(C.c_uint64)]),
     ("kmz_route_ids", C.c_int, [_P, C.c_uint32, _P, C.c_uint64, C.c_int, _P]),
     ("kmz_route_ids_fixed", C.c_int, [_P, C.c_uint32, C.c_uint64, _P, C.c_int]),
+    ("kmz_route_ids_join", C.c_int, [_P, C.c_uint32, C.c_uint64, _P]),
+    ("kmz_route_wait", C.c_int, [_P, _P, C.POINTER(C.c_int)]),
     ("kmz_get_graph_stats", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     ("kmz_id_repeats", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.POINTER(C.c_uint32)]),
     ("kmz_id_repeats_seg_begin", C.c_int, [_P, _P, C.c_uint32, C.c_uint64, _P]),

@@ -66,6 +66,7 @@ struct kmz_ctx {
   DevBuf rt_hist, rt_tot, rt_out, rt_ctr;  // cross-shard repeated-id guard: routing scratch, certificate counters
   DevBuf rt_pool1, rt_dir, rt_pool2, rt_cur;  // ... and its own certificate buffers (the run's stay as the run left them)
   DevBuf rt_tsz;                               // ... segment tile sizes (kmz_id_repeats_seg_begin)
+  DevBuf rt_jcur;                              // ... the join-folded routing's per-owner cursors (128 B each)
   // kmz_id_repeats_seg_begin/_end: the open check's stream, segment size, plan
   // and pinned read-back (counters, then the largest count)
   bool rs_open = false;
@@ -179,6 +180,12 @@ struct kmz_ctx {
   bool epp_filled = false;  // this run's endpoint partials were filled with its counters (run_enqueue)
   hipEvent_t ev_fork = nullptr, ev_k3 = nullptr, ev_join = nullptr, ev_done = nullptr;
   bool overlap = false;  // this run uses the side stream
+  // kmz_route_ids_join: the next run routes its span ids into these fixed
+  // segments (in the join where it can, else by kmz_route_ids_fixed's pass),
+  // then records ev_route; kmz_route_wait makes a stream wait for it
+  JoinRoute rt_arm;
+  bool rt_armed = false, rt_routed = false, rt_in_join = false;
+  hipEvent_t ev_route = nullptr;
 
   // profiling
   // kmz_fetch_begin / _end: transfer stream, snapshot of the results, the open fetch
@@ -368,7 +375,8 @@ kmz_ctx *kmz_create(int device, void *stream) {
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_k3, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_route, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return nullptr;
   }
@@ -408,7 +416,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->rt_tsz, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->rt_tsz, &c->rt_jcur, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt,
                     &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->tl_lbkt, &c->tl_lbn, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
@@ -436,7 +444,7 @@ void kmz_destroy(kmz_ctx *c) {
     hipStreamSynchronize(c->side2);
     hipStreamDestroy(c->side2);
   }
-  for (hipEvent_t e : {c->ev_fork, c->ev_k3, c->ev_join, c->ev_done, c->ev_cert})
+  for (hipEvent_t e : {c->ev_fork, c->ev_k3, c->ev_join, c->ev_done, c->ev_cert, c->ev_route})
     if (e) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
@@ -868,6 +876,14 @@ static int run_join(kmz_ctx *c, bool *ok) {
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned int *cur2 = P<unsigned int>(c->ccur);
   if (ensure(c, c->mkey, (size_t)c->mcap * 8) || ensure(c, c->mval, (size_t)c->mcap * 4)) return KMZ_E_HIP;
+  // an armed routing (kmz_route_ids_join) rides in the join's pass 1 when the
+  // run has no certificate of its own and the owners fit the pass-1 bins
+  JoinRoute rt;
+  if (c->rt_armed && c->no_cert && !early && c->rt_arm.world <= (1u << pl.B1)) {
+    if (ensure(c, c->rt_jcur, (size_t)c->rt_arm.world * ROUTE_CUR_STRIDE * 8)) return KMZ_E_HIP;
+    rt = c->rt_arm;
+    rt.cur = P<unsigned long long>(c->rt_jcur);
+  }
   if (early) {  // (behind the side stream's K3: the main stream waits for that one near the end)
     c->stream = c->side;
     {
@@ -893,6 +909,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
     Timed t(c, KMZ_K_MEMSET);
     FillArgs f;
     if (!early) f.add(cur2, cert_cur_words(pl) * 4, 0);
+    if (rt.out) f.add(rt.cur, (size_t)rt.world * ROUTE_CUR_STRIDE * 8, 0);
     f.add(c->mkey.p, (size_t)c->mcap * 8, 0);
     f.add(c->mval.p, (size_t)c->mcap * 4, 0xFF);  // ids not in the batch: NONE
     launch_fill(c->stream, f);
@@ -903,7 +920,14 @@ static int run_join(kmz_ctx *c, bool *ok) {
     // bins on its own or KMZ_RUN_NO_CERT leaves it to the caller)
     launch_join(c->stream, c->sid, c->pid, c->kind, n, P<uint32_t>(c->cparent), P<uint32_t>(c->dp),
                 P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, pl,
-                c->ablate | (c->no_cert || early ? 64u : 0u));
+                c->ablate | ((c->no_cert && !rt.out) || early ? 64u : 0u), rt);
+  }
+  if (rt.out) {  // the segments' counts, then the event the exchange waits for
+    launch_route_counts(c->stream, rt.world, rt.segw, rt.cur, ROUTE_CUR_STRIDE, rt.out);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev_route, c->stream));
+    c->rt_armed = false;
+    c->rt_routed = c->rt_in_join = true;
   }
   // (KMZ_ABLATE2 bit 15, for comparison: with a chain table past the MALL
   // the certificate beside the settle instead of on the main stream between
@@ -1740,6 +1764,16 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     return r;
   }
   if ((r = launch_cert_deferred(c))) return r;  // (a path with no walk after the join)
+  if (c->rt_armed) {  // an armed routing the join did not take (fused or table path, a certificate, world past
+    // the bins): kmz_route_ids_fixed's pass on the main stream
+    if (ensure(c, c->rt_tot, (size_t)c->rt_arm.world * 8)) return KMZ_E_HIP;
+    if (!launch_route_fixed(c->stream, c->sid, (uint32_t)c->n, c->rt_arm.world, c->rt_arm.segw,
+                            P<unsigned long long>(c->rt_tot), c->rt_arm.out))
+      return fail(c, KMZ_E_HIP, "routing launch");
+    HIPCHK(c, hipEventRecord(c->ev_route, c->stream));
+    c->rt_armed = false;
+    c->rt_routed = true;
+  }
   if (k3_mid && !c->k3_ran && (r = run_stats(c, smode))) return r;  // (its shape level ran inside run_deps)
   if (c->overlap) {  // everything queued on the side stream, before the read-back
     HIPCHK(c, hipEventRecord(c->ev_done, c->side));
@@ -1792,7 +1826,7 @@ static uint64_t run_key(kmz_ctx *c, uint32_t flags) {
 // run + fetch, Bookinfo / mesh / config 5); KMZ_HIPGRAPH=0 turns them off.
 // (Not while kernels are timed: the bench's live events keep them off.)
 static int run_enqueue_graphed(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, unsigned long long *s64) {
-  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && c->graphs_on &&
+  const bool eligible = c->n > 0 && c->n < (1ull << 23) && !c->prof && c->graphs_on && !c->rt_armed &&
                         !c->table_hint && !c->walk_once && !(c->ablate & (32u | 16u));
   if (!eligible) return run_enqueue(c, flags, links, h, s64);
   const uint64_t key = run_key(c, flags);
@@ -1909,7 +1943,11 @@ int kmz_run_begin(kmz_ctx *c, uint32_t flags) {
   unsigned long long *s64 = reinterpret_cast<unsigned long long *>(h + C_COUNT);
   c->k4_now = (flags & KMZ_RUN_DEPS) ? k4_direct(c) : false;
   c->no_cert = (flags & KMZ_RUN_NO_CERT) != 0;
-  if (int r = run_attempt(c, flags, links, h, s64)) return r;
+  c->rt_routed = c->rt_in_join = false;  // (kmz_route_wait: this run's routing only)
+  if (int r = run_attempt(c, flags, links, h, s64)) {
+    c->rt_armed = false;
+    return r;
+  }
   c->run_open = true;
   c->run_flags = flags;
   return KMZ_OK;
@@ -2762,6 +2800,26 @@ int kmz_route_ids_fixed(kmz_ctx *c, uint32_t world, uint64_t seg, uint64_t *out,
     HIPCHK(c, hipMemcpyAsync(out, dst, words * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
+  return KMZ_OK;
+}
+
+int kmz_route_ids_join(kmz_ctx *c, uint32_t world, uint64_t seg, uint64_t *out) {
+  if (!c || world == 0 || world > 1024 || seg < 2 || !out) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
+  if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_route_ids_join before kmz_load");
+  c->rt_arm.world = world;
+  c->rt_arm.segw = seg;
+  c->rt_arm.out = reinterpret_cast<unsigned long long *>(out);
+  c->rt_armed = true;
+  c->rt_routed = false;
+  return KMZ_OK;
+}
+
+int kmz_route_wait(kmz_ctx *c, void *stream, int *in_join) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->rt_routed) return fail(c, KMZ_E_STATE, "kmz_route_wait: no routed run (kmz_route_ids_join, then kmz_run_begin)");
+  HIPCHK(c, hipStreamWaitEvent(stream ? (hipStream_t)stream : c->stream, c->ev_route, 0));
+  if (in_join) *in_join = c->rt_in_join ? 1 : 0;
   return KMZ_OK;
 }
 

@@ -181,9 +181,14 @@ __global__ void __launch_bounds__(RT_T) k_route_fixed(const uint64_t *__restrict
 }
 
 __global__ void __launch_bounds__(RT_T) k_route_counts(uint32_t world, uint64_t segw,
-                                                       const unsigned long long *__restrict__ cur,
+                                                       const unsigned long long *__restrict__ cur, uint32_t stride,
                                                        unsigned long long *__restrict__ out) {
-  for (uint32_t r = threadIdx.x; r < world; r += RT_T) out[(uint64_t)r * segw] = cur[r];
+  for (uint32_t r = threadIdx.x; r < world; r += RT_T) out[(uint64_t)r * segw] = cur[(uint64_t)r * stride];
+}
+
+void launch_route_counts(hipStream_t s, uint32_t world, uint64_t segw, const unsigned long long *cur, uint32_t stride,
+                         unsigned long long *out) {
+  hipLaunchKernelGGL(k_route_counts, dim3(1), dim3(RT_T), 0, s, world, segw, cur, stride, out);
 }
 
 bool launch_route_fixed(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t world, uint64_t segw,
@@ -191,7 +196,7 @@ bool launch_route_fixed(hipStream_t s, const uint64_t *sid, uint32_t n, uint32_t
   if (world == 0 || world > RT_MAXW || segw < 2) return false;
   if (hipMemsetAsync(cur, 0, (size_t)world * 8, s) != hipSuccess) return false;
   if (n) hipLaunchKernelGGL(k_route_fixed, dim3((n + RF_CH - 1) / RF_CH), dim3(RT_T), 0, s, sid, n, world, segw, cur, out);
-  hipLaunchKernelGGL(k_route_counts, dim3(1), dim3(RT_T), 0, s, world, segw, cur, out);
+  launch_route_counts(s, world, segw, cur, 1, out);
   return true;
 }
 

@@ -65,8 +65,10 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
                                                      uint32_t *__restrict__ cparent, uint32_t *__restrict__ dp,
                                                      unsigned long long *__restrict__ pool1,
                                                      uint16_t *__restrict__ jdir,
-                                                     unsigned int *__restrict__ counters, uint32_t ablate) {
+                                                     unsigned int *__restrict__ counters, uint32_t ablate,
+                                                     const JoinRoute rt) {
   constexpr uint32_t NW = JTT / 64, BINS = 1u << B1;
+  const bool route = rt.out != nullptr;  // (kmz_route_ids_join: pass 1 bins by owner into the segments)
   __shared__ uint64_t lsid[KW];
   // the window's LDS hash (kmz_joinw.h jh8): per bucket 8 entries (local
   // index + 1, u16) and their 8-bit fingerprints in one u64, so that a lookup
@@ -297,7 +299,9 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   if (ablate & 64) return;  // diagnostic: no certificate pass 1
   // certificate pass 1: the tile's hashed ids into 2^B1 bins.  Ranks come
   // from per-wave bin counters (LDS atomics with return), or where the LDS
-  // has no room for them (2^8 bins) from wave ballots.
+  // has no room for them (2^8 bins) from wave ballots.  (Routing: into the
+  // owner ranks' bins instead, world <= 2^B1.)
+  auto bin_of = [&](uint64_t h) -> uint32_t { return route ? id_owner(h, rt.world) : (uint32_t)(h >> (64 - B1)); };
   for (uint32_t e = threadIdx.x; e < BINS * NW; e += JTT) wcnt[e] = 0;
   __syncthreads();  // the hash entries are free from here on
   uint64_t *stg = reinterpret_cast<uint64_t *>(lidx);
@@ -317,7 +321,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
 #pragma unroll
     for (int q = 0; q < PT; ++q) {
       const uint32_t i = t0 + q * JTT + threadIdx.x;
-      rk[q] = i < t1 ? atomicAdd(&wmaj[w * BINS + (uint32_t)(hv[q] >> (64 - B1))], 1u) : 0u;
+      rk[q] = i < t1 ? atomicAdd(&wmaj[w * BINS + bin_of(hv[q])], 1u) : 0u;
     }
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < BINS * NW; e += JTT) wcnt[e] = wmaj[(e % NW) * BINS + e / NW];
@@ -328,7 +332,7 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   for (int q = 0; q < PT; ++q) {
     const uint32_t i = t0 + q * JTT + threadIdx.x;
     const bool ok = i < t1;
-    const uint32_t bin = (uint32_t)(hv[q] >> (64 - B1));
+    const uint32_t bin = bin_of(hv[q]);
     const uint64_t peers = match_bits<B1>(bin, __ballot(ok));
     uint32_t prior = 0;
     if (ok) prior = wcnt[bin * NW + w];
@@ -338,16 +342,36 @@ __global__ void __launch_bounds__(JTT, 6) k_join_window(const uint64_t *__restri
   }
   __syncthreads();
   block_scan_lds(wcnt, BINS * NW, wsum);  // bin-major, wave-minor offsets
-  // tile-major output, bins in order: no global atomics; the bin offsets go
-  // to the tile's directory row for pass 2
-  for (uint32_t b = threadIdx.x; b < BINS; b += JTT) jdir[(uint64_t)blockIdx.x * BINS + b] = (uint16_t)wcnt[b * NW];
+  uint32_t *const rbase = lcnt4;  // (routing: each owner's run in its segment; the fill counts are free)
+  static_assert(JB / 4 >= BINS, "an owner run base per pass-1 bin");
+  if (route) {
+    // each owner's run of this tile reserved in its segment by one device
+    // atomic, issued before the staging so that its round trip overlaps it
+    for (uint32_t r = threadIdx.x; r < rt.world; r += JTT) {
+      const uint32_t o = wcnt[r * NW], e = r + 1 < BINS ? wcnt[(r + 1) * NW] : t1 - t0;
+      rbase[r] = e > o ? (uint32_t)atomicAdd(&rt.cur[(uint64_t)r * ROUTE_CUR_STRIDE], (unsigned long long)(e - o)) : 0u;
+    }
+  } else {
+    // tile-major output, bins in order: no global atomics; the bin offsets go
+    // to the tile's directory row for pass 2
+    for (uint32_t b = threadIdx.x; b < BINS; b += JTT) jdir[(uint64_t)blockIdx.x * BINS + b] = (uint16_t)wcnt[b * NW];
+  }
 #pragma unroll
   for (int q = 0; q < PT; ++q) {
     const uint32_t i = t0 + q * JTT + threadIdx.x;
-    if (i < t1) stg[wcnt[(uint32_t)(hv[q] >> (64 - B1)) * NW + w] + rk[q]] = hv[q];
+    if (i < t1) stg[wcnt[bin_of(hv[q]) * NW + w] + rk[q]] = hv[q];
   }
   __syncthreads();
-  for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) pool1[(uint64_t)t0 + e] = stg[e];
+  if (route) {
+    for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) {
+      const uint64_t x = stg[e];
+      const uint32_t r = id_owner(x, rt.world);
+      const uint64_t pos = (uint64_t)rbase[r] + (e - wcnt[r * NW]);
+      if (pos + 1 < rt.segw) rt.out[(uint64_t)r * rt.segw + 1 + pos] = x;  // (full: its count says so)
+    }
+  } else {
+    for (uint32_t e = threadIdx.x; e < t1 - t0; e += JTT) pool1[(uint64_t)t0 + e] = stg[e];
+  }
   KMZ_JSTAMP(4);
   if (dbg_t && threadIdx.x == 0)
     for (int kk = 0; kk < 5; ++kk) atomicAdd(&g_join_dbg[kk], tacc[kk]);
@@ -983,14 +1007,14 @@ uint64_t cert_dir_entries(uint32_t n, const CertPlan &pl) { return (uint64_t)joi
 
 void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
                  uint32_t *cparent, uint32_t *dp, unsigned long long *pool1, uint16_t *jdir, unsigned int *counters,
-                 const CertPlan &pl, uint32_t ablate) {
+                 const CertPlan &pl, uint32_t ablate, const JoinRoute &rt) {
   if (!n) return;
   if (pl.B1 == CERT_B1W)
     hipLaunchKernelGGL(k_join_window<CERT_B1W>, dim3(join_tiles(n)), dim3(JTT), 0, s, sid, pid, kind, n, cparent, dp,
-                       pool1, jdir, counters, ablate);
+                       pool1, jdir, counters, ablate, rt);
   else
     hipLaunchKernelGGL(k_join_window<CERT_B1>, dim3(join_tiles(n)), dim3(JTT), 0, s, sid, pid, kind, n, cparent, dp,
-                       pool1, jdir, counters, ablate);
+                       pool1, jdir, counters, ablate, rt);
 }
 
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,

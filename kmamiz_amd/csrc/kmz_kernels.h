@@ -301,9 +301,24 @@ bool cert_plan(uint32_t n, CertPlan *pl, bool wide = true, bool force_wide = fal
 uint64_t cert_pool1_words(uint32_t n);
 uint64_t cert_dir_entries(uint32_t n, const CertPlan &pl);
 __host__ __device__ uint32_t join_tiles(uint32_t n);
+// The guard's routing folded into the join (kmz_route_ids_join): with `out`
+// set, the join's certificate pass 1 bins the tile's hashed ids by owner rank
+// (id_owner, world <= the pass-1 bins) and writes them into the owners' fixed
+// segments of segw words (word 0 the count, kmz_route_ids_fixed's layout),
+// each (tile, owner) run reserved by one device atomic on cur[owner * 16]
+// (one 128-byte line per owner); no pool1 / directory.
+struct JoinRoute {
+  uint32_t world = 0;
+  uint64_t segw = 0;
+  unsigned long long *cur = nullptr, *out = nullptr;
+};
+constexpr uint32_t ROUTE_CUR_STRIDE = 16;
 void launch_join(hipStream_t s, const uint64_t *sid, const uint64_t *pid, const uint8_t *kind, uint32_t n,
                  uint32_t *cparent, uint32_t *dp, unsigned long long *pool1, uint16_t *jdir, unsigned int *counters,
-                 const CertPlan &pl, uint32_t ablate = 0);
+                 const CertPlan &pl, uint32_t ablate = 0, const JoinRoute &rt = JoinRoute());
+// the segments' count words from cur[owner * stride] (after the routing)
+void launch_route_counts(hipStream_t s, uint32_t world, uint64_t segw, const unsigned long long *cur, uint32_t stride,
+                         unsigned long long *out);
 // tsz: per-tile sizes (the guard's segment tiles, launch_cert_bin_seg); null: dense tiles of n values
 void launch_cert_split(hipStream_t s, uint32_t n, const unsigned long long *pool1, const uint16_t *jdir,
                        const CertPlan &pl, unsigned long long *pool2, unsigned int *cur2, unsigned int *counters,

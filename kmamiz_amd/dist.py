@@ -244,7 +244,14 @@ class IdGuard:
 
     Every span id of every shard, the owner's own included, is routed and
     checked, so a repeat inside one shard is found too: a run covered by a
-    guard may skip its own certificate (KMZ_RUN_NO_CERT)."""
+    guard may skip its own certificate (KMZ_RUN_NO_CERT).
+
+    ``start(fold=True)`` (RCCL, fixed segments) instead arms the routing into
+    the next run (kmz_route_ids_join: the run's join writes the segments from
+    the id hashes it bins anyway, no pass of its own); the caller runs
+    ``post()`` after ``run_begin``, which posts the exchange on the guard's
+    stream behind the join (kmz_route_wait) and the certificate behind it,
+    both beside the rest of the run."""
 
     def __init__(self, engine=None, dev=None, group=None, span_ids: Optional[np.ndarray] = None, *,
                  world: Optional[int] = None, backend: Optional[str] = None):
@@ -263,6 +270,8 @@ class IdGuard:
         self.gobj = group if group is not None or world is not None else dist.distributed_c10d._get_default_group()
         self.work = self.fixed = self.pending = None
         self.seg_open = False  # kmz_id_repeats_seg_begin enqueued, not yet ended
+        self.armed = False  # start(fold=True): routing armed into the next run, exchange not yet posted
+        self.in_join = None  # post(): whether the run's join wrote the segments (else its fallback pass)
 
     # the guard's collectives (a single-process test overrides both)
     def _a2a(self, out, inp, out_splits=None, in_splits=None, async_op=False):
@@ -283,10 +292,18 @@ class IdGuard:
         e = _ID_SEG.get((id(self.gobj), self.world))
         return e[1] if e is not None and e[0] is self.gobj else None
 
-    def start(self) -> "IdGuard":
+    def start(self, fold: bool = False) -> "IdGuard":
         if self.world == 1:
             return self
         seg = self._seg_size() if self.engine is not None else None
+        if seg is not None and fold and self.on_dev:
+            # the run routes (kmz_route_ids_join); post() exchanges after run_begin
+            self.fixed = seg
+            self.send = torch.empty(self.world * seg, dtype=torch.int64, device=self.route_dev)
+            self.recv = torch.empty_like(self.send)
+            self.engine.route_ids_join(self.world, seg, self.send.data_ptr())
+            self.armed = True
+            return self
         if seg is not None:
             self.fixed = seg
             if self.route_dev is not None:  # enqueued on the engine's stream, no wait
@@ -322,6 +339,28 @@ class IdGuard:
             return self
         return self._start_counts()
 
+    def post(self) -> "IdGuard":
+        """After run_begin of the run start(fold=True) armed: the exchange on
+        the guard's stream once the run's join has written the segments, and
+        the certificate over what arrives, both beside the rest of the run
+        (every rank posts it, in the same order as its other collectives)."""
+        if not self.armed:
+            return self
+        self.armed = False
+        gs = _guard_stream(self.route_dev)
+        self.in_join = self.engine.route_wait(gs.cuda_stream)
+        with torch.cuda.stream(gs):
+            self.work = self._a2a(self.recv, self.send, async_op=True)
+            self.work.wait()
+        self.send.record_stream(gs)
+        self.recv.record_stream(gs)
+        try:
+            self.engine.id_repeats_seg_begin(self.recv.data_ptr(), self.world, self.fixed, gs.cuda_stream)
+            self.seg_open = True
+        except Exception:  # noqa: BLE001 (the certificate cannot take it: finish() checks by compaction)
+            self.seg_open = False
+        return self
+
     def _start_counts(self) -> "IdGuard":
         """The exact protocol: counts first, then the values with those splits."""
         self.fixed = None
@@ -348,6 +387,8 @@ class IdGuard:
     def abandon(self) -> None:
         """Wait for a posted exchange without checking it (every rank calls
         this when the merge is refused before the guard's verdict)."""
+        if self.armed:  # (its exchange is still every rank's to post)
+            self.post()
         if self.seg_open:  # (its certificate reads the received segments: wait for it)
             self.seg_open = False
             self.engine.id_repeats_seg_end()
@@ -421,6 +462,8 @@ class IdGuard:
         with ``raise_``)."""
         if self.world == 1:
             return False
+        if self.armed:
+            self.post()
         if self.work is None and self.pending is None and not self.seg_open:
             self.start()
         if (self.fixed is not None and self.engine is not None and self.route_dev is not None

@@ -459,6 +459,18 @@ class Engine:
         L.check(self.ctx, self._lib.kmz_route_ids_fixed(self.ctx, world, seg, C.c_void_p(dst_ptr),
                                                         L.MEM_DEVICE if device else L.MEM_HOST))
 
+    def route_ids_join(self, world: int, seg: int, dst_ptr: int) -> None:
+        """kmz_route_ids_join: the next run writes kmz_route_ids_fixed's
+        segments (device memory at dst) from its join; nothing enqueued here."""
+        L.check(self.ctx, self._lib.kmz_route_ids_join(self.ctx, world, seg, C.c_void_p(dst_ptr)))
+
+    def route_wait(self, stream: int = 0) -> bool:
+        """kmz_route_wait: ``stream`` (a hipStream_t handle; 0: the engine's)
+        waits for the last run's routing.  -> whether the join wrote it."""
+        j = C.c_int()
+        L.check(self.ctx, self._lib.kmz_route_wait(self.ctx, C.c_void_p(stream) if stream else None, C.byref(j)))
+        return bool(j.value)
+
     def id_repeats(self, src_ptr: int, n: int, device: bool) -> Optional[bool]:
         """Whether any of the n routed values occurs twice (kmz_id_repeats);
         None when the certificate cannot decide (the caller checks another way)."""

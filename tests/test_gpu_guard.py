@@ -95,6 +95,81 @@ def test_route_ids_fixed_equals_host_mirror(engine, world, device):
             o += int(c[r])
 
 
+@pytest.mark.parametrize("world,ntr,in_join", [(2, 3000, True), (3, 3000, True), (8, 3000, True), (64, 3000, True),
+                                               (65, 3000, False), (8, 40000, False), (8, 370000, True)])
+def test_route_in_join_equals_route_fixed(engine, world, ntr, in_join):
+    """kmz_route_ids_join: the run's join writes kmz_route_ids_fixed's
+    segments (word 0 the true count, then exactly the owner's hashes; a
+    subset past an overflowed segment) when the owners fit its pass-1 bins
+    (64 at these sizes), else the run's fallback pass does (world 65; the
+    fused join + walk at 40 000 traces); the run's results are those of a run
+    without routing; the arming is one-shot.  (The fused case on an engine of
+    its own with chain interning forced, KMZ_ABLATE bit 29: the shared
+    engine may have switched this shape table to direct enumeration, which
+    takes the window join.)"""
+    if ntr == 40000:
+        own = _engine_ablate(1 << 29)
+        try:
+            _route_in_join_case(own, world, ntr, in_join)
+        finally:
+            own.close()
+        return
+    _route_in_join_case(engine, world, ntr, in_join)
+
+
+def _engine_ablate(ablate):
+    import os
+
+    from kmamiz_amd import Engine
+
+    old = os.environ.get("KMZ_ABLATE")
+    os.environ["KMZ_ABLATE"] = str(ablate)
+    try:
+        return Engine(0)
+    finally:
+        if old is None:
+            del os.environ["KMZ_ABLATE"]
+        else:
+            os.environ["KMZ_ABLATE"] = old
+
+
+def _route_in_join_case(engine, world, ntr, in_join):
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import dist as kdist
+    from kmamiz_amd import synth
+
+    batch, _ = synth.host_batch(synth.MESH, 0, ntr)
+    engine.load(batch, synth.shape_table(synth.MESH))
+    flags = L.RUN_STATS_TAG | L.RUN_DEPS | L.RUN_NO_CERT
+    engine.run(flags)
+    g0, k0 = engine.groups().tobytes(), engine.triples().copy()
+    h, c = kdist.route_ids_np(batch.span_id, world)
+    for seg in (int(c.max()) + 1 + 7, max(2, int(c.max()) // 2)):
+        out = torch.zeros(world * seg, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        engine.route_ids_join(world, seg, out.data_ptr())
+        engine.run(flags)
+        assert engine.route_wait(0) is in_join
+        torch.cuda.synchronize()
+        assert engine.groups().tobytes() == g0
+        assert np.array_equal(engine.triples(), k0)
+        got = out.cpu().numpy().view(np.uint64).reshape(world, seg)
+        assert got[:, 0].tolist() == c.tolist()
+        o = 0
+        for r in range(world):
+            k = min(int(c[r]), seg - 1)
+            mine = h[o : o + int(c[r])]
+            if k == int(c[r]):
+                assert np.array_equal(np.sort(got[r, 1 : 1 + k]), np.sort(mine))
+            else:
+                assert np.isin(got[r, 1:], mine).all()
+            o += int(c[r])
+    # one-shot: the next run routes nothing
+    engine.run(flags)
+    with pytest.raises(Exception):
+        engine.route_wait(0)
+
+
 def _guard_worker(rank, world, port, q, dev_kind):
     import os
 
@@ -277,7 +352,8 @@ class _LoopGuard:
         return G()
 
 
-def test_id_guard_device_wiring_single_process():
+@pytest.mark.parametrize("fold,ntr,in_join", [(False, 3000, None), (True, 3000, True), (True, 40000, False)])
+def test_id_guard_device_wiring_single_process(fold, ntr, in_join):
     """the RCCL branch of IdGuard.start/finish as the multi-GPU
     bench wires it (one explicit stream for torch and the engine, the run
     without its own certificate beside the guard), on one process: the first
@@ -285,21 +361,35 @@ def test_id_guard_device_wiring_single_process():
     enqueued on the guard stream (seg_open); a repeat inside the shard and one
     across two sources' segments are found, clean steps pass, and when
     kmz_id_repeats_seg_begin fails start() falls back to finish()'s
-    compaction check with the same verdicts."""
+    compaction check with the same verdicts.  With ``fold`` the routing rides
+    in the run (kmz_route_ids_join) and post() exchanges after run_begin: in
+    the join at 3000 traces (~8e4 spans, the window join), by the fallback
+    pass at 40 000 (~1.1e6 spans: the fused join + walk)."""
     from kmamiz_amd import Engine
     from kmamiz_amd import _lib as L
     from kmamiz_amd import dist as kdist
     from kmamiz_amd import synth
 
+    import os
+
     stream = torch.cuda.Stream()
     prev = torch.cuda.current_stream()
     torch.cuda.set_stream(stream)
-    e = Engine(0, stream=stream.cuda_stream)
+    old = os.environ.get("KMZ_ABLATE")
+    if ntr == 40000:  # (chain interning forced: the fused join + walk, whose routing is the fallback pass)
+        os.environ["KMZ_ABLATE"] = str(1 << 29)
+    try:
+        e = Engine(0, stream=stream.cuda_stream)
+    finally:
+        if old is None:
+            os.environ.pop("KMZ_ABLATE", None)
+        else:
+            os.environ["KMZ_ABLATE"] = old
     try:
         table = synth.shape_table(synth.MESH)
         kdist._ID_SEG.pop((id(None), 2), None)  # (this process's stand-in group: no agreed size yet)
-        clean, _ = synth.host_batch(synth.MESH, 0, 3000)
-        rep_in, _ = synth.host_batch(synth.MESH, 0, 3000)
+        clean, _ = synth.host_batch(synth.MESH, 0, ntr)
+        rep_in, _ = synth.host_batch(synth.MESH, 0, ntr)
         rep_in.span_id[len(rep_in) - 1] = rep_in.span_id[5]
 
         def step(batch, inject=None, fail_seg=False):
@@ -310,8 +400,15 @@ def test_id_guard_device_wiring_single_process():
                     raise RuntimeError("KMZ_E_UNSUPPORTED (test)")
                 e.id_repeats_seg_begin = boom
             try:
-                g.start()
-                e.run(L.RUN_STATS_TAG | L.RUN_DEPS | L.RUN_NO_CERT)  # beside the guard, as the bench runs
+                g.start(fold=fold)
+                e.run_begin(L.RUN_STATS_TAG | L.RUN_DEPS | L.RUN_NO_CERT)  # beside the guard, as the bench runs
+                armed = g.armed
+                g.post()
+                e.run_end()
+                if armed:
+                    assert g.in_join is in_join
+                else:
+                    assert not fold or g.fixed is None
                 opened = g.seg_open
                 fixed = g.fixed is not None
                 got = g.finish(raise_=False)

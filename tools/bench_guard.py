@@ -13,6 +13,11 @@ repeats, on the engine's stream = torch's (as bench.py):
                     segments on a stream of its own: routing, then the run
                     (no certificate) beside the copy + the segment
                     certificate on the guard's stream, then its verdict
+  guarded_fold_ms   the same with the routing folded into the run's join
+                    (kmz_route_ids_join; the copy waits for kmz_route_wait,
+                    i.e. the join's end, then runs beside the rest of the
+                    run), as bench.py runs it since round 6; step_route_ms:
+                    the run with the routing armed and nothing else
 The exchange over xGMI itself is not timed here (one GPU): its projection
 is the bytes each rank sends over its peer links at ~153 GB/s each.  Prints
 one JSON object."""
@@ -90,11 +95,35 @@ def main():
             assert rep is False
 
         guarded_ms = _timed(guarded)
+
+        def routed_run():
+            eng.route_ids_join(world, seg, send.data_ptr())
+            eng.run(flags | L.RUN_NO_CERT)
+
+        step_route = _timed(routed_run)
+        in_join = eng.route_wait(0)
+
+        def guarded_fold():
+            eng.route_ids_join(world, seg, send.data_ptr())
+            eng.run_begin(flags | L.RUN_NO_CERT)
+            eng.route_wait(cs.cuda_stream)
+            with torch.cuda.stream(cs):
+                recv.copy_(send)  # (stands in for the all-to-all)
+            gs.wait_stream(cs)
+            eng.id_repeats_seg_begin(recv.data_ptr(), world, seg, gs.cuda_stream)
+            eng.run_end()
+            rep, _ = eng.id_repeats_seg_end()
+            assert rep is False
+
+        fold_ms = _timed(guarded_fold)
         peer_bytes = 8 * n / world
         a2a = peer_bytes / 153e9 * 1e3
         out["worlds"][world] = {"spans_rank0": n, "step_ms": round(step, 3), "step_nocert_ms": round(step_nc, 3),
                                 "route_fixed_ms": round(route, 3), "route_fixed_hist_ms": round(route_hist, 3),
                                 "seg_certificate_ms": round(cert, 3), "guarded_step_ms": round(guarded_ms, 3),
+                                "step_route_ms": round(step_route, 3), "route_in_join": in_join,
+                                "guarded_fold_ms": round(fold_ms, 3),
+                                "guard_fold_ms_measured": round(fold_ms - step, 3),
                                 "all_to_all_bytes_per_rank": int(8 * n * (world - 1) / world),
                                 "all_to_all_ms_projected": round(a2a, 3),
                                 # the guard's cost on the step: what the guarded step adds to the
