@@ -856,6 +856,30 @@ __global__ void __launch_bounds__(256) k_chain_settle(const unsigned long long *
 // The pending spans (ancestry outside their LDS window), one pass: each hashes
 // its own and its parent's ancestry over the global contracted parents, then
 // joins or inserts its chain exactly like the tile kernel (no ordering needed).
+// The first PB ancestors of the walk stay in registers, so that a row's keys
+// are formed without walking again and their edge-set probes and claims go
+// out together (one round trip each instead of one per ancestor, in turn:
+// the pending spans are the deepest ancestries, and this kernel is a serial
+// latency chain on small batches -- 62 us of config 5's 2 500-trace tick).
+#ifndef KMZ_PEND_PB
+#define KMZ_PEND_PB 16
+#endif
+constexpr int PB = KMZ_PEND_PB;
+// edge_insert from the slot after `pos` (its home slot was taken by another key)
+__device__ __forceinline__ void edge_insert_after(uint64_t key, uint64_t pos, unsigned long long *__restrict__ trip,
+                                                  uint64_t tcap, uint32_t *flags) {
+  for (uint32_t z = 1; z < PROBE_MAX; ++z) {
+    pos = eset_next(pos, tcap);
+    uint64_t cur = trip[pos];
+    if (cur == key) return;
+    if (cur == 0) {
+      cur = atomicCAS(&trip[pos], 0ull, (unsigned long long)key);
+      if (cur == 0 || cur == key) return;
+    }
+  }
+  *flags |= F_TRIPLE_OVERFLOW;
+}
+
 __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict__ plist, uint32_t pcap,
                                                      const uint8_t *__restrict__ kind,
                                                      const uint32_t *__restrict__ shape,
@@ -886,23 +910,43 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     uint32_t d = 0;
     bool bad = false;
     const uint32_t a = cparent[i];
-    for (uint32_t cur = a; cur != NONE; cur = cparent[cur]) {
-      if (cur >= n) {  // CYC (a CLIENT loop); never another value (k_pend/k_resolve leave indices < n)
-        if (cur == CYC) flags |= F_CYCLE;
-        else flags |= F_RANGE;
-        bad = true;
-        break;
+    uint32_t aid[PB], ash[PB];  // the first PB ancestors: index, shape, SERVER or not
+    bool asrv[PB];
+    uint32_t cur = a;
+    auto hop = [&](uint32_t c, uint32_t &sa, bool &srv) -> bool {  // one ancestor into the folds
+      if (c >= n) {  // CYC (a CLIENT loop); never another value (k_pend/k_resolve leave indices < n)
+        flags |= c == CYC ? F_CYCLE : F_RANGE;
+        return false;
       }
       if (++d > MAX_DEPTH) {
         flags |= F_CYCLE;
-        bad = true;
-        break;
+        return false;
       }
-      const uint32_t sa = shape[cur];
+      sa = shape[c];
+      srv = kind[c] == KIND_SERVER;
       const uint32_t ea = sa < n_shapes ? (by_shape ? sa : dep_ep[sa]) : NONE;
-      const uint64_t el = sig_elem(ea, kind[cur] == KIND_SERVER, seed);
+      const uint64_t el = sig_elem(ea, srv, seed);
       acc = sig_step(acc, el);
       pacc = d == 1 ? el : sig_step(pacc, el);
+      return true;
+    };
+#pragma unroll
+    for (int k = 0; k < PB; ++k) {
+      aid[k] = 0;
+      ash[k] = NONE;
+      asrv[k] = false;
+      if (bad || cur == NONE) continue;
+      aid[k] = cur;
+      if (!hop(cur, ash[k], asrv[k])) {
+        bad = true;
+        continue;
+      }
+      cur = cparent[cur];
+    }
+    for (; !bad && cur != NONE; cur = cparent[cur]) {  // deeper than PB: folded, not kept
+      uint32_t sa;
+      bool srv;
+      if (!hop(cur, sa, srv)) bad = true;
     }
     if (bad) continue;
     const uint64_t sg = sig_final(acc, d, seed, &flags), psig = a == NONE ? ROOT_SIG : sig_final(pacc, d - 1, seed, &flags);
@@ -912,18 +956,56 @@ __global__ void __launch_bounds__(256) k4_chain_pend(const uint32_t *__restrict_
     if (r == 0) flags |= F_SPIN;  // (the row is not counted: the run is redone on the exact walk)
     if (r <= 0) continue;         // (-1: F_CHAIN_OVERFLOW, redone with a larger table)
     if (on) {  // a row: its relations, keys (new chain) and non-SERVER ancestors
-      uint32_t kk = 0;
-      for (uint32_t cur = a; cur != NONE; cur = cparent[cur]) {
-        ++kk;
-        const uint8_t ka = kind[cur];
-        const uint32_t sa = shape[cur];
-        const uint32_t ea = sa < n_shapes ? dep_ep[sa] : NONE;
-        if (ea >= n_ep) {
+      const uint32_t dk = min(d, (uint32_t)PB);
+      // every load of the kept ancestors issued before any is used
+      uint32_t eak[PB];
+      int64_t tk[PB];
+#pragma unroll
+      for (int k = 0; k < PB; ++k) {
+        eak[k] = n_shapes ? dep_ep[(uint32_t)k < dk && ash[k] < n_shapes ? ash[k] : 0] : NONE;
+        tk[k] = ts[aid[k]];
+      }
+      uint64_t key[PB], pos[PB], cv[PB];
+      bool ins[PB], ok = true;
+#pragma unroll
+      for (int k = 0; k < PB; ++k) {
+        ins[k] = false;
+        if ((uint32_t)k >= dk || !ok) continue;
+        const uint32_t ea = ash[k] < n_shapes ? eak[k] : NONE;
+        if (ea >= n_ep) {  // (as the walk: the keys stop at the first unmapped ancestor)
           flags |= F_RANGE;
-          break;
+          ok = false;
+          continue;
         }
-        if (r != 2) edge_insert(edge_key(ea, es, kk, ka == KIND_SERVER), trip, tcap, &flags);
-        if (ka != KIND_SERVER) atomicMax(&ep_ts[ea], (unsigned long long)((uint64_t)ts[cur] ^ TS_BIAS));
+        key[k] = edge_key(ea, es, k + 1, asrv[k]);
+        ins[k] = r != 2 && !(flags & F_TRIPLE_OVERFLOW);
+        if (!asrv[k]) atomicMax(&ep_ts[ea], (unsigned long long)((uint64_t)tk[k] ^ TS_BIAS));
+      }
+#pragma unroll
+      for (int k = 0; k < PB; ++k) {  // home slots: loads, then claims, in flight together
+        pos[k] = ins[k] ? eslot(key[k], tcap) : 0;
+        cv[k] = ins[k] ? trip[pos[k]] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < PB; ++k)
+        if (ins[k] && cv[k] == 0) cv[k] = atomicCAS(&trip[pos[k]], 0ull, (unsigned long long)key[k]);
+#pragma unroll
+      for (int k = 0; k < PB; ++k)  // (rare: the home slot held another key)
+        if (ins[k] && cv[k] != 0 && cv[k] != key[k]) edge_insert_after(key[k], pos[k], trip, tcap, &flags);
+      if (d > PB && ok) {  // deeper ancestors, one at a time
+        uint32_t kk = PB;
+        for (uint32_t c = cparent[aid[PB - 1]]; c != NONE; c = cparent[c]) {
+          ++kk;
+          const uint8_t ka = kind[c];
+          const uint32_t sa = shape[c];
+          const uint32_t ea = sa < n_shapes ? dep_ep[sa] : NONE;
+          if (ea >= n_ep) {
+            flags |= F_RANGE;
+            break;
+          }
+          if (r != 2) edge_insert(edge_key(ea, es, kk, ka == KIND_SERVER), trip, tcap, &flags);
+          if (ka != KIND_SERVER) atomicMax(&ep_ts[ea], (unsigned long long)((uint64_t)ts[c] ^ TS_BIAS));
+        }
       }
       atomicAdd(&stats64[S_ROWS], 1ull);
       atomicAdd(&stats64[S_REL], (unsigned long long)d);

@@ -458,7 +458,10 @@ void launch_chain_settle_list(hipStream_t s, uint32_t nt, void *ctab, uint64_t c
                               const unsigned long long *defer, uint32_t dcap, uint32_t *gpos, uint32_t gcap,
                               uint32_t ablate, const uint32_t *id_ep, uint32_t n_ids) {
   if (!nt) return;
-  hipLaunchKernelGGL(k_chain_settle_list, dim3(std::min<uint32_t>(2048, std::max<uint32_t>(64, nt))), dim3(256), 0, s,
+  // (2048 workgroups at any size: the lists' lengths are on the device, and a
+  // small batch's keys taken ~8 per thread, each insert a round trip, made
+  // this a serial latency chain: 28 / 65 us of the mesh / config 5 ticks)
+  hipLaunchKernelGGL(k_chain_settle_list, dim3(2048), dim3(256), 0, s,
                      stage, scap, defer, dcap, trip, tcap, reinterpret_cast<unsigned long long *>(ctab), ccap, counters,
                      stats64, gpos, gcap, spin_bound(ablate), id_ep, n_ids);
   launch_tile_sum(s, tile_stats, nt, 4u, 4u, stats64 + S_ROWS, 2u);  // rows, rel, maxd, chains
