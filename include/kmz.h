@@ -262,6 +262,17 @@ int kmz_get_span_links(kmz_ctx *ctx, uint32_t *cparent, uint64_t *rowpos, uint64
  * Pinned (page-locked) output buffers copy fastest. */
 int kmz_fetch(kmz_ctx *ctx, kmz_group *groups, uint64_t groups_cap, uint64_t *triples, uint64_t triples_cap,
               uint64_t *n_triples, kmz_endpoint *endpoints, uint64_t endpoints_cap);
+/* kmz_fetch with only the USED groups (combined > 0), in ascending group id:
+ * ids[k] is group k's index in the dense array, groups[k] its value.  The
+ * toCombinedRealtimeData entries are exactly these (RealtimeDataList.ts:22-45
+ * emits a group per (endpoint, status) that occurs); a small batch touches a
+ * few percent of the (endpoint x status) space, so the dense copy was most of
+ * a 2 500-trace tick's fetch.  *n_used receives the count (groups_cap 0 and
+ * no other set: the count alone).  KMZ_E_UNSUPPORTED past 2^22 groups (use
+ * kmz_fetch). */
+int kmz_fetch_used(kmz_ctx *ctx, uint32_t *ids, kmz_group *groups, uint64_t groups_cap, uint64_t *n_used,
+                   uint64_t *triples, uint64_t triples_cap, uint64_t *n_triples, kmz_endpoint *endpoints,
+                   uint64_t endpoints_cap);
 /* kmz_fetch in two halves, for a loop over consecutive batches: _begin takes
  * a device copy of the run's three result sets (on the run's stream, so the
  * next kmz_run may overwrite its own buffers at once) and queues their copies

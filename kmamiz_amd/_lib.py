@@ -171,6 +171,8 @@ SIGNATURES = [
     ("kmz_json_forget", C.c_int, [_P]),
     ("kmz_fetch", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64]),
     ("kmz_fetch_begin", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64]),
+    ("kmz_fetch_used", C.c_int, [_P, _P, _P, C.c_uint64, C.POINTER(C.c_uint64), _P, C.c_uint64,
+                                 C.POINTER(C.c_uint64), _P, C.c_uint64]),
     ("kmz_fetch_end", C.c_int, [_P]),
     ("kmz_group_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),
     ("kmz_endpoint_partials", C.c_int, [_P, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]),

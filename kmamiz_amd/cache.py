@@ -585,23 +585,28 @@ class CombinedColumns:
 
     @classmethod
     def from_groups(cls, groups: np.ndarray, n_status: int, ep_fields, statuses: Sequence,
-                    like: Optional["CombinedColumns"] = None) -> "CombinedColumns":
+                    like: Optional["CombinedColumns"] = None, used: Optional[np.ndarray] = None) -> "CombinedColumns":
         """Columns of RealtimeDataList.toCombinedRealtimeData() straight from the
         engine's dense groups (kmz_get_groups, [n_ep * n_status]): used groups
         ordered by their endpoint's first row, then their own first row
         (RealtimeDataList.ts:22-45).  ep_fields(e): the row fields of endpoint e
         (Traces.ts:73-99; long-lived dicts, memoised by identity); statuses[s]:
-        the interned status values.  No Envoy logs here (no content types)."""
+        the interned status values.  No Envoy logs here (no content types).
+        With ``used`` (kmz_fetch_used's ids), ``groups`` holds only the used
+        groups, groups[k] the one of id used[k]."""
         out = cls(like.tab if like else None)
         T = out.tab
-        used = np.nonzero(groups["combined"] > 0)[0]
+        if used is None:
+            used = np.nonzero(groups["combined"] > 0)[0]
+            groups = groups[used]
+        used = np.asarray(used, dtype=np.int64)
         ep, st = used // n_status, used % n_status
-        first = groups["first"][used]
+        first = groups["first"]
         if len(used):
             epf = np.full(int(ep.max()) + 1, np.iinfo(np.uint64).max, np.uint64)
             np.minimum.at(epf, ep, first)
             o = np.lexsort((first, epf[ep]))
-            used, ep, st = used[o], ep[o], st[o]
+            used, ep, st, groups = used[o], ep[o], st[o], groups[o]
         st_txt = [tpl(v) for v in statuses]
         keys, metas = [], []
         for e, s in zip(ep.tolist(), st.tolist()):
@@ -618,11 +623,11 @@ class CombinedColumns:
             metas.append(hit[1])
         out.key = np.array(keys, np.int64)
         out.meta = np.array(metas, np.int64)
-        out.combined = groups["combined"][used].astype(np.int64)
-        out.latest = groups["latest_timestamp"][used].astype(np.float64)
+        out.combined = groups["combined"].astype(np.int64)
+        out.latest = groups["latest_timestamp"].astype(np.float64)
         out.latest_int = np.ones(len(used), bool)
-        out.mean = groups["mean"][used].astype(np.float64)
-        out.cv = groups["cv"][used].astype(np.float64)
+        out.mean = groups["mean"].astype(np.float64)
+        out.cv = groups["cv"].astype(np.float64)
         out.body = {f: _undef_col(len(used)) for f in _BODY_FIELDS}
         return out
 

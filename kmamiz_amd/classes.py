@@ -252,7 +252,7 @@ class RealtimeDataList:
             eng = traces._load()
             eng.run(L.RUN_STATS_RT if rule == "rt" else L.RUN_STATS_TAG)
             batch, d, _ = traces._ingest()
-            return CombinedRealtimeDataList(_combine_native(eng.groups(), eng.index_base, batch, d, rule, replicas,
+            return CombinedRealtimeDataList(_combine_native(_run_groups(eng), eng.index_base, batch, d, rule, replicas,
                                                             traces if logs else None, logs))
         rows = self._rows or []
         batch, table, d, first_row = ingest_rows(rows)
@@ -260,17 +260,43 @@ class RealtimeDataList:
         eng.load(batch, table)
         eng._loaded_token = None
         eng.run(L.RUN_STATS_RT)
-        return CombinedRealtimeDataList(_combine_rows(eng.groups(), rows, d, table.n_status))
+        return CombinedRealtimeDataList(_combine_rows(_run_groups(eng), rows, d, table.n_status))
 
 
-def _ordered_groups(groups: np.ndarray, n_status: int):
+class _UsedGroups:
+    """The used groups of a run (kmz_fetch_used: ids ascending, their records),
+    indexable by group id like the dense array."""
+
+    def __init__(self, ids: np.ndarray, recs: np.ndarray):
+        self.ids = np.asarray(ids, dtype=np.int64)
+        self.recs = recs
+
+    def __getitem__(self, g):
+        return self.recs[int(np.searchsorted(self.ids, g))]
+
+
+def _run_groups(eng):
+    """The last stats run's groups: only the used ones where the engine
+    compacts them (a small batch touches a few percent of the groups), else
+    the dense array."""
+    try:
+        ids, recs, _, _ = eng.fetch_used(deps=False)
+    except Exception:  # noqa: BLE001 (KMZ_E_UNSUPPORTED past 2^22 groups: the dense copy)
+        return eng.groups()
+    return _UsedGroups(ids.copy(), recs.copy())
+
+
+def _ordered_groups(groups, n_status: int):
     """Used groups in toCombinedRealtimeData order: endpoints by first row,
     statuses by first row within the endpoint (RealtimeDataList.ts:24-45)."""
-    used = np.nonzero(groups["combined"] > 0)[0]
+    if isinstance(groups, _UsedGroups):
+        used, first = groups.ids, groups.recs["first"]
+    else:
+        used = np.nonzero(groups["combined"] > 0)[0]
+        first = groups["first"][used]
     if len(used) == 0:
         return []
     ep = used // n_status
-    first = groups["first"][used]
     ep_first = {}
     for e, f in zip(ep.tolist(), first.tolist()):
         if e not in ep_first or f < ep_first[e]:

@@ -67,6 +67,9 @@ struct kmz_ctx {
   DevBuf rt_pool1, rt_dir, rt_pool2, rt_cur;  // ... and its own certificate buffers (the run's stay as the run left them)
   DevBuf rt_tsz;                               // ... segment tile sizes (kmz_id_repeats_seg_begin)
   DevBuf rt_jcur;                              // ... the join-folded routing's per-owner cursors (128 B each)
+  DevBuf gu_ids, gu_grp, gu_bcnt;              // the used groups compacted (kmz_fetch_used)
+  bool gu_ok = false;    // grp_final's used groups are compacted in gu_* (G <= 2^22)
+  bool gu_host = false;  // ... and their count is in the run's read-back (not after kmz_finalize)
   // kmz_id_repeats_seg_begin/_end: the open check's stream, segment size, plan
   // and pinned read-back (counters, then the largest count)
   bool rs_open = false;
@@ -416,7 +419,7 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->synth_cnt, &c->synth_off, &c->dur_table, &c->k3pool, &c->k3dir, &c->k3part,
                     &c->tile_tmp, &c->sgrp, &c->dp, &c->cpool1, &c->cpool2, &c->ccur, &c->cdir, &c->mkey,
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
-                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->rt_tsz, &c->rt_jcur, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
+                    &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->rt_tsz, &c->rt_jcur, &c->gu_ids, &c->gu_grp, &c->gu_bcnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_pset, &c->tl_pkey, &c->tl_pval,
                     &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt,
                     &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->tl_lbkt, &c->tl_lbn, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
@@ -1535,6 +1538,20 @@ static int run_deps(kmz_ctx *c, bool links) {
   return KMZ_OK;
 }
 
+// finalisation of the endpoint groups, with the used groups compacted beside
+// it where G allows (kmz_fetch_used)
+static int finalize_groups(kmz_ctx *c) {
+  const uint32_t G = c->G;
+  c->gu_ok = G && used_chunks(G) <= USED_MAX_CHUNKS;
+  if (c->gu_ok && (ensure(c, c->gu_ids, (size_t)G * 4) || ensure(c, c->gu_grp, (size_t)G * sizeof(kmz_group)) ||
+                   ensure(c, c->gu_bcnt, (size_t)used_chunks(G) * 4)))
+    return KMZ_E_HIP;
+  GroupsUsed u{P<uint32_t>(c->gu_ids), P<uint32_t>(c->gu_bcnt), P<kmz_group>(c->gu_grp),
+               P<unsigned long long>(c->stats64) + S_GUSED};
+  launch_finalize(c->stream, P<unsigned long long>(c->grp), G, P<kmz_group>(c->grp_final), c->gu_ok ? &u : nullptr);
+  return KMZ_OK;
+}
+
 static int run_stats(kmz_ctx *c, uint32_t mode) {
   uint32_t n_ep = mode == KMZ_RUN_STATS_RT ? c->n_rt : c->n_tag;
   const uint32_t *tab = mode == KMZ_RUN_STATS_RT ? P<uint32_t>(c->d_rt) : P<uint32_t>(c->d_tag);
@@ -1557,7 +1574,7 @@ static int run_stats(kmz_ctx *c, uint32_t mode) {
     Timed t(c, KMZ_K_FINAL);
     launch_collapse_groups(c->stream, P<unsigned long long>(c->sgrp), c->n_shapes, c->n_status, tab, n_ep, grp,
                            P<unsigned int>(c->counters));
-    launch_finalize(c->stream, grp, c->G, P<kmz_group>(c->grp_final));
+    if (int r2 = finalize_groups(c)) return r2;
   }
   return KMZ_OK;
 }
@@ -1629,6 +1646,9 @@ static int remap_results(kmz_ctx *c, uint32_t flags, bool links) {
     launch_remap_index(c->stream, P<unsigned long long>(c->grp) + 5ull * c->G, c->G, 1, 0, ls, gs, c->imap_n);
     launch_remap_index(c->stream, P<unsigned long long>(c->grp_final) + 1, c->G, sizeof(kmz_group) / 8, 0, ls, gs,
                        c->imap_n);
+    if (c->gu_ok)  // (entries past the used count are remapped too: harmless)
+      launch_remap_index(c->stream, P<unsigned long long>(c->gu_grp) + 1, c->G, sizeof(kmz_group) / 8, 0, ls, gs,
+                         c->imap_n);
   }
   if (flags & KMZ_RUN_DEPS) {
     launch_remap_index(c->stream, P<unsigned long long>(c->epp) + c->n_dep, c->n_dep, 1, 1, ls, gs, c->imap_n);
@@ -1944,6 +1964,7 @@ int kmz_run_begin(kmz_ctx *c, uint32_t flags) {
   c->k4_now = (flags & KMZ_RUN_DEPS) ? k4_direct(c) : false;
   c->no_cert = (flags & KMZ_RUN_NO_CERT) != 0;
   c->rt_routed = c->rt_in_join = false;  // (kmz_route_wait: this run's routing only)
+  c->gu_host = true;
   if (int r = run_attempt(c, flags, links, h, s64)) {
     c->rt_armed = false;
     return r;
@@ -2194,6 +2215,45 @@ int kmz_fetch(kmz_ctx *c, kmz_group *groups, uint64_t gcap, uint64_t *trip, uint
     any = true;
   }
   if (any) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (eps) endpoints_from(reinterpret_cast<const uint64_t *>(c->hep), c->n_dep, eps);
+  return KMZ_OK;
+}
+
+int kmz_fetch_used(kmz_ctx *c, uint32_t *ids, kmz_group *groups, uint64_t gcap, uint64_t *n_used, uint64_t *trip,
+                   uint64_t tcap, uint64_t *n_trip, kmz_endpoint *eps, uint64_t ecap) {
+  if (!c || !n_used || (gcap && (!ids || !groups))) return KMZ_E_ARG;
+  if (c->run_open) return run_busy(c);
+  if (c->fetch_open) {
+    const int r = kmz_fetch_end(c);
+    if (r) return r;
+  }
+  uint64_t nt = 0;
+  if (int r = fetch_check(c, nullptr, 0, trip, tcap, n_trip, eps, ecap, &nt)) return r;
+  if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
+  if (!c->gu_ok) return fail(c, KMZ_E_UNSUPPORTED, "more than 2^22 groups: kmz_fetch the dense groups");
+  uint64_t nu;
+  if (c->hpin_valid && c->gu_host) {
+    nu = reinterpret_cast<const unsigned long long *>(reinterpret_cast<const unsigned int *>(c->hpin) + C_COUNT)[S_GUSED];
+  } else {
+    unsigned long long v = 0;
+    HIPCHK(c, hipMemcpyAsync(&v, P<unsigned long long>(c->stats64) + S_GUSED, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    nu = v;
+  }
+  *n_used = nu;
+  if (!gcap && !trip && !eps) return KMZ_OK;  // (the count only)
+  if (gcap < nu) return fail(c, KMZ_E_ARG, "output too small");
+  if (nu) {
+    HIPCHK(c, hipMemcpyAsync(ids, c->gu_ids.p, nu * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(groups, c->gu_grp.p, nu * sizeof(kmz_group), hipMemcpyDeviceToHost, c->stream));
+  }
+  if (trip && nt) HIPCHK(c, hipMemcpyAsync(trip, c->trip_out.p, nt * 8, hipMemcpyDeviceToHost, c->stream));
+  const size_t eb = (size_t)c->n_dep * 16;
+  if (eps && c->n_dep) {
+    if (int r = pinned_staging(c, c->hep, c->hep_bytes, eb)) return r;
+    HIPCHK(c, hipMemcpyAsync(c->hep, c->epp.p, eb, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   if (eps) endpoints_from(reinterpret_cast<const uint64_t *>(c->hep), c->n_dep, eps);
   return KMZ_OK;
 }
@@ -2933,8 +2993,9 @@ int kmz_finalize(kmz_ctx *c) {
   if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
   {
     Timed t(c, KMZ_K_FINAL);
-    launch_finalize(c->stream, P<unsigned long long>(c->grp), c->G, P<kmz_group>(c->grp_final));
+    if (int r = finalize_groups(c)) return r;
   }
+  c->gu_host = false;  // (the used count is on the device only)
   return kmz_sync(c);
 }
 

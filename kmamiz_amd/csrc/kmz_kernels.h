@@ -45,7 +45,7 @@ constexpr uint32_t CERT_DUP = 1u, CERT_OVF = 2u;
 constexpr uint32_t MISSV = 0xFFFFFFFDu;  // dp: parent id not in the span's window
 constexpr uint32_t PEND = 0xFFFFFFFCu;   // cparent: CLIENT chain leaves the window
 // u64 device statistics
-enum { S_ROWS = 0, S_REL = 1, S_MAXD = 2, S_CHAINS = 3, S_SERVER = 4, S_TRIP_OUT = 5, S_DEPENT = 6, S_COUNT = 8 };
+enum { S_ROWS = 0, S_REL = 1, S_MAXD = 2, S_CHAINS = 3, S_SERVER = 4, S_TRIP_OUT = 5, S_DEPENT = 6, S_GUSED = 7, S_COUNT = 8 };
 
 struct DupEntry {
   uint32_t pos, idx, winner, pad;
@@ -102,7 +102,17 @@ void launch_walk(hipStream_t s, const uint64_t *sid, const uint8_t *kind, const 
                  const unsigned int *dval, uint32_t dcap, unsigned long long *trip, uint64_t tcap,
                  unsigned long long *ep_ts, unsigned long long *ep_first, unsigned long long *rowpos,
                  unsigned int *counters, unsigned long long *stats64, uint32_t ablate = 0);
-void launch_finalize(hipStream_t s, unsigned long long *grp, uint32_t G, kmz_group *out);
+// the used groups (combined > 0) compacted in ascending id beside the dense
+// finalisation (kmz_fetch_used): ids, groups, per-chunk counts, the total
+struct GroupsUsed {
+  uint32_t *ids, *bcnt;
+  kmz_group *groups;
+  unsigned long long *total;
+};
+constexpr uint32_t USED_MAX_CHUNKS = 4096;  // (1024 groups a chunk: G <= 2^22)
+uint32_t used_chunks(uint32_t G);
+void launch_finalize(hipStream_t s, unsigned long long *grp, uint32_t G, kmz_group *out,
+                     const GroupsUsed *u = nullptr);
 void launch_compact(hipStream_t s, const unsigned long long *trip, uint64_t tcap, unsigned long long *out,
                     unsigned long long *count);
 void launch_synth_count(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, uint64_t *cnt);

@@ -536,15 +536,77 @@ __global__ void __launch_bounds__(256) k_walk(const uint64_t *__restrict__ sid, 
 // ---------------------------------------------------------------------------
 // finalisation / compaction
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_finalize(GroupAcc acc, uint32_t G, kmz_group *__restrict__ out) {
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < G; g += gridDim.x * blockDim.x) {
-    kmz_group r;
-    r.combined = acc.cnt[g];
-    r.first = acc.fst[g];
-    r.latest_timestamp = (int64_t)(acc.tsx[g] ^ TS_BIAS);
-    finalize_moments(acc.cnt[g], acc.s1[g], acc.s2a[g], acc.s2b[g], &r.mean, &r.cv);
-    out[g] = r;
+// Each workgroup finalises whole chunks of FZ_CH groups; with `bcnt` (one
+// chunk per workgroup) it also counts the chunk's used groups (combined > 0)
+// for k_used_scatter.
+constexpr uint32_t FZ_T = 256, FZ_PT = 4, FZ_CH = FZ_T * FZ_PT;
+__global__ void __launch_bounds__(FZ_T) k_finalize(GroupAcc acc, uint32_t G, kmz_group *__restrict__ out,
+                                                   uint32_t *__restrict__ bcnt) {
+  __shared__ uint32_t wsum[FZ_T / 64];
+  for (uint64_t base = (uint64_t)blockIdx.x * FZ_CH; base < G; base += (uint64_t)gridDim.x * FZ_CH) {
+    uint32_t used = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < FZ_PT; ++q) {
+      const uint64_t g = base + q * FZ_T + threadIdx.x;
+      if (g >= G) continue;
+      kmz_group r;
+      r.combined = acc.cnt[g];
+      r.first = acc.fst[g];
+      r.latest_timestamp = (int64_t)(acc.tsx[g] ^ TS_BIAS);
+      finalize_moments(acc.cnt[g], acc.s1[g], acc.s2a[g], acc.s2b[g], &r.mean, &r.cv);
+      out[g] = r;
+      used += r.combined != 0;
+    }
+    if (bcnt) {  // (one chunk per workgroup)
+      for (int o = 32; o > 0; o >>= 1) used += __shfl_xor(used, o, 64);
+      if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = used;
+      __syncthreads();
+      if (threadIdx.x == 0) bcnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    }
   }
+}
+
+// The used groups in ascending id, compacted (kmz_fetch_used copies only
+// them: a 2 500-trace tick touches 7-19 % of the groups, and the dense copy
+// was most of its fetch).  Workgroup b: its chunk's offset = the used counts
+// of the chunks before it (at most 2^12 of them), then the chunk's used
+// groups in order by wave ballots; the last workgroup stores the total.
+__global__ void __launch_bounds__(FZ_T) k_used_scatter(const kmz_group *__restrict__ dense, uint32_t G,
+                                                       const uint32_t *__restrict__ bcnt, uint32_t *__restrict__ ids,
+                                                       kmz_group *__restrict__ used,
+                                                       unsigned long long *__restrict__ total) {
+  __shared__ uint32_t wsum[FZ_T / 64];
+  __shared__ uint32_t wpre[FZ_PT][FZ_T / 64];
+  const uint32_t b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t pre = 0;
+  for (uint32_t k = threadIdx.x; k < b; k += FZ_T) pre += bcnt[k];
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  bool f[FZ_PT];
+  uint64_t m[FZ_PT];
+#pragma unroll
+  for (uint32_t q = 0; q < FZ_PT; ++q) {
+    const uint64_t g = (uint64_t)b * FZ_CH + q * FZ_T + threadIdx.x;
+    f[q] = g < G && dense[g].combined != 0;
+    m[q] = __ballot(f[q]);
+    if (lane == 0) wpre[q][w] = __popcll(m[q]);
+  }
+  if (lane == 0) wsum[w] = pre;
+  __syncthreads();
+  uint32_t off = wsum[0] + wsum[1] + wsum[2] + wsum[3];  // the chunks before this one
+  const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+  for (uint32_t q = 0; q < FZ_PT; ++q) {
+    uint32_t at = off;
+    for (uint32_t v = 0; v < w; ++v) at += wpre[q][v];
+    if (f[q]) {
+      const uint64_t g = (uint64_t)b * FZ_CH + q * FZ_T + threadIdx.x;
+      const uint32_t pos = at + (uint32_t)__popcll(m[q] & lt);
+      ids[pos] = (uint32_t)g;
+      used[pos] = dense[g];
+    }
+    for (uint32_t v = 0; v < FZ_T / 64; ++v) off += wpre[q][v];
+  }
+  if (b + 1 == gridDim.x && threadIdx.x == 0) *total = off;
 }
 
 // K3 runs once per batch over (shape x status).  The endpoint groups of either
@@ -795,10 +857,18 @@ void launch_fill(hipStream_t s, const FillArgs &a) {
   hipLaunchKernelGGL(k_fill, dim3(gx, a.n), dim3(256), 0, s, a);
 }
 
-void launch_finalize(hipStream_t s, unsigned long long *grp, uint32_t G, kmz_group *out) {
+uint32_t used_chunks(uint32_t G) { return (G + FZ_CH - 1) / FZ_CH; }
+
+void launch_finalize(hipStream_t s, unsigned long long *grp, uint32_t G, kmz_group *out, const GroupsUsed *u) {
   if (!G) return;
   GroupAcc a{grp, grp + G, grp + 2ull * G, grp + 3ull * G, grp + 4ull * G, grp + 5ull * G};
-  hipLaunchKernelGGL(k_finalize, dim3(grid_for(G, 1024)), dim3(256), 0, s, a, G, out);
+  if (u && used_chunks(G) <= USED_MAX_CHUNKS) {
+    const uint32_t nb = used_chunks(G);
+    hipLaunchKernelGGL(k_finalize, dim3(nb), dim3(FZ_T), 0, s, a, G, out, u->bcnt);
+    hipLaunchKernelGGL(k_used_scatter, dim3(nb), dim3(FZ_T), 0, s, out, G, u->bcnt, u->ids, u->groups, u->total);
+  } else {
+    hipLaunchKernelGGL(k_finalize, dim3(grid_for(G, 1024)), dim3(FZ_T), 0, s, a, G, out, (uint32_t *)nullptr);
+  }
 }
 
 void launch_collapse_groups(hipStream_t s, const unsigned long long *sg, uint32_t n_shapes, uint32_t S,

@@ -222,7 +222,7 @@ def test_combined_columns_from_engine_groups():
     the C oracle's groups of a mixed batch; and merges like them."""
     from kmamiz_amd import _lib as L
     from kmamiz_amd.cache import CombinedColumns
-    from kmamiz_amd.classes import CombinedRealtimeDataList, _combine_native
+    from kmamiz_amd.classes import CombinedRealtimeDataList, _combine_native, _UsedGroups
     from kmamiz_amd.ingest import ingest_traces
 
     def groups_of(traces):
@@ -245,6 +245,12 @@ def test_combined_columns_from_engine_groups():
             first_shape.setdefault(e, sh)
         cols = CombinedColumns.from_groups(g, t.n_status, lambda e: idents[first_shape[e]].fields, d.statuses)
         assert cols.toJSON() == rows
+        # the used groups alone (kmz_fetch_used's form): the same columns and rows
+        used = np.nonzero(g["combined"] > 0)[0]
+        cu = CombinedColumns.from_groups(g[used].copy(), t.n_status, lambda e: idents[first_shape[e]].fields,
+                                         d.statuses, used=used.astype(np.uint32))
+        assert cu.toJSON() == rows
+        assert _combine_native(_UsedGroups(used, g[used].copy()), 0, batch, d, "tag", None) == rows
         parts.append((cols, rows))
     got = parts[0][0].combineWith(parts[1][0]).toJSON()
     exp = CombinedRealtimeDataList(copy.deepcopy(parts[0][1])).combineWith(

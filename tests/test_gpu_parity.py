@@ -1296,6 +1296,8 @@ def test_shard_generation_and_index_map(engine, config, t0, t1, world):
         engine.set_index_map(ls, gs)
         engine.run(flags)
         host = engine.fetch()
+        host = (host[0].copy(), host[1].copy(), host[2].copy())
+        _check_fetch_used(engine, host)  # (the compacted groups remapped to global indices too)
         assert dev[0].tobytes() == host[0].tobytes()
         assert np.array_equal(dev[1], np.sort(host[1]))
         assert dev[2].tobytes() == host[2].tobytes()
@@ -1326,6 +1328,45 @@ def test_shard_generation_and_index_map(engine, config, t0, t1, world):
     engine.export_partials(L.PART_ENDPOINTS, we.ctypes.data, ew, False)
     assert np.array_equal(canon_limbs(wg), canon_limbs(g))
     assert np.array_equal(we, e)
+
+
+def _check_fetch_used(engine, dense):
+    """kmz_fetch_used == the dense fetch's used groups (ascending ids), the
+    same edge keys and endpoints."""
+    g, t, e = dense
+    ids, gu, tu, eu = engine.fetch_used()
+    used = np.nonzero(g["combined"] > 0)[0]
+    assert np.array_equal(ids.astype(np.int64), used)
+    assert gu.tobytes() == g[used].tobytes()
+    assert np.array_equal(np.sort(tu), np.sort(t))
+    assert eu.tobytes() == e.tobytes()
+
+
+@pytest.mark.parametrize("config,ntr", [(2, 2500), (3, 2500), (5, 2500), (3, 40000), (5, 20000), (3, 370000)])
+def test_fetch_used_equals_dense_fetch(engine, config, ntr):
+    """The used groups compacted on the device (k_finalize's per-chunk counts
+    + k_used_scatter) after a run, and again after kmz_finalize (the merge
+    path, whose count is read from the device)."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+
+    engine.load_synthetic(config, synth.SEED, 0, ntr)
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    d = engine.fetch()
+    d = (d[0].copy(), d[1].copy(), d[2].copy())
+    assert (d[0]["combined"] > 0).sum() > 0
+    _check_fetch_used(engine, d)
+    gw = engine.partials_words(L.PART_GROUPS)
+    g = np.zeros(gw, np.uint64)
+    engine.export_partials(L.PART_GROUPS, g.ctypes.data, gw, False)
+    g[: gw // 6] = 0  # every group unused but those set again below: the compaction follows the import
+    g[0] = 3
+    engine.import_partials(L.PART_GROUPS, g.ctypes.data, gw, False)
+    engine.finalize()
+    d2 = engine.fetch()
+    d2 = (d2[0].copy(), d2[1].copy(), d2[2].copy())
+    assert (d2[0]["combined"] > 0).sum() == 1
+    _check_fetch_used(engine, d2)
 
 
 def canon_limbs(g):

@@ -40,26 +40,32 @@ def main():
         # (kmz_fuse.hip) where the batch allows; separate: k_join_window + the
         # tile walk (KMZ_ABLATE2 bit 4); direct: launches one at a time
         # (KMZ_ABLATE2 bit 23, = KMZ_HIPGRAPH=0); serial: no side stream (bit 25)
-        for mode, knob, knob2 in (("default", 0, 0), ("separate", 0, 16), ("direct", 0, 1 << 23),
+        # used: default, fetching only the used groups (kmz_fetch_used, round 6)
+        for mode, knob, knob2 in (("default", 0, 0), ("used", 0, 0), ("separate", 0, 16), ("direct", 0, 1 << 23),
                                   ("serial", 1 << 25, 0)):
             os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"] = str(knob), str(knob2)
             e = Engine(0)
             del os.environ["KMZ_ABLATE"], os.environ["KMZ_ABLATE2"]
+            fetch = e.fetch_used if mode == "used" else e.fetch
             for _ in range(10):  # warm: buffers, the graph capture
                 e.load(batch, table)
                 e.run(flags)
-                e.fetch()
-            t_run, t_tick = [], []
+                fetch()
+            t_run, t_tick, t_fetch = [], [], []
             for _ in range(args.ticks):
                 t0 = time.perf_counter()
                 e.load(batch, table)
                 t1 = time.perf_counter()
                 e.run(flags)
-                e.fetch()
+                tf = time.perf_counter()
+                fetch()
                 t2 = time.perf_counter()
                 t_run.append(t2 - t1)
                 t_tick.append(t2 - t0)
+                t_fetch.append(t2 - tf)
             res[mode] = {"run_fetch_us_median": round(float(np.median(t_run)) * 1e6, 1),
+                         "fetch_us_median": round(float(np.median(t_fetch)) * 1e6, 1),
+                         "groups": int(e.info()["n_groups"]), "groups_used": int(len(e.fetch_used()[0])),
                          "tick_us_median": round(float(np.median(t_tick)) * 1e6, 1),
                          "tick_us_p99": round(float(np.percentile(t_tick, 99)) * 1e6, 1),
                          "graph_replays": e.graph_stats()[0]}
