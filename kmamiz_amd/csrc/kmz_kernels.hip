@@ -668,44 +668,53 @@ __global__ void __launch_bounds__(256) k_collapse_endpoints(const unsigned long 
   }
 }
 
-// Edge-set compaction: each workgroup owns a contiguous slice of the table,
-// counts its keys, reserves their output range with ONE atomic, then writes
-// them (a second, cache-resident read of the slice).  Output order is free
-// (the keys are a set).
-constexpr uint32_t COMPACT_BLOCKS = 512;
-__global__ void __launch_bounds__(256) k_compact(const unsigned long long *__restrict__ trip, uint64_t tcap,
-                                                 unsigned long long *__restrict__ out,
-                                                 unsigned long long *__restrict__ count) {
-  __shared__ uint32_t wsum[4];
-  __shared__ unsigned long long base;
-  const uint64_t per = (tcap + gridDim.x - 1) / gridDim.x;
-  const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(tcap, b0 + per);
+// Edge-set compaction: each workgroup takes chunks of CP_CH slots, each wave
+// a contiguous quarter of the chunk, CP_PL slots per lane held in registers
+// (every load in flight at once, one read of the table); the wave counts its
+// keys by ballots, the workgroup reserves the chunk's output range with ONE
+// atomic, and each wave writes its keys in slot order, one ballot prefix per
+// 64 slots (no barrier inside the loop).  Output order is free (the keys are
+// a set).  (The form with a second, cache-resident read of the slice and two
+// barriers per 256 slots took 148 us on config 5's 2^25-slot set.)
+constexpr uint32_t CP_T = 256, CP_PL = 32, CP_CH = CP_T * CP_PL;
+__global__ void __launch_bounds__(CP_T) k_compact(const unsigned long long *__restrict__ trip, uint64_t tcap,
+                                                  unsigned long long *__restrict__ out,
+                                                  unsigned long long *__restrict__ count) {
+  __shared__ uint32_t wsum[CP_T / 64];
+  __shared__ unsigned long long wbase[CP_T / 64];
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint32_t c = 0;
-  for (uint64_t p = b0 + threadIdx.x; p < b1; p += 256) c += trip[p] != 0;
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if (lane == 0) wsum[w] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    base = t ? atomicAdd(count, (unsigned long long)t) : 0;
-  }
-  __syncthreads();
-  unsigned long long run = base;
-  for (uint64_t p0 = b0; p0 < b1; p0 += 256) {
-    const uint64_t p = p0 + threadIdx.x;
-    const unsigned long long k = p < b1 ? trip[p] : 0;
-    const uint64_t m = __ballot(k != 0);
-    if (lane == 0) wsum[w] = __popcll(m);
-    __syncthreads();
-    uint32_t before = 0, tot = 0;
-    for (uint32_t v = 0; v < 4; ++v) {
-      before += v < w ? wsum[v] : 0;
-      tot += wsum[v];
+  const uint64_t lt = (1ull << lane) - 1;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * CP_CH; c0 < tcap; c0 += (uint64_t)gridDim.x * CP_CH) {
+    const uint64_t wb = c0 + (uint64_t)w * (CP_CH / (CP_T / 64));
+    unsigned long long k[CP_PL];
+#pragma unroll
+    for (uint32_t j = 0; j < CP_PL; ++j) {
+      const uint64_t p = wb + j * 64 + lane;
+      k[j] = p < tcap ? trip[p] : 0ull;
     }
-    if (k) out[run + before + __popcll(m & ((1ull << lane) - 1))] = k;
-    run += tot;
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < CP_PL; ++j) c += (uint32_t)__popcll(__ballot(k[j] != 0));
+    if (lane == 0) wsum[w] = c;
     __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (uint32_t v = 0; v < CP_T / 64; ++v) t += wsum[v];
+      unsigned long long b = t ? atomicAdd(count, (unsigned long long)t) : 0ull;
+      for (uint32_t v = 0; v < CP_T / 64; ++v) {
+        wbase[v] = b;
+        b += wsum[v];
+      }
+    }
+    __syncthreads();
+    unsigned long long run = wbase[w];
+#pragma unroll
+    for (uint32_t j = 0; j < CP_PL; ++j) {
+      const uint64_t m = __ballot(k[j] != 0);
+      if (k[j]) out[run + __popcll(m & lt)] = k[j];
+      run += __popcll(m);
+    }
+    __syncthreads();  // (wsum / wbase reused by the next chunk)
   }
 }
 
@@ -889,10 +898,10 @@ void launch_collapse_endpoints(hipStream_t s, const unsigned long long *sg, uint
 
 void launch_compact(hipStream_t s, const unsigned long long *trip, uint64_t tcap, unsigned long long *out,
                     unsigned long long *count) {
-  // (<= 8192 slots per workgroup: config 5's 2^25-slot set in 512 workgroups
-  // was a 256-step dependent loop per workgroup, 0.28 ms)
-  const uint32_t g = (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(COMPACT_BLOCKS, tcap / 8192));
-  hipLaunchKernelGGL(k_compact, dim3(g), dim3(256), 0, s, trip, tcap, out, count);
+  // (one CP_CH-slot chunk per workgroup up to 2^13 workgroups: config 5's
+  // 2^25-slot set in 512 workgroups was a 256-step dependent loop each, 0.28 ms)
+  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(8192, (tcap + CP_CH - 1) / CP_CH));
+  hipLaunchKernelGGL(k_compact, dim3(g), dim3(CP_T), 0, s, trip, tcap, out, count);
 }
 
 void launch_synth_count(hipStream_t s, int config, uint64_t seed, uint64_t t0, uint64_t nt, uint64_t *cnt) {
