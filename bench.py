@@ -222,7 +222,7 @@ def main():
         import numpy as np
 
         from kmamiz_amd.ingest import SHAPE_TAGS, UNDEFINED, tag_identity
-        from kmamiz_amd.tail import maps_for_synth, realtime_risk_columns, realtime_risk_from_sums, run_tail
+        from kmamiz_amd.tail import maps_for_synth, realtime_risk_columns, realtime_risk_from_sums, tail_begin, tail_end
 
         args.no_fetch = False
         tmaps = maps_for_synth(config)
@@ -246,17 +246,25 @@ def main():
         phases[name] = phases.get(name, 0.0) + (now - t)
         return now
 
-    def service_tail():
+    tail_sync = os.environ.get("KMZ_BENCH_TAIL_SYNC", "0") == "1"
+
+    def service_tail_begin():
         # the device half: what reads this run's buffers (the edge keys where
-        # the run left them in HBM; the combined groups)
+        # the run left them in HBM; the combined groups), enqueued right after
+        # the run so that the GPU goes on while the host fetches
         tp = time.perf_counter()
-        t = run_tail(eng, tmaps)
-        tp = mark("tail_run", tp)
+        tail_begin(eng, tmaps)
         # RiskAnalyzer.RealtimeRisk: the per-service sums over the combined
         # groups on the device (kmz_service_sums, bit-equal to the host's row
         # sums), the rest over the ~10^3 services on the host
-        sums = eng.service_sums()
-        mark("service_sums", tp)
+        eng.service_sums_begin()
+        mark("tail_begin", tp)
+
+    def service_tail_end():
+        tp = time.perf_counter()
+        t = tail_end(eng, tmaps)
+        sums = eng.service_sums_end()
+        mark("tail_end", tp)
         state["tail_host"] = (t, sums)
 
     def tail_host():
@@ -313,6 +321,10 @@ def main():
             eng.import_partials(L.PART_GROUPS, g.data_ptr(), gw, True)
             eng.import_partials(L.PART_ENDPOINTS, e.data_ptr(), ew, True)
             eng.finalize()
+        # (KMZ_BENCH_TAIL_SYNC=1, for comparison: the tail after the fetch,
+        # each half right after the other, as before round 6)
+        if tail_on and not tail_sync:
+            service_tail_begin()
         if not args.no_fetch:  # the three result sets (with the tail on, the edge keys stay
             # in HBM for kmz_tail_run: the service tail is the output)
             if args.fetch == "pipelined":
@@ -322,7 +334,9 @@ def main():
                 state["groups"], state["keys"], state["endpoints"] = eng.fetch(keys=not tail_on)
             mark("fetch", tp)
         if tail_on:
-            service_tail()
+            if tail_sync:
+                service_tail_begin()
+            service_tail_end()
 
     for w in range(args.warmup):
         step()

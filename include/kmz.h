@@ -466,6 +466,14 @@ int kmz_tail_map_set(kmz_ctx *ctx, const kmz_tail_map *map);
 /* run the tail over the context's current edge set (after KMZ_RUN_DEPS and
  * any kmz_merge_triples); synchronous, returns the result sizes */
 int kmz_tail_run(kmz_ctx *ctx, uint64_t *n_details, uint64_t *n_pairs);
+/* kmz_tail_run in two halves: _begin enqueues the tail on the context's
+ * stream (no wait), _end waits for it (repeating it with larger tables when
+ * one overflowed) and returns the result sizes.  Between them the host is
+ * free (a step's fetch and host finish run while the GPU computes the tail);
+ * kmz_run_begin, kmz_tail_map_set and the tail's getters are refused while
+ * a tail is open. */
+int kmz_tail_begin(kmz_ctx *ctx);
+int kmz_tail_end(kmz_ctx *ctx, uint64_t *n_details, uint64_t *n_pairs);
 /* per-service counters of the last tail run, 8 u32 per service id:
  *   [0] linked services with dependingBy > 0, [1] with dependingOn > 0
  *       (toServiceInstability, EndpointDependencies.ts:618-628)
@@ -500,6 +508,9 @@ typedef struct kmz_service_sum {
 int kmz_service_map_set(kmz_ctx *ctx, const uint32_t *sid_of_ep, uint32_t n_ep, uint32_t n_sid, const uint8_t *is_5xx,
                         uint32_t n_status);
 int kmz_service_sums(kmz_ctx *ctx, kmz_service_sum *out, uint64_t cap);
+/* kmz_service_sums in two halves (enqueue; wait and copy out), as the tail */
+int kmz_service_sums_begin(kmz_ctx *ctx);
+int kmz_service_sums_end(kmz_ctx *ctx, kmz_service_sum *out, uint64_t cap);
 /* copy the results: details and pairs in no particular order; has_in[e] = 1
  * when endpoint e's merged row has a non-empty dependingBy */
 int kmz_tail_get(kmz_ctx *ctx, kmz_tail_detail *details, uint64_t dcap, kmz_tail_pair *pairs, uint64_t pcap,

@@ -197,11 +197,15 @@ SIGNATURES = [
     ("kmz_get_global_index", C.c_int, [_P, _P, C.c_uint64, C.c_int]),
     ("kmz_tail_map_set", C.c_int, [_P, C.POINTER(TailMap)]),
     ("kmz_tail_run", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("kmz_tail_begin", C.c_int, [_P]),
+    ("kmz_tail_end", C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("kmz_tail_get", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, _P, C.c_uint64]),
     ("kmz_tail_service_stats", C.c_int, [_P, _P, C.c_uint64, _P, C.c_uint64, C.POINTER(C.c_uint32)]),
     ("kmz_tail_service_first", C.c_int, [_P, _P, C.c_uint64]),
     ("kmz_service_map_set", C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P, C.c_uint32]),
     ("kmz_service_sums", C.c_int, [_P, _P, C.c_uint64]),
+    ("kmz_service_sums_begin", C.c_int, [_P]),
+    ("kmz_service_sums_end", C.c_int, [_P, _P, C.c_uint64]),
     ("kmz_finalize", C.c_int, [_P]),
     ("kmz_finalize_host", None, [_P, C.c_uint64, _P]),
     ("kmz_host_exp", None, [_P, _P, C.c_uint64]),

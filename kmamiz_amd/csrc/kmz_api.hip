@@ -99,6 +99,9 @@ struct kmz_ctx {
   uint32_t tl_n_ep = 0, tl_n_cls = 0, tl_n_svc = 0, tl_n_dist = 64, tl_deep = 0;
   uint32_t tl_rel_dist = 0;  // distances in the last run's relying table (0: not complete, use the details)
   bool tl_map = false, tl_ran = false;
+  bool tl_open = false;       // kmz_tail_begin enqueued, kmz_tail_end not yet
+  uint64_t tl_nt = 0;         // ... its edge-key count
+  uint32_t tl_nd_run = 0;     // ... its relying-table width
   uint64_t tl_acap = 0, tl_pacap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0, tl_bcap = 0;
   uint32_t tl_bbits = 0;  // link-key buckets: 2^tl_bbits
   DevBuf tl_sfirst;              // per service: first row (k_tail_service_rows)
@@ -107,6 +110,9 @@ struct kmz_ctx {
   // RiskAnalyzer.RealtimeRisk's per-service sums (k_service_sums): CSR of the
   // services' stats endpoints, 5xx status mask, output
   DevBuf sv_off, sv_eps, sv_5xx, sv_out;
+  void *sv_host = nullptr;    // kmz_service_sums_begin's read-back (pinned)
+  size_t sv_host_bytes = 0;
+  bool sv_open = false;
   uint32_t sv_n_ep = 0, sv_n_sid = 0, sv_n_status = 0;
   bool sv_map = false;
   bool ctab_dirty = true;  // the chain table holds entries no list records (new, or a list overflowed)
@@ -435,6 +441,7 @@ void kmz_destroy(kmz_ctx *c) {
   if (c->hpin) hipHostFree(c->hpin);
   if (c->rs_pin) hipHostFree(c->rs_pin);
   if (c->hep) hipHostFree(c->hep);
+  if (c->sv_host) hipHostFree(c->sv_host);
   if (c->fhep) hipHostFree(c->fhep);
   if (c->xfer) hipStreamDestroy(c->xfer);
   if (c->ev_snap) hipEventDestroy(c->ev_snap);
@@ -1946,6 +1953,7 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
 int kmz_run_begin(kmz_ctx *c, uint32_t flags) {
   if (!c) return KMZ_E_ARG;
   if (c->run_open) return fail(c, KMZ_E_STATE, "kmz_run_begin while a run is open (kmz_run_end first)");
+  if (c->tl_open) return fail(c, KMZ_E_STATE, "kmz_run_begin while a service tail is open (kmz_tail_end first)");
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_run before kmz_load");
   uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
   if (smode == (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG)) return fail(c, KMZ_E_ARG, "choose one stats identity per run");
@@ -2514,6 +2522,7 @@ static uint64_t pow2_at_least(uint64_t x) {
 }
 
 int kmz_tail_map_set(kmz_ctx *c, const kmz_tail_map *m) {
+  if (c && c->tl_open) return fail(c, KMZ_E_STATE, "kmz_tail_map_set while a service tail is open");
   if (!c || !m || !m->svc || !m->cls || (m->n_cls && !m->lsvc)) return KMZ_E_ARG;
   if (c->run_open) return run_busy(c);
   const uint32_t lim = 1u << 24;
@@ -2539,9 +2548,134 @@ int kmz_tail_map_set(kmz_ctx *c, const kmz_tail_map *m) {
   return KMZ_OK;
 }
 
-int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
+// one attempt of the service tail, enqueued on the context's stream up to
+// the read-back of its counters and per-service outputs (kmz_tail_begin, and
+// kmz_tail_end's repeats)
+static int tail_enqueue(kmz_ctx *c) {
+  const uint64_t nt = c->tl_nt;
+  unsigned long long *st = P<unsigned long long>(c->stats64);
+  const uint64_t acap = c->tl_acap, pacap = c->tl_pacap, pcap = c->tl_pcap;
+  // link-key buckets: two link keys per edge key at most, spread by a hash
+  // of their (service, linked service) pair, each pass-A workgroup writing
+  // its own slab of every bucket (2 x its mean share + 64: hot pairs weigh
+  // some buckets); grown on overflow
+  const uint32_t bits = c->tl_bbits, nbk = 1u << bits, nwg = tail_part_grid(nt);
+  c->tl_bcap = std::max<uint64_t>(c->tl_bcap, (2 * nt) / ((uint64_t)nbk * nwg) * 2 + 64);
+  const uint64_t slab = c->tl_bcap;
+  if (slab >= 0xFFFFFFFFull) return fail(c, KMZ_E_OVERFLOW, "service tail buckets");
+  if (ensure(c, c->tl_lbkt, slab * nbk * nwg * 8) || ensure(c, c->tl_lbn, (size_t)nbk * nwg * 4) ||
+      ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
+      ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
+      ensure(c, c->tl_sstat, (size_t)c->tl_n_svc * 32) || ensure(c, c->tl_rel, (size_t)c->tl_n_svc * c->tl_n_dist * 4) ||
+      ensure(c, c->tl_sfirst, (size_t)c->tl_n_svc * 8 + 8))
+    return KMZ_E_HIP;
+  // the read-back (pinned): counters [64 B], stats [n_svc x 8 u32], first rows [n_svc u64], relying table
+  const uint32_t nd_run = c->tl_n_dist;
+  c->tl_nd_run = nd_run;
+  const size_t hb = 64 + (size_t)c->tl_n_svc * 40 + (size_t)c->tl_n_svc * nd_run * 4;
+  if (c->tl_host_bytes < hb) {
+    if (c->tl_host) hipHostFree(c->tl_host);
+    c->tl_host_bytes = 0;
+    if (hipHostMalloc(&c->tl_host, hb, hipHostMallocDefault) != hipSuccess) {
+      c->tl_host = nullptr;
+      return fail(c, KMZ_E_HIP, "hipHostMalloc (tail read-back)");
+    }
+    c->tl_host_bytes = hb;
+  }
+  {
+    Timed t(c, KMZ_K_MEMSET);
+    FillArgs f;
+    f.add(c->tl_pset.p, pcap * 8, 0);
+    f.add(c->tl_pkey.p, pacap * 8, 0);
+    f.add(c->tl_pval.p, pacap * 4, 0);
+    f.add(c->tl_hasin.p, c->tl_n_ep ? c->tl_n_ep : 1, 0);
+    f.add(c->tl_cnt.p, 64, 0);
+    if (c->tl_n_svc) {
+      f.add(c->tl_sstat.p, (size_t)c->tl_n_svc * 32, 0);
+      f.add(c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4, 0);
+      f.add(c->tl_sfirst.p, (size_t)c->tl_n_svc * 8, 0xFF);
+    }
+    launch_fill(c->stream, f);
+  }
+  unsigned long long *cnt64 = P<unsigned long long>(c->tl_cnt);  // [0] flags (u32), [1] details, [2] pairs
+  {
+    Timed t(c, KMZ_K_TAIL);
+    launch_tail(c->stream, P<unsigned long long>(c->trip_out), st + S_TRIP_OUT, nt, P<uint32_t>(c->tl_svc),
+                P<uint32_t>(c->tl_cls), P<uint32_t>(c->tl_lsvc), P<uint32_t>(c->tl_svc), c->tl_n_ep, c->tl_n_cls,
+                bits, P<unsigned long long>(c->tl_lbkt), (uint32_t)slab, P<uint32_t>(c->tl_lbn),
+                P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey), P<uint32_t>(c->tl_pval),
+                pacap, P<uint8_t>(c->tl_hasin), P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), nd_run,
+                P<unsigned int>(c->tl_cnt), P<kmz_tail_detail>(c->tl_det), acap, P<uint32_t>(c->tl_pairs), cnt64 + 1,
+                // diagnostic knobs (timing only, wrong results): KMZ_ABLATE bit 7 skips the
+                // link keys, bit 12 the cohesion pairs
+                ((c->ablate >> 7) & 1u) | (((c->ablate >> 12) & 1u) << 1));
+    launch_tail_service_rows(c->stream, P<unsigned long long>(c->epp) + c->n_dep, P<uint32_t>(c->tl_svc),
+                             P<uint8_t>(c->tl_hasin), c->tl_n_ep, P<uint32_t>(c->tl_sstat),
+                             P<unsigned long long>(c->tl_sfirst));
+  }
+  // one read-back and one synchronisation for the counters and every per-service output
+  char *hh = static_cast<char *>(c->tl_host);
+  HIPCHK(c, hipMemcpyAsync(hh, c->tl_cnt.p, 64, hipMemcpyDeviceToHost, c->stream));
+  if (c->tl_n_svc) {
+    HIPCHK(c, hipMemcpyAsync(hh + 64, c->tl_sstat.p, (size_t)c->tl_n_svc * 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(hh + 64 + (size_t)c->tl_n_svc * 32, c->tl_sfirst.p, (size_t)c->tl_n_svc * 8,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(hh + 64 + (size_t)c->tl_n_svc * 40, c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4,
+                             hipMemcpyDeviceToHost, c->stream));
+  }
+  return KMZ_OK;
+}
+
+// kmz_tail_end's wait for one attempt: 1 = done, 0 = repeat (tables grown), else an error
+static int tail_finish(kmz_ctx *c, int attempt, uint64_t *n_details, uint64_t *n_pairs) {
+  const uint64_t nt = c->tl_nt;
+  char *hh = static_cast<char *>(c->tl_host);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  harvest(c);
+  unsigned long long h[6];
+  memcpy(h, hh, sizeof(h));
+  const uint32_t fl = (uint32_t)h[0];
+  if (fl & F_RANGE) return fail(c, KMZ_E_RANGE, "edge key endpoint outside the tail map");
+  const bool bucket_full = (uint32_t)h[5] != 0;  // (u32 word 10) a bucket outgrew its LDS tables
+  if ((fl & F_TRIPLE_OVERFLOW) || bucket_full) {
+    if (attempt >= 3) return fail(c, KMZ_E_OVERFLOW, "service tail table overflow");
+    if (bucket_full) {
+      if (c->tl_bbits >= tail_bucket_bits_max()) return fail(c, KMZ_E_OVERFLOW, "service tail: too many link keys");
+      ++c->tl_bbits;
+    }
+    if (fl & F_TRIPLE_OVERFLOW) {
+      c->tl_acap = std::max(c->tl_acap * 4, pow2_at_least(nt / 2 + 4096));
+      c->tl_pacap = std::max(c->tl_pacap * 4, pow2_at_least(nt / 4 + 4096));
+      c->tl_pcap = std::max(c->tl_pcap * 4, pow2_at_least(2 * nt + 64));
+      c->tl_bcap *= 2;
+    }
+    return 0;
+  }
+  const uint64_t won_p = (uint32_t)(h[4] >> 32);
+  c->tl_pcap = pow2_at_least(2 * won_p + 4096);  // the next run's pair set (this run's pairs at load <= 1/2)
+  // the detail output / pair tables at 2x this run's counts for the next
+  // run (they start at nt / 2 and nt / 4); a larger next batch overflows and
+  // repeats the tail 4x larger
+  c->tl_acap = pow2_at_least(2 * h[1] + 4096);
+  c->tl_pacap = pow2_at_least(2 * h[2] + 4096);
+  c->tl_nd = h[1];
+  c->tl_np = h[2];
+  // relying-factor distances beyond the dense table: reported, and the
+  // table grows for the next run (the host takes them from the details)
+  c->tl_deep = (uint32_t)h[3];
+  if (c->tl_deep >= c->tl_n_dist && (uint64_t)c->tl_n_svc * (c->tl_deep + 1) <= (1ull << 26))
+    c->tl_n_dist = c->tl_deep + 1;
+  c->tl_rel_dist = c->tl_deep ? 0 : c->tl_nd_run;
+  c->tl_ran = true;
+  if (n_details) *n_details = h[1];
+  if (n_pairs) *n_pairs = h[2];
+  return 1;
+}
+
+int kmz_tail_begin(kmz_ctx *c) {
   if (!c) return KMZ_E_ARG;
   if (c->run_open) return run_busy(c);
+  if (c->tl_open) return fail(c, KMZ_E_STATE, "kmz_tail_begin while a tail is open (kmz_tail_end first)");
   if (!(c->ran & KMZ_RUN_DEPS)) return fail(c, KMZ_E_STATE, "no dependency run");
   if (!c->tl_map) return fail(c, KMZ_E_STATE, "kmz_tail_map_set first");
   if (c->tl_n_ep != c->n_dep) return fail(c, KMZ_E_ARG, "tail map size differs from the dependency endpoints");
@@ -2563,122 +2697,34 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
   if (!c->tl_pcap) c->tl_pcap = pow2_at_least(2 * nt + 64);
   if (!c->tl_acap) c->tl_acap = pow2_at_least(nt / 2 + 4096);
   if (!c->tl_pacap) c->tl_pacap = pow2_at_least(nt / 4 + 4096);
+  c->tl_nt = nt;
+  if (int r = tail_enqueue(c)) return r;
+  c->tl_open = true;
+  return KMZ_OK;
+}
+
+int kmz_tail_end(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
+  if (!c) return KMZ_E_ARG;
+  if (!c->tl_open) return fail(c, KMZ_E_STATE, "kmz_tail_end without kmz_tail_begin");
+  c->tl_open = false;
   for (int attempt = 0;; ++attempt) {
-    const uint64_t acap = c->tl_acap, pacap = c->tl_pacap, pcap = c->tl_pcap;
-    // link-key buckets: two link keys per edge key at most, spread by a hash
-    // of their (service, linked service) pair, each pass-A workgroup writing
-    // its own slab of every bucket (2 x its mean share + 64: hot pairs weigh
-    // some buckets); grown on overflow
-    const uint32_t bits = c->tl_bbits, nbk = 1u << bits, nwg = tail_part_grid(nt);
-    c->tl_bcap = std::max<uint64_t>(c->tl_bcap, (2 * nt) / ((uint64_t)nbk * nwg) * 2 + 64);
-    const uint64_t slab = c->tl_bcap;
-    if (slab >= 0xFFFFFFFFull) return fail(c, KMZ_E_OVERFLOW, "service tail buckets");
-    if (ensure(c, c->tl_lbkt, slab * nbk * nwg * 8) || ensure(c, c->tl_lbn, (size_t)nbk * nwg * 4) ||
-        ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
-        ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
-        ensure(c, c->tl_sstat, (size_t)c->tl_n_svc * 32) || ensure(c, c->tl_rel, (size_t)c->tl_n_svc * c->tl_n_dist * 4) ||
-        ensure(c, c->tl_sfirst, (size_t)c->tl_n_svc * 8 + 8))
-      return KMZ_E_HIP;
-    // the read-back (pinned): counters [64 B], stats [n_svc x 8 u32], first rows [n_svc u64], relying table
-    const uint32_t nd_run = c->tl_n_dist;
-    const size_t hb = 64 + (size_t)c->tl_n_svc * 40 + (size_t)c->tl_n_svc * nd_run * 4;
-    if (c->tl_host_bytes < hb) {
-      if (c->tl_host) hipHostFree(c->tl_host);
-      c->tl_host_bytes = 0;
-      if (hipHostMalloc(&c->tl_host, hb, hipHostMallocDefault) != hipSuccess) {
-        c->tl_host = nullptr;
-        return fail(c, KMZ_E_HIP, "hipHostMalloc (tail read-back)");
-      }
-      c->tl_host_bytes = hb;
-    }
-    {
-      Timed t(c, KMZ_K_MEMSET);
-      FillArgs f;
-      f.add(c->tl_pset.p, pcap * 8, 0);
-      f.add(c->tl_pkey.p, pacap * 8, 0);
-      f.add(c->tl_pval.p, pacap * 4, 0);
-      f.add(c->tl_hasin.p, c->tl_n_ep ? c->tl_n_ep : 1, 0);
-      f.add(c->tl_cnt.p, 64, 0);
-      if (c->tl_n_svc) {
-        f.add(c->tl_sstat.p, (size_t)c->tl_n_svc * 32, 0);
-        f.add(c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4, 0);
-        f.add(c->tl_sfirst.p, (size_t)c->tl_n_svc * 8, 0xFF);
-      }
-      launch_fill(c->stream, f);
-    }
-    unsigned long long *cnt64 = P<unsigned long long>(c->tl_cnt);  // [0] flags (u32), [1] details, [2] pairs
-    {
-      Timed t(c, KMZ_K_TAIL);
-      launch_tail(c->stream, P<unsigned long long>(c->trip_out), st + S_TRIP_OUT, nt, P<uint32_t>(c->tl_svc),
-                  P<uint32_t>(c->tl_cls), P<uint32_t>(c->tl_lsvc), P<uint32_t>(c->tl_svc), c->tl_n_ep, c->tl_n_cls,
-                  bits, P<unsigned long long>(c->tl_lbkt), (uint32_t)slab, P<uint32_t>(c->tl_lbn),
-                  P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey), P<uint32_t>(c->tl_pval),
-                  pacap, P<uint8_t>(c->tl_hasin), P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), nd_run,
-                  P<unsigned int>(c->tl_cnt), P<kmz_tail_detail>(c->tl_det), acap, P<uint32_t>(c->tl_pairs), cnt64 + 1,
-                  // diagnostic knobs (timing only, wrong results): KMZ_ABLATE bit 7 skips the
-                  // link keys, bit 12 the cohesion pairs
-                  ((c->ablate >> 7) & 1u) | (((c->ablate >> 12) & 1u) << 1));
-      launch_tail_service_rows(c->stream, P<unsigned long long>(c->epp) + c->n_dep, P<uint32_t>(c->tl_svc),
-                               P<uint8_t>(c->tl_hasin), c->tl_n_ep, P<uint32_t>(c->tl_sstat),
-                               P<unsigned long long>(c->tl_sfirst));
-    }
-    // one read-back and one synchronisation for the counters and every per-service output
-    char *hh = static_cast<char *>(c->tl_host);
-    HIPCHK(c, hipMemcpyAsync(hh, c->tl_cnt.p, 64, hipMemcpyDeviceToHost, c->stream));
-    if (c->tl_n_svc) {
-      HIPCHK(c, hipMemcpyAsync(hh + 64, c->tl_sstat.p, (size_t)c->tl_n_svc * 32, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipMemcpyAsync(hh + 64 + (size_t)c->tl_n_svc * 32, c->tl_sfirst.p, (size_t)c->tl_n_svc * 8,
-                               hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipMemcpyAsync(hh + 64 + (size_t)c->tl_n_svc * 40, c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4,
-                               hipMemcpyDeviceToHost, c->stream));
-    }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    harvest(c);
-    unsigned long long h[6];
-    memcpy(h, hh, sizeof(h));
-    const uint32_t fl = (uint32_t)h[0];
-    if (fl & F_RANGE) return fail(c, KMZ_E_RANGE, "edge key endpoint outside the tail map");
-    const bool bucket_full = (uint32_t)h[5] != 0;  // (u32 word 10) a bucket outgrew its LDS tables
-    if ((fl & F_TRIPLE_OVERFLOW) || bucket_full) {
-      if (attempt >= 3) return fail(c, KMZ_E_OVERFLOW, "service tail table overflow");
-      if (bucket_full) {
-        if (c->tl_bbits >= tail_bucket_bits_max()) return fail(c, KMZ_E_OVERFLOW, "service tail: too many link keys");
-        ++c->tl_bbits;
-      }
-      if (fl & F_TRIPLE_OVERFLOW) {
-        c->tl_acap = std::max(c->tl_acap * 4, pow2_at_least(nt / 2 + 4096));
-        c->tl_pacap = std::max(c->tl_pacap * 4, pow2_at_least(nt / 4 + 4096));
-        c->tl_pcap = std::max(c->tl_pcap * 4, pow2_at_least(2 * nt + 64));
-        c->tl_bcap *= 2;
-      }
-      continue;
-    }
-    const uint64_t won_p = (uint32_t)(h[4] >> 32);
-    c->tl_pcap = pow2_at_least(2 * won_p + 4096);  // the next run's pair set (this run's pairs at load <= 1/2)
-    // the detail output / pair tables at 2x this run's counts for the next
-    // run (they start at nt / 2 and nt / 4); a larger next batch overflows and
-    // repeats the tail 4x larger
-    c->tl_acap = pow2_at_least(2 * h[1] + 4096);
-    c->tl_pacap = pow2_at_least(2 * h[2] + 4096);
-    c->tl_nd = h[1];
-    c->tl_np = h[2];
-    // relying-factor distances beyond the dense table: reported, and the
-    // table grows for the next run (the host takes them from the details)
-    c->tl_deep = (uint32_t)h[3];
-    if (c->tl_deep >= c->tl_n_dist && (uint64_t)c->tl_n_svc * (c->tl_deep + 1) <= (1ull << 26))
-      c->tl_n_dist = c->tl_deep + 1;
-    c->tl_rel_dist = c->tl_deep ? 0 : nd_run;
-    c->tl_ran = true;
-    if (n_details) *n_details = h[1];
-    if (n_pairs) *n_pairs = h[2];
-    return KMZ_OK;
+    const int r = tail_finish(c, attempt, n_details, n_pairs);
+    if (r == 1) return KMZ_OK;
+    if (r != 0) return r;
+    if (int e = tail_enqueue(c)) return e;
   }
+}
+
+int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
+  const int r = kmz_tail_begin(c);
+  return r ? r : kmz_tail_end(c, n_details, n_pairs);
 }
 
 int kmz_tail_service_stats(kmz_ctx *c, uint32_t *stats, uint64_t scap, uint32_t *by_dist, uint64_t dcap,
                            uint32_t *n_dist) {
   if (!c || !n_dist) return KMZ_E_ARG;
   if (c->run_open) return run_busy(c);
+  if (c->tl_open) return fail(c, KMZ_E_STATE, "service tail open (kmz_tail_end first)");
   if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
   *n_dist = c->tl_rel_dist;
   const uint64_t ns = (uint64_t)c->tl_n_svc * 8, nd = (uint64_t)c->tl_n_svc * c->tl_rel_dist;
@@ -2692,6 +2738,7 @@ int kmz_tail_service_stats(kmz_ctx *c, uint32_t *stats, uint64_t scap, uint32_t 
 int kmz_tail_service_first(kmz_ctx *c, uint64_t *first, uint64_t cap) {
   if (!c || (!first && cap)) return KMZ_E_ARG;
   if (c->run_open) return run_busy(c);
+  if (c->tl_open) return fail(c, KMZ_E_STATE, "service tail open (kmz_tail_end first)");
   if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
   if (cap < c->tl_n_svc) return fail(c, KMZ_E_ARG, "output too small");
   if (c->tl_n_svc) memcpy(first, static_cast<const char *>(c->tl_host) + 64 + (size_t)c->tl_n_svc * 32, (size_t)c->tl_n_svc * 8);
@@ -2724,26 +2771,48 @@ int kmz_service_map_set(kmz_ctx *c, const uint32_t *sid_of_ep, uint32_t n_ep, ui
   return KMZ_OK;
 }
 
-int kmz_service_sums(kmz_ctx *c, kmz_service_sum *out, uint64_t cap) {
-  if (!c || (!out && cap)) return KMZ_E_ARG;
+int kmz_service_sums_begin(kmz_ctx *c) {
+  if (!c) return KMZ_E_ARG;
   if (c->run_open) return run_busy(c);
   if (!c->sv_map) return fail(c, KMZ_E_STATE, "kmz_service_map_set first");
   if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
   if ((uint64_t)c->sv_n_ep * c->sv_n_status != c->G) return fail(c, KMZ_E_ARG, "service map size differs from the groups");
-  if (cap < c->sv_n_sid) return fail(c, KMZ_E_ARG, "output too small");
+  c->sv_open = true;
   if (!c->sv_n_sid) return KMZ_OK;
+  const size_t bytes = (size_t)c->sv_n_sid * sizeof(kmz_service_sum);
+  if (int r = pinned_staging(c, c->sv_host, c->sv_host_bytes, bytes)) {
+    c->sv_open = false;
+    return r;
+  }
   launch_service_sums(c->stream, P<kmz_group>(c->grp_final), c->sv_n_status, P<uint32_t>(c->sv_off),
                       P<uint32_t>(c->sv_eps), P<uint8_t>(c->sv_5xx), c->sv_n_sid, P<kmz_service_sum>(c->sv_out));
-  HIPCHK(c, hipMemcpyAsync(out, c->sv_out.p, (size_t)c->sv_n_sid * sizeof(kmz_service_sum), hipMemcpyDeviceToHost,
-                           c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->sv_host, c->sv_out.p, bytes, hipMemcpyDeviceToHost, c->stream));
   return KMZ_OK;
+}
+
+int kmz_service_sums_end(kmz_ctx *c, kmz_service_sum *out, uint64_t cap) {
+  if (!c || (!out && cap)) return KMZ_E_ARG;
+  if (!c->sv_open) return fail(c, KMZ_E_STATE, "kmz_service_sums_end without kmz_service_sums_begin");
+  if (cap < c->sv_n_sid) return fail(c, KMZ_E_ARG, "output too small");
+  c->sv_open = false;
+  if (!c->sv_n_sid) return KMZ_OK;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  memcpy(out, c->sv_host, (size_t)c->sv_n_sid * sizeof(kmz_service_sum));
+  return KMZ_OK;
+}
+
+int kmz_service_sums(kmz_ctx *c, kmz_service_sum *out, uint64_t cap) {
+  if (!c || (!out && cap)) return KMZ_E_ARG;
+  if (c->sv_map && cap < c->sv_n_sid) return fail(c, KMZ_E_ARG, "output too small");
+  const int r = kmz_service_sums_begin(c);
+  return r ? r : kmz_service_sums_end(c, out, cap);
 }
 
 int kmz_tail_get(kmz_ctx *c, kmz_tail_detail *det, uint64_t dcap, kmz_tail_pair *pairs, uint64_t pcap,
                  uint8_t *has_in, uint64_t hcap) {
   if (!c) return KMZ_E_ARG;
   if (c->run_open) return run_busy(c);
+  if (c->tl_open) return fail(c, KMZ_E_STATE, "service tail open (kmz_tail_end first)");
   if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
   if ((det && dcap < c->tl_nd) || (pairs && pcap < c->tl_np) || (has_in && hcap < c->tl_n_ep))
     return fail(c, KMZ_E_ARG, "output too small");

@@ -542,8 +542,17 @@ class Engine:
         ``tail.service_sums`` returns them for the same rows: services in
         first-occurrence order, sum(cv * combined) added in ascending group
         order, sum(combined), sum(combined of 5xx)."""
+        self.service_sums_begin()
+        return self.service_sums_end()
+
+    def service_sums_begin(self) -> None:
+        """``service_sums`` enqueued only (kmz_service_sums_begin)."""
+        L.check(self.ctx, self._lib.kmz_service_sums_begin(self.ctx))
+
+    def service_sums_end(self):
+        """Waits for ``service_sums_begin``'s sums: the same result as ``service_sums``."""
         out = np.empty(self._n_sid, dtype=L.SERVICE_SUM_DTYPE)
-        L.check(self.ctx, self._lib.kmz_service_sums(self.ctx, L.ptr(out), len(out)))
+        L.check(self.ctx, self._lib.kmz_service_sums_end(self.ctx, L.ptr(out), len(out)))
         big = np.iinfo(np.uint64).max
         present = np.nonzero(out["first"] != big)[0]
         order = present[np.argsort(out["first"][present], kind="stable")]

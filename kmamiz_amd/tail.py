@@ -120,13 +120,26 @@ def run_tail(eng, maps: TailMaps, endpoints: Optional[np.ndarray] = None) -> "Se
     and first row); the link details and cohesion pairs are copied when a list
     output needs them.  ``endpoints`` is no longer needed (kept for callers
     that pass it)."""
+    tail_begin(eng, maps)
+    return tail_end(eng, maps)
+
+
+def tail_begin(eng, maps: TailMaps) -> None:
+    """run_tail's first half: the tail enqueued on the engine's stream
+    (kmz_tail_begin); the host is free until ``tail_end``."""
     lib = L.lib()
     if getattr(eng, "_tail_maps", None) is not maps:
         m = maps.c_struct()
         L.check(eng.ctx, lib.kmz_tail_map_set(eng.ctx, C.byref(m)))
         eng._tail_maps = maps
+    L.check(eng.ctx, lib.kmz_tail_begin(eng.ctx))
+
+
+def tail_end(eng, maps: TailMaps) -> "ServiceTail":
+    """Waits for ``tail_begin``'s tail: run_tail's result."""
+    lib = L.lib()
     nd, npairs = C.c_uint64(), C.c_uint64()
-    L.check(eng.ctx, lib.kmz_tail_run(eng.ctx, C.byref(nd), C.byref(npairs)))
+    L.check(eng.ctx, lib.kmz_tail_end(eng.ctx, C.byref(nd), C.byref(npairs)))
     n_svc = len(maps.svc_names)
     nd_, npairs_ = nd.value, npairs.value
     dist = C.c_uint32()

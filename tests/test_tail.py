@@ -361,3 +361,39 @@ def test_service_sums_on_device_equal_row_sums(engine, config, ntr):
     rb = realtime_risk_from_sums(tail, names, *host)
     for k in ra:
         assert ra[k].tobytes() == rb[k].tobytes(), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,ntr", [(5, 60000), (3, 3000)])
+def test_tail_and_sums_in_halves_equal_the_synchronous_calls(engine, config, ntr):
+    """kmz_tail_begin / _end and kmz_service_sums_begin / _end (the bench's
+    order: both enqueued right after the run, the fetch in between) give what
+    kmz_tail_run and kmz_service_sums give; a run is refused while the tail
+    is open."""
+    from kmamiz_amd import _lib as L
+    from kmamiz_amd import synth
+    from kmamiz_amd.tail import maps_for_synth, run_tail, tail_begin, tail_end
+
+    sid, names, is5 = _synth_service_map(config)
+    maps = maps_for_synth(config)
+    engine.load_synthetic(config, synth.SEED, 0, ntr)
+    engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    engine.set_service_map(sid, len(names), is5)
+    a = run_tail(engine, maps)
+    sa = engine.service_sums()
+    tail_begin(engine, maps)
+    engine.service_sums_begin()
+    with pytest.raises(Exception):
+        engine.run(L.RUN_STATS_TAG | L.RUN_DEPS)
+    g, t, e = engine.fetch(keys=False)
+    b = tail_end(engine, maps)
+    sb = engine.service_sums_end()
+    assert a.stats.tobytes() == b.stats.tobytes()
+    assert a.by_dist.tobytes() == b.by_dist.tobytes()
+    assert (a.n_details, a.n_pairs) == (b.n_details, b.n_pairs)
+    for x, y in zip(sa, sb):
+        assert x.tobytes() == y.tobytes()
+    ma, mb = a.metrics(), b.metrics()
+    assert ma.keys() == mb.keys()
+    for k in ma:
+        assert np.asarray(ma[k]).tobytes() == np.asarray(mb[k]).tobytes(), k
