@@ -94,7 +94,7 @@ struct kmz_ctx {
   DevBuf ctile;           // K4 per-workgroup stats (apart from K3's tile_tmp: the two run concurrently)
   DevBuf kwpos, kwpos_n;  // chain-table slots written by a run (cleared after it: no per-run memset)
   // service tail (kmz_tail.hip): maps, pair set / table, outputs, link-key buckets
-  DevBuf tl_svc, tl_cls, tl_lsvc, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs, tl_cnt, tl_sstat, tl_rel,
+  DevBuf tl_svc, tl_cls, tl_lsvc, tl_pset, tl_pkey, tl_pval, tl_hasin, tl_det, tl_pairs, tl_rb,
       tl_lbkt, tl_lbn;
   uint32_t tl_n_ep = 0, tl_n_cls = 0, tl_n_svc = 0, tl_n_dist = 64, tl_deep = 0;
   uint32_t tl_rel_dist = 0;  // distances in the last run's relying table (0: not complete, use the details)
@@ -104,7 +104,9 @@ struct kmz_ctx {
   uint32_t tl_nd_run = 0;     // ... its relying-table width
   uint64_t tl_acap = 0, tl_pacap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0, tl_bcap = 0;
   uint32_t tl_bbits = 0;  // link-key buckets: 2^tl_bbits
-  DevBuf tl_sfirst;              // per service: first row (k_tail_service_rows)
+  // tl_rb: the tail's read-back in one device buffer, laid out as its pinned
+  // host copy: counters [64 B], stats [n_svc x 8 u32], first rows [n_svc u64]
+  // (k_tail_service_rows), relying table [n_svc x n_dist u32] -- one copy
   void *tl_host = nullptr;       // pinned: the tail's counters, per-service stats, relying table, first rows
   size_t tl_host_bytes = 0;
   // RiskAnalyzer.RealtimeRisk's per-service sums (k_service_sums): CSR of the
@@ -427,8 +429,8 @@ void kmz_destroy(kmz_ctx *c) {
                     &c->mval, &c->ctab, &c->cetab, &c->plist, &c->kstage, &c->kstage_n, &c->kdefer, &c->kdefer_n,
                     &c->kbucket, &c->kbucket_n, &c->mkeys_in, &c->mtab, &c->kwpos, &c->kwpos_n, &c->ctile, &c->gd_out, &c->gd_in, &c->gd_set, &c->gd_cnt, &c->rt_hist, &c->rt_tot, &c->rt_out, &c->rt_ctr, &c->rt_pool1, &c->rt_dir, &c->rt_pool2, &c->rt_cur, &c->rt_tsz, &c->rt_jcur, &c->gu_ids, &c->gu_grp, &c->gu_bcnt, &c->imap_l, &c->imap_g, &c->tl_svc, &c->tl_cls, &c->tl_lsvc,
                     &c->tl_pset, &c->tl_pkey, &c->tl_pval,
-                    &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_cnt,
-                    &c->tl_sstat, &c->tl_rel, &c->tl_sfirst, &c->tl_lbkt, &c->tl_lbn, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
+                    &c->tl_hasin, &c->tl_det, &c->tl_pairs, &c->tl_rb,
+                    &c->tl_lbkt, &c->tl_lbn, &c->sv_off, &c->sv_eps, &c->sv_5xx, &c->sv_out,
                     &c->o_key, &c->o_val, &c->o_out,
                     &c->o_rts, &c->o_rsh, &c->j_buf, &c->j_elem, &c->j_state, &c->j_jsc, &c->j_mask,
                     &c->j_cnt, &c->j_off, &c->j_csc, &c->j_small, &c->j_starts, &c->j_slices, &c->j_tslot,
@@ -2532,7 +2534,7 @@ int kmz_tail_map_set(kmz_ctx *c, const kmz_tail_map *m) {
   for (uint32_t k = 0; k < m->n_cls; ++k)
     if (m->lsvc[k] >= m->n_lsvc) return fail(c, KMZ_E_RANGE, "tail link-class id out of range");
   if (ensure(c, c->tl_svc, (size_t)m->n_ep * 4) || ensure(c, c->tl_cls, (size_t)m->n_ep * 4) ||
-      ensure(c, c->tl_lsvc, (size_t)m->n_cls * 4) || ensure(c, c->tl_hasin, m->n_ep) || ensure(c, c->tl_cnt, 64))
+      ensure(c, c->tl_lsvc, (size_t)m->n_cls * 4) || ensure(c, c->tl_hasin, m->n_ep))
     return KMZ_E_HIP;
   if (m->n_ep) {
     HIPCHK(c, hipMemcpyAsync(c->tl_svc.p, m->svc, (size_t)m->n_ep * 4, hipMemcpyHostToDevice, c->stream));
@@ -2566,8 +2568,7 @@ static int tail_enqueue(kmz_ctx *c) {
   if (ensure(c, c->tl_lbkt, slab * nbk * nwg * 8) || ensure(c, c->tl_lbn, (size_t)nbk * nwg * 4) ||
       ensure(c, c->tl_pset, pcap * 8) || ensure(c, c->tl_pkey, pacap * 8) || ensure(c, c->tl_pval, pacap * 4) ||
       ensure(c, c->tl_det, acap * sizeof(kmz_tail_detail)) || ensure(c, c->tl_pairs, pacap * sizeof(kmz_tail_pair)) ||
-      ensure(c, c->tl_sstat, (size_t)c->tl_n_svc * 32) || ensure(c, c->tl_rel, (size_t)c->tl_n_svc * c->tl_n_dist * 4) ||
-      ensure(c, c->tl_sfirst, (size_t)c->tl_n_svc * 8 + 8))
+      ensure(c, c->tl_rb, 64 + (size_t)c->tl_n_svc * 40 + (size_t)c->tl_n_svc * c->tl_n_dist * 4 + 8))
     return KMZ_E_HIP;
   // the read-back (pinned): counters [64 B], stats [n_svc x 8 u32], first rows [n_svc u64], relying table
   const uint32_t nd_run = c->tl_n_dist;
@@ -2582,6 +2583,11 @@ static int tail_enqueue(kmz_ctx *c) {
     }
     c->tl_host_bytes = hb;
   }
+  char *rb = static_cast<char *>(c->tl_rb.p);
+  unsigned int *rb_cnt = reinterpret_cast<unsigned int *>(rb);
+  uint32_t *rb_sstat = reinterpret_cast<uint32_t *>(rb + 64);
+  unsigned long long *rb_sfirst = reinterpret_cast<unsigned long long *>(rb + 64 + (size_t)c->tl_n_svc * 32);
+  uint32_t *rb_rel = reinterpret_cast<uint32_t *>(rb + 64 + (size_t)c->tl_n_svc * 40);
   {
     Timed t(c, KMZ_K_MEMSET);
     FillArgs f;
@@ -2589,40 +2595,32 @@ static int tail_enqueue(kmz_ctx *c) {
     f.add(c->tl_pkey.p, pacap * 8, 0);
     f.add(c->tl_pval.p, pacap * 4, 0);
     f.add(c->tl_hasin.p, c->tl_n_ep ? c->tl_n_ep : 1, 0);
-    f.add(c->tl_cnt.p, 64, 0);
+    f.add(rb_cnt, 64, 0);
     if (c->tl_n_svc) {
-      f.add(c->tl_sstat.p, (size_t)c->tl_n_svc * 32, 0);
-      f.add(c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4, 0);
-      f.add(c->tl_sfirst.p, (size_t)c->tl_n_svc * 8, 0xFF);
+      f.add(rb_sstat, (size_t)c->tl_n_svc * 32, 0);
+      f.add(rb_rel, (size_t)c->tl_n_svc * nd_run * 4, 0);
+      f.add(rb_sfirst, (size_t)c->tl_n_svc * 8, 0xFF);
     }
     launch_fill(c->stream, f);
   }
-  unsigned long long *cnt64 = P<unsigned long long>(c->tl_cnt);  // [0] flags (u32), [1] details, [2] pairs
+  unsigned long long *cnt64 = reinterpret_cast<unsigned long long *>(rb_cnt);  // [0] flags (u32), [1] details, [2] pairs
   {
     Timed t(c, KMZ_K_TAIL);
     launch_tail(c->stream, P<unsigned long long>(c->trip_out), st + S_TRIP_OUT, nt, P<uint32_t>(c->tl_svc),
                 P<uint32_t>(c->tl_cls), P<uint32_t>(c->tl_lsvc), P<uint32_t>(c->tl_svc), c->tl_n_ep, c->tl_n_cls,
                 bits, P<unsigned long long>(c->tl_lbkt), (uint32_t)slab, P<uint32_t>(c->tl_lbn),
                 P<unsigned long long>(c->tl_pset), pcap, P<unsigned long long>(c->tl_pkey), P<uint32_t>(c->tl_pval),
-                pacap, P<uint8_t>(c->tl_hasin), P<uint32_t>(c->tl_sstat), P<uint32_t>(c->tl_rel), nd_run,
-                P<unsigned int>(c->tl_cnt), P<kmz_tail_detail>(c->tl_det), acap, P<uint32_t>(c->tl_pairs), cnt64 + 1,
+                pacap, P<uint8_t>(c->tl_hasin), rb_sstat, rb_rel, nd_run,
+                rb_cnt, P<kmz_tail_detail>(c->tl_det), acap, P<uint32_t>(c->tl_pairs), cnt64 + 1,
                 // diagnostic knobs (timing only, wrong results): KMZ_ABLATE bit 7 skips the
                 // link keys, bit 12 the cohesion pairs
                 ((c->ablate >> 7) & 1u) | (((c->ablate >> 12) & 1u) << 1));
     launch_tail_service_rows(c->stream, P<unsigned long long>(c->epp) + c->n_dep, P<uint32_t>(c->tl_svc),
-                             P<uint8_t>(c->tl_hasin), c->tl_n_ep, P<uint32_t>(c->tl_sstat),
-                             P<unsigned long long>(c->tl_sfirst));
+                             P<uint8_t>(c->tl_hasin), c->tl_n_ep, rb_sstat, rb_sfirst);
   }
   // one read-back and one synchronisation for the counters and every per-service output
   char *hh = static_cast<char *>(c->tl_host);
-  HIPCHK(c, hipMemcpyAsync(hh, c->tl_cnt.p, 64, hipMemcpyDeviceToHost, c->stream));
-  if (c->tl_n_svc) {
-    HIPCHK(c, hipMemcpyAsync(hh + 64, c->tl_sstat.p, (size_t)c->tl_n_svc * 32, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(hh + 64 + (size_t)c->tl_n_svc * 32, c->tl_sfirst.p, (size_t)c->tl_n_svc * 8,
-                             hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(hh + 64 + (size_t)c->tl_n_svc * 40, c->tl_rel.p, (size_t)c->tl_n_svc * nd_run * 4,
-                             hipMemcpyDeviceToHost, c->stream));
-  }
+  HIPCHK(c, hipMemcpyAsync(hh, rb, hb, hipMemcpyDeviceToHost, c->stream));
   return KMZ_OK;
 }
 
