@@ -261,6 +261,7 @@ def main():
         mark("tail_begin", tp)
 
     def service_tail_end():
+        state["tail_open"] = False
         tp = time.perf_counter()
         t = tail_end(eng, tmaps)
         sums = eng.service_sums_end()
@@ -296,6 +297,8 @@ def main():
         state["guard_start_s"] = state.get("guard_start_s", 0.0) + (time.perf_counter() - tg)
         tp = time.perf_counter()
         eng.run_begin(flags)
+        if state.get("tail_open"):  # the previous step's tail, done while this run was being enqueued
+            service_tail_end()
         if guard is not None:
             tg = time.perf_counter()
             guard.post()
@@ -325,6 +328,7 @@ def main():
         # each half right after the other, as before round 6)
         if tail_on and not tail_sync:
             service_tail_begin()
+            state["tail_open"] = True  # (ended by the next step, behind its run_begin)
         if not args.no_fetch:  # the three result sets (with the tail on, the edge keys stay
             # in HBM for kmz_tail_run: the service tail is the output)
             if args.fetch == "pipelined":
@@ -333,9 +337,8 @@ def main():
             else:
                 state["groups"], state["keys"], state["endpoints"] = eng.fetch(keys=not tail_on)
             mark("fetch", tp)
-        if tail_on:
-            if tail_sync:
-                service_tail_begin()
+        if tail_on and tail_sync:
+            service_tail_begin()
             service_tail_end()
 
     for w in range(args.warmup):
@@ -392,6 +395,9 @@ def main():
     fetch_done()  # (the last step's results on the host)
     barrier()
     t1 = time.perf_counter()
+    if state.get("tail_open"):  # (the last step's tail: its GPU half ran inside the timed region)
+        service_tail_end()
+        tail_host()
     gc.enable()
     if os.environ.get("KMZ_BENCH_TRACE"):  # diagnostic: per-step wall times
         print("step ms:", [round((b - a) * 1e3, 3) for a, b in zip([t0] + marks, marks + [t1])], file=sys.stderr)

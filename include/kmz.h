@@ -469,9 +469,12 @@ int kmz_tail_run(kmz_ctx *ctx, uint64_t *n_details, uint64_t *n_pairs);
 /* kmz_tail_run in two halves: _begin enqueues the tail on the context's
  * stream (no wait), _end waits for it (repeating it with larger tables when
  * one overflowed) and returns the result sizes.  Between them the host is
- * free (a step's fetch and host finish run while the GPU computes the tail);
- * kmz_run_begin, kmz_tail_map_set and the tail's getters are refused while
- * a tail is open. */
+ * free (a step's fetch and host finish run while the GPU computes the tail).
+ * The next kmz_run_begin may come before _end: its kernels follow the tail's
+ * on the stream and _end waits for the tail alone (if the tail then has to be
+ * repeated with larger tables, _end fails with KMZ_E_STATE: the run has
+ * replaced its inputs).  kmz_tail_map_set and the tail's getters are refused
+ * while a tail is open. */
 int kmz_tail_begin(kmz_ctx *ctx);
 int kmz_tail_end(kmz_ctx *ctx, uint64_t *n_details, uint64_t *n_pairs);
 /* per-service counters of the last tail run, 8 u32 per service id:
@@ -508,7 +511,8 @@ typedef struct kmz_service_sum {
 int kmz_service_map_set(kmz_ctx *ctx, const uint32_t *sid_of_ep, uint32_t n_ep, uint32_t n_sid, const uint8_t *is_5xx,
                         uint32_t n_status);
 int kmz_service_sums(kmz_ctx *ctx, kmz_service_sum *out, uint64_t cap);
-/* kmz_service_sums in two halves (enqueue; wait and copy out), as the tail */
+/* kmz_service_sums in two halves (enqueue; wait and copy out), as the tail;
+ * _end waits for the sums alone (a run may be enqueued in between) */
 int kmz_service_sums_begin(kmz_ctx *ctx);
 int kmz_service_sums_end(kmz_ctx *ctx, kmz_service_sum *out, uint64_t cap);
 /* copy the results: details and pairs in no particular order; has_in[e] = 1

@@ -102,6 +102,7 @@ struct kmz_ctx {
   bool tl_open = false;       // kmz_tail_begin enqueued, kmz_tail_end not yet
   uint64_t tl_nt = 0;         // ... its edge-key count
   uint32_t tl_nd_run = 0;     // ... its relying-table width
+  bool tl_run_after = false;  // ... a run was begun behind it (a repeat is then impossible)
   uint64_t tl_acap = 0, tl_pacap = 0, tl_pcap = 0, tl_nd = 0, tl_np = 0, tl_bcap = 0;
   uint32_t tl_bbits = 0;  // link-key buckets: 2^tl_bbits
   // tl_rb: the tail's read-back in one device buffer, laid out as its pinned
@@ -197,6 +198,10 @@ struct kmz_ctx {
   JoinRoute rt_arm;
   bool rt_armed = false, rt_routed = false, rt_in_join = false;
   hipEvent_t ev_route = nullptr;
+  // the service tail's and the service sums' read-backs: their _end calls
+  // wait for these, not for the stream, so that the next run may be enqueued
+  // behind an open tail (the bench's step pipelining)
+  hipEvent_t ev_tail = nullptr, ev_sums = nullptr;
 
   // profiling
   // kmz_fetch_begin / _end: transfer stream, snapshot of the results, the open fetch
@@ -387,7 +392,9 @@ kmz_ctx *kmz_create(int device, void *stream) {
       hipEventCreateWithFlags(&c->ev_k3, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_route, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_route, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_tail, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_sums, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return nullptr;
   }
@@ -456,7 +463,7 @@ void kmz_destroy(kmz_ctx *c) {
     hipStreamSynchronize(c->side2);
     hipStreamDestroy(c->side2);
   }
-  for (hipEvent_t e : {c->ev_fork, c->ev_k3, c->ev_join, c->ev_done, c->ev_cert, c->ev_route})
+  for (hipEvent_t e : {c->ev_fork, c->ev_k3, c->ev_join, c->ev_done, c->ev_cert, c->ev_route, c->ev_tail, c->ev_sums})
     if (e) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
@@ -1955,7 +1962,9 @@ int kmz_run(kmz_ctx *c, uint32_t flags) {
 int kmz_run_begin(kmz_ctx *c, uint32_t flags) {
   if (!c) return KMZ_E_ARG;
   if (c->run_open) return fail(c, KMZ_E_STATE, "kmz_run_begin while a run is open (kmz_run_end first)");
-  if (c->tl_open) return fail(c, KMZ_E_STATE, "kmz_run_begin while a service tail is open (kmz_tail_end first)");
+  // (a run may begin behind an open service tail: its kernels follow the
+  // tail's on the stream, and kmz_tail_end waits for the tail's event only)
+  if (c->tl_open) c->tl_run_after = true;
   if (!c->loaded) return fail(c, KMZ_E_STATE, "kmz_run before kmz_load");
   uint32_t smode = flags & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG);
   if (smode == (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG)) return fail(c, KMZ_E_ARG, "choose one stats identity per run");
@@ -2621,6 +2630,7 @@ static int tail_enqueue(kmz_ctx *c) {
   // one read-back and one synchronisation for the counters and every per-service output
   char *hh = static_cast<char *>(c->tl_host);
   HIPCHK(c, hipMemcpyAsync(hh, rb, hb, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_tail, c->stream));
   return KMZ_OK;
 }
 
@@ -2628,8 +2638,8 @@ static int tail_enqueue(kmz_ctx *c) {
 static int tail_finish(kmz_ctx *c, int attempt, uint64_t *n_details, uint64_t *n_pairs) {
   const uint64_t nt = c->tl_nt;
   char *hh = static_cast<char *>(c->tl_host);
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  harvest(c);
+  HIPCHK(c, hipEventSynchronize(c->ev_tail));
+  if (!c->tl_run_after) harvest(c);  // (else the run behind it is timed too: its kmz_run_end harvests both)
   unsigned long long h[6];
   memcpy(h, hh, sizeof(h));
   const uint32_t fl = (uint32_t)h[0];
@@ -2637,6 +2647,8 @@ static int tail_finish(kmz_ctx *c, int attempt, uint64_t *n_details, uint64_t *n
   const bool bucket_full = (uint32_t)h[5] != 0;  // (u32 word 10) a bucket outgrew its LDS tables
   if ((fl & F_TRIPLE_OVERFLOW) || bucket_full) {
     if (attempt >= 3) return fail(c, KMZ_E_OVERFLOW, "service tail table overflow");
+    if (c->tl_run_after)  // (a run enqueued behind the open tail has overwritten the edge keys it read)
+      return fail(c, KMZ_E_STATE, "service tail tables overflowed after the next run began: kmz_tail_run again");
     if (bucket_full) {
       if (c->tl_bbits >= tail_bucket_bits_max()) return fail(c, KMZ_E_OVERFLOW, "service tail: too many link keys");
       ++c->tl_bbits;
@@ -2698,6 +2710,7 @@ int kmz_tail_begin(kmz_ctx *c) {
   c->tl_nt = nt;
   if (int r = tail_enqueue(c)) return r;
   c->tl_open = true;
+  c->tl_run_after = false;
   return KMZ_OK;
 }
 
@@ -2721,7 +2734,7 @@ int kmz_tail_run(kmz_ctx *c, uint64_t *n_details, uint64_t *n_pairs) {
 int kmz_tail_service_stats(kmz_ctx *c, uint32_t *stats, uint64_t scap, uint32_t *by_dist, uint64_t dcap,
                            uint32_t *n_dist) {
   if (!c || !n_dist) return KMZ_E_ARG;
-  if (c->run_open) return run_busy(c);
+  // (a host copy: readable while a run behind the tail is open)
   if (c->tl_open) return fail(c, KMZ_E_STATE, "service tail open (kmz_tail_end first)");
   if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
   *n_dist = c->tl_rel_dist;
@@ -2735,7 +2748,7 @@ int kmz_tail_service_stats(kmz_ctx *c, uint32_t *stats, uint64_t scap, uint32_t 
 
 int kmz_tail_service_first(kmz_ctx *c, uint64_t *first, uint64_t cap) {
   if (!c || (!first && cap)) return KMZ_E_ARG;
-  if (c->run_open) return run_busy(c);
+  // (a host copy: readable while a run behind the tail is open)
   if (c->tl_open) return fail(c, KMZ_E_STATE, "service tail open (kmz_tail_end first)");
   if (!c->tl_ran) return fail(c, KMZ_E_STATE, "no tail run");
   if (cap < c->tl_n_svc) return fail(c, KMZ_E_ARG, "output too small");
@@ -2775,6 +2788,7 @@ int kmz_service_sums_begin(kmz_ctx *c) {
   if (!c->sv_map) return fail(c, KMZ_E_STATE, "kmz_service_map_set first");
   if (!(c->ran & (KMZ_RUN_STATS_RT | KMZ_RUN_STATS_TAG))) return fail(c, KMZ_E_STATE, "no stats run");
   if ((uint64_t)c->sv_n_ep * c->sv_n_status != c->G) return fail(c, KMZ_E_ARG, "service map size differs from the groups");
+  if (c->sv_open) return fail(c, KMZ_E_STATE, "kmz_service_sums_begin while sums are open (kmz_service_sums_end first)");
   c->sv_open = true;
   if (!c->sv_n_sid) return KMZ_OK;
   const size_t bytes = (size_t)c->sv_n_sid * sizeof(kmz_service_sum);
@@ -2785,6 +2799,7 @@ int kmz_service_sums_begin(kmz_ctx *c) {
   launch_service_sums(c->stream, P<kmz_group>(c->grp_final), c->sv_n_status, P<uint32_t>(c->sv_off),
                       P<uint32_t>(c->sv_eps), P<uint8_t>(c->sv_5xx), c->sv_n_sid, P<kmz_service_sum>(c->sv_out));
   HIPCHK(c, hipMemcpyAsync(c->sv_host, c->sv_out.p, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_sums, c->stream));
   return KMZ_OK;
 }
 
@@ -2794,7 +2809,7 @@ int kmz_service_sums_end(kmz_ctx *c, kmz_service_sum *out, uint64_t cap) {
   if (cap < c->sv_n_sid) return fail(c, KMZ_E_ARG, "output too small");
   c->sv_open = false;
   if (!c->sv_n_sid) return KMZ_OK;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipEventSynchronize(c->ev_sums));
   memcpy(out, c->sv_host, (size_t)c->sv_n_sid * sizeof(kmz_service_sum));
   return KMZ_OK;
 }
