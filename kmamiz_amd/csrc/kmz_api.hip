@@ -3,6 +3,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -202,6 +203,10 @@ struct kmz_ctx {
   // wait for these, not for the stream, so that the next run may be enqueued
   // behind an open tail (the bench's step pipelining)
   hipEvent_t ev_tail = nullptr, ev_sums = nullptr;
+  // KMZ_RUNBEGIN_PROFILE=1 (diagnostic): host time of kmz_run_begin's stages
+  // (what the enqueue costs before the GPU has the run's big kernels)
+  bool rb_prof = false;
+  std::vector<std::pair<const char *, double>> rb_marks;
 
   // profiling
   // kmz_fetch_begin / _end: transfer stream, snapshot of the results, the open fetch
@@ -301,6 +306,12 @@ struct Timed {
   }
 };
 
+static void rb_mark(kmz_ctx *c, const char *what) {
+  if (c->rb_prof)
+    c->rb_marks.emplace_back(what, std::chrono::duration<double, std::micro>(
+                                       std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
 void harvest(kmz_ctx *c) {
   for (auto &ep : c->pending) {
     float t = 0.f;
@@ -399,6 +410,7 @@ kmz_ctx *kmz_create(int device, void *stream) {
     return nullptr;
   }
   if (const char *a = getenv("KMZ_ABLATE")) c->ablate = (uint32_t)strtoul(a, nullptr, 0);
+  if (const char *a = getenv("KMZ_RUNBEGIN_PROFILE")) c->rb_prof = atoi(a) != 0;
   if (const char *a = getenv("KMZ_ABLATE2")) c->ablate2 = (uint32_t)strtoul(a, nullptr, 0);
   // run graphs: on by default (round 6); KMZ_HIPGRAPH=0 or KMZ_ABLATE2 bit 23
   // turn them off, KMZ_ABLATE bit 13 (or KMZ_HIPGRAPH=1) keeps them on
@@ -868,6 +880,7 @@ static int launch_cert_deferred(kmz_ctx *c) {
 static int run_join(kmz_ctx *c, bool *ok) {
   const uint32_t n = (uint32_t)c->n;
   *ok = false;
+  rb_mark(c, "join:entry");
   // The certificate beside the join and the walk only while the chain table
   // fits the 256 MB MALL: then the walk's probes leave HBM to the certificate
   // (measured: mesh 5.21 -> 5.12 ms, Bookinfo 0.385 -> 0.323 ms); a chain
@@ -897,6 +910,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
   if (ensure(c, c->mkey, (size_t)c->mcap * 8) || ensure(c, c->mval, (size_t)c->mcap * 4)) return KMZ_E_HIP;
   // an armed routing (kmz_route_ids_join) rides in the join's pass 1 when the
   // run has no certificate of its own and the owners fit the pass-1 bins
+  rb_mark(c, "join:ensure");
   JoinRoute rt;
   if (c->rt_armed && c->no_cert && !early && c->rt_arm.world <= (1u << pl.B1)) {
     if (ensure(c, c->rt_jcur, (size_t)c->rt_arm.world * ROUTE_CUR_STRIDE * 8)) return KMZ_E_HIP;
@@ -941,6 +955,7 @@ static int run_join(kmz_ctx *c, bool *ok) {
                 P<unsigned long long>(c->cpool1), P<uint16_t>(c->cdir), cnt, pl,
                 c->ablate | ((c->no_cert && !rt.out) || early ? 64u : 0u), rt);
   }
+  rb_mark(c, "join:fill+launch");
   if (rt.out) {  // the segments' counts, then the event the exchange waits for
     launch_route_counts(c->stream, rt.world, rt.segw, rt.cur, ROUTE_CUR_STRIDE, rt.out);
     HIPCHK(c, hipGetLastError());
@@ -1267,6 +1282,7 @@ static int run_fused(kmz_ctx *c, bool links) {
 // the same global lists, settle, pending pass and slot clearing as the fused
 // kernel's tail (run_fused), after the window join (run_join / run_table).
 static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
+  rb_mark(c, "chain:entry");
   const uint32_t n = (uint32_t)c->n;
   unsigned int *cnt = P<unsigned int>(c->counters);
   unsigned long long *st = P<unsigned long long>(c->stats64);
@@ -1343,6 +1359,7 @@ static int run_chain_tiles(kmz_ctx *c, bool links, bool joined) {
                           c->n_shapes, P<uint4>(c->cetab), P<uint32_t>(c->ctile), a);
     }
   }
+  rb_mark(c, "walk:launch");
   if (int r2 = launch_cert_deferred(c)) return r2;
   if (c->k3_late && !c->sstats)
     if (int r2 = run_shape_stats(c)) return r2;
@@ -1749,6 +1766,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     }
     launch_fill(c->stream, f);
   }
+  rb_mark(c, "fill");
   int r;
   c->main = c->stream;
   // (KMZ_ABLATE2 bit 17, for comparison: K3 on the main stream between the
@@ -1789,6 +1807,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
   }
   if (r) return r;
+  rb_mark(c, "k3/fork");
   if ((flags & KMZ_RUN_DEPS) && (r = run_deps(c, links))) {
     c->stream = c->main;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1819,6 +1838,7 @@ static int run_enqueue(kmz_ctx *c, uint32_t flags, bool links, unsigned int *h, 
     HIPCHK(c, hipEventRecord(c->ev_cert, c->side2));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_cert, 0));
   }
+  rb_mark(c, "deps");
   static_assert(C_COUNT * 4 % 8 == 0, "the statistics follow the counters in one buffer and in hpin");
   (void)s64;
   HIPCHK(c, hipMemcpyAsync(h, c->counters.p, C_COUNT * 4 + S_COUNT * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1980,6 +2000,10 @@ int kmz_run_begin(kmz_ctx *c, uint32_t flags) {
   }
   unsigned int *h = reinterpret_cast<unsigned int *>(c->hpin);
   unsigned long long *s64 = reinterpret_cast<unsigned long long *>(h + C_COUNT);
+  if (c->rb_prof) {
+    c->rb_marks.clear();
+    rb_mark(c, "begin");
+  }
   c->k4_now = (flags & KMZ_RUN_DEPS) ? k4_direct(c) : false;
   c->no_cert = (flags & KMZ_RUN_NO_CERT) != 0;
   c->rt_routed = c->rt_in_join = false;  // (kmz_route_wait: this run's routing only)
@@ -1990,6 +2014,13 @@ int kmz_run_begin(kmz_ctx *c, uint32_t flags) {
   }
   c->run_open = true;
   c->run_flags = flags;
+  if (c->rb_prof) {
+    rb_mark(c, "end");
+    for (size_t k = 1; k < c->rb_marks.size(); ++k)
+      fprintf(stderr, "%s%s %.1f", k == 1 ? "run_begin us:" : ",", c->rb_marks[k].first,
+              c->rb_marks[k].second - c->rb_marks[k - 1].second);
+    fprintf(stderr, "\n");
+  }
   return KMZ_OK;
 }
 
