@@ -60,7 +60,8 @@ def main():
     gs = torch.cuda.Stream()
     cs = torch.cuda.Stream()
     flags = L.RUN_STATS_TAG | L.RUN_DEPS
-    for world in (2, 4, 8):
+    worlds = [int(w) for w in os.environ.get("KMZ_GUARD_WORLDS", "2,4,8").split(",")]
+    for world in worlds:
         n = eng.load_synthetic_shard(synth.MESH, synth.SEED, 0, ntr, world, 0)
         step = _timed(lambda: eng.run(flags))
         step_nc = _timed(lambda: eng.run(flags | L.RUN_NO_CERT))
