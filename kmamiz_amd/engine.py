@@ -354,9 +354,9 @@ class Engine:
         info = self.info()
         keys = keys and deps
         nu = C.c_uint64()
-        L.check(self.ctx, self._lib.kmz_fetch_used(self.ctx, None, None, 0, C.byref(nu), None, 0, None, None, 0))
-        ids = self._pinned_array("gids", nu.value, np.uint32)
-        g = self._pinned_array("gused", nu.value, L.GROUP_DTYPE)
+        G = info["n_groups"]  # (buffers for every group: one call, the count comes with the copies)
+        ids = self._pinned_array("gids", G, np.uint32)
+        g = self._pinned_array("gused", G, L.GROUP_DTYPE)
         t = self._pinned_array("triples", info["n_triples"], np.uint64) if keys else None
         e = np.empty(self.n_dep_ep, dtype=L.ENDPOINT_DTYPE) if deps else None
         n = C.c_uint64()
@@ -364,7 +364,7 @@ class Engine:
                                                    L.ptr(t) if keys else None, len(t) if keys else 0,
                                                    C.byref(n) if deps else None, L.ptr(e) if deps else None,
                                                    len(e) if deps else 0))
-        return ids, g, t, e
+        return ids[: nu.value], g[: nu.value], t, e
 
     def fetch_begin(self, groups: bool = True, deps: bool = True, keys: bool = True):
         """First half of ``fetch`` for a loop over consecutive batches
